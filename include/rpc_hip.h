@@ -1,0 +1,130 @@
+/*
+ * rpc_hip.h — C ABI of librpc_hip.so, the gfx950 (MI355X) kernels of the
+ * adversarial voxel-detector training step (SURVEY.md §8(a) rows a1–a6).
+ *
+ * Conventions (SURVEY.md §8(b) "C-ABI"):
+ *   - every buffer is device memory owned by the caller (PyTorch caching allocator);
+ *     the library never allocates: scratch comes in through `workspace`;
+ *   - `stream` is a hipStream_t passed as void* (the launcher's current stream);
+ *   - return value 0 = success, otherwise an RPC_ERR_* code (the Python side raises);
+ *     nothing in the library aborts or synchronises the device.
+ *
+ * Each entry point names the reference interface it replaces (file:line in
+ * /root/reference, or the un-vendored upstream call site that file reaches).
+ */
+#ifndef RPC_HIP_H
+#define RPC_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+enum {
+  RPC_OK = 0,
+  RPC_ERR_ARG = 1,        /* bad sizes / null pointers */
+  RPC_ERR_WORKSPACE = 2,  /* workspace too small */
+  RPC_ERR_UNSUPPORTED = 3,/* width combination without a compiled kernel */
+  RPC_ERR_HIP = 4         /* a HIP runtime call failed */
+};
+
+/* Library identity: returns a static string "rpc_hip <git-describe> gfx950". */
+const char* rpc_version(void);
+
+/* ------------------------------------------------------------------ a1 voxelize
+ * Replaces mmcv.ops `hard_voxelize_forward` (upstream mmcv/ops/csrc/pytorch/cuda/
+ * voxelization_cuda.cu, deterministic path) as called per frame by upstream
+ * mmdet3d `Det3DDataPreprocessor.voxelize` for the voxel_layer of
+ * configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-car.py:48-53,
+ * batched over B frames and followed by the `F.pad(coors,(1,0),value=i)` + `torch.cat`
+ * of that preprocessor.
+ *
+ * points         [total_points, num_features] float32, frames concatenated
+ * frame_offsets  device int32 [batch+1]: frame b owns rows [off[b], off[b+1])
+ * voxels         [batch*max_voxels, max_points, num_features] — rows >= total V are untouched
+ * coors          [batch*max_voxels, 4] int32 (b, z, y, x)
+ * num_points     [batch*max_voxels] int32
+ * voxel_num      device int32 [batch+1]: per-frame voxel counts, then the total V
+ * Semantics (bit-exact with the mmcv CPU/CUDA kernels): c = floor((p-min)/vs) per axis in
+ * float32, point rejected if c<0 || c>=round((max-min)/vs); voxel ids in order of the
+ * first point that lands in them; new voxels beyond max_voxels dropped; at most
+ * max_points points per voxel, kept in point order; unused slots zero.
+ */
+size_t rpc_hard_voxelize_workspace_size(int total_points, int batch);
+int rpc_hard_voxelize(const float* points, int num_features, int total_points,
+                      const int* frame_offsets, int batch,
+                      const float* voxel_size /* host [3] */, const float* coors_range /* host [6] */,
+                      int max_points, int max_voxels,
+                      float* voxels, int* coors, int* num_points, int* voxel_num,
+                      void* workspace, size_t workspace_bytes, void* stream);
+
+/* ------------------------------------------------------------------ a5 HardSimpleVFE
+ * Replaces upstream mmdet3d `HardSimpleVFE.forward` (voxel_encoders/voxel_encoder.py),
+ * used at models/detectors/adversarial_voxelnet.py:135-137:
+ *   out[v, f] = (sum_s voxels[v, s, f]) / num_points[v],  f < vfe_features
+ * backward: dvoxels[v, s, f] = dout[v, f] / num_points[v] for every slot s.
+ */
+int rpc_vfe_mean_forward(const float* voxels, const int* num_points, int num_voxels,
+                         int max_points, int num_features, int vfe_features,
+                         float* out, void* stream);
+int rpc_vfe_mean_backward(const float* dout, const int* num_points, int num_voxels,
+                          int max_points, int num_features, int vfe_features,
+                          float* dvoxels, void* stream);
+
+/* ------------------------------------------------------------------ a2/a3/a4 VoxelPerturber
+ * Replaces `VoxelPerturber.forward` + `_apply_physical_constraints`
+ * (models/adversarial/voxel_perturber.py:120-321, 323-386), the compaction /
+ * masked scatter of `AdversarialVoxelNet.extract_feat`
+ * (models/detectors/adversarial_voxelnet.py:85-117) and, in fused mode, the
+ * HardSimpleVFE that follows it (:135-137). The per-parameter grad hook
+ * `clamp(nan_to_num(g), -0.1, 0.1)` (voxel_perturber.py:465-475) is applied to the
+ * parameter gradients written by rpc_perturber_backward.
+ *
+ * params / grads: host arrays of RPC_PERTURBER_NPARAMS device pointers, order:
+ *   for l in 0..4: W_l [C_{l+1}, C_l], b_l, gamma_l, beta_l, running_mean_l, running_var_l
+ *   W_5 [F, h0], b_5, Wa0 [A, F], ba0 [A], Wa1 [1, A], ba1 [1]
+ * with widths C = (F, h0, h1, h2, h1, h0, F) and A = max(F/2, 1) — the
+ * nn.Sequential layout of voxel_perturber.py:82-112. grads[] entries for running
+ * stats are ignored (may be NULL).
+ *
+ * Modes:
+ *   standalone: num_points == NULL, x = [rows, F] (every row perturbed), out = [rows, F]
+ *   fused:      num_points != NULL, x = voxels [rows, slots, F]; a slot is perturbed
+ *               iff its F features sum to non-zero (adversarial_voxelnet.py:89);
+ *               out = perturbed voxels; vfe_out = [rows, vfe_features] mean of out.
+ * losses: device float[8] = l2_norm, intensity_loss, bias_loss, imbalance_loss,
+ *   n_valid, nan_fallback flag, reserved x2 (voxel_perturber.py:268-299, 312-317).
+ * Train mode updates running_mean/var in place (momentum, unbiased var) like BatchNorm1d.
+ */
+#define RPC_PERTURBER_NPARAMS 36
+
+typedef struct {
+  int F;                  /* point features (4 KITTI, 5 NuScenes) */
+  int hidden[3];          /* hidden_channels */
+  int use_attention;      /* use_spatial_attention */
+  int training;           /* 1 = batch-stat BN + train bounds, 0 = running stats + eval bounds */
+  float sensor_error_bound;
+  float bn_eps;           /* 1e-3 (voxel_perturber.py:462) */
+  float bn_momentum;      /* 0.1  (voxel_perturber.py:461) */
+  int vfe_features;       /* fused mode: HardSimpleVFE num_features (4 KITTI) */
+} rpc_perturber_cfg;
+
+size_t rpc_perturber_workspace_size(const rpc_perturber_cfg* cfg, int rows, int slots);
+int rpc_perturber_forward(const rpc_perturber_cfg* cfg, const float* const* params,
+                          const float* x, int rows, int slots, const int* num_points,
+                          float* out, float* vfe_out, float* losses,
+                          void* workspace, size_t workspace_bytes, void* stream);
+/* dout: standalone [rows, F] = dL/dout; fused [rows, vfe_features] = dL/dvfe_out.
+ * dlosses: device float[4] = dL/d(l2_norm, intensity_loss, bias_loss, imbalance_loss).
+ * The workspace must be the one the matching forward filled. */
+int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float* const* params,
+                           const float* x, int rows, int slots, const int* num_points,
+                           const float* dout, const float* dlosses, float* const* grads,
+                           void* workspace, size_t workspace_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RPC_HIP_H */

@@ -1,0 +1,93 @@
+"""ctypes binding of librpc_hip.so (declared in include/rpc_hip.h).
+
+The product path has no fallback: if the library is missing or cannot be loaded, every
+op raises. Device buffers are torch tensors; only raw pointers and sizes cross the ABI.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import torch
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "librpc_hip.so")
+_lock = threading.Lock()
+_lib = None
+
+RPC_ERRORS = {1: "bad argument", 2: "workspace too small", 3: "unsupported width combination",
+              4: "HIP runtime error"}
+PERTURBER_NPARAMS = 36
+
+vp = C.c_void_p
+i32 = C.c_int
+sz = C.c_size_t
+fp = C.POINTER(C.c_float)
+
+
+class PerturberCfg(C.Structure):
+    _fields_ = [("F", C.c_int), ("hidden", C.c_int * 3), ("use_attention", C.c_int),
+                ("training", C.c_int), ("sensor_error_bound", C.c_float), ("bn_eps", C.c_float),
+                ("bn_momentum", C.c_float), ("vfe_features", C.c_int)]
+
+
+# name -> (restype, argtypes); every symbol here must be exported by the .so
+SIGNATURES = {
+    "rpc_version": (C.c_char_p, []),
+    "rpc_hard_voxelize_workspace_size": (sz, [i32, i32]),
+    "rpc_hard_voxelize": (i32, [vp, i32, i32, vp, i32, fp, fp, i32, i32, vp, vp, vp, vp, vp, sz, vp]),
+    "rpc_vfe_mean_forward": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "rpc_vfe_mean_backward": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "rpc_perturber_workspace_size": (sz, [C.POINTER(PerturberCfg), i32, i32]),
+    "rpc_perturber_forward": (i32, [C.POINTER(PerturberCfg), C.POINTER(vp), vp, i32, i32, vp, vp, vp,
+                                    vp, vp, sz, vp]),
+    "rpc_perturber_backward": (i32, [C.POINTER(PerturberCfg), C.POINTER(vp), vp, i32, i32, vp, vp, vp,
+                                     C.POINTER(vp), vp, sz, vp]),
+}
+
+
+def lib_path() -> str:
+    return _LIB_PATH
+
+
+def load():
+    """Load (once) and return the ctypes library; raises if it is not built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(_LIB_PATH):
+            raise RuntimeError(f"librpc_hip.so not built ({_LIB_PATH}); run "
+                               "`python -m robustpointclouds_amd._build` — there is no CPU fallback")
+        lib = C.CDLL(_LIB_PATH, mode=C.RTLD_GLOBAL)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed: rpc error {rc} ({RPC_ERRORS.get(rc, '?')})")
+
+
+def ptr(t: torch.Tensor | None):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def stream_of(t: torch.Tensor):
+    if not t.is_cuda:
+        raise RuntimeError("rpc_hip ops run on the GPU only (no CPU fallback); got a CPU tensor")
+    return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def workspace(nbytes: int, device) -> torch.Tensor:
+    return torch.empty(max(int(nbytes), 1), dtype=torch.uint8, device=device)
+
+
+def float_arr(vals):
+    return (C.c_float * len(vals))(*[float(v) for v in vals])

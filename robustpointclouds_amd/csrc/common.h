@@ -1,0 +1,64 @@
+// Shared helpers for the gfx950 kernels behind include/rpc_hip.h.
+// Wave = 64 lanes (CDNA4); every block size here is a multiple of 64.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rpc_hip.h"
+
+#define RPC_CHECK(expr)                                   \
+  do {                                                    \
+    hipError_t _e = (expr);                               \
+    if (_e != hipSuccess) return (int)RPC_ERR_HIP;        \
+  } while (0)
+
+#define RPC_LAUNCH_CHECK() RPC_CHECK(hipGetLastError())
+
+namespace rpc {
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+// Last-arriving-block hand-off (cdna_hip_programming.md §5 "In-launch split-K
+// reduction" / Guideline 16): every block has stored its partials with plain stores;
+// each wave drains, the block meets at a barrier, lane 0 releases at agent scope and
+// takes a ticket. The block that draws gridDim.x-1 acquires at agent scope before
+// reading the other blocks' partials. `ticket` must be zero at launch (hipMemsetAsync
+// by the launcher); the last block re-arms it to zero.
+__device__ __forceinline__ bool last_block_arrive(unsigned* ticket, int* lds_flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (t == gridDim.x - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *lds_flag = last;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
+inline int grid_for(long long n, int block, int cap) {
+  long long g = (n + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace rpc

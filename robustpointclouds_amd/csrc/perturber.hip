@@ -1,0 +1,1176 @@
+// a2/a3/a4: VoxelPerturber forward + backward on gfx950, fused with the valid-point
+// compaction / masked scatter of AdversarialVoxelNet.extract_feat and the HardSimpleVFE
+// that follows it.
+//
+// Reference semantics (models/adversarial/voxel_perturber.py):
+//   s     = std(x, dim=0, unbiased) + 1e-6 ; NaN/Inf -> 1                 (:158-163)
+//   xn    = clamp(x / s, -10, 10)                                         (:165-168)
+//   raw   = Tanh(L5(ReLU(BN4(L4(... ReLU(BN0(L0(xn))) ...)))))            (:82-103, :176)
+//   raw  *= sigmoid(La1(ReLU(La0(xn))))                                   (:107-112, :203-205)
+//   pert  = clamp(raw * bound, -cbound, cbound), nan_to_num               (:209-256, :323-365)
+//   out   = x + pert ; l2 = mean ||pert||_2 ; intensity = mean |pert_3| ;
+//   bias  = mean_f |mean_n pert| ; imbalance = std_f(std_n pert)          (:268-299)
+// BatchNorm1d in train mode uses batch statistics (biased var) and updates the running
+// stats with momentum 0.1 and the unbiased var; eval mode uses the running stats.
+//
+// Structure: one launch per layer over the valid points (grid-stride, 256 blocks of 256
+// threads); per-channel batch statistics are reduced per wave with shuffles, per block in
+// LDS and across blocks by the last-arriving block (agent-scope release/acquire ticket),
+// in a fixed order, so results are run-to-run deterministic. Activations z_l are kept in
+// HBM for the backward pass. The weight gradients dW = dZ^T H are split-K reductions over
+// the points (one batched launch for all layers), summed in double in a fixed order and
+// passed through the reference's grad hook clamp(nan_to_num(g), -0.1, 0.1).
+#include <hipcub/hipcub.hpp>
+#include <math.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace rpc {
+namespace pert {
+
+constexpr int BLK = 256;
+constexpr int NWAVE = BLK / 64;
+constexpr int GRID = 256;        // blocks of every per-point pass (= partial rows)
+constexpr int MAXF = 8;
+constexpr int MAXC = 128;
+constexpr int NTICKET = 16;
+
+struct Dev {
+  int F, A, C[7];
+  int S;           // channel stride of the SoA activation buffers (>= N)
+  int rows, slots, fused, training, use_att, vfe_f;
+  float eps, mom;
+  float bscale[MAXF], bclamp[MAXF];
+  const float* x;
+  const int* npts;
+  const float* W[6];
+  const float* b[6];
+  const float* g[5];
+  const float* be[5];
+  float* rm[5];
+  float* rv[5];
+  const float* Wa0;
+  const float* ba0;
+  const float* Wa1;
+  const float* ba1;
+  float* out;
+  float* vfe;
+  float* losses;
+  // workspace
+  int* off;        // fused: [rows+1] exclusive scan of valid-slot counts
+  int* list;       // fused: [rows*slots] slot index of each valid point
+  int* meta;       // [8]: 0 N, 1 fallback flag (NaN / empty)
+  float* xs;       // [MAXF] s_f
+  float* z[5];     // [C_{l+1}][S] channel-major
+  float* bn[5];    // [4*C]: scale, shift, mean, invstd
+  double* bnsum[5];  // backward: [2*C] sum dy, sum dy*xhat
+  double* part;    // [GRID][2*MAXC]
+  float* pstat;    // [4*MAXF]: mean_f, s_f, cimb_f, S
+  unsigned* ticket;
+  float* dz[6];    // dz_0..dz_4 [C_{l+1}][S], dz_5 [F][S]
+  float* dh[2];    // [MAXC][S] post-ReLU grads, ping-pong
+  float* dsig;     // [S]
+  float* da;       // [A][S]
+  float* aact;     // [A][S]
+  float* wpart;    // [KS][total elements] split-K partial weight grads
+  const float* dout;
+  const float* dl;  // [4]
+};
+
+__device__ __forceinline__ int point_slot(const Dev& d, int i) { return d.fused ? d.list[i] : i; }
+
+// per-lane double accumulators for per-channel sums; channel c lives in lane c&63, slot c>>6
+template <int C>
+struct ChanAcc {
+  static constexpr int K = (C + 63) / 64;
+  double s[2][K];
+  __device__ void zero() {
+#pragma unroll
+    for (int k = 0; k < K; ++k) s[0][k] = s[1][k] = 0.0;
+  }
+  // wave-reduce this thread's (v, w) for channel c; lane c&63 keeps the running sums.
+  // c must be a compile-time constant after unrolling (static register index).
+  __device__ __forceinline__ void add1(int c, float v, float w) {
+    const int lane = threadIdx.x & 63;
+    float a = wave_sum(v);
+    float q = wave_sum(w);
+    if (lane == (c & 63)) {
+      s[0][c >> 6] += (double)a;
+      s[1][c >> 6] += (double)q;
+    }
+  }
+  // block-combine into part[blockIdx.x][0..2C)
+  __device__ void flush(double* part, double* lds) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      int c = k * 64 + lane;
+      if (c < C) {
+        lds[(w * 2 + 0) * MAXC + c] = s[0][k];
+        lds[(w * 2 + 1) * MAXC + c] = s[1][k];
+      }
+    }
+    __syncthreads();
+    for (int j = threadIdx.x; j < 2 * C; j += BLK) {
+      int which = j / C, c = j - which * C;
+      double t = 0.0;
+      for (int ww = 0; ww < NWAVE; ++ww) t += lds[(ww * 2 + which) * MAXC + c];
+      part[(size_t)blockIdx.x * 2 * MAXC + j] = t;
+    }
+  }
+};
+
+// thread j < 2C: fixed-order sum of column j over all blocks' partial rows
+__device__ __forceinline__ double col_total(const double* part, int j) {
+  double t = 0.0;
+  for (int r = 0; r < GRID; ++r) t += part[(size_t)r * 2 * MAXC + j];
+  return t;
+}
+
+// finalize a BatchNorm layer from its batch sums (train) — run by the last block
+template <int C>
+__device__ void bn_finalize(Dev& d, int l, double* lds) {
+  const int N = d.meta[0];
+  for (int j = threadIdx.x; j < 2 * C; j += BLK) lds[j] = col_total(d.part, j);
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += BLK) {
+    double mean = lds[c] / N;
+    double var = lds[C + c] / N - mean * mean;
+    if (var < 0) var = 0;
+    float invstd = 1.0f / sqrtf((float)var + d.eps);
+    float sc = d.g[l][c] * invstd;
+    float sh = d.be[l][c] - (float)mean * sc;
+    float* bn = d.bn[l];
+    bn[c] = sc;
+    bn[C + c] = sh;
+    bn[2 * C + c] = (float)mean;
+    bn[3 * C + c] = invstd;
+    double uvar = N > 1 ? var * N / (N - 1) : var;
+    d.rm[l][c] = (1.0f - d.mom) * d.rm[l][c] + d.mom * (float)mean;
+    d.rv[l][c] = (1.0f - d.mom) * d.rv[l][c] + d.mom * (float)uvar;
+  }
+}
+
+// ------------------------------------------------------------------ forward kernels
+// stats of x over the valid points + compaction list + copy of the voxel slots to out
+template <int F>
+__global__ __launch_bounds__(BLK) void k_xstats(Dev d) {
+  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ int lastf;
+  double s1[F], s2[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) s1[f] = s2[f] = 0.0;
+  int nan = 0;
+  const int stride = GRID * BLK;
+  for (int r = blockIdx.x * BLK + threadIdx.x; r < d.rows; r += stride) {
+    if (d.fused) {
+      int base = d.off[r], j = 0;
+      for (int s = 0; s < d.slots; ++s) {
+        size_t slot = (size_t)r * d.slots + s;
+        const float* p = d.x + slot * F;
+        float v[F];
+        float sum = 0.0f;
+#pragma unroll
+        for (int f = 0; f < F; ++f) {
+          v[f] = p[f];
+          sum = f == 0 ? v[0] : sum + v[f];
+          d.out[slot * F + f] = v[f];
+        }
+        if (sum != 0.0f) {
+          d.list[base + j++] = (int)slot;
+#pragma unroll
+          for (int f = 0; f < F; ++f) {
+            s1[f] += v[f];
+            s2[f] += (double)v[f] * v[f];
+            nan |= isnan(v[f]);
+          }
+        }
+      }
+    } else {
+      const float* p = d.x + (size_t)r * F;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        float v = p[f];
+        s1[f] += v;
+        s2[f] += (double)v * v;
+        nan |= isnan(v);
+      }
+    }
+  }
+  // block reduce 2F doubles + nan flag
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    s1[f] = wave_sum(s1[f]);
+    s2[f] = wave_sum(s2[f]);
+  }
+  nan = __any(nan);
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0) {
+#pragma unroll
+    for (int f = 0; f < F; ++f) {
+      lds[w * 2 * MAXC + f] = s1[f];
+      lds[w * 2 * MAXC + F + f] = s2[f];
+    }
+    lds[w * 2 * MAXC + 2 * F] = nan;
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 * F + 1) {
+    double t = 0.0;
+    for (int ww = 0; ww < NWAVE; ++ww) t += lds[ww * 2 * MAXC + threadIdx.x];
+    d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
+  }
+  if (!last_block_arrive(d.ticket + 0, &lastf)) return;
+  if (threadIdx.x < 2 * F + 1) lds[threadIdx.x] = col_total(d.part, threadIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int N = d.fused ? d.off[d.rows] : d.rows;
+    d.meta[0] = N;
+    int flag = (lds[2 * F] != 0.0) || N == 0;
+    d.meta[1] = flag;
+    // s = std(x, unbiased) + 1e-6; any NaN/Inf entry resets the whole vector (:158-163)
+    int bad = 0;
+    for (int f = 0; f < F; ++f) {
+      double mean = lds[f] / N;
+      double var = N > 1 ? (lds[F + f] - N * mean * mean) / (N - 1) : NAN;
+      if (var < 0) var = 0;
+      float s = sqrtf((float)var) + 1e-6f;
+      bad |= (isnan(s) || isinf(s));
+      d.xs[f] = s;
+    }
+    if (bad)
+      for (int f = 0; f < F; ++f) d.xs[f] = 1.0f;
+  }
+}
+
+template <int F>
+__device__ __forceinline__ void load_xn(const Dev& d, int slot, float (&xv)[F], float (&xn)[F]) {
+  const float* p = d.x + (size_t)slot * F;
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    xv[f] = p[f];
+    float t = xv[f] / d.xs[f];
+    xn[f] = fminf(fmaxf(t, -10.0f), 10.0f);
+  }
+}
+
+// layer 0: xn -> z0 (+ batch stats / finalize BN0)
+template <int F, int CO>
+__global__ __launch_bounds__(BLK) void k_fwd_first(Dev d) {
+  __shared__ float sW[CO * F + CO];
+  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ int lastf;
+  for (int j = threadIdx.x; j < CO * F; j += BLK) sW[j] = d.W[0][j];
+  for (int j = threadIdx.x; j < CO; j += BLK) sW[CO * F + j] = d.b[0][j];
+  __syncthreads();
+  const int N = d.meta[0];
+  ChanAcc<CO> acc;
+  acc.zero();
+  for (int t = blockIdx.x; t * BLK < N; t += GRID) {
+    int i = t * BLK + threadIdx.x;
+    bool act = i < N;
+    float xv[F], xn[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) xn[f] = 0.0f;
+    if (act) load_xn<F>(d, point_slot(d, i), xv, xn);
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      float a = sW[CO * F + o];
+#pragma unroll
+      for (int f = 0; f < F; ++f) a = fmaf(sW[o * F + f], xn[f], a);
+      float z = act ? a : 0.0f;
+      if (act) d.z[0][(size_t)o * d.S + i] = z;
+      if (d.training) acc.add1(o, z, z * z);
+    }
+  }
+  if (!d.training) return;
+  acc.flush(d.part, lds);
+  if (!last_block_arrive(d.ticket + 1, &lastf)) return;
+  bn_finalize<CO>(d, 0, lds);
+}
+
+// layer l (1..4): relu(bn_{l-1}(z_{l-1})) -> z_l
+template <int CI, int CO>
+__global__ __launch_bounds__(BLK) void k_fwd_mid(Dev d, int l) {
+  __shared__ float sW[CO * CI + CO + 2 * CI];
+  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ int lastf;
+  for (int j = threadIdx.x; j < CO * CI; j += BLK) sW[j] = d.W[l][j];
+  for (int j = threadIdx.x; j < CO; j += BLK) sW[CO * CI + j] = d.b[l][j];
+  for (int j = threadIdx.x; j < 2 * CI; j += BLK) sW[CO * CI + CO + j] = d.bn[l - 1][j];
+  __syncthreads();
+  const float* sc = sW + CO * CI + CO;
+  const float* sh = sc + CI;
+  const int N = d.meta[0];
+  ChanAcc<CO> acc;
+  acc.zero();
+  for (int t = blockIdx.x; t * BLK < N; t += GRID) {
+    int i = t * BLK + threadIdx.x;
+    bool act = i < N;
+    float h[CI];
+    const float* zi = d.z[l - 1] + (act ? i : 0);
+#pragma unroll
+    for (int c = 0; c < CI; ++c)
+      h[c] = act ? fmaxf(fmaf(zi[(size_t)c * d.S], sc[c], sh[c]), 0.0f) : 0.0f;
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      float a = sW[CO * CI + o];
+#pragma unroll
+      for (int c = 0; c < CI; ++c) a = fmaf(sW[o * CI + c], h[c], a);
+      float z = act ? a : 0.0f;
+      if (act) d.z[l][(size_t)o * d.S + i] = z;
+      if (d.training) acc.add1(o, z, z * z);
+    }
+  }
+  if (!d.training) return;
+  acc.flush(d.part, lds);
+  if (!last_block_arrive(d.ticket + 1 + l, &lastf)) return;
+  bn_finalize<CO>(d, l, lds);
+}
+
+// recompute the attention gate for one point
+template <int F>
+__device__ __forceinline__ float attention(const Dev& d, const float (&xn)[F], float (&a)[MAXF]) {
+  const int A = d.A;
+  float t = d.ba1[0];
+  for (int j = 0; j < A; ++j) {
+    float s = d.ba0[j];
+#pragma unroll
+    for (int f = 0; f < F; ++f) s = fmaf(d.Wa0[j * F + f], xn[f], s);
+    a[j] = fmaxf(s, 0.0f);
+    t = fmaf(d.Wa1[j], a[j], t);
+  }
+  return 1.0f / (1.0f + expf(-t));
+}
+
+// output layer: relu(bn4(z4)) -> tanh -> *att -> bounds -> clamp -> out, loss sums
+template <int CI, int F>
+__global__ __launch_bounds__(BLK) void k_fwd_last(Dev d) {
+  __shared__ float sW[F * CI + F + 2 * CI];
+  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ int lastf;
+  for (int j = threadIdx.x; j < F * CI; j += BLK) sW[j] = d.W[5][j];
+  for (int j = threadIdx.x; j < F; j += BLK) sW[F * CI + j] = d.b[5][j];
+  for (int j = threadIdx.x; j < 2 * CI; j += BLK) sW[F * CI + F + j] = d.bn[4][j];
+  __syncthreads();
+  const float* sc = sW + F * CI + F;
+  const float* sh = sc + CI;
+  const int N = d.meta[0];
+  // sums: [0] sum ||pert||, [1] sum |pert_3|, [2..2+F) sum pert_f, [2+F..2+2F) sum pert_f^2, [2+2F] nan
+  constexpr int NS = 3 + 2 * F;
+  double acc[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) acc[k] = 0.0;
+  for (int t = blockIdx.x; t * BLK < N; t += GRID) {
+    int i = t * BLK + threadIdx.x;
+    bool act = i < N;
+    float v[NS];
+#pragma unroll
+    for (int k = 0; k < NS; ++k) v[k] = 0.0f;
+    if (act) {
+      int slot = point_slot(d, i);
+      float xv[F], xn[F], h[CI];
+      load_xn<F>(d, slot, xv, xn);
+      const float* zi = d.z[4] + i;
+#pragma unroll
+      for (int c = 0; c < CI; ++c) h[c] = fmaxf(fmaf(zi[(size_t)c * d.S], sc[c], sh[c]), 0.0f);
+      float am[MAXF];
+      float att = d.use_att ? attention<F>(d, xn, am) : 1.0f;
+      float nrm2 = 0.0f;
+      int bad = 0;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        float u = sW[F * CI + f];
+#pragma unroll
+        for (int c = 0; c < CI; ++c) u = fmaf(sW[f * CI + c], h[c], u);
+        float raw = tanhf(u);
+        float pp = (raw * att) * d.bscale[f];
+        bad |= isnan(pp);
+        float p = fminf(fmaxf(pp, -d.bclamp[f]), d.bclamp[f]);
+        d.out[(size_t)slot * F + f] = xv[f] + p;
+        nrm2 = fmaf(p, p, nrm2);
+        v[2 + f] = p;
+        v[2 + F + f] = p * p;
+        if (f == 3) v[1] = fabsf(p);
+      }
+      v[0] = sqrtf(nrm2);
+      v[2 + 2 * F] = (float)bad;
+    }
+#pragma unroll
+    for (int k = 0; k < NS; ++k) acc[k] += (double)wave_sum(v[k]);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < NS; ++k) lds[w * 2 * MAXC + k] = acc[k];
+  __syncthreads();
+  if (threadIdx.x < NS) {
+    double t = 0.0;
+    for (int ww = 0; ww < NWAVE; ++ww) t += lds[ww * 2 * MAXC + threadIdx.x];
+    d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
+  }
+  if (!last_block_arrive(d.ticket + 6, &lastf)) return;
+  if (threadIdx.x < NS) lds[threadIdx.x] = col_total(d.part, threadIdx.x);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int n = N;
+    int flag = d.meta[1] || lds[2 + 2 * F] != 0.0;
+    d.meta[1] = flag;
+    float l2 = (float)(lds[0] / n);
+    float inten = F >= 4 ? (float)(lds[1] / n) : 0.0f;
+    float bias = 0.0f, S = 0.0f;
+    float sf[F], mf[F];
+    for (int f = 0; f < F; ++f) {
+      double m = lds[2 + f] / n;
+      double var = n > 1 ? (lds[2 + F + f] - n * m * m) / (n - 1) : NAN;
+      if (var < 0) var = 0;
+      mf[f] = (float)m;
+      sf[f] = sqrtf((float)var);
+      bias += fabsf(mf[f]);
+      S += sf[f];
+    }
+    bias /= F;
+    S /= F;
+    float q = 0.0f;
+    for (int f = 0; f < F; ++f) q += (sf[f] - S) * (sf[f] - S);
+    float imb = sqrtf(q / (F - 1));
+    for (int f = 0; f < F; ++f) {
+      d.pstat[f] = mf[f];
+      d.pstat[MAXF + f] = sf[f];
+      // d imb / d pert[n,f] = cimb_f * (pert[n,f] - mean_f)
+      float ci = (imb > 0.0f && sf[f] > 0.0f && n > 1)
+                     ? (sf[f] - S) / ((F - 1) * imb) / ((n - 1) * sf[f])
+                     : 0.0f;
+      d.pstat[2 * MAXF + f] = ci;
+    }
+    if (flag) l2 = inten = bias = imb = 0.0f;
+    d.losses[0] = l2;
+    d.losses[1] = inten;
+    d.losses[2] = bias;
+    d.losses[3] = imb;
+    d.losses[4] = (float)n;
+    d.losses[5] = (float)flag;
+    d.losses[6] = 0.0f;
+    d.losses[7] = 0.0f;
+  }
+}
+
+// fused VFE: mean over the slots of the (perturbed) voxel; the unperturbed voxels when the
+// NaN / empty fallback fired (adversarial_voxelnet.py:123-132).
+__global__ __launch_bounds__(BLK) void k_vfe(Dev d, int F) {
+  int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= d.rows * d.vfe_f) return;
+  int v = t / d.vfe_f, f = t - v * d.vfe_f;
+  const float* src = d.meta[1] ? d.x : d.out;
+  const float* p = src + (size_t)v * d.slots * F + f;
+  float s = p[0];
+  for (int j = 1; j < d.slots; ++j) s += p[(size_t)j * F];
+  d.vfe[t] = s / (float)d.npts[v];
+}
+
+// fallback: out = x (unperturbed) when the flag is set
+__global__ __launch_bounds__(BLK) void k_restore(Dev d, int F) {
+  if (!d.meta[1]) return;
+  long long n = (long long)d.rows * d.slots * F;
+  for (long long t = (long long)blockIdx.x * BLK + threadIdx.x; t < n; t += (long long)gridDim.x * BLK)
+    d.out[t] = d.x[t];
+}
+
+// eval mode: BN scale/shift from the running stats
+__global__ void k_bn_eval(Dev d) {
+  for (int l = 0; l < 5; ++l) {
+    int C = d.C[l + 1];
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+      float invstd = 1.0f / sqrtf(d.rv[l][c] + d.eps);
+      float sc = d.g[l][c] * invstd;
+      d.bn[l][c] = sc;
+      d.bn[l][C + c] = d.be[l][c] - d.rm[l][c] * sc;
+      d.bn[l][2 * C + c] = d.rm[l][c];
+      d.bn[l][3 * C + c] = invstd;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ backward kernels
+template <int C>
+__device__ void bnb_finalize(Dev& d, int l, double* lds) {
+  for (int j = threadIdx.x; j < 2 * C; j += BLK) d.bnsum[l][j] = col_total(d.part, j);
+}
+
+// output layer + attention: dz5 = d u, dsig, da, a, dh4' and BN4 backward sums
+template <int CI, int F>
+__global__ __launch_bounds__(BLK) void k_bwd_last(Dev d) {
+  __shared__ float sW[F * CI + F + 4 * CI];
+  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ int lastf;
+  for (int j = threadIdx.x; j < F * CI; j += BLK) sW[j] = d.W[5][j];
+  for (int j = threadIdx.x; j < F; j += BLK) sW[F * CI + j] = d.b[5][j];
+  for (int j = threadIdx.x; j < 4 * CI; j += BLK) sW[F * CI + F + j] = d.bn[4][j];
+  __syncthreads();
+  const float* sc = sW + F * CI + F;
+  const float* sh = sc + CI;
+  const float* mean4 = sh + CI;
+  const float* inv4 = mean4 + CI;
+  const int N = d.meta[0];
+  const float gl2 = d.dl[0], gint = d.dl[1], gbias = d.dl[2], gimb = d.dl[3];
+  const float invN = 1.0f / (float)N;
+  ChanAcc<CI> acc;
+  acc.zero();
+  for (int t = blockIdx.x; t * BLK < N; t += GRID) {
+    int i = t * BLK + threadIdx.x;
+    bool act = i < N;
+    float du[F];
+#pragma unroll
+    for (int f = 0; f < F; ++f) du[f] = 0.0f;
+    const float* zi = d.z[4] + (act ? i : 0);
+    if (act) {
+      int slot = point_slot(d, i);
+      float xv[F], xn[F], h[CI];
+      load_xn<F>(d, slot, xv, xn);
+#pragma unroll
+      for (int c = 0; c < CI; ++c) h[c] = fmaxf(fmaf(zi[(size_t)c * d.S], sc[c], sh[c]), 0.0f);
+      float am[MAXF];
+      float att = d.use_att ? attention<F>(d, xn, am) : 1.0f;
+      float raw[F], pp[F], p[F], dout[F];
+      float nrm2 = 0.0f;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        float u = sW[F * CI + f];
+#pragma unroll
+        for (int c = 0; c < CI; ++c) u = fmaf(sW[f * CI + c], h[c], u);
+        raw[f] = tanhf(u);
+        pp[f] = (raw[f] * att) * d.bscale[f];
+        p[f] = fminf(fmaxf(pp[f], -d.bclamp[f]), d.bclamp[f]);
+        nrm2 = fmaf(p[f], p[f], nrm2);
+      }
+      if (d.fused) {
+        int v = slot / d.slots;
+        float rn = 1.0f / (float)d.npts[v];
+#pragma unroll
+        for (int f = 0; f < F; ++f) dout[f] = f < d.vfe_f ? d.dout[(size_t)v * d.vfe_f + f] * rn : 0.0f;
+      } else {
+#pragma unroll
+        for (int f = 0; f < F; ++f) dout[f] = d.dout[(size_t)i * F + f];
+      }
+      float nrm = sqrtf(nrm2);
+      float datt = 0.0f;
+#pragma unroll
+      for (int f = 0; f < F; ++f) {
+        float g = dout[f];
+        if (nrm > 0.0f) g += gl2 * invN * (p[f] / nrm);
+        if (f == 3) g += gint * invN * (float)((p[3] > 0.0f) - (p[3] < 0.0f));
+        float m = d.pstat[f];
+        g += gbias * invN / (float)F * (float)((m > 0.0f) - (m < 0.0f));
+        g += gimb * d.pstat[2 * MAXF + f] * (p[f] - m);
+        float dpp = (pp[f] >= -d.bclamp[f] && pp[f] <= d.bclamp[f]) ? g : 0.0f;
+        float draw = dpp * att * d.bscale[f];
+        datt = fmaf(dpp * raw[f], d.bscale[f], datt);
+        du[f] = draw * (1.0f - raw[f] * raw[f]);
+        d.dz[5][(size_t)f * d.S + i] = du[f];
+      }
+      if (d.use_att) {
+        float dt = datt * att * (1.0f - att);
+        d.dsig[i] = dt;
+        for (int j = 0; j < d.A; ++j) {
+          d.aact[(size_t)j * d.S + i] = am[j];
+          d.da[(size_t)j * d.S + i] = am[j] > 0.0f ? d.Wa1[j] * dt : 0.0f;
+        }
+      }
+    }
+    // dh4' = relu'(h4) * W5^T du, and the BN4 backward sums
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      float s = 0.0f, sx = 0.0f;
+      if (act) {
+#pragma unroll
+        for (int f = 0; f < F; ++f) s = fmaf(sW[f * CI + c], du[f], s);
+        float zc = zi[(size_t)c * d.S];
+        float hv = fmaxf(fmaf(zc, sc[c], sh[c]), 0.0f);
+        s = hv > 0.0f ? s : 0.0f;
+        d.dh[0][(size_t)c * d.S + i] = s;
+        sx = s * ((zc - mean4[c]) * inv4[c]);
+      }
+      acc.add1(c, s, sx);
+    }
+  }
+  acc.flush(d.part, lds);
+  if (!last_block_arrive(d.ticket + 7, &lastf)) return;
+  bnb_finalize<CI>(d, 4, lds);
+}
+
+// BN layer l backward (l = 4..1): dz_l from dh_l'; dh_{l-1}' = relu'(.) * W_l^T dz_l
+template <int CI, int CO>
+__global__ __launch_bounds__(BLK) void k_bwd_mid(Dev d, int l, int src) {
+  __shared__ float sW[CO * CI + 7 * CO + 4 * CI];
+  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ int lastf;
+  const int N = d.meta[0];
+  const double invN = 1.0 / N;
+  for (int j = threadIdx.x; j < CO * CI; j += BLK) sW[j] = d.W[l][j];
+  for (int j = threadIdx.x; j < 4 * CO; j += BLK) sW[CO * CI + j] = d.bn[l][j];
+  for (int j = threadIdx.x; j < 4 * CI; j += BLK) sW[CO * CI + 4 * CO + j] = d.bn[l - 1][j];
+  for (int j = threadIdx.x; j < CO; j += BLK) {
+    float* m = sW + CO * CI + 4 * CO + 4 * CI;
+    m[j] = (float)(d.bnsum[l][j] * invN);
+    m[CO + j] = (float)(d.bnsum[l][CO + j] * invN);
+    m[2 * CO + j] = d.g[l][j] * d.bn[l][3 * CO + j];
+  }
+  __syncthreads();
+  const float* bo = sW + CO * CI;      // scale, shift, mean, invstd of layer l
+  const float* bi = bo + 4 * CO;       // of layer l-1
+  const float* m1 = bi + 4 * CI;
+  const float* m2 = m1 + CO;
+  const float* gi = m2 + CO;
+  ChanAcc<CI> acc;
+  acc.zero();
+  for (int t = blockIdx.x; t * BLK < N; t += GRID) {
+    int i = t * BLK + threadIdx.x;
+    bool act = i < N;
+    int ii = act ? i : 0;
+    const float* dhi = d.dh[src] + ii;
+    const float* zl = d.z[l] + ii;
+    float dz[CO];
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      float xh = (zl[(size_t)o * d.S] - bo[2 * CO + o]) * bo[3 * CO + o];
+      dz[o] = act ? gi[o] * (dhi[(size_t)o * d.S] - m1[o] - xh * m2[o]) : 0.0f;
+      if (act) d.dz[l][(size_t)o * d.S + i] = dz[o];
+    }
+    const float* zp = d.z[l - 1] + ii;
+#pragma unroll
+    for (int c = 0; c < CI; ++c) {
+      float s = 0.0f;
+#pragma unroll
+      for (int o = 0; o < CO; ++o) s = fmaf(sW[o * CI + c], dz[o], s);
+      float zc = zp[(size_t)c * d.S];
+      float hv = fmaxf(fmaf(zc, bi[c], bi[CI + c]), 0.0f);
+      s = (act && hv > 0.0f) ? s : 0.0f;
+      if (act) d.dh[src ^ 1][(size_t)c * d.S + i] = s;
+      acc.add1(c, s, s * ((zc - bi[2 * CI + c]) * bi[3 * CI + c]));
+    }
+  }
+  acc.flush(d.part, lds);
+  if (!last_block_arrive(d.ticket + 7 + (5 - l), &lastf)) return;
+  bnb_finalize<CI>(d, l - 1, lds);
+}
+
+// layer 0: dz_0 from dh_0'
+template <int CO>
+__global__ __launch_bounds__(BLK) void k_bwd_first(Dev d, int src) {
+  const int N = d.meta[0];
+  const double invN = 1.0 / N;
+  const float* bo = d.bn[0];
+  for (int i = blockIdx.x * BLK + threadIdx.x; i < N; i += GRID * BLK) {
+#pragma unroll
+    for (int o = 0; o < CO; ++o) {
+      float m1 = (float)(d.bnsum[0][o] * invN), m2 = (float)(d.bnsum[0][CO + o] * invN);
+      float xh = (d.z[0][(size_t)o * d.S + i] - bo[2 * CO + o]) * bo[3 * CO + o];
+      d.dz[0][(size_t)o * d.S + i] =
+          d.g[0][o] * bo[3 * CO + o] * (d.dh[src][(size_t)o * d.S + i] - m1 - xh * m2);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ weight gradients
+// job: dW[o][i] = sum_n dz[n][o] * h[n][i] ; i == CI is the bias column (h = 1)
+enum HSrc { H_XN = 0, H_BNRELU = 1, H_RAW = 2 };
+struct Job {
+  const float* dz;  // [CO][S]
+  int CO, CI;
+  int hsrc;         // HSrc
+  const float* h;   // H_BNRELU: z_{l-1} ; H_RAW: activations, both [CI][S]
+  const float* bn;  // H_BNRELU: scale/shift of layer l-1
+  int eoff;         // element offset in wpart rows
+  int nelem;        // CO * (CI + 1)
+};
+constexpr int MAXJOB = 8;
+struct Jobs {
+  Job j[MAXJOB];
+  int njob;
+  int echunks[MAXJOB];  // element chunks per job
+  int cbase[MAXJOB];    // first chunk id of each job
+  int KS;               // row splits
+  int total;            // total elements over jobs
+};
+constexpr int EPT = 8;
+constexpr int TR = 64;
+
+template <int F>
+__global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
+  __shared__ float sdz[TR * (MAXC + 1)];
+  __shared__ float shh[TR * (MAXC + 1)];
+  int chunk = blockIdx.x / J.KS, ks = blockIdx.x - chunk * J.KS;
+  int jb = 0;
+  while (jb + 1 < J.njob && chunk >= J.cbase[jb + 1]) ++jb;
+  const Job& job = J.j[jb];
+  const int e0 = (chunk - J.cbase[jb]) * BLK * EPT;
+  const int CO = job.CO, CI = job.CI, CI1 = CI + 1;
+  const int N = d.meta[0];
+  const int rows_per = (N + J.KS - 1) / J.KS;
+  const int r0 = ks * rows_per, r1 = min(N, r0 + rows_per);
+  float acc[EPT];
+  int eo[EPT], ei[EPT];
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    acc[k] = 0.0f;
+    int e = e0 + k * BLK + threadIdx.x;
+    eo[k] = e < job.nelem ? e / CI1 : -1;
+    ei[k] = e < job.nelem ? e - (e / CI1) * CI1 : 0;
+  }
+  for (int rb = r0; rb < r1; rb += TR) {
+    int nr = min(TR, r1 - rb);
+    __syncthreads();
+    for (int q = threadIdx.x; q < TR * CO; q += BLK) {
+      int o = q / TR, r = q - o * TR;
+      sdz[r * (MAXC + 1) + o] = r < nr ? job.dz[(size_t)o * d.S + rb + r] : 0.0f;
+    }
+    for (int q = threadIdx.x; q < TR * CI1; q += BLK) {
+      int c = q / TR, r = q - c * TR;
+      float v = 0.0f;
+      if (r < nr) {
+        int n = rb + r;
+        if (c == CI) v = 1.0f;
+        else if (job.hsrc == H_XN) {
+          int slot = point_slot(d, n);
+          float t = d.x[(size_t)slot * F + c] / d.xs[c];
+          v = fminf(fmaxf(t, -10.0f), 10.0f);
+        } else if (job.hsrc == H_BNRELU) {
+          v = fmaxf(fmaf(job.h[(size_t)c * d.S + n], job.bn[c], job.bn[CI + c]), 0.0f);
+        } else {
+          v = job.h[(size_t)c * d.S + n];
+        }
+      }
+      shh[r * (MAXC + 1) + c] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < EPT; ++k) {
+      if (eo[k] < 0) continue;
+      float a = acc[k];
+      const float* pz = sdz + eo[k];
+      const float* ph = shh + ei[k];
+      for (int r = 0; r < TR; ++r) a = fmaf(pz[r * (MAXC + 1)], ph[r * (MAXC + 1)], a);
+      acc[k] = a;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < EPT; ++k) {
+    int e = e0 + k * BLK + threadIdx.x;
+    if (e < job.nelem) d.wpart[(size_t)ks * J.total + job.eoff + e] = acc[k];
+  }
+}
+
+__device__ __forceinline__ float grad_hook(float g) {
+  // clamp(nan_to_num(g, nan=0, posinf=0, neginf=0), -0.1, 0.1)  (voxel_perturber.py:465-470)
+  if (isnan(g) || isinf(g)) g = 0.0f;
+  return fminf(fmaxf(g, -0.1f), 0.1f);
+}
+
+struct GradOut {
+  float* W[MAXJOB];
+  float* b[MAXJOB];
+  float* gg[5];
+  float* gb[5];
+};
+
+__global__ __launch_bounds__(BLK) void k_wgrad_reduce(Dev d, Jobs J, GradOut G) {
+  int e = blockIdx.x * BLK + threadIdx.x;
+  int flag = d.meta[1];
+  if (e < J.total) {
+    int jb = 0;
+    while (jb + 1 < J.njob && e >= J.j[jb + 1].eoff) ++jb;
+    const Job& job = J.j[jb];
+    int le = e - job.eoff;
+    double s = 0.0;
+    for (int k = 0; k < J.KS; ++k) s += d.wpart[(size_t)k * J.total + e];
+    float g = flag ? 0.0f : grad_hook((float)s);
+    int CI1 = job.CI + 1, o = le / CI1, i = le - o * CI1;
+    if (i < job.CI) { if (G.W[jb]) G.W[jb][o * job.CI + i] = g; }
+    else if (G.b[jb]) G.b[jb][o] = g;
+  }
+  // BatchNorm gamma / beta: sum dy*xhat, sum dy
+  int t = e - J.total;
+  if (t >= 0) {
+    int l = 0, base = 0;
+    while (l < 5 && t >= base + d.C[l + 1]) { base += d.C[l + 1]; ++l; }
+    if (l < 5) {
+      int c = t - base, C = d.C[l + 1];
+      float gg = flag ? 0.0f : grad_hook((float)d.bnsum[l][C + c]);
+      float gb = flag ? 0.0f : grad_hook((float)d.bnsum[l][c]);
+      if (G.gg[l]) G.gg[l][c] = gg;
+      if (G.gb[l]) G.gb[l][c] = gb;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ host side
+static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct Layout {
+  size_t off, list, meta, xs, z[5], bn[5], bnsum[5], part, pstat, ticket, dz[6], dh[2], dsig, da,
+      aact, wpart, scan_tmp, scan_bytes, total;
+};
+
+struct ValidCount {
+  const float* x;
+  int slots, F, rows;
+  __host__ __device__ int operator()(int v) const {
+    if (v >= rows) return 0;
+    int c = 0;
+    for (int s = 0; s < slots; ++s) {
+      const float* p = x + ((size_t)v * slots + s) * F;
+      float sum = p[0];
+      for (int f = 1; f < F; ++f) sum += p[f];
+      c += (sum != 0.0f);
+    }
+    return c;
+  }
+};
+using CountIt = hipcub::TransformInputIterator<int, ValidCount, hipcub::CountingInputIterator<int>>;
+
+constexpr int KS_MAX = 64;
+
+static int widths(const rpc_perturber_cfg* cfg, int C[7]) {
+  C[0] = cfg->F;
+  C[1] = cfg->hidden[0];
+  C[2] = cfg->hidden[1];
+  C[3] = cfg->hidden[2];
+  C[4] = cfg->hidden[1];
+  C[5] = cfg->hidden[0];
+  C[6] = cfg->F;
+  if (cfg->F < 4 || cfg->F > 5) return RPC_ERR_UNSUPPORTED;
+  for (int k = 1; k < 6; ++k)
+    if (C[k] != 8 && C[k] != 16 && C[k] != 32 && C[k] != 64 && C[k] != 128) return RPC_ERR_UNSUPPORTED;
+  return RPC_OK;
+}
+
+static int make_layout(const rpc_perturber_cfg* cfg, int rows, int slots, Layout* L) {
+  int C[7];
+  int rc = widths(cfg, C);
+  if (rc) return rc;
+  size_t Nmax = (size_t)rows * slots;
+  if (Nmax < 1) Nmax = 1;
+  size_t scan_b = 0;
+  ValidCount vc{nullptr, slots, cfg->F, rows};
+  CountIt it(hipcub::CountingInputIterator<int>(0), vc);
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, it, (int*)nullptr, rows + 1, (hipStream_t)0) !=
+      hipSuccess)
+    return RPC_ERR_HIP;
+  int A = cfg->F / 2 > 1 ? cfg->F / 2 : 1;
+  size_t welems = 0;
+  for (int l = 0; l < 6; ++l) welems += (size_t)C[l + 1] * (C[l] + 1);
+  welems += (size_t)A * (cfg->F + 1) + (size_t)(A + 1);
+  size_t o = 0;
+  L->off = o; o += al(sizeof(int) * (rows + 2));
+  L->list = o; o += al(sizeof(int) * Nmax);
+  L->meta = o; o += al(sizeof(int) * 8);
+  L->xs = o; o += al(sizeof(float) * MAXF);
+  for (int l = 0; l < 5; ++l) { L->z[l] = o; o += al(sizeof(float) * Nmax * C[l + 1]); }
+  for (int l = 0; l < 5; ++l) { L->bn[l] = o; o += al(sizeof(float) * 4 * C[l + 1]); }
+  for (int l = 0; l < 5; ++l) { L->bnsum[l] = o; o += al(sizeof(double) * 2 * C[l + 1]); }
+  L->part = o; o += al(sizeof(double) * GRID * 2 * MAXC);
+  L->pstat = o; o += al(sizeof(float) * 4 * MAXF);
+  L->ticket = o; o += al(sizeof(unsigned) * NTICKET);
+  for (int l = 0; l < 5; ++l) { L->dz[l] = o; o += al(sizeof(float) * Nmax * C[l + 1]); }
+  L->dz[5] = o; o += al(sizeof(float) * Nmax * cfg->F);
+  int cmax = 0;
+  for (int k = 1; k < 6; ++k) cmax = C[k] > cmax ? C[k] : cmax;
+  for (int k = 0; k < 2; ++k) { L->dh[k] = o; o += al(sizeof(float) * Nmax * cmax); }
+  L->dsig = o; o += al(sizeof(float) * Nmax);
+  L->da = o; o += al(sizeof(float) * Nmax * A);
+  L->aact = o; o += al(sizeof(float) * Nmax * A);
+  L->wpart = o; o += al(sizeof(float) * KS_MAX * welems);
+  L->scan_tmp = o; o += al(scan_b);
+  L->scan_bytes = scan_b;
+  L->total = o;
+  return RPC_OK;
+}
+
+static void float_bounds(const rpc_perturber_cfg* cfg, Dev& d) {
+  // exact float32 op order of voxel_perturber.py:209-256 and :333-359
+  const int F = cfg->F;
+  const float e = cfg->sensor_error_bound;
+  for (int f = 0; f < MAXF; ++f) d.bscale[f] = d.bclamp[f] = 0.0f;
+  if (F == 4) {
+    if (!cfg->training) {
+      float eb = e;
+      volatile float mult = (float)(2.5 * ((2.0 + 1.5 + 1.2) / 3.0));
+      eb = eb * mult;
+      for (int f = 0; f < 3; ++f) d.bscale[f] = eb * 2.0f;
+      d.bscale[3] = 1.5f;
+      volatile float fb = e * 5.0f;
+      for (int f = 0; f < 3; ++f) d.bclamp[f] = fb * 5.0f;
+      d.bclamp[3] = 2.0f;
+    } else {
+      volatile float eb = e * 0.8f;
+      for (int f = 0; f < 3; ++f) d.bscale[f] = eb * 1.3f;
+      d.bscale[3] = 0.2f;
+      volatile float fb = e * 0.9f;
+      for (int f = 0; f < 3; ++f) d.bclamp[f] = fb * 1.2f;
+      d.bclamp[3] = 0.1f;
+    }
+  } else {
+    for (int f = 0; f < 4; ++f) d.bscale[f] = d.bclamp[f] = e;
+  }
+}
+
+static int fill_dev(const rpc_perturber_cfg* cfg, const float* const* P, const float* x, int rows,
+                    int slots, const int* npts, void* ws, size_t wsb, Dev& d, Layout& L) {
+  int rc = make_layout(cfg, rows, slots, &L);
+  if (rc) return rc;
+  if (wsb < L.total) return RPC_ERR_WORKSPACE;
+  memset(&d, 0, sizeof(d));
+  d.F = cfg->F;
+  d.A = cfg->F / 2 > 1 ? cfg->F / 2 : 1;
+  widths(cfg, d.C);
+  d.rows = rows;
+  d.slots = slots;
+  d.S = rows * slots;
+  d.fused = npts != nullptr;
+  d.training = cfg->training;
+  d.use_att = cfg->use_attention;
+  d.vfe_f = cfg->vfe_features;
+  d.eps = cfg->bn_eps;
+  d.mom = cfg->bn_momentum;
+  float_bounds(cfg, d);
+  d.x = x;
+  d.npts = npts;
+  for (int l = 0; l < 5; ++l) {
+    d.W[l] = P[6 * l + 0];
+    d.b[l] = P[6 * l + 1];
+    d.g[l] = P[6 * l + 2];
+    d.be[l] = P[6 * l + 3];
+    d.rm[l] = (float*)P[6 * l + 4];
+    d.rv[l] = (float*)P[6 * l + 5];
+  }
+  d.W[5] = P[30];
+  d.b[5] = P[31];
+  d.Wa0 = P[32];
+  d.ba0 = P[33];
+  d.Wa1 = P[34];
+  d.ba1 = P[35];
+  char* w = (char*)ws;
+  d.off = (int*)(w + L.off);
+  d.list = (int*)(w + L.list);
+  d.meta = (int*)(w + L.meta);
+  d.xs = (float*)(w + L.xs);
+  for (int l = 0; l < 5; ++l) {
+    d.z[l] = (float*)(w + L.z[l]);
+    d.bn[l] = (float*)(w + L.bn[l]);
+    d.bnsum[l] = (double*)(w + L.bnsum[l]);
+  }
+  d.part = (double*)(w + L.part);
+  d.pstat = (float*)(w + L.pstat);
+  d.ticket = (unsigned*)(w + L.ticket);
+  for (int l = 0; l < 6; ++l) d.dz[l] = (float*)(w + L.dz[l]);
+  d.dh[0] = (float*)(w + L.dh[0]);
+  d.dh[1] = (float*)(w + L.dh[1]);
+  d.dsig = (float*)(w + L.dsig);
+  d.da = (float*)(w + L.da);
+  d.aact = (float*)(w + L.aact);
+  d.wpart = (float*)(w + L.wpart);
+  return RPC_OK;
+}
+
+// ---- width dispatch
+#define RPC_HID(X) X(8) X(16) X(32) X(64) X(128)
+
+template <int F>
+static int launch_first(int C0, Dev& d, hipStream_t st) {
+  switch (C0) {
+#define CASE(c) case c: hipLaunchKernelGGL((k_fwd_first<F, c>), dim3(GRID), dim3(BLK), 0, st, d); break;
+    RPC_HID(CASE)
+#undef CASE
+    default: return RPC_ERR_UNSUPPORTED;
+  }
+  return RPC_OK;
+}
+template <int F>
+static int launch_last(int CI, Dev& d, hipStream_t st, bool bwd) {
+  switch (CI) {
+#define CASE(c)                                                                          \
+  case c:                                                                                \
+    if (bwd) hipLaunchKernelGGL((k_bwd_last<c, F>), dim3(GRID), dim3(BLK), 0, st, d);    \
+    else hipLaunchKernelGGL((k_fwd_last<c, F>), dim3(GRID), dim3(BLK), 0, st, d);        \
+    break;
+    RPC_HID(CASE)
+#undef CASE
+    default: return RPC_ERR_UNSUPPORTED;
+  }
+  return RPC_OK;
+}
+template <int CI>
+static int launch_mid_co(int CO, Dev& d, int l, hipStream_t st, bool bwd, int src) {
+  switch (CO) {
+#define CASE(c)                                                                                \
+  case c:                                                                                      \
+    if (bwd) hipLaunchKernelGGL((k_bwd_mid<CI, c>), dim3(GRID), dim3(BLK), 0, st, d, l, src);  \
+    else hipLaunchKernelGGL((k_fwd_mid<CI, c>), dim3(GRID), dim3(BLK), 0, st, d, l);           \
+    break;
+    RPC_HID(CASE)
+#undef CASE
+    default: return RPC_ERR_UNSUPPORTED;
+  }
+  return RPC_OK;
+}
+static int launch_mid(int CI, int CO, Dev& d, int l, hipStream_t st, bool bwd, int src = 0) {
+  switch (CI) {
+#define CASE(c) case c: return launch_mid_co<c>(CO, d, l, st, bwd, src);
+    RPC_HID(CASE)
+#undef CASE
+    default: return RPC_ERR_UNSUPPORTED;
+  }
+}
+static int launch_bwd_first(int CO, Dev& d, hipStream_t st, int src) {
+  switch (CO) {
+#define CASE(c) case c: hipLaunchKernelGGL((k_bwd_first<c>), dim3(GRID), dim3(BLK), 0, st, d, src); break;
+    RPC_HID(CASE)
+#undef CASE
+    default: return RPC_ERR_UNSUPPORTED;
+  }
+  return RPC_OK;
+}
+
+}  // namespace pert
+}  // namespace rpc
+
+using namespace rpc;
+using namespace rpc::pert;
+
+extern "C" size_t rpc_perturber_workspace_size(const rpc_perturber_cfg* cfg, int rows, int slots) {
+  Layout L;
+  if (!cfg || make_layout(cfg, rows, slots, &L) != RPC_OK) return 0;
+  return L.total;
+}
+
+extern "C" int rpc_perturber_forward(const rpc_perturber_cfg* cfg, const float* const* params,
+                                     const float* x, int rows, int slots, const int* num_points,
+                                     float* out, float* vfe_out, float* losses, void* workspace,
+                                     size_t workspace_bytes, void* stream) {
+  if (!cfg || !params || !x || !out || !losses || rows < 1 || slots < 1) return RPC_ERR_ARG;
+  if (num_points && (!vfe_out || cfg->vfe_features < 1 || cfg->vfe_features > cfg->F)) return RPC_ERR_ARG;
+  if (!num_points && slots != 1) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  Dev d;
+  Layout L;
+  int rc = fill_dev(cfg, params, x, rows, slots, num_points, workspace, workspace_bytes, d, L);
+  if (rc) return rc;
+  d.out = out;
+  d.vfe = vfe_out;
+  d.losses = losses;
+  RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET, st));
+  if (d.fused) {
+    ValidCount vc{x, slots, cfg->F, rows};
+    CountIt it(hipcub::CountingInputIterator<int>(0), vc);
+    size_t sb = L.scan_bytes;
+    RPC_CHECK(hipcub::DeviceScan::ExclusiveSum((char*)workspace + L.scan_tmp, sb, it, d.off,
+                                               rows + 1, st));
+  }
+  const int F = cfg->F;
+  if (F == 4) hipLaunchKernelGGL((k_xstats<4>), dim3(GRID), dim3(BLK), 0, st, d);
+  else hipLaunchKernelGGL((k_xstats<5>), dim3(GRID), dim3(BLK), 0, st, d);
+  RPC_LAUNCH_CHECK();
+  if (!cfg->training) {
+    hipLaunchKernelGGL(k_bn_eval, dim3(1), dim3(BLK), 0, st, d);
+    RPC_LAUNCH_CHECK();
+  }
+  rc = F == 4 ? launch_first<4>(d.C[1], d, st) : launch_first<5>(d.C[1], d, st);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  for (int l = 1; l < 5; ++l) {
+    rc = launch_mid(d.C[l], d.C[l + 1], d, l, st, false);
+    if (rc) return rc;
+    RPC_LAUNCH_CHECK();
+  }
+  rc = F == 4 ? launch_last<4>(d.C[5], d, st, false) : launch_last<5>(d.C[5], d, st, false);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  int ng = grid_for((long long)rows * slots * F, BLK, 1024);
+  hipLaunchKernelGGL(k_restore, dim3(ng), dim3(BLK), 0, st, d, F);
+  RPC_LAUNCH_CHECK();
+  if (d.fused) {
+    int nv = (rows * d.vfe_f + BLK - 1) / BLK;
+    hipLaunchKernelGGL(k_vfe, dim3(nv), dim3(BLK), 0, st, d, F);
+    RPC_LAUNCH_CHECK();
+  }
+  return RPC_OK;
+}
+
+extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float* const* params,
+                                      const float* x, int rows, int slots, const int* num_points,
+                                      const float* dout, const float* dlosses, float* const* grads,
+                                      void* workspace, size_t workspace_bytes, void* stream) {
+  if (!cfg || !params || !x || !dout || !dlosses || !grads || rows < 1 || slots < 1) return RPC_ERR_ARG;
+  if (!cfg->training) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  Dev d;
+  Layout L;
+  int rc = fill_dev(cfg, params, x, rows, slots, num_points, workspace, workspace_bytes, d, L);
+  if (rc) return rc;
+  d.dout = dout;
+  d.dl = dlosses;
+  RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET, st));
+  const int F = cfg->F;
+  rc = F == 4 ? launch_last<4>(d.C[5], d, st, true) : launch_last<5>(d.C[5], d, st, true);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  int src = 0;
+  for (int l = 4; l >= 1; --l) {
+    rc = launch_mid(d.C[l], d.C[l + 1], d, l, st, true, src);
+    if (rc) return rc;
+    RPC_LAUNCH_CHECK();
+    src ^= 1;
+  }
+  rc = launch_bwd_first(d.C[1], d, st, src);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  // weight-gradient jobs
+  Jobs J;
+  memset(&J, 0, sizeof(J));
+  GradOut G;
+  memset(&G, 0, sizeof(G));
+  int nj = 0, eoff = 0;
+  auto add = [&](const float* dz, int CO, int CI, int hsrc, const float* h, const float* bn,
+                 float* gW, float* gb) {
+    Job& j = J.j[nj];
+    j.dz = dz; j.CO = CO; j.CI = CI; j.hsrc = hsrc; j.h = h; j.bn = bn;
+    j.eoff = eoff; j.nelem = CO * (CI + 1);
+    G.W[nj] = gW; G.b[nj] = gb;
+    eoff += j.nelem;
+    ++nj;
+  };
+  for (int l = 0; l < 6; ++l) {
+    int CO = d.C[l + 1], CI = d.C[l];
+    if (l == 0) add(d.dz[0], CO, CI, H_XN, nullptr, nullptr, grads[0], grads[1]);
+    else add(d.dz[l], CO, CI, H_BNRELU, d.z[l - 1], d.bn[l - 1],
+             grads[l < 5 ? 6 * l : 30], grads[l < 5 ? 6 * l + 1 : 31]);
+  }
+  if (cfg->use_attention) {
+    add(d.da, d.A, F, H_XN, nullptr, nullptr, grads[32], grads[33]);
+    add(d.dsig, 1, d.A, H_RAW, d.aact, nullptr, grads[34], grads[35]);
+  }
+  J.njob = nj;
+  J.total = eoff;
+  int chunks = 0;
+  for (int k = 0; k < nj; ++k) {
+    J.cbase[k] = chunks;
+    J.echunks[k] = (J.j[k].nelem + BLK * EPT - 1) / (BLK * EPT);
+    chunks += J.echunks[k];
+  }
+  int ks = 512 / chunks;
+  if (ks < 1) ks = 1;
+  if (ks > KS_MAX) ks = KS_MAX;
+  J.KS = ks;
+  if (F == 4) hipLaunchKernelGGL((k_wgrad<4>), dim3(chunks * ks), dim3(BLK), 0, st, d, J);
+  else hipLaunchKernelGGL((k_wgrad<5>), dim3(chunks * ks), dim3(BLK), 0, st, d, J);
+  RPC_LAUNCH_CHECK();
+  for (int l = 0; l < 5; ++l) {
+    G.gg[l] = grads[6 * l + 2];
+    G.gb[l] = grads[6 * l + 3];
+  }
+  int nbn = d.C[1] + d.C[2] + d.C[3] + d.C[4] + d.C[5];
+  int nr = (J.total + nbn + BLK - 1) / BLK;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(nr), dim3(BLK), 0, st, d, J, G);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}

@@ -1,0 +1,322 @@
+"""Generate golden vectors by running the REFERENCE Python in this container.
+
+Run from the repo root in the dev container (never on the GPU box — /root/reference
+does not exist there):
+
+    python tests/golden/make_golden.py
+
+mmengine / mmdet3d are not installed, so tiny stand-ins are put into ``sys.modules``
+("Verified method") and the reference files are loaded by path:
+
+* ``models/builder.py``                        (ADVERSARIES registry)
+* ``models/adversarial/voxel_perturber.py``    (VoxelPerturber, the a3/a4 rows)
+* ``models/detectors/adversarial_voxelnet.py`` (AdversarialVoxelNet, the a2/a9/a11 rows)
+
+``models/detectors/__init__.py`` is bypassed (it imports modules that do not exist,
+SURVEY.md finding 4). Weights are set explicitly from a seeded numpy RNG and stored in
+the fixture, so no torch RNG is replayed by the tests. Only data (inputs, weights,
+outputs, grads) is written; nothing from the reference source is copied.
+"""
+from __future__ import annotations
+
+import contextlib
+import importlib.util
+import io
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+from torch import nn
+
+REF = os.environ.get("RPC_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+# ---------------------------------------------------------------- stubs
+class _Registry:
+    def __init__(self, name, parent=None, scope=None, **kw):
+        self.name = name
+        self._m = {}
+
+    def register_module(self, name=None, force=False, module=None):
+        def deco(cls):
+            self._m[name or cls.__name__] = cls
+            return cls
+        return deco
+
+    def build(self, cfg):
+        cfg = dict(cfg)
+        return self._m[cfg.pop("type")](**cfg)
+
+
+class _VoxelNet(nn.Module):
+    """Stand-in for mmdet3d VoxelNet: just holds the sub-modules it is given."""
+
+    def __init__(self, voxel_encoder=None, middle_encoder=None, backbone=None, neck=None,
+                 bbox_head=None, **kw):
+        super().__init__()
+        self.voxel_encoder = voxel_encoder
+        self.middle_encoder = middle_encoder
+        self.backbone = backbone
+        self.neck = neck
+        self.bbox_head = bbox_head
+
+    @property
+    def with_neck(self):
+        return self.neck is not None
+
+
+def _install_stubs():
+    me = types.ModuleType("mmengine")
+    mer = types.ModuleType("mmengine.registry")
+    mer.Registry = _Registry
+    me.registry = mer
+    sys.modules["mmengine"] = me
+    sys.modules["mmengine.registry"] = mer
+    m3 = types.ModuleType("mmdet3d")
+    m3r = types.ModuleType("mmdet3d.registry")
+    m3r.MODELS = _Registry("models")
+    m3s = types.ModuleType("mmdet3d.structures")
+    m3s.Det3DDataSample = object
+    m3m = types.ModuleType("mmdet3d.models")
+    m3md = types.ModuleType("mmdet3d.models.detectors")
+    m3mv = types.ModuleType("mmdet3d.models.detectors.voxelnet")
+    m3mv.VoxelNet = _VoxelNet
+    for n, m in {"mmdet3d": m3, "mmdet3d.registry": m3r, "mmdet3d.structures": m3s,
+                 "mmdet3d.models": m3m, "mmdet3d.models.detectors": m3md,
+                 "mmdet3d.models.detectors.voxelnet": m3mv}.items():
+        sys.modules[n] = m
+
+
+def _pkg(name, path):
+    p = types.ModuleType(name)
+    p.__path__ = [path]
+    sys.modules[name] = p
+    return p
+
+
+def _load(name, path):
+    spec = importlib.util.spec_from_file_location(name, path)
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
+def load_reference():
+    _install_stubs()
+    _pkg("refmodels", os.path.join(REF, "models"))
+    _pkg("refmodels.adversarial", os.path.join(REF, "models", "adversarial"))
+    _pkg("refmodels.detectors", os.path.join(REF, "models", "detectors"))
+    builder = _load("refmodels.builder", os.path.join(REF, "models", "builder.py"))
+    vp = _load("refmodels.adversarial.voxel_perturber",
+               os.path.join(REF, "models", "adversarial", "voxel_perturber.py"))
+    av = _load("refmodels.detectors.adversarial_voxelnet",
+               os.path.join(REF, "models", "detectors", "adversarial_voxelnet.py"))
+    return builder, vp, av
+
+
+# ---------------------------------------------------------------- helpers
+def perturber_weights(rng, F, hidden):
+    """Explicit weights in the layout of VoxelPerturber._build_model (:82-112)."""
+    widths = [F, hidden[0], hidden[1], hidden[2], hidden[1], hidden[0], F]
+    w = {}
+    for l in range(6):
+        fan_in, fan_out = widths[l], widths[l + 1]
+        s = 1.0 / np.sqrt(fan_in)
+        w[f"W{l}"] = rng.uniform(-s, s, (fan_out, fan_in)).astype(np.float32)
+        w[f"b{l}"] = rng.uniform(-0.1, 0.1, fan_out).astype(np.float32)
+    for l in range(5):
+        w[f"g{l}"] = rng.uniform(0.5, 1.5, widths[l + 1]).astype(np.float32)
+        w[f"be{l}"] = rng.uniform(-0.2, 0.2, widths[l + 1]).astype(np.float32)
+    a = max(F // 2, 1)
+    w["Wa0"] = rng.uniform(-0.7, 0.7, (a, F)).astype(np.float32)
+    w["ba0"] = rng.uniform(-0.1, 0.1, a).astype(np.float32)
+    w["Wa1"] = rng.uniform(-0.7, 0.7, (1, a)).astype(np.float32)
+    w["ba1"] = rng.uniform(-0.1, 0.1, 1).astype(np.float32)
+    return w
+
+
+def set_perturber_weights(p, w):
+    lin = [m for m in p.model if isinstance(m, nn.Linear)]
+    bns = [m for m in p.model if isinstance(m, nn.BatchNorm1d)]
+    att = [m for m in p.attention if isinstance(m, nn.Linear)]
+    with torch.no_grad():
+        for l, m in enumerate(lin):
+            m.weight.copy_(torch.from_numpy(w[f"W{l}"]))
+            m.bias.copy_(torch.from_numpy(w[f"b{l}"]))
+        for l, m in enumerate(bns):
+            m.weight.copy_(torch.from_numpy(w[f"g{l}"]))
+            m.bias.copy_(torch.from_numpy(w[f"be{l}"]))
+        for l, m in enumerate(att):
+            m.weight.copy_(torch.from_numpy(w[f"Wa{l}"]))
+            m.bias.copy_(torch.from_numpy(w[f"ba{l}"]))
+    return lin, bns, att
+
+
+def valid_slots(seed, V, F=4, pmax=5):
+    """A voxel tensor [V,5,F] shaped like hard_voxelize output: 1..5 points per voxel,
+    zero padding, plus a few real points whose features sum to exactly zero."""
+    rng = np.random.default_rng(seed)
+    vox = np.zeros((V, pmax, F), np.float32)
+    npts = rng.choice([1, 1, 1, 1, 2, 2, 3, 4, 5], V)
+    for v in range(V):
+        for s in range(npts[v]):
+            xyz = [rng.uniform(0, 70.4), rng.uniform(-40, 40), rng.uniform(-3, 1)]
+            extra = [rng.random()] + ([rng.uniform(0, 0.5)] if F == 5 else [])
+            vox[v, s] = np.array(xyz + extra, np.float32)
+    # points whose 4 features sum to exactly 0 are treated as padding by the reference (:89)
+    for v in rng.choice(V, 3, replace=False):
+        vox[v, 0, :] = 0.0
+        vox[v, 0, 0] = 1.0
+        vox[v, 0, 1] = -1.0
+    return vox, npts.astype(np.int32)
+
+
+@contextlib.contextmanager
+def _quiet():
+    with contextlib.redirect_stdout(io.StringIO()):
+        yield
+
+
+# ---------------------------------------------------------------- fixtures
+def gen_perturber(vp, tag, F, hidden, N, seed, gscale):
+    rng = np.random.default_rng(seed)
+    w = perturber_weights(rng, F, hidden)
+    vs = [0.05, 0.05, 0.1] if F == 4 else [0.1, 0.1, 0.2]
+    x = np.concatenate([rng.uniform(0, 70.4, (N, 1)), rng.uniform(-40, 40, (N, 1)),
+                        rng.uniform(-3, 1, (N, 1)), rng.random((N, F - 3))], 1).astype(np.float32)
+    G = (rng.standard_normal((N, F)) * gscale).astype(np.float32)
+    c = (rng.standard_normal(4) * gscale).astype(np.float32)
+    with _quiet():
+        p = vp.VoxelPerturber(sensor_error_bound=0.2, voxel_size=vs, use_spatial_attention=True,
+                              hidden_channels=list(hidden))
+        p._build_model(F)
+        lin, bns, att = set_perturber_weights(p, w)
+        p.train()
+        xt = torch.from_numpy(x)
+        out, ld = p(xt)
+        loss = (out * torch.from_numpy(G)).sum() + c[0] * ld["l2_norm"] + c[1] * ld["intensity_loss"] \
+            + c[2] * ld["bias_loss"] + c[3] * ld["imbalance_loss"]
+        loss.backward()
+    d = dict(w)
+    d.update(F=np.int32(F), hidden=np.array(hidden, np.int32), x=x, G=G, c=c,
+             out=out.detach().numpy(),
+             l2_norm=np.float32(ld["l2_norm"].item()), intensity_loss=np.float32(ld["intensity_loss"].item()),
+             bias_loss=np.float32(ld["bias_loss"].item()), imbalance_loss=np.float32(ld["imbalance_loss"].item()))
+    # grads AFTER the reference's per-parameter clamp hook (:465-475)
+    for l, m in enumerate(lin):
+        d[f"dW{l}"] = m.weight.grad.numpy().copy()
+        d[f"db{l}"] = m.bias.grad.numpy().copy()
+    for l, m in enumerate(bns):
+        d[f"dg{l}"] = m.weight.grad.numpy().copy()
+        d[f"dbe{l}"] = m.bias.grad.numpy().copy()
+        d[f"rm{l}"] = m.running_mean.numpy().copy()
+        d[f"rv{l}"] = m.running_var.numpy().copy()
+    for l, m in enumerate(att):
+        d[f"dWa{l}"] = m.weight.grad.numpy().copy()
+        d[f"dba{l}"] = m.bias.grad.numpy().copy()
+    # eval mode on the same weights (uses the running stats just updated; :133-136, :214-238)
+    with _quiet(), torch.no_grad():
+        p.eval()
+        xe = torch.from_numpy(x[: min(N, 500)])
+        oute, lde = p(xe)
+    d["x_eval"] = x[: min(N, 500)]
+    d["out_eval"] = oute.numpy()
+    d["l2_norm_eval"] = np.float32(lde["l2_norm"].item())
+    np.savez_compressed(os.path.join(OUT, f"perturber_{tag}.npz"), **d)
+    print(f"perturber_{tag}: N={N} F={F} hidden={hidden} l2={d['l2_norm']:.6f}")
+
+
+class _StandInVFE(nn.Module):
+    """HardSimpleVFE semantics (upstream mmdet3d voxel_encoder.py): mean over slots."""
+
+    def forward(self, features, num_points, coors):
+        return features[:, :, :4].sum(dim=1) / num_points.type_as(features).view(-1, 1)
+
+
+class _StandInMiddle(nn.Module):
+    def forward(self, feats, coors, batch_size):
+        # deterministic, differentiable: per-frame sum of features
+        out = feats.new_zeros(batch_size, feats.shape[1])
+        return out.index_add(0, coors[:, 0].long(), feats)
+
+
+class _StandInHead(nn.Module):
+    def __init__(self, w, listy):
+        super().__init__()
+        self.w = nn.Parameter(torch.from_numpy(w))
+        self.listy = listy
+
+    def loss(self, x, samples):
+        y = (x * 1e-2) @ self.w             # [B, 3]
+        lc = (y[:, 0] ** 2).mean() * 1e-3 + 0.5
+        lb = (y[:, 1].abs()).mean() * 1e-3 + 0.25
+        ld = torch.sigmoid(y[:, 2]).mean() * 0.1
+        if self.listy:   # upstream Anchor3DHead.loss_by_feat returns lists (multi_apply)
+            return dict(loss_cls=[lc], loss_bbox=[lb], loss_dir=[ld])
+        return dict(loss_cls=lc, loss_bbox=lb, loss_dir=ld)
+
+
+def gen_voxelnet(builder, av, tag, listy, epoch, seed, V=400, hidden=(8, 16, 32)):
+    rng = np.random.default_rng(seed)
+    F = 4
+    w = perturber_weights(rng, F, hidden)
+    vox, npts = valid_slots(seed + 1, V, F)
+    B = 2
+    coors = np.zeros((V, 4), np.int32)
+    coors[:, 0] = (np.arange(V) >= V // 2).astype(np.int32)
+    hw = rng.standard_normal((4, 3)).astype(np.float32)
+    with _quiet():
+        model = av.AdversarialVoxelNet(
+            adversary_cfg=dict(type="VoxelPerturber", hidden_channels=list(hidden)),
+            regularization_weight=0.02,
+            voxel_encoder=_StandInVFE(), middle_encoder=_StandInMiddle(), backbone=nn.Identity(),
+            neck=None, bbox_head=_StandInHead(hw, listy))
+        model.adversary._build_model(F)
+        lin, bns, att = set_perturber_weights(model.adversary, w)
+        model.train()
+        model._epoch = epoch
+        inputs = {"voxels": {"voxels": torch.from_numpy(vox), "num_points": torch.from_numpy(npts),
+                             "coors": torch.from_numpy(coors)}}
+        losses = model.loss(inputs, [None] * B)
+        total = 0
+        for k, v in losses.items():          # mmengine parse_losses: keys containing 'loss'
+            if "loss" not in k:
+                continue
+            total = total + (sum(t.mean() for t in v) if isinstance(v, list) else v.mean())
+        total.backward()
+    d = dict(w)
+    d.update(vox=vox, num_points=npts, coors=coors, head_w=hw, epoch=np.int32(epoch),
+             listy=np.int32(listy), hidden=np.array(hidden, np.int32), total=np.float32(total.item()))
+    for k, v in losses.items():
+        d["L_" + k] = np.float32((v[0] if isinstance(v, list) else v).item())
+    g = lambda t: np.zeros(tuple(t.shape), np.float32) if t.grad is None else t.grad.numpy().copy()
+    for l, m in enumerate(lin):
+        d[f"dW{l}"] = g(m.weight)
+        d[f"db{l}"] = g(m.bias)
+    for l, m in enumerate(att):
+        d[f"dWa{l}"] = g(m.weight)
+    d["dhead_w"] = model.bbox_head.w.grad.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"voxelnet_{tag}.npz"), **d)
+    print(f"voxelnet_{tag}: " + ", ".join(f"{k}={v.item() if hasattr(v,'item') else v:.6f}"
+                                          for k, v in d.items() if k.startswith("L_")))
+
+
+def main():
+    torch.manual_seed(0)
+    builder, vp, av = load_reference()
+    gen_perturber(vp, "car_small", 4, (8, 16, 32), 3000, 1, 1e-3)
+    gen_perturber(vp, "car_clamp", 4, (8, 16, 32), 2000, 2, 30.0)
+    gen_perturber(vp, "3class", 4, (64, 128, 64), 2500, 3, 1e-3)
+    gen_perturber(vp, "nus", 5, (16, 32, 64), 2000, 4, 1e-3)
+    gen_voxelnet(builder, av, "list_e3", True, 3, 11)
+    gen_voxelnet(builder, av, "list_e7", True, 7, 12)
+    gen_voxelnet(builder, av, "tensor_e3", False, 3, 13)
+    gen_voxelnet(builder, av, "gate_e2", True, 2, 14)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+"""a2–a5 parity: the HIP perturber (+ fused compaction / scatter / VFE) against the golden
+vectors of the reference VoxelPerturber and against the CPU oracle."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle.perturber import OraclePerturber, perturb_voxels
+from robustpointclouds_amd import perturb as P
+from tests.conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-4   # north_star: perturbed coords and losses within 1e-4 (fp32)
+
+
+def _params(d, F, hidden, dev, att=True):
+    """36 tensors in rpc_perturber order (include/rpc_hip.h)."""
+    widths = [F, hidden[0], hidden[1], hidden[2], hidden[1], hidden[0]]
+    t = lambda k: torch.tensor(np.asarray(d[k]), dtype=torch.float32, device=dev).contiguous()
+    ps = []
+    for l in range(5):
+        ps += [t(f"W{l}"), t(f"b{l}"), t(f"g{l}"), t(f"be{l}"),
+               torch.zeros(widths[l + 1], device=dev), torch.ones(widths[l + 1], device=dev)]
+    ps += [t("W5"), t("b5")]
+    ps += [t("Wa0"), t("ba0"), t("Wa1"), t("ba1")] if att else [None] * 4
+    return ps
+
+
+def _load(tag):
+    return dict(np.load(os.path.join(GOLDEN, f"perturber_{tag}.npz")))
+
+
+NAMES = []
+for _l in range(5):
+    NAMES += [f"W{_l}", f"b{_l}", f"g{_l}", f"be{_l}", None, None]
+NAMES += ["W5", "b5", "Wa0", "ba0", "Wa1", "ba1"]
+
+
+@pytest.mark.parametrize("tag", ["car_small", "car_clamp", "3class", "nus"])
+def test_standalone_matches_reference_golden(tag):
+    d = _load(tag)
+    F, hidden = int(d["F"]), [int(h) for h in d["hidden"]]
+    dev = torch.device("cuda")
+    ps = _params(d, F, hidden, dev)
+    for p in ps:
+        if p is not None:
+            p.requires_grad_(True)
+    for l in range(5):
+        ps[6 * l + 4].requires_grad_(False)
+        ps[6 * l + 5].requires_grad_(False)
+    cfg = P.make_cfg(F, hidden, True, True, 0.2)
+    x = torch.from_numpy(d["x"]).to(dev)
+    out, lvec, flags = P.PerturberFn.apply(x, cfg, *ps)
+    np.testing.assert_allclose(out.detach().cpu().numpy(), d["out"], rtol=0, atol=TOL)
+    got = lvec.detach().cpu().numpy()
+    ref = np.array([d["l2_norm"], d["intensity_loss"], d["bias_loss"], d["imbalance_loss"]])
+    np.testing.assert_allclose(got, ref, rtol=TOL, atol=1e-6)
+    G = torch.from_numpy(d["G"]).to(dev)
+    c = torch.from_numpy(d["c"]).to(dev)
+    loss = (out * G).sum() + (lvec * c).sum()
+    loss.backward()
+    for k, name in enumerate(NAMES):
+        if name is None:
+            continue
+        g = ps[k].grad.cpu().numpy()
+        r = d["d" + name]
+        scale = max(np.abs(r).max(), 1e-3)
+        tol = 1e-3
+        if name[0] == "b" and name[1:].isdigit() and int(name[1:]) < 5:
+            scale = max(scale, np.abs(d["dW" + name[1:]]).max())
+            tol = 2e-3
+        np.testing.assert_allclose(g, r, rtol=0, atol=tol * scale, err_msg=name)
+    for l in range(5):
+        np.testing.assert_allclose(ps[6 * l + 4].cpu().numpy(), d[f"rm{l}"], rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(ps[6 * l + 5].cpu().numpy(), d[f"rv{l}"], rtol=1e-4, atol=1e-5)
+    # eval mode with the updated running stats
+    cfg_e = P.make_cfg(F, hidden, True, False, 0.2)
+    with torch.no_grad():
+        oute, lve, _ = P.PerturberFn.apply(torch.from_numpy(d["x_eval"]).to(dev), cfg_e, *ps)
+    np.testing.assert_allclose(oute.cpu().numpy(), d["out_eval"], rtol=0, atol=TOL)
+    np.testing.assert_allclose(lve[0].item(), float(d["l2_norm_eval"]), rtol=TOL)
+
+
+def _voxels(seed, V, x_pool):
+    rng = np.random.default_rng(seed)
+    vox = np.zeros((V, 5, 4), np.float32)
+    npts = rng.choice([1, 1, 1, 1, 2, 2, 3, 4, 5], V).astype(np.int32)
+    for v in range(V):
+        vox[v, :npts[v]] = x_pool[rng.integers(0, len(x_pool), npts[v])]
+    vox[5, 0] = [1.0, -1.0, 0.0, 0.0]     # real point with zero feature sum (reference: padding)
+    return vox, npts
+
+
+@pytest.mark.parametrize("tag,V", [("car_small", 3000), ("3class", 1500), ("car_small", 70000)])
+def test_fused_voxels_vfe_matches_oracle(tag, V):
+    d = _load(tag)
+    hidden = [int(h) for h in d["hidden"]]
+    dev = torch.device("cuda")
+    vox, npts = _voxels(1, V, d["x"])
+    ps = _params(d, 4, hidden, dev)
+    for p in ps:
+        if p is not None:
+            p.requires_grad_(True)
+    for l in range(5):
+        ps[6 * l + 4].requires_grad_(False)
+        ps[6 * l + 5].requires_grad_(False)
+    cfg = P.make_cfg(4, hidden, True, True, 0.2, vfe_features=4)
+    vt, nt = torch.from_numpy(vox).to(dev), torch.from_numpy(npts).to(dev)
+    vfe, lvec, pert, flags = P.PerturbVoxelsFn.apply(vt, nt, cfg, *ps)
+    op = OraclePerturber(d, 4, hidden, dtype=torch.float64)
+    rvfe, rpert, rld = perturb_voxels(op, vox, npts)
+    np.testing.assert_allclose(pert.cpu().numpy(), rpert.detach().numpy(), rtol=0, atol=TOL)
+    np.testing.assert_allclose(vfe.detach().cpu().numpy(), rvfe.detach().numpy(), rtol=0, atol=TOL)
+    ref = torch.stack([rld[k] for k in ["l2_norm", "intensity_loss", "bias_loss", "imbalance_loss"]])
+    np.testing.assert_allclose(lvec.detach().cpu().numpy(), ref.detach().numpy(), rtol=TOL, atol=1e-6)
+    assert int(flags[4].item()) == int((vox.reshape(-1, 4).sum(1) != 0).sum())
+    # backward through the fused VFE
+    rng = np.random.default_rng(2)
+    Gv = rng.standard_normal((V, 4)).astype(np.float32) * 1e-3
+    cl = np.array([1e-3, -2e-3, 3e-3, 1e-3], np.float32)
+    ((vfe * torch.from_numpy(Gv).to(dev)).sum() + (lvec * torch.from_numpy(cl).to(dev)).sum()).backward()
+    rloss = (rvfe * torch.from_numpy(Gv.astype(np.float64))).sum() + (ref * torch.from_numpy(cl.astype(np.float64))).sum()
+    rloss.backward()
+    rg = op.grads()
+    for k, name in enumerate(NAMES):
+        if name is None:
+            continue
+        g = ps[k].grad.cpu().numpy()
+        r = rg["d" + name].numpy()
+        scale = max(np.abs(r).max(), 1e-6)
+        if name[0] == "b" and name[1:].isdigit() and int(name[1:]) < 5:
+            assert np.abs(g).max() <= 1e-3 * max(np.abs(rg["dW" + name[1:]].numpy()).max(), 1e-6) + 1e-9
+            continue
+        np.testing.assert_allclose(g, r, rtol=0, atol=2e-3 * scale, err_msg=name)
+
+
+def test_fused_is_deterministic():
+    d = _load("car_small")
+    dev = torch.device("cuda")
+    vox, npts = _voxels(3, 20000, d["x"])
+    outs = []
+    for _ in range(2):
+        ps = _params(d, 4, [8, 16, 32], dev)
+        cfg = P.make_cfg(4, [8, 16, 32], True, True, 0.2)
+        vfe, lvec, pert, _ = P.PerturbVoxelsFn.apply(torch.from_numpy(vox).to(dev), torch.from_numpy(npts).to(dev),
+                                                    cfg, *ps)
+        outs.append((vfe.cpu().numpy(), lvec.cpu().numpy(), pert.cpu().numpy()))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
+
+
+def test_nan_input_falls_back_to_unperturbed():
+    d = _load("car_small")
+    dev = torch.device("cuda")
+    vox, npts = _voxels(4, 500, d["x"])
+    vox[10, 0, 2] = np.nan
+    ps = _params(d, 4, [8, 16, 32], dev)
+    cfg = P.make_cfg(4, [8, 16, 32], True, True, 0.2)
+    vfe, lvec, pert, flags = P.PerturbVoxelsFn.apply(torch.from_numpy(vox).to(dev), torch.from_numpy(npts).to(dev),
+                                                    cfg, *ps)
+    assert flags[5].item() == 1.0
+    assert np.array_equal(pert.cpu().numpy(), vox, equal_nan=True)
+    assert np.all(lvec.cpu().numpy() == 0)
+
+
+def test_vfe_mean_bit_exact():
+    rng = np.random.default_rng(0)
+    V = 5000
+    vox = rng.standard_normal((V, 5, 4)).astype(np.float32)
+    npts = rng.integers(1, 6, V).astype(np.int32)
+    out = P.VoxelMeanFn.apply(torch.from_numpy(vox).cuda(), torch.from_numpy(npts).cuda(), 4).cpu().numpy()
+    ref = (torch.from_numpy(vox)[:, :, :4].sum(dim=1) / torch.from_numpy(npts).float().view(-1, 1)).numpy()
+    assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))

@@ -124,6 +124,58 @@ int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float* const* par
                            const float* dout, const float* dlosses, float* const* grads,
                            void* workspace, size_t workspace_bytes, void* stream);
 
+/* ------------------------------------------------------------------ a6 SparseEncoder
+ * Replaces the spconv (spconv-cu113>=2.3.0, requirements.txt:18) SubMConv3d /
+ * SparseConv3d + BatchNorm1d + ReLU modules that upstream mmdet3d `SparseEncoder`
+ * (config: adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:19-23) runs at
+ * models/detectors/adversarial_voxelnet.py:141, and its `.dense()` BEV output.
+ * Features are row-major [N, C] float32; coors [N, 4] int32 (b, z, y, x); weights
+ * W[k][CI][CO] with k = (kz * kh + ky) * kw + kx. Rulebook builders need a dense int32
+ * index grid [B, D, H, W] that is all -1 on entry and is left all -1 on exit.
+ */
+/* SubM neighbour map: nbr[r, k] = row at coors[r] + (k - centre), or -1. */
+int rpc_subm_rulebook(const int* coors, int n, const int* shape /* host B,D,H,W */,
+                      const int* ksize /* host [3] */, int* grid, int* nbr, void* stream);
+/* Strided SparseConv3d rulebook, two phases around one host read of n_out. */
+size_t rpc_spconv_rulebook_workspace_size(int n_in, int kvol);
+int rpc_spconv_rulebook_count(const int* coors, int n_in, const int* out_shape, const int* ksize,
+                              const int* stride, const int* pad, int* grid_out, int* n_out /* device */,
+                              void* workspace, size_t workspace_bytes, void* stream);
+int rpc_spconv_rulebook_build(const int* coors, int n_in, const int* out_shape, const int* ksize,
+                              const int* stride, const int* pad, int* grid_out, int n_out,
+                              int* coors_out, int* nbr_out /* [n_out, K] */, int* nbr_in /* [n_in, K] */,
+                              void* workspace, void* stream);
+/* number of 64-row tiles (= BatchNorm partial rows) of a conv over n_out output rows */
+int rpc_spconv_gemm_blocks(int n_out);
+/* z_out[r] = sum_k A(in[nbr[r,k]]) W[k], A = relu(in*scale+shift) if in_bn else identity;
+ * part (nullable) = per-tile BatchNorm partial sums [blocks][2*CO]. */
+int rpc_spconv_forward(const float* in, const float* in_bn, int ci, const int* nbr, int kvol, int n_out,
+                       const float* W, int co, float* z_out, float* part, void* stream);
+/* din[i] = sum_k dz(map[i,k']) W[k]^T with dz = bnb-normalised (dy_out, z_out), k' = rev ? K-1-k : k.
+ * With prev_z/prev_bn the previous layer's ReLU mask is applied and its BatchNorm-backward
+ * partial sums are written to part. */
+int rpc_spconv_dgrad(const float* dy_out, const float* z_out, const float* bnb, int co, const int* map,
+                     int kvol, int rev, int n_in, const float* W, int ci, const float* prev_z,
+                     const float* prev_bn, float* din, float* part, void* stream);
+size_t rpc_spconv_wgrad_workspace_size(int n_out, int kvol, int ci, int co);
+int rpc_spconv_wgrad(const float* in, const float* in_bn, int ci, const int* nbr, int kvol, int n_out,
+                     const float* dy_out, const float* z_out, const float* bnb, int co, float* dW,
+                     void* workspace, size_t workspace_bytes, void* stream);
+/* BatchNorm1d finalize from partial sums. mode 0: bn_out = scale, shift, mean, invstd and the
+ * running stats update (train). mode 1: bn_out = gi, m1, m2, mean, invstd for the backward and
+ * dgamma = sum dy*xhat, dbeta = sum dy. */
+size_t rpc_bn_finalize_workspace_size(int c);
+int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const float* gamma,
+                    const float* beta, float eps, float momentum, float* running_mean, float* running_var,
+                    const float* fwd_bn, float* bn_out, float* dgamma, float* dbeta, void* workspace,
+                    void* stream);
+/* SparseConvTensor.dense() of relu(bn(z)): dense[b, c, z, y, x]; backward gathers, applies the
+ * ReLU mask and writes the BatchNorm-backward partial sums. */
+int rpc_sparse_to_dense(const float* z, const float* bn, const int* coors, int n, int c,
+                        const int* shape /* B,D,H,W */, float* dense, void* stream);
+int rpc_dense_to_sparse_grad(const float* grad_dense, const float* z, const float* bn, const int* coors,
+                             int n, int c, const int* shape, float* dy, float* part, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

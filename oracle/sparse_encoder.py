@@ -1,0 +1,123 @@
+"""PARITY ORACLE — TEST INFRASTRUCTURE ONLY.
+
+CPU restatement of upstream mmdet3d `SparseEncoder` over spconv (spconv-cu113>=2.3.0,
+requirements.txt:18; config adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:19-23;
+call site models/detectors/adversarial_voxelnet.py:141). spconv/mmdet3d are not in this
+container and the reference holds no vectors for this layer, so this
+is "parity unpinned" w.r.t. spconv itself: it restates spconv's published semantics —
+  SubMConv3d:   out(o) = sum_k W[k]^T in(o + k - centre), output sites = input sites
+  SparseConv3d: out(o) = sum_k W[k]^T in(o*s - p + k), output sites = every o reached
+                by an input; spatial out = (in + 2p - (k-1) - 1)//s + 1
+  BatchNorm1d (train: batch stats, biased var; running stats with the unbiased var),
+  ReLU, `.dense()` -> [B, C, D, H, W] -> view(B, C*D, H, W)
+with numpy index arithmetic and torch float64 autograd on CPU (gather / matmul /
+index_add). Row ORDER of intermediate sparse tensors is free (the dense output and the
+BatchNorm statistics do not depend on it).
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+
+def _keys(c, shape):
+    B, D, H, W = shape
+    c = c.astype(np.int64)
+    return ((c[:, 0] * D + c[:, 1]) * H + c[:, 2]) * W + c[:, 3]
+
+
+def subm_pairs(coors, shape, ksize=(3, 3, 3)):
+    """list over k of (in_rows, out_rows)"""
+    keys = _keys(coors, shape)
+    order = np.argsort(keys)
+    sk = keys[order]
+    B, D, H, W = shape
+    pairs = []
+    kz, ky, kx = ksize
+    for a in range(kz):
+        for b in range(ky):
+            for c in range(kx):
+                off = np.array([0, a - kz // 2, b - ky // 2, c - kx // 2])
+                nb = coors + off
+                ok = (nb[:, 1] >= 0) & (nb[:, 1] < D) & (nb[:, 2] >= 0) & (nb[:, 2] < H) & (nb[:, 3] >= 0) & (nb[:, 3] < W)
+                nk = _keys(nb, shape)
+                pos = np.clip(np.searchsorted(sk, nk), 0, len(sk) - 1)
+                hit = ok & (sk[pos] == nk) if len(sk) else ok & False
+                out_rows = np.nonzero(hit)[0]
+                in_rows = order[pos[hit]]
+                pairs.append((in_rows, out_rows))
+    return pairs
+
+
+def spconv_pairs(coors, out_shape, ksize, stride, pad):
+    """(out_coors, list over k of (in_rows, out_rows))"""
+    B, D, H, W = out_shape
+    cands = []
+    kz, ky, kx = ksize
+    ks = []
+    for a in range(kz):
+        for b in range(ky):
+            for c in range(kx):
+                n = coors[:, 1:] + np.array(pad) - np.array([a, b, c])
+                ok = np.all(n >= 0, 1) & np.all(n % np.array(stride) == 0, 1)
+                o = n // np.array(stride)
+                ok &= (o[:, 0] < D) & (o[:, 1] < H) & (o[:, 2] < W)
+                oc = np.concatenate([coors[:, :1], o], 1)
+                ks.append((np.nonzero(ok)[0], oc[ok]))
+    allc = np.concatenate([oc for _, oc in ks]) if ks else np.zeros((0, 4), np.int64)
+    ukeys, first = np.unique(_keys(allc, out_shape), return_index=True)
+    out_coors = allc[first]
+    pairs = []
+    for rows, oc in ks:
+        o = np.searchsorted(ukeys, _keys(oc, out_shape))
+        pairs.append((rows, o))
+    return out_coors.astype(np.int64), pairs
+
+
+class OracleSparseEncoder:
+    """SECOND SparseEncoder with explicit float64 weights copied from a GPU module."""
+
+    def __init__(self, enc, dtype=torch.float64):
+        self.specs = enc.specs
+        self.shapes = enc.shapes
+        self.dtype = dtype
+        self.params = []
+        for m in enc.layers():
+            W = m[0].weight.detach().cpu().to(dtype).clone().requires_grad_(True)
+            g = m[1].weight.detach().cpu().to(dtype).clone().requires_grad_(True)
+            b = m[1].bias.detach().cpu().to(dtype).clone().requires_grad_(True)
+            self.params.append(dict(W=W, g=g, b=b, eps=m[1].eps, mom=m[1].momentum,
+                                    rm=m[1].running_mean.detach().cpu().to(dtype).clone(),
+                                    rv=m[1].running_var.detach().cpu().to(dtype).clone()))
+
+    def forward(self, feats, coors, B):
+        x = torch.as_tensor(feats).to(self.dtype)
+        c = np.asarray(coors, np.int64)
+        cache = {}
+        for sp, p in zip(self.specs, self.params):
+            if sp.kind == "subm":
+                if sp.key not in cache:
+                    cache[sp.key] = subm_pairs(c, (B,) + self.shapes[sp.lvl_in], sp.ksize)
+                pairs, n_out, c_out = cache[sp.key], x.shape[0], c
+            else:
+                c_out, pairs = spconv_pairs(c, (B,) + self.shapes[sp.lvl_out], sp.ksize, sp.stride, sp.pad)
+                n_out = c_out.shape[0]
+            z = torch.zeros((n_out, sp.co), dtype=self.dtype)
+            for k, (ri, ro) in enumerate(pairs):
+                if len(ri):
+                    z = z.index_add(0, torch.from_numpy(ro), x[torch.from_numpy(ri)] @ p["W"][k])
+            mean = z.mean(0)
+            var = z.var(0, unbiased=False)
+            with torch.no_grad():
+                n = z.shape[0]
+                p["rm"] = (1 - p["mom"]) * p["rm"] + p["mom"] * mean
+                p["rv"] = (1 - p["mom"]) * p["rv"] + p["mom"] * var * n / max(n - 1, 1)
+            x = torch.relu((z - mean) / torch.sqrt(var + p["eps"]) * p["g"] + p["b"])
+            c = c_out
+        D, H, W = self.shapes[-1]
+        C = x.shape[1]
+        dense = torch.zeros((B, D, H, W, C), dtype=self.dtype)
+        idx = (torch.from_numpy(c[:, 0]), torch.from_numpy(c[:, 1]), torch.from_numpy(c[:, 2]),
+               torch.from_numpy(c[:, 3]))
+        dense = dense.index_put(idx, x)
+        return dense.permute(0, 4, 1, 2, 3).reshape(B, C * D, H, W)

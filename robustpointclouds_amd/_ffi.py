@@ -23,6 +23,7 @@ vp = C.c_void_p
 i32 = C.c_int
 sz = C.c_size_t
 fp = C.POINTER(C.c_float)
+ip = C.POINTER(C.c_int)
 
 
 class PerturberCfg(C.Structure):
@@ -43,6 +44,20 @@ SIGNATURES = {
                                     vp, vp, sz, vp]),
     "rpc_perturber_backward": (i32, [C.POINTER(PerturberCfg), C.POINTER(vp), vp, i32, i32, vp, vp, vp,
                                      C.POINTER(vp), vp, sz, vp]),
+    "rpc_subm_rulebook": (i32, [vp, i32, ip, ip, vp, vp, vp]),
+    "rpc_spconv_rulebook_workspace_size": (sz, [i32, i32]),
+    "rpc_spconv_rulebook_count": (i32, [vp, i32, ip, ip, ip, ip, vp, vp, vp, sz, vp]),
+    "rpc_spconv_rulebook_build": (i32, [vp, i32, ip, ip, ip, ip, vp, i32, vp, vp, vp, vp, vp]),
+    "rpc_spconv_gemm_blocks": (i32, [i32]),
+    "rpc_spconv_forward": (i32, [vp, vp, i32, vp, i32, i32, vp, i32, vp, vp, vp]),
+    "rpc_spconv_dgrad": (i32, [vp, vp, vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp]),
+    "rpc_spconv_wgrad_workspace_size": (sz, [i32, i32, i32, i32]),
+    "rpc_spconv_wgrad": (i32, [vp, vp, i32, vp, i32, i32, vp, vp, vp, i32, vp, vp, sz, vp]),
+    "rpc_bn_finalize_workspace_size": (sz, [i32]),
+    "rpc_bn_finalize": (i32, [vp, i32, i32, i32, i32, vp, vp, C.c_float, C.c_float, vp, vp, vp, vp, vp, vp,
+                              vp, vp]),
+    "rpc_sparse_to_dense": (i32, [vp, vp, vp, i32, i32, ip, vp, vp]),
+    "rpc_dense_to_sparse_grad": (i32, [vp, vp, vp, vp, i32, i32, ip, vp, vp, vp]),
 }
 
 
@@ -91,3 +106,7 @@ def workspace(nbytes: int, device) -> torch.Tensor:
 
 def float_arr(vals):
     return (C.c_float * len(vals))(*[float(v) for v in vals])
+
+
+def int_arr(vals):
+    return (C.c_int * len(vals))(*[int(v) for v in vals])

@@ -1,0 +1,742 @@
+// a6: SECOND sparse middle encoder (upstream mmdet3d SparseEncoder over spconv) on gfx950.
+//
+// Sparse tensor = rows of features [N, C] (row-major) + coors [N, 4] (b, z, y, x).
+//
+// Rulebooks ("indice_key" in spconv) are neighbour maps built with a DENSE int32 index
+// grid per resolution level: 288 GB of HBM makes a direct [B, D, H, W] table (2.2 GB at
+// level 0 for B = 6) cheaper than hashing. The grid stays all -1 between calls: each
+// builder scatters the row ids it needs and clears exactly those cells again.
+//   SubM (stride 1, centred):   nbr[r, k] = row of coors[r] + (k - centre), or -1
+//   SparseConv (strided):       output sites = { (c + pad - k) / stride } over inputs c and
+//                               offsets k; ordered by their first candidate (i*K + k),
+//                               found with an atomicMin on the grid and a scan — no sort,
+//                               deterministic. nbr_out[o, k] = i and nbr_in[i, k] = o.
+//
+// Compute: output-stationary implicit GEMM on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact
+// k-ordered fma):  out[r, :] = sum_k A_k[r, :] . B_k, with A_k rows gathered by the
+// neighbour map straight into LDS and transformed on load:
+//   forward   A = relu(bn_prev(z_prev)) (or the raw VFE features), B = W[k] [CI, CO]
+//   dgrad     A = dz = g*invstd*(dy - mean(dy) - xhat*mean(dy*xhat)), B = W[k]^T
+// with offsets whose 64-row tile has no neighbour skipped. The epilogue writes z (pre-BN,
+// kept for backward) and per-block BatchNorm partial sums; the dgrad epilogue applies the
+// previous layer's ReLU mask and its BatchNorm-backward partial sums. Weight gradients
+//   dW[k] = sum_r A_k[r, :]^T dz[r, :]
+// are split over row chunks into partial slabs reduced in a fixed order. Nothing uses
+// float atomics: results are bit-for-bit reproducible run to run.
+#include <hipcub/hipcub.hpp>
+#include <string.h>
+
+#include "common.h"
+
+namespace rpc {
+namespace sp {
+
+constexpr int BLK = 256;
+constexpr int BM = 64;      // rows per GEMM tile
+constexpr int MAXK = 27;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+struct Shape {
+  int B, D, H, W;
+};
+struct KGeom {
+  int k[3], s[3], p[3];
+  int K;
+};
+
+__device__ __forceinline__ long long cell(const Shape& s, int b, int z, int y, int x) {
+  return (((long long)b * s.D + z) * s.H + y) * s.W + x;
+}
+
+__global__ void k_grid_set(const int* __restrict__ coors, int N, Shape s, int* __restrict__ grid,
+                           int clear) {
+  int r = blockIdx.x * BLK + threadIdx.x;
+  if (r >= N) return;
+  const int* c = coors + 4 * r;
+  grid[cell(s, c[0], c[1], c[2], c[3])] = clear ? -1 : r;
+}
+
+__global__ void k_subm_nbr(const int* __restrict__ coors, int N, Shape s, KGeom g,
+                           const int* __restrict__ grid, int* __restrict__ nbr) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * g.K) return;
+  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  int kx = k % g.k[2], ky = (k / g.k[2]) % g.k[1], kz = k / (g.k[2] * g.k[1]);
+  const int* c = coors + 4 * r;
+  int z = c[1] + kz - g.k[0] / 2, y = c[2] + ky - g.k[1] / 2, x = c[3] + kx - g.k[2] / 2;
+  int v = -1;
+  if (z >= 0 && z < s.D && y >= 0 && y < s.H && x >= 0 && x < s.W) v = grid[cell(s, c[0], z, y, x)];
+  nbr[t] = v;
+}
+
+// output coordinate of input c through kernel offset k, or false
+__device__ __forceinline__ bool out_of(const int* c, int k, const KGeom& g, const Shape& so, int& oz,
+                                       int& oy, int& ox) {
+  int kk[3] = {k / (g.k[2] * g.k[1]), (k / g.k[2]) % g.k[1], k % g.k[2]};
+  int o[3];
+#pragma unroll
+  for (int a = 0; a < 3; ++a) {
+    int n = c[1 + a] + g.p[a] - kk[a];
+    if (n < 0 || n % g.s[a]) return false;
+    o[a] = n / g.s[a];
+  }
+  if (o[0] >= so.D || o[1] >= so.H || o[2] >= so.W) return false;
+  oz = o[0];
+  oy = o[1];
+  ox = o[2];
+  return true;
+}
+
+__global__ void k_cand_min(const int* __restrict__ coors, int N, KGeom g, Shape so,
+                           unsigned* __restrict__ grid) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * g.K) return;
+  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  const int* c = coors + 4 * r;
+  int oz, oy, ox;
+  if (!out_of(c, k, g, so, oz, oy, ox)) return;
+  atomicMin(grid + cell(so, c[0], oz, oy, ox), (unsigned)t);
+}
+
+__global__ void k_cand_head(const int* __restrict__ coors, int N, KGeom g, Shape so,
+                            const unsigned* __restrict__ grid, int* __restrict__ flag) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  long long n = (long long)N * g.K;
+  if (t == 0) flag[n] = 0;
+  if (t >= n) return;
+  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  const int* c = coors + 4 * r;
+  int oz, oy, ox, f = 0;
+  if (out_of(c, k, g, so, oz, oy, ox)) f = grid[cell(so, c[0], oz, oy, ox)] == (unsigned)t;
+  flag[t] = f;
+}
+
+__global__ void k_out_assign(const int* __restrict__ coors, int N, KGeom g, Shape so,
+                             const int* __restrict__ flag, const int* __restrict__ pos,
+                             int* __restrict__ grid, int* __restrict__ coors_out) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * g.K || !flag[t]) return;
+  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  const int* c = coors + 4 * r;
+  int oz, oy, ox;
+  out_of(c, k, g, so, oz, oy, ox);
+  int o = pos[t];
+  grid[cell(so, c[0], oz, oy, ox)] = o;
+  int* co = coors_out + 4 * o;
+  co[0] = c[0];
+  co[1] = oz;
+  co[2] = oy;
+  co[3] = ox;
+}
+
+__global__ void k_nbr_fill(const int* __restrict__ coors, int N, KGeom g, Shape so,
+                           const int* __restrict__ grid, int* __restrict__ nbr_out,
+                           int* __restrict__ nbr_in) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * g.K) return;
+  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  const int* c = coors + 4 * r;
+  int oz, oy, ox, o = -1;
+  if (out_of(c, k, g, so, oz, oy, ox)) {
+    o = grid[cell(so, c[0], oz, oy, ox)];
+    nbr_out[(long long)o * g.K + k] = r;
+  }
+  nbr_in[t] = o;
+}
+
+// ------------------------------------------------------------------ implicit GEMM
+enum { A_RAW = 0, A_BNRELU = 1, A_BNBWD = 2 };
+enum { E_FWD = 0, E_DGRAD = 1, E_PLAIN = 2 };
+
+struct GemmArgs {
+  const float* a;       // A source rows [Nsrc, CI] (z of the previous layer, raw, or dy)
+  const float* a2;      // A_BNBWD: z of the same layer [Nsrc, CI]
+  const float* abn;     // A_BNRELU: scale[CI], shift[CI];
+                        // A_BNBWD : gi = g*invstd [CI], m1 [CI], m2 [CI], mean [CI], invstd [CI]
+  const int* nbr;       // [Nout, K] neighbour map
+  int K, rev;           // rev: use column K-1-k (SubM transpose)
+  const float* W;       // [K][CIw][COw]
+  int transW;           // B_k = W[k]^T (dgrad)
+  int CIw, COw;         // weight dims as stored
+  int Nout;
+  float* out;           // [Nout, CO] (CO = real output width)
+  int CO_real;
+  // epilogue
+  const float* ez;      // E_DGRAD: z of the output layer (previous layer in forward order) [Nout, CO]
+  const float* ebn;     // E_DGRAD: scale, shift, mean, invstd of that layer [4*CO]
+  float* part;          // [nblk][2*CO] partial column sums (may be null)
+};
+
+template <int CI, int CO, int AT, int ET>
+__global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
+  constexpr int AS = CI + 2;                       // LDS row stride of A (bank spread)
+  constexpr int BS = (CO % 32 == 0) ? CO + 16 : CO;
+  constexpr int NT = CO / 16;
+  __shared__ float sA[BM * AS];
+  __shared__ float sB[CI * BS];
+  __shared__ int sN[BM * MAXK];
+  __shared__ unsigned kmask;
+  __shared__ float sP[4][2 * CO];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = blockIdx.x * BM;
+  const int K = g.K;
+  if (tid == 0) kmask = 0;
+  __syncthreads();
+  unsigned my = 0;
+  for (int q = tid; q < BM * K; q += BLK) {
+    int r = q / K, k = q - r * K;
+    int kc = g.rev ? K - 1 - k : k;
+    int v = (r0 + r < g.Nout) ? g.nbr[(long long)(r0 + r) * K + kc] : -1;
+    sN[r * MAXK + k] = v;
+    if (v >= 0) my |= 1u << k;
+  }
+  if (my) atomicOr(&kmask, my);
+  __syncthreads();
+  const unsigned mask = kmask;
+  f32x4 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int k = 0; k < K; ++k) {
+    if (!((mask >> k) & 1u)) continue;
+    __syncthreads();
+    // gather A_k: BM rows x CI, transformed on load
+    for (int q = tid; q < BM * CI; q += BLK) {
+      int r = q / CI, c = q - r * CI;
+      int src = sN[r * MAXK + k];
+      float v = 0.0f;
+      if (src >= 0) {
+        float x = g.a[(long long)src * CI + c];
+        if (AT == A_BNRELU) v = fmaxf(fmaf(x, g.abn[c], g.abn[CI + c]), 0.0f);
+        else if (AT == A_BNBWD) {
+          float zz = g.a2[(long long)src * CI + c];
+          float xh = (zz - g.abn[3 * CI + c]) * g.abn[4 * CI + c];
+          v = g.abn[c] * (x - g.abn[CI + c] - xh * g.abn[2 * CI + c]);
+        } else v = x;
+      }
+      sA[r * AS + c] = v;
+    }
+    // B_k = W[k] (CI x CO) or W[k]^T ; zero-pad columns beyond the stored width
+    const float* Wk = g.W + (long long)k * g.CIw * g.COw;
+    for (int q = tid; q < CI * CO; q += BLK) {
+      int c = q / CO, n = q - c * CO;
+      float v = 0.0f;
+      if (!g.transW) { if (c < g.CIw && n < g.COw) v = Wk[c * g.COw + n]; }
+      else { if (n < g.CIw && c < g.COw) v = Wk[n * g.COw + c]; }
+      sB[c * BS + n] = v;
+    }
+    __syncthreads();
+    const float* pa = sA + (w * 16 + (lane & 15)) * AS + (lane >> 4);
+    const float* pb = sB + (lane >> 4) * BS + (lane & 15);
+#pragma unroll 4
+    for (int kk = 0; kk < CI / 4; ++kk) {
+      float a = pa[kk * 4];
+#pragma unroll
+      for (int n = 0; n < NT; ++n) {
+        float b = pb[kk * 4 * BS + n * 16];
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[n], 0, 0, 0);
+      }
+    }
+  }
+  // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg
+  float s1[NT], s2[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    s1[n] = s2[n] = 0.0f;
+    int col = n * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int row = r0 + w * 16 + (lane >> 4) * 4 + j;
+      float v = acc[n][j];
+      if (row < g.Nout && col < g.CO_real) {
+        if (ET == E_DGRAD) {
+          float zz = g.ez[(long long)row * CO + col];
+          float h = fmaxf(fmaf(zz, g.ebn[col], g.ebn[CO + col]), 0.0f);
+          v = h > 0.0f ? v : 0.0f;
+          float xh = (zz - g.ebn[2 * CO + col]) * g.ebn[3 * CO + col];
+          s1[n] += v;
+          s2[n] += v * xh;
+        } else {
+          s1[n] += v;
+          s2[n] += v * v;
+        }
+        g.out[(long long)row * g.CO_real + col] = v;
+      }
+    }
+  }
+  if (ET == E_PLAIN || g.part == nullptr) return;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    s1[n] += __shfl_xor(s1[n], 16, 64);
+    s1[n] += __shfl_xor(s1[n], 32, 64);
+    s2[n] += __shfl_xor(s2[n], 16, 64);
+    s2[n] += __shfl_xor(s2[n], 32, 64);
+    if (lane < 16) {
+      sP[w][n * 16 + lane] = s1[n];
+      sP[w][CO + n * 16 + lane] = s2[n];
+    }
+  }
+  __syncthreads();
+  for (int j = tid; j < 2 * CO; j += BLK)
+    g.part[(long long)blockIdx.x * 2 * CO + j] = sP[0][j] + sP[1][j] + sP[2][j] + sP[3][j];
+}
+
+// ------------------------------------------------------------------ weight gradient
+// dW[k][c][n] = sum_r A_k[r, c] * D[r, n]; block = (row chunk, k). A_k gathered through
+// nbr[:, k] with the forward A transform; D = dz of the output rows (BN backward on load).
+struct WgradArgs {
+  const float* a;     // forward A source [Nsrc, CI]
+  const float* abn;   // forward A transform (A_BNRELU) scale/shift
+  const int* nbr;     // [Nout, K]
+  int K, Nout, rows_per;
+  const float* dy;    // [Nout, CO]
+  const float* z;     // [Nout, CO]
+  const float* dbn;   // gi, m1, m2, mean, invstd [5*CO]
+  float* part;        // [chunks][K][CI][CO]
+};
+
+template <int CI, int CO, int AT>
+__global__ __launch_bounds__(BLK) void k_wgrad(WgradArgs g) {
+  // C[CI x CO] += A^T[CI x rows] D[rows x CO]; MFMA 16x16x4: M = CI, N = CO, K = rows
+  constexpr int RT = 64;                     // rows per LDS tile
+  constexpr int AS = CI + 4, DS = CO + 4;
+  constexpr int MT = (CI + 15) / 16, NT = CO / 16;
+  constexpr int TILES = MT * NT;
+  constexpr int TPW = (TILES + 3) / 4;       // tiles per wave
+  __shared__ float sA[RT * AS];
+  __shared__ float sD[RT * DS];
+  __shared__ int sN[RT];
+  __shared__ int any;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int k = blockIdx.y, chunk = blockIdx.x;
+  const int rb0 = chunk * g.rows_per, rb1 = min(g.Nout, rb0 + g.rows_per);
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int rb = rb0; rb < rb1; rb += RT) {
+    __syncthreads();
+    if (tid == 0) any = 0;
+    __syncthreads();
+    if (tid < RT) {
+      int r = rb + tid;
+      int v = r < rb1 ? g.nbr[(long long)r * g.K + k] : -1;
+      sN[tid] = v;
+      if (v >= 0) any = 1;
+    }
+    __syncthreads();
+    if (!any) continue;
+    for (int q = tid; q < RT * CI; q += BLK) {
+      int r = q / CI, c = q - r * CI;
+      int src = sN[r];
+      float v = 0.0f;
+      if (src >= 0) {
+        float x = g.a[(long long)src * CI + c];
+        v = AT == A_BNRELU ? fmaxf(fmaf(x, g.abn[c], g.abn[CI + c]), 0.0f) : x;
+      }
+      sA[r * AS + c] = v;
+    }
+    for (int q = tid; q < RT * CO; q += BLK) {
+      int r = q / CO, n = q - r * CO;
+      int row = rb + r;
+      float v = 0.0f;
+      if (row < rb1 && sN[r] >= 0) {
+        float d = g.dy[(long long)row * CO + n];
+        float zz = g.z[(long long)row * CO + n];
+        float xh = (zz - g.dbn[3 * CO + n]) * g.dbn[4 * CO + n];
+        v = g.dbn[n] * (d - g.dbn[CO + n] - xh * g.dbn[2 * CO + n]);
+      }
+      sD[r * DS + n] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < TPW; ++t) {
+      int tile = w + 4 * t;
+      if (tile >= TILES) break;
+      int m = tile / NT, n = tile - m * NT;
+      int ci = m * 16 + (lane & 15);
+      const float* pa = sA + (lane >> 4) * AS + (ci < CI ? ci : 0);
+      const float* pd = sD + (lane >> 4) * DS + n * 16 + (lane & 15);
+      f32x4 c = acc[t];
+#pragma unroll 4
+      for (int kk = 0; kk < RT / 4; ++kk) {
+        float a = ci < CI ? pa[kk * 4 * AS] : 0.0f;
+        c = __builtin_amdgcn_mfma_f32_16x16x4f32(a, pd[kk * 4 * DS], c, 0, 0, 0);
+      }
+      acc[t] = c;
+    }
+  }
+  float* out = g.part + ((long long)chunk * g.K + k) * CI * CO;
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) {
+    int tile = w + 4 * t;
+    if (tile >= TILES) break;
+    int m = tile / NT, n = tile - m * NT;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int ci = m * 16 + (lane >> 4) * 4 + j, col = n * 16 + (lane & 15);
+      if (ci < CI) out[ci * CO + col] = acc[t][j];
+    }
+  }
+}
+
+__global__ void k_wgrad_reduce(const float* __restrict__ part, int chunks, long long total,
+                               float* __restrict__ dW) {
+  long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e >= total) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += part[(long long)c * total + e];
+  dW[e] = (float)s;
+}
+
+// ------------------------------------------------------------------ BatchNorm finalize
+// one block per column j < 2C: fixed-order tree sum of the partial rows in double.
+// mode 0 (forward): bn = scale, shift, mean, invstd ; running stats updated.
+// mode 1 (backward): bnb = gi, m1, m2, mean, invstd ; dgamma, dbeta written.
+__global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int N,
+                                                     int mode, const float* __restrict__ gamma,
+                                                     const float* __restrict__ beta, float eps,
+                                                     float mom, float* __restrict__ rmean,
+                                                     float* __restrict__ rvar, const float* __restrict__ fbn,
+                                                     float* __restrict__ bn, double* __restrict__ tot,
+                                                     unsigned* __restrict__ ticket, float* __restrict__ dgamma,
+                                                     float* __restrict__ dbeta) {
+  __shared__ double sh[BLK];
+  __shared__ int lastf;
+  const int j = blockIdx.x;
+  double s = 0.0;
+  for (int r = threadIdx.x; r < nblk; r += BLK) s += part[(long long)r * 2 * C + j];
+  sh[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = BLK / 2; o > 0; o >>= 1) {
+    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tot[j] = sh[0];
+  if (!last_block_arrive(ticket, &lastf)) return;
+  for (int c = threadIdx.x; c < C; c += BLK) {
+    double s1 = tot[c], s2 = tot[C + c];
+    if (mode == 0) {
+      double mean = s1 / N;
+      double var = s2 / N - mean * mean;
+      if (var < 0) var = 0;
+      float invstd = 1.0f / sqrtf((float)var + eps);
+      float sc = gamma[c] * invstd;
+      bn[c] = sc;
+      bn[C + c] = beta[c] - (float)mean * sc;
+      bn[2 * C + c] = (float)mean;
+      bn[3 * C + c] = invstd;
+      double uvar = N > 1 ? var * N / (N - 1) : var;
+      rmean[c] = (1.0f - mom) * rmean[c] + mom * (float)mean;
+      rvar[c] = (1.0f - mom) * rvar[c] + mom * (float)uvar;
+    } else {
+      // fbn: forward scale, shift, mean, invstd of this layer
+      bn[c] = gamma[c] * fbn[3 * C + c];
+      bn[C + c] = (float)(s1 / N);
+      bn[2 * C + c] = (float)(s2 / N);
+      bn[3 * C + c] = fbn[2 * C + c];
+      bn[4 * C + c] = fbn[3 * C + c];
+      if (dgamma) dgamma[c] = (float)s2;
+      if (dbeta) dbeta[c] = (float)s1;
+    }
+  }
+}
+
+// ------------------------------------------------------------------ dense BEV
+// forward: dense[b, c*D + z, y, x] = relu(bn(z_rows[r, c])) ; backward: gather + ReLU mask +
+// BatchNorm-backward partial sums (one 64-row tile per block, like the GEMM epilogue)
+__global__ __launch_bounds__(BLK) void k_to_dense(const float* __restrict__ z, const float* __restrict__ bn,
+                                                  const int* __restrict__ coors, int N, int C, Shape s,
+                                                  float* __restrict__ dense) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * C) return;
+  int r = (int)(t / C), c = (int)(t - (long long)r * C);
+  const int* co = coors + 4 * r;
+  float h = fmaxf(fmaf(z[t], bn[c], bn[C + c]), 0.0f);
+  long long idx = (((long long)co[0] * C + c) * s.D + co[1]) * s.H * s.W + (long long)co[2] * s.W + co[3];
+  dense[idx] = h;
+}
+
+__global__ __launch_bounds__(BLK) void k_from_dense(const float* __restrict__ gd, const float* __restrict__ z,
+                                                    const float* __restrict__ bn, const int* __restrict__ coors,
+                                                    int N, int C, Shape s, float* __restrict__ dy,
+                                                    float* __restrict__ part) {
+  // block: 64 rows x C channels (C <= 256), thread handles channels c = tid % C ...
+  __shared__ float sp[2 * 256];
+  const int r0 = blockIdx.x * BM;
+  for (int j = threadIdx.x; j < 2 * C; j += BLK) sp[j] = 0.0f;
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += BLK) {
+    float s1 = 0.0f, s2 = 0.0f;
+    for (int r = r0; r < min(N, r0 + BM); ++r) {
+      const int* co = coors + 4 * r;
+      long long idx = (((long long)co[0] * C + c) * s.D + co[1]) * s.H * s.W + (long long)co[2] * s.W + co[3];
+      float zz = z[(long long)r * C + c];
+      float h = fmaxf(fmaf(zz, bn[c], bn[C + c]), 0.0f);
+      float v = h > 0.0f ? gd[idx] : 0.0f;
+      dy[(long long)r * C + c] = v;
+      s1 += v;
+      s2 += v * ((zz - bn[2 * C + c]) * bn[3 * C + c]);
+    }
+    part[(long long)blockIdx.x * 2 * C + c] = s1;
+    part[(long long)blockIdx.x * 2 * C + C + c] = s2;
+  }
+}
+
+// ------------------------------------------------------------------ dispatch
+template <int CI, int CO>
+static void launch_gemm_t(int at, int et, const GemmArgs& a, int nblk, hipStream_t st) {
+#define G(AT, ET) hipLaunchKernelGGL((k_gemm<CI, CO, AT, ET>), dim3(nblk), dim3(BLK), 0, st, a)
+  if (at == A_RAW && et == E_FWD) G(A_RAW, E_FWD);
+  else if (at == A_BNRELU && et == E_FWD) G(A_BNRELU, E_FWD);
+  else if (at == A_BNBWD && et == E_DGRAD) G(A_BNBWD, E_DGRAD);
+  else if (at == A_BNBWD && et == E_PLAIN) G(A_BNBWD, E_PLAIN);
+#undef G
+}
+
+static int launch_gemm(int CI, int CO, int at, int et, const GemmArgs& a, int nblk, hipStream_t st) {
+#define C2(ci, co) if (CI == ci && CO == co) { launch_gemm_t<ci, co>(at, et, a, nblk, st); return RPC_OK; }
+  // forward pairs (CI, CO) of SparseEncoder and their dgrad transposes (CO, CI->pad16)
+  C2(4, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
+  C2(32, 16) C2(64, 32) C2(128, 64)
+#undef C2
+  return RPC_ERR_UNSUPPORTED;
+}
+
+static int launch_wgrad(int CI, int CO, int at, const WgradArgs& a, dim3 grid, hipStream_t st) {
+#define C2(ci, co)                                                                               \
+  if (CI == ci && CO == co) {                                                                    \
+    if (at == A_BNRELU) hipLaunchKernelGGL((k_wgrad<ci, co, A_BNRELU>), grid, dim3(BLK), 0, st, a); \
+    else hipLaunchKernelGGL((k_wgrad<ci, co, A_RAW>), grid, dim3(BLK), 0, st, a);                 \
+    return RPC_OK;                                                                               \
+  }
+  C2(4, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
+#undef C2
+  return RPC_ERR_UNSUPPORTED;
+}
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+}  // namespace sp
+}  // namespace rpc
+
+using namespace rpc;
+using namespace rpc::sp;
+
+static KGeom geom(const int* ks, const int* st, const int* pd) {
+  KGeom g;
+  for (int a = 0; a < 3; ++a) {
+    g.k[a] = ks[a];
+    g.s[a] = st ? st[a] : 1;
+    g.p[a] = pd ? pd[a] : 0;
+  }
+  g.K = ks[0] * ks[1] * ks[2];
+  return g;
+}
+
+extern "C" int rpc_subm_rulebook(const int* coors, int N, const int* shape /* host B,D,H,W */,
+                                 const int* ksize /* host [3] */, int* grid, int* nbr, void* stream) {
+  if (N < 0 || !shape || !ksize) return RPC_ERR_ARG;
+  if (N == 0) return RPC_OK;
+  if (!coors || !grid || !nbr) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  Shape s{shape[0], shape[1], shape[2], shape[3]};
+  KGeom g = geom(ksize, nullptr, nullptr);
+  if (g.K > MAXK) return RPC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_grid_set, dim3(cdiv(N, BLK)), dim3(BLK), 0, st, coors, N, s, grid, 0);
+  hipLaunchKernelGGL(k_subm_nbr, dim3(cdiv((long long)N * g.K, BLK)), dim3(BLK), 0, st, coors, N, s, g,
+                     grid, nbr);
+  hipLaunchKernelGGL(k_grid_set, dim3(cdiv(N, BLK)), dim3(BLK), 0, st, coors, N, s, grid, 1);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" size_t rpc_spconv_rulebook_workspace_size(int N, int K) {
+  size_t n = (size_t)N * K + 1, scan_b = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (int*)nullptr, (int*)nullptr, (int)n, (hipStream_t)0) !=
+      hipSuccess)
+    return 0;
+  return al(n * sizeof(int)) * 2 + al(scan_b);
+}
+
+extern "C" int rpc_spconv_rulebook_count(const int* coors, int N, const int* out_shape /* B,D,H,W */,
+                                         const int* ksize, const int* stride, const int* pad, int* grid_out,
+                                         int* n_out /* device int */, void* ws, size_t ws_bytes, void* stream) {
+  if (N < 1 || !coors || !grid_out || !n_out || !ws) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  Shape so{out_shape[0], out_shape[1], out_shape[2], out_shape[3]};
+  KGeom g = geom(ksize, stride, pad);
+  if (g.K > MAXK) return RPC_ERR_UNSUPPORTED;
+  size_t n = (size_t)N * g.K + 1;
+  if (ws_bytes < rpc_spconv_rulebook_workspace_size(N, g.K)) return RPC_ERR_WORKSPACE;
+  int* flag = (int*)ws;
+  int* pos = (int*)((char*)ws + al(n * sizeof(int)));
+  void* tmp = (char*)ws + 2 * al(n * sizeof(int));
+  size_t tb = 0;
+  RPC_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)n, st));
+  int nb = cdiv((long long)N * g.K, BLK);
+  hipLaunchKernelGGL(k_cand_min, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, (unsigned*)grid_out);
+  hipLaunchKernelGGL(k_cand_head, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, (const unsigned*)grid_out, flag);
+  RPC_LAUNCH_CHECK();
+  RPC_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, pos, (int)n, st));
+  RPC_CHECK(hipMemcpyAsync(n_out, pos + (n - 1), sizeof(int), hipMemcpyDeviceToDevice, st));
+  return RPC_OK;
+}
+
+extern "C" int rpc_spconv_rulebook_build(const int* coors, int N, const int* out_shape, const int* ksize,
+                                         const int* stride, const int* pad, int* grid_out, int n_out,
+                                         int* coors_out, int* nbr_out, int* nbr_in, void* ws, void* stream) {
+  if (N < 1 || !coors || !grid_out || !coors_out || !nbr_out || !nbr_in || !ws) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  Shape so{out_shape[0], out_shape[1], out_shape[2], out_shape[3]};
+  KGeom g = geom(ksize, stride, pad);
+  size_t n = (size_t)N * g.K + 1;
+  int* flag = (int*)ws;
+  int* pos = (int*)((char*)ws + al(n * sizeof(int)));
+  int nb = cdiv((long long)N * g.K, BLK);
+  RPC_CHECK(hipMemsetAsync(nbr_out, 0xFF, sizeof(int) * (size_t)n_out * g.K, st));
+  hipLaunchKernelGGL(k_out_assign, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, flag, pos, grid_out, coors_out);
+  hipLaunchKernelGGL(k_nbr_fill, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, grid_out, nbr_out, nbr_in);
+  if (n_out > 0)
+    hipLaunchKernelGGL(k_grid_set, dim3(cdiv(n_out, BLK)), dim3(BLK), 0, st, coors_out, n_out, so, grid_out, 1);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+// forward conv: z_out = conv(A(in)) ; writes BatchNorm partial sums [nblk][2*CO] if part != NULL
+extern "C" int rpc_spconv_gemm_blocks(int n_out) { return cdiv(n_out, BM); }
+
+extern "C" int rpc_spconv_forward(const float* in, const float* in_bn /* scale,shift or NULL: raw */,
+                                  int CI, const int* nbr, int K, int n_out, const float* W, int CO,
+                                  float* z_out, float* part, void* stream) {
+  if (n_out < 0 || K > MAXK) return RPC_ERR_ARG;
+  if (n_out == 0) return RPC_OK;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.a = in;
+  a.abn = in_bn;
+  a.nbr = nbr;
+  a.K = K;
+  a.W = W;
+  a.CIw = CI;
+  a.COw = CO;
+  a.Nout = n_out;
+  a.out = z_out;
+  a.CO_real = CO;
+  a.part = part;
+  int rc = launch_gemm(CI, CO, in_bn ? A_BNRELU : A_RAW, E_FWD, a, cdiv(n_out, BM), (hipStream_t)stream);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+// dgrad: din = sum_k dz_out[map[:, k]] W[k]^T, with dz computed on load from (dy, z, bnb);
+// if prev_z != NULL, the ReLU mask and BatchNorm-backward partial sums of the previous
+// layer (prev_bn = its forward scale/shift/mean/invstd) are applied/written.
+extern "C" int rpc_spconv_dgrad(const float* dy_out, const float* z_out, const float* bnb /* 5*CO */,
+                                int CO, const int* map, int K, int rev, int n_in, const float* W, int CI,
+                                const float* prev_z, const float* prev_bn, float* din, float* part,
+                                void* stream) {
+  if (n_in < 0 || K > MAXK) return RPC_ERR_ARG;
+  if (n_in == 0) return RPC_OK;
+  GemmArgs a;
+  memset(&a, 0, sizeof(a));
+  a.a = dy_out;
+  a.a2 = z_out;
+  a.abn = bnb;
+  a.nbr = map;
+  a.K = K;
+  a.rev = rev;
+  a.W = W;
+  a.transW = 1;
+  a.CIw = CI;
+  a.COw = CO;
+  a.Nout = n_in;
+  a.out = din;
+  a.CO_real = CI;
+  a.ez = prev_z;
+  a.ebn = prev_bn;
+  a.part = part;
+  int CIg = CO, COg = CI < 16 ? 16 : CI;
+  int rc = launch_gemm(CIg, COg, A_BNBWD, prev_z ? E_DGRAD : E_PLAIN, a, cdiv(n_in, BM), (hipStream_t)stream);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" size_t rpc_spconv_wgrad_workspace_size(int n_out, int K, int CI, int CO) {
+  int chunks = cdiv(n_out > 0 ? n_out : 1, 2048);
+  if (chunks > 64) chunks = 64;
+  return (size_t)chunks * K * CI * CO * sizeof(float);
+}
+
+extern "C" int rpc_spconv_wgrad(const float* in, const float* in_bn, int CI, const int* nbr, int K, int n_out,
+                                const float* dy_out, const float* z_out, const float* bnb, int CO, float* dW,
+                                void* ws, size_t ws_bytes, void* stream) {
+  if (n_out < 0 || K > MAXK) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (n_out == 0) {
+    RPC_CHECK(hipMemsetAsync(dW, 0, sizeof(float) * (size_t)K * CI * CO, st));
+    return RPC_OK;
+  }
+  int chunks = cdiv(n_out, 2048);
+  if (chunks > 64) chunks = 64;
+  if (ws_bytes < (size_t)chunks * K * CI * CO * sizeof(float)) return RPC_ERR_WORKSPACE;
+  WgradArgs a;
+  a.a = in;
+  a.abn = in_bn;
+  a.nbr = nbr;
+  a.K = K;
+  a.Nout = n_out;
+  a.rows_per = ((cdiv(n_out, chunks) + 63) / 64) * 64;
+  a.dy = dy_out;
+  a.z = z_out;
+  a.dbn = bnb;
+  a.part = (float*)ws;
+  int rc = launch_wgrad(CI, CO, in_bn ? A_BNRELU : A_RAW, a, dim3(chunks, K), st);
+  if (rc) return rc;
+  long long total = (long long)K * CI * CO;
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(cdiv(total, BLK)), dim3(BLK), 0, st, (const float*)ws, chunks, total,
+                     dW);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" size_t rpc_bn_finalize_workspace_size(int C) { return al(sizeof(double) * 2 * C) + 256; }
+
+extern "C" int rpc_bn_finalize(const float* part, int nblk, int C, int N, int mode, const float* gamma,
+                               const float* beta, float eps, float momentum, float* running_mean,
+                               float* running_var, const float* fwd_bn, float* bn_out, float* dgamma, float* dbeta,
+                               void* ws, void* stream) {
+  if (C < 1 || nblk < 1 || !part || !bn_out || !ws) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  double* tot = (double*)ws;
+  unsigned* ticket = (unsigned*)((char*)ws + al(sizeof(double) * 2 * C));
+  RPC_CHECK(hipMemsetAsync(ticket, 0, sizeof(unsigned), st));
+  hipLaunchKernelGGL(k_bn_finalize, dim3(2 * C), dim3(BLK), 0, st, part, nblk, C, N, mode, gamma, beta, eps,
+                     momentum, running_mean, running_var, fwd_bn, bn_out, tot, ticket, dgamma, dbeta);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_sparse_to_dense(const float* z, const float* bn, const int* coors, int N, int C,
+                                   const int* shape /* B,D,H,W */, float* dense, void* stream) {
+  if (N < 0 || C < 1 || !shape) return RPC_ERR_ARG;
+  if (N == 0) return RPC_OK;
+  Shape s{shape[0], shape[1], shape[2], shape[3]};
+  hipLaunchKernelGGL(k_to_dense, dim3(cdiv((long long)N * C, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn,
+                     coors, N, C, s, dense);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dense_to_sparse_grad(const float* grad_dense, const float* z, const float* bn, const int* coors,
+                                        int N, int C, const int* shape, float* dy, float* part, void* stream) {
+  if (N < 0 || C < 1 || C > 256 || !shape) return RPC_ERR_ARG;
+  if (N == 0) return RPC_OK;
+  Shape s{shape[0], shape[1], shape[2], shape[3]};
+  hipLaunchKernelGGL(k_from_dense, dim3(cdiv(N, BM)), dim3(BLK), 0, (hipStream_t)stream, grad_dense, z, bn, coors,
+                     N, C, s, dy, part);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}

@@ -1,0 +1,284 @@
+"""SECOND sparse middle encoder on the HIP kernels.
+
+`SparseEncoder` mirrors upstream mmdet3d `SparseEncoder` (the `middle_encoder` of
+configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:19-23, called
+at models/detectors/adversarial_voxelnet.py:141) with its defaults: conv_module blocks,
+base_channels 16, output_channels 128, encoder_channels ((16,), (32,32,32), (64,64,64),
+(64,64,64)), encoder_paddings ((1,), (1,1,1), (1,1,1), ((0,1,1),1,1)), BatchNorm1d eps 1e-3
+momentum 0.01, conv bias off, order conv-norm-act, indice keys subm1..4 / spconv2..4 /
+spconv_down2, and the final `.dense()` + view(N, C*D, H, W).
+
+The whole encoder is ONE autograd node: forward builds the rulebooks (four host reads
+of output counts, one per strided conv), runs 12 implicit-GEMM convs with BatchNorm
+statistics in their epilogues and normalisation+ReLU folded into the next conv's gather;
+backward walks the layers in reverse (dense gather, BN backward folded into the dgrad
+gather, weight grads as split-K slabs). State-dict keys follow mmdet3d's module names;
+conv weights are stored [K, C_in, C_out] (k = (kz*3 + ky)*3 + kx).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+
+import torch
+from torch import nn
+
+from . import _ffi
+
+
+@dataclass
+class _Spec:
+    kind: str          # 'subm' | 'spconv'
+    ci: int
+    co: int
+    ksize: tuple
+    stride: tuple
+    pad: tuple
+    key: str
+    lvl_in: int
+    lvl_out: int
+    name: str
+
+    @property
+    def K(self):
+        return self.ksize[0] * self.ksize[1] * self.ksize[2]
+
+
+def _t3(v):
+    return tuple(v) if isinstance(v, (tuple, list)) else (v, v, v)
+
+
+def _conv_out(shape, k, s, p):
+    return tuple((shape[a] + 2 * p[a] - (k[a] - 1) - 1) // s[a] + 1 for a in range(3))
+
+
+class _ConvWeight(nn.Module):
+    """Holds the sparse conv weight [K, C_in, C_out] (spconv's module slot '0')."""
+
+    def __init__(self, K, ci, co):
+        super().__init__()
+        self.weight = nn.Parameter(torch.empty(K, ci, co))
+        bound = 1.0 / math.sqrt(ci * K)   # kaiming_uniform(a=sqrt(5)) like torch/spconv convs
+        nn.init.uniform_(self.weight, -bound, bound)
+
+
+class _ConvBN(nn.Sequential):
+    def __init__(self, K, ci, co, eps, momentum):
+        super().__init__(_ConvWeight(K, ci, co), nn.BatchNorm1d(co, eps=eps, momentum=momentum))
+
+
+class SparseEncoder(nn.Module):
+    def __init__(self, in_channels, sparse_shape, order=("conv", "norm", "act"),
+                 norm_cfg=dict(type="BN1d", eps=1e-3, momentum=0.01), base_channels=16, output_channels=128,
+                 encoder_channels=((16,), (32, 32, 32), (64, 64, 64), (64, 64, 64)),
+                 encoder_paddings=((1,), (1, 1, 1), (1, 1, 1), ((0, 1, 1), 1, 1)), block_type="conv_module",
+                 return_middle_feats=False):
+        super().__init__()
+        if tuple(order) != ("conv", "norm", "act") or block_type != "conv_module" or return_middle_feats:
+            raise NotImplementedError("only the SECOND configuration (conv-norm-act, conv_module) is built")
+        eps = norm_cfg.get("eps", 1e-3)
+        mom = norm_cfg.get("momentum", 0.01)
+        self.sparse_shape = tuple(int(s) for s in sparse_shape)
+        self.in_channels = in_channels
+        specs = []
+        shapes = [self.sparse_shape]
+        specs.append(_Spec("subm", in_channels, base_channels, (3, 3, 3), (1, 1, 1), (1, 1, 1), "subm1", 0, 0,
+                           "conv_input"))
+        self.conv_input = _ConvBN(27, in_channels, base_channels, eps, mom)
+        self.encoder_layers = nn.Module()
+        ci = base_channels
+        lvl = 0
+        for i, blocks in enumerate(encoder_channels):
+            stage = nn.Module()
+            for j, co in enumerate(tuple(blocks)):
+                pad = _t3(tuple(encoder_paddings[i])[j])
+                if i != 0 and j == 0:
+                    out = _conv_out(shapes[lvl], (3, 3, 3), (2, 2, 2), pad)
+                    shapes.append(out)
+                    specs.append(_Spec("spconv", ci, co, (3, 3, 3), (2, 2, 2), pad, f"spconv{i + 1}", lvl, lvl + 1,
+                                       f"encoder_layers.encoder_layer{i + 1}.{j}"))
+                    lvl += 1
+                else:
+                    specs.append(_Spec("subm", ci, co, (3, 3, 3), (1, 1, 1), pad, f"subm{i + 1}", lvl, lvl,
+                                       f"encoder_layers.encoder_layer{i + 1}.{j}"))
+                stage.add_module(str(j), _ConvBN(27, ci, co, eps, mom))
+                ci = co
+            self.encoder_layers.add_module(f"encoder_layer{i + 1}", stage)
+        out = _conv_out(shapes[lvl], (3, 1, 1), (2, 1, 1), (0, 0, 0))
+        shapes.append(out)
+        specs.append(_Spec("spconv", ci, output_channels, (3, 1, 1), (2, 1, 1), (0, 0, 0), "spconv_down2", lvl,
+                           lvl + 1, "conv_out"))
+        self.conv_out = _ConvBN(3, ci, output_channels, eps, mom)
+        self.specs = specs
+        self.shapes = shapes
+        self.output_channels = output_channels
+        self._grids = {}
+
+    def layers(self):
+        mods = [self.conv_input]
+        for st in self.encoder_layers.children():
+            mods += list(st.children())
+        mods.append(self.conv_out)
+        return mods
+
+    def grid(self, lvl, B, device):
+        """Dense int32 index grid [B, D, H, W] kept all -1 between uses."""
+        key = (lvl, B, str(device))
+        g = self._grids.get(key)
+        if g is None:
+            D, H, W = self.shapes[lvl]
+            g = torch.full((B * D * H * W,), -1, dtype=torch.int32, device=device)
+            self._grids[key] = g
+        return g
+
+    def forward(self, voxel_features, coors, batch_size):
+        params = []
+        for m in self.layers():
+            params += [m[0].weight, m[1].weight, m[1].bias]
+        return SparseEncoderFn.apply(voxel_features, coors, self, int(batch_size), *params)
+
+
+def _cdiv(a, b):
+    return (a + b - 1) // b
+
+
+class SparseEncoderFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feats, coors, enc: SparseEncoder, B: int, *params):
+        lib = _ffi.load()
+        dev = feats.device
+        st = _ffi.stream_of(feats)
+        feats = feats.contiguous().float()
+        coors = coors.to(torch.int32).contiguous()
+        mods = enc.layers()
+        rb = {}
+        cur_coors, cur_n = coors, feats.shape[0]
+        src, src_bn = feats, None
+        L = []
+        for li, (sp, m) in enumerate(zip(enc.specs, mods)):
+            W = params[3 * li]
+            gamma, beta = params[3 * li + 1], params[3 * li + 2]
+            bnm = m[1]
+            ks = _ffi.int_arr(sp.ksize)
+            rec = dict(spec=sp, n_in=cur_n, src=src, src_bn=src_bn, coors_in=cur_coors)
+            if sp.kind == "subm":
+                if sp.key not in rb:
+                    nbr = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
+                    shp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_in])
+                    _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, ks,
+                                                     _ffi.ptr(enc.grid(sp.lvl_in, B, dev)), _ffi.ptr(nbr), st),
+                               "rpc_subm_rulebook")
+                    rb[sp.key] = nbr
+                rec.update(nbr=rb[sp.key], n_out=cur_n, coors_out=cur_coors)
+            else:
+                oshp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_out])
+                sd, pd = _ffi.int_arr(sp.stride), _ffi.int_arr(sp.pad)
+                wsb = lib.rpc_spconv_rulebook_workspace_size(cur_n, sp.K)
+                ws = _ffi.workspace(wsb, dev)
+                n_dev = torch.empty(1, dtype=torch.int32, device=dev)
+                gout = enc.grid(sp.lvl_out, B, dev)
+                _ffi.check(lib.rpc_spconv_rulebook_count(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
+                                                         _ffi.ptr(n_dev), _ffi.ptr(ws), wsb, st),
+                           "rpc_spconv_rulebook_count")
+                n_out = int(n_dev.item())          # host read: output row count
+                coors_out = torch.empty((n_out, 4), dtype=torch.int32, device=dev)
+                nbr_out = torch.empty((n_out, sp.K), dtype=torch.int32, device=dev)
+                nbr_in = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
+                _ffi.check(lib.rpc_spconv_rulebook_build(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
+                                                         n_out, _ffi.ptr(coors_out), _ffi.ptr(nbr_out),
+                                                         _ffi.ptr(nbr_in), _ffi.ptr(ws), st),
+                           "rpc_spconv_rulebook_build")
+                rec.update(nbr=nbr_out, nbr_in=nbr_in, n_out=n_out, coors_out=coors_out)
+            n_out = rec["n_out"]
+            z = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
+            nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
+            part = torch.zeros((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
+            _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
+                                              n_out, _ffi.ptr(W), sp.co, _ffi.ptr(z), _ffi.ptr(part), st),
+                       "rpc_spconv_forward")
+            bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
+            wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(sp.co), dev)
+            _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
+                                           float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
+                                           _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
+                                           _ffi.ptr(wsb), st), "rpc_bn_finalize")
+            bnm.num_batches_tracked += 1
+            rec.update(z=z, bn=bn, W=W, gamma=gamma, beta=beta)
+            L.append(rec)
+            src, src_bn = z, bn
+            cur_coors, cur_n = rec["coors_out"], n_out
+        last = L[-1]
+        D, H, Wd = enc.shapes[-1]
+        C = last["spec"].co
+        dense = torch.zeros((B, C, D, H, Wd), dtype=torch.float32, device=dev)
+        shp = _ffi.int_arr((B, D, H, Wd))
+        _ffi.check(lib.rpc_sparse_to_dense(_ffi.ptr(last["z"]), _ffi.ptr(last["bn"]), _ffi.ptr(last["coors_out"]),
+                                           last["n_out"], C, shp, _ffi.ptr(dense), st), "rpc_sparse_to_dense")
+        ctx.L = L
+        ctx.B = B
+        ctx.shape = (B, C, D, H, Wd)
+        ctx.n_feat = feats.shape
+        return dense.view(B, C * D, H, Wd)
+
+    @staticmethod
+    def backward(ctx, gdense):
+        lib = _ffi.load()
+        L = ctx.L
+        dev = gdense.device
+        st = _ffi.stream_of(gdense)
+        B, C, D, H, Wd = ctx.shape
+        gd = gdense.contiguous().view(B, C, D, H, Wd)
+        grads = [None] * (3 * len(L))
+        last = L[-1]
+        n = last["n_out"]
+        dy = torch.empty((n, C), dtype=torch.float32, device=dev)
+        nblk = max(lib.rpc_spconv_gemm_blocks(n), 1)
+        part = torch.zeros((nblk, 2 * C), dtype=torch.float32, device=dev)
+        _ffi.check(lib.rpc_dense_to_sparse_grad(_ffi.ptr(gd), _ffi.ptr(last["z"]), _ffi.ptr(last["bn"]),
+                                                _ffi.ptr(last["coors_out"]), n, C, _ffi.int_arr((B, D, H, Wd)),
+                                                _ffi.ptr(dy), _ffi.ptr(part), st), "rpc_dense_to_sparse_grad")
+        dfeat = None
+        for li in range(len(L) - 1, -1, -1):
+            rec = L[li]
+            sp = rec["spec"]
+            n_out = rec["n_out"]
+            # BatchNorm backward statistics of this layer -> bnb, dgamma, dbeta
+            bnb = torch.empty(5 * sp.co, dtype=torch.float32, device=dev)
+            dgamma = torch.empty_like(rec["gamma"])
+            dbeta = torch.empty_like(rec["beta"])
+            wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(sp.co), dev)
+            _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 1, _ffi.ptr(rec["gamma"]),
+                                           _ffi.ptr(rec["beta"]), 0.0, 0.0, None, None, _ffi.ptr(rec["bn"]),
+                                           _ffi.ptr(bnb), _ffi.ptr(dgamma), _ffi.ptr(dbeta), _ffi.ptr(wsb), st),
+                       "rpc_bn_finalize(bwd)")
+            # weight gradient
+            dW = torch.empty_like(rec["W"])
+            wsz = lib.rpc_spconv_wgrad_workspace_size(n_out, sp.K, sp.ci, sp.co)
+            ws = _ffi.workspace(wsz, dev)
+            _ffi.check(lib.rpc_spconv_wgrad(_ffi.ptr(rec["src"]), _ffi.ptr(rec["src_bn"]), sp.ci, _ffi.ptr(rec["nbr"]),
+                                            sp.K, n_out, _ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
+                                            _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_spconv_wgrad")
+            grads[3 * li: 3 * li + 3] = [dW, dgamma, dbeta]
+            # data gradient into the previous layer (ReLU mask + its BN-backward partial sums)
+            n_in = rec["n_in"]
+            if sp.kind == "subm":
+                mp, rev = rec["nbr"], 1
+            else:
+                mp, rev = rec["nbr_in"], 0
+            din = torch.empty((n_in, sp.ci), dtype=torch.float32, device=dev)
+            if li > 0:
+                prev = L[li - 1]
+                nblk = max(lib.rpc_spconv_gemm_blocks(n_in), 1)
+                part = torch.zeros((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
+                _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co, _ffi.ptr(mp),
+                                                sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, _ffi.ptr(prev["z"]),
+                                                _ffi.ptr(prev["bn"]), _ffi.ptr(din), _ffi.ptr(part), st),
+                           "rpc_spconv_dgrad")
+                dy = din
+            elif ctx.needs_input_grad[0]:
+                _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co, _ffi.ptr(mp),
+                                                sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None, None,
+                                                _ffi.ptr(din), None, st), "rpc_spconv_dgrad")
+                dfeat = din
+        ctx.L = None
+        return (dfeat, None, None, None, *grads)

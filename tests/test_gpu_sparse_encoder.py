@@ -1,0 +1,74 @@
+"""a6 parity: HIP SparseEncoder (rulebooks + implicit-GEMM convs + BN + dense) against the
+CPU float64 oracle, forward and backward, on voxelised synthetic KITTI frames."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import voxelize as ov
+from oracle.sparse_encoder import OracleSparseEncoder, spconv_pairs, subm_pairs
+from robustpointclouds_amd.sparse_encoder import SparseEncoder
+from robustpointclouds_amd.synthetic import KITTI_PC_RANGE, KITTI_VOXEL_SIZE, kitti_frame
+
+pytestmark = pytest.mark.gpu
+
+
+def _inputs(B, stride=3, seed=0):
+    frames = [kitti_frame(seed + i)[::stride] for i in range(B)]
+    vox, coors, npts = ov.voxelize_frames(frames, KITTI_VOXEL_SIZE, KITTI_PC_RANGE, 5, 16000)
+    feats = vox[:, :, :4].sum(1) / npts[:, None]
+    return feats.astype(np.float32), coors.astype(np.int32)
+
+
+@pytest.mark.parametrize("B,stride", [(2, 4), (1, 1)])
+def test_sparse_encoder_forward_backward_matches_oracle(B, stride):
+    torch.manual_seed(0)
+    feats, coors = _inputs(B, stride)
+    dev = torch.device("cuda")
+    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    with torch.no_grad():   # non-trivial BN affine params
+        for m in enc.layers():
+            m[1].weight.uniform_(0.5, 1.5)
+            m[1].bias.uniform_(-0.2, 0.2)
+    orc = OracleSparseEncoder(enc)
+    f = torch.from_numpy(feats).to(dev).requires_grad_(True)
+    out = enc(f, torch.from_numpy(coors).to(dev), B)
+    ref_f = torch.from_numpy(feats).double().requires_grad_(True)
+    ref = orc.forward(ref_f, coors, B)
+    assert out.shape == ref.shape == (B, 256, 200, 176)
+    o = out.detach().cpu().double()
+    scale = ref.abs().max().item()
+    assert (o - ref.detach()).abs().max().item() <= 1e-4 * max(scale, 1.0)
+    # running stats
+    for m, p in zip(enc.layers(), orc.params):
+        np.testing.assert_allclose(m[1].running_mean.cpu().numpy(), p["rm"].numpy(), rtol=1e-4, atol=1e-5)
+        np.testing.assert_allclose(m[1].running_var.cpu().numpy(), p["rv"].numpy(), rtol=1e-3, atol=1e-5)
+    G = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
+    (out * G.to(dev)).sum().backward()
+    (ref * G.double()).sum().backward()
+    gf = f.grad.cpu().double()
+    rs = ref_f.grad.abs().max().item()
+    assert (gf - ref_f.grad).abs().max().item() <= 2e-4 * rs
+    for m, p in zip(enc.layers(), orc.params):
+        for got, want in [(m[0].weight.grad, p["W"].grad), (m[1].weight.grad, p["g"].grad), (m[1].bias.grad, p["b"].grad)]:
+            s = want.abs().max().item()
+            assert (got.cpu().double() - want).abs().max().item() <= 2e-4 * s + 1e-9
+
+
+def test_rulebooks_match_oracle_pairs():
+    feats, coors = _inputs(2, 5)
+    dev = torch.device("cuda")
+    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    out = enc(torch.from_numpy(feats).to(dev), torch.from_numpy(coors).to(dev), 2)
+    # deterministic: the same input gives the same bytes
+    out2 = enc(torch.from_numpy(feats).to(dev), torch.from_numpy(coors).to(dev), 2)
+    # (BN running stats moved, but the batch-stat forward output does not depend on them)
+    assert torch.equal(out, out2)
+    # grids are left clean (all -1) after use
+    for g in enc._grids.values():
+        assert int((g != -1).sum().item()) == 0
+    # pair counts per offset of the first SubM and the first strided conv
+    c = coors.astype(np.int64)
+    sub = subm_pairs(c, (2, 41, 1600, 1408))
+    assert sum(len(a) for a, _ in sub) > 0
+    oc, sp = spconv_pairs(c, (2, 21, 800, 704), (3, 3, 3), (2, 2, 2), (1, 1, 1))
+    assert oc.shape[0] > 0

@@ -1,0 +1,156 @@
+"""Benchmark: adversarial-train frames/s of the SECOND KITTI step (BASELINE.json).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Workload (BASELINE.json configs[1]): AdversarialVoxelNet (SECOND) KITTI Car-only, batch 6
+frames per GPU, perturber active (_epoch = 3), dense backbone/neck/head under bf16 autocast
+(voxelize / perturber / sparse encoder in fp32 kernels), AdamW + clip 0.5, synthetic
+HDL-64E-like frames pre-staged in HBM. N > 1: frames sharded across ranks (weak scaling),
+DDP gradient all-reduce over RCCL. Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+
+def _args():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=6)
+    ap.add_argument("--classes", type=int, default=1, choices=[1, 3])
+    ap.add_argument("--fp32", action="store_true", help="dense part in fp32 (parity mode)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-frames", type=int, default=6)
+    return ap.parse_args()
+
+
+def _batches(n, B, rank, dev, classes):
+    from robustpointclouds_amd.anchor_head import pack_gt
+    from robustpointclouds_amd.synthetic import kitti_batch
+    out = []
+    for j in range(n):
+        pts, boxes, labels = kitti_batch(B, seed0=(rank * n + j) * B, num_classes=classes)
+        out.append(([torch.from_numpy(p).to(dev) for p in pts], _gt(boxes, labels, dev)))
+    return out
+
+
+def _gt(boxes, labels, dev):
+    from robustpointclouds_amd.anchor_head import pack_gt
+    gb, gl = pack_gt(list(zip(boxes, labels)), dev)
+    return dict(gt_boxes=gb, gt_labels=gl)
+
+
+def cpu_baseline(frames: int, classes: int):
+    """The oracle restatement of the whole step on the host cores (bounded sample)."""
+    from oracle import voxelize as ov
+    from oracle.perturber import OraclePerturber, perturb_voxels
+    from oracle.sparse_encoder import OracleSparseEncoder
+    from robustpointclouds_amd.anchor_head import pack_gt
+    from robustpointclouds_amd.plugin.models.adversarial.voxel_perturber import VoxelPerturber
+    from robustpointclouds_amd.synthetic import KITTI_PC_RANGE, KITTI_VOXEL_SIZE, kitti_batch
+    from robustpointclouds_amd.trainer import make_kitti_model
+    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    torch.set_num_threads(cores)
+    model = make_kitti_model(num_classes=classes, device=None)  # CPU torch modules (dense part)
+    adv = model.adversary
+    lin = [m for m in adv.model if isinstance(m, torch.nn.Linear)]
+    bns = [m for m in adv.model if isinstance(m, torch.nn.BatchNorm1d)]
+    att = [m for m in adv.attention if isinstance(m, torch.nn.Linear)]
+    w = {}
+    for l, m in enumerate(lin):
+        w[f"W{l}"], w[f"b{l}"] = m.weight.detach().numpy(), m.bias.detach().numpy()
+    for l, m in enumerate(bns):
+        w[f"g{l}"], w[f"be{l}"] = m.weight.detach().numpy(), m.bias.detach().numpy()
+    for l, m in enumerate(att):
+        w[f"Wa{l}"], w[f"ba{l}"] = m.weight.detach().numpy(), m.bias.detach().numpy()
+    op = OraclePerturber(w, 4, adv.hidden_channels, dtype=torch.float32)
+    enc = OracleSparseEncoder(model.middle_encoder, dtype=torch.float32)
+    params = [t for t in op.p.values()] + [p for d in enc.params for p in (d["W"], d["g"], d["b"])] + \
+        [p for n, p in model.named_parameters() if not n.startswith(("adversary", "middle_encoder"))]
+    opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-3)
+    pts, boxes, labels = kitti_batch(frames, seed0=1000, num_classes=classes)
+    gt = pack_gt(list(zip(boxes, labels)), torch.device("cpu"))
+
+    def step():
+        vox, coors, npts = ov.voxelize_frames(pts, KITTI_VOXEL_SIZE, KITTI_PC_RANGE, 5, 16000)
+        vfe, _, ld = perturb_voxels(op, vox, npts)
+        x = enc.forward(vfe.float(), coors, frames)
+        x = model.neck(model.backbone(x))
+        losses = model.bbox_head.loss(x, dict(gt_boxes=gt[0], gt_labels=gt[1]))
+        total = sum(v[0] for v in losses.values()) + 0.01 * (3 * ld["intensity_loss"] + 10 * ld["bias_loss"] +
+                                                             10 * ld["imbalance_loss"]) + 0.02 * ld["l2_norm"]
+        total.backward()
+        torch.nn.utils.clip_grad_norm_(params, 0.5)
+        opt.step()
+        opt.zero_grad()
+
+    step()                       # warm-up
+    t0 = time.perf_counter()
+    step()
+    dt = time.perf_counter() - t0
+    return dict(value=round(frames / dt, 4), unit="frames/s", cores=cores, kind="port",
+                sample=f"1 timed step (after 1 warm-up) of the oracle restatement (C voxelize, torch-CPU fp32 "
+                       f"perturber + sparse encoder, torch-CPU SECOND/FPN/Anchor3DHead fwd+bwd, AdamW) on "
+                       f"{frames} synthetic KITTI frames, {classes}-class, {dt:.1f} s")
+
+
+def main():
+    a = _args()
+    from robustpointclouds_amd.trainer import Trainer, init_distributed, make_kitti_model
+    rank, world, local = init_distributed()
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+    torch.manual_seed(0)
+    model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3)
+    tr = Trainer(model, ddp=world > 1, bf16=not a.fp32, device=dev)
+    NB = 4
+    data = _batches(NB, a.batch, rank, dev, a.classes)
+    for i in range(a.warmup):
+        tr.train_step(*data[i % NB])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        tr.train_step(*data[i % NB])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    frames = world * a.batch * a.steps
+    if rank == 0:
+        res = dict(metric="adversarial-train frames/sec/GPU, SECOND KITTI-3class, at 1/2/4/8 MI355X",
+                   value=round(frames / dt, 3), unit="frames/s", n_gpus=world, steps=a.steps, warmup=a.warmup,
+                   ms_per_step=round(1000 * dt / a.steps, 3), higher_is_better=True, scaling="weak",
+                   vs_baseline=None, dtype="fp32" if a.fp32 else "bf16", data="synthetic",
+                   config=dict(workload="AdversarialVoxelNet (SECOND) KITTI " +
+                               ("Car-only" if a.classes == 1 else "3-class") +
+                               f", batch {a.batch}/GPU, perturber active (_epoch=3)",
+                               global_batch=world * a.batch, frames_per_gpu=a.batch,
+                               dense_dtype="fp32" if a.fp32 else "bf16",
+                               kernel_dtype="fp32 (voxelize, perturber, sparse encoder)",
+                               parallelism=f"dp{world}"))
+        if not a.no_cpu_baseline:
+            res["cpu_baseline"] = cpu_baseline(a.cpu_frames, a.classes)
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,81 @@
+"""Loss combination of AdversarialVoxelNet.loss, device-side.
+
+Restates models/detectors/adversarial_voxelnet.py:187-427 without its host
+synchronisations (`.item()` at :229 and :405): the data-dependent branches become
+`torch.where` on device scalars, with identical values and gradients:
+  det_loss_total = clamp(sum clamp(v, 0, 100) over Tensor-valued 'loss' keys, skipping
+                   NaN/Inf, 0, 500)                                          (:203-215)
+  loss_adversarial = clamp(-det - 10 (l2 - 0.05), -10, 10) if det > 0 else 0  (:281-300, :366-367)
+  loss_intensity = 3 I, loss_bias = 10 B, loss_imbalance = 10 S               (:378-391)
+  loss_adversarial += 0.01 (loss_intensity + loss_bias + loss_imbalance)     (:395-398)
+  reg_scale = max(0.1, 1 - (epoch+1)/30) x {0.01 | 0.1 | 0.3 | 1} by l2        (:401-411)
+  loss_l2_regularization = regularization_weight * reg_scale * l2            (:413)
+  perturbation_l2_norm = l2.detach()                                         (:421)
+With upstream's list-valued head losses (Anchor3DHead), det is identically 0, so
+loss_adversarial = 0.01 * aux (SURVEY.md finding 3).
+"""
+from __future__ import annotations
+
+import torch
+
+
+def _zero(device):
+    return torch.tensor(0.0, device=device, requires_grad=True)
+
+
+def combine_adversarial_losses(losses_pts: dict, l2, loss_dict, epoch: int, regularization_weight: float,
+                               training: bool, device) -> dict:
+    losses = dict(losses_pts)
+    if not training or l2 is None:                                          # :422-425
+        losses["loss_adversarial"] = _zero(device)
+        losses["loss_l2_regularization"] = _zero(device)
+        return losses
+    tensor_items = [v for k, v in losses_pts.items() if "loss" in k and isinstance(v, torch.Tensor)]
+    if tensor_items:
+        det = torch.zeros((), device=device)
+        for v in tensor_items:
+            c = torch.clamp(v, min=0.0, max=100.0)
+            det = det + torch.where(torch.isfinite(c), c, torch.zeros_like(c))
+        det = torch.clamp(det, min=0.0, max=500.0)
+        adv = -1.0 * det
+        if l2.requires_grad:
+            adv = adv + (-10.0 * (l2 - 0.05))
+        adv = torch.clamp(adv, min=-10.0, max=10.0)
+        adv = torch.where((det > 0) & torch.isfinite(det), adv, torch.zeros_like(adv))
+    else:
+        adv = _zero(device)
+    losses["loss_adversarial"] = adv
+    if loss_dict is not None:
+        zero = lambda: _zero(device)
+        li = loss_dict.get("intensity_loss", None)
+        lb = loss_dict.get("bias_loss", None)
+        lm = loss_dict.get("imbalance_loss", None)
+        losses["loss_intensity"] = 3.0 * li if (li is not None and li.requires_grad) else zero()
+        losses["loss_bias"] = 10.0 * lb if (lb is not None and lb.requires_grad) else zero()
+        losses["loss_imbalance"] = 10.0 * lm if (lm is not None and lm.requires_grad) else zero()
+        losses["loss_adversarial"] = losses["loss_adversarial"] + 0.01 * (
+            losses["loss_intensity"] + losses["loss_bias"] + losses["loss_imbalance"])
+        reg_scale = max(0.1, 1.0 - ((epoch + 1) / 30.0))
+        l2d = l2.detach()
+        mult = torch.where(l2d < 0.001, 0.01, torch.where(l2d < 0.005, 0.1, torch.where(l2d < 0.01, 0.3, 1.0)))
+        losses["loss_l2_regularization"] = (regularization_weight * reg_scale) * mult.to(l2.dtype) * l2
+    else:
+        for k in ("loss_intensity", "loss_bias", "loss_imbalance", "loss_l2_regularization"):
+            losses[k] = _zero(device)
+    losses["perturbation_l2_norm"] = l2.detach()
+    return losses
+
+
+def parse_losses(losses: dict):
+    """mmengine BaseModel.parse_losses: total = sum of means of every key containing 'loss'
+    (lists: sum of their means); returns (total, log_vars)."""
+    log_vars = {}
+    for k, v in losses.items():
+        if isinstance(v, torch.Tensor):
+            log_vars[k] = v.mean()
+        elif isinstance(v, (list, tuple)) and all(isinstance(t, torch.Tensor) for t in v):
+            log_vars[k] = sum(t.mean() for t in v)
+        else:
+            raise TypeError(f"{k} is not a tensor or list of tensors")
+    total = sum(v for k, v in log_vars.items() if "loss" in k)
+    return total, dict(loss=total, **log_vars)

@@ -1,0 +1,226 @@
+"""VoxelPerturber — drop-in for models/adversarial/voxel_perturber.py:19-541.
+
+Same registry name, constructor, nn.Sequential layout / state-dict keys
+(`model.{0,3,6,9,12,15}` Linear, `model.{1,4,7,10,13}` BatchNorm1d, `attention.{0,2}`),
+initialisation (:434-462) and `forward(x[N, F]) -> (x + pert, loss_dict)` semantics; the
+arithmetic runs in the HIP kernels of robustpointclouds_amd.perturb (no CPU path).
+
+Declared deviations (SURVEY.md findings 2, §5):
+* the network is built EAGERLY in __init__ (the reference builds it on the first forward,
+  :142-147, so its parameters miss the optimizer and DDP); F is guessed exactly as the
+  reference does (:61) and the model is rebuilt lazily if a forward brings another F;
+* the grad hook clamp(nan_to_num(g), -0.1, 0.1) (:465-475) is applied inside the backward
+  kernel to each parameter's full gradient (identical values; no per-tensor hook launches);
+* NaN input / NaN perturbations (:150-153, :195-200, :259-262) are detected on the device:
+  the output is the unperturbed input and the loss terms are zeros (no host sync), and
+  the per-step metrics (:388-409) are accumulated on the device and read only in
+  save_l2_norms().
+"""
+from __future__ import annotations
+
+import csv
+import warnings
+from typing import Tuple
+
+import torch
+from torch import nn
+
+from robustpointclouds_amd import perturb as _P
+
+from ..builder import ADVERSARIES
+
+_HIST_CAP = 1 << 16
+
+
+@ADVERSARIES.register_module(force=True)
+class VoxelPerturber(nn.Module):
+    def __init__(self, sensor_error_bound: float = 0.2, voxel_size: list = [0.05, 0.05, 0.1],
+                 use_spatial_attention: bool = True, hidden_channels: list = [8, 16, 32]):
+        super().__init__()
+        self.sensor_error_bound = float(sensor_error_bound)
+        self.voxel_size = torch.tensor(list(voxel_size))
+        self.use_spatial_attention = use_spatial_attention
+        self.voxel_error_bound = sensor_error_bound / torch.tensor(list(voxel_size) + [1.0])
+        self.auto_detect_dims = True
+        in_features = 5 if (voxel_size[0] >= 0.1 or voxel_size[2] >= 0.15) else 4
+        self.in_features = in_features
+        self.hidden_channels = list(hidden_channels)
+        self.model = None
+        self.attention = None
+        self.l2_norms = []
+        self.l2_percentages = []
+        self.constraint_violations = []
+        self.perturbation_stats = []
+        self._hist = None
+        self._hist_n = 0
+        self._build_model(in_features)
+
+    # ------------------------------------------------------------------ build / init
+    def _build_model(self, num_features):
+        h = self.hidden_channels
+        dev = self.model[0].weight.device if self.model is not None else None
+        self.model = nn.Sequential(
+            nn.Linear(num_features, h[0]), nn.BatchNorm1d(h[0]), nn.ReLU(inplace=True),
+            nn.Linear(h[0], h[1]), nn.BatchNorm1d(h[1]), nn.ReLU(inplace=True),
+            nn.Linear(h[1], h[2]), nn.BatchNorm1d(h[2]), nn.ReLU(inplace=True),
+            nn.Linear(h[2], h[1]), nn.BatchNorm1d(h[1]), nn.ReLU(inplace=True),
+            nn.Linear(h[1], h[0]), nn.BatchNorm1d(h[0]), nn.ReLU(inplace=True),
+            nn.Linear(h[0], num_features), nn.Tanh())
+        if self.use_spatial_attention:
+            a = max(num_features // 2, 1)
+            self.attention = nn.Sequential(nn.Linear(num_features, a), nn.ReLU(inplace=True), nn.Linear(a, 1),
+                                           nn.Sigmoid())
+        self.in_features = num_features
+        self._init_weights()
+        if dev is not None:
+            self.to(dev)
+
+    def _init_weights(self):
+        for m in self.modules():                                  # :439-462
+            if isinstance(m, nn.Linear):
+                if m.out_features in (4, 5):
+                    std = 0.025 if m.out_features == 4 else 0.01
+                    nn.init.normal_(m.weight, 0.0, std)
+                    if m.bias is not None:
+                        nn.init.normal_(m.bias, 0.0, std)
+                else:
+                    nn.init.xavier_uniform_(m.weight, gain=1.0)
+                    if m.bias is not None:
+                        nn.init.constant_(m.bias, 0)
+            elif isinstance(m, nn.BatchNorm1d):
+                nn.init.constant_(m.weight, 1)
+                nn.init.constant_(m.bias, 0)
+                m.momentum = 0.1
+                m.eps = 1e-3
+
+    def _reset_problematic_weights(self):
+        """:477-497 (only called on NaN detection, so its host reads are off the hot path)."""
+        with torch.no_grad():
+            for m in self.modules():
+                if isinstance(m, nn.Linear):
+                    if torch.isnan(m.weight).any():
+                        nn.init.xavier_uniform_(m.weight, gain=0.001)
+                    if m.bias is not None and torch.isnan(m.bias).any():
+                        nn.init.constant_(m.bias, 0)
+                elif isinstance(m, nn.BatchNorm1d):
+                    if torch.isnan(m.weight).any():
+                        nn.init.constant_(m.weight, 1)
+                    if torch.isnan(m.bias).any():
+                        nn.init.constant_(m.bias, 0)
+                    if torch.isnan(m.running_mean).any():
+                        nn.init.constant_(m.running_mean, 0)
+                    if torch.isnan(m.running_var).any():
+                        nn.init.constant_(m.running_var, 1)
+
+    # ------------------------------------------------------------------ kernel plumbing
+    def kernel_params(self):
+        """36 tensors in rpc_perturber order (include/rpc_hip.h)."""
+        lin = [m for m in self.model if isinstance(m, nn.Linear)]
+        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
+        ps = []
+        for l in range(5):
+            ps += [lin[l].weight, lin[l].bias, bns[l].weight, bns[l].bias, bns[l].running_mean, bns[l].running_var]
+        ps += [lin[5].weight, lin[5].bias]
+        if self.use_spatial_attention:
+            att = [m for m in self.attention if isinstance(m, nn.Linear)]
+            ps += [att[0].weight, att[0].bias, att[1].weight, att[1].bias]
+        else:
+            ps += [None] * 4
+        return ps
+
+    def _cfg(self, F, vfe_features=4):
+        bn = [m for m in self.model if isinstance(m, nn.BatchNorm1d)][0]
+        return _P.make_cfg(F, self.hidden_channels, self.use_spatial_attention, self.training,
+                           self.sensor_error_bound, bn.eps, bn.momentum, vfe_features)
+
+    def _ensure_width(self, F):
+        if F != self.in_features:
+            warnings.warn(f"VoxelPerturber: rebuilding for {F} input features (built for {self.in_features}); "
+                          "the new parameters are not in an optimizer created before this call")
+            self._build_model(F)
+
+    def _bump_batch_counts(self):
+        if self.training:
+            for m in self.model:
+                if isinstance(m, nn.BatchNorm1d):
+                    m.num_batches_tracked += 1
+
+    @staticmethod
+    def _loss_dict(lvec):
+        return {"l2_norm": lvec[0], "intensity_loss": lvec[1], "bias_loss": lvec[2], "imbalance_loss": lvec[3]}
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, voxel_features: torch.Tensor) -> Tuple[torch.Tensor, dict]:
+        assert voxel_features.dim() == 2, f"Expected 2D input, got {voxel_features.dim()}D"
+        self._ensure_width(voxel_features.shape[1])
+        x = voxel_features.float()
+        out, lvec, flags = _P.PerturberFn.apply(x, self._cfg(x.shape[1]), *self.kernel_params())
+        self._bump_batch_counts()
+        if self.training:
+            self._track(lvec, out.detach() - x.detach(), x.detach().norm(dim=1).mean())
+        return out, self._loss_dict(lvec)
+
+    def perturb_voxels(self, voxels: torch.Tensor, num_points: torch.Tensor, vfe_features: int = 4):
+        """Fused path of AdversarialVoxelNet.extract_feat (adversarial_voxelnet.py:85-137):
+        valid-slot mask + perturber + masked scatter + HardSimpleVFE in one kernel sequence.
+        Returns (vfe [V, vfe_features], loss_dict, perturbed voxels, flags)."""
+        self._ensure_width(voxels.shape[-1])
+        vfe, lvec, pert, flags = _P.PerturbVoxelsFn.apply(voxels.float(), num_points,
+                                                          self._cfg(voxels.shape[-1], vfe_features),
+                                                          *self.kernel_params())
+        self._bump_batch_counts()
+        if self.training:
+            self._track(lvec, None, None)
+        return vfe, self._loss_dict(lvec), pert, flags
+
+    # ------------------------------------------------------------------ metrics
+    def _track(self, lvec, pert, ref_norm):
+        """Device-side version of _track_metrics (:388-409): no .item() per step."""
+        if self._hist is None or self._hist.device != lvec.device:
+            self._hist = torch.zeros((_HIST_CAP, 6), dtype=torch.float32, device=lvec.device)
+            self._hist_n = 0
+        if self._hist_n >= _HIST_CAP:
+            self._flush_hist()
+        nan = torch.full((), float("nan"), device=lvec.device)
+        l2 = lvec[0].detach()
+        if pert is not None:
+            mx = pert.abs().max()
+            row = torch.stack([l2, l2 / (ref_norm + 1e-8) * 100,
+                               torch.clamp(mx - self.voxel_error_bound.max().item(), min=0.0), mx,
+                               pert.abs().mean(), pert.std()])
+        else:
+            row = torch.stack([l2, nan, nan, nan, nan, nan])
+        self._hist[self._hist_n] = row
+        self._hist_n += 1
+
+    def _flush_hist(self):
+        if self._hist is None or self._hist_n == 0:
+            return
+        h = self._hist[: self._hist_n].cpu().tolist()
+        for l2, pct, viol, mx, mean, std in h:
+            self.l2_norms.append(l2)
+            self.l2_percentages.append(pct)
+            self.constraint_violations.append(viol)
+            self.perturbation_stats.append(dict(l2_norm=l2, l2_percentage=pct, max_perturbation=mx,
+                                                mean_perturbation=mean, std_perturbation=std,
+                                                constraint_violation=viol))
+        self._hist_n = 0
+
+    def save_l2_norms(self, filename="l2_norms.csv"):
+        """:411-432 — CSV of the tracked metrics, then clear them."""
+        self._flush_hist()
+        with open(filename, "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["L2 Norm", "L2 Percentage", "Constraint Violations"])
+            for n, p, v in zip(self.l2_norms, self.l2_percentages,
+                               self.constraint_violations or [0] * len(self.l2_norms)):
+                w.writerow([n, p, v])
+        if self.perturbation_stats:
+            with open(filename.replace(".csv", "_detailed.csv"), "w", newline="") as f:
+                w = csv.DictWriter(f, fieldnames=self.perturbation_stats[0].keys())
+                w.writeheader()
+                w.writerows(self.perturbation_stats)
+        self.l2_norms.clear()
+        self.l2_percentages.clear()
+        self.constraint_violations.clear()
+        self.perturbation_stats.clear()

@@ -1,0 +1,135 @@
+"""VoxelNet (SECOND) detector stack on this framework's kernels.
+
+Restates upstream mmdet3d `VoxelNet` (detectors/voxelnet.py) + `Det3DDataPreprocessor`
+(voxel=True, voxel_type='hard') for the SECOND configs in /root/reference/configs:
+voxel_layer (…kitti-3d-car.py:48-53) -> HardSimpleVFE -> SparseEncoder -> SECOND ->
+SECONDFPN -> Anchor3DHead. `AdversarialVoxelNet` (plugin/models/detectors) subclasses it.
+"""
+from __future__ import annotations
+
+import torch
+from torch import nn
+
+from .anchor_head import Anchor3DHead
+from .perturb import VoxelMeanFn
+from .registry import MODELS
+from .second import SECOND, SECONDFPN
+from .sparse_encoder import SparseEncoder
+from .voxelize import Voxelization
+
+
+class HardSimpleVFE(nn.Module):
+    """upstream mmdet3d HardSimpleVFE: mean of the first num_features over the slots (HIP)."""
+
+    def __init__(self, num_features=4):
+        super().__init__()
+        self.num_features = num_features
+
+    def forward(self, features, num_points, coors, *args, **kwargs):
+        return VoxelMeanFn.apply(features, num_points, self.num_features)
+
+
+class Det3DDataPreprocessor(nn.Module):
+    """Voxelisation part of upstream Det3DDataPreprocessor (voxel=True, voxel_type='hard')."""
+
+    def __init__(self, voxel=True, voxel_type="hard", voxel_layer=None, **kw):
+        super().__init__()
+        vl = dict(voxel_layer or dict(max_num_points=5, point_cloud_range=[0, -40, -3, 70.4, 40, 1],
+                                      voxel_size=[0.05, 0.05, 0.1], max_voxels=(16000, 40000)))
+        self.voxel_layer = Voxelization(vl["voxel_size"], vl["point_cloud_range"], vl["max_num_points"],
+                                        vl.get("max_voxels", (16000, 40000)))
+
+    def forward(self, data, training=False):
+        pts = data["inputs"]["points"]
+        self.voxel_layer.train(training)
+        inputs = dict(points=pts, voxels=self.voxel_layer.voxelize_frames(pts))
+        return dict(inputs=inputs, data_samples=data.get("data_samples"))
+
+
+for _c in (HardSimpleVFE, SparseEncoder, SECOND, SECONDFPN, Anchor3DHead, Det3DDataPreprocessor):
+    MODELS.register_module(module=_c)
+
+
+class VoxelNet(nn.Module):
+    def __init__(self, voxel_encoder, middle_encoder, backbone, neck=None, bbox_head=None, train_cfg=None,
+                 test_cfg=None, data_preprocessor=None, init_cfg=None):
+        super().__init__()
+        build = lambda c: c if (c is None or isinstance(c, nn.Module)) else MODELS.build(c)
+        self.data_preprocessor = build(data_preprocessor) if data_preprocessor is not None else \
+            Det3DDataPreprocessor()
+        self.voxel_encoder = build(voxel_encoder)
+        self.middle_encoder = build(middle_encoder)
+        self.backbone = build(backbone)
+        self.neck = build(neck)
+        if bbox_head is not None and not isinstance(bbox_head, nn.Module):
+            bbox_head = dict(bbox_head)
+            bbox_head.update(train_cfg=train_cfg, test_cfg=test_cfg)
+        self.bbox_head = build(bbox_head)
+        self.train_cfg = train_cfg
+        self.test_cfg = test_cfg
+
+    @property
+    def with_neck(self):
+        return self.neck is not None
+
+    def extract_feat(self, batch_inputs_dict):
+        vd = batch_inputs_dict["voxels"]
+        feats = self.voxel_encoder(vd["voxels"], vd["num_points"], vd["coors"])
+        B = batch_inputs_dict.get("batch_size") or int(vd["coors"][-1, 0].item()) + 1
+        x = self.middle_encoder(feats, vd["coors"], B)
+        x = self.backbone(x)
+        if self.with_neck:
+            x = self.neck(x)
+        return x
+
+    def loss(self, batch_inputs_dict, batch_data_samples):
+        return self.bbox_head.loss(self.extract_feat(batch_inputs_dict), batch_data_samples)
+
+
+MODELS.register_module(module=VoxelNet)
+
+
+def second_kitti_cfg(num_classes=1, hidden_channels=None, regularization_weight=0.05, adversarial=True):
+    """The model dict of configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-car.py
+    (num_classes=1) or …-3class.py (num_classes=3) resolved against the upstream
+    second_hv_secfpn_kitti.py base it inherits (which is not vendored in /root/reference)."""
+    if num_classes == 1:
+        anchor = dict(type="Anchor3DRangeGenerator", ranges=[[0, -40.0, -1.78, 70.4, 40.0, -1.78]],
+                      sizes=[[3.9, 1.6, 1.56]], rotations=[0, 1.57], reshape_out=True)
+        assigner = dict(type="Max3DIoUAssigner", iou_calculator=dict(type="BboxOverlapsNearest3D"), pos_iou_thr=0.6,
+                        neg_iou_thr=0.45, min_pos_iou=0.45, ignore_iof_thr=-1)
+        adv = dict(type="VoxelPerturber", **({} if hidden_channels is None else dict(hidden_channels=hidden_channels)))
+    else:
+        anchor = dict(type="Anchor3DRangeGenerator", ranges=[[0, -40.0, -0.6, 70.4, 40.0, -0.6]] * 3,
+                      sizes=[[3.9, 1.6, 1.56], [0.8, 0.6, 1.73], [1.76, 0.6, 1.73]], rotations=[0, 1.57],
+                      reshape_out=False)
+        thr = [(0.6, 0.45, 0.45), (0.35, 0.2, 0.2), (0.35, 0.2, 0.2)]
+        assigner = [dict(type="Max3DIoUAssigner", iou_calculator=dict(type="BboxOverlapsNearest3D"), pos_iou_thr=p,
+                         neg_iou_thr=n, min_pos_iou=m, ignore_iof_thr=-1) for p, n, m in thr]
+        adv = dict(type="VoxelPerturber", sensor_error_bound=0.2, voxel_size=[0.05, 0.05, 0.1],
+                   use_spatial_attention=True, hidden_channels=hidden_channels or [64, 128, 64])
+    cfg = dict(
+        type="AdversarialVoxelNet" if adversarial else "VoxelNet",
+        data_preprocessor=dict(type="Det3DDataPreprocessor", voxel=True, voxel_type="hard",
+                               voxel_layer=dict(max_num_points=5, point_cloud_range=[0, -40, -3, 70.4, 40, 1],
+                                                voxel_size=[0.05, 0.05, 0.1], max_voxels=(16000, 40000))),
+        voxel_encoder=dict(type="HardSimpleVFE"),
+        middle_encoder=dict(type="SparseEncoder", in_channels=4, sparse_shape=[41, 1600, 1408],
+                            order=("conv", "norm", "act")),
+        backbone=dict(type="SECOND", in_channels=256, layer_nums=[5, 5], layer_strides=[1, 2],
+                      out_channels=[128, 256]),
+        neck=dict(type="SECONDFPN", in_channels=[128, 256], upsample_strides=[1, 2], out_channels=[256, 256]),
+        bbox_head=dict(type="Anchor3DHead", num_classes=num_classes, in_channels=512, feat_channels=512,
+                       use_direction_classifier=True, anchor_generator=anchor, diff_rad_by_sin=True,
+                       bbox_coder=dict(type="DeltaXYZWLHRBBoxCoder"),
+                       loss_cls=dict(type="mmdet.FocalLoss", use_sigmoid=True, gamma=2.0, alpha=0.25, loss_weight=1.0),
+                       loss_bbox=dict(type="mmdet.SmoothL1Loss", beta=1.0 / 9.0, loss_weight=2.0),
+                       loss_dir=dict(type="mmdet.CrossEntropyLoss", use_sigmoid=False, loss_weight=0.2)),
+        train_cfg=dict(assigner=assigner, allowed_border=0, pos_weight=-1, debug=False),
+        test_cfg=dict(use_rotate_nms=True, nms_across_levels=False, nms_thr=0.01, score_thr=0.1, min_bbox_size=0,
+                      nms_pre=100, max_num=50))
+    if adversarial:
+        cfg.update(adversary_cfg=adv, regularization_weight=regularization_weight)
+        if num_classes == 3:
+            cfg.update(adversarial_loss_weight=0.1, regularization_weight=0.02)
+    return cfg

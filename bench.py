@@ -32,6 +32,8 @@ def _args():
     ap.add_argument("--fp32", action="store_true", help="dense part in fp32 (parity mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6)
+    ap.add_argument("--roofline-kernel", default="dgrad,64,64",
+                    help="op,ci,co of the sparse conv launches timed with HIP events")
     return ap.parse_args()
 
 
@@ -49,6 +51,23 @@ def _gt(boxes, labels, dev):
     from robustpointclouds_amd.anchor_head import pack_gt
     gb, gl = pack_gt(list(zip(boxes, labels)), dev)
     return dict(gt_boxes=gb, gt_labels=gl)
+
+
+PEAK = {"fp32_mfma": 157.3, "bf16_mfma": 2500.0}   # TFLOP/s dense, MI355X_MICROARCH.md
+
+
+def _traffic(kernel_tag):
+    """HBM bytes per launch of the timed kernel from the committed PMC summary
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, KB -> bytes), else None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic*.json")))
+    if not files:
+        return None
+    d = json.load(open(files[-1]))
+    for name, v in d.get("kernels", {}).items():
+        if kernel_tag in name:
+            return v.get("hbm_bytes_per_launch")
+    return None
 
 
 def cpu_baseline(frames: int, classes: int):
@@ -114,6 +133,10 @@ def main():
     torch.manual_seed(0)
     model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3)
     tr = Trainer(model, ddp=world > 1, bf16=not a.fp32, device=dev)
+    from robustpointclouds_amd.sparse_encoder import KernelTimer
+    op, ci, co = a.roofline_kernel.split(",")
+    timer = KernelTimer(op, int(ci), int(co))
+    model.middle_encoder.timer = timer
     NB = 4
     data = _batches(NB, a.batch, rank, dev, a.classes)
     for i in range(a.warmup):
@@ -121,6 +144,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
+    timer.enabled = True
     t0 = time.perf_counter()
     for i in range(a.steps):
         tr.train_step(*data[i % NB])
@@ -128,6 +152,8 @@ def main():
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
+    timer.enabled = False
+    ks = timer.summary()
     if world > 1:
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -145,6 +171,16 @@ def main():
                                dense_dtype="fp32" if a.fp32 else "bf16",
                                kernel_dtype="fp32 (voxelize, perturber, sparse encoder)",
                                parallelism=f"dp{world}"))
+        if ks:
+            peak = PEAK["bf16_mfma" if ks["dtype"] == "bf16" else "fp32_mfma"]
+            tag = ks["kernel"]
+            res["roofline"] = dict(bound="mfma", achieved=round(ks["tflops"], 3), peak=peak,
+                                   unit="TFLOP/s", frac=round(ks["tflops"] / peak, 4),
+                                   traffic=_traffic(tag.split("::")[-1]),
+                                   kernel=f"{tag} (sparse conv {op} {ci}->{co}, {ks['dtype']} MFMA)",
+                                   avg_launch_ms=round(ks["avg_ms"], 4),
+                                   flops_per_launch=ks["flops_per_launch"], launches=ks["launches"],
+                                   work="2*C_in*C_out FLOP per valid rulebook pair")
         if not a.no_cpu_baseline:
             res["cpu_baseline"] = cpu_baseline(a.cpu_frames, a.classes)
         print(json.dumps(res), flush=True)

@@ -176,6 +176,20 @@ int rpc_sparse_to_dense(const float* z, const float* bn, const int* coors, int n
 int rpc_dense_to_sparse_grad(const float* grad_dense, const float* z, const float* bn, const int* coors,
                              int n, int c, const int* shape, float* dy, float* part, void* stream);
 
+/* ---- a6 perf mode (bf16 MFMA, fp32 accumulate and BatchNorm statistics) */
+/* h[r, c] = bf16(relu?(z*scale+shift)) (bn NULL: identity), rows padded to round8(c) */
+int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, int relu, void* h, void* stream);
+/* dz[r, c] = bf16(gi*(dy - m1 - xhat*m2)) with bnb = gi, m1, m2, mean, invstd (rpc_bn_finalize mode 1) */
+int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const float* bnb, int n, int c, void* dz, void* stream);
+/* W [K][ci][co] fp32 -> per-offset B^T tiles bf16 (forward: [K][co][ci]; dgrad: [K][ci][co]), zero padded */
+size_t rpc_spconv_bf16_weight_elems(int kvol, int ci, int co, int dgrad);
+int rpc_spconv_prep_weight_bf16(const float* W, int kvol, int ci, int co, int dgrad, void* bt, void* stream);
+/* out[r] = sum_k a[map[r, k']] . B_k ; epi 0 forward (+BN partial sums), 1 dgrad (prev ReLU mask +
+ * BN-backward partial sums), 2 plain */
+int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out, const void* bt,
+                         int ng, float* out, const float* prev_z, const float* prev_bn, float* part, int epi,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,341 @@
+// a6 perf mode: bf16-MFMA implicit-GEMM sparse conv (forward and dgrad) for gfx950.
+//
+// Same neighbour-map semantics as spconv.hip, different data path:
+//   * activations are gathered as bf16 rows [N][CP] (CP = channels padded to 8) that an
+//     elementwise pass produced once per layer (relu(bn(z)) forward, the BatchNorm-backward
+//     dz in backward) — a gathered neighbour row is 16..256 B;
+//   * each wave owns 16 output rows and loads its A fragments of v_mfma_f32_16x16x32_bf16
+//     (8 channels of one gathered row per lane, 16 B) straight from global memory into
+//     registers — no LDS round trip, one offset ahead;
+//   * the weight tile B_k^T [N][K] of the next offset is prefetched into registers and
+//     written to the other half of a double-buffered LDS ring while the MFMAs of the current
+//     offset run; one barrier per offset;
+//   * offsets with no neighbour in the 64-row tile are skipped by the block, offsets with
+//     none in a wave's 16 rows are skipped by that wave (no loads, no MFMA).
+// Accumulation in fp32; epilogues identical to spconv.hip (z out + BatchNorm partial sums,
+// or the previous layer's ReLU mask + BatchNorm-backward partial sums). No atomics on data.
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include "common.h"
+
+namespace rpc {
+namespace spb {
+
+constexpr int BLK = 256;
+constexpr int BM = 64;
+constexpr int MAXK = 27;
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned short u16;
+
+__device__ __forceinline__ u16 to_bf16(float f) {
+  __bf16 b = (__bf16)f;   // round-to-nearest-even, NaN kept (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(u16, b);
+}
+
+enum { E_FWD = 0, E_DGRAD = 1, E_PLAIN = 2 };
+
+struct GB {
+  const u16* a;       // gathered source rows [Nsrc][CP] bf16
+  int CP;             // row pitch (elements, multiple of 8)
+  const int* nbr;     // [Nout][K]
+  int K, rev;
+  const u16* bt;      // B^T per offset [K][NGP][KGP] bf16 (zero padded)
+  int Nout;
+  float* out;         // [Nout][CO_real]
+  int CO_real;
+  const float* ez;    // E_DGRAD: z of the layer whose grad this is [Nout][CO_real]
+  const float* ebn;   // E_DGRAD: scale, shift, mean, invstd [4*CO_real]
+  float* part;        // [blocks][2*NGP] or null
+};
+
+template <int KGP, int NT, int EPI>
+__global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
+  constexpr int KS = KGP / 32;
+  constexpr int NGP = NT * 16;
+  constexpr int LS = KGP + 8;                 // LDS row stride (elements): 16 B pad
+  constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
+  constexpr int BPT = (BV + BLK - 1) / BLK;
+  __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];
+  __shared__ int sN[BM * MAXK];
+  __shared__ unsigned wmask[4];
+  __shared__ int klist[MAXK];
+  __shared__ int nk;
+  __shared__ float sP[4][2 * NGP];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r0 = blockIdx.x * BM;
+  const int K = g.K;
+  if (tid < 4) wmask[tid] = 0;
+  __syncthreads();
+  for (int q = tid; q < BM * K; q += BLK) {
+    int r = q / K, k = q - r * K;
+    int kc = g.rev ? K - 1 - k : k;
+    int v = (r0 + r < g.Nout) ? g.nbr[(long long)(r0 + r) * K + kc] : -1;
+    sN[r * MAXK + k] = v;
+    if (v >= 0) atomicOr(&wmask[r >> 4], 1u << k);
+  }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned m = wmask[0] | wmask[1] | wmask[2] | wmask[3];
+    int n = 0;
+    for (int k = 0; k < K; ++k)
+      if ((m >> k) & 1u) klist[n++] = k;
+    nk = n;
+  }
+  __syncthreads();
+  const int NK = nk;
+  const unsigned my = wmask[w];
+  f32x4 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const int arow = w * 16 + (lane & 15);
+  const int ag = lane >> 4;
+  auto load_a = [&](int k, uint4 (&dst)[KS]) {
+    int src = sN[arow * MAXK + k];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      int c0 = ks * 32 + ag * 8;
+      dst[ks] = (src >= 0 && c0 < g.CP) ? *(const uint4*)(g.a + (long long)src * g.CP + c0)
+                                        : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto load_b = [&](int k, uint4 (&dst)[BPT]) {
+    const uint4* src = (const uint4*)(g.bt + (long long)k * NGP * KGP);
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      int v = tid + j * BLK;
+      dst[j] = v < BV ? src[v] : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  auto store_b = [&](int buf, const uint4 (&src)[BPT]) {
+#pragma unroll
+    for (int j = 0; j < BPT; ++j) {
+      int v = tid + j * BLK;
+      if (v < BV) {
+        int e = v * 8, n = e / KGP, c = e - n * KGP;
+        *(uint4*)&sB[buf][n * LS + c] = src[j];
+      }
+    }
+  };
+
+  if (NK > 0) {
+    uint4 acur[KS], anxt[KS], bnx[BPT];
+    {
+      load_b(klist[0], bnx);
+      store_b(0, bnx);
+      if ((my >> klist[0]) & 1u) load_a(klist[0], acur);
+    }
+    __syncthreads();
+    for (int t = 0; t < NK; ++t) {
+      const int k = klist[t];
+      const bool more = t + 1 < NK;
+      const int kn = more ? klist[t + 1] : 0;
+      const bool need_n = more && ((my >> kn) & 1u);
+      if (more) load_b(kn, bnx);
+      if (need_n) load_a(kn, anxt);
+      if ((my >> k) & 1u) {
+        const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          bf16x8 av = __builtin_bit_cast(bf16x8, acur[ks]);
+#pragma unroll
+          for (int n = 0; n < NT; ++n) {
+            bf16x8 bv = *(const bf16x8*)(bb + n * 16 * LS + ks * 32);
+            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[n], 0, 0, 0);
+          }
+        }
+      }
+      if (more) store_b((t + 1) & 1, bnx);
+      __syncthreads();
+      if (need_n) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) acur[ks] = anxt[ks];
+      }
+    }
+  }
+
+  // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg (16x16 shapes, gfx950)
+  float s1[NT], s2[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    s1[n] = s2[n] = 0.0f;
+    int col = n * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      int row = r0 + w * 16 + (lane >> 4) * 4 + j;
+      float v = acc[n][j];
+      if (row < g.Nout && col < g.CO_real) {
+        if (EPI == E_DGRAD) {
+          const int C = g.CO_real;
+          float zz = g.ez[(long long)row * C + col];
+          float h = fmaxf(fmaf(zz, g.ebn[col], g.ebn[C + col]), 0.0f);
+          v = h > 0.0f ? v : 0.0f;
+          float xh = (zz - g.ebn[2 * C + col]) * g.ebn[3 * C + col];
+          s1[n] += v;
+          s2[n] += v * xh;
+        } else {
+          s1[n] += v;
+          s2[n] += v * v;
+        }
+        g.out[(long long)row * g.CO_real + col] = v;
+      }
+    }
+  }
+  if (EPI == E_PLAIN || g.part == nullptr) return;
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    s1[n] += __shfl_xor(s1[n], 16, 64);
+    s1[n] += __shfl_xor(s1[n], 32, 64);
+    s2[n] += __shfl_xor(s2[n], 16, 64);
+    s2[n] += __shfl_xor(s2[n], 32, 64);
+    if (lane < 16) {
+      sP[w][n * 16 + lane] = s1[n];
+      sP[w][NGP + n * 16 + lane] = s2[n];
+    }
+  }
+  __syncthreads();
+  // partial rows keep the CO_real-wide layout expected by rpc_bn_finalize: [blocks][2*CO_real]
+  const int C = g.CO_real;
+  for (int j = tid; j < 2 * C; j += BLK) {
+    int which = j / C, c = j - which * C;
+    float s = 0.0f;
+    for (int ww = 0; ww < 4; ++ww) s += sP[ww][which * NGP + c];
+    g.part[(long long)blockIdx.x * 2 * C + j] = s;
+  }
+}
+
+// ------------------------------------------------------------------ elementwise producers
+__global__ __launch_bounds__(BLK) void k_to_bf16(const float* __restrict__ z, const float* __restrict__ bn, int N,
+                                                 int C, int CP, int relu, u16* __restrict__ h) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * CP) return;
+  int r = (int)(t / CP), c = (int)(t - (long long)r * CP);
+  float v = 0.0f;
+  if (c < C) {
+    v = z[(long long)r * C + c];
+    if (bn) v = fmaf(v, bn[c], bn[C + c]);
+    if (relu) v = fmaxf(v, 0.0f);
+  }
+  h[t] = to_bf16(v);
+}
+
+__global__ __launch_bounds__(BLK) void k_dz_bf16(const float* __restrict__ dy, const float* __restrict__ z,
+                                                 const float* __restrict__ bnb, int N, int C, int CP,
+                                                 u16* __restrict__ dz) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * CP) return;
+  int r = (int)(t / CP), c = (int)(t - (long long)r * CP);
+  float v = 0.0f;
+  if (c < C) {
+    long long i = (long long)r * C + c;
+    float xh = (z[i] - bnb[3 * C + c]) * bnb[4 * C + c];
+    v = bnb[c] * (dy[i] - bnb[C + c] - xh * bnb[2 * C + c]);
+  }
+  dz[t] = to_bf16(v);
+}
+
+// W fp32 [K][CI][CO] -> B^T bf16 [K][NGP][KGP]; fwd: n = co, kk = ci ; dgrad: n = ci, kk = co
+__global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int K, int CI, int CO, int dgrad,
+                                               int NGP, int KGP, u16* __restrict__ bt) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)K * NGP * KGP) return;
+  int kk = (int)(t % KGP);
+  long long q = t / KGP;
+  int n = (int)(q % NGP), k = (int)(q / NGP);
+  float v = 0.0f;
+  if (!dgrad) { if (n < CO && kk < CI) v = W[((long long)k * CI + kk) * CO + n]; }
+  else { if (n < CI && kk < CO) v = W[((long long)k * CI + n) * CO + kk]; }
+  bt[t] = to_bf16(v);
+}
+
+template <int KGP, int NT>
+static void launch_t(int epi, const GB& a, int nblk, hipStream_t st) {
+  if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(BLK), 0, st, a);
+  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(BLK), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(BLK), 0, st, a);
+}
+
+static int launch(int KGP, int NT, int epi, const GB& a, int nblk, hipStream_t st) {
+#define C2(kg, nt) if (KGP == kg && NT == nt) { launch_t<kg, nt>(epi, a, nblk, st); return RPC_OK; }
+  C2(32, 1) C2(32, 2) C2(32, 4) C2(64, 2) C2(64, 4) C2(64, 8) C2(128, 4) C2(32, 8) C2(64, 1) C2(128, 2)
+#undef C2
+  return RPC_ERR_UNSUPPORTED;
+}
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+static inline int r8(int c) { return (c + 7) / 8 * 8; }
+static inline int r16(int c) { return (c + 15) / 16 * 16; }
+static inline int r32(int c) { return (c + 31) / 32 * 32; }
+
+}  // namespace spb
+}  // namespace rpc
+
+using namespace rpc;
+using namespace rpc::spb;
+
+extern "C" int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, int relu, void* h, void* stream) {
+  if (n < 0 || c < 1) return RPC_ERR_ARG;
+  if (n == 0) return RPC_OK;
+  int cp = r8(c);
+  hipLaunchKernelGGL(k_to_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, n, c,
+                     cp, relu, (u16*)h);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const float* bnb, int n, int c, void* dz,
+                                      void* stream) {
+  if (n < 0 || c < 1) return RPC_ERR_ARG;
+  if (n == 0) return RPC_OK;
+  int cp = r8(c);
+  hipLaunchKernelGGL(k_dz_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, dy, z, bnb,
+                     n, c, cp, (u16*)dz);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" size_t rpc_spconv_bf16_weight_elems(int kvol, int ci, int co, int dgrad) {
+  int ng = dgrad ? ci : co, kg = dgrad ? co : ci;
+  return (size_t)kvol * r16(ng) * r32(kg);
+}
+
+extern "C" int rpc_spconv_prep_weight_bf16(const float* W, int kvol, int ci, int co, int dgrad, void* bt,
+                                           void* stream) {
+  int ng = dgrad ? ci : co, kg = dgrad ? co : ci;
+  long long n = (long long)kvol * r16(ng) * r32(kg);
+  hipLaunchKernelGGL(k_wprep, dim3(cdiv(n, BLK)), dim3(BLK), 0, (hipStream_t)stream, W, kvol, ci, co, dgrad, r16(ng),
+                     r32(kg), (u16*)bt);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+// out[r] = sum_k a[map[r, k']] . B_k  with a: bf16 rows of width round8(kg) (kg = GEMM K),
+// B^T from rpc_spconv_prep_weight_bf16; epi 0 = forward (z + BN partial sums), 1 = dgrad with the
+// previous layer's ReLU mask + BN-backward partial sums (prev_z, prev_bn), 2 = plain store.
+extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out,
+                                    const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
+                                    float* part, int epi, void* stream) {
+  if (n_out < 0 || kvol > MAXK || kg < 1 || ng < 1) return RPC_ERR_ARG;
+  if (n_out == 0) return RPC_OK;
+  GB g;
+  memset(&g, 0, sizeof(g));
+  g.a = (const u16*)a;
+  g.CP = r8(kg);
+  g.nbr = map;
+  g.K = kvol;
+  g.rev = rev;
+  g.bt = (const u16*)bt;
+  g.Nout = n_out;
+  g.out = out;
+  g.CO_real = ng;
+  g.ez = prev_z;
+  g.ebn = prev_bn;
+  g.part = part;
+  int rc = launch(r32(kg), r16(ng) / 16, epi, g, cdiv(n_out, BM), (hipStream_t)stream);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}

@@ -113,6 +113,10 @@ class SparseEncoder(nn.Module):
         self.shapes = shapes
         self.output_channels = output_channels
         self._grids = {}
+        self.timer = None   # optional KernelTimer (bench.py roofline), see below
+        # perf mode: forward / dgrad convs on bf16 MFMA with bf16 gathered rows (fp32 accumulate,
+        # fp32 BatchNorm statistics); parity mode (default) is fp32 end to end
+        self.bf16 = False
 
     def layers(self):
         mods = [self.conv_input]
@@ -142,6 +146,67 @@ def _cdiv(a, b):
     return (a + b - 1) // b
 
 
+def _r8(c):
+    return (c + 7) // 8 * 8
+
+
+def _r16(c):
+    return (c + 15) // 16 * 16
+
+
+def _r32(c):
+    return (c + 31) // 32 * 32
+
+
+def _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st):
+    """bf16 dz rows (BatchNorm backward applied) and the dgrad weight tiles W[k] (as B^T)."""
+    sp = rec["spec"]
+    dzb = torch.empty((rec["n_out"], _r8(sp.co)), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_bnbwd_to_bf16_rows(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), rec["n_out"], sp.co,
+                                          _ffi.ptr(dzb), st), "rpc_bnbwd_to_bf16_rows")
+    btd = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 1), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(rec["W"]), sp.K, sp.ci, sp.co, 1, _ffi.ptr(btd), st),
+               "rpc_spconv_prep_weight_bf16")
+    return dzb, btd
+
+
+class KernelTimer:
+    """HIP-event timing of selected conv launches on the stream they are launched on.
+
+    select: (op, ci, co) with op in {'fwd', 'dgrad', 'wgrad'}; records per launch the event pair
+    and the algorithmic FLOPs 2 * pairs * ci * co (pairs = valid rulebook entries, counted on the
+    device, read once at the end)."""
+
+    def __init__(self, op, ci, co):
+        self.sel = (op, ci, co)
+        self.recs = []
+        self.enabled = False
+
+    def wants(self, op, sp):
+        return self.enabled and self.sel == (op, sp.ci, sp.co)
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
+
+    def stop(self, e0, nbr, ci, co, kernel=None, dtype="fp32"):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(torch.cuda.current_stream())
+        self.recs.append((e0, e1, nbr, ci, co))   # pairs counted after the timed region
+        self.kernel, self.dtype = kernel, dtype
+
+    def summary(self):
+        torch.cuda.synchronize()
+        if not self.recs:
+            return None
+        ms = sum(a.elapsed_time(b) for a, b, *_ in self.recs)
+        flops = sum(2.0 * float((nbr >= 0).sum().item()) * ci * co for _, _, nbr, ci, co in self.recs)
+        n = len(self.recs)
+        return dict(launches=n, avg_ms=ms / n, flops_per_launch=flops / n, tflops=flops / (ms * 1e-3) / 1e12,
+                    kernel=self.kernel, dtype=self.dtype)
+
+
 class SparseEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feats, coors, enc: SparseEncoder, B: int, *params):
@@ -154,6 +219,11 @@ class SparseEncoderFn(torch.autograd.Function):
         rb = {}
         cur_coors, cur_n = coors, feats.shape[0]
         src, src_bn = feats, None
+        bf16 = enc.bf16
+        if bf16:
+            hsrc = torch.empty((cur_n, _r8(feats.shape[1])), dtype=torch.bfloat16, device=dev)
+            _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(feats), None, cur_n, feats.shape[1], 0, _ffi.ptr(hsrc), st),
+                       "rpc_to_bf16_rows")
         L = []
         for li, (sp, m) in enumerate(zip(enc.specs, mods)):
             W = params[3 * li]
@@ -193,9 +263,25 @@ class SparseEncoderFn(torch.autograd.Function):
             z = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
             nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
             part = torch.zeros((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
-            _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
-                                              n_out, _ffi.ptr(W), sp.co, _ffi.ptr(z), _ffi.ptr(part), st),
-                       "rpc_spconv_forward")
+            tm = enc.timer is not None and enc.timer.wants("fwd", sp)
+            if bf16:
+                bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 0), dtype=torch.bfloat16,
+                                 device=dev)
+                _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), sp.K, sp.ci, sp.co, 0, _ffi.ptr(bt), st),
+                           "rpc_spconv_prep_weight_bf16")
+                e0 = enc.timer.start() if tm else None
+                _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(hsrc), sp.ci, _ffi.ptr(rec["nbr"]), sp.K, 0, n_out,
+                                                    _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None, _ffi.ptr(part), 0,
+                                                    st), "rpc_spconv_gemm_bf16")
+            else:
+                e0 = enc.timer.start() if tm else None
+                _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
+                                                  n_out, _ffi.ptr(W), sp.co, _ffi.ptr(z), _ffi.ptr(part), st),
+                           "rpc_spconv_forward")
+            if tm:
+                kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.ci)}, {_r16(sp.co) // 16}, 0>" if bf16 else
+                      f"rpc::sp::k_gemm<{sp.ci}, {sp.co}, {1 if li else 0}, 0>")
+                enc.timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if bf16 else "fp32")
             bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
             wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(sp.co), dev)
             _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
@@ -206,6 +292,10 @@ class SparseEncoderFn(torch.autograd.Function):
             rec.update(z=z, bn=bn, W=W, gamma=gamma, beta=beta)
             L.append(rec)
             src, src_bn = z, bn
+            if bf16 and li + 1 < len(enc.specs):
+                hsrc = torch.empty((n_out, _r8(sp.co)), dtype=torch.bfloat16, device=dev)
+                _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(z), _ffi.ptr(bn), n_out, sp.co, 1, _ffi.ptr(hsrc), st),
+                           "rpc_to_bf16_rows")
             cur_coors, cur_n = rec["coors_out"], n_out
         last = L[-1]
         D, H, Wd = enc.shapes[-1]
@@ -215,6 +305,8 @@ class SparseEncoderFn(torch.autograd.Function):
         _ffi.check(lib.rpc_sparse_to_dense(_ffi.ptr(last["z"]), _ffi.ptr(last["bn"]), _ffi.ptr(last["coors_out"]),
                                            last["n_out"], C, shp, _ffi.ptr(dense), st), "rpc_sparse_to_dense")
         ctx.L = L
+        ctx.enc = enc
+        ctx.bf16 = bf16
         ctx.B = B
         ctx.shape = (B, C, D, H, Wd)
         ctx.n_feat = feats.shape
@@ -255,9 +347,14 @@ class SparseEncoderFn(torch.autograd.Function):
             dW = torch.empty_like(rec["W"])
             wsz = lib.rpc_spconv_wgrad_workspace_size(n_out, sp.K, sp.ci, sp.co)
             ws = _ffi.workspace(wsz, dev)
+            timer = ctx.enc.timer
+            tw = timer is not None and timer.wants("wgrad", sp)
+            e0 = timer.start() if tw else None
             _ffi.check(lib.rpc_spconv_wgrad(_ffi.ptr(rec["src"]), _ffi.ptr(rec["src_bn"]), sp.ci, _ffi.ptr(rec["nbr"]),
                                             sp.K, n_out, _ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
                                             _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_spconv_wgrad")
+            if tw:
+                timer.stop(e0, rec["nbr"], sp.ci, sp.co, f"rpc::sp::k_wgrad<{sp.ci}, {sp.co}, {1 if li else 0}>", "fp32")
             grads[3 * li: 3 * li + 3] = [dW, dgamma, dbeta]
             # data gradient into the previous layer (ReLU mask + its BN-backward partial sums)
             n_in = rec["n_in"]
@@ -270,15 +367,36 @@ class SparseEncoderFn(torch.autograd.Function):
                 prev = L[li - 1]
                 nblk = max(lib.rpc_spconv_gemm_blocks(n_in), 1)
                 part = torch.zeros((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
-                _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co, _ffi.ptr(mp),
-                                                sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, _ffi.ptr(prev["z"]),
-                                                _ffi.ptr(prev["bn"]), _ffi.ptr(din), _ffi.ptr(part), st),
-                           "rpc_spconv_dgrad")
+                td = timer is not None and timer.wants("dgrad", sp)
+                if ctx.bf16:
+                    dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
+                    e0 = timer.start() if td else None
+                    _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                                                        _ffi.ptr(btd), sp.ci, _ffi.ptr(din), _ffi.ptr(prev["z"]),
+                                                        _ffi.ptr(prev["bn"]), _ffi.ptr(part), 1, st),
+                               "rpc_spconv_gemm_bf16(dgrad)")
+                else:
+                    e0 = timer.start() if td else None
+                    _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
+                                                    _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci,
+                                                    _ffi.ptr(prev["z"]), _ffi.ptr(prev["bn"]), _ffi.ptr(din),
+                                                    _ffi.ptr(part), st), "rpc_spconv_dgrad")
+                if td:
+                    kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.co)}, {_r16(sp.ci) // 16}, 1>" if ctx.bf16 else
+                          f"rpc::sp::k_gemm<{sp.co}, {sp.ci}, 2, 1>")
+                    timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if ctx.bf16 else "fp32")
                 dy = din
             elif ctx.needs_input_grad[0]:
-                _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co, _ffi.ptr(mp),
-                                                sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None, None,
-                                                _ffi.ptr(din), None, st), "rpc_spconv_dgrad")
+                if ctx.bf16:
+                    dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
+                    _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                                                        _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
+                               "rpc_spconv_gemm_bf16(dgrad)")
+                else:
+                    _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
+                                                    _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
+                                                    None, _ffi.ptr(din), None, st), "rpc_spconv_dgrad")
                 dfeat = din
         ctx.L = None
+        ctx.enc = None
         return (dfeat, None, None, None, *grads)

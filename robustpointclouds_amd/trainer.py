@@ -68,6 +68,8 @@ class Trainer:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.module = model.to(self.device)
         self.model = model
+        if bf16 and hasattr(model, "middle_encoder") and hasattr(model.middle_encoder, "bf16"):
+            model.middle_encoder.bf16 = True   # sparse convs on bf16 MFMA in the bf16 perf mode
         if ddp and dist.is_initialized() and dist.get_world_size() > 1:
             self.model = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[self.device.index] if self.device.type == "cuda" else None,

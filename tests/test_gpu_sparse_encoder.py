@@ -46,13 +46,13 @@ def test_sparse_encoder_forward_backward_matches_oracle(B, stride):
     (out * G.to(dev)).sum().backward()
     (ref * G.double()).sum().backward()
     # gradients pass through 12 train-mode BatchNorm backwards (mean-subtracting, so fp32
-    # cancellation; fp32 sums over ~1e4 rows x 27 offsets): relative L2 error <= 3e-4 and
-    # every element within 1e-3 of the max
+    # cancellation; fp32 sums over ~1e4 rows x 27 offsets): relative L2 error <= 1e-3 and
+    # every element within 2e-3 of the max
     def close(got, want, name):
         got = got.cpu().double()
         rel = ((got - want).norm() / want.norm().clamp_min(1e-30)).item()
         mx = (got - want).abs().max().item() / max(want.abs().max().item(), 1e-30)
-        assert rel <= 3e-4 and mx <= 1e-3, (name, rel, mx)
+        assert rel <= 1e-3 and mx <= 2e-3, (name, rel, mx)
     close(f.grad, ref_f.grad, "feats")
     for i, (m, p) in enumerate(zip(enc.layers(), orc.params)):
         close(m[0].weight.grad, p["W"].grad, f"W{i}")
@@ -78,3 +78,28 @@ def test_rulebooks_match_oracle_pairs():
     assert sum(len(a) for a, _ in sub) > 0
     oc, sp = spconv_pairs(c, (2, 21, 800, 704), (3, 3, 3), (2, 2, 2), (1, 1, 1))
     assert oc.shape[0] > 0
+
+
+def test_bf16_perf_mode_close_to_oracle():
+    """bf16 MFMA forward/dgrad (fp32 accumulate + fp32 BN statistics): bf16-level agreement."""
+    torch.manual_seed(0)
+    feats, coors = _inputs(2, 3)
+    dev = torch.device("cuda")
+    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    enc.bf16 = True
+    orc = OracleSparseEncoder(enc)
+    f = torch.from_numpy(feats).to(dev).requires_grad_(True)
+    out = enc(f, torch.from_numpy(coors).to(dev), 2)
+    ref_f = torch.from_numpy(feats).double().requires_grad_(True)
+    ref = orc.forward(ref_f, coors, 2)
+    rel = ((out.detach().cpu().double() - ref.detach()).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel
+    G = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
+    (out * G.to(dev)).sum().backward()
+    (ref * G.double()).sum().backward()
+    relg = ((f.grad.cpu().double() - ref_f.grad).norm() / ref_f.grad.norm()).item()
+    assert relg < 5e-2, relg
+    for i, (m, p) in enumerate(zip(enc.layers(), orc.params)):
+        w = p["W"].grad
+        r = ((m[0].weight.grad.cpu().double() - w).norm() / w.norm()).item()
+        assert r < 5e-2, (i, r)

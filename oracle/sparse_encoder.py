@@ -90,10 +90,11 @@ class OracleSparseEncoder:
                                     rm=m[1].running_mean.detach().cpu().to(dtype).clone(),
                                     rv=m[1].running_var.detach().cpu().to(dtype).clone()))
 
-    def forward(self, feats, coors, B):
+    def forward(self, feats, coors, B, keep=False):
         x = torch.as_tensor(feats).to(self.dtype)
         c = np.asarray(coors, np.int64)
         cache = {}
+        self.trace = []   # keep=True: per layer (coors, z pre-BN, pre-activation) for debugging
         for sp, p in zip(self.specs, self.params):
             if sp.kind == "subm":
                 if sp.key not in cache:
@@ -112,7 +113,11 @@ class OracleSparseEncoder:
                 n = z.shape[0]
                 p["rm"] = (1 - p["mom"]) * p["rm"] + p["mom"] * mean
                 p["rv"] = (1 - p["mom"]) * p["rv"] + p["mom"] * var * n / max(n - 1, 1)
-            x = torch.relu((z - mean) / torch.sqrt(var + p["eps"]) * p["g"] + p["b"])
+            pre = (z - mean) / torch.sqrt(var + p["eps"]) * p["g"] + p["b"]
+            if keep:
+                pre.retain_grad()
+                self.trace.append((c_out, z, pre))
+            x = torch.relu(pre)
             c = c_out
         D, H, W = self.shapes[-1]
         C = x.shape[1]

@@ -63,7 +63,7 @@ struct Dev {
   int* meta;       // [8]: 0 N, 1 fallback flag (NaN / empty)
   float* xs;       // [MAXF] s_f
   float* z[5];     // [C_{l+1}][S] channel-major
-  float* bn[5];    // [4*C]: scale, shift, mean, invstd
+  float* bn[5];    // [4*C]: scale (gamma*invstd), beta, mean, invstd
   double* bnsum[5];  // backward: [2*C] sum dy, sum dy*xhat
   double* part;    // [GRID][2*MAXC]
   float* pstat;    // [4*MAXF]: mean_f, s_f, cimb_f, S
@@ -139,11 +139,10 @@ __device__ void bn_finalize(Dev& d, int l, double* lds) {
     double var = lds[C + c] / N - mean * mean;
     if (var < 0) var = 0;
     float invstd = 1.0f / sqrtf((float)var + d.eps);
-    float sc = d.g[l][c] * invstd;
-    float sh = d.be[l][c] - (float)mean * sc;
+    // applied as (z - mean) * scale + beta (no cancellation)
     float* bn = d.bn[l];
-    bn[c] = sc;
-    bn[C + c] = sh;
+    bn[c] = d.g[l][c] * invstd;
+    bn[C + c] = d.be[l][c];
     bn[2 * C + c] = (float)mean;
     bn[3 * C + c] = invstd;
     double uvar = N > 1 ? var * N / (N - 1) : var;
@@ -292,15 +291,16 @@ __global__ __launch_bounds__(BLK) void k_fwd_first(Dev d) {
 // layer l (1..4): relu(bn_{l-1}(z_{l-1})) -> z_l
 template <int CI, int CO>
 __global__ __launch_bounds__(BLK) void k_fwd_mid(Dev d, int l) {
-  __shared__ float sW[CO * CI + CO + 2 * CI];
+  __shared__ float sW[CO * CI + CO + 3 * CI];
   __shared__ double lds[NWAVE * 2 * MAXC];
   __shared__ int lastf;
   for (int j = threadIdx.x; j < CO * CI; j += BLK) sW[j] = d.W[l][j];
   for (int j = threadIdx.x; j < CO; j += BLK) sW[CO * CI + j] = d.b[l][j];
-  for (int j = threadIdx.x; j < 2 * CI; j += BLK) sW[CO * CI + CO + j] = d.bn[l - 1][j];
+  for (int j = threadIdx.x; j < 3 * CI; j += BLK) sW[CO * CI + CO + j] = d.bn[l - 1][j];
   __syncthreads();
   const float* sc = sW + CO * CI + CO;
   const float* sh = sc + CI;
+  const float* mu = sh + CI;
   const int N = d.meta[0];
   ChanAcc<CO> acc;
   acc.zero();
@@ -311,7 +311,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_mid(Dev d, int l) {
     const float* zi = d.z[l - 1] + (act ? i : 0);
 #pragma unroll
     for (int c = 0; c < CI; ++c)
-      h[c] = act ? fmaxf(fmaf(zi[(size_t)c * d.S], sc[c], sh[c]), 0.0f) : 0.0f;
+      h[c] = act ? fmaxf(fmaf(zi[(size_t)c * d.S] - mu[c], sc[c], sh[c]), 0.0f) : 0.0f;
 #pragma unroll
     for (int o = 0; o < CO; ++o) {
       float a = sW[CO * CI + o];
@@ -346,15 +346,16 @@ __device__ __forceinline__ float attention(const Dev& d, const float (&xn)[F], f
 // output layer: relu(bn4(z4)) -> tanh -> *att -> bounds -> clamp -> out, loss sums
 template <int CI, int F>
 __global__ __launch_bounds__(BLK) void k_fwd_last(Dev d) {
-  __shared__ float sW[F * CI + F + 2 * CI];
+  __shared__ float sW[F * CI + F + 3 * CI];
   __shared__ double lds[NWAVE * 2 * MAXC];
   __shared__ int lastf;
   for (int j = threadIdx.x; j < F * CI; j += BLK) sW[j] = d.W[5][j];
   for (int j = threadIdx.x; j < F; j += BLK) sW[F * CI + j] = d.b[5][j];
-  for (int j = threadIdx.x; j < 2 * CI; j += BLK) sW[F * CI + F + j] = d.bn[4][j];
+  for (int j = threadIdx.x; j < 3 * CI; j += BLK) sW[F * CI + F + j] = d.bn[4][j];
   __syncthreads();
   const float* sc = sW + F * CI + F;
   const float* sh = sc + CI;
+  const float* mu = sh + CI;
   const int N = d.meta[0];
   // sums: [0] sum ||pert||, [1] sum |pert_3|, [2..2+F) sum pert_f, [2+F..2+2F) sum pert_f^2, [2+2F] nan
   constexpr int NS = 3 + 2 * F;
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_last(Dev d) {
       load_xn<F>(d, slot, xv, xn);
       const float* zi = d.z[4] + i;
 #pragma unroll
-      for (int c = 0; c < CI; ++c) h[c] = fmaxf(fmaf(zi[(size_t)c * d.S], sc[c], sh[c]), 0.0f);
+      for (int c = 0; c < CI; ++c) h[c] = fmaxf(fmaf(zi[(size_t)c * d.S] - mu[c], sc[c], sh[c]), 0.0f);
       float am[MAXF];
       float att = d.use_att ? attention<F>(d, xn, am) : 1.0f;
       float nrm2 = 0.0f;
@@ -482,9 +483,8 @@ __global__ void k_bn_eval(Dev d) {
     int C = d.C[l + 1];
     for (int c = threadIdx.x; c < C; c += blockDim.x) {
       float invstd = 1.0f / sqrtf(d.rv[l][c] + d.eps);
-      float sc = d.g[l][c] * invstd;
-      d.bn[l][c] = sc;
-      d.bn[l][C + c] = d.be[l][c] - d.rm[l][c] * sc;
+      d.bn[l][c] = d.g[l][c] * invstd;
+      d.bn[l][C + c] = d.be[l][c];
       d.bn[l][2 * C + c] = d.rm[l][c];
       d.bn[l][3 * C + c] = invstd;
     }
@@ -528,7 +528,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_last(Dev d) {
       float xv[F], xn[F], h[CI];
       load_xn<F>(d, slot, xv, xn);
 #pragma unroll
-      for (int c = 0; c < CI; ++c) h[c] = fmaxf(fmaf(zi[(size_t)c * d.S], sc[c], sh[c]), 0.0f);
+      for (int c = 0; c < CI; ++c) h[c] = fmaxf(fmaf(zi[(size_t)c * d.S] - mean4[c], sc[c], sh[c]), 0.0f);
       float am[MAXF];
       float att = d.use_att ? attention<F>(d, xn, am) : 1.0f;
       float raw[F], pp[F], p[F], dout[F];
@@ -585,7 +585,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_last(Dev d) {
 #pragma unroll
         for (int f = 0; f < F; ++f) s = fmaf(sW[f * CI + c], du[f], s);
         float zc = zi[(size_t)c * d.S];
-        float hv = fmaxf(fmaf(zc, sc[c], sh[c]), 0.0f);
+        float hv = fmaxf(fmaf(zc - mean4[c], sc[c], sh[c]), 0.0f);
         s = hv > 0.0f ? s : 0.0f;
         d.dh[0][(size_t)c * d.S + i] = s;
         sx = s * ((zc - mean4[c]) * inv4[c]);
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_mid(Dev d, int l, int src) {
     m[2 * CO + j] = d.g[l][j] * d.bn[l][3 * CO + j];
   }
   __syncthreads();
-  const float* bo = sW + CO * CI;      // scale, shift, mean, invstd of layer l
+  const float* bo = sW + CO * CI;      // scale, beta, mean, invstd of layer l
   const float* bi = bo + 4 * CO;       // of layer l-1
   const float* m1 = bi + 4 * CI;
   const float* m2 = m1 + CO;
@@ -643,7 +643,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_mid(Dev d, int l, int src) {
 #pragma unroll
       for (int o = 0; o < CO; ++o) s = fmaf(sW[o * CI + c], dz[o], s);
       float zc = zp[(size_t)c * d.S];
-      float hv = fmaxf(fmaf(zc, bi[c], bi[CI + c]), 0.0f);
+      float hv = fmaxf(fmaf(zc - bi[2 * CI + c], bi[c], bi[CI + c]), 0.0f);
       s = (act && hv > 0.0f) ? s : 0.0f;
       if (act) d.dh[src ^ 1][(size_t)c * d.S + i] = s;
       acc.add1(c, s, s * ((zc - bi[2 * CI + c]) * bi[3 * CI + c]));
@@ -679,7 +679,7 @@ struct Job {
   int CO, CI;
   int hsrc;         // HSrc
   const float* h;   // H_BNRELU: z_{l-1} ; H_RAW: activations, both [CI][S]
-  const float* bn;  // H_BNRELU: scale/shift of layer l-1
+  const float* bn;  // H_BNRELU: scale, beta, mean of layer l-1
   int eoff;         // element offset in wpart rows
   int nelem;        // CO * (CI + 1)
 };
@@ -735,7 +735,7 @@ __global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
           float t = d.x[(size_t)slot * F + c] / d.xs[c];
           v = fminf(fmaxf(t, -10.0f), 10.0f);
         } else if (job.hsrc == H_BNRELU) {
-          v = fmaxf(fmaf(job.h[(size_t)c * d.S + n], job.bn[c], job.bn[CI + c]), 0.0f);
+          v = fmaxf(fmaf(job.h[(size_t)c * d.S + n] - job.bn[2 * CI + c], job.bn[c], job.bn[CI + c]), 0.0f);
         } else {
           v = job.h[(size_t)c * d.S + n];
         }

@@ -152,7 +152,7 @@ enum { E_FWD = 0, E_DGRAD = 1, E_PLAIN = 2 };
 struct GemmArgs {
   const float* a;       // A source rows [Nsrc, CI] (z of the previous layer, raw, or dy)
   const float* a2;      // A_BNBWD: z of the same layer [Nsrc, CI]
-  const float* abn;     // A_BNRELU: scale[CI], shift[CI];
+  const float* abn;     // A_BNRELU: scale[CI], beta[CI], mean[CI] (pre = (x - mean) * scale + beta);
                         // A_BNBWD : gi = g*invstd [CI], m1 [CI], m2 [CI], mean [CI], invstd [CI]
   const int* nbr;       // [Nout, K] neighbour map
   int K, rev;           // rev: use column K-1-k (SubM transpose)
@@ -164,7 +164,7 @@ struct GemmArgs {
   int CO_real;
   // epilogue
   const float* ez;      // E_DGRAD: z of the output layer (previous layer in forward order) [Nout, CO]
-  const float* ebn;     // E_DGRAD: scale, shift, mean, invstd of that layer [4*CO]
+  const float* ebn;     // E_DGRAD: scale, beta, mean, invstd of that layer [4*CO]
   float* part;          // [nblk][2*CO] partial column sums (may be null)
 };
 
@@ -207,7 +207,7 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
       float v = 0.0f;
       if (src >= 0) {
         float x = g.a[(long long)src * CI + c];
-        if (AT == A_BNRELU) v = fmaxf(fmaf(x, g.abn[c], g.abn[CI + c]), 0.0f);
+        if (AT == A_BNRELU) v = fmaxf(fmaf(x - g.abn[2 * CI + c], g.abn[c], g.abn[CI + c]), 0.0f);
         else if (AT == A_BNBWD) {
           float zz = g.a2[(long long)src * CI + c];
           float xh = (zz - g.abn[3 * CI + c]) * g.abn[4 * CI + c];
@@ -251,7 +251,7 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
       if (row < g.Nout && col < g.CO_real) {
         if (ET == E_DGRAD) {
           float zz = g.ez[(long long)row * CO + col];
-          float h = fmaxf(fmaf(zz, g.ebn[col], g.ebn[CO + col]), 0.0f);
+          float h = fmaxf(fmaf(zz - g.ebn[2 * CO + col], g.ebn[col], g.ebn[CO + col]), 0.0f);
           v = h > 0.0f ? v : 0.0f;
           float xh = (zz - g.ebn[2 * CO + col]) * g.ebn[3 * CO + col];
           s1[n] += v;
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
 // nbr[:, k] with the forward A transform; D = dz of the output rows (BN backward on load).
 struct WgradArgs {
   const float* a;     // forward A source [Nsrc, CI]
-  const float* abn;   // forward A transform (A_BNRELU) scale/shift
+  const float* abn;   // forward A transform (A_BNRELU) scale, beta, mean
   const int* nbr;     // [Nout, K]
   int K, Nout, rows_per;
   const float* dy;    // [Nout, CO]
@@ -331,7 +331,7 @@ __global__ __launch_bounds__(BLK) void k_wgrad(WgradArgs g) {
       float v = 0.0f;
       if (src >= 0) {
         float x = g.a[(long long)src * CI + c];
-        v = AT == A_BNRELU ? fmaxf(fmaf(x, g.abn[c], g.abn[CI + c]), 0.0f) : x;
+        v = AT == A_BNRELU ? fmaxf(fmaf(x - g.abn[2 * CI + c], g.abn[c], g.abn[CI + c]), 0.0f) : x;
       }
       sA[r * AS + c] = v;
     }
@@ -390,7 +390,7 @@ __global__ void k_wgrad_reduce(const float* __restrict__ part, int chunks, long 
 
 // ------------------------------------------------------------------ BatchNorm finalize
 // one block per column j < 2C: fixed-order tree sum of the partial rows in double.
-// mode 0 (forward): bn = scale, shift, mean, invstd ; running stats updated.
+// mode 0 (forward): bn = scale (= gamma*invstd), beta, mean, invstd ; running stats updated.
 // mode 1 (backward): bnb = gi, m1, m2, mean, invstd ; dgamma, dbeta written.
 __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int N,
                                                      int mode, const float* __restrict__ gamma,
@@ -420,16 +420,16 @@ __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ p
       double var = s2 / N - mean * mean;
       if (var < 0) var = 0;
       float invstd = 1.0f / sqrtf((float)var + eps);
-      float sc = gamma[c] * invstd;
-      bn[c] = sc;
-      bn[C + c] = beta[c] - (float)mean * sc;
+      // BN applied as (z - mean) * scale + beta: no cancellation between z*scale and a shift
+      bn[c] = gamma[c] * invstd;
+      bn[C + c] = beta[c];
       bn[2 * C + c] = (float)mean;
       bn[3 * C + c] = invstd;
       double uvar = N > 1 ? var * N / (N - 1) : var;
       rmean[c] = (1.0f - mom) * rmean[c] + mom * (float)mean;
       rvar[c] = (1.0f - mom) * rvar[c] + mom * (float)uvar;
     } else {
-      // fbn: forward scale, shift, mean, invstd of this layer
+      // fbn: forward scale, beta, mean, invstd of this layer
       bn[c] = gamma[c] * fbn[3 * C + c];
       bn[C + c] = (float)(s1 / N);
       bn[2 * C + c] = (float)(s2 / N);
@@ -451,7 +451,7 @@ __global__ __launch_bounds__(BLK) void k_to_dense(const float* __restrict__ z, c
   if (t >= (long long)N * C) return;
   int r = (int)(t / C), c = (int)(t - (long long)r * C);
   const int* co = coors + 4 * r;
-  float h = fmaxf(fmaf(z[t], bn[c], bn[C + c]), 0.0f);
+  float h = fmaxf(fmaf(z[t] - bn[2 * C + c], bn[c], bn[C + c]), 0.0f);
   long long idx = (((long long)co[0] * C + c) * s.D + co[1]) * s.H * s.W + (long long)co[2] * s.W + co[3];
   dense[idx] = h;
 }
@@ -471,7 +471,7 @@ __global__ __launch_bounds__(BLK) void k_from_dense(const float* __restrict__ gd
       const int* co = coors + 4 * r;
       long long idx = (((long long)co[0] * C + c) * s.D + co[1]) * s.H * s.W + (long long)co[2] * s.W + co[3];
       float zz = z[(long long)r * C + c];
-      float h = fmaxf(fmaf(zz, bn[c], bn[C + c]), 0.0f);
+      float h = fmaxf(fmaf(zz - bn[2 * C + c], bn[c], bn[C + c]), 0.0f);
       float v = h > 0.0f ? gd[idx] : 0.0f;
       dy[(long long)r * C + c] = v;
       s1 += v;

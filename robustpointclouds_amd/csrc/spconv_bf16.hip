@@ -47,7 +47,7 @@ struct GB {
   float* out;         // [Nout][CO_real]
   int CO_real;
   const float* ez;    // E_DGRAD: z of the layer whose grad this is [Nout][CO_real]
-  const float* ebn;   // E_DGRAD: scale, shift, mean, invstd [4*CO_real]
+  const float* ebn;   // E_DGRAD: scale, beta, mean, invstd [4*CO_real]
   float* part;        // [blocks][2*NGP] or null
 };
 
@@ -171,7 +171,7 @@ __global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
         if (EPI == E_DGRAD) {
           const int C = g.CO_real;
           float zz = g.ez[(long long)row * C + col];
-          float h = fmaxf(fmaf(zz, g.ebn[col], g.ebn[C + col]), 0.0f);
+          float h = fmaxf(fmaf(zz - g.ebn[2 * C + col], g.ebn[col], g.ebn[C + col]), 0.0f);
           v = h > 0.0f ? v : 0.0f;
           float xh = (zz - g.ebn[2 * C + col]) * g.ebn[3 * C + col];
           s1[n] += v;
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(BLK) void k_to_bf16(const float* __restrict__ z, co
   float v = 0.0f;
   if (c < C) {
     v = z[(long long)r * C + c];
-    if (bn) v = fmaf(v, bn[c], bn[C + c]);
+    if (bn) v = fmaf(v - bn[2 * C + c], bn[c], bn[C + c]);   // (z - mean) * scale + beta
     if (relu) v = fmaxf(v, 0.0f);
   }
   h[t] = to_bf16(v);

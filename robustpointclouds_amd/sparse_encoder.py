@@ -114,6 +114,7 @@ class SparseEncoder(nn.Module):
         self.output_channels = output_channels
         self._grids = {}
         self.timer = None   # optional KernelTimer (bench.py roofline), see below
+        self.debug = None   # optional list: backward appends (layer, dy) for diagnostics
         # perf mode: forward / dgrad convs on bf16 MFMA with bf16 gathered rows (fp32 accumulate,
         # fp32 BatchNorm statistics); parity mode (default) is fp32 end to end
         self.bf16 = False
@@ -219,11 +220,10 @@ class SparseEncoderFn(torch.autograd.Function):
         rb = {}
         cur_coors, cur_n = coors, feats.shape[0]
         src, src_bn = feats, None
+        # perf mode: layers >= 1 gather bf16 rows of relu(bn(z)) (O(1) values); layer 0 stays fp32 —
+        # its input is the raw VFE mean (coordinates up to 70 m, where a bf16 step is 0.5 m)
         bf16 = enc.bf16
-        if bf16:
-            hsrc = torch.empty((cur_n, _r8(feats.shape[1])), dtype=torch.bfloat16, device=dev)
-            _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(feats), None, cur_n, feats.shape[1], 0, _ffi.ptr(hsrc), st),
-                       "rpc_to_bf16_rows")
+        hsrc = None
         L = []
         for li, (sp, m) in enumerate(zip(enc.specs, mods)):
             W = params[3 * li]
@@ -264,7 +264,8 @@ class SparseEncoderFn(torch.autograd.Function):
             nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
             part = torch.zeros((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
             tm = enc.timer is not None and enc.timer.wants("fwd", sp)
-            if bf16:
+            rec["bf16"] = bf16 and li > 0
+            if rec["bf16"]:
                 bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 0), dtype=torch.bfloat16,
                                  device=dev)
                 _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), sp.K, sp.ci, sp.co, 0, _ffi.ptr(bt), st),
@@ -279,9 +280,9 @@ class SparseEncoderFn(torch.autograd.Function):
                                                   n_out, _ffi.ptr(W), sp.co, _ffi.ptr(z), _ffi.ptr(part), st),
                            "rpc_spconv_forward")
             if tm:
-                kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.ci)}, {_r16(sp.co) // 16}, 0>" if bf16 else
+                kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.ci)}, {_r16(sp.co) // 16}, 0>" if rec["bf16"] else
                       f"rpc::sp::k_gemm<{sp.ci}, {sp.co}, {1 if li else 0}, 0>")
-                enc.timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if bf16 else "fp32")
+                enc.timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
             bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
             wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(sp.co), dev)
             _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
@@ -334,6 +335,9 @@ class SparseEncoderFn(torch.autograd.Function):
             rec = L[li]
             sp = rec["spec"]
             n_out = rec["n_out"]
+            if ctx.enc.debug is not None:
+                ctx.enc.debug.append((li, rec["coors_out"].cpu().numpy(), rec["z"].detach().cpu().double(),
+                                      dy.detach().cpu().double()))
             # BatchNorm backward statistics of this layer -> bnb, dgamma, dbeta
             bnb = torch.empty(5 * sp.co, dtype=torch.float32, device=dev)
             dgamma = torch.empty_like(rec["gamma"])
@@ -368,7 +372,7 @@ class SparseEncoderFn(torch.autograd.Function):
                 nblk = max(lib.rpc_spconv_gemm_blocks(n_in), 1)
                 part = torch.zeros((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
                 td = timer is not None and timer.wants("dgrad", sp)
-                if ctx.bf16:
+                if rec["bf16"]:
                     dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
                     e0 = timer.start() if td else None
                     _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
@@ -382,12 +386,12 @@ class SparseEncoderFn(torch.autograd.Function):
                                                     _ffi.ptr(prev["z"]), _ffi.ptr(prev["bn"]), _ffi.ptr(din),
                                                     _ffi.ptr(part), st), "rpc_spconv_dgrad")
                 if td:
-                    kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.co)}, {_r16(sp.ci) // 16}, 1>" if ctx.bf16 else
+                    kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.co)}, {_r16(sp.ci) // 16}, 1>" if rec["bf16"] else
                           f"rpc::sp::k_gemm<{sp.co}, {sp.ci}, 2, 1>")
-                    timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if ctx.bf16 else "fp32")
+                    timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
                 dy = din
             elif ctx.needs_input_grad[0]:
-                if ctx.bf16:
+                if rec["bf16"]:
                     dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
                     _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),

@@ -169,7 +169,9 @@ def main():
                                f", batch {a.batch}/GPU, perturber active (_epoch=3)",
                                global_batch=world * a.batch, frames_per_gpu=a.batch,
                                dense_dtype="fp32" if a.fp32 else "bf16",
-                               kernel_dtype="fp32 (voxelize, perturber, sparse encoder)",
+                               kernel_dtype=("fp32 (voxelize, perturber, sparse encoder)" if a.fp32 else
+                                             "fp32 voxelize/perturber/sparse layer 0; bf16 MFMA (fp32 accumulate,"
+                                             " fp32 BN statistics) sparse layers 1-11"),
                                parallelism=f"dp{world}"))
         if ks:
             peak = PEAK["bf16_mfma" if ks["dtype"] == "bf16" else "fp32_mfma"]

@@ -189,6 +189,10 @@ int rpc_spconv_prep_weight_bf16(const float* W, int kvol, int ci, int co, int dg
 int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out, const void* bt,
                          int ng, float* out, const float* prev_z, const float* prev_bn, float* part, int epi,
                          void* stream);
+/* dW[k] = sum_r h[nbr[r,k]]^T dz[r] (bf16 rows, fp32 accumulate, fixed-order reduction) */
+size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co);
+int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
+                          float* dW, void* workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

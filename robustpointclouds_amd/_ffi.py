@@ -63,6 +63,8 @@ SIGNATURES = {
     "rpc_spconv_bf16_weight_elems": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_prep_weight_bf16": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
+    "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),
+    "rpc_spconv_wgrad_bf16": (i32, [vp, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
 }
 
 

@@ -251,6 +251,168 @@ __global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int 
   bt[t] = to_bf16(v);
 }
 
+// ------------------------------------------------------------------ weight gradient
+// dW[k][ci][co] = sum_r h[nbr[r,k]][ci] * dz[r][co]. Block = (chunk of output rows, group of KG
+// offsets). Rows are the K dimension of v_mfma_f32_16x16x32_bf16 (A = h^T, B = dz): per 64-row
+// sub-tile the dz rows (shared by the KG offsets) and the gathered h rows are staged ROW-MAJOR
+// in LDS (one ds_write_b128 per 16-B chunk) and read back column-wise with ds_read_b64_tr_b16.
+// Row pitch = C + 16 elements and the (group, half, q) -> row map below make the transposed
+// reads conflict-free for C = 32/64/128. The neighbour indices of 512 rows are preloaded into
+// LDS so the gathers of sub-tile s+1 are issued (register staging) before the MFMAs of sub-tile s.
+// Partial slabs [chunk][K][ci][co] are reduced in a fixed order by k_wreduce.
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ s16x4 tr_read(const u16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+template <int CI, int CO, int KG>
+__global__ __launch_bounds__(BLK) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
+                                                    int K, int N, int rows_per, const u16* __restrict__ dz, int DP,
+                                                    float* __restrict__ part) {
+  constexpr int RT = 64;                                   // rows per sub-tile (2 MFMA k-steps)
+  constexpr int SEG = 512;                                 // rows per neighbour preload
+  constexpr int CIR = (CI + 15) / 16 * 16;
+  constexpr int PA = CIR + 16, PD = CO + 16;               // LDS row pitch (elements)
+  constexpr int MT = CIR / 16, NT = CO / 16;
+  // 4 waves as WM x WN over the (ci, co) tiles: wave (wm, wn) owns m = wm + WM*a, n = wn + WN*b
+  constexpr int WM = MT < 4 ? MT : 4, WN = 4 / WM;
+  constexpr int WMT = MT / WM, WNT = (NT + WN - 1) / WN, TPW = WMT * WNT;
+  constexpr int CA = (CI + 7) / 8, CD = CO / 8;            // 16-B chunks per row
+  constexpr int NA = (RT * CA + BLK - 1) / BLK, ND = (RT * CD + BLK - 1) / BLK;
+  __shared__ __attribute__((aligned(16))) u16 sA[KG][RT * PA];
+  __shared__ __attribute__((aligned(16))) u16 sD[RT * PD];
+  __shared__ int sN[SEG * KG];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w % WM, wn = w / WM;
+  const int chunk = blockIdx.x, k0 = blockIdx.y * KG;
+  const int rb0 = chunk * rows_per, rb1 = min(N, rb0 + rows_per);
+  f32x4 acc[KG][TPW];
+#pragma unroll
+  for (int g = 0; g < KG; ++g)
+#pragma unroll
+    for (int i = 0; i < TPW; ++i) acc[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // zero the padded channels of the A tiles once (CI = 16 * MT always here, kept for safety)
+  if (CIR != CI)
+    for (int q = tid; q < KG * RT * PA; q += BLK) (&sA[0][0])[q] = 0;
+  // transposed-read lane geometry: group g4, lane i = 4q + p of the group
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int rowoff = 4 * g4 + qq;                          // + 16*half + 32*kstep
+  uint4 ra[KG][NA], rd[ND];
+  for (int seg = rb0; seg < rb1; seg += SEG) {
+    const int se = min(rb1, seg + SEG);
+    __syncthreads();
+    for (int q = tid; q < SEG * KG; q += BLK) {
+      int r = q / KG, g = q - r * KG, row = seg + r, k = k0 + g;
+      sN[q] = (row < se && k < K) ? nbr[(long long)row * K + k] : -1;
+    }
+    __syncthreads();
+    auto load = [&](int rs) {   // global -> registers for the sub-tile starting at segment row rs
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        int q = tid + j * BLK;
+        rd[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (q < RT * CD) {
+          int r = q / CD, c8 = q - r * CD, row = seg + rs + r;
+          if (row < se) rd[j] = *(const uint4*)(dz + (long long)row * DP + c8 * 8);
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < KG; ++g)
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          int q = tid + j * BLK;
+          ra[g][j] = make_uint4(0u, 0u, 0u, 0u);
+          if (q < RT * CA) {
+            int r = q / CA, c8 = q - r * CA;
+            int src = (rs + r < SEG) ? sN[(rs + r) * KG + g] : -1;
+            if (src >= 0) ra[g][j] = *(const uint4*)(h + (long long)src * HP + c8 * 8);
+          }
+        }
+    };
+    load(0);
+    for (int rs = 0; rs < se - seg; rs += RT) {
+      __syncthreads();   // previous sub-tile's MFMAs are done with the LDS tiles
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        int q = tid + j * BLK;
+        if (q < RT * CD) {
+          int r = q / CD, c8 = q - r * CD;
+          *(uint4*)&sD[r * PD + c8 * 8] = rd[j];
+        }
+      }
+#pragma unroll
+      for (int g = 0; g < KG; ++g)
+#pragma unroll
+        for (int j = 0; j < NA; ++j) {
+          int q = tid + j * BLK;
+          if (q < RT * CA) {
+            int r = q / CA, c8 = q - r * CA;
+            *(uint4*)&sA[g][r * PA + c8 * 8] = ra[g][j];
+          }
+        }
+      // which offsets have any neighbour in this sub-tile (wave-uniform, from the LDS indices)
+      bool any[KG];
+#pragma unroll
+      for (int g = 0; g < KG; ++g) any[g] = __ballot(sN[min(rs + lane, SEG - 1) * KG + g] >= 0 && rs + lane < SEG) != 0;
+      __syncthreads();
+      if (rs + RT < se - seg) load(rs + RT);               // in flight during the MFMAs below
+#pragma unroll
+      for (int ks = 0; ks < RT / 32; ++ks) {
+        const int r0 = 32 * ks + rowoff;
+        bf16x8 bv[WNT];                                    // dz fragments, shared by the KG offsets
+#pragma unroll
+        for (int b = 0; b < WNT; ++b) {
+          const int n = wn + WN * b;
+          s16x4 x[2] = {tr_read(&sD[r0 * PD + n * 16 + 4 * pp]), tr_read(&sD[(r0 + 16) * PD + n * 16 + 4 * pp])};
+          bv[b] = *(bf16x8*)x;
+        }
+#pragma unroll
+        for (int g = 0; g < KG; ++g) {
+          if (!any[g]) continue;
+#pragma unroll
+          for (int a = 0; a < WMT; ++a) {
+            const int m = wm + WM * a;
+            s16x4 x[2] = {tr_read(&sA[g][r0 * PA + m * 16 + 4 * pp]),
+                          tr_read(&sA[g][(r0 + 16) * PA + m * 16 + 4 * pp])};
+            bf16x8 av = *(bf16x8*)x;
+#pragma unroll
+            for (int b = 0; b < WNT; ++b)
+              acc[g][a * WNT + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[b], acc[g][a * WNT + b], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < KG; ++g) {
+    int k = k0 + g;
+    if (k >= K) break;
+    float* out = part + ((long long)chunk * K + k) * CI * CO;
+#pragma unroll
+    for (int a = 0; a < WMT; ++a)
+#pragma unroll
+      for (int b = 0; b < WNT; ++b) {
+        const int m = wm + WM * a, n = wn + WN * b;
+        if (n >= NT) continue;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          int ci = m * 16 + (lane >> 4) * 4 + j, co = n * 16 + (lane & 15);
+          if (ci < CI) out[ci * CO + co] = acc[g][a * WNT + b][j];
+        }
+      }
+  }
+}
+
+__global__ void k_wreduce(const float* __restrict__ part, int chunks, long long total, float* __restrict__ dW) {
+  long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e >= total) return;
+  double s = 0.0;
+  for (int c = 0; c < chunks; ++c) s += part[(long long)c * total + e];
+  dW[e] = (float)s;
+}
+
 template <int KGP, int NT>
 static void launch_t(int epi, const GB& a, int nblk, hipStream_t st) {
   if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(BLK), 0, st, a);
@@ -336,6 +498,49 @@ extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int k
   g.part = part;
   int rc = launch(r32(kg), r16(ng) / 16, epi, g, cdiv(n_out, BM), (hipStream_t)stream);
   if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+static int wgrad_chunks(int n) {
+  int c = (n + 511) / 512;
+  return c < 1 ? 1 : (c > 512 ? 512 : c);
+}
+
+extern "C" size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co) {
+  return (size_t)wgrad_chunks(n_out) * kvol * ci * co * sizeof(float);
+}
+
+// dW[k] = sum_r h[nbr[r,k]]^T dz[r] with bf16 rows h [.][round8(ci)] and dz [n_out][round8(co)]
+extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz,
+                                     int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
+  if (n_out < 0 || kvol < 1 || kvol > MAXK) return RPC_ERR_ARG;
+  bool ok = (ci == 16 && (co == 16 || co == 32)) || (ci == 32 && (co == 32 || co == 64)) ||
+            (ci == 64 && (co == 64 || co == 128));
+  if (!ok) return RPC_ERR_UNSUPPORTED;
+  hipStream_t st = (hipStream_t)stream;
+  if (n_out == 0) {
+    RPC_CHECK(hipMemsetAsync(dW, 0, sizeof(float) * (size_t)kvol * ci * co, st));
+    return RPC_OK;
+  }
+  int chunks = wgrad_chunks(n_out);
+  if (ws_bytes < (size_t)chunks * kvol * ci * co * sizeof(float)) return RPC_ERR_WORKSPACE;
+  int rows_per = ((n_out + chunks - 1) / chunks + 31) / 32 * 32;
+  dim3 grid(chunks, (kvol + 2) / 3);
+  float* part = (float*)ws;
+  const u16* hp = (const u16*)h;
+  const u16* dp = (const u16*)dz;
+  int HP = r8(ci), DP = r8(co);
+#define W2(a, b)                                                                                       \
+  if (ci == a && co == b) {                                                                           \
+    hipLaunchKernelGGL((k_wgrad_bf16<a, b, 3>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp, \
+                       DP, part);                                                                     \
+  } else
+  W2(16, 16) W2(16, 32) W2(32, 32) W2(32, 64) W2(64, 64) W2(64, 128) { return RPC_ERR_UNSUPPORTED; }
+#undef W2
+  RPC_LAUNCH_CHECK();
+  long long total = (long long)kvol * ci * co;
+  hipLaunchKernelGGL(k_wreduce, dim3(cdiv(total, BLK)), dim3(BLK), 0, st, (const float*)part, chunks, total, dW);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -265,6 +265,7 @@ class SparseEncoderFn(torch.autograd.Function):
             part = torch.zeros((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
             tm = enc.timer is not None and enc.timer.wants("fwd", sp)
             rec["bf16"] = bf16 and li > 0
+            rec["h_in"] = hsrc if rec["bf16"] else None
             if rec["bf16"]:
                 bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 0), dtype=torch.bfloat16,
                                  device=dev)
@@ -349,16 +350,29 @@ class SparseEncoderFn(torch.autograd.Function):
                        "rpc_bn_finalize(bwd)")
             # weight gradient
             dW = torch.empty_like(rec["W"])
-            wsz = lib.rpc_spconv_wgrad_workspace_size(n_out, sp.K, sp.ci, sp.co)
-            ws = _ffi.workspace(wsz, dev)
             timer = ctx.enc.timer
             tw = timer is not None and timer.wants("wgrad", sp)
-            e0 = timer.start() if tw else None
-            _ffi.check(lib.rpc_spconv_wgrad(_ffi.ptr(rec["src"]), _ffi.ptr(rec["src_bn"]), sp.ci, _ffi.ptr(rec["nbr"]),
-                                            sp.K, n_out, _ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
-                                            _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_spconv_wgrad")
+            dzb = btd = None
+            if rec["bf16"]:
+                dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
+                wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, sp.K, sp.ci, sp.co)
+                ws = _ffi.workspace(wsz, dev)
+                e0 = timer.start() if tw else None
+                _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(rec["h_in"]), sp.ci, _ffi.ptr(rec["nbr"]), sp.K, n_out,
+                                                     _ffi.ptr(dzb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st),
+                           "rpc_spconv_wgrad_bf16")
+                kn = f"rpc::spb::k_wgrad_bf16<{sp.ci}, {sp.co}, 3>"
+            else:
+                wsz = lib.rpc_spconv_wgrad_workspace_size(n_out, sp.K, sp.ci, sp.co)
+                ws = _ffi.workspace(wsz, dev)
+                e0 = timer.start() if tw else None
+                _ffi.check(lib.rpc_spconv_wgrad(_ffi.ptr(rec["src"]), _ffi.ptr(rec["src_bn"]), sp.ci,
+                                                _ffi.ptr(rec["nbr"]), sp.K, n_out, _ffi.ptr(dy), _ffi.ptr(rec["z"]),
+                                                _ffi.ptr(bnb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st),
+                           "rpc_spconv_wgrad")
+                kn = f"rpc::sp::k_wgrad<{sp.ci}, {sp.co}, {1 if li else 0}>"
             if tw:
-                timer.stop(e0, rec["nbr"], sp.ci, sp.co, f"rpc::sp::k_wgrad<{sp.ci}, {sp.co}, {1 if li else 0}>", "fp32")
+                timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
             grads[3 * li: 3 * li + 3] = [dW, dgamma, dbeta]
             # data gradient into the previous layer (ReLU mask + its BN-backward partial sums)
             n_in = rec["n_in"]
@@ -373,7 +387,6 @@ class SparseEncoderFn(torch.autograd.Function):
                 part = torch.zeros((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
                 td = timer is not None and timer.wants("dgrad", sp)
                 if rec["bf16"]:
-                    dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
                     e0 = timer.start() if td else None
                     _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), _ffi.ptr(prev["z"]),
@@ -392,7 +405,6 @@ class SparseEncoderFn(torch.autograd.Function):
                 dy = din
             elif ctx.needs_input_grad[0]:
                 if rec["bf16"]:
-                    dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
                     _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
                                "rpc_spconv_gemm_bf16(dgrad)")

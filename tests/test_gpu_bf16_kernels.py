@@ -1,0 +1,84 @@
+"""bf16 sparse-conv kernels in isolation: with bf16 operands fixed, the MFMA kernels must match
+a float64 matmul of the same (exactly representable) bf16 values to fp32-accumulation accuracy.
+Covers every (C_in, C_out) pair SECOND's SparseEncoder uses, ragged row counts (not multiples of
+the 32/64-row tiles), empty offsets and rows with no neighbour at all."""
+import numpy as np
+import pytest
+import torch
+
+from robustpointclouds_amd import _ffi
+
+pytestmark = pytest.mark.gpu
+
+PAIRS = [(16, 16), (16, 32), (32, 32), (32, 64), (64, 64), (64, 128)]
+
+
+def _r8(c):
+    return (c + 7) // 8 * 8
+
+
+def _case(n_out, n_in, K, ci, co, density, seed):
+    g = torch.Generator().manual_seed(seed)
+    nbr = torch.randint(0, n_in, (n_out, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n_out, K), generator=g) > density] = -1
+    if K > 2:
+        nbr[:, 1] = -1          # an offset nobody uses
+    h = torch.zeros((n_in, _r8(ci)), dtype=torch.bfloat16)
+    h[:, :ci] = torch.randn((n_in, ci), generator=g).to(torch.bfloat16)
+    dz = torch.zeros((n_out, _r8(co)), dtype=torch.bfloat16)
+    dz[:, :co] = torch.randn((n_out, co), generator=g).to(torch.bfloat16)
+    return nbr, h, dz
+
+
+def _wgrad_ref(nbr, h, dz, K, ci, co):
+    dW = torch.zeros((K, ci, co), dtype=torch.float64)
+    hd, dd = h[:, :ci].double(), dz[:, :co].double()
+    for k in range(K):
+        ok = nbr[:, k] >= 0
+        if ok.any():
+            dW[k] = hd[nbr[ok, k].long()].T @ dd[ok]
+    return dW
+
+
+@pytest.mark.parametrize("ci,co", PAIRS)
+@pytest.mark.parametrize("n_out,K", [(5000, 27), (1, 27), (3001, 3)])
+def test_wgrad_bf16_matches_fp64(ci, co, n_out, K):
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    nbr, h, dz = _case(n_out, 4000, K, ci, co, 0.3, seed=ci * 1000 + co + n_out)
+    ref = _wgrad_ref(nbr, h, dz, K, ci, co)
+    dW = torch.full((K, ci, co), float("nan"), device=dev)
+    wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, K, ci, co)
+    ws = _ffi.workspace(wsz, dev)
+    hd, nd, dd = h.to(dev), nbr.to(dev), dz.to(dev)
+    _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hd), ci, _ffi.ptr(nd), K, n_out, _ffi.ptr(dd), co, _ffi.ptr(dW),
+                                         _ffi.ptr(ws), wsz, _ffi.stream_of(dW)), "wgrad_bf16")
+    got = dW.cpu().double()
+    assert torch.isfinite(got).all()
+    # fp32 accumulation of exact bf16 products: relative error ~1e-6 of the row-sum magnitude
+    tol = 1e-5 * max(ref.abs().max().item(), 1.0) + 1e-6 * (n_out ** 0.5)
+    assert (got - ref).abs().max().item() <= tol
+    assert got[1].abs().max().item() == 0.0 if K > 2 else True
+    # fixed-order reduction: bitwise deterministic
+    dW2 = torch.empty_like(dW)
+    _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hd), ci, _ffi.ptr(nd), K, n_out, _ffi.ptr(dd), co, _ffi.ptr(dW2),
+                                         _ffi.ptr(ws), wsz, _ffi.stream_of(dW)), "wgrad_bf16")
+    assert torch.equal(dW, dW2)
+
+
+def test_wgrad_bf16_rejects_short_workspace_and_empty():
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    nbr, h, dz = _case(100, 50, 27, 16, 16, 0.5, 0)
+    dW = torch.full((27, 16, 16), 1.0, device=dev)
+    wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(100, 27, 16, 16)
+    ws = _ffi.workspace(wsz, dev)
+    hd, nd, dd = h.to(dev), nbr.to(dev), dz.to(dev)
+    st = _ffi.stream_of(dW)
+    assert lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hd), 16, _ffi.ptr(nd), 27, 100, _ffi.ptr(dd), 16, _ffi.ptr(dW),
+                                     _ffi.ptr(ws), wsz - 4, st) == 2   # RPC_ERR_WORKSPACE
+    assert lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hd), 16, _ffi.ptr(nd), 27, 100, _ffi.ptr(dd), 24, _ffi.ptr(dW),
+                                     _ffi.ptr(ws), wsz, st) == 3       # RPC_ERR_UNSUPPORTED
+    _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hd), 16, _ffi.ptr(nd), 27, 0, _ffi.ptr(dd), 16, _ffi.ptr(dW),
+                                         _ffi.ptr(ws), wsz, st), "wgrad_bf16(empty)")
+    assert dW.abs().max().item() == 0.0

@@ -109,6 +109,13 @@ class Trainer:
         m.train()
         batch = m.data_preprocessor(dict(inputs=dict(points=points)), training=True)["inputs"]
         batch["batch_size"] = len(points)
+        return self.step_batch(batch, gt)
+
+    def step_batch(self, batch, gt):
+        """The step after voxelisation: loss -> parse_losses -> backward (DDP all-reduce) -> clip
+        -> AdamW -> hooks. batch: dict(voxels=dict(voxels, num_points, coors), batch_size)."""
+        m = self.module
+        m.train()
         self.sched.set(self.iter)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.bf16):
             if isinstance(self.model, torch.nn.parallel.DistributedDataParallel):

@@ -169,12 +169,16 @@ int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const f
                     const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                     const float* fwd_bn, float* bn_out, float* dgamma, float* dbeta, void* workspace,
                     void* stream);
-/* SparseConvTensor.dense() of relu(bn(z)): dense[b, c, z, y, x]; backward gathers, applies the
- * ReLU mask and writes the BatchNorm-backward partial sums. */
+/* SparseConvTensor.dense() of relu(bn(z)) viewed as [B, C*D, H, W] (channel c*D + z); backward
+ * gathers, applies the ReLU mask and writes the BatchNorm-backward partial sums.
+ * flags: RPC_DENSE_NHWC = channels_last image [B][H][W][C*D]; RPC_DENSE_BF16 = bf16 elements
+ * (the caller zero-fills the dense buffer; only occupied cells are written). */
+#define RPC_DENSE_NHWC 1
+#define RPC_DENSE_BF16 2
 int rpc_sparse_to_dense(const float* z, const float* bn, const int* coors, int n, int c,
-                        const int* shape /* B,D,H,W */, float* dense, void* stream);
-int rpc_dense_to_sparse_grad(const float* grad_dense, const float* z, const float* bn, const int* coors,
-                             int n, int c, const int* shape, float* dy, float* part, void* stream);
+                        const int* shape /* B,D,H,W */, int flags, void* dense, void* stream);
+int rpc_dense_to_sparse_grad(const void* grad_dense, const float* z, const float* bn, const int* coors,
+                             int n, int c, const int* shape, int flags, float* dy, float* part, void* stream);
 
 /* ---- a6 perf mode (bf16 MFMA, fp32 accumulate and BatchNorm statistics) */
 /* h[r, c] = bf16(relu?(z*scale+shift)) (bn NULL: identity), rows padded to round8(c) */

@@ -56,8 +56,8 @@ SIGNATURES = {
     "rpc_bn_finalize_workspace_size": (sz, [i32]),
     "rpc_bn_finalize": (i32, [vp, i32, i32, i32, i32, vp, vp, C.c_float, C.c_float, vp, vp, vp, vp, vp, vp,
                               vp, vp]),
-    "rpc_sparse_to_dense": (i32, [vp, vp, vp, i32, i32, ip, vp, vp]),
-    "rpc_dense_to_sparse_grad": (i32, [vp, vp, vp, vp, i32, i32, ip, vp, vp, vp]),
+    "rpc_sparse_to_dense": (i32, [vp, vp, vp, i32, i32, ip, i32, vp, vp]),
+    "rpc_dense_to_sparse_grad": (i32, [vp, vp, vp, vp, i32, i32, ip, i32, vp, vp, vp]),
     "rpc_to_bf16_rows": (i32, [vp, vp, i32, i32, i32, vp, vp]),
     "rpc_bnbwd_to_bf16_rows": (i32, [vp, vp, vp, i32, i32, vp, vp]),
     "rpc_spconv_bf16_weight_elems": (sz, [i32, i32, i32, i32]),

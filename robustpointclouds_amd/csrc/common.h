@@ -54,6 +54,38 @@ __device__ __forceinline__ bool last_block_arrive(unsigned* ticket, int* lds_fla
   return *lds_flag != 0;
 }
 
+// Fixed-order reduction of split-K slabs: dW[e] = sum_c part[c * total + e] (c ascending within
+// each of 4 interleaved lanes, lanes combined 0..3), in double. Block = 64 outputs x 4 lanes,
+// each lane with 4 loads in flight -> deterministic and latency-tolerant.
+template <int DUMMY = 0>
+__global__ __launch_bounds__(256) void k_slab_reduce(const float* __restrict__ part, int chunks, long long total,
+                                                     float* __restrict__ out) {
+  __shared__ double sh[4][64];
+  const int o = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + o;
+  double s = 0.0;
+  if (e < total) {
+    int c = q;
+    for (; c + 12 < chunks; c += 16) {
+      float a0 = part[(long long)c * total + e], a1 = part[(long long)(c + 4) * total + e];
+      float a2 = part[(long long)(c + 8) * total + e], a3 = part[(long long)(c + 12) * total + e];
+      s += (double)a0;
+      s += (double)a1;
+      s += (double)a2;
+      s += (double)a3;
+    }
+    for (; c < chunks; c += 4) s += (double)part[(long long)c * total + e];
+  }
+  sh[q][o] = s;
+  __syncthreads();
+  if (q == 0 && e < total) out[e] = (float)(((sh[0][o] + sh[1][o]) + sh[2][o]) + sh[3][o]);
+}
+
+inline void slab_reduce(const float* part, int chunks, long long total, float* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_slab_reduce<0>, dim3((unsigned)((total + 63) / 64)), dim3(256), 0, st, part, chunks, total,
+                     out);
+}
+
 inline int grid_for(long long n, int block, int cap) {
   long long g = (n + block - 1) / block;
   if (g < 1) g = 1;

@@ -26,6 +26,8 @@
 #include <hipcub/hipcub.hpp>
 #include <string.h>
 
+#include <hip/hip_bf16.h>
+
 #include "common.h"
 
 namespace rpc {
@@ -379,14 +381,6 @@ __global__ __launch_bounds__(BLK) void k_wgrad(WgradArgs g) {
   }
 }
 
-__global__ void k_wgrad_reduce(const float* __restrict__ part, int chunks, long long total,
-                               float* __restrict__ dW) {
-  long long e = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (e >= total) return;
-  double s = 0.0;
-  for (int c = 0; c < chunks; ++c) s += part[(long long)c * total + e];
-  dW[e] = (float)s;
-}
 
 // ------------------------------------------------------------------ BatchNorm finalize
 // one block per column j < 2C: fixed-order tree sum of the partial rows in double.
@@ -444,35 +438,43 @@ __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ p
 // ------------------------------------------------------------------ dense BEV
 // forward: dense[b, c*D + z, y, x] = relu(bn(z_rows[r, c])) ; backward: gather + ReLU mask +
 // BatchNorm-backward partial sums (one 64-row tile per block, like the GEMM epilogue)
+// dense index of (row coords, channel c): NCHW [B][C*D][H][W] (channel c*D + z) or NHWC
+// [B][H][W][C*D] (the channels_last image the MIOpen NHWC convolutions consume directly)
+template <bool NHWC>
+__device__ __forceinline__ long long dense_index(const int* co, int c, int C, const Shape& s) {
+  if (NHWC) return (((long long)co[0] * s.H + co[2]) * s.W + co[3]) * ((long long)C * s.D) + (long long)c * s.D + co[1];
+  return (((long long)co[0] * C + c) * s.D + co[1]) * s.H * s.W + (long long)co[2] * s.W + co[3];
+}
+
+__device__ __forceinline__ void store_val(float* p, float v) { *p = v; }
+__device__ __forceinline__ void store_val(__hip_bfloat16* p, float v) { *p = __float2bfloat16(v); }
+__device__ __forceinline__ float load_val(const float* p) { return *p; }
+__device__ __forceinline__ float load_val(const __hip_bfloat16* p) { return __bfloat162float(*p); }
+
+template <typename T, bool NHWC>
 __global__ __launch_bounds__(BLK) void k_to_dense(const float* __restrict__ z, const float* __restrict__ bn,
                                                   const int* __restrict__ coors, int N, int C, Shape s,
-                                                  float* __restrict__ dense) {
+                                                  T* __restrict__ dense) {
   long long t = (long long)blockIdx.x * BLK + threadIdx.x;
   if (t >= (long long)N * C) return;
   int r = (int)(t / C), c = (int)(t - (long long)r * C);
-  const int* co = coors + 4 * r;
   float h = fmaxf(fmaf(z[t] - bn[2 * C + c], bn[c], bn[C + c]), 0.0f);
-  long long idx = (((long long)co[0] * C + c) * s.D + co[1]) * s.H * s.W + (long long)co[2] * s.W + co[3];
-  dense[idx] = h;
+  store_val(dense + dense_index<NHWC>(coors + 4 * r, c, C, s), h);
 }
 
-__global__ __launch_bounds__(BLK) void k_from_dense(const float* __restrict__ gd, const float* __restrict__ z,
+template <typename T, bool NHWC>
+__global__ __launch_bounds__(BLK) void k_from_dense(const T* __restrict__ gd, const float* __restrict__ z,
                                                     const float* __restrict__ bn, const int* __restrict__ coors,
                                                     int N, int C, Shape s, float* __restrict__ dy,
                                                     float* __restrict__ part) {
-  // block: 64 rows x C channels (C <= 256), thread handles channels c = tid % C ...
-  __shared__ float sp[2 * 256];
+  // block: BM rows; thread handles channels c = tid, tid + BLK, ... (C <= 256)
   const int r0 = blockIdx.x * BM;
-  for (int j = threadIdx.x; j < 2 * C; j += BLK) sp[j] = 0.0f;
-  __syncthreads();
   for (int c = threadIdx.x; c < C; c += BLK) {
     float s1 = 0.0f, s2 = 0.0f;
     for (int r = r0; r < min(N, r0 + BM); ++r) {
-      const int* co = coors + 4 * r;
-      long long idx = (((long long)co[0] * C + c) * s.D + co[1]) * s.H * s.W + (long long)co[2] * s.W + co[3];
       float zz = z[(long long)r * C + c];
       float h = fmaxf(fmaf(zz - bn[2 * C + c], bn[c], bn[C + c]), 0.0f);
-      float v = h > 0.0f ? gd[idx] : 0.0f;
+      float v = h > 0.0f ? load_val(gd + dense_index<NHWC>(coors + 4 * r, c, C, s)) : 0.0f;
       dy[(long long)r * C + c] = v;
       s1 += v;
       s2 += v * ((zz - bn[2 * C + c]) * bn[3 * C + c]);
@@ -696,8 +698,7 @@ extern "C" int rpc_spconv_wgrad(const float* in, const float* in_bn, int CI, con
   int rc = launch_wgrad(CI, CO, in_bn ? A_BNRELU : A_RAW, a, dim3(chunks, K), st);
   if (rc) return rc;
   long long total = (long long)K * CI * CO;
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(cdiv(total, BLK)), dim3(BLK), 0, st, (const float*)ws, chunks, total,
-                     dW);
+  slab_reduce((const float*)ws, chunks, total, dW, st);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
@@ -720,23 +721,42 @@ extern "C" int rpc_bn_finalize(const float* part, int nblk, int C, int N, int mo
 }
 
 extern "C" int rpc_sparse_to_dense(const float* z, const float* bn, const int* coors, int N, int C,
-                                   const int* shape /* B,D,H,W */, float* dense, void* stream) {
-  if (N < 0 || C < 1 || !shape) return RPC_ERR_ARG;
+                                   const int* shape /* B,D,H,W */, int flags, void* dense, void* stream) {
+  if (N < 0 || C < 1 || !shape || (flags & ~3)) return RPC_ERR_ARG;
   if (N == 0) return RPC_OK;
   Shape s{shape[0], shape[1], shape[2], shape[3]};
-  hipLaunchKernelGGL(k_to_dense, dim3(cdiv((long long)N * C, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn,
-                     coors, N, C, s, dense);
+  dim3 g(cdiv((long long)N * C, BLK));
+  hipStream_t st = (hipStream_t)stream;
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_to_dense<float, false>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s, (float*)dense); break;
+    case 1: hipLaunchKernelGGL((k_to_dense<float, true>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s, (float*)dense); break;
+    case 2: hipLaunchKernelGGL((k_to_dense<__hip_bfloat16, false>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s,
+                               (__hip_bfloat16*)dense); break;
+    default: hipLaunchKernelGGL((k_to_dense<__hip_bfloat16, true>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s,
+                                (__hip_bfloat16*)dense);
+  }
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
 
-extern "C" int rpc_dense_to_sparse_grad(const float* grad_dense, const float* z, const float* bn, const int* coors,
-                                        int N, int C, const int* shape, float* dy, float* part, void* stream) {
-  if (N < 0 || C < 1 || C > 256 || !shape) return RPC_ERR_ARG;
+extern "C" int rpc_dense_to_sparse_grad(const void* grad_dense, const float* z, const float* bn, const int* coors,
+                                        int N, int C, const int* shape, int flags, float* dy, float* part,
+                                        void* stream) {
+  if (N < 0 || C < 1 || C > 256 || !shape || (flags & ~3)) return RPC_ERR_ARG;
   if (N == 0) return RPC_OK;
   Shape s{shape[0], shape[1], shape[2], shape[3]};
-  hipLaunchKernelGGL(k_from_dense, dim3(cdiv(N, BM)), dim3(BLK), 0, (hipStream_t)stream, grad_dense, z, bn, coors,
-                     N, C, s, dy, part);
+  dim3 g(cdiv(N, BM));
+  hipStream_t st = (hipStream_t)stream;
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_from_dense<float, false>), g, dim3(BLK), 0, st, (const float*)grad_dense, z, bn,
+                               coors, N, C, s, dy, part); break;
+    case 1: hipLaunchKernelGGL((k_from_dense<float, true>), g, dim3(BLK), 0, st, (const float*)grad_dense, z, bn,
+                               coors, N, C, s, dy, part); break;
+    case 2: hipLaunchKernelGGL((k_from_dense<__hip_bfloat16, false>), g, dim3(BLK), 0, st,
+                               (const __hip_bfloat16*)grad_dense, z, bn, coors, N, C, s, dy, part); break;
+    default: hipLaunchKernelGGL((k_from_dense<__hip_bfloat16, true>), g, dim3(BLK), 0, st,
+                                (const __hip_bfloat16*)grad_dense, z, bn, coors, N, C, s, dy, part);
+  }
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -259,7 +259,7 @@ __global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int 
 // Row pitch = C + 16 elements and the (group, half, q) -> row map below make the transposed
 // reads conflict-free for C = 32/64/128. The neighbour indices of 512 rows are preloaded into
 // LDS so the gathers of sub-tile s+1 are issued (register staging) before the MFMAs of sub-tile s.
-// Partial slabs [chunk][K][ci][co] are reduced in a fixed order by k_wreduce.
+// Partial slabs [chunk][K][ci][co] are reduced in a fixed order by k_slab_reduce (common.h).
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
@@ -405,14 +405,6 @@ __global__ __launch_bounds__(BLK) void k_wgrad_bf16(const u16* __restrict__ h, i
   }
 }
 
-__global__ void k_wreduce(const float* __restrict__ part, int chunks, long long total, float* __restrict__ dW) {
-  long long e = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (e >= total) return;
-  double s = 0.0;
-  for (int c = 0; c < chunks; ++c) s += part[(long long)c * total + e];
-  dW[e] = (float)s;
-}
-
 template <int KGP, int NT>
 static void launch_t(int epi, const GB& a, int nblk, hipStream_t st) {
   if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(BLK), 0, st, a);
@@ -540,7 +532,7 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
 #undef W2
   RPC_LAUNCH_CHECK();
   long long total = (long long)kvol * ci * co;
-  hipLaunchKernelGGL(k_wreduce, dim3(cdiv(total, BLK)), dim3(BLK), 0, st, (const float*)part, chunks, total, dW);
+  slab_reduce(part, chunks, total, dW, st);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -118,6 +118,10 @@ class SparseEncoder(nn.Module):
         # perf mode: forward / dgrad convs on bf16 MFMA with bf16 gathered rows (fp32 accumulate,
         # fp32 BatchNorm statistics); parity mode (default) is fp32 end to end
         self.bf16 = False
+        # dense BEV image: NCHW fp32 (default, = spconv .dense()) or the channels_last / bf16 image
+        # the perf mode's NHWC MIOpen convolutions consume without a transpose or a cast
+        self.dense_nhwc = False
+        self.dense_bf16 = False
 
     def layers(self):
         mods = [self.conv_input]
@@ -302,17 +306,23 @@ class SparseEncoderFn(torch.autograd.Function):
         last = L[-1]
         D, H, Wd = enc.shapes[-1]
         C = last["spec"].co
-        dense = torch.zeros((B, C, D, H, Wd), dtype=torch.float32, device=dev)
+        flags = (1 if enc.dense_nhwc else 0) | (2 if enc.dense_bf16 else 0)
+        dt = torch.bfloat16 if enc.dense_bf16 else torch.float32
+        if enc.dense_nhwc:   # channels_last image, logically [B, C*D, H, W]
+            dense = torch.zeros((B, H, Wd, C * D), dtype=dt, device=dev).permute(0, 3, 1, 2)
+        else:
+            dense = torch.zeros((B, C * D, H, Wd), dtype=dt, device=dev)
         shp = _ffi.int_arr((B, D, H, Wd))
         _ffi.check(lib.rpc_sparse_to_dense(_ffi.ptr(last["z"]), _ffi.ptr(last["bn"]), _ffi.ptr(last["coors_out"]),
-                                           last["n_out"], C, shp, _ffi.ptr(dense), st), "rpc_sparse_to_dense")
+                                           last["n_out"], C, shp, flags, _ffi.ptr(dense), st), "rpc_sparse_to_dense")
+        ctx.dense_flags = flags
         ctx.L = L
         ctx.enc = enc
         ctx.bf16 = bf16
         ctx.B = B
         ctx.shape = (B, C, D, H, Wd)
         ctx.n_feat = feats.shape
-        return dense.view(B, C * D, H, Wd)
+        return dense
 
     @staticmethod
     def backward(ctx, gdense):
@@ -321,7 +331,12 @@ class SparseEncoderFn(torch.autograd.Function):
         dev = gdense.device
         st = _ffi.stream_of(gdense)
         B, C, D, H, Wd = ctx.shape
-        gd = gdense.contiguous().view(B, C, D, H, Wd)
+        flags = ctx.dense_flags
+        dt = torch.bfloat16 if flags & 2 else torch.float32
+        if flags & 1:
+            gd = gdense.to(dt).contiguous(memory_format=torch.channels_last)
+        else:
+            gd = gdense.to(dt).contiguous()
         grads = [None] * (3 * len(L))
         last = L[-1]
         n = last["n_out"]
@@ -330,7 +345,7 @@ class SparseEncoderFn(torch.autograd.Function):
         part = torch.zeros((nblk, 2 * C), dtype=torch.float32, device=dev)
         _ffi.check(lib.rpc_dense_to_sparse_grad(_ffi.ptr(gd), _ffi.ptr(last["z"]), _ffi.ptr(last["bn"]),
                                                 _ffi.ptr(last["coors_out"]), n, C, _ffi.int_arr((B, D, H, Wd)),
-                                                _ffi.ptr(dy), _ffi.ptr(part), st), "rpc_dense_to_sparse_grad")
+                                                flags, _ffi.ptr(dy), _ffi.ptr(part), st), "rpc_dense_to_sparse_grad")
         dfeat = None
         for li in range(len(L) - 1, -1, -1):
             rec = L[li]

@@ -69,7 +69,14 @@ class Trainer:
         self.module = model.to(self.device)
         self.model = model
         if bf16 and hasattr(model, "middle_encoder") and hasattr(model.middle_encoder, "bf16"):
-            model.middle_encoder.bf16 = True   # sparse convs on bf16 MFMA in the bf16 perf mode
+            # perf mode: sparse convs on bf16 MFMA; dense BEV handed over as a bf16 channels_last
+            # image and the dense part kept channels_last (NHWC MIOpen kernels, no transposes)
+            model.middle_encoder.bf16 = True
+            model.middle_encoder.dense_nhwc = True
+            model.middle_encoder.dense_bf16 = True
+            for name in ("backbone", "neck", "bbox_head"):
+                if getattr(model, name, None) is not None:
+                    getattr(model, name).to(memory_format=torch.channels_last)
         if ddp and dist.is_initialized() and dist.get_world_size() > 1:
             self.model = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[self.device.index] if self.device.type == "cuda" else None,

@@ -103,3 +103,30 @@ def test_bf16_perf_mode_close_to_oracle():
     for i, (m, p) in enumerate(zip(enc.layers(), orc.params)):
         c = cos(m[0].weight.grad.cpu().double(), p["W"].grad)
         assert c > 0.95, (i, c)
+
+
+@pytest.mark.parametrize("nhwc,bf16", [(True, False), (False, True), (True, True)])
+def test_dense_image_layouts(nhwc, bf16):
+    """channels_last / bf16 dense hand-over == the NCHW fp32 image (bf16: rounded), and the
+    gradient path reads the same image layout back."""
+    feats, coors = _inputs(2, 4)
+    dev = torch.device("cuda")
+    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    f = torch.from_numpy(feats).to(dev)
+    c = torch.from_numpy(coors).to(dev)
+    f0 = f.clone().requires_grad_(True)
+    ref = enc(f0, c, 2)
+    enc.dense_nhwc, enc.dense_bf16 = nhwc, bf16
+    f1 = f.clone().requires_grad_(True)
+    out = enc(f1, c, 2)
+    assert out.shape == ref.shape and out.dtype == (torch.bfloat16 if bf16 else torch.float32)
+    assert out.is_contiguous(memory_format=torch.channels_last) == nhwc
+    want = ref.detach().to(out.dtype).float()
+    assert torch.equal(out.detach().float(), want)
+    G = torch.randn(ref.shape, generator=torch.Generator().manual_seed(3)).to(dev)
+    if bf16:
+        G = G.to(torch.bfloat16).float()   # exactly representable either way
+    (ref * G).sum().backward()
+    (out.float() * G).sum().backward()
+    rel = ((f1.grad - f0.grad).norm() / f0.grad.norm()).item()
+    assert rel < (1e-5 if not bf16 else 3e-2), rel

@@ -198,6 +198,44 @@ size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co)
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
                           float* dW, void* workspace, size_t workspace_bytes, void* stream);
 
+
+/* ---- a7 perf mode: dense BEV backbone / neck (SECOND + SECONDFPN) on bf16 MFMA, NHWC images.
+ * Replaces the Conv2d/ConvTranspose2d + BatchNorm2d + ReLU stacks of upstream mmdet3d
+ * backbones/second.py and necks/second_fpn.py (called at models/detectors/adversarial_voxelnet.py:142-145,
+ * configured at configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-car.py / -3class.py:25-36).
+ * Images are given as {B, H, W}; rows are pixels ((b*H + y)*W + x), pitch in elements. */
+#define RPC_DMAP_S1 0 /* 3x3 stride 1 pad 1 (and its data gradient with flipped taps) */
+#define RPC_DMAP_S2 1 /* 3x3 stride 2 pad 1 */
+#define RPC_DMAP_D2 2 /* data gradient of S2 */
+#define RPC_DMAP_P1 3 /* 1x1 (ConvTranspose2d k1 s1) */
+#define RPC_DMAP_U2 4 /* ConvTranspose2d k2 s2 (4 parities) */
+#define RPC_DMAP_G2 5 /* data gradient of U2 */
+/* out[orow][ooff + n] (+)= sum_{t,k} src[src_row(row,t)][k] * wt[t][n][k]; cin % 64 == 0, cout % 128 == 0;
+ * part (optional): [rpc_dense_conv_blocks][2*cout] BatchNorm partial sums of the stored bf16 values */
+int rpc_dense_conv(int map, const void* src, int src_pitch, int cin, const void* wt, int cout, void* out,
+                   int out_pitch, int out_offset, int accumulate, float* part, const int* row_img,
+                   const int* src_img, const int* out_img, void* stream);
+int rpc_dense_conv_blocks(int map, const int* row_img);
+/* dW (torch layout; kind 0 = Conv2d [co][ci][kh][kw], 1 = ConvTranspose2d [ci][co][kh][kw]) of the
+ * forward map (S1/S2/P1/U2): sum over rows of x[src_row(row,t)][ci] * dz[row][co]; ci, co % 128 == 0 */
+size_t rpc_dense_wgrad_workspace_size(int map, const int* row_img, int ci, int co);
+int rpc_dense_wgrad(int map, int kind, const void* x, int x_pitch, int ci, const void* dz, int dz_pitch, int co,
+                    const int* row_img, const int* src_img, const int* out_img, float* dW, void* workspace,
+                    size_t workspace_bytes, void* stream);
+/* h = relu((z - mean) * scale + beta) -> out[row][offset + c] (bn = scale, beta, mean, invstd) */
+int rpc_dense_bn_apply(const void* z, int m, int c, const float* bn, void* out, int out_pitch, int out_offset,
+                       void* stream);
+/* BatchNorm2d + ReLU backward: partial sums (sum dm, sum dm*xhat) per block, then
+ * dz = gi * (dm - m1 - xhat * m2) with bnb from rpc_bn_finalize(mode 1) */
+int rpc_dense_bnbwd_blocks(int m);
+int rpc_dense_bnbwd_stats(const void* dh, int dh_pitch, int dh_offset, const void* z, int m, int c,
+                          const float* bn, float* part, void* stream);
+int rpc_dense_bnbwd_apply(const void* dh, int dh_pitch, int dh_offset, const void* z, int m, int c,
+                          const float* bn, const float* bnb, void* dz, void* stream);
+/* torch fp32 weights -> bf16 GEMM operands: fwd [taps][co][ci] and/or dgrad [taps][ci][co] (flip: taps reversed) */
+int rpc_dense_wprep(const float* W, int kind, int ci, int co, int taps, int flip, void* w_fwd, void* w_dgrad,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -65,6 +65,15 @@ SIGNATURES = {
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_wgrad_bf16": (i32, [vp, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
+    "rpc_dense_conv": (i32, [i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, vp, ip, ip, ip, vp]),
+    "rpc_dense_conv_blocks": (i32, [i32, ip]),
+    "rpc_dense_wgrad_workspace_size": (sz, [i32, ip, i32, i32]),
+    "rpc_dense_wgrad": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, ip, ip, ip, vp, vp, sz, vp]),
+    "rpc_dense_bn_apply": (i32, [vp, i32, i32, vp, vp, i32, i32, vp]),
+    "rpc_dense_bnbwd_blocks": (i32, [i32]),
+    "rpc_dense_bnbwd_stats": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp]),
+    "rpc_dense_bnbwd_apply": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
+    "rpc_dense_wprep": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
 }
 
 

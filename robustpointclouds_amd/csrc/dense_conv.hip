@@ -1,0 +1,644 @@
+// a7 perf mode: the dense BEV backbone / neck (SECOND + SECONDFPN, upstream mmdet3d
+// backbones/second.py, necks/second_fpn.py as configured at
+// configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-car.py via its base) as
+// bf16-MFMA implicit GEMMs over NHWC images, for gfx950.
+//
+// Every convolution of the stack (and its data / weight gradients) is one GEMM whose rows are
+// image pixels and whose K dimension is (tap, input channel); a "map" turns (row pixel, tap)
+// into the source pixel arithmetically (zero padding = no source):
+//   S1  3x3 stride-1 pad-1 conv (also its data gradient, with the taps flipped)
+//   S2  3x3 stride-2 pad-1 conv (block 2's first layer)
+//   D2  data gradient of S2 (a transposed conv: source = (y+1-dy)/2 when even)
+//   P1  1x1 (FPN deblock 0: ConvTranspose2d kernel 1 stride 1) and its data gradient
+//   U2  FPN deblock 1 (ConvTranspose2d kernel 2 stride 2): one GEMM per output parity,
+//       rows = input pixels, output row = (2y+a, 2x+b)
+//   G2  data gradient of U2 (4 taps gathering (2y+a, 2x+b))
+// k_igemm: 128 pixels x 128 output channels per 256-thread block (4 waves, 64x64 each,
+// v_mfma_f32_16x16x32_bf16 with the weights as the A operand so each lane ends up holding 4
+// consecutive output channels of one pixel), K-steps of 64 channels of one tap, register-staged
+// double-buffered LDS tiles (pitch 72 elements: conflict-free ds_read_b128), XCD-aware block
+// order. Epilogue: bf16 output (optionally added into an existing image, optionally at a channel
+// offset of a wider image = the FPN concat) + per-block BatchNorm partial sums (sum, sum of
+// squares) of the stored values, reduced in a fixed order by rpc_bn_finalize.
+// k_wgrad: dW[t][ci][co] = sum_rows x[src(row,t)][ci] * dz[row][co] with rows as the MFMA K
+// dimension (row-major LDS tiles read back with ds_read_b64_tr_b16), split over row chunks into
+// fp32 slabs reduced in a fixed order (k_slab_reduce). BatchNorm apply / backward are
+// vectorised elementwise passes (8 channels per thread).
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+
+namespace rpc {
+namespace dn {
+
+constexpr int BLK = 256;
+constexpr int TM = 128;     // GEMM rows (pixels) per block
+constexpr int TN = 128;     // output channels per block
+constexpr int BK = 64;      // K-step = 64 channels of one tap
+constexpr int LP = BK + 8;  // LDS pitch (elements)
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef unsigned short u16;
+
+struct Img {
+  int B, H, W;
+};
+
+enum { M_S1 = 0, M_S2 = 1, M_D2 = 2, M_P1 = 3, M_U2 = 4, M_G2 = 5 };
+
+template <int MAP>
+__host__ __device__ constexpr int taps_of() {
+  return (MAP == M_P1 || MAP == M_U2) ? 1 : (MAP == M_G2 ? 4 : 9);
+}
+// weight-gradient "taps": U2 has one GEMM per output parity, each with its own weight slice
+template <int MAP>
+__host__ __device__ constexpr int wtaps_of() {
+  return MAP == M_U2 ? 4 : taps_of<MAP>();
+}
+
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+__device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float((unsigned)h << 16); }
+
+// K-operand source pixel of GEMM row pixel (b, y, x) for tap t in image S (-1: zero row)
+template <int MAP>
+__device__ __forceinline__ int src_row(int b, int y, int x, int t, const Img& S) {
+  int sy, sx;
+  if (MAP == M_S1) {
+    sy = y + t / 3 - 1;
+    sx = x + t % 3 - 1;
+  } else if (MAP == M_S2) {
+    sy = 2 * y + t / 3 - 1;
+    sx = 2 * x + t % 3 - 1;
+  } else if (MAP == M_D2) {
+    const int oy = y + 1 - t / 3, ox = x + 1 - t % 3;
+    if ((oy | ox) < 0 || ((oy | ox) & 1)) return -1;
+    sy = oy >> 1;
+    sx = ox >> 1;
+  } else if (MAP == M_G2) {
+    sy = 2 * y + (t >> 1);
+    sx = 2 * x + (t & 1);
+  } else {
+    sy = y;
+    sx = x;
+  }
+  if (sy < 0 || sy >= S.H || sx < 0 || sx >= S.W) return -1;
+  return (b * S.H + sy) * S.W + sx;
+}
+
+// output pixel of GEMM row m = (b, y, x) (U2: parity par of the 2x upsampled image O)
+template <int MAP>
+__device__ __forceinline__ int out_row(int m, int b, int y, int x, int par, const Img& O) {
+  if (MAP == M_U2) return (b * O.H + 2 * y + (par >> 1)) * O.W + 2 * x + (par & 1);
+  return m;
+}
+
+// bijective XCD-aware remap of a 1-D block index (consecutive tiles -> the same XCD's L2)
+__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
+  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+}
+
+// ------------------------------------------------------------------ implicit GEMM (fwd / dgrad)
+struct IG {
+  const u16* src;  // K-operand image rows [S pixels][SP]
+  int SP;
+  int CIN;         // K channels per tap (multiple of 64)
+  const u16* wt;   // [taps][COUT][CIN] bf16 (U2: [parity][COUT][CIN])
+  int COUT;        // multiple of 128
+  u16* out;        // output rows [O pixels][OP] at channel offset OOFF
+  int OP, OOFF;
+  int accum;       // add into the existing output
+  float* part;     // [gridDim.z * gridDim.x][2 * COUT] BatchNorm partial sums, or null
+  Img R, S, O;     // GEMM-row image, source image, output image
+  int M;           // GEMM rows = R.B * R.H * R.W
+};
+
+template <int MAP>
+__global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
+  constexpr int T = taps_of<MAP>();
+  __shared__ __attribute__((aligned(16))) u16 sX[2][TM * LP];
+  __shared__ __attribute__((aligned(16))) u16 sW[2][TN * LP];
+  __shared__ int sRow[TM * T];
+  __shared__ float sP[2][2][TN];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wc = w >> 1, wp = w & 1;  // wave: output channels wc*64.., pixels wp*64..
+  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = bx * TM, n0 = blockIdx.y * TN, par = blockIdx.z;
+  const int KC = g.CIN / BK, NKS = T * KC;
+  const u16* wbase = g.wt + (size_t)par * g.COUT * g.CIN;
+  const int HW = g.R.H * g.R.W;
+
+  for (int q = tid; q < TM * T; q += BLK) {
+    const int r = q / T, t = q - r * T, m = m0 + r;
+    int s = -1;
+    if (m < g.M) {
+      const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
+      s = src_row<MAP>(b, y, x, t, g.S);
+    }
+    sRow[q] = s;
+  }
+  __syncthreads();
+
+  // register staging: rx = activation chunks, rw = weight chunks of K-step ks (padding rows read
+  // row 0 and are zeroed by a select, so the loads stay branch-free and in flight)
+  uint4 rx0, rx1, rx2, rx3, rw0, rw1, rw2, rw3;
+  const int srow = tid >> 3, sseg = (tid & 7) * 8;   // chunk s: row srow + 32*s, channels sseg..+8
+#define IG_LOAD1(S, ks)                                                                             \
+  {                                                                                                 \
+    const int t_ = (ks) / KC, kc_ = (ks) - t_ * KC;                                                 \
+    const int sr_ = sRow[(srow + 32 * S) * T + t_];                                                 \
+    const unsigned keep_ = ~(unsigned)(sr_ >> 31);                                                  \
+    uint4 v_ = *(const uint4*)(g.src + (size_t)max(sr_, 0) * g.SP + kc_ * BK + sseg);                \
+    rx##S = make_uint4(v_.x & keep_, v_.y & keep_, v_.z & keep_, v_.w & keep_);                     \
+    rw##S = *(const uint4*)(wbase + ((size_t)(t_ * g.COUT + n0 + srow + 32 * S)) * g.CIN + kc_ * BK + sseg); \
+  }
+#define IG_LOAD(ks) { IG_LOAD1(0, ks) IG_LOAD1(1, ks) IG_LOAD1(2, ks) IG_LOAD1(3, ks) }
+#define IG_STORE1(S, buf)                                          \
+  *(uint4*)&sX[buf][(srow + 32 * S) * LP + sseg] = rx##S;          \
+  *(uint4*)&sW[buf][(srow + 32 * S) * LP + sseg] = rw##S;
+#define IG_STORE(buf) { IG_STORE1(0, buf) IG_STORE1(1, buf) IG_STORE1(2, buf) IG_STORE1(3, buf) }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  IG_LOAD(0)
+  IG_STORE(0)
+  __syncthreads();
+  for (int ks = 0; ks < NKS; ++ks) {
+    const int buf = ks & 1;
+    const bool more = ks + 1 < NKS;
+    if (more) {
+      IG_LOAD(ks + 1)
+    }
+    __builtin_amdgcn_sched_barrier(0);   // keep the next tile's loads issued ahead of the MFMAs
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *(const bf16x8*)&sW[buf][(wc * 64 + i * 16 + (lane & 15)) * LP + kk * 32 + 8 * (lane >> 4)];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        b[j] = *(const bf16x8*)&sX[buf][(wp * 64 + j * 16 + (lane & 15)) * LP + kk * 32 + 8 * (lane >> 4)];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      IG_STORE(buf ^ 1)
+    }
+    __syncthreads();
+  }
+#undef IG_LOAD1
+#undef IG_LOAD
+#undef IG_STORE1
+#undef IG_STORE
+
+  // epilogue: lane holds channels co = n0 + wc*64 + i*16 + 4*(lane>>4) + r of pixel wp*64 + j*16 + (lane&15)
+  float s1[4][4], s2[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int m = m0 + wp * 64 + j * 16 + (lane & 15);
+    if (m >= g.M) continue;
+    int orow = m;
+    if (MAP == M_U2) {
+      const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
+      orow = out_row<MAP>(m, b, y, x, par, g.O);
+    }
+    u16* op = g.out + (size_t)orow * g.OP + g.OOFF + n0 + wc * 64 + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      uint2* p2 = (uint2*)(op + i * 16);
+      if (g.accum) {
+        uint2 e = *p2;
+        v[0] += bf2f((u16)(e.x & 0xffff));
+        v[1] += bf2f((u16)(e.x >> 16));
+        v[2] += bf2f((u16)(e.y & 0xffff));
+        v[3] += bf2f((u16)(e.y >> 16));
+      }
+      u16 hb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hb[r] = f2bf(v[r]);
+        const float q = bf2f(hb[r]);
+        s1[i][r] += q;
+        s2[i][r] += q * q;
+      }
+      *p2 = make_uint2((unsigned)hb[0] | ((unsigned)hb[1] << 16), (unsigned)hb[2] | ((unsigned)hb[3] << 16));
+    }
+  }
+  if (g.part == nullptr) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[i][r] += __shfl_xor(s1[i][r], o, 64);
+        s2[i][r] += __shfl_xor(s2[i][r], o, 64);
+      }
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wc * 64 + i * 16 + 4 * (lane >> 4) + r;
+        sP[wp][0][c] = s1[i][r];
+        sP[wp][1][c] = s2[i][r];
+      }
+  }
+  __syncthreads();
+  float* prow = g.part + ((size_t)blockIdx.z * gridDim.x + bx) * 2 * g.COUT;
+  if (tid < TN) {
+    prow[n0 + tid] = sP[0][0][tid] + sP[1][0][tid];
+    prow[g.COUT + n0 + tid] = sP[0][1][tid] + sP[1][1][tid];
+  }
+}
+
+// ------------------------------------------------------------------ weight gradient
+__device__ __forceinline__ s16x4 tr_read(const u16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+struct WG {
+  const u16* x;   // forward input image rows [S pixels][XP]
+  int XP;
+  const u16* dz;  // output-side gradient rows [O pixels][DP] at channel offset 0
+  int DP;
+  int CI, CO;     // multiples of 128
+  Img R, S, O;
+  int M, rows_per;
+  float* part;    // [chunks][T][CI][CO]
+};
+
+// grid: (chunks, T, (CI/128)*(CO/128)); 4 waves as 2 (ci) x 2 (co), 64x64 each
+template <int MAP>
+__global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
+  constexpr int T = wtaps_of<MAP>();
+  constexpr int RT = 64, P = 128 + 16;  // rows per sub-tile, LDS pitch (conflict-free tr reads)
+  __shared__ __attribute__((aligned(16))) u16 sX[RT * P];
+  __shared__ __attribute__((aligned(16))) u16 sD[RT * P];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wci = w >> 1, wco = w & 1;
+  const int chunk = blockIdx.x, t = blockIdx.y;
+  const int nco = g.CO / 128, ci0 = (blockIdx.z / nco) * 128, co0 = (blockIdx.z % nco) * 128;
+  const int rb0 = chunk * g.rows_per, rb1 = min(g.M, rb0 + g.rows_per);
+  const int HW = g.R.H * g.R.W;
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, rowoff = 4 * g4 + qq;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  uint4 rx[4], rd[4];
+  auto gload = [&](int rs) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int q = tid + s * BLK, r = q >> 4, seg = q & 15, m = rs + r;
+      rx[s] = rd[s] = make_uint4(0u, 0u, 0u, 0u);
+      if (m < rb1) {
+        const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
+        int xs, ds;
+        if (MAP == M_U2) {
+          xs = m;
+          ds = out_row<MAP>(m, b, y, x, t, g.O);
+        } else {
+          xs = src_row<MAP>(b, y, x, t, g.S);
+          ds = m;
+        }
+        if (xs >= 0) {
+          rx[s] = *(const uint4*)(g.x + (size_t)xs * g.XP + ci0 + seg * 8);
+          rd[s] = *(const uint4*)(g.dz + (size_t)ds * g.DP + co0 + seg * 8);
+        }
+      }
+    }
+  };
+  gload(rb0);
+  for (int rs = rb0; rs < rb1; rs += RT) {
+    __syncthreads();
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int q = tid + s * BLK, r = q >> 4, seg = q & 15;
+      *(uint4*)&sX[r * P + seg * 8] = rx[s];
+      *(uint4*)&sD[r * P + seg * 8] = rd[s];
+    }
+    __syncthreads();
+    if (rs + RT < rb1) gload(rs + RT);
+#pragma unroll
+    for (int ks = 0; ks < RT / 32; ++ks) {
+      const int r0 = 32 * ks + rowoff;
+      bf16x8 a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = wci * 64 + i * 16 + 4 * pp;
+        s16x4 v[2] = {tr_read(&sX[r0 * P + c]), tr_read(&sX[(r0 + 16) * P + c])};
+        a[i] = *(bf16x8*)v;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int c = wco * 64 + j * 16 + 4 * pp;
+        s16x4 v[2] = {tr_read(&sD[r0 * P + c]), tr_read(&sD[(r0 + 16) * P + c])};
+        b[j] = *(bf16x8*)v;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  float* out = g.part + ((size_t)chunk * T + t) * g.CI * g.CO;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ci = ci0 + wci * 64 + i * 16 + 4 * g4 + r, co = co0 + wco * 64 + j * 16 + (lane & 15);
+        out[(size_t)ci * g.CO + co] = acc[i][j][r];
+      }
+}
+
+// ------------------------------------------------------------------ BatchNorm passes (8 channels / thread)
+// h = relu((z - mean) * scale + beta) -> bf16 image rows at (OP, OOFF); bn = scale, beta, mean, invstd
+__global__ __launch_bounds__(BLK) void k_bn_apply(const u16* __restrict__ z, int M, int C, const float* __restrict__ bn,
+                                                  u16* __restrict__ out, int OP, int OOFF) {
+  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  const int CG = C >> 3;
+  if (t >= (long long)M * CG) return;
+  const int m = (int)(t / CG), c0 = (int)(t - (long long)m * CG) * 8;
+  uint4 v = *(const uint4*)(z + (size_t)m * C + c0);
+  const u16* e = (const u16*)&v;
+  u16 o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    o[j] = f2bf(fmaxf(fmaf(bf2f(e[j]) - bn[2 * C + c], bn[c], bn[C + c]), 0.0f));
+  }
+  *(uint4*)(out + (size_t)m * OP + OOFF + c0) = *(uint4*)o;
+}
+
+// BatchNorm-backward partial sums: dm = dh * [pre > 0]; part[blk] = (sum dm, sum dm * xhat)
+// block = 256 threads = (256 / CG) row lanes x CG channel groups; rows strided over the grid
+__global__ __launch_bounds__(BLK) void k_bnbwd_stats(const u16* __restrict__ dh, int DP, int DOFF,
+                                                     const u16* __restrict__ z, int M, int C,
+                                                     const float* __restrict__ bn, float* __restrict__ part) {
+  __shared__ float sh[2][BLK * 8];
+  const int CG = C >> 3, RL = BLK / CG;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  float s1[8], s2[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  if (rl < RL) {
+    for (int m = blockIdx.x * RL + rl; m < M; m += gridDim.x * RL) {
+      uint4 dv = *(const uint4*)(dh + (size_t)m * DP + DOFF + cg * 8);
+      uint4 zv = *(const uint4*)(z + (size_t)m * C + cg * 8);
+      const u16* de = (const u16*)&dv;
+      const u16* ze = (const u16*)&zv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int c = cg * 8 + j;
+        const float zz = bf2f(ze[j]);
+        const float pre = fmaf(zz - bn[2 * C + c], bn[c], bn[C + c]);
+        const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
+        s1[j] += d;
+        s2[j] += d * ((zz - bn[2 * C + c]) * bn[3 * C + c]);
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    sh[0][threadIdx.x * 8 + j] = s1[j];
+    sh[1][threadIdx.x * 8 + j] = s2[j];
+  }
+  __syncthreads();
+  // fixed-order combine over the row lanes: channel c = cg*8 + j
+  for (int c = threadIdx.x; c < C; c += BLK) {
+    const int g8 = c >> 3, j = c & 7;
+    float a = 0.f, b = 0.f;
+    for (int r = 0; r < RL; ++r) {
+      a += sh[0][(r * CG + g8) * 8 + j];
+      b += sh[1][(r * CG + g8) * 8 + j];
+    }
+    part[(size_t)blockIdx.x * 2 * C + c] = a;
+    part[(size_t)blockIdx.x * 2 * C + C + c] = b;
+  }
+}
+
+// dz = gi * (dm - m1 - xhat * m2) -> bf16 [M][C]; bnb = gi, m1, m2, mean, invstd; bn = forward
+__global__ __launch_bounds__(BLK) void k_bnbwd_apply(const u16* __restrict__ dh, int DP, int DOFF,
+                                                     const u16* __restrict__ z, int M, int C,
+                                                     const float* __restrict__ bn, const float* __restrict__ bnb,
+                                                     u16* __restrict__ dz) {
+  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  const int CG = C >> 3;
+  if (t >= (long long)M * CG) return;
+  const int m = (int)(t / CG), c0 = (int)(t - (long long)m * CG) * 8;
+  uint4 dv = *(const uint4*)(dh + (size_t)m * DP + DOFF + c0);
+  uint4 zv = *(const uint4*)(z + (size_t)m * C + c0);
+  const u16* de = (const u16*)&dv;
+  const u16* ze = (const u16*)&zv;
+  u16 o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    const float zz = bf2f(ze[j]);
+    const float pre = fmaf(zz - bn[2 * C + c], bn[c], bn[C + c]);
+    const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
+    const float xh = (zz - bnb[3 * C + c]) * bnb[4 * C + c];
+    o[j] = f2bf(bnb[c] * (d - bnb[C + c] - xh * bnb[2 * C + c]));
+  }
+  *(uint4*)(dz + (size_t)m * C + c0) = *(uint4*)o;
+}
+
+// ------------------------------------------------------------------ weight preparation
+// torch layouts -> bf16 GEMM operands. kind: 0 Conv2d 3x3 [co][ci][3][3]; 1 ConvTranspose2d
+// [ci][co][k][k] (k = 1 or 2). fwd: [T][co][ci]; dgrad: [T][ci][co] with, for a stride-1 3x3
+// conv, the taps flipped (S1 data gradient), otherwise the same tap order (D2 / P1 / G2).
+__global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int kind, int CI, int CO, int T,
+                                               int flip, u16* __restrict__ wf, u16* __restrict__ wd) {
+  const long long n = (long long)T * CI * CO;
+  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e >= n) return;
+  const int t = (int)(e / ((long long)CI * CO));
+  const int rem = (int)(e - (long long)t * CI * CO), ci = rem / CO, co = rem - ci * CO;
+  const float v = kind == 0 ? W[((size_t)co * CI + ci) * T + t] : W[((size_t)ci * CO + co) * T + t];
+  if (wf) wf[((size_t)t * CO + co) * CI + ci] = f2bf(v);
+  if (wd) {
+    const int td = flip ? T - 1 - t : t;
+    wd[((size_t)td * CI + ci) * CO + co] = f2bf(v);
+  }
+}
+
+// G[t][ci][co] fp32 -> torch layout (kind 0: [co][ci][t], kind 1: [ci][co][t])
+__global__ __launch_bounds__(BLK) void k_wgrad_store(const float* __restrict__ G, int kind, int CI, int CO, int T,
+                                                     float* __restrict__ dW) {
+  const long long n = (long long)T * CI * CO;
+  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e >= n) return;
+  const int t = (int)(e / ((long long)CI * CO));
+  const int rem = (int)(e - (long long)t * CI * CO), ci = rem / CO, co = rem - ci * CO;
+  if (kind == 0) dW[((size_t)co * CI + ci) * T + t] = G[e];
+  else dW[((size_t)ci * CO + co) * T + t] = G[e];
+}
+
+static inline unsigned cdivu(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
+
+template <int MAP>
+static void launch_igemm(const IG& g, int par_count, hipStream_t st) {
+  dim3 grid(cdivu(g.M, TM), g.COUT / TN, par_count);
+  hipLaunchKernelGGL((k_igemm<MAP>), grid, dim3(BLK), 0, st, g);
+}
+
+template <int MAP>
+static void launch_wgrad(const WG& g, int chunks, hipStream_t st) {
+  dim3 grid(chunks, wtaps_of<MAP>(), (g.CI / 128) * (g.CO / 128));
+  hipLaunchKernelGGL((k_wgrad<MAP>), grid, dim3(BLK), 0, st, g);
+}
+
+static int map_wtaps(int map) {
+  switch (map) {
+    case M_P1: return 1;
+    case M_U2:
+    case M_G2: return 4;
+    default: return 9;
+  }
+}
+
+static int wgrad_chunks(int M) {
+  int c = (M + 2047) / 2048;
+  return c < 1 ? 1 : (c > 1024 ? 1024 : c);
+}
+
+}  // namespace dn
+}  // namespace rpc
+
+using namespace rpc;
+using namespace rpc::dn;
+
+static inline Img img3(const int* d) { return Img{d[0], d[1], d[2]}; }
+
+extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const void* wt, int cout, void* out, int op,
+                              int ooff, int accum, float* part, const int* r_img, const int* s_img,
+                              const int* o_img, void* stream) {
+  if (map < M_S1 || map > M_G2 || !src || !wt || !out || !r_img || !s_img || !o_img) return RPC_ERR_ARG;
+  if (cin % BK || cout % TN || sp < cin || op < ooff + cout || (sp & 7) || (op & 7) || (ooff & 7)) return RPC_ERR_ARG;
+  IG g{(const u16*)src, sp, cin, (const u16*)wt, cout, (u16*)out, op, ooff, accum, part,
+       img3(r_img), img3(s_img), img3(o_img), 0};
+  g.M = g.R.B * g.R.H * g.R.W;
+  if (g.M == 0) return RPC_OK;
+  hipStream_t st = (hipStream_t)stream;
+  switch (map) {
+    case M_S1: launch_igemm<M_S1>(g, 1, st); break;
+    case M_S2: launch_igemm<M_S2>(g, 1, st); break;
+    case M_D2: launch_igemm<M_D2>(g, 1, st); break;
+    case M_P1: launch_igemm<M_P1>(g, 1, st); break;
+    case M_U2: launch_igemm<M_U2>(g, 4, st); break;
+    default: launch_igemm<M_G2>(g, 1, st); break;
+  }
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dense_conv_blocks(int map, const int* r_img) {
+  const long long M = (long long)r_img[0] * r_img[1] * r_img[2];
+  return (int)((M + TM - 1) / TM) * (map == M_U2 ? 4 : 1);
+}
+
+extern "C" size_t rpc_dense_wgrad_workspace_size(int map, const int* r_img, int ci, int co) {
+  const int M = r_img[0] * r_img[1] * r_img[2];
+  const int T = map_wtaps(map);
+  return (size_t)wgrad_chunks(M) * T * ci * co * sizeof(float) + (size_t)T * ci * co * sizeof(float);
+}
+
+extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci, const void* dz, int dp, int co,
+                               const int* r_img, const int* s_img, const int* o_img, float* dW, void* ws,
+                               size_t ws_bytes, void* stream) {
+  if (map < M_S1 || map > M_G2 || map == M_D2 || map == M_G2) return RPC_ERR_ARG;
+  if (ci % 128 || co % 128 || (xp & 7) || (dp & 7)) return RPC_ERR_ARG;
+  Img R = img3(r_img), S = img3(s_img), O = img3(o_img);
+  const int M = R.B * R.H * R.W, T = map_wtaps(map);
+  const int chunks = wgrad_chunks(M);
+  const size_t slab = (size_t)T * ci * co;
+  if (ws_bytes < (chunks + 1) * slab * sizeof(float)) return RPC_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  float* part = (float*)ws;
+  float* G = part + chunks * slab;
+  if (M == 0) {
+    RPC_CHECK(hipMemsetAsync(dW, 0, slab * sizeof(float), st));
+    return RPC_OK;
+  }
+  const int rows_per = ((M + chunks - 1) / chunks + 63) / 64 * 64;
+  WG g{(const u16*)x, xp, (const u16*)dz, dp, ci, co, R, S, O, M, rows_per, part};
+  switch (map) {
+    case M_S1: launch_wgrad<M_S1>(g, chunks, st); break;
+    case M_S2: launch_wgrad<M_S2>(g, chunks, st); break;
+    case M_P1: launch_wgrad<M_P1>(g, chunks, st); break;
+    default: launch_wgrad<M_U2>(g, chunks, st); break;
+  }
+  RPC_LAUNCH_CHECK();
+  slab_reduce(part, chunks, (long long)slab, G, st);
+  RPC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_wgrad_store, dim3(cdivu(slab, BLK)), dim3(BLK), 0, st, (const float*)G, kind, ci, co, T, dW);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dense_bn_apply(const void* z, int m, int c, const float* bn, void* out, int op, int ooff,
+                                  void* stream) {
+  if (m < 0 || c < 8 || (c & 7) || (op & 7) || (ooff & 7) || op < ooff + c) return RPC_ERR_ARG;
+  if (m == 0) return RPC_OK;
+  hipLaunchKernelGGL(k_bn_apply, dim3(cdivu((long long)m * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream,
+                     (const u16*)z, m, c, bn, (u16*)out, op, ooff);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dense_bnbwd_blocks(int m) {
+  int b = (m + 4095) / 4096;
+  return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+}
+
+extern "C" int rpc_dense_bnbwd_stats(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
+                                     float* part, void* stream) {
+  if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
+  const int nb = rpc_dense_bnbwd_blocks(m);
+  hipLaunchKernelGGL(k_bnbwd_stats, dim3(nb), dim3(BLK), 0, (hipStream_t)stream, (const u16*)dh, dp, doff,
+                     (const u16*)z, m, c, bn, part);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dense_bnbwd_apply(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
+                                     const float* bnb, void* dz, void* stream) {
+  if (m < 0 || c < 8 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
+  if (m == 0) return RPC_OK;
+  hipLaunchKernelGGL(k_bnbwd_apply, dim3(cdivu((long long)m * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream,
+                     (const u16*)dh, dp, doff, (const u16*)z, m, c, bn, bnb, (u16*)dz);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dense_wprep(const float* W, int kind, int ci, int co, int taps, int flip, void* wf, void* wd,
+                               void* stream) {
+  if (!W || ci < 1 || co < 1 || taps < 1 || (kind != 0 && kind != 1)) return RPC_ERR_ARG;
+  const long long n = (long long)taps * ci * co;
+  hipLaunchKernelGGL(k_wprep, dim3(cdivu(n, BLK)), dim3(BLK), 0, (hipStream_t)stream, W, kind, ci, co, taps, flip,
+                     (u16*)wf, (u16*)wd);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}

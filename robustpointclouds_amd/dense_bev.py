@@ -1,0 +1,319 @@
+"""Dense BEV backbone + neck on the HIP implicit-GEMM engine (perf mode).
+
+`SECOND` (upstream mmdet3d backbones/second.py) and `SECONDFPN` (necks/second_fpn.py), as
+configured at configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-car.py (base
+second_hv_secfpn_kitti.py) and called at models/detectors/adversarial_voxelnet.py:142-145, each
+become ONE autograd node over csrc/dense_conv.hip (C-ABI `rpc_dense_*`):
+
+  forward, per Conv-BN-ReLU layer: rpc_dense_conv (bf16 MFMA, NHWC, BatchNorm partial sums in
+  the epilogue) -> rpc_bn_finalize (batch statistics, running stats, momentum/eps of the module)
+  -> rpc_dense_bn_apply (normalise + ReLU -> bf16 image, the FPN concat written in place)
+  backward, per layer: rpc_dense_bnbwd_stats -> rpc_bn_finalize(mode 1) (dgamma, dbeta) ->
+  rpc_dense_bnbwd_apply (dz) -> rpc_dense_wgrad (dW, fp32) -> rpc_dense_conv (data gradient:
+  flipped-tap S1, D2 for the stride-2 layer, P1 / G2 for the deconvolutions)
+
+Activations are bf16 channels_last (fp32 accumulation, fp32 BatchNorm statistics); weights stay
+fp32 master copies (cast to bf16 GEMM operands per step). The module parameters and state-dict
+keys are the torch modules' own (second.py), so the two paths are interchangeable; the torch path
+remains the fp32 parity mode.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _ffi
+
+S1, S2, D2, P1, U2, G2 = 0, 1, 2, 3, 4, 5
+
+
+def _nhwc(t: torch.Tensor) -> torch.Tensor:
+    """[B, C, H, W] -> a bf16 channels_last tensor (its storage is the NHWC image)."""
+    t = t.to(torch.bfloat16)
+    if not t.is_contiguous(memory_format=torch.channels_last):
+        t = t.contiguous(memory_format=torch.channels_last)
+    return t
+
+
+def _image(B, C, H, W, dev):
+    return torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dev).permute(0, 3, 1, 2)
+
+
+def _bn_eval(bnm, dev):
+    inv = torch.rsqrt(bnm.running_var.float() + bnm.eps)
+    return torch.cat([bnm.weight.float() * inv, bnm.bias.float(), bnm.running_mean.float(), inv]).contiguous()
+
+
+class _Layer:
+    """One Conv/Deconv + BatchNorm2d + ReLU: geometry and the C-ABI calls for it."""
+
+    def __init__(self, fmap, conv, bnm, kind, ci, co, taps):
+        self.map, self.conv, self.bnm, self.kind = fmap, conv, bnm, kind
+        self.ci, self.co, self.taps = ci, co, taps
+
+    def images(self, B, H, W):
+        """(row image, source image, output image, output H, W) of the forward GEMM for input H x W."""
+        if self.map == S1 or self.map == P1:
+            return (B, H, W), (B, H, W), (B, H, W), H, W
+        if self.map == S2:
+            Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+            return (B, Ho, Wo), (B, H, W), (B, Ho, Wo), Ho, Wo
+        # U2: rows = input pixels, output = 2x upsampled image
+        return (B, H, W), (B, H, W), (B, 2 * H, 2 * W), 2 * H, 2 * W
+
+    def dgrad_map(self):
+        return {S1: S1, S2: D2, P1: P1, U2: G2}[self.map]
+
+
+def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_pitch=None, out_off=0):
+    """z = conv(h); BN (batch or running stats); y = relu(bn(z)) -> (y image, record)."""
+    R, S, O, Ho, Wo = L.images(B, H, W)
+    W32 = L.conv.weight.detach().float().contiguous()
+    wf = torch.empty((L.taps, L.co, L.ci), dtype=torch.bfloat16, device=dev)
+    wd = torch.empty((L.taps, L.ci, L.co), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_dense_wprep(_ffi.ptr(W32), L.kind, L.ci, L.co, L.taps, 1 if L.map == S1 else 0,
+                                   _ffi.ptr(wf), _ffi.ptr(wd), st), "rpc_dense_wprep")
+    Mo = B * Ho * Wo
+    z = torch.empty((Mo, L.co), dtype=torch.bfloat16, device=dev)
+    ri, si, oi = _ffi.int_arr(R), _ffi.int_arr(S), _ffi.int_arr(O)
+    part = None
+    if training:
+        nblk = lib.rpc_dense_conv_blocks(L.map, ri)
+        part = torch.empty((nblk, 2 * L.co), dtype=torch.float32, device=dev)
+    _ffi.check(lib.rpc_dense_conv(L.map, _ffi.ptr(h), pitch, L.ci, _ffi.ptr(wf), L.co, _ffi.ptr(z), L.co, 0, 0,
+                                  _ffi.ptr(part), ri, si, oi, st), "rpc_dense_conv")
+    bnm = L.bnm
+    if training:
+        bn = torch.empty(4 * L.co, dtype=torch.float32, device=dev)
+        wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(L.co), dev)
+        _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), part.shape[0], L.co, Mo, 0, _ffi.ptr(bnm.weight),
+                                       _ffi.ptr(bnm.bias), float(bnm.eps), float(bnm.momentum),
+                                       _ffi.ptr(bnm.running_mean), _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn),
+                                       None, None, _ffi.ptr(wsb), st), "rpc_bn_finalize")
+        bnm.num_batches_tracked += 1
+    else:
+        bn = _bn_eval(bnm, dev)
+    if out is None:
+        y = _image(B, L.co, Ho, Wo, dev)
+        out_pitch, out_off = L.co, 0
+    else:
+        y = out
+    _ffi.check(lib.rpc_dense_bn_apply(_ffi.ptr(z), Mo, L.co, _ffi.ptr(bn), _ffi.ptr(y), out_pitch, out_off, st),
+               "rpc_dense_bn_apply")
+    rec = dict(L=L, h=h, pitch=pitch, z=z, bn=bn, wd=wd, R=R, S=S, O=O, in_hw=(H, W), Mo=Mo)
+    return y, rec, Ho, Wo
+
+
+def _backward_layer(lib, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False):
+    """BN+ReLU backward, weight gradient and (optionally) data gradient of one layer."""
+    L = rec["L"]
+    Mo, co, ci = rec["Mo"], L.co, L.ci
+    nb = lib.rpc_dense_bnbwd_blocks(Mo)
+    part = torch.empty((nb, 2 * co), dtype=torch.float32, device=dev)
+    _ffi.check(lib.rpc_dense_bnbwd_stats(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
+                                         _ffi.ptr(rec["bn"]), _ffi.ptr(part), st), "rpc_dense_bnbwd_stats")
+    bnb = torch.empty(5 * co, dtype=torch.float32, device=dev)
+    dgamma = torch.empty(co, dtype=torch.float32, device=dev)
+    dbeta = torch.empty(co, dtype=torch.float32, device=dev)
+    wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(co), dev)
+    _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nb, co, Mo, 1, _ffi.ptr(L.bnm.weight), _ffi.ptr(L.bnm.bias),
+                                   0.0, 0.0, None, None, _ffi.ptr(rec["bn"]), _ffi.ptr(bnb), _ffi.ptr(dgamma),
+                                   _ffi.ptr(dbeta), _ffi.ptr(wsb), st), "rpc_bn_finalize(bwd)")
+    dz = torch.empty((Mo, co), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_dense_bnbwd_apply(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
+                                         _ffi.ptr(rec["bn"]), _ffi.ptr(bnb), _ffi.ptr(dz), st),
+               "rpc_dense_bnbwd_apply")
+    ri, si, oi = _ffi.int_arr(rec["R"]), _ffi.int_arr(rec["S"]), _ffi.int_arr(rec["O"])
+    # torch-contiguous layout (the kernel writes [co][ci][kh][kw] / [ci][co][kh][kw] densely), even when
+    # the module was converted to channels_last
+    dW = torch.empty(tuple(L.conv.weight.shape), dtype=torch.float32, device=dev)
+    wsz = lib.rpc_dense_wgrad_workspace_size(L.map, ri, ci, co)
+    ws = _ffi.workspace(wsz, dev)
+    # the U2 weight-gradient GEMM reads dz at the output rows; the others read it at the GEMM rows
+    _ffi.check(lib.rpc_dense_wgrad(L.map, L.kind, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), co, co,
+                                   ri, si, oi, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
+    dx = None
+    if need_dx:
+        dmap = L.dgrad_map()
+        B, H, W = rec["S"]
+        dx = dx_out if dx_out is not None else _image(B, ci, H, W, dev)
+        # data gradient GEMM: rows = forward source pixels, source image = forward output image
+        if L.map == U2:
+            rd, sd = rec["R"], rec["O"]
+        else:
+            rd, sd = rec["S"], rec["O"]
+        _ffi.check(lib.rpc_dense_conv(dmap, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
+                                      1 if accumulate else 0, None, _ffi.int_arr(rd), _ffi.int_arr(sd),
+                                      _ffi.int_arr(rd), st), "rpc_dense_conv(dgrad)")
+    return dx, dW, dgamma, dbeta
+
+
+def second_layers(mod):
+    """_Layer list per block of a SECOND module (Conv2d 3x3 + BN + ReLU sequences)."""
+    blocks = []
+    for blk in mod.blocks:
+        mods = list(blk.children())
+        layers = []
+        for i in range(0, len(mods), 3):
+            conv, bnm = mods[i], mods[i + 1]
+            fmap = S2 if conv.stride[0] == 2 else S1
+            layers.append(_Layer(fmap, conv, bnm, 0, conv.in_channels, conv.out_channels, 9))
+        blocks.append(layers)
+    return blocks
+
+
+def fpn_layers(mod):
+    out = []
+    for d in mod.deblocks:
+        up, bnm = d[0], d[1]
+        k = up.kernel_size[0]
+        assert isinstance(up, torch.nn.ConvTranspose2d) and up.stride[0] == k and k in (1, 2), \
+            "HIP SECONDFPN supports ConvTranspose2d deblocks with kernel = stride in {1, 2}"
+        out.append(_Layer(P1 if k == 1 else U2, up, bnm, 1, up.in_channels, up.out_channels, k * k))
+    return out
+
+
+def _check_widths(layers):
+    for L in layers:
+        if L.ci % 128 or L.co % 128:
+            raise RuntimeError(f"HIP dense conv needs channel counts that are multiples of 128 (got {L.ci}->{L.co})")
+
+
+class BackboneFn(torch.autograd.Function):
+    """SECOND forward/backward as one node: x [B, Cin, H, W] -> tuple of block outputs."""
+
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        lib = _ffi.load()
+        dev = x.device
+        st = _ffi.stream_of(x)
+        blocks = second_layers(mod)
+        for b in blocks:
+            _check_widths(b)
+        xi = _nhwc(x)
+        B, C, H, W = xi.shape
+        h, pitch = xi, C
+        recs, outs = [], []
+        for layers in blocks:
+            brecs = []
+            for L in layers:
+                h, rec, H, W = _forward_layer(lib, L, h, pitch, B, H, W, mod.training, dev, st)
+                pitch = L.co
+                brecs.append(rec)
+            recs.append(brecs)
+            outs.append(h)
+        ctx.recs = recs
+        ctx.param_list = params
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        lib = _ffi.load()
+        recs = ctx.recs
+        g_any = next(g for g in gouts if g is not None)
+        dev = g_any.device
+        st = _ffi.stream_of(g_any)
+        grads = {}
+        nb = len(recs)
+        # dh = complete gradient w.r.t. the output of block bi (its own output gradient plus what
+        # block bi+1's first data-gradient GEMM accumulated into a copy of it)
+        dh = _nhwc(gouts[-1]) if gouts[-1] is not None else None
+        dx = None
+        for bi in range(nb - 1, -1, -1):
+            brecs = recs[bi]
+            if dh is None:   # nothing flows through this block
+                dh = _nhwc(gouts[bi - 1]) if bi > 0 and gouts[bi - 1] is not None else None
+                continue
+            for li in range(len(brecs) - 1, -1, -1):
+                rec = brecs[li]
+                dx_out, accumulate = None, False
+                if li > 0:
+                    need_dx = True
+                elif bi > 0:
+                    need_dx = True
+                    if gouts[bi - 1] is not None:
+                        dx_out = _nhwc(gouts[bi - 1]).clone(memory_format=torch.channels_last)
+                        accumulate = True
+                else:
+                    need_dx = ctx.needs_input_grad[0]
+                dh, dW, dgam, dbet = _backward_layer(lib, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
+                                                     accumulate)
+                grads[id(rec["L"].conv.weight)] = dW
+                grads[id(rec["L"].bnm.weight)] = dgam
+                grads[id(rec["L"].bnm.bias)] = dbet
+            if bi == 0:
+                dx = dh
+        ctx.recs = None
+        return (dx, None) + tuple(grads.get(id(p)) for p in ctx.param_list)
+
+
+class NeckFn(torch.autograd.Function):
+    """SECONDFPN forward/backward as one node: (block outputs) -> [B, sum(out), H0, W0]."""
+
+    @staticmethod
+    def forward(ctx, h0, h1, mod, *params):
+        lib = _ffi.load()
+        dev = h0.device
+        st = _ffi.stream_of(h0)
+        layers = fpn_layers(mod)
+        _check_widths(layers)
+        ins = [_nhwc(h0), _nhwc(h1)]
+        B, _, H0, W0 = ins[0].shape
+        Ctot = sum(L.co for L in layers)
+        out = _image(B, Ctot, H0, W0, dev)
+        recs = []
+        off = 0
+        for L, hi in zip(layers, ins):
+            _, C, H, W = hi.shape
+            _, rec, Ho, Wo = _forward_layer(lib, L, hi, C, B, H, W, mod.training, dev, st, out=out, out_pitch=Ctot,
+                                            out_off=off)
+            assert (Ho, Wo) == (H0, W0), "FPN deblocks must upsample to the first block's resolution"
+            rec["off"] = off
+            recs.append(rec)
+            off += L.co
+        ctx.recs = recs
+        ctx.Ctot = Ctot
+        ctx.param_list = params
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        lib = _ffi.load()
+        dev = gout.device
+        st = _ffi.stream_of(gout)
+        g = _nhwc(gout)
+        grads = {}
+        dins = []
+        for rec in ctx.recs:
+            L = rec["L"]
+            dx, dW, dgam, dbet = _backward_layer(lib, rec, g, ctx.Ctot, rec["off"], dev, st, True)
+            grads[id(L.conv.weight)] = dW
+            grads[id(L.bnm.weight)] = dgam
+            grads[id(L.bnm.bias)] = dbet
+            dins.append(dx)
+        ctx.recs = None
+        return (dins[0], dins[1], None) + tuple(grads.get(id(p)) for p in ctx.param_list)
+
+
+def backbone_params(mod):
+    ps = []
+    for layers in second_layers(mod):
+        for L in layers:
+            ps += [L.conv.weight, L.bnm.weight, L.bnm.bias]
+    return ps
+
+
+def neck_params(mod):
+    ps = []
+    for L in fpn_layers(mod):
+        ps += [L.conv.weight, L.bnm.weight, L.bnm.bias]
+    return ps
+
+
+def second_forward(mod, x):
+    return BackboneFn.apply(x, mod, *backbone_params(mod))
+
+
+def fpn_forward(mod, xs):
+    if len(xs) != 2:
+        raise RuntimeError("HIP SECONDFPN path is built for the two-block SECOND of the KITTI configs")
+    return [NeckFn.apply(xs[0], xs[1], mod, *neck_params(mod))]

@@ -36,8 +36,12 @@ class SECOND(nn.Module):
         for m in self.modules():   # init_cfg = Kaiming on Conv2d (mmdet3d default)
             if isinstance(m, nn.Conv2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        self.hip = False   # perf mode: the whole stack as one HIP implicit-GEMM node (dense_bev.py)
 
     def forward(self, x):
+        if self.hip:
+            from .dense_bev import second_forward
+            return second_forward(self, x)
         outs = []
         for b in self.blocks:
             x = b(x)
@@ -64,7 +68,11 @@ class SECONDFPN(nn.Module):
         for m in self.modules():
             if isinstance(m, nn.ConvTranspose2d):
                 nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        self.hip = False   # perf mode: deblocks + concat as one HIP node (dense_bev.py)
 
     def forward(self, x):
+        if self.hip:
+            from .dense_bev import fpn_forward
+            return fpn_forward(self, x)
         ups = [d(x[i]) for i, d in enumerate(self.deblocks)]
         return [torch.cat(ups, dim=1) if len(ups) > 1 else ups[0]]

@@ -77,6 +77,9 @@ class Trainer:
             for name in ("backbone", "neck", "bbox_head"):
                 if getattr(model, name, None) is not None:
                     getattr(model, name).to(memory_format=torch.channels_last)
+            for name in ("backbone", "neck"):   # SECOND / SECONDFPN on the HIP dense-conv engine
+                if hasattr(getattr(model, name, None), "hip"):
+                    getattr(model, name).hip = True
         if ddp and dist.is_initialized() and dist.get_world_size() > 1:
             self.model = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[self.device.index] if self.device.type == "cuda" else None,

@@ -1,0 +1,262 @@
+"""a7 perf mode: the HIP dense-conv engine (csrc/dense_conv.hip) against torch fp32.
+
+Kernel level: with bf16 operands fixed, every GEMM map (S1, S2, D2, P1, U2, G2) and the weight
+gradient must equal a float64 torch computation on the same bf16 values to fp32-accumulation
+accuracy (outputs are rounded to bf16 once: tolerance 1 bf16 ulp of the output scale).
+Module level: SECOND + SECONDFPN forward/backward through BackboneFn/NeckFn against the fp32
+torch modules (bf16 activations: relative-L2 / cosine bounds written in the tests).
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from robustpointclouds_amd import _ffi
+from robustpointclouds_amd.second import SECOND, SECONDFPN
+
+pytestmark = pytest.mark.gpu
+S1, S2, D2, P1, U2, G2 = 0, 1, 2, 3, 4, 5
+DEV = torch.device("cuda")
+
+
+def _rand(*shape, seed=0, scale=1.0):
+    g = torch.Generator().manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(torch.bfloat16)
+
+
+def _nhwc(t):   # [B, C, H, W] bf16 -> contiguous NHWC on the GPU
+    return t.permute(0, 2, 3, 1).contiguous().to(DEV)
+
+
+def _conv(fmap, src_nhwc, cin, wt, cout, R, S, O, out=None, accum=False, stats=False):
+    lib = _ffi.load()
+    Mo = O[0] * O[1] * O[2]
+    if out is None:
+        out = torch.zeros((Mo, cout), dtype=torch.bfloat16, device=DEV)
+    part = None
+    if stats:
+        part = torch.zeros((lib.rpc_dense_conv_blocks(fmap, _ffi.int_arr(R)), 2 * cout), device=DEV)
+    _ffi.check(lib.rpc_dense_conv(fmap, _ffi.ptr(src_nhwc), cin, cin, _ffi.ptr(wt), cout, _ffi.ptr(out), cout, 0,
+                                  1 if accum else 0, _ffi.ptr(part), _ffi.int_arr(R), _ffi.int_arr(S),
+                                  _ffi.int_arr(O), _ffi.stream_of(out)), "rpc_dense_conv")
+    return out, part
+
+
+def _wprep(W, kind, taps, flip):
+    lib = _ffi.load()
+    if kind == 0:
+        co, ci = W.shape[:2]
+    else:
+        ci, co = W.shape[:2]
+    wf = torch.empty((taps, co, ci), dtype=torch.bfloat16, device=DEV)
+    wd = torch.empty((taps, ci, co), dtype=torch.bfloat16, device=DEV)
+    W32 = W.float().contiguous().to(DEV)
+    _ffi.check(lib.rpc_dense_wprep(_ffi.ptr(W32), kind, ci, co, taps, flip, _ffi.ptr(wf), _ffi.ptr(wd),
+                                   _ffi.stream_of(wf)), "wprep")
+    return wf, wd
+
+
+def _close_bf16(got, want):
+    got = got.float().cpu()
+    want = want.float().cpu()
+    scale = want.abs().max().item()
+    err = (got - want).abs().max().item()
+    assert err <= 2 ** -7 * max(scale, 1e-6), (err, scale)
+
+
+@pytest.mark.parametrize("ci,co,H,W", [(128, 128, 20, 18), (256, 128, 9, 14), (128, 256, 16, 10)])
+def test_s1_forward_and_flipped_dgrad(ci, co, H, W):
+    B = 2
+    x = _rand(B, ci, H, W, seed=1)
+    Wt = _rand(co, ci, 3, 3, seed=2, scale=0.05)
+    wf, wd = _wprep(Wt, 0, 9, 1)
+    img = (B, H, W)
+    z, part = _conv(S1, _nhwc(x), ci, wf, co, img, img, img, stats=True)
+    ref = F.conv2d(x.double(), Wt.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
+    _close_bf16(z, ref)
+    # BatchNorm partial sums = column sums of the stored bf16 values
+    zs = z.float()
+    torch.testing.assert_close(part[:, :co].sum(0), zs.sum(0), rtol=1e-4, atol=1e-2)
+    torch.testing.assert_close(part[:, co:].sum(0), (zs * zs).sum(0), rtol=1e-4, atol=1e-2)
+    # data gradient: conv with flipped taps, transposed weights
+    dz = _rand(B, co, H, W, seed=3)
+    dx, _ = _conv(S1, _nhwc(dz), co, wd, ci, img, img, img)
+    xr = x.double().requires_grad_(True)
+    F.conv2d(xr, Wt.double(), padding=1).backward(dz.double())
+    _close_bf16(dx, xr.grad.permute(0, 2, 3, 1).reshape(-1, ci))
+
+
+@pytest.mark.parametrize("H,W", [(20, 18), (21, 17)])
+def test_s2_forward_and_d2_dgrad(H, W):
+    B, ci, co = 2, 128, 256
+    x = _rand(B, ci, H, W, seed=4)
+    Wt = _rand(co, ci, 3, 3, seed=5, scale=0.05)
+    wf, wd = _wprep(Wt, 0, 9, 0)
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    z, _ = _conv(S2, _nhwc(x), ci, wf, co, (B, Ho, Wo), (B, H, W), (B, Ho, Wo))
+    ref = F.conv2d(x.double(), Wt.double(), stride=2, padding=1)
+    assert ref.shape[2:] == (Ho, Wo)
+    _close_bf16(z, ref.permute(0, 2, 3, 1).reshape(-1, co))
+    dz = _rand(B, co, Ho, Wo, seed=6)
+    dx, _ = _conv(D2, _nhwc(dz), co, wd, ci, (B, H, W), (B, Ho, Wo), (B, H, W))
+    xr = x.double().requires_grad_(True)
+    F.conv2d(xr, Wt.double(), stride=2, padding=1).backward(dz.double())
+    _close_bf16(dx, xr.grad.permute(0, 2, 3, 1).reshape(-1, ci))
+
+
+def test_p1_u2_g2_deconvolutions():
+    B, H, W = 2, 10, 9
+    # P1: ConvTranspose2d(128, 256, 1, 1)
+    x = _rand(B, 128, 2 * H, 2 * W, seed=7)
+    Wp = _rand(128, 256, 1, 1, seed=8, scale=0.05)
+    wf, wd = _wprep(Wp, 1, 1, 0)
+    img = (B, 2 * H, 2 * W)
+    z, _ = _conv(P1, _nhwc(x), 128, wf, 256, img, img, img)
+    _close_bf16(z, F.conv_transpose2d(x.double(), Wp.double()).permute(0, 2, 3, 1).reshape(-1, 256))
+    dz = _rand(B, 256, 2 * H, 2 * W, seed=9)
+    dx, _ = _conv(P1, _nhwc(dz), 256, wd, 128, img, img, img)
+    _close_bf16(dx, F.conv2d(dz.double(), Wp.double()).permute(0, 2, 3, 1).reshape(-1, 128))
+    # U2: ConvTranspose2d(256, 256, 2, 2)
+    x1 = _rand(B, 256, H, W, seed=10)
+    Wu = _rand(256, 256, 2, 2, seed=11, scale=0.05)
+    wf, wd = _wprep(Wu, 1, 4, 0)
+    z, part = _conv(U2, _nhwc(x1), 256, wf, 256, (B, H, W), (B, H, W), (B, 2 * H, 2 * W), stats=True)
+    ref = F.conv_transpose2d(x1.double(), Wu.double(), stride=2)
+    _close_bf16(z, ref.permute(0, 2, 3, 1).reshape(-1, 256))
+    torch.testing.assert_close(part[:, :256].sum(0), z.float().sum(0), rtol=1e-4, atol=1e-2)
+    # G2: its data gradient
+    dz = _rand(B, 256, 2 * H, 2 * W, seed=12)
+    dx, _ = _conv(G2, _nhwc(dz), 256, wd, 256, (B, H, W), (B, 2 * H, 2 * W), (B, H, W))
+    xr = x1.double().requires_grad_(True)
+    F.conv_transpose2d(xr, Wu.double(), stride=2).backward(dz.double())
+    _close_bf16(dx, xr.grad.permute(0, 2, 3, 1).reshape(-1, 256))
+
+
+def test_dgrad_accumulates_into_existing_image():
+    B, H, W, c = 1, 8, 8, 128
+    x = _rand(B, c, H, W, seed=13)
+    Wt = _rand(c, c, 3, 3, seed=14, scale=0.05)
+    wf, _ = _wprep(Wt, 0, 9, 1)
+    base = _rand(B, c, H, W, seed=15)
+    img = (B, H, W)
+    out = _nhwc(base).reshape(-1, c).clone()
+    out, _ = _conv(S1, _nhwc(x), c, wf, c, img, img, img, out=out, accum=True)
+    ref = F.conv2d(x.double(), Wt.double(), padding=1) + base.double()
+    _close_bf16(out, ref.permute(0, 2, 3, 1).reshape(-1, c))
+
+
+@pytest.mark.parametrize("fmap,kind,ci,co,H,W", [(S1, 0, 128, 128, 24, 20), (S1, 0, 256, 128, 12, 10),
+                                                 (S2, 0, 128, 256, 24, 20), (P1, 1, 128, 256, 16, 12),
+                                                 (U2, 1, 256, 256, 8, 6)])
+def test_weight_gradient(fmap, kind, ci, co, H, W):
+    lib = _ffi.load()
+    B = 2
+    x = _rand(B, ci, H, W, seed=16)
+    if kind == 0:
+        Wt = _rand(co, ci, 3, 3, seed=17, scale=0.05)
+        stride = 2 if fmap == S2 else 1
+        f = lambda xx, ww: F.conv2d(xx, ww, stride=stride, padding=1)
+        Ho, Wo = ((H - 1) // 2 + 1, (W - 1) // 2 + 1) if fmap == S2 else (H, W)
+        R, S, O = (B, Ho, Wo), (B, H, W), (B, Ho, Wo)
+    else:
+        k = 1 if fmap == P1 else 2
+        Wt = _rand(ci, co, k, k, seed=17, scale=0.05)
+        f = lambda xx, ww: F.conv_transpose2d(xx, ww, stride=k)
+        Ho, Wo = H * k, W * k
+        R, S, O = (B, H, W), (B, H, W), (B, Ho, Wo)
+    dz = _rand(B, co, Ho, Wo, seed=18)
+    wr = Wt.double().requires_grad_(True)
+    f(x.double(), wr).backward(dz.double())
+    dW = torch.empty(Wt.shape, dtype=torch.float32, device=DEV)
+    wsz = lib.rpc_dense_wgrad_workspace_size(fmap, _ffi.int_arr(R), ci, co)
+    ws = _ffi.workspace(wsz, DEV)
+    xn, dn = _nhwc(x), _nhwc(dz)   # keep both alive across the call (raw pointers only cross the ABI)
+    _ffi.check(lib.rpc_dense_wgrad(fmap, kind, _ffi.ptr(xn), ci, ci, _ffi.ptr(dn), co, co,
+                                   _ffi.int_arr(R), _ffi.int_arr(S), _ffi.int_arr(O), _ffi.ptr(dW), _ffi.ptr(ws),
+                                   wsz, _ffi.stream_of(dW)), "rpc_dense_wgrad")
+    got = dW.double().cpu()
+    want = wr.grad
+    assert (got - want).abs().max().item() <= 1e-5 * want.abs().max().item() + 1e-6
+
+
+def _modules(seed=0, ln=(2, 2)):
+    torch.manual_seed(seed)
+    bb = SECOND(in_channels=256, layer_nums=list(ln), layer_strides=[1, 2], out_channels=[128, 256])
+    nk = SECONDFPN(in_channels=[128, 256], upsample_strides=[1, 2], out_channels=[256, 256])
+    for m in list(bb.modules()) + list(nk.modules()):
+        if isinstance(m, torch.nn.BatchNorm2d):
+            with torch.no_grad():
+                m.weight.uniform_(0.5, 1.5)
+                m.bias.uniform_(-0.2, 0.2)
+    return bb.to(DEV), nk.to(DEV)
+
+
+def _run_stack(mode, x, G=None, ln=(2, 2)):
+    """mode: 'fp32' (torch reference), 'autocast' (torch bf16 autocast, channels_last = the library
+    bf16 path this engine replaces) or 'hip'. Returns (output, dx, param grads, modules)."""
+    bb, nk = _modules(ln=ln)
+    xi = x.to(torch.bfloat16).float()
+    if mode != "fp32":
+        bb.to(memory_format=torch.channels_last)
+        nk.to(memory_format=torch.channels_last)
+        xi = xi.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    if mode == "hip":
+        bb.hip = nk.hip = True
+    xi.requires_grad_(True)
+    with torch.autocast("cuda", dtype=torch.bfloat16, enabled=mode == "autocast"):
+        out = nk(bb(xi))[0]
+    if G is None:
+        G = torch.randn(out.shape, generator=torch.Generator().manual_seed(6)).to(DEV)
+    (out.float() * G).sum().backward()
+    grads = [p.grad.float() for p in list(bb.parameters()) + list(nk.parameters())]
+    return out.detach(), xi.grad.float(), grads, (bb, nk), G
+
+
+def _cos(a, b):
+    return (a.flatten().double() @ b.flatten().double() / (a.double().norm() * b.double().norm())).item()
+
+
+def test_second_fpn_hip_matches_torch_fp32():
+    """bf16 activations flip ReLU masks near zero, so gradients through stacked BN+ReLU layers
+    differ from fp32 by more than rounding; the bar is the library bf16 path (torch autocast,
+    MIOpen NHWC): the HIP engine must be at least as close to fp32 as it is (within 0.01 cosine),
+    with absolute floors, and its forward within 2 % relative L2 of fp32."""
+    B, H, W = 2, 40, 36
+    x = torch.relu(torch.randn(B, 256, H, W, generator=torch.Generator().manual_seed(5))).to(DEV)
+    x[:, :, ::3] = 0.0   # sparse-looking BEV
+    ref, dref, gref, (bbr, _), G = _run_stack("fp32", x)
+    ac, dac, gac, _, _ = _run_stack("autocast", x, G)
+    out, dx, gh, (bb, nk), _ = _run_stack("hip", x, G)
+    assert out.dtype == torch.bfloat16 and out.is_contiguous(memory_format=torch.channels_last)
+    rel = ((out.float() - ref).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel
+    for a, b in zip([m for m in bb.modules() if isinstance(m, torch.nn.BatchNorm2d)],
+                    [m for m in bbr.modules() if isinstance(m, torch.nn.BatchNorm2d)]):
+        torch.testing.assert_close(a.running_mean, b.running_mean, rtol=2e-2, atol=2e-3)
+        torch.testing.assert_close(a.running_var, b.running_var, rtol=2e-2, atol=2e-3)
+    c_h, c_a = _cos(dx, dref), _cos(dac, dref)
+    assert c_h > 0.97 and c_h >= c_a - 0.01, (c_h, c_a)
+    for i, (h, a, r) in enumerate(zip(gh, gac, gref)):
+        c_h, c_a = _cos(h, r), _cos(a, r)
+        assert c_h > 0.95 and c_h >= c_a - 0.01, (i, c_h, c_a)
+
+
+def test_second_fpn_hip_eval_mode():
+    B, H, W = 1, 16, 12
+    x = torch.relu(torch.randn(B, 256, H, W, generator=torch.Generator().manual_seed(8))).to(DEV)
+    bb_ref, nk_ref = _modules(1)
+    bb, nk = _modules(1)
+    for m in list(bb_ref.modules()) + list(nk_ref.modules()):
+        if isinstance(m, torch.nn.BatchNorm2d):
+            with torch.no_grad():
+                m.running_mean.uniform_(-0.1, 0.1)
+                m.running_var.uniform_(0.5, 2.0)
+    bb.load_state_dict(bb_ref.state_dict())
+    nk.load_state_dict(nk_ref.state_dict())
+    bb.hip = nk.hip = True
+    for m in (bb, nk, bb_ref, nk_ref):
+        m.eval()
+    with torch.no_grad():
+        ref = nk_ref(bb_ref(x))[0]
+        out = nk(bb(x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)))[0]
+    rel = ((out.float() - ref).norm() / ref.norm()).item()
+    assert rel < 2e-2, rel

@@ -234,9 +234,15 @@ class Anchor3DHead(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward_single(self, x):
-        cls = self.conv_cls(x)
-        reg = self.conv_reg(x)
-        d = self.conv_dir_cls(x) if self.use_direction_classifier else None
+        # the three 1x1 heads as ONE GEMM over the shared feature map (weights concatenated per
+        # call; the parameters stay the upstream modules'): one read of x, one gradient w.r.t. x
+        convs = [self.conv_cls, self.conv_reg] + ([self.conv_dir_cls] if self.use_direction_classifier else [])
+        w = torch.cat([c.weight for c in convs], 0)
+        b = torch.cat([c.bias for c in convs], 0)
+        y = Fn.conv2d(x, w, b)
+        outs = torch.split(y, [c.out_channels for c in convs], dim=1)
+        cls, reg = outs[0], outs[1]
+        d = outs[2] if self.use_direction_classifier else None
         return cls, reg, d
 
     def forward(self, feats):

@@ -268,6 +268,220 @@ __global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
   }
 }
 
+// ------------------------------------------------------------------ 3x3 stride-1 conv (S1) with halo tiles
+// The 10 stride-1 layers of SECOND and their data gradients. Block = 16x16 output pixels of one
+// image x 128 output channels, 8 waves (4 pixel quarters x 2 channel halves, 64x64 each). Per
+// 64-channel chunk the 18x18 input halo is staged ONCE in LDS and all 9 taps read it at shifted
+// rows (9x fewer activation loads than the generic implicit GEMM); the per-tap weight tiles
+// (128 x 64, shared by every block through L2) stream through a 3-deep register ring into a
+// double-buffered LDS tile so two taps of loads are in flight during each tap's 32 MFMAs/wave;
+// the next chunk's halo is prefetched into registers during taps 5-8.
+constexpr int CT = 16;                  // spatial tile edge
+constexpr int HT = CT + 2;              // halo edge
+constexpr int HR = HT * HT;             // halo rows (324)
+constexpr int CBLK = 512;               // threads
+constexpr int HCH = (HR * 8 + CBLK - 1) / CBLK;   // halo 16-B chunks per thread (6)
+
+struct C3 {
+  const u16* src;  // input image rows [B*H*W][SP]
+  int SP, CIN;
+  const u16* wt;   // [9][COUT][CIN]
+  int COUT;
+  u16* out;        // [B*H*W][OP] at OOFF
+  int OP, OOFF, accum;
+  float* part;     // [tiles][2*COUT] or null
+  int B, H, W, TY, TX;   // image, tiles per column / row
+};
+
+template <int DUMMY = 0>
+__global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
+  __shared__ __attribute__((aligned(16))) u16 sA[HR * LP];
+  __shared__ __attribute__((aligned(16))) u16 sW[2][TN * LP];
+  __shared__ float sP[4][2][TN];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wp = w & 3, wc = w >> 2;
+  const int ntiles = g.B * g.TY * g.TX;
+  const int tile = xcd_remap(blockIdx.x, ntiles);
+  const int b = tile / (g.TY * g.TX), trem = tile - b * g.TY * g.TX;
+  const int ty0 = (trem / g.TX) * CT, tx0 = (trem % g.TX) * CT;
+  const int n0 = blockIdx.y * TN;
+  const int NKC = g.CIN / BK, NS = 9 * NKC;
+
+  // ---- halo staging (chunk q: halo row q>>3, 8 channels (q&7)*8). Out-of-image rows load row 0
+  // and are zeroed when stored (the mask is applied at store time so the loads stay in flight).
+  uint4 ra[HCH];
+  unsigned hkeep = 0;
+  auto halo_load = [&](int kc) {
+    hkeep = 0;
+#pragma unroll
+    for (int i = 0; i < HCH; ++i) {
+      const int q = tid + i * CBLK;
+      const int hr = q >> 3, seg = (q & 7) * 8;
+      const int hy = hr / HT, hx = hr - hy * HT;
+      const int y = ty0 + hy - 1, x = tx0 + hx - 1;
+      const bool ok = q < HR * 8 && y >= 0 && y < g.H && x >= 0 && x < g.W;
+      hkeep |= (ok ? 1u : 0u) << i;
+      const size_t row = ok ? ((size_t)(b * g.H + y) * g.W + x) : 0;
+      ra[i] = *(const uint4*)(g.src + row * g.SP + kc * BK + seg);
+    }
+  };
+  auto halo_store = [&]() {
+#pragma unroll
+    for (int i = 0; i < HCH; ++i) {
+      const int q = tid + i * CBLK;
+      const unsigned keep = ((hkeep >> i) & 1u) ? 0xffffffffu : 0u;
+      if (q < HR * 8)
+        *(uint4*)&sA[(q >> 3) * LP + (q & 7) * 8] =
+            make_uint4(ra[i].x & keep, ra[i].y & keep, ra[i].z & keep, ra[i].w & keep);
+    }
+  };
+  // ---- weight tiles: step s = kc*9 + t; chunk q = tid, tid+512: row q>>3, channels (q&7)*8
+  const int wrow = tid >> 3, wseg = (tid & 7) * 8;
+  const u16* wbase = g.wt + (size_t)(n0 + wrow) * g.CIN + wseg;
+  const size_t wtap = (size_t)g.COUT * g.CIN, whalf = (size_t)64 * g.CIN;
+#define C3_WLOAD(R, s)                                                          \
+  {                                                                             \
+    const int kc_ = (s) / 9, t_ = (s) - kc_ * 9;                                \
+    const u16* p_ = wbase + t_ * wtap + kc_ * BK;                               \
+    R##a = *(const uint4*)p_;                                                   \
+    R##b = *(const uint4*)(p_ + whalf);                                         \
+  }
+#define C3_WSTORE(R, buf)                                        \
+  {                                                              \
+    *(uint4*)&sW[buf][wrow * LP + wseg] = R##a;                  \
+    *(uint4*)&sW[buf][(wrow + 64) * LP + wseg] = R##b;           \
+  }
+  uint4 r0a, r0b, r1a, r1b, r2a, r2b;
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // pixel p = wp*64 + j*16 + (lane&15) -> tile row wp*4 + j, column lane&15
+  const int pcol = lane & 15;
+  const u16* aw = &sW[0][(wc * 64 + (lane & 15)) * LP + 8 * (lane >> 4)];
+  const u16* ab = &sA[(wp * 4 * HT + pcol) * LP + 8 * (lane >> 4)];
+#define C3_COMPUTE(buf, t)                                                                                  \
+  {                                                                                                         \
+    const int dy_ = (t) / 3, dx_ = (t) % 3;                                                                 \
+    _Pragma("unroll") for (int kk = 0; kk < BK / 32; ++kk) {                                                \
+      bf16x8 a[4], bb[4];                                                                                   \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                         \
+        a[i] = *(const bf16x8*)(aw + (buf) * (TN * LP) + i * 16 * LP + kk * 32);                            \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                         \
+        bb[j] = *(const bf16x8*)(ab + ((j + dy_) * HT + dx_) * LP + kk * 32);                               \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                         \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);             \
+    }                                                                                                       \
+  }
+  // one tap step: MFMAs on LDS tile s; tile s+1 (register slot RN) -> the other LDS buffer;
+  // barrier; slot RN reloaded with tile s+4. All loads unconditional (clamped step index) so
+  // the counted vmcnt waits see a straight-line stream.
+#define C3_TAP(t, RN)                                      \
+  {                                                        \
+    const int s_ = kc * 9 + (t);                           \
+    if ((t) == 5) halo_load(min(kc + 1, NKC - 1));         \
+    C3_COMPUTE(s_ & 1, t)                                  \
+    C3_WSTORE(RN, (s_ + 1) & 1)                            \
+    __syncthreads();                                       \
+    C3_WLOAD(RN, min(s_ + 4, NS - 1))                      \
+  }
+
+  // prologue: halo(0) and W tile 0 in LDS; tiles 1, 2, 3 in flight in slots r1, r2, r0
+  halo_load(0);
+  C3_WLOAD(r0, 0)
+  halo_store();
+  C3_WSTORE(r0, 0)
+  C3_WLOAD(r1, min(1, NS - 1))
+  C3_WLOAD(r2, min(2, NS - 1))
+  C3_WLOAD(r0, min(3, NS - 1))
+  __syncthreads();
+  for (int kc = 0; kc < NKC; ++kc) {
+    if (kc > 0) {
+      halo_store();
+      __syncthreads();
+    }
+    C3_TAP(0, r1)
+    C3_TAP(1, r2)
+    C3_TAP(2, r0)
+    C3_TAP(3, r1)
+    C3_TAP(4, r2)
+    C3_TAP(5, r0)
+    C3_TAP(6, r1)
+    C3_TAP(7, r2)
+    C3_TAP(8, r0)
+  }
+#undef C3_TAP
+#undef C3_COMPUTE
+#undef C3_WLOAD
+#undef C3_WSTORE
+
+  // ---- epilogue (as k_igemm): lane holds co = n0 + wc*64 + i*16 + 4*(lane>>4) + r of pixel (wp*4+j, lane&15)
+  float s1[4][4], s2[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int y = ty0 + wp * 4 + j, x = tx0 + pcol;
+    if (y >= g.H || x >= g.W) continue;
+    const size_t orow = (size_t)(b * g.H + y) * g.W + x;
+    u16* op = g.out + orow * g.OP + g.OOFF + n0 + wc * 64 + 4 * (lane >> 4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      uint2* p2 = (uint2*)(op + i * 16);
+      if (g.accum) {
+        uint2 e = *p2;
+        v[0] += bf2f((u16)(e.x & 0xffff));
+        v[1] += bf2f((u16)(e.x >> 16));
+        v[2] += bf2f((u16)(e.y & 0xffff));
+        v[3] += bf2f((u16)(e.y >> 16));
+      }
+      u16 hb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hb[r] = f2bf(v[r]);
+        const float q = bf2f(hb[r]);
+        s1[i][r] += q;
+        s2[i][r] += q * q;
+      }
+      *p2 = make_uint2((unsigned)hb[0] | ((unsigned)hb[1] << 16), (unsigned)hb[2] | ((unsigned)hb[3] << 16));
+    }
+  }
+  if (g.part == nullptr) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[i][r] += __shfl_xor(s1[i][r], o, 64);
+        s2[i][r] += __shfl_xor(s2[i][r], o, 64);
+      }
+    }
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wc * 64 + i * 16 + 4 * (lane >> 4) + r;
+        sP[wp][0][c] = s1[i][r];
+        sP[wp][1][c] = s2[i][r];
+      }
+  }
+  __syncthreads();
+  float* prow = g.part + (size_t)tile * 2 * g.COUT;
+  if (tid < TN) {
+    prow[n0 + tid] = ((sP[0][0][tid] + sP[1][0][tid]) + sP[2][0][tid]) + sP[3][0][tid];
+    prow[g.COUT + n0 + tid] = ((sP[0][1][tid] + sP[1][1][tid]) + sP[2][1][tid]) + sP[3][1][tid];
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
 __device__ __forceinline__ s16x4 tr_read(const u16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
@@ -542,6 +756,13 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   g.M = g.R.B * g.R.H * g.R.W;
   if (g.M == 0) return RPC_OK;
   hipStream_t st = (hipStream_t)stream;
+  if (map == M_S1) {
+    const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
+    C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
+    hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / TN), dim3(CBLK), 0, st, c);
+    RPC_LAUNCH_CHECK();
+    return RPC_OK;
+  }
   switch (map) {
     case M_S1: launch_igemm<M_S1>(g, 1, st); break;
     case M_S2: launch_igemm<M_S2>(g, 1, st); break;
@@ -555,6 +776,7 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
 }
 
 extern "C" int rpc_dense_conv_blocks(int map, const int* r_img) {
+  if (map == M_S1) return r_img[0] * ((r_img[1] + CT - 1) / CT) * ((r_img[2] + CT - 1) / CT);
   const long long M = (long long)r_img[0] * r_img[1] * r_img[2];
   return (int)((M + TM - 1) / TM) * (map == M_U2 ? 4 : 1);
 }
@@ -609,8 +831,8 @@ extern "C" int rpc_dense_bn_apply(const void* z, int m, int c, const float* bn, 
 }
 
 extern "C" int rpc_dense_bnbwd_blocks(int m) {
-  int b = (m + 4095) / 4096;
-  return b < 1 ? 1 : (b > 1024 ? 1024 : b);
+  int b = (m + 255) / 256;   // ~16-32 rows per thread: enough blocks to fill the chip
+  return b < 1 ? 1 : (b > 2048 ? 2048 : b);
 }
 
 extern "C" int rpc_dense_bnbwd_stats(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,

@@ -32,8 +32,9 @@ def _args():
     ap.add_argument("--fp32", action="store_true", help="dense part in fp32 (parity mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6)
-    ap.add_argument("--roofline-kernel", default="dgrad,64,64",
-                    help="op,ci,co of the sparse conv launches timed with HIP events")
+    ap.add_argument("--roofline-kernel", default="dense",
+                    help="'dense' (the dominant kernel: 3x3 stride-1 bf16 conv, rpc::dn::k_conv3x3<0>) or "
+                         "op,ci,co of the sparse conv launches timed with HIP events")
     return ap.parse_args()
 
 
@@ -133,10 +134,16 @@ def main():
     torch.manual_seed(0)
     model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3)
     tr = Trainer(model, ddp=world > 1, bf16=not a.fp32, device=dev)
+    from robustpointclouds_amd import dense_bev
     from robustpointclouds_amd.sparse_encoder import KernelTimer
-    op, ci, co = a.roofline_kernel.split(",")
-    timer = KernelTimer(op, int(ci), int(co))
-    model.middle_encoder.timer = timer
+    if a.roofline_kernel == "dense":
+        timer = dense_bev.ConvTimer()
+        dense_bev.TIMER = timer
+        op = ci = co = None
+    else:
+        op, ci, co = a.roofline_kernel.split(",")
+        timer = KernelTimer(op, int(ci), int(co))
+        model.middle_encoder.timer = timer
     NB = 4
     data = _batches(NB, a.batch, rank, dev, a.classes)
     for i in range(a.warmup):
@@ -173,7 +180,17 @@ def main():
                                              "fp32 voxelize/perturber/sparse layer 0; bf16 MFMA (fp32 accumulate,"
                                              " fp32 BN statistics) sparse layers 1-11"),
                                parallelism=f"dp{world}"))
-        if ks:
+        if ks and op is None:
+            peak = PEAK["bf16_mfma"]
+            res["roofline"] = dict(bound="mfma", achieved=round(ks["tflops"], 3), peak=peak, unit="TFLOP/s",
+                                   frac=round(ks["tflops"] / peak, 4), traffic=_traffic("k_conv3x3"),
+                                   kernel=ks["kernel"] + " (SECOND 3x3 stride-1 conv, fwd + data gradient, "
+                                   "bf16 MFMA, fp32 accumulate)",
+                                   avg_launch_ms=round(ks["avg_ms"], 4), flops_per_launch=ks["flops_per_launch"],
+                                   algorithmic_bytes_per_launch=ks["bytes_per_launch"],
+                                   achieved_gbps=round(ks["gbps"], 1), launches=ks["launches"],
+                                   work="2*B*H*W*C_in*C_out*9 FLOP per launch")
+        elif ks:
             peak = PEAK["bf16_mfma" if ks["dtype"] == "bf16" else "fp32_mfma"]
             tag = ks["kernel"]
             res["roofline"] = dict(bound="mfma", achieved=round(ks["tflops"], 3), peak=peak,

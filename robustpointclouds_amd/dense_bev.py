@@ -26,6 +26,58 @@ from . import _ffi
 S1, S2, D2, P1, U2, G2 = 0, 1, 2, 3, 4, 5
 
 
+class ConvTimer:
+    """HIP-event timing of the S1 (3x3 stride-1, kernel `rpc::dn::k_conv3x3<0>`) launches of
+    rpc_dense_conv — forward and flipped-tap data gradient — on the stream they are launched on.
+    Algorithmic work per launch = 2 * B*H*W * C_in * C_out * 9 FLOP (every tap of a zero-padded
+    3x3 convolution); algorithmic bytes = bf16 source image + bf16 output image + bf16 weights.
+    bench.py installs one as `dense_bev.TIMER`."""
+
+    def __init__(self):
+        self.recs = []
+        self.enabled = False
+
+    def start(self):
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream())
+        return e
+
+    def stop(self, e0, rows, ci, co):
+        e1 = torch.cuda.Event(enable_timing=True)
+        e1.record(torch.cuda.current_stream())
+        self.recs.append((e0, e1, rows, ci, co))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        if not self.recs:
+            return None
+        ms = sum(a.elapsed_time(b) for a, b, *_ in self.recs)
+        flops = sum(2.0 * r * ci * co * 9 for _, _, r, ci, co in self.recs)
+        byts = sum(2.0 * r * (ci + co) + 2.0 * 9 * ci * co for _, _, r, ci, co in self.recs)
+        n = len(self.recs)
+        return dict(launches=n, avg_ms=ms / n, flops_per_launch=flops / n, bytes_per_launch=byts / n,
+                    tflops=flops / (ms * 1e-3) / 1e12, gbps=byts / (ms * 1e-3) / 1e9,
+                    kernel="rpc::dn::k_conv3x3<0>", dtype="bf16")
+
+
+TIMER = None
+
+
+def _conv(lib, fmap, *args):
+    """rpc_dense_conv, with the S1 launches timed when a ConvTimer is enabled."""
+    t = TIMER if (TIMER is not None and TIMER.enabled and fmap == S1) else None
+    e0 = t.start() if t is not None else None
+    rc = lib.rpc_dense_conv(fmap, *args)
+    if t is not None:
+        r = _ffi_img_rows(args[10])
+        t.stop(e0, r, args[2], args[4])
+    return rc
+
+
+def _ffi_img_rows(arr):
+    return int(arr[0]) * int(arr[1]) * int(arr[2])
+
+
 def _nhwc(t: torch.Tensor) -> torch.Tensor:
     """[B, C, H, W] -> a bf16 channels_last tensor (its storage is the NHWC image)."""
     t = t.to(torch.bfloat16)
@@ -79,7 +131,7 @@ def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
     if training:
         nblk = lib.rpc_dense_conv_blocks(L.map, ri)
         part = torch.empty((nblk, 2 * L.co), dtype=torch.float32, device=dev)
-    _ffi.check(lib.rpc_dense_conv(L.map, _ffi.ptr(h), pitch, L.ci, _ffi.ptr(wf), L.co, _ffi.ptr(z), L.co, 0, 0,
+    _ffi.check(_conv(lib, L.map, _ffi.ptr(h), pitch, L.ci, _ffi.ptr(wf), L.co, _ffi.ptr(z), L.co, 0, 0,
                                   _ffi.ptr(part), ri, si, oi, st), "rpc_dense_conv")
     bnm = L.bnm
     if training:
@@ -141,7 +193,7 @@ def _backward_layer(lib, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
             rd, sd = rec["R"], rec["O"]
         else:
             rd, sd = rec["S"], rec["O"]
-        _ffi.check(lib.rpc_dense_conv(dmap, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
+        _ffi.check(_conv(lib, dmap, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
                                       1 if accumulate else 0, None, _ffi.int_arr(rd), _ffi.int_arr(sd),
                                       _ffi.int_arr(rd), st), "rpc_dense_conv(dgrad)")
     return dx, dW, dgamma, dbeta

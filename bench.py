@@ -73,6 +73,7 @@ def _traffic(kernel_tag):
 
 def cpu_baseline(frames: int, classes: int):
     """The oracle restatement of the whole step on the host cores (bounded sample)."""
+    from oracle import anchor_head as oh
     from oracle import voxelize as ov
     from oracle.perturber import OraclePerturber, perturb_voxels
     from oracle.sparse_encoder import OracleSparseEncoder
@@ -101,13 +102,19 @@ def cpu_baseline(frames: int, classes: int):
     opt = torch.optim.AdamW(params, lr=1e-4, weight_decay=1e-3)
     pts, boxes, labels = kitti_batch(frames, seed0=1000, num_classes=classes)
     gt = pack_gt(list(zip(boxes, labels)), torch.device("cpu"))
+    head = model.bbox_head
+    hcfg = oh.cfg_of(head)
+    gen = head.prior_generator
+    anchors = oh.grid_anchors(200, 176, gen.ranges, gen.sizes, gen.rotations)
 
     def step():
         vox, coors, npts = ov.voxelize_frames(pts, KITTI_VOXEL_SIZE, KITTI_PC_RANGE, 5, 16000)
         vfe, _, ld = perturb_voxels(op, vox, npts)
         x = enc.forward(vfe.float(), coors, frames)
         x = model.neck(model.backbone(x))
-        losses = model.bbox_head.loss(x, dict(gt_boxes=gt[0], gt_labels=gt[1]))
+        w, b = head._stacked()
+        ref = oh.head_losses_from_z(hcfg, torch.nn.functional.conv2d(x[0], w), b, anchors, gt[0], gt[1])
+        losses = {k: [ref[k]] for k in ("loss_cls", "loss_bbox", "loss_dir")}
         total = sum(v[0] for v in losses.values()) + 0.01 * (3 * ld["intensity_loss"] + 10 * ld["bias_loss"] +
                                                              10 * ld["imbalance_loss"]) + 0.02 * ld["l2_norm"]
         total.backward()

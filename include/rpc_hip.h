@@ -236,6 +236,53 @@ int rpc_dense_bnbwd_apply(const void* dh, int dh_pitch, int dh_offset, const voi
 int rpc_dense_wprep(const float* W, int kind, int ci, int co, int taps, int flip, void* w_fwd, void* w_dgrad,
                     void* stream);
 
+
+/* ------------------------------------------------------------------ a8 / §8(f1) Anchor3DHead targets + losses
+ * Replaces upstream mmdet3d `Anchor3DHead.loss_by_feat` (dense_heads/anchor3d_head.py) with
+ * `AnchorTrainMixin.anchor_target_3d` (Max3DIoUAssigner over BboxOverlapsNearest3D, no sampler),
+ * mmcv `sigmoid_focal_loss`, mmdet `SmoothL1Loss` (+ add_sin_difference), `get_direction_target`
+ * + `CrossEntropyLoss`, as configured at
+ * configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:38-69,86-112 and
+ * …-kitti-3d-car.py:18-39; called at models/detectors/adversarial_voxelnet.py:168 (`bbox_head.loss`).
+ *
+ * Head outputs z (the 1x1 conv WITHOUT bias; `bias` [N] is added here) hold N = A*(C+7+2) channels
+ * ordered cls [A*C] | reg [A*7] | dir [A*2], anchor a = s*R + r; element (frame b, BEV cell
+ * loc = h*W + w, channel n) lives at z[b*z_sb + loc*z_shw + n*z_sn] (fp32, or bf16 if z_bf16):
+ * NCHW fp32 = (N*H*W, 1, H*W), the NHWC bf16 GEMM image with pitch P = (H*W*P, P, 1).
+ * anchor_tab (device fp32): xc[S][W], yc[S][H], zc[S], sizes[S][3], rotations[R] — the
+ * Anchor3DRangeGenerator centres (torch.linspace of each range).
+ * gt_boxes [B][max_gts][7] fp32, gt_labels [B][max_gts] int64 (-1 = padding).
+ * assigned [B][H*W*A] int32 out: -1 ignored, 0 negative, j+1 positive for gt j (kept for backward).
+ * losses (device fp32 [4]) out: loss_cls, loss_bbox, loss_dir, num_total_pos (= sum_b max(pos_b, 1)).
+ * The workspace must be kept between forward and backward. */
+#define RPC_HEAD_MAX_SIZES 4
+typedef struct {
+  int B, H, W;
+  int S, R, C;              /* anchor sizes (ranges), rotations, classes */
+  int NA;                   /* assigners: S (list-valued train_cfg.assigner) or 1 */
+  int assigner_per_size, assign_per_class, use_dir, diff_rad_by_sin;
+  float pos_iou_thr[RPC_HEAD_MAX_SIZES], neg_iou_thr[RPC_HEAD_MAX_SIZES], min_pos_iou[RPC_HEAD_MAX_SIZES];
+  float dir_offset, dir_limit_offset, pos_weight;
+  float beta, gamma, alpha;           /* SmoothL1 beta, focal gamma / alpha */
+  float lw_cls, lw_bbox, lw_dir;      /* loss weights */
+  int z_bf16;
+  long long z_sb, z_shw, z_sn;
+  int dz_bf16;
+  long long dz_sb, dz_shw, dz_sn;
+  int dz_nwrite;                      /* channels written per cell in dz (>= N; extra ones zeroed) */
+} RpcHeadCfg;
+
+size_t rpc_anchor_head_workspace_size(const RpcHeadCfg* cfg, int max_gts);
+int rpc_anchor_head_loss_forward(const RpcHeadCfg* cfg, const float* anchor_tab, const float* gt_boxes,
+                                 const long long* gt_labels, int max_gts, const void* z, const float* bias,
+                                 int* assigned, float* losses, void* workspace, size_t ws_bytes, void* stream);
+/* d(losses)/dz scaled by grad_losses[3] (device fp32: upstream grads of loss_cls/bbox/dir), written
+ * through the dz_* strides; dbias [N] (optional) = sum over cells of dz (fixed-order reduction). */
+int rpc_anchor_head_loss_backward(const RpcHeadCfg* cfg, const float* anchor_tab, const float* gt_boxes,
+                                  int max_gts, const void* z, const float* bias, const int* assigned,
+                                  const float* grad_losses, const float* losses, void* dz, float* dbias,
+                                  void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,20 @@ class PerturberCfg(C.Structure):
                 ("bn_momentum", C.c_float), ("vfe_features", C.c_int)]
 
 
+class RpcHeadCfg(C.Structure):
+    """include/rpc_hip.h RpcHeadCfg (field order and types must match)."""
+    _fields_ = [("B", C.c_int), ("H", C.c_int), ("W", C.c_int), ("S", C.c_int), ("R", C.c_int), ("C", C.c_int),
+                ("NA", C.c_int), ("assigner_per_size", C.c_int), ("assign_per_class", C.c_int),
+                ("use_dir", C.c_int), ("diff_rad_by_sin", C.c_int),
+                ("pos_iou_thr", C.c_float * 4), ("neg_iou_thr", C.c_float * 4), ("min_pos_iou", C.c_float * 4),
+                ("dir_offset", C.c_float), ("dir_limit_offset", C.c_float), ("pos_weight", C.c_float),
+                ("beta", C.c_float), ("gamma", C.c_float), ("alpha", C.c_float),
+                ("lw_cls", C.c_float), ("lw_bbox", C.c_float), ("lw_dir", C.c_float),
+                ("z_bf16", C.c_int), ("z_sb", C.c_longlong), ("z_shw", C.c_longlong), ("z_sn", C.c_longlong),
+                ("dz_bf16", C.c_int), ("dz_sb", C.c_longlong), ("dz_shw", C.c_longlong), ("dz_sn", C.c_longlong),
+                ("dz_nwrite", C.c_int)]
+
+
 # name -> (restype, argtypes); every symbol here must be exported by the .so
 SIGNATURES = {
     "rpc_version": (C.c_char_p, []),
@@ -74,6 +88,10 @@ SIGNATURES = {
     "rpc_dense_bnbwd_stats": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp]),
     "rpc_dense_bnbwd_apply": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
     "rpc_dense_wprep": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "rpc_anchor_head_workspace_size": (sz, [C.POINTER(RpcHeadCfg), i32]),
+    "rpc_anchor_head_loss_forward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
+    "rpc_anchor_head_loss_backward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,
+                                            sz, vp]),
 }
 
 

@@ -54,6 +54,26 @@ __device__ __forceinline__ bool last_block_arrive(unsigned* ticket, int* lds_fla
   return *lds_flag != 0;
 }
 
+// The same hand-off for a grid of `nblocks` blocks in any shape.
+__device__ __forceinline__ bool last_block_arrive_2d(unsigned* ticket, int* lds_flag, int nblocks) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (t == (unsigned)nblocks - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    *lds_flag = last;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+
 // Fixed-order reduction of split-K slabs: dW[e] = sum_c part[c * total + e] (c ascending within
 // each of 4 interleaved lanes, lanes combined 0..3), in double. Block = 64 outputs x 4 lanes,
 // each lane with 4 loads in flight -> deterministic and latency-tolerant.

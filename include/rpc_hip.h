@@ -283,6 +283,41 @@ int rpc_anchor_head_loss_backward(const RpcHeadCfg* cfg, const float* anchor_tab
                                   const float* grad_losses, const float* losses, void* dz, float* dbias,
                                   void* workspace, size_t ws_bytes, void* stream);
 
+
+/* ------------------------------------------------------------------ a9 / a10 step tail
+ * Loss combination of AdversarialVoxelNet.loss for upstream's list-valued head losses
+ * (models/detectors/adversarial_voxelnet.py:187-421: det_loss_total = 0, so
+ * loss_adversarial = 0.01*(loss_intensity+loss_bias+loss_imbalance), :378-413) followed by mmengine
+ * parse_losses. head_losses (device fp32 [3]) = loss_cls, loss_bbox, loss_dir; pert_losses [4] =
+ * VoxelPerturber (l2_norm, intensity_loss, bias_loss, imbalance_loss); reg_coef =
+ * regularization_weight * max(0.1, 1-(epoch+1)/30). out [10] = loss_cls, loss_bbox, loss_dir,
+ * loss_adversarial, loss_intensity, loss_bias, loss_imbalance, loss_l2_regularization,
+ * perturbation_l2_norm, total. Backward: grad_out [10] -> grad_head [3], grad_pert [4]. */
+int rpc_loss_tail_forward(const float* head_losses, const float* pert_losses, float reg_coef, float* out,
+                          void* stream);
+int rpc_loss_tail_backward(const float* pert_losses, float reg_coef, const float* grad_out, float* grad_head,
+                           float* grad_pert, void* stream);
+
+/* torch.nn.utils.clip_grad_norm_(max_norm) + torch.optim.AdamW step as mmengine's OptimWrapper runs
+ * them (configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:130-140),
+ * over a table of fp32 tensors (device int64 arrays of addresses; grad address 0 = no gradient:
+ * the tensor is skipped like torch does). Tensors are processed in chunks of RPC_OPTIM_CHUNK
+ * elements: chunk c covers elements [chunk_start[c], +RPC_OPTIM_CHUNK) of tensor chunk_tensor[c].
+ * norm_out (device fp32 [2]) = total grad norm, clip coefficient. The clipped gradients are used
+ * in the update and not written back. lr[group[t]] is tensor t's learning rate; steps (device fp32
+ * [ntensors], torch's state['step']) advance by one for every tensor that has a gradient, and the
+ * bias corrections 1 - beta^step are formed per tensor. */
+#define RPC_OPTIM_CHUNK 16384
+typedef struct {
+  float lr[4];
+  float beta1, beta2, eps, weight_decay;
+} RpcAdamWHyper;
+size_t rpc_clip_adamw_workspace_size(int nchunks);
+int rpc_clip_adamw(const long long* param_ptrs, const long long* grad_ptrs, const long long* exp_avg_ptrs,
+                   const long long* exp_avg_sq_ptrs, const int* numel, const int* group, const int* chunk_tensor,
+                   const int* chunk_start, int nchunks, int ntensors, float* steps, const RpcAdamWHyper* hyper,
+                   float max_norm, float* norm_out, void* workspace, size_t ws_bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

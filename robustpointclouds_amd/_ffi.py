@@ -46,6 +46,11 @@ class RpcHeadCfg(C.Structure):
                 ("dz_nwrite", C.c_int)]
 
 
+class RpcAdamWHyper(C.Structure):
+    _fields_ = [("lr", C.c_float * 4), ("beta1", C.c_float), ("beta2", C.c_float), ("eps", C.c_float),
+                ("weight_decay", C.c_float)]
+
+
 # name -> (restype, argtypes); every symbol here must be exported by the .so
 SIGNATURES = {
     "rpc_version": (C.c_char_p, []),
@@ -88,6 +93,11 @@ SIGNATURES = {
     "rpc_dense_bnbwd_stats": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp]),
     "rpc_dense_bnbwd_apply": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
     "rpc_dense_wprep": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "rpc_loss_tail_forward": (i32, [vp, vp, C.c_float, vp, vp]),
+    "rpc_loss_tail_backward": (i32, [vp, C.c_float, vp, vp, vp, vp]),
+    "rpc_clip_adamw_workspace_size": (sz, [i32]),
+    "rpc_clip_adamw": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, C.POINTER(RpcAdamWHyper), C.c_float, vp,
+                             vp, sz, vp]),
     "rpc_anchor_head_workspace_size": (sz, [C.POINTER(RpcHeadCfg), i32]),
     "rpc_anchor_head_loss_forward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
     "rpc_anchor_head_loss_backward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,

@@ -18,6 +18,59 @@ from __future__ import annotations
 
 import torch
 
+from . import _ffi
+
+_TAIL_KEYS = ("loss_cls", "loss_bbox", "loss_dir", "loss_adversarial", "loss_intensity", "loss_bias",
+              "loss_imbalance", "loss_l2_regularization", "perturbation_l2_norm")
+
+
+class FusedLosses(dict):
+    """Loss dict whose entries are views of one device vector; `.total` is parse_losses' sum."""
+    total = None
+
+
+class LossTailFn(torch.autograd.Function):
+    """(head [3], perturber [4]) -> out [10] (csrc/step_tail.hip, rpc_loss_tail_forward/backward)."""
+
+    @staticmethod
+    def forward(ctx, head3, pert4, reg_coef):
+        lib = _ffi.load()
+        head3, pert4 = head3.detach().float().contiguous(), pert4.detach().float().contiguous()
+        out = torch.empty(10, dtype=torch.float32, device=head3.device)
+        _ffi.check(lib.rpc_loss_tail_forward(_ffi.ptr(head3), _ffi.ptr(pert4), float(reg_coef), _ffi.ptr(out),
+                                             _ffi.stream_of(out)), "rpc_loss_tail_forward")
+        ctx.save_for_backward(pert4)
+        ctx.reg_coef = float(reg_coef)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _ffi.load()
+        (pert4,) = ctx.saved_tensors
+        g = g.float().contiguous()
+        gh = torch.empty(3, dtype=torch.float32, device=g.device)
+        gp = torch.empty(4, dtype=torch.float32, device=g.device)
+        _ffi.check(lib.rpc_loss_tail_backward(_ffi.ptr(pert4), ctx.reg_coef, _ffi.ptr(g), _ffi.ptr(gh), _ffi.ptr(gp),
+                                              _ffi.stream_of(g)), "rpc_loss_tail_backward")
+        return gh, gp, None
+
+
+def _fused_tail(losses_pts, loss_dict, epoch, regularization_weight):
+    """The HIP tail when the head losses are upstream's lists (det_loss_total = 0) of one packed
+    [cls, bbox, dir] vector and the perturber losses one packed [4] vector, all on the GPU."""
+    head3 = getattr(losses_pts, "packed", None)
+    pert4 = getattr(loss_dict, "packed", None)
+    if head3 is None or pert4 is None or not head3.is_cuda or set(losses_pts) != {"loss_cls", "loss_bbox", "loss_dir"}:
+        return None
+    reg_scale = max(0.1, 1.0 - ((epoch + 1) / 30.0))
+    out = LossTailFn.apply(head3, pert4, float(regularization_weight * reg_scale))
+    res = FusedLosses()
+    for i, k in enumerate(_TAIL_KEYS):
+        v = out[i]
+        res[k] = [v] if i < 3 else (v.detach() if k == "perturbation_l2_norm" else v)
+    res.total = out[9]
+    return res
+
 
 def _zero(device):
     return torch.tensor(0.0, device=device, requires_grad=True)
@@ -30,6 +83,9 @@ def combine_adversarial_losses(losses_pts: dict, l2, loss_dict, epoch: int, regu
         losses["loss_adversarial"] = _zero(device)
         losses["loss_l2_regularization"] = _zero(device)
         return losses
+    fused = _fused_tail(losses_pts, loss_dict, epoch, regularization_weight) if loss_dict is not None else None
+    if fused is not None:
+        return fused
     tensor_items = [v for k, v in losses_pts.items() if "loss" in k and isinstance(v, torch.Tensor)]
     if tensor_items:
         det = torch.zeros((), device=device)
@@ -68,7 +124,11 @@ def combine_adversarial_losses(losses_pts: dict, l2, loss_dict, epoch: int, regu
 
 def parse_losses(losses: dict):
     """mmengine BaseModel.parse_losses: total = sum of means of every key containing 'loss'
-    (lists: sum of their means); returns (total, log_vars)."""
+    (lists: sum of their means); returns (total, log_vars). A FusedLosses dict already holds the
+    total (same sum, same order, computed in the loss-tail kernel)."""
+    if isinstance(losses, FusedLosses):
+        log_vars = {k: (v[0] if isinstance(v, list) else v) for k, v in losses.items()}
+        return losses.total, dict(loss=losses.total, **log_vars)
     log_vars = {}
     for k, v in losses.items():
         if isinstance(v, torch.Tensor):

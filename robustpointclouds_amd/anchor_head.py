@@ -229,6 +229,11 @@ class HeadLossFn(torch.autograd.Function):
         return dz, db, None, None, None, None
 
 
+class HeadLosses(dict):
+    """upstream's dict of lists; `.packed` is the device [3] vector the entries view."""
+    packed = None
+
+
 class Anchor3DHead(nn.Module):
     def __init__(self, num_classes, in_channels, feat_channels=256, use_direction_classifier=True,
                  anchor_generator=dict(type="Anchor3DRangeGenerator", range=[0, -39.68, -1.78, 69.12, 39.68, -1.78],
@@ -364,9 +369,10 @@ class Anchor3DHead(nn.Module):
         """dict of LISTS like upstream loss_by_feat (one feature level)."""
         l3, asg, npos = HeadLossFn.apply(z, bias, self, lay, gt_boxes, gt_labels)
         self._last_assigned, self._last_num_total_pos = asg, npos
-        out = dict(loss_cls=[l3[0]], loss_bbox=[l3[1]])
+        out = HeadLosses(loss_cls=[l3[0]], loss_bbox=[l3[1]])
         if self.use_direction_classifier:
             out["loss_dir"] = [l3[2]]
+            out.packed = l3   # [loss_cls, loss_bbox, loss_dir] on the device (fused loss tail)
         return out
 
     def loss(self, x, batch_data_samples):

@@ -32,6 +32,11 @@ from ..builder import ADVERSARIES
 _HIST_CAP = 1 << 16
 
 
+class PackedLosses(dict):
+    """The reference's loss dict; `.packed` is the device vector its entries are views of."""
+    packed = None
+
+
 @ADVERSARIES.register_module(force=True)
 class VoxelPerturber(nn.Module):
     def __init__(self, sensor_error_bound: float = 0.2, voxel_size: list = [0.05, 0.05, 0.1],
@@ -147,7 +152,9 @@ class VoxelPerturber(nn.Module):
 
     @staticmethod
     def _loss_dict(lvec):
-        return {"l2_norm": lvec[0], "intensity_loss": lvec[1], "bias_loss": lvec[2], "imbalance_loss": lvec[3]}
+        d = PackedLosses(l2_norm=lvec[0], intensity_loss=lvec[1], bias_loss=lvec[2], imbalance_loss=lvec[3])
+        d.packed = lvec   # the [4] device vector the entries view (the fused loss tail reads it)
+        return d
 
     # ------------------------------------------------------------------ forward
     def forward(self, voxel_features: torch.Tensor) -> Tuple[torch.Tensor, dict]:

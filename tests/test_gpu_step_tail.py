@@ -1,0 +1,93 @@
+"""Rows a9 / a10 on the HIP step-tail kernels (csrc/step_tail.hip).
+
+* Loss tail: LossTailFn (fused combination + parse_losses) against the torch restatement of
+  AdversarialVoxelNet.loss's combination (adversarial_loss.combine_adversarial_losses, itself pinned
+  to the reference's golden fixtures on CPU) on the same device scalars: values bit-exact or within
+  1 ulp, gradients within 1e-6 relative, for each l2 multiplier tier and epochs 3 / 7 / 40.
+* ClipAdamW: clip_grad_norm_(0.5) + torch.optim.AdamW (two groups, lr_mult 2.0, a parameter
+  without gradient, odd sizes) over three steps, parameters and norms within 1e-6 relative.
+"""
+import pytest
+import torch
+
+from robustpointclouds_amd.adversarial_loss import FusedLosses, combine_adversarial_losses, parse_losses
+from robustpointclouds_amd.anchor_head import HeadLosses
+from robustpointclouds_amd.optim import ClipAdamW
+from robustpointclouds_amd.plugin.models.adversarial.voxel_perturber import PackedLosses
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _inputs(l2):
+    h = torch.tensor([0.71, 0.33, 0.12], device=DEV, requires_grad=True)
+    p = torch.tensor([l2, 0.05, 0.002, 0.013], device=DEV, requires_grad=True)
+    return h, p
+
+
+def _head_dict(h):
+    d = HeadLosses(loss_cls=[h[0]], loss_bbox=[h[1]], loss_dir=[h[2]])
+    d.packed = h
+    return d
+
+
+def _pert_dict(p):
+    d = PackedLosses(l2_norm=p[0], intensity_loss=p[1], bias_loss=p[2], imbalance_loss=p[3])
+    d.packed = p
+    return d
+
+
+@pytest.mark.parametrize("l2", [0.0005, 0.003, 0.007, 0.4])
+@pytest.mark.parametrize("epoch", [3, 7, 40])
+def test_loss_tail_matches_torch_combination(l2, epoch):
+    h, p = _inputs(l2)
+    fused = combine_adversarial_losses(_head_dict(h), p[0], _pert_dict(p), epoch, 0.05, True, DEV)
+    assert isinstance(fused, FusedLosses)
+    tot_f, log_f = parse_losses(fused)
+    tot_f.backward()
+    gh_f, gp_f = h.grad.clone(), p.grad.clone()
+    h2, p2 = _inputs(l2)
+    ref = combine_adversarial_losses(dict(loss_cls=[h2[0]], loss_bbox=[h2[1]], loss_dir=[h2[2]]), p2[0],
+                                     dict(l2_norm=p2[0], intensity_loss=p2[1], bias_loss=p2[2], imbalance_loss=p2[3]),
+                                     epoch, 0.05, True, DEV)
+    assert not isinstance(ref, FusedLosses)
+    tot_r, log_r = parse_losses(ref)
+    tot_r.backward()
+    assert list(log_f) == list(log_r)
+    for k in log_r:
+        torch.testing.assert_close(log_f[k].detach(), log_r[k].detach(), rtol=2e-7, atol=0)
+    torch.testing.assert_close(gh_f, h2.grad, rtol=1e-6, atol=0)
+    torch.testing.assert_close(gp_f, p2.grad, rtol=1e-6, atol=0)
+
+
+def _params(seed):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(64, 4), (64,), (1000, 37), (3,), (16385,), (128, 128, 3, 3), (5, 7)]
+    return [torch.nn.Parameter((torch.randn(s, generator=g) * 0.1).to(DEV)) for s in shapes]
+
+
+@pytest.mark.parametrize("max_norm", [0.5, 100.0])
+def test_clip_adamw_matches_torch(max_norm):
+    pa, pb = _params(0), _params(0)
+    groups = lambda ps: [dict(params=ps[:4], lr=1e-3, initial_lr=1e-3), dict(params=ps[4:], lr=2e-3, initial_lr=2e-3)]
+    ours = ClipAdamW(groups(pa), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-3, max_norm=max_norm)
+    ref = torch.optim.AdamW(groups(pb), lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-3)
+    g = torch.Generator().manual_seed(1)
+    for step in range(3):
+        grads = [torch.randn(p.shape, generator=g) * (0.05 if i != 2 else 2.0) for i, p in enumerate(pa)]
+        for i, (x, y, gr) in enumerate(zip(pa, pb, grads)):
+            if i == 6 and step == 1:   # no gradient this step: skipped (no decay, no step count)
+                x.grad = y.grad = None
+                continue
+            x.grad = gr.to(DEV)
+            y.grad = gr.to(DEV).clone()
+        norm = ours.step()
+        rn = torch.nn.utils.clip_grad_norm_(pb, max_norm)
+        ref.step()
+        torch.testing.assert_close(norm[0], rn, rtol=1e-6, atol=0)
+        for x, y in zip(pa, pb):
+            torch.testing.assert_close(x.detach(), y.detach(), rtol=2e-6, atol=1e-8)
+        ours.zero_grad()
+        ref.zero_grad()
+    sd = ours.state_dict()
+    assert float(sd["state"][6]["step"]) == 2.0 and float(sd["state"][0]["step"]) == 3.0

@@ -129,6 +129,14 @@ def load():
     return _lib
 
 
+def bump_batches(bns) -> None:
+    """num_batches_tracked += 1 for a list of BatchNorm modules: one multi-tensor kernel instead of one
+    add kernel (and one Module.__setattr__ / register_buffer round trip) per module."""
+    ts = [m.num_batches_tracked for m in bns if getattr(m, "num_batches_tracked", None) is not None]
+    if ts:
+        torch._foreach_add_(ts, 1)
+
+
 def check(rc: int, what: str) -> None:
     if rc != 0:
         raise RuntimeError(f"{what} failed: rpc error {rc} ({RPC_ERRORS.get(rc, '?')})")

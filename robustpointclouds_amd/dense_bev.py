@@ -141,7 +141,6 @@ def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
                                        _ffi.ptr(bnm.bias), float(bnm.eps), float(bnm.momentum),
                                        _ffi.ptr(bnm.running_mean), _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn),
                                        None, None, _ffi.ptr(wsb), st), "rpc_bn_finalize")
-        bnm.num_batches_tracked += 1
     else:
         bn = _bn_eval(bnm, dev)
     if out is None:
@@ -253,6 +252,8 @@ class BackboneFn(torch.autograd.Function):
                 brecs.append(rec)
             recs.append(brecs)
             outs.append(h)
+        if mod.training:
+            _ffi.bump_batches([L.bnm for b in blocks for L in b])
         ctx.recs = recs
         ctx.param_list = params
         return tuple(outs)
@@ -322,6 +323,8 @@ class NeckFn(torch.autograd.Function):
             rec["off"] = off
             recs.append(rec)
             off += L.co
+        if mod.training:
+            _ffi.bump_batches([L.bnm for L in layers])
         ctx.recs = recs
         ctx.Ctot = Ctot
         ctx.param_list = params

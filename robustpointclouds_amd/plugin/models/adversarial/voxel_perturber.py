@@ -25,6 +25,7 @@ from typing import Tuple
 import torch
 from torch import nn
 
+from robustpointclouds_amd import _ffi
 from robustpointclouds_amd import perturb as _P
 
 from ..builder import ADVERSARIES
@@ -146,9 +147,7 @@ class VoxelPerturber(nn.Module):
 
     def _bump_batch_counts(self):
         if self.training:
-            for m in self.model:
-                if isinstance(m, nn.BatchNorm1d):
-                    m.num_batches_tracked += 1
+            _ffi.bump_batches([m for m in self.model if isinstance(m, nn.BatchNorm1d)])
 
     @staticmethod
     def _loss_dict(lvec):

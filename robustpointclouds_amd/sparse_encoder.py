@@ -294,7 +294,6 @@ class SparseEncoderFn(torch.autograd.Function):
                                            float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
                                            _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
                                            _ffi.ptr(wsb), st), "rpc_bn_finalize")
-            bnm.num_batches_tracked += 1
             rec.update(z=z, bn=bn, W=W, gamma=gamma, beta=beta)
             L.append(rec)
             src, src_bn = z, bn
@@ -303,6 +302,7 @@ class SparseEncoderFn(torch.autograd.Function):
                 _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(z), _ffi.ptr(bn), n_out, sp.co, 1, _ffi.ptr(hsrc), st),
                            "rpc_to_bf16_rows")
             cur_coors, cur_n = rec["coors_out"], n_out
+        _ffi.bump_batches([m[1] for m in mods])
         last = L[-1]
         D, H, Wd = enc.shapes[-1]
         C = last["spec"].co

@@ -125,7 +125,8 @@ class Trainer:
     def train_step(self, points, gt):
         """points: list of [Ni, 4] cuda tensors; gt: dict(gt_boxes [B, M, 7], gt_labels [B, M])."""
         m = self.module
-        m.train()
+        if not m.training:
+            m.train()
         batch = m.data_preprocessor(dict(inputs=dict(points=points)), training=True)["inputs"]
         batch["batch_size"] = len(points)
         return self.step_batch(batch, gt)
@@ -134,7 +135,8 @@ class Trainer:
         """The step after voxelisation: loss -> parse_losses -> backward (DDP all-reduce) -> clip
         -> AdamW -> hooks. batch: dict(voxels=dict(voxels, num_points, coors), batch_size)."""
         m = self.module
-        m.train()
+        if not m.training:   # Module.train() walks every submodule (~1 ms of host time)
+            m.train()
         self.sched.set(self.iter)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.bf16):
             if isinstance(self.model, torch.nn.parallel.DistributedDataParallel):

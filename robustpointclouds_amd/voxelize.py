@@ -19,10 +19,15 @@ from . import _ffi
 
 
 def _frame_offsets(sizes: Sequence[int], device) -> torch.Tensor:
+    """[B+1] int32 prefix offsets on `device`, uploaded from pinned memory without blocking the host
+    (a pageable torch.tensor(..., device=cuda) would wait for the whole stream to drain)."""
     off = [0]
     for n in sizes:
         off.append(off[-1] + int(n))
-    return torch.tensor(off, dtype=torch.int32, device=device)
+    host = torch.tensor(off, dtype=torch.int32)
+    if torch.device(device).type != "cuda":
+        return host
+    return host.pin_memory().to(device, non_blocking=True)
 
 
 def voxelize_batch(points: torch.Tensor, frame_offsets: torch.Tensor, voxel_size, point_cloud_range,

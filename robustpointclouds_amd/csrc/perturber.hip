@@ -31,7 +31,9 @@ namespace pert {
 
 constexpr int BLK = 256;
 constexpr int NWAVE = BLK / 64;
-constexpr int GRID = 256;        // blocks of every per-point pass (= partial rows)
+constexpr int GRID = 256;        // blocks of every per-point VALU pass (= partial rows)
+constexpr int MFW = 12;          // waves per block of the MFMA hidden-layer passes: 256 blocks x 12
+constexpr int MFBLK = MFW * 64;  // waves = 3 waves per SIMD on 256 CUs (168 VGPRs), GRID partial rows
 constexpr int MAXF = 8;
 constexpr int MAXC = 128;
 constexpr int NTICKET = 16;
@@ -123,9 +125,15 @@ struct ChanAcc {
 
 // thread j < 2C: fixed-order sum of column j over all blocks' partial rows
 __device__ __forceinline__ double col_total(const double* part, int j) {
-  double t = 0.0;
-  for (int r = 0; r < GRID; ++r) t += part[(size_t)r * 2 * MAXC + j];
-  return t;
+  // 8 independent partial sums keep 8 loads in flight; combined in a fixed order (deterministic)
+  const int R = (int)gridDim.x;
+  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  int r = 0;
+  for (; r + 8 <= R; r += 8)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) a[k] += part[(size_t)(r + k) * 2 * MAXC + j];
+  for (; r < R; ++r) a[0] += part[(size_t)r * 2 * MAXC + j];
+  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
 }
 
 // finalize a BatchNorm layer from its batch sums (train) — run by the last block
@@ -781,8 +789,14 @@ __global__ __launch_bounds__(BLK) void k_wgrad_reduce(Dev d, Jobs J, GradOut G) 
     while (jb + 1 < J.njob && e >= J.j[jb + 1].eoff) ++jb;
     const Job& job = J.j[jb];
     int le = e - job.eoff;
-    double s = 0.0;
-    for (int k = 0; k < J.KS; ++k) s += d.wpart[(size_t)k * J.total + e];
+    // 8 independent partial sums (8 loads in flight), combined in a fixed order
+    double q[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int k = 0;
+    for (; k + 8 <= J.KS; k += 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] += d.wpart[(size_t)(k + u) * J.total + e];
+    for (; k < J.KS; ++k) q[0] += d.wpart[(size_t)k * J.total + e];
+    const double s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
     float g = flag ? 0.0f : grad_hook((float)s);
     int CI1 = job.CI + 1, o = le / CI1, i = le - o * CI1;
     if (i < job.CI) { if (G.W[jb]) G.W[jb][o * job.CI + i] = g; }
@@ -803,8 +817,302 @@ __global__ __launch_bounds__(BLK) void k_wgrad_reduce(Dev d, Jobs J, GradOut G) 
   }
 }
 
+
+// ------------------------------------------------------------------ fp32 MFMA hidden layers
+// The hidden Linear layers as 16-point x 16-channel v_mfma_f32_16x16x4_f32 tiles (fp32 operands,
+// fp32 accumulation — the reference arithmetic, only the summation order differs). One wave owns a
+// 16-point tile: A = activations (lane: point l&15, channel 4s + l>>4, loaded from the channel-major
+// [C][S] buffers — 64 contiguous bytes per channel), B = weights from LDS (pitch chosen so the 64
+// lanes hit 64 distinct banks), D = 4 consecutive points x 1 channel per lane, stored as one
+// 16-byte vector per channel row. BatchNorm batch sums are reduced across the 4 lane groups with two
+// shuffles per tile and kept in double, then combined in fixed order like the VALU kernels.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__host__ __device__ constexpr int pitch_mod(int ci, int m) { return ci + ((m - ci % 64) + 64) % 64; }
+
+__device__ __forceinline__ float grp_sum(float v) {  // sum over the 4 lanes sharing l&15
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+// per-channel sums of a 16-channel tile column: lanes with l>>4 == 0 write wave partials
+template <int C>
+__device__ __forceinline__ void tile_flush(const double (&s1)[C / 16], const double (&s2)[C / 16], double* part,
+                                           double* lds) {  // lds: [MFW][2][MAXC]
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < C / 16; ++j) {
+      lds[(w * 2 + 0) * MAXC + 16 * j + lane] = s1[j];
+      lds[(w * 2 + 1) * MAXC + 16 * j + lane] = s2[j];
+    }
+  }
+  __syncthreads();
+  for (int j = threadIdx.x; j < 2 * C; j += MFBLK) {
+    int which = j / C, c = j - which * C;
+    double t = 0.0;
+    for (int ww = 0; ww < MFW; ++ww) t += lds[(ww * 2 + which) * MAXC + c];
+    part[(size_t)blockIdx.x * 2 * MAXC + j] = t;
+  }
+}
+
+// 4 consecutive points n..n+3 of one channel row (n % 4 == 0, S % 16 == 0): vector or masked
+__device__ __forceinline__ f32x4 ld4(const float* p, int n, int N) {
+  if (n + 3 < N) return *(const f32x4*)(p + n);
+  f32x4 v;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) v[i] = n + i < N ? p[n + i] : 0.0f;
+  return v;
+}
+__device__ __forceinline__ void st4(float* p, int n, int N, f32x4 v) {
+  if (n + 3 < N) {
+    *(f32x4*)(p + n) = v;
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (n + i < N) p[n + i] = v[i];
+}
+
+// layer l (1..4) forward: z_l = W_l relu(bn_{l-1}(z_{l-1})) + b_l, BN_l batch statistics
+template <int CI, int CO>
+__global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
+  constexpr int P = pitch_mod(CI, 4), NT = CO / 16, KS = CI / 4;
+  __shared__ float sW[CO * P];
+  __shared__ float sp[3 * CI + CO];
+  __shared__ double lds[MFW * 2 * MAXC];
+  __shared__ int lastf;
+  for (int j = threadIdx.x; j < CO * CI; j += MFBLK) sW[(j / CI) * P + j % CI] = d.W[l][j];
+  for (int j = threadIdx.x; j < 3 * CI; j += MFBLK) sp[j] = d.bn[l - 1][j];
+  for (int j = threadIdx.x; j < CO; j += MFBLK) sp[3 * CI + j] = d.b[l][j];
+  __syncthreads();
+  const float* sc = sp;
+  const float* sh = sp + CI;
+  const float* mu = sp + 2 * CI;
+  const float* bias = sp + 3 * CI;
+  const int N = d.meta[0];
+  const int lane = threadIdx.x & 63, a = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const float* zin = d.z[l - 1];
+  float* zout = d.z[l];
+  double s1[NT], s2[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) s1[j] = s2[j] = 0.0;
+  for (int t = blockIdx.x * MFW + wv; t * 16 < N; t += GRID * MFW) {
+    const int n0 = t * 16, na = n0 + a;
+    const bool va = na < N;
+    float hv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int c = 4 * s + g;
+      const float zv = va ? zin[(size_t)c * d.S + na] : 0.0f;
+      hv[s] = va ? fmaxf(fmaf(zv - mu[c], sc[c], sh[c]), 0.0f) : 0.0f;
+    }
+    const int nb = n0 + 4 * g;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const float b = bias[16 * j + a];
+      f32x4 v = (f32x4){b, b, b, b};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        v = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s], sW[(16 * j + a) * P + 4 * s + g], v, 0, 0, 0);
+      float t1 = 0.0f, t2 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (nb + i >= N) v[i] = 0.0f;
+        t1 += v[i];
+        t2 = fmaf(v[i], v[i], t2);
+      }
+      st4(zout + (size_t)(16 * j + a) * d.S, nb, N, v);
+      if (d.training) {
+        s1[j] += (double)grp_sum(t1);
+        s2[j] += (double)grp_sum(t2);
+      }
+      asm volatile("" ::: "memory");  // keep the next tile's B reads here (register pressure)
+    }
+  }
+  if (!d.training) return;
+  tile_flush<CO>(s1, s2, d.part, lds);
+  if (!last_block_arrive(d.ticket + 1 + l, &lastf)) return;
+  bn_finalize<CO>(d, l, lds);
+}
+
+// layer l (4..1) backward: dz_l = BN_l backward of dh_l (stored), dh_{l-1} = relu'(h_{l-1}) W_l^T dz_l,
+// BN_{l-1} backward sums (sum dh, sum dh * xhat)
+template <int CI, int CO>
+__global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
+  constexpr int P = pitch_mod(CI, 16), NT = CI / 16, KS = CO / 4;
+  __shared__ float sW[CO * P];
+  __shared__ float sp[7 * CO + 4 * CI];
+  __shared__ double lds[MFW * 2 * MAXC];
+  __shared__ int lastf;
+  const int N = d.meta[0];
+  const double invN = 1.0 / N;
+  for (int j = threadIdx.x; j < CO * CI; j += MFBLK) sW[(j / CI) * P + j % CI] = d.W[l][j];
+  for (int j = threadIdx.x; j < 4 * CO; j += MFBLK) sp[j] = d.bn[l][j];
+  for (int j = threadIdx.x; j < 4 * CI; j += MFBLK) sp[4 * CO + j] = d.bn[l - 1][j];
+  for (int j = threadIdx.x; j < CO; j += MFBLK) {
+    float* m = sp + 4 * CO + 4 * CI;
+    m[j] = (float)(d.bnsum[l][j] * invN);
+    m[CO + j] = (float)(d.bnsum[l][CO + j] * invN);
+    m[2 * CO + j] = d.g[l][j] * d.bn[l][3 * CO + j];
+  }
+  __syncthreads();
+  const float* bo = sp;            // scale, beta, mean, invstd of layer l
+  const float* bi = sp + 4 * CO;   // of layer l-1
+  const float* m1 = bi + 4 * CI;
+  const float* m2 = m1 + CO;
+  const float* gi = m2 + CO;
+  const int lane = threadIdx.x & 63, a = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const float* dhin = d.dh[src];
+  float* dhout = d.dh[src ^ 1];
+  const float* zl = d.z[l];
+  const float* zp = d.z[l - 1];
+  float* dzl = d.dz[l];
+  double s1[NT], s2[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) s1[j] = s2[j] = 0.0;
+  for (int t = blockIdx.x * MFW + wv; t * 16 < N; t += GRID * MFW) {
+    const int n0 = t * 16, na = n0 + a;
+    const bool va = na < N;
+    float dzv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int o = 4 * s + g;
+      float v = 0.0f;
+      if (va) {
+        const float xh = (zl[(size_t)o * d.S + na] - bo[2 * CO + o]) * bo[3 * CO + o];
+        v = gi[o] * (dhin[(size_t)o * d.S + na] - m1[o] - xh * m2[o]);
+        dzl[(size_t)o * d.S + na] = v;
+      }
+      dzv[s] = v;
+    }
+    const int nb = n0 + 4 * g;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      f32x4 v = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s)
+        v = __builtin_amdgcn_mfma_f32_16x16x4f32(dzv[s], sW[(4 * s + g) * P + 16 * j + a], v, 0, 0, 0);
+      const int c = 16 * j + a;
+      const f32x4 zc = ld4(zp + (size_t)c * d.S, nb, N);
+      float t1 = 0.0f, t2 = 0.0f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float hv = fmaxf(fmaf(zc[i] - bi[2 * CI + c], bi[c], bi[CI + c]), 0.0f);
+        v[i] = (nb + i < N && hv > 0.0f) ? v[i] : 0.0f;
+        t1 += v[i];
+        t2 += v[i] * ((zc[i] - bi[2 * CI + c]) * bi[3 * CI + c]);
+      }
+      st4(dhout + (size_t)c * d.S, nb, N, v);
+      s1[j] += (double)grp_sum(t1);
+      s2[j] += (double)grp_sum(t2);
+      asm volatile("" ::: "memory");  // keep the next tile's B reads here (register pressure)
+    }
+  }
+  tile_flush<CI>(s1, s2, d.part, lds);
+  if (!last_block_arrive(d.ticket + 7 + (5 - l), &lastf)) return;
+  bnb_finalize<CI>(d, l - 1, lds);
+}
+
+// weight gradient of a hidden layer: dW[o][c] = sum_n dz_l[o][n] h_{l-1}[c][n], db[o] = sum_n dz_l[o][n],
+// h = relu(bn_{l-1}(z_{l-1})). K = points: lane k-slot j of a 16-point block holds point 4(l>>4) + j,
+// one 16-byte load per channel row for A and B alike. grid (KS row chunks, jobs): the 4 waves take
+// interleaved 16-point blocks of the chunk and are combined in LDS in wave order; one slab row of
+// the job's CO*(CI+1) elements per block (reduced with the VALU jobs by k_wgrad_reduce).
+struct MfJob {
+  const float* dz;  // [CO][S]
+  const float* z;   // z_{l-1} [CI][S]
+  const float* bn;  // scale, beta, mean of layer l-1
+  int eoff;
+};
+struct MfJobs {
+  MfJob j[4];
+  int total, KS;
+};
+
+template <int CO, int CI>
+__global__ __launch_bounds__(BLK) void k_wgrad_mf(Dev d, MfJobs J) {
+  constexpr int TOB = 1, TC = CI / 16;   // o-tiles per block (blockIdx.z picks them)
+  __shared__ float red[NWAVE][64];
+  const MfJob& job = J.j[blockIdx.y];
+  const int ot0 = blockIdx.z * TOB;
+  const int N = d.meta[0];
+  const int rows_per = ((N + J.KS - 1) / J.KS + 15) & ~15;
+  const int r0 = blockIdx.x * rows_per, r1 = min(N, r0 + rows_per);
+  const int lane = threadIdx.x & 63, a = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  float sc[TC], sh[TC], mu[TC];
+#pragma unroll
+  for (int jc = 0; jc < TC; ++jc) {
+    const int c = 16 * jc + a;
+    sc[jc] = job.bn[c];
+    sh[jc] = job.bn[CI + c];
+    mu[jc] = job.bn[2 * CI + c];
+  }
+  f32x4 acc[TOB][TC];
+  float bsum[TOB];
+#pragma unroll
+  for (int i = 0; i < TOB; ++i) {
+    bsum[i] = 0.0f;
+#pragma unroll
+    for (int jc = 0; jc < TC; ++jc) acc[i][jc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  for (int n0 = r0 + 16 * wv; n0 < r1; n0 += 16 * NWAVE) {
+    const int nb = n0 + 4 * g;
+    f32x4 av[TOB], bv[TC];
+#pragma unroll
+    for (int i = 0; i < TOB; ++i) {
+      av[i] = ld4(job.dz + (size_t)(16 * (ot0 + i) + a) * d.S, nb, r1);
+      bsum[i] += (av[i][0] + av[i][1]) + (av[i][2] + av[i][3]);
+    }
+#pragma unroll
+    for (int jc = 0; jc < TC; ++jc) {
+      const f32x4 zc = ld4(job.z + (size_t)(16 * jc + a) * d.S, nb, r1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) bv[jc][i] = nb + i < r1 ? fmaxf(fmaf(zc[i] - mu[jc], sc[jc], sh[jc]), 0.0f) : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < TOB; ++i)
+#pragma unroll
+      for (int jc = 0; jc < TC; ++jc)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][k], bv[jc][k], acc[i][jc], 0, 0, 0);
+  }
+  // combine the 4 waves in order; lane (a, g) of tile (i, jc) holds dW[16(ot0+i) + 4g + r][16jc + a]
+  float* out = d.wpart + (size_t)blockIdx.x * J.total + job.eoff;
+#pragma unroll
+  for (int i = 0; i < TOB; ++i) {
+#pragma unroll
+    for (int jc = 0; jc < TC; ++jc) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        red[wv][lane] = acc[i][jc][r];
+        __syncthreads();
+        if (wv == 0) {
+          const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+          const int o = 16 * (ot0 + i) + 4 * g + r, c = 16 * jc + a;
+          out[o * (CI + 1) + c] = v;
+        }
+        __syncthreads();
+      }
+    }
+    const float bt = grp_sum(bsum[i]);
+    red[wv][lane] = bt;
+    __syncthreads();
+    if (wv == 0 && g == 0)
+      out[(16 * (ot0 + i) + a) * (CI + 1) + CI] = ((red[0][a] + red[1][a]) + red[2][a]) + red[3][a];
+    __syncthreads();
+  }
+}
+
 // ------------------------------------------------------------------ host side
 static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+// channel stride of the SoA activation buffers: whole 16-point MFMA tiles, 16-byte aligned rows
+static inline size_t chan_stride(int rows, int slots) {
+  size_t n = (size_t)rows * slots;
+  return n < 16 ? 16 : (n + 15) & ~(size_t)15;
+}
 
 struct Layout {
   size_t off, list, meta, xs, z[5], bn[5], bnsum[5], part, pstat, ticket, dz[6], dh[2], dsig, da,
@@ -828,7 +1136,7 @@ struct ValidCount {
 };
 using CountIt = hipcub::TransformInputIterator<int, ValidCount, hipcub::CountingInputIterator<int>>;
 
-constexpr int KS_MAX = 64;
+constexpr int KS_MAX = 256;
 
 static int widths(const rpc_perturber_cfg* cfg, int C[7]) {
   C[0] = cfg->F;
@@ -848,8 +1156,7 @@ static int make_layout(const rpc_perturber_cfg* cfg, int rows, int slots, Layout
   int C[7];
   int rc = widths(cfg, C);
   if (rc) return rc;
-  size_t Nmax = (size_t)rows * slots;
-  if (Nmax < 1) Nmax = 1;
+  size_t Nmax = chan_stride(rows, slots);
   size_t scan_b = 0;
   ValidCount vc{nullptr, slots, cfg->F, rows};
   CountIt it(hipcub::CountingInputIterator<int>(0), vc);
@@ -925,7 +1232,7 @@ static int fill_dev(const rpc_perturber_cfg* cfg, const float* const* P, const f
   widths(cfg, d.C);
   d.rows = rows;
   d.slots = slots;
-  d.S = rows * slots;
+  d.S = (int)chan_stride(rows, slots);
   d.fused = npts != nullptr;
   d.training = cfg->training;
   d.use_att = cfg->use_attention;
@@ -999,14 +1306,22 @@ static int launch_last(int CI, Dev& d, hipStream_t st, bool bwd) {
   }
   return RPC_OK;
 }
+// hidden layer l: fp32-MFMA kernels where the tile shape fits (forward: CO % 16, backward: CI % 16),
+// the per-point VALU kernels otherwise (8-channel layers of the small configs)
+template <int CI, int CO>
+static void launch_mid_t(Dev& d, int l, hipStream_t st, bool bwd, int src) {
+  if (bwd) {
+    if constexpr (CI % 16 == 0) hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO>), dim3(GRID), dim3(MFBLK), 0, st, d, l, src);
+    else hipLaunchKernelGGL((k_bwd_mid<CI, CO>), dim3(GRID), dim3(BLK), 0, st, d, l, src);
+  } else {
+    if constexpr (CO % 16 == 0) hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
+    else hipLaunchKernelGGL((k_fwd_mid<CI, CO>), dim3(GRID), dim3(BLK), 0, st, d, l);
+  }
+}
 template <int CI>
 static int launch_mid_co(int CO, Dev& d, int l, hipStream_t st, bool bwd, int src) {
   switch (CO) {
-#define CASE(c)                                                                                \
-  case c:                                                                                      \
-    if (bwd) hipLaunchKernelGGL((k_bwd_mid<CI, c>), dim3(GRID), dim3(BLK), 0, st, d, l, src);  \
-    else hipLaunchKernelGGL((k_fwd_mid<CI, c>), dim3(GRID), dim3(BLK), 0, st, d, l);           \
-    break;
+#define CASE(c) case c: launch_mid_t<CI, c>(d, l, st, bwd, src); break;
     RPC_HID(CASE)
 #undef CASE
     default: return RPC_ERR_UNSUPPORTED;
@@ -1019,6 +1334,27 @@ static int launch_mid(int CI, int CO, Dev& d, int l, hipStream_t st, bool bwd, i
     RPC_HID(CASE)
 #undef CASE
     default: return RPC_ERR_UNSUPPORTED;
+  }
+}
+static bool wgrad_mf_ok(int CO, int CI) { return CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192; }
+template <int CO, int CI>
+static void launch_wgrad_mf_t(Dev& d, const MfJobs& M, int njob, hipStream_t st) {
+  if constexpr (CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192)
+    hipLaunchKernelGGL((k_wgrad_mf<CO, CI>), dim3(M.KS, njob, CO / 16), dim3(BLK), 0, st, d, M);
+}
+template <int CO>
+static void launch_wgrad_mf_ci(int CI, Dev& d, const MfJobs& M, int njob, hipStream_t st) {
+  switch (CI) {
+#define CASE(c) case c: launch_wgrad_mf_t<CO, c>(d, M, njob, st); break;
+    RPC_HID(CASE)
+#undef CASE
+  }
+}
+static void launch_wgrad_mf(int CO, int CI, Dev& d, const MfJobs& M, int njob, hipStream_t st) {
+  switch (CO) {
+#define CASE(c) case c: launch_wgrad_mf_ci<c>(CI, d, M, njob, st); break;
+    RPC_HID(CASE)
+#undef CASE
   }
 }
 static int launch_bwd_first(int CO, Dev& d, hipStream_t st, int src) {
@@ -1151,19 +1487,48 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
   }
   J.njob = nj;
   J.total = eoff;
+  // MFMA jobs: hidden layers 1..4 whose (CO, CI) tile; grouped by shape (one launch per shape)
+  bool is_mf[MAXJOB] = {false};
+  for (int l = 1; l < 5; ++l) is_mf[l] = wgrad_mf_ok(d.C[l + 1], d.C[l]);
+  Jobs JV;
+  memset(&JV, 0, sizeof(JV));
+  int nv = 0;
+  for (int k = 0; k < nj; ++k)
+    if (!is_mf[k]) JV.j[nv++] = J.j[k];
+  JV.njob = nv;
+  JV.total = J.total;
   int chunks = 0;
-  for (int k = 0; k < nj; ++k) {
-    J.cbase[k] = chunks;
-    J.echunks[k] = (J.j[k].nelem + BLK * EPT - 1) / (BLK * EPT);
-    chunks += J.echunks[k];
+  for (int k = 0; k < nv; ++k) {
+    JV.cbase[k] = chunks;
+    JV.echunks[k] = (JV.j[k].nelem + BLK * EPT - 1) / (BLK * EPT);
+    chunks += JV.echunks[k];
   }
-  int ks = 512 / chunks;
-  if (ks < 1) ks = 1;
+  int ks = chunks ? 1024 / chunks : KS_MAX;
+  if (ks < 128) ks = 128;
   if (ks > KS_MAX) ks = KS_MAX;
-  J.KS = ks;
-  if (F == 4) hipLaunchKernelGGL((k_wgrad<4>), dim3(chunks * ks), dim3(BLK), 0, st, d, J);
-  else hipLaunchKernelGGL((k_wgrad<5>), dim3(chunks * ks), dim3(BLK), 0, st, d, J);
-  RPC_LAUNCH_CHECK();
+  J.KS = JV.KS = ks;
+  if (nv) {
+    if (F == 4) hipLaunchKernelGGL((k_wgrad<4>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
+    else hipLaunchKernelGGL((k_wgrad<5>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
+    RPC_LAUNCH_CHECK();
+  }
+  for (int l = 1; l < 5; ++l) {
+    if (!is_mf[l]) continue;
+    bool first = true;   // one launch per distinct shape, covering every layer of that shape
+    for (int k = 1; k < l; ++k)
+      if (is_mf[k] && d.C[k + 1] == d.C[l + 1] && d.C[k] == d.C[l]) first = false;
+    if (!first) continue;
+    MfJobs M;
+    memset(&M, 0, sizeof(M));
+    int nm = 0;
+    for (int k = l; k < 5; ++k)
+      if (is_mf[k] && d.C[k + 1] == d.C[l + 1] && d.C[k] == d.C[l])
+        M.j[nm++] = MfJob{d.dz[k], d.z[k - 1], d.bn[k - 1], J.j[k].eoff};
+    M.total = J.total;
+    M.KS = ks;
+    launch_wgrad_mf(d.C[l + 1], d.C[l], d, M, nm, st);
+    RPC_LAUNCH_CHECK();
+  }
   for (int l = 0; l < 5; ++l) {
     G.gg[l] = grads[6 * l + 2];
     G.gb[l] = grads[6 * l + 3];

@@ -68,8 +68,11 @@ def test_standalone_matches_reference_golden(tag):
         scale = max(np.abs(r).max(), 1e-3)
         tol = 1e-3
         if name[0] == "b" and name[1:].isdigit() and int(name[1:]) < 5:
+            # bias of a Linear feeding a train-mode BatchNorm: the exact gradient is 0 (BN removes
+            # any constant); reference and kernel both return fp32 cancellation noise, whose pattern
+            # follows the summation order -> bounded by 1e-2 of the layer's dW scale
             scale = max(scale, np.abs(d["dW" + name[1:]]).max())
-            tol = 2e-3
+            tol = 1e-2
         np.testing.assert_allclose(g, r, rtol=0, atol=tol * scale, err_msg=name)
     for l in range(5):
         np.testing.assert_allclose(ps[6 * l + 4].cpu().numpy(), d[f"rm{l}"], rtol=1e-4, atol=1e-5)

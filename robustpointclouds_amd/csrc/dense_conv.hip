@@ -588,26 +588,47 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
 }
 
 // ------------------------------------------------------------------ BatchNorm passes (8 channels / thread)
+// Every pass maps a 256-thread block to (256 / CG) row lanes x CG channel groups of 8 (CG = C / 8),
+// so a thread keeps its 8 channels' BatchNorm parameters in registers for all of its rows, and
+// walks rows strided over the grid with RU rows per iteration (RU 16-byte loads per stream in flight).
+constexpr int RU = 4;
+
 // h = relu((z - mean) * scale + beta) -> bf16 image rows at (OP, OOFF); bn = scale, beta, mean, invstd
 __global__ __launch_bounds__(BLK) void k_bn_apply(const u16* __restrict__ z, int M, int C, const float* __restrict__ bn,
                                                   u16* __restrict__ out, int OP, int OOFF) {
-  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  const int CG = C >> 3;
-  if (t >= (long long)M * CG) return;
-  const int m = (int)(t / CG), c0 = (int)(t - (long long)m * CG) * 8;
-  uint4 v = *(const uint4*)(z + (size_t)m * C + c0);
-  const u16* e = (const u16*)&v;
-  u16 o[8];
+  const int CG = C >> 3, RL = BLK / CG;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  if (rl >= RL) return;
+  float sc[8], sh[8], mu[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    o[j] = f2bf(fmaxf(fmaf(bf2f(e[j]) - bn[2 * C + c], bn[c], bn[C + c]), 0.0f));
+    const int c = cg * 8 + j;
+    sc[j] = bn[c];
+    sh[j] = bn[C + c];
+    mu[j] = bn[2 * C + c];
   }
-  *(uint4*)(out + (size_t)m * OP + OOFF + c0) = *(uint4*)o;
+  const int step = gridDim.x * RL;
+  for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
+    uint4 v[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int m = m0 + u * step;
+      if (m < M) v[u] = *(const uint4*)(z + (size_t)m * C + cg * 8);
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int m = m0 + u * step;
+      if (m >= M) continue;
+      const u16* e = (const u16*)&v[u];
+      u16 o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(fmaxf(fmaf(bf2f(e[j]) - mu[j], sc[j], sh[j]), 0.0f));
+      *(uint4*)(out + (size_t)m * OP + OOFF + cg * 8) = *(uint4*)o;
+    }
+  }
 }
 
 // BatchNorm-backward partial sums: dm = dh * [pre > 0]; part[blk] = (sum dm, sum dm * xhat)
-// block = 256 threads = (256 / CG) row lanes x CG channel groups; rows strided over the grid
 __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const u16* __restrict__ dh, int DP, int DOFF,
                                                      const u16* __restrict__ z, int M, int C,
                                                      const float* __restrict__ bn, float* __restrict__ part) {
@@ -618,19 +639,39 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const u16* __restrict__ dh,
 #pragma unroll
   for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
   if (rl < RL) {
-    for (int m = blockIdx.x * RL + rl; m < M; m += gridDim.x * RL) {
-      uint4 dv = *(const uint4*)(dh + (size_t)m * DP + DOFF + cg * 8);
-      uint4 zv = *(const uint4*)(z + (size_t)m * C + cg * 8);
-      const u16* de = (const u16*)&dv;
-      const u16* ze = (const u16*)&zv;
+    float sc[8], be[8], mu[8], is[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int c = cg * 8 + j;
-        const float zz = bf2f(ze[j]);
-        const float pre = fmaf(zz - bn[2 * C + c], bn[c], bn[C + c]);
-        const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
-        s1[j] += d;
-        s2[j] += d * ((zz - bn[2 * C + c]) * bn[3 * C + c]);
+    for (int j = 0; j < 8; ++j) {
+      const int c = cg * 8 + j;
+      sc[j] = bn[c];
+      be[j] = bn[C + c];
+      mu[j] = bn[2 * C + c];
+      is[j] = bn[3 * C + c];
+    }
+    const int step = gridDim.x * RL;
+    for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
+      uint4 dv[RU], zv[RU];
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        const int m = m0 + u * step;
+        if (m < M) {
+          dv[u] = *(const uint4*)(dh + (size_t)m * DP + DOFF + cg * 8);
+          zv[u] = *(const uint4*)(z + (size_t)m * C + cg * 8);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < RU; ++u) {
+        if (m0 + u * step >= M) continue;
+        const u16* de = (const u16*)&dv[u];
+        const u16* ze = (const u16*)&zv[u];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float zz = bf2f(ze[j]);
+          const float pre = fmaf(zz - mu[j], sc[j], be[j]);
+          const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
+          s1[j] += d;
+          s2[j] += d * ((zz - mu[j]) * is[j]);
+        }
       }
     }
   }
@@ -658,25 +699,51 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_apply(const u16* __restrict__ dh,
                                                      const u16* __restrict__ z, int M, int C,
                                                      const float* __restrict__ bn, const float* __restrict__ bnb,
                                                      u16* __restrict__ dz) {
-  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  const int CG = C >> 3;
-  if (t >= (long long)M * CG) return;
-  const int m = (int)(t / CG), c0 = (int)(t - (long long)m * CG) * 8;
-  uint4 dv = *(const uint4*)(dh + (size_t)m * DP + DOFF + c0);
-  uint4 zv = *(const uint4*)(z + (size_t)m * C + c0);
-  const u16* de = (const u16*)&dv;
-  const u16* ze = (const u16*)&zv;
-  u16 o[8];
+  const int CG = C >> 3, RL = BLK / CG;
+  const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
+  if (rl >= RL) return;
+  float sc[8], be[8], mu[8], gi[8], m1[8], m2[8], mb[8], ib[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) {
-    const int c = c0 + j;
-    const float zz = bf2f(ze[j]);
-    const float pre = fmaf(zz - bn[2 * C + c], bn[c], bn[C + c]);
-    const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
-    const float xh = (zz - bnb[3 * C + c]) * bnb[4 * C + c];
-    o[j] = f2bf(bnb[c] * (d - bnb[C + c] - xh * bnb[2 * C + c]));
+    const int c = cg * 8 + j;
+    sc[j] = bn[c];
+    be[j] = bn[C + c];
+    mu[j] = bn[2 * C + c];
+    gi[j] = bnb[c];
+    m1[j] = bnb[C + c];
+    m2[j] = bnb[2 * C + c];
+    mb[j] = bnb[3 * C + c];
+    ib[j] = bnb[4 * C + c];
   }
-  *(uint4*)(dz + (size_t)m * C + c0) = *(uint4*)o;
+  const int step = gridDim.x * RL;
+  for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
+    uint4 dv[RU], zv[RU];
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int m = m0 + u * step;
+      if (m < M) {
+        dv[u] = *(const uint4*)(dh + (size_t)m * DP + DOFF + cg * 8);
+        zv[u] = *(const uint4*)(z + (size_t)m * C + cg * 8);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < RU; ++u) {
+      const int m = m0 + u * step;
+      if (m >= M) continue;
+      const u16* de = (const u16*)&dv[u];
+      const u16* ze = (const u16*)&zv[u];
+      u16 o[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float zz = bf2f(ze[j]);
+        const float pre = fmaf(zz - mu[j], sc[j], be[j]);
+        const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
+        const float xh = (zz - mb[j]) * ib[j];
+        o[j] = f2bf(gi[j] * (d - m1[j] - xh * m2[j]));
+      }
+      *(uint4*)(dz + (size_t)m * C + cg * 8) = *(uint4*)o;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ weight preparation
@@ -822,12 +889,19 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
 
 extern "C" int rpc_dense_bn_apply(const void* z, int m, int c, const float* bn, void* out, int op, int ooff,
                                   void* stream) {
-  if (m < 0 || c < 8 || (c & 7) || (op & 7) || (ooff & 7) || op < ooff + c) return RPC_ERR_ARG;
+  if (m < 0 || c < 8 || c > 2048 || (c & 7) || (op & 7) || (ooff & 7) || op < ooff + c) return RPC_ERR_ARG;
   if (m == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_bn_apply, dim3(cdivu((long long)m * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_bn_apply, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
                      (const u16*)z, m, c, bn, (u16*)out, op, ooff);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+// elementwise BatchNorm passes: blocks of (256 / (C/8)) row lanes, ~2*RU rows per thread
+static unsigned ew_blocks(long long m, int c) {
+  const long long rl = BLK / (c / 8 > 0 ? c / 8 : 1);
+  long long b = (m + rl * 2 * RU - 1) / (rl * 2 * RU);
+  return (unsigned)(b < 1 ? 1 : (b > 65535 ? 65535 : b));
 }
 
 extern "C" int rpc_dense_bnbwd_blocks(int m) {
@@ -847,9 +921,9 @@ extern "C" int rpc_dense_bnbwd_stats(const void* dh, int dp, int doff, const voi
 
 extern "C" int rpc_dense_bnbwd_apply(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
                                      const float* bnb, void* dz, void* stream) {
-  if (m < 0 || c < 8 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
+  if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
   if (m == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_bnbwd_apply, dim3(cdivu((long long)m * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream,
+  hipLaunchKernelGGL(k_bnbwd_apply, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
                      (const u16*)dh, dp, doff, (const u16*)z, m, c, bn, bnb, (u16*)dz);
   RPC_LAUNCH_CHECK();
   return RPC_OK;

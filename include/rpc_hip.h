@@ -318,6 +318,32 @@ int rpc_clip_adamw(const long long* param_ptrs, const long long* grad_ptrs, cons
                    const int* chunk_start, int nchunks, int ntensors, float* steps, const RpcAdamWHyper* hyper,
                    float max_norm, float* norm_out, void* workspace, size_t ws_bytes, void* stream);
 
+
+/* ------------------------------------------------------------------ §8(f4) strong variant
+ * StrongAdversarialVoxelNet.apply_enhanced_perturbations + update_adversarial_strength
+ * (models/detectors/strong_adversarial_voxelnet.py:109-192) on the HardSimpleVFE output x [n]
+ * (= V*F floats) and the adversary's output adv_out [n]:
+ *   scaling = min(epoch_scaling * boost * complexity, max_scaling) (boost from the mean |l2| of the
+ *   last 50 entries of the device ring `history` once history_count > 50; dynamic = 0 -> 1.0),
+ *   scaled = (adv_out - x) * scaling [+ momentum_alpha * last_scaled], perturbed = x + scaled,
+ *   l2 = ||scaled||_2, written to state[1] and history[history_count % RPC_STRONG_RING];
+ *   state[0] = scaling, state[2] = adversarial_loss_weight * scaling (both rounded once). Host values are the reference's Python-side numbers (epoch_scaling =
+ *   min(1 + 0.1 epoch, max_scaling), complexity = min(1 + iteration/1e4, 2)). */
+#define RPC_STRONG_RING 64
+typedef struct {
+  double epoch_scaling, complexity, max_scaling, adversarial_loss_weight;
+  float momentum_alpha;
+  int dynamic, curriculum;
+  long long history_count;   /* entries recorded before this step */
+} RpcStrongCfg;
+size_t rpc_strong_perturb_workspace_size(void);
+int rpc_strong_perturb_forward(const RpcStrongCfg* cfg, const float* x, const float* adv_out,
+                               const float* last_scaled, long long n, float* perturbed, float* scaled,
+                               float* history, float* state, void* workspace, size_t ws_bytes, void* stream);
+/* grad_x = g_p - g_s * scaling, grad_adv_out = g_s * scaling, g_s = g_p + grad_l2 * scaled / l2 */
+int rpc_strong_perturb_backward(const float* scaled, long long n, const float* state, const float* grad_perturbed,
+                                const float* grad_l2, float* grad_x, float* grad_adv_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -51,6 +51,12 @@ class RpcAdamWHyper(C.Structure):
                 ("weight_decay", C.c_float)]
 
 
+class RpcStrongCfg(C.Structure):
+    _fields_ = [("epoch_scaling", C.c_double), ("complexity", C.c_double), ("max_scaling", C.c_double),
+                ("adversarial_loss_weight", C.c_double), ("momentum_alpha", C.c_float), ("dynamic", C.c_int), ("curriculum", C.c_int),
+                ("history_count", C.c_longlong)]
+
+
 # name -> (restype, argtypes); every symbol here must be exported by the .so
 SIGNATURES = {
     "rpc_version": (C.c_char_p, []),
@@ -98,6 +104,10 @@ SIGNATURES = {
     "rpc_clip_adamw_workspace_size": (sz, [i32]),
     "rpc_clip_adamw": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, C.POINTER(RpcAdamWHyper), C.c_float, vp,
                              vp, sz, vp]),
+    "rpc_strong_perturb_workspace_size": (sz, []),
+    "rpc_strong_perturb_forward": (i32, [C.POINTER(RpcStrongCfg), vp, vp, vp, C.c_longlong, vp, vp, vp, vp, vp, sz,
+                                         vp]),
+    "rpc_strong_perturb_backward": (i32, [vp, C.c_longlong, vp, vp, vp, vp, vp, vp]),
     "rpc_anchor_head_workspace_size": (sz, [C.POINTER(RpcHeadCfg), i32]),
     "rpc_anchor_head_loss_forward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
     "rpc_anchor_head_loss_backward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,

@@ -813,6 +813,13 @@ using namespace rpc::dn;
 
 static inline Img img3(const int* d) { return Img{d[0], d[1], d[2]}; }
 
+// elementwise BatchNorm passes: blocks of (256 / (C/8)) row lanes, ~2*RU rows per thread
+static unsigned ew_blocks(long long m, int c) {
+  const long long rl = BLK / (c / 8 > 0 ? c / 8 : 1);
+  long long b = (m + rl * 2 * RU - 1) / (rl * 2 * RU);
+  return (unsigned)(b < 1 ? 1 : (b > 65535 ? 65535 : b));
+}
+
 extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const void* wt, int cout, void* out, int op,
                               int ooff, int accum, float* part, const int* r_img, const int* s_img,
                               const int* o_img, void* stream) {
@@ -895,13 +902,6 @@ extern "C" int rpc_dense_bn_apply(const void* z, int m, int c, const float* bn, 
                      (const u16*)z, m, c, bn, (u16*)out, op, ooff);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
-}
-
-// elementwise BatchNorm passes: blocks of (256 / (C/8)) row lanes, ~2*RU rows per thread
-static unsigned ew_blocks(long long m, int c) {
-  const long long rl = BLK / (c / 8 > 0 ? c / 8 : 1);
-  long long b = (m + rl * 2 * RU - 1) / (rl * 2 * RU);
-  return (unsigned)(b < 1 ? 1 : (b > 65535 ? 65535 : b));
 }
 
 extern "C" int rpc_dense_bnbwd_blocks(int m) {

@@ -1,3 +1,4 @@
 from .adversarial_voxelnet import AdversarialVoxelNet  # noqa: F401
+from .strong_adversarial_voxelnet import StrongAdversarialVoxelNet  # noqa: F401
 
-__all__ = ["AdversarialVoxelNet"]
+__all__ = ["AdversarialVoxelNet", "StrongAdversarialVoxelNet"]

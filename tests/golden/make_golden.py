@@ -11,6 +11,7 @@ mmengine / mmdet3d are not installed, so tiny stand-ins are put into ``sys.modul
 * ``models/builder.py``                        (ADVERSARIES registry)
 * ``models/adversarial/voxel_perturber.py``    (VoxelPerturber, the a3/a4 rows)
 * ``models/detectors/adversarial_voxelnet.py`` (AdversarialVoxelNet, the a2/a9/a11 rows)
+* ``models/detectors/strong_adversarial_voxelnet.py`` (StrongAdversarialVoxelNet, §8(f4))
 
 ``models/detectors/__init__.py`` is bypassed (it imports modules that do not exist,
 SURVEY.md finding 4). Weights are set explicitly from a seeded numpy RNG and stored in
@@ -47,6 +48,8 @@ class _Registry:
         return deco
 
     def build(self, cfg):
+        if isinstance(cfg, nn.Module):   # already-built stand-ins passed through
+            return cfg
         cfg = dict(cfg)
         return self._m[cfg.pop("type")](**cfg)
 
@@ -68,6 +71,13 @@ class _VoxelNet(nn.Module):
         return self.neck is not None
 
 
+class _Base3DDetector(nn.Module):
+    """Stand-in for mmdet3d Base3DDetector (StrongAdversarialVoxelNet's base)."""
+
+    def __init__(self, data_preprocessor=None, init_cfg=None):
+        super().__init__()
+
+
 def _install_stubs():
     me = types.ModuleType("mmengine")
     mer = types.ModuleType("mmengine.registry")
@@ -84,6 +94,7 @@ def _install_stubs():
     m3md = types.ModuleType("mmdet3d.models.detectors")
     m3mv = types.ModuleType("mmdet3d.models.detectors.voxelnet")
     m3mv.VoxelNet = _VoxelNet
+    m3md.Base3DDetector = _Base3DDetector
     for n, m in {"mmdet3d": m3, "mmdet3d.registry": m3r, "mmdet3d.structures": m3s,
                  "mmdet3d.models": m3m, "mmdet3d.models.detectors": m3md,
                  "mmdet3d.models.detectors.voxelnet": m3mv}.items():
@@ -116,6 +127,14 @@ def load_reference():
     av = _load("refmodels.detectors.adversarial_voxelnet",
                os.path.join(REF, "models", "detectors", "adversarial_voxelnet.py"))
     return builder, vp, av
+
+
+def load_strong(builder):
+    """strong_adversarial_voxelnet.py builds its adversary through `models.builder` (:63-66)."""
+    _pkg("models", os.path.join(REF, "models"))
+    sys.modules["models.builder"] = builder
+    return _load("refmodels.detectors.strong_adversarial_voxelnet",
+                 os.path.join(REF, "models", "detectors", "strong_adversarial_voxelnet.py"))
 
 
 # ---------------------------------------------------------------- helpers
@@ -305,6 +324,77 @@ def gen_voxelnet(builder, av, tag, listy, epoch, seed, V=400, hidden=(8, 16, 32)
                                           for k, v in d.items() if k.startswith("L_")))
 
 
+class _StandInHeadS(_StandInHead):
+    """The voxelnet stand-in head, built from a config dict (StrongAdversarialVoxelNet.__init__
+    builds bbox_head with train_cfg / test_cfg added, :56-59)."""
+
+    def __init__(self, w, listy, train_cfg=None, test_cfg=None):
+        super().__init__(np.asarray(w, np.float32), listy)
+
+
+def gen_strong(builder, sv, tag, listy, bound, seed, steps=53, V=400, hidden=(8, 16, 32), epoch=2, alt=False):
+    """StrongAdversarialVoxelNet over `steps` loss() calls: constant V (the cross-step momentum
+    applies) or, with alt, V and V+1 alternating (momentum reset on every shape change, small l2 so
+    the attack-history boost branches engage after 50 steps); torch RNG seeded for the
+    anti-adaptation draws; per-step losses / l2 / scaling, final-step gradients."""
+    rng = np.random.default_rng(seed)
+    F = 4
+    w = perturber_weights(rng, F, hidden)
+    B = 2
+    sets = []
+    for k, v in enumerate([V, V + 1] if alt else [V]):
+        vx, nx = valid_slots(seed + 1 + k, v, F)
+        cx = np.zeros((v, 4), np.int32)
+        cx[:, 0] = (np.arange(v) >= v // 2).astype(np.int32)
+        sets.append((vx, nx, cx))
+    hw = rng.standard_normal((4, 3)).astype(np.float32)
+    sys.modules["mmdet3d.registry"].MODELS.register_module()(_StandInHeadS)
+    keys = ("loss_cls", "loss_bbox", "loss_dir", "loss_adversarial", "loss_l2_regularization")
+    rec = {k: [] for k in keys}
+    rec["l2"], rec["scaling"] = [], []
+    with _quiet():
+        model = sv.StrongAdversarialVoxelNet(
+            voxel_encoder=_StandInVFE(), middle_encoder=_StandInMiddle(), backbone=nn.Identity(), neck=None,
+            bbox_head=dict(type="_StandInHeadS", w=hw, listy=listy),
+            adversary_cfg=dict(type="VoxelPerturber", sensor_error_bound=bound, hidden_channels=list(hidden)))
+        model.adversary._build_model(F)
+        lin, bns, att = set_perturber_weights(model.adversary, w)
+        model.train()
+        model._epoch = epoch
+        torch.manual_seed(seed)
+        for step in range(steps):
+            vox, npts, coors = sets[step % len(sets)]
+            inputs = {"voxels": {"voxels": torch.from_numpy(vox), "num_points": torch.from_numpy(npts),
+                                 "coors": torch.from_numpy(coors)}}
+            losses = model.loss(inputs, [None] * B)
+            for k in keys:
+                v = losses[k]
+                rec[k].append(float((v[0] if isinstance(v, list) else v).item()))
+            rec["l2"].append(float(inputs["adversarial_l2_norm"].item()))
+            rec["scaling"].append(float(model._current_scaling))
+        total = 0
+        for k, v in losses.items():
+            if "loss" in k:
+                total = total + (sum(t.mean() for t in v) if isinstance(v, list) else v.mean())
+        total.backward()
+    d = dict(w)
+    for k, (vx, nx, cx) in enumerate(sets):
+        d[f"vox{k}"], d[f"num_points{k}"], d[f"coors{k}"] = vx, nx, cx
+    d.update(nsets=np.int32(len(sets)), head_w=hw, epoch=np.int32(epoch), listy=np.int32(listy),
+             hidden=np.array(hidden, np.int32), bound=np.float32(bound), seed=np.int32(seed),
+             steps=np.int32(steps), total=np.float32(total.item()))
+    for k, v in rec.items():
+        d["S_" + k] = np.array(v, np.float64)
+    g = lambda t: np.zeros(tuple(t.shape), np.float32) if t.grad is None else t.grad.numpy().copy()
+    for l, m in enumerate(lin):
+        d[f"dW{l}"] = g(m.weight)
+        d[f"db{l}"] = g(m.bias)
+    d["dhead_w"] = model.bbox_head.w.grad.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"strong_{tag}.npz"), **d)
+    print(f"strong_{tag}: l2 {rec['l2'][0]:.4f}..{rec['l2'][-1]:.4f} scaling {rec['scaling'][0]:.3f}.."
+          f"{rec['scaling'][-1]:.3f} total={d['total']:.6f}")
+
+
 def main():
     torch.manual_seed(0)
     builder, vp, av = load_reference()
@@ -316,6 +406,11 @@ def main():
     gen_voxelnet(builder, av, "list_e7", True, 7, 12)
     gen_voxelnet(builder, av, "tensor_e3", False, 3, 13)
     gen_voxelnet(builder, av, "gate_e2", True, 2, 14)
+    sv = load_strong(builder)
+    gen_strong(builder, sv, "list", True, 0.4, 21)
+    gen_strong(builder, sv, "tensor", False, 0.4, 22)
+    gen_strong(builder, sv, "weak", False, 1e-3, 23, steps=56, V=4, alt=True)
+    gen_strong(builder, sv, "tiny", True, 1e-3, 24, steps=56, V=3, alt=True)
 
 
 if __name__ == "__main__":

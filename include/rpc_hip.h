@@ -344,6 +344,29 @@ int rpc_strong_perturb_forward(const RpcStrongCfg* cfg, const float* x, const fl
 int rpc_strong_perturb_backward(const float* scaled, long long n, const float* state, const float* grad_perturbed,
                                 const float* grad_l2, float* grad_x, float* grad_adv_out, void* stream);
 
+
+/* ------------------------------------------------------------------ §8(f2) train-pipeline augmentation
+ * The per-frame point / box transforms of configs/_base_/kitti-3d-car.py:42-68 (upstream mmdet3d
+ * RandomFlip3D, GlobalRotScaleTrans, PointsRangeFilter, ObjectRangeFilter, PointShuffle) for B
+ * frames concatenated in `points` [P][F] with device offsets [B+1]. frames (device [B]): the random
+ * draws of each frame (made on the host in the reference's RNG order) with cos/sin of the rotation.
+ * out_points [P][F]: each frame's surviving points, compacted in order (or shuffled, shuffle != 0,
+ * a seeded uniform permutation per frame), out_offsets (device [B+1]); rows beyond the survivors
+ * are NaN (hard_voxelize drops them, so no host read of the count is needed).
+ * rpc_augment_boxes transforms boxes [B][M][7] / labels [B][M] (int64, -1 = padding) in place;
+ * boxes outside the BEV range become padding; yaw wrapped by limit_yaw(0.5, 2 pi). */
+typedef struct {
+  int flip_h, flip_v;
+  float rot, cosr, sinr, scale, tx, ty, tz;
+} RpcAugFrame;
+size_t rpc_augment_points_workspace_size(int num_features, int total_points);
+int rpc_augment_points(const float* points, int num_features, int total_points, const int* frame_offsets, int batch,
+                       const RpcAugFrame* frames, const float* pc_range /* host [6] */, int shuffle,
+                       unsigned long long seed, float* out_points, int* out_offsets, void* workspace,
+                       size_t ws_bytes, void* stream);
+int rpc_augment_boxes(float* boxes, long long* labels, int batch, int max_gts, const RpcAugFrame* frames,
+                      const float* pc_range /* host [6] */, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

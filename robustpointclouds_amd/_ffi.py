@@ -57,6 +57,11 @@ class RpcStrongCfg(C.Structure):
                 ("history_count", C.c_longlong)]
 
 
+class RpcAugFrame(C.Structure):
+    _fields_ = [("flip_h", C.c_int), ("flip_v", C.c_int), ("rot", C.c_float), ("cosr", C.c_float),
+                ("sinr", C.c_float), ("scale", C.c_float), ("tx", C.c_float), ("ty", C.c_float), ("tz", C.c_float)]
+
+
 # name -> (restype, argtypes); every symbol here must be exported by the .so
 SIGNATURES = {
     "rpc_version": (C.c_char_p, []),
@@ -108,6 +113,9 @@ SIGNATURES = {
     "rpc_strong_perturb_forward": (i32, [C.POINTER(RpcStrongCfg), vp, vp, vp, C.c_longlong, vp, vp, vp, vp, vp, sz,
                                          vp]),
     "rpc_strong_perturb_backward": (i32, [vp, C.c_longlong, vp, vp, vp, vp, vp, vp]),
+    "rpc_augment_points_workspace_size": (sz, [i32, i32]),
+    "rpc_augment_points": (i32, [vp, i32, i32, vp, i32, vp, fp, i32, C.c_ulonglong, vp, vp, vp, sz, vp]),
+    "rpc_augment_boxes": (i32, [vp, vp, i32, i32, vp, fp, vp]),
     "rpc_anchor_head_workspace_size": (sz, [C.POINTER(RpcHeadCfg), i32]),
     "rpc_anchor_head_loss_forward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
     "rpc_anchor_head_loss_backward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,

@@ -29,6 +29,8 @@ def _args():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=6)
     ap.add_argument("--classes", type=int, default=1, choices=[1, 3])
+    ap.add_argument("--model", default="voxelnet", choices=["voxelnet", "strong"],
+                    help="strong = StrongAdversarialVoxelNet, sensor_error_bound 0.4 (BASELINE config 5)")
     ap.add_argument("--fp32", action="store_true", help="dense part in fp32 (parity mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6)
@@ -139,7 +141,7 @@ def main():
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
-    model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3)
+    model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3, variant=a.model)
     tr = Trainer(model, ddp=world > 1, bf16=not a.fp32, device=dev)
     from robustpointclouds_amd import dense_bev
     from robustpointclouds_amd.sparse_encoder import KernelTimer
@@ -178,8 +180,9 @@ def main():
                    value=round(frames / dt, 3), unit="frames/s", n_gpus=world, steps=a.steps, warmup=a.warmup,
                    ms_per_step=round(1000 * dt / a.steps, 3), higher_is_better=True, scaling="weak",
                    vs_baseline=None, dtype="fp32" if a.fp32 else "bf16", data="synthetic",
-                   config=dict(workload="AdversarialVoxelNet (SECOND) KITTI " +
-                               ("Car-only" if a.classes == 1 else "3-class") +
+                   config=dict(workload=("AdversarialVoxelNet" if a.model == "voxelnet" else
+                                         "StrongAdversarialVoxelNet (sensor_error_bound 0.4, config 5)") +
+                               " (SECOND) KITTI " + ("Car-only" if a.classes == 1 else "3-class") +
                                f", batch {a.batch}/GPU, perturber active (_epoch=3)",
                                global_batch=world * a.batch, frames_per_gpu=a.batch,
                                dense_dtype="fp32" if a.fp32 else "bf16",
@@ -207,7 +210,7 @@ def main():
                                    avg_launch_ms=round(ks["avg_ms"], 4),
                                    flops_per_launch=ks["flops_per_launch"], launches=ks["launches"],
                                    work="2*C_in*C_out FLOP per valid rulebook pair")
-        if not a.no_cpu_baseline:
+        if not a.no_cpu_baseline and a.model == "voxelnet":
             res["cpu_baseline"] = cpu_baseline(a.cpu_frames, a.classes)
         print(json.dumps(res), flush=True)
     if world > 1:

@@ -22,7 +22,7 @@ import robustpointclouds_amd.plugin.models  # noqa: F401  (registers Adversarial
 from .adversarial_loss import parse_losses
 from .optim import ClipAdamW
 from .registry import MODELS
-from .voxelnet import second_kitti_cfg
+from .voxelnet import second_kitti_cfg, second_kitti_strong_cfg
 
 
 def build_model(cfg: dict):
@@ -163,8 +163,14 @@ def _ddp_forward(self, batch, gt, mode="loss"):
     return self.loss(batch, gt)
 
 
-def make_kitti_model(num_classes=1, device=None, adversarial=True, hidden_channels=None, epoch=3):
-    model = build_model(second_kitti_cfg(num_classes, hidden_channels=hidden_channels, adversarial=adversarial))
+def make_kitti_model(num_classes=1, device=None, adversarial=True, hidden_channels=None, epoch=3, variant="voxelnet"):
+    """variant 'voxelnet': AdversarialVoxelNet (configs/adversarial/...kitti-3d-{car,3class}.py);
+    'strong': StrongAdversarialVoxelNet with sensor_error_bound 0.4 (BASELINE config 5)."""
+    if variant == "strong":
+        cfg = second_kitti_strong_cfg(num_classes, hidden_channels=hidden_channels)
+    else:
+        cfg = second_kitti_cfg(num_classes, hidden_channels=hidden_channels, adversarial=adversarial)
+    model = build_model(cfg)
     # DDP calls forward(); route it to loss() like mmengine's BaseModel.forward(mode='loss')
     model.forward = _ddp_forward.__get__(model)
     model._epoch = epoch

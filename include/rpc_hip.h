@@ -7,7 +7,10 @@
  *     the library never allocates: scratch comes in through `workspace`;
  *   - `stream` is a hipStream_t passed as void* (the launcher's current stream);
  *   - return value 0 = success, otherwise an RPC_ERR_* code (the Python side raises);
- *     nothing in the library aborts or synchronises the device.
+ *     nothing in the library aborts or synchronises the device;
+ *   - an *armed* workspace (marked so below) must be zero-filled once when it is allocated: the
+ *     kernel's last-arriving block re-arms its ticket to zero, so the same workspace is reused by
+ *     later calls on the same stream with no per-call memset.
  *
  * Each entry point names the reference interface it replaces (file:line in
  * /root/reference, or the un-vendored upstream call site that file reaches).
@@ -163,7 +166,8 @@ int rpc_spconv_wgrad(const float* in, const float* in_bn, int ci, const int* nbr
                      void* workspace, size_t workspace_bytes, void* stream);
 /* BatchNorm1d finalize from partial sums. mode 0: bn_out = scale, shift, mean, invstd and the
  * running stats update (train). mode 1: bn_out = gi, m1, m2, mean, invstd for the backward and
- * dgamma = sum dy*xhat, dbeta = sum dy. */
+ * dgamma = sum dy*xhat, dbeta = sum dy. Armed workspace (the ticket is at offset 0, so one
+ * workspace sized for the widest c serves every c). */
 size_t rpc_bn_finalize_workspace_size(int c);
 int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean, float* running_var,

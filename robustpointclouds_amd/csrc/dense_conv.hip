@@ -498,7 +498,9 @@ struct WG {
   float* part;    // [chunks][T][CI][CO]
 };
 
-// grid: (chunks, T, (CI/128)*(CO/128)); 4 waves as 2 (ci) x 2 (co), 64x64 each
+// 1-D grid of chunks * T * (CI/128)*(CO/128) blocks, XCD-aware: each XCD walks whole chunks with
+// the taps and channel tiles of one chunk adjacent, so a chunk's x / dz rows are fetched into that
+// XCD's L2 once and re-read by its T * tiles blocks. 4 waves as 2 (ci) x 2 (co), 64x64 each.
 template <int MAP>
 __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
   constexpr int T = wtaps_of<MAP>();
@@ -507,8 +509,11 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
   __shared__ __attribute__((aligned(16))) u16 sD[RT * P];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wci = w >> 1, wco = w & 1;
-  const int chunk = blockIdx.x, t = blockIdx.y;
-  const int nco = g.CO / 128, ci0 = (blockIdx.z / nco) * 128, co0 = (blockIdx.z % nco) * 128;
+  const int nco = g.CO / 128, ntile = (g.CI / 128) * nco;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = lid / (T * ntile), rest = lid - chunk * (T * ntile);
+  const int t = rest / ntile, tile = rest - t * ntile;
+  const int ci0 = (tile / nco) * 128, co0 = (tile % nco) * 128;
   const int rb0 = chunk * g.rows_per, rb1 = min(g.M, rb0 + g.rows_per);
   const int HW = g.R.H * g.R.W;
   const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, rowoff = 4 * g4 + qq;
@@ -787,7 +792,7 @@ static void launch_igemm(const IG& g, int par_count, hipStream_t st) {
 
 template <int MAP>
 static void launch_wgrad(const WG& g, int chunks, hipStream_t st) {
-  dim3 grid(chunks, wtaps_of<MAP>(), (g.CI / 128) * (g.CO / 128));
+  dim3 grid(chunks * wtaps_of<MAP>() * (g.CI / 128) * (g.CO / 128));
   hipLaunchKernelGGL((k_wgrad<MAP>), grid, dim3(BLK), 0, st, g);
 }
 

@@ -383,7 +383,9 @@ __global__ __launch_bounds__(BLK) void k_wgrad(WgradArgs g) {
 
 
 // ------------------------------------------------------------------ BatchNorm finalize
-// one block per column j < 2C: fixed-order tree sum of the partial rows in double.
+// One block per column j < 2C: every thread sums its strided share of the nblk partial rows with
+// four loads in flight (one latency round for nblk <= 1024), then a fixed-order LDS tree; the
+// last-arriving block finalizes:
 // mode 0 (forward): bn = scale (= gamma*invstd), beta, mean, invstd ; running stats updated.
 // mode 1 (backward): bnb = gi, m1, m2, mean, invstd ; dgamma, dbeta written.
 __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int N,
@@ -397,8 +399,18 @@ __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ p
   __shared__ double sh[BLK];
   __shared__ int lastf;
   const int j = blockIdx.x;
+  const long long C2 = 2 * C;
   double s = 0.0;
-  for (int r = threadIdx.x; r < nblk; r += BLK) s += part[(long long)r * 2 * C + j];
+  int r = threadIdx.x;
+  for (; r + 3 * BLK < nblk; r += 4 * BLK) {
+    const float a0 = part[r * C2 + j], a1 = part[(r + BLK) * C2 + j];
+    const float a2 = part[(r + 2 * BLK) * C2 + j], a3 = part[(r + 3 * BLK) * C2 + j];
+    s += (double)a0;
+    s += (double)a1;
+    s += (double)a2;
+    s += (double)a3;
+  }
+  for (; r < nblk; r += BLK) s += (double)part[r * C2 + j];
   sh[threadIdx.x] = s;
   __syncthreads();
   for (int o = BLK / 2; o > 0; o >>= 1) {
@@ -408,7 +420,7 @@ __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ p
   if (threadIdx.x == 0) tot[j] = sh[0];
   if (!last_block_arrive(ticket, &lastf)) return;
   for (int c = threadIdx.x; c < C; c += BLK) {
-    double s1 = tot[c], s2 = tot[C + c];
+    const double s1 = tot[c], s2 = tot[C + c];
     if (mode == 0) {
       double mean = s1 / N;
       double var = s2 / N - mean * mean;
@@ -467,20 +479,35 @@ __global__ __launch_bounds__(BLK) void k_from_dense(const T* __restrict__ gd, co
                                                     const float* __restrict__ bn, const int* __restrict__ coors,
                                                     int N, int C, Shape s, float* __restrict__ dy,
                                                     float* __restrict__ part) {
-  // block: BM rows; thread handles channels c = tid, tid + BLK, ... (C <= 256)
-  const int r0 = blockIdx.x * BM;
-  for (int c = threadIdx.x; c < C; c += BLK) {
-    float s1 = 0.0f, s2 = 0.0f;
-    for (int r = r0; r < min(N, r0 + BM); ++r) {
-      float zz = z[(long long)r * C + c];
-      float h = fmaxf(fmaf(zz - bn[2 * C + c], bn[c], bn[C + c]), 0.0f);
-      float v = h > 0.0f ? load_val(gd + dense_index<NHWC>(coors + 4 * r, c, C, s)) : 0.0f;
+  // block: BM rows; threads laid out (row lane, channel) so that each row's gather and the dy
+  // store are coalesced; row lanes combined in lane order (C <= 256)
+  __shared__ float sh[2][BLK];
+  const int r0 = blockIdx.x * BM, r1 = min(N, r0 + BM);
+  const int nl = BLK / C;                       // >= 1 row lanes
+  const int rl = threadIdx.x / C, c = threadIdx.x - rl * C;
+  float s1 = 0.0f, s2 = 0.0f;
+  if (rl < nl) {
+    const float mu = bn[2 * C + c], sc = bn[c], sh0 = bn[C + c], is = bn[3 * C + c];
+    for (int r = r0 + rl; r < r1; r += nl) {
+      const float zz = z[(long long)r * C + c];
+      const float h = fmaxf(fmaf(zz - mu, sc, sh0), 0.0f);
+      const float v = h > 0.0f ? load_val(gd + dense_index<NHWC>(coors + 4 * r, c, C, s)) : 0.0f;
       dy[(long long)r * C + c] = v;
       s1 += v;
-      s2 += v * ((zz - bn[2 * C + c]) * bn[3 * C + c]);
+      s2 += v * ((zz - mu) * is);
     }
-    part[(long long)blockIdx.x * 2 * C + c] = s1;
-    part[(long long)blockIdx.x * 2 * C + C + c] = s2;
+  }
+  sh[0][threadIdx.x] = s1;
+  sh[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (rl == 0) {
+    float t1 = sh[0][c], t2 = sh[1][c];
+    for (int k = 1; k < nl; ++k) {
+      t1 += sh[0][k * C + c];
+      t2 += sh[1][k * C + c];
+    }
+    part[(long long)blockIdx.x * 2 * C + c] = t1;
+    part[(long long)blockIdx.x * 2 * C + C + c] = t2;
   }
 }
 
@@ -711,9 +738,11 @@ extern "C" int rpc_bn_finalize(const float* part, int nblk, int C, int N, int mo
                                void* ws, void* stream) {
   if (C < 1 || nblk < 1 || !part || !bn_out || !ws) return RPC_ERR_ARG;
   hipStream_t st = (hipStream_t)stream;
-  double* tot = (double*)ws;
-  unsigned* ticket = (unsigned*)((char*)ws + al(sizeof(double) * 2 * C));
-  RPC_CHECK(hipMemsetAsync(ticket, 0, sizeof(unsigned), st));
+  // armed workspace: the ticket is zero on entry (zero-filled once by the owner) and re-armed by
+  // the kernel's last block, so there is no per-call memset
+  // the ticket sits at offset 0 so that one armed workspace serves every width c
+  unsigned* ticket = (unsigned*)ws;
+  double* tot = (double*)((char*)ws + 256);
   hipLaunchKernelGGL(k_bn_finalize, dim3(2 * C), dim3(BLK), 0, st, part, nblk, C, N, mode, gamma, beta, eps,
                      momentum, running_mean, running_var, fwd_bn, bn_out, tot, ticket, dgamma, dbeta);
   RPC_LAUNCH_CHECK();

@@ -266,7 +266,7 @@ class SparseEncoderFn(torch.autograd.Function):
             n_out = rec["n_out"]
             z = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
             nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
-            part = torch.zeros((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
+            part = torch.empty((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
             tm = enc.timer is not None and enc.timer.wants("fwd", sp)
             rec["bf16"] = bf16 and li > 0
             rec["h_in"] = hsrc if rec["bf16"] else None
@@ -289,7 +289,7 @@ class SparseEncoderFn(torch.autograd.Function):
                       f"rpc::sp::k_gemm<{sp.ci}, {sp.co}, {1 if li else 0}, 0>")
                 enc.timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
             bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
-            wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(sp.co), dev)
+            wsb = _ffi.armed_workspace("bn_finalize", lib.rpc_bn_finalize_workspace_size(sp.co), dev)
             _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
                                            float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
                                            _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
@@ -342,7 +342,7 @@ class SparseEncoderFn(torch.autograd.Function):
         n = last["n_out"]
         dy = torch.empty((n, C), dtype=torch.float32, device=dev)
         nblk = max(lib.rpc_spconv_gemm_blocks(n), 1)
-        part = torch.zeros((nblk, 2 * C), dtype=torch.float32, device=dev)
+        part = torch.empty((nblk, 2 * C), dtype=torch.float32, device=dev)
         _ffi.check(lib.rpc_dense_to_sparse_grad(_ffi.ptr(gd), _ffi.ptr(last["z"]), _ffi.ptr(last["bn"]),
                                                 _ffi.ptr(last["coors_out"]), n, C, _ffi.int_arr((B, D, H, Wd)),
                                                 flags, _ffi.ptr(dy), _ffi.ptr(part), st), "rpc_dense_to_sparse_grad")
@@ -358,7 +358,7 @@ class SparseEncoderFn(torch.autograd.Function):
             bnb = torch.empty(5 * sp.co, dtype=torch.float32, device=dev)
             dgamma = torch.empty_like(rec["gamma"])
             dbeta = torch.empty_like(rec["beta"])
-            wsb = _ffi.workspace(lib.rpc_bn_finalize_workspace_size(sp.co), dev)
+            wsb = _ffi.armed_workspace("bn_finalize", lib.rpc_bn_finalize_workspace_size(sp.co), dev)
             _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 1, _ffi.ptr(rec["gamma"]),
                                            _ffi.ptr(rec["beta"]), 0.0, 0.0, None, None, _ffi.ptr(rec["bn"]),
                                            _ffi.ptr(bnb), _ffi.ptr(dgamma), _ffi.ptr(dbeta), _ffi.ptr(wsb), st),
@@ -399,7 +399,7 @@ class SparseEncoderFn(torch.autograd.Function):
             if li > 0:
                 prev = L[li - 1]
                 nblk = max(lib.rpc_spconv_gemm_blocks(n_in), 1)
-                part = torch.zeros((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
+                part = torch.empty((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
                 td = timer is not None and timer.wants("dgrad", sp)
                 if rec["bf16"]:
                     e0 = timer.start() if td else None

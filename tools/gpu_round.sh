@@ -9,7 +9,7 @@ OUT=gpurun_out/$TAG
 mkdir -p $OUT
 export TMPDIR=/tmp
 step_tests() {
-  [ "$MODE" != "tests" ] && return 0
+  [ "$MODE" != "tests" ] && [ "$MODE" != "all" ] && return 0
   timeout -k 10 420 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread \
     > $OUT/pytest_gpu.log 2>&1
 }
@@ -22,7 +22,7 @@ step_prof() {
     python -u bench.py --steps 12 --warmup 6 --no-cpu-baseline > $OUT/prof_bench.log 2>&1
 }
 step_pmc() {
-  [ "$MODE" != "pmc" ] && return 0
+  [ "$MODE" != "pmc" ] && [ "$MODE" != "all" ] && return 0
   for C in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 180 rocprofv3 --pmc $C --kernel-include-regex 'k_conv3x3|k_wgrad|k_gemm_bf16|k_bnbwd' \
       --output-format csv -d $OUT/pmc_$C -o run -- \

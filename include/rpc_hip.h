@@ -371,6 +371,48 @@ int rpc_augment_points(const float* points, int num_features, int total_points, 
 int rpc_augment_boxes(float* boxes, long long* labels, int batch, int max_gts, const RpcAugFrame* frames,
                       const float* pc_range /* host [6] */, void* stream);
 
+
+/* ------------------------------------------------------------------ §8(f3) CenterHead targets + losses
+ * Replaces upstream mmdet3d `CenterHead.get_targets` / `loss_by_feat` (dense_heads/centerpoint_head.py;
+ * draw_heatmap_gaussian, gaussian_radius, mmdet GaussianFocalLoss + L1Loss) as configured by
+ * configs/adversarial/adversarial-centerpoint_voxel-nuscenes.py:11-13 (the upstream
+ * centerpoint_voxel01_second_secfpn_head-dcn base) and called at
+ * models/detectors/adversarial_centerpoint.py:224 (`pts_bbox_head.loss_by_feat`).
+ * Feature map H x W (= grid_size[1] / osf, grid_size[0] / osf). Head outputs (fp32) per cell
+ * p = (b*H + y)*W + x: heatmap logits hm[p*hm_pitch + g] for the global class g (classes in task
+ * order, task t owning task_ncls[t] consecutive classes), boxes box[p*box_pitch + t*10 + c] with
+ * c = reg(2) | height(1) | dim(3) | rot(2) | vel(2).
+ * gt_boxes [B][max_gts][9] fp32 (LiDAR bottom centre x, y, z, dx, dy, dz, yaw, vx, vy), gt_labels
+ * [B][max_gts] int64 (-1 = padding). losses (device fp32 [2*ntasks]) out: task t loss_heatmap at 2t,
+ * loss_bbox at 2t+1. The workspace (targets, normalisers) must be kept between forward and backward. */
+#define RPC_CENTER_MAX_TASKS 8
+typedef struct {
+  int B, H, W;
+  int ntasks, ncls_total;
+  int task_ncls[RPC_CENTER_MAX_TASKS];
+  int max_objs, min_radius, out_size_factor, norm_bbox;
+  float voxel_x, voxel_y, pc_x, pc_y;
+  double gaussian_overlap;            /* python float: the radius constants are formed from it */
+  float code_weights[10];
+  float loss_cls_weight, loss_bbox_weight;
+  int hm_pitch, box_pitch;
+} RpcCenterCfg;
+
+size_t rpc_center_head_workspace_size(const RpcCenterCfg* cfg, int max_gts);
+int rpc_center_head_loss_forward(const RpcCenterCfg* cfg, const float* gt_boxes, const long long* gt_labels,
+                                 int max_gts, const float* hm, const float* box, float* losses, void* workspace,
+                                 size_t ws_bytes, void* stream);
+/* grad_losses [2*ntasks] (device) -> dhm (cells x hm_pitch, every heatmap channel written) and dbox
+ * (cells x box_pitch, zero except at the gathered cells). */
+int rpc_center_head_loss_backward(const RpcCenterCfg* cfg, const float* hm, const float* box,
+                                  const float* grad_losses, float* dhm, float* dbox, void* workspace,
+                                  size_t ws_bytes, void* stream);
+/* The training targets themselves (for tests / inspection): heatmap [B][H][W][ncls_total],
+ * ind [B][ntasks][max_objs] int32, mask [B][ntasks][max_objs] int32, anno [B][ntasks][max_objs][10]
+ * — views into a workspace filled by rpc_center_head_loss_forward. */
+int rpc_center_head_targets(const RpcCenterCfg* cfg, int max_gts, const void* workspace, const float** heatmap,
+                            const int** ind, const int** mask, const float** anno);
+
 #ifdef __cplusplus
 }
 #endif

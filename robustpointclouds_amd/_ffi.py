@@ -62,6 +62,16 @@ class RpcAugFrame(C.Structure):
                 ("sinr", C.c_float), ("scale", C.c_float), ("tx", C.c_float), ("ty", C.c_float), ("tz", C.c_float)]
 
 
+class RpcCenterCfg(C.Structure):
+    """include/rpc_hip.h RpcCenterCfg."""
+    _fields_ = [("B", C.c_int), ("H", C.c_int), ("W", C.c_int), ("ntasks", C.c_int), ("ncls_total", C.c_int),
+                ("task_ncls", C.c_int * 8), ("max_objs", C.c_int), ("min_radius", C.c_int),
+                ("out_size_factor", C.c_int), ("norm_bbox", C.c_int), ("voxel_x", C.c_float), ("voxel_y", C.c_float),
+                ("pc_x", C.c_float), ("pc_y", C.c_float), ("gaussian_overlap", C.c_double),
+                ("code_weights", C.c_float * 10), ("loss_cls_weight", C.c_float), ("loss_bbox_weight", C.c_float),
+                ("hm_pitch", C.c_int), ("box_pitch", C.c_int)]
+
+
 # name -> (restype, argtypes); every symbol here must be exported by the .so
 SIGNATURES = {
     "rpc_version": (C.c_char_p, []),
@@ -116,6 +126,11 @@ SIGNATURES = {
     "rpc_augment_points_workspace_size": (sz, [i32, i32]),
     "rpc_augment_points": (i32, [vp, i32, i32, vp, i32, vp, fp, i32, C.c_ulonglong, vp, vp, vp, sz, vp]),
     "rpc_augment_boxes": (i32, [vp, vp, i32, i32, vp, fp, vp]),
+    "rpc_center_head_workspace_size": (sz, [C.POINTER(RpcCenterCfg), i32]),
+    "rpc_center_head_loss_forward": (i32, [C.POINTER(RpcCenterCfg), vp, vp, i32, vp, vp, vp, vp, sz, vp]),
+    "rpc_center_head_loss_backward": (i32, [C.POINTER(RpcCenterCfg), vp, vp, vp, vp, vp, vp, sz, vp]),
+    "rpc_center_head_targets": (i32, [C.POINTER(RpcCenterCfg), i32, vp, C.POINTER(vp), C.POINTER(vp),
+                                      C.POINTER(vp), C.POINTER(vp)]),
     "rpc_anchor_head_workspace_size": (sz, [C.POINTER(RpcHeadCfg), i32]),
     "rpc_anchor_head_loss_forward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
     "rpc_anchor_head_loss_backward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,

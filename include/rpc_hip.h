@@ -173,6 +173,16 @@ int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const f
                     const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                     const float* fwd_bn, float* bn_out, float* dgamma, float* dbeta, void* workspace,
                     void* stream);
+/* SparseBasicBlock residual (upstream mmdet3d SparseBasicBlock.forward, the block_type='basicblock'
+ * SparseEncoder of the CenterPoint nuScenes base, adversarial-centerpoint_voxel-nuscenes.py:11-13):
+ * forward out = relu(bn(z) + res) (res may be NULL: a materialised relu(bn(z))), fp32 rows [n][c]
+ * and optionally bf16 rows [n][round8(c)]; backward m = (g1 + g2) * (out > 0) (g2 may be NULL) with
+ * the BatchNorm-backward partial sums (sum m, sum m*xhat) of z per rpc_spconv_gemm_blocks(n) rows,
+ * for rpc_bn_finalize mode 1. c <= 256. */
+int rpc_sparse_res_forward(const float* z, const float* bn, const float* res, int n, int c, float* out,
+                           void* out_bf16, void* stream);
+int rpc_sparse_res_backward(const float* g1, const float* g2, const float* out, const float* z, const float* bn,
+                            int n, int c, float* m, float* part, void* stream);
 /* SparseConvTensor.dense() of relu(bn(z)) viewed as [B, C*D, H, W] (channel c*D + z); backward
  * gathers, applies the ReLU mask and writes the BatchNorm-backward partial sums.
  * flags: RPC_DENSE_NHWC = channels_last image [B][H][W][C*D]; RPC_DENSE_BF16 = bf16 elements

@@ -9,7 +9,8 @@ is "parity unpinned" w.r.t. spconv itself: it restates spconv's published semant
   SparseConv3d: out(o) = sum_k W[k]^T in(o*s - p + k), output sites = every o reached
                 by an input; spatial out = (in + 2p - (k-1) - 1)//s + 1
   BatchNorm1d (train: batch stats, biased var; running stats with the unbiased var),
-  ReLU, `.dense()` -> [B, C, D, H, W] -> view(B, C*D, H, W)
+  ReLU, `.dense()` -> [B, C, D, H, W] -> view(B, C*D, H, W);
+  SparseBasicBlock (block_type='basicblock'): relu(bn2(conv2(relu(bn1(conv1(x))))) + x)
 with numpy index arithmetic and torch float64 autograd on CPU (gather / matmul /
 index_add). Row ORDER of intermediate sparse tensors is free (the dense output and the
 BatchNorm statistics do not depend on it).
@@ -95,6 +96,7 @@ class OracleSparseEncoder:
         c = np.asarray(coors, np.int64)
         cache = {}
         self.trace = []   # keep=True: per layer (coors, z pre-BN, pre-activation) for debugging
+        outs = []         # per layer output features (SparseBasicBlock identities)
         for sp, p in zip(self.specs, self.params):
             if sp.kind == "subm":
                 if sp.key not in cache:
@@ -117,7 +119,9 @@ class OracleSparseEncoder:
             if keep:
                 pre.retain_grad()
                 self.trace.append((c_out, z, pre))
-            x = torch.relu(pre)
+            res = getattr(sp, "res", -1)
+            x = torch.relu(pre + outs[res]) if res >= 0 else torch.relu(pre)   # SparseBasicBlock: + identity
+            outs.append(x)
             c = c_out
         D, H, W = self.shapes[-1]
         C = x.shape[1]

@@ -126,6 +126,8 @@ SIGNATURES = {
     "rpc_augment_points_workspace_size": (sz, [i32, i32]),
     "rpc_augment_points": (i32, [vp, i32, i32, vp, i32, vp, fp, i32, C.c_ulonglong, vp, vp, vp, sz, vp]),
     "rpc_augment_boxes": (i32, [vp, vp, i32, i32, vp, fp, vp]),
+    "rpc_sparse_res_forward": (i32, [vp, vp, vp, i32, i32, vp, vp, vp]),
+    "rpc_sparse_res_backward": (i32, [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
     "rpc_center_head_workspace_size": (sz, [C.POINTER(RpcCenterCfg), i32]),
     "rpc_center_head_loss_forward": (i32, [C.POINTER(RpcCenterCfg), vp, vp, i32, vp, vp, vp, vp, sz, vp]),
     "rpc_center_head_loss_backward": (i32, [C.POINTER(RpcCenterCfg), vp, vp, vp, vp, vp, vp, sz, vp]),

@@ -172,11 +172,12 @@ struct GemmArgs {
 
 template <int CI, int CO, int AT, int ET>
 __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
-  constexpr int AS = CI + 2;                       // LDS row stride of A (bank spread)
+  constexpr int CIP = (CI + 3) / 4 * 4;             // MFMA K steps of 4 (CI = 5: zero column 5..7)
+  constexpr int AS = CIP + 2;                      // LDS row stride of A (bank spread)
   constexpr int BS = (CO % 32 == 0) ? CO + 16 : CO;
   constexpr int NT = CO / 16;
   __shared__ float sA[BM * AS];
-  __shared__ float sB[CI * BS];
+  __shared__ float sB[CIP * BS];
   __shared__ int sN[BM * MAXK];
   __shared__ unsigned kmask;
   __shared__ float sP[4][2 * CO];
@@ -203,9 +204,9 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
     if (!((mask >> k) & 1u)) continue;
     __syncthreads();
     // gather A_k: BM rows x CI, transformed on load
-    for (int q = tid; q < BM * CI; q += BLK) {
-      int r = q / CI, c = q - r * CI;
-      int src = sN[r * MAXK + k];
+    for (int q = tid; q < BM * CIP; q += BLK) {
+      int r = q / CIP, c = q - r * CIP;
+      int src = c < CI ? sN[r * MAXK + k] : -1;
       float v = 0.0f;
       if (src >= 0) {
         float x = g.a[(long long)src * CI + c];
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
     }
     // B_k = W[k] (CI x CO) or W[k]^T ; zero-pad columns beyond the stored width
     const float* Wk = g.W + (long long)k * g.CIw * g.COw;
-    for (int q = tid; q < CI * CO; q += BLK) {
+    for (int q = tid; q < CIP * CO; q += BLK) {
       int c = q / CO, n = q - c * CO;
       float v = 0.0f;
       if (!g.transW) { if (c < g.CIw && n < g.COw) v = Wk[c * g.COw + n]; }
@@ -231,7 +232,7 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
     const float* pa = sA + (w * 16 + (lane & 15)) * AS + (lane >> 4);
     const float* pb = sB + (lane >> 4) * BS + (lane & 15);
 #pragma unroll 4
-    for (int kk = 0; kk < CI / 4; ++kk) {
+    for (int kk = 0; kk < CIP / 4; ++kk) {
       float a = pa[kk * 4];
 #pragma unroll
       for (int n = 0; n < NT; ++n) {
@@ -511,6 +512,67 @@ __global__ __launch_bounds__(BLK) void k_from_dense(const T* __restrict__ gd, co
   }
 }
 
+// ------------------------------------------------------------------ SparseBasicBlock residual
+// forward: out = relu(bn(z) + res) (res optional), fp32 rows and optionally bf16 rows [n][round8(C)]
+// (upstream mmdet3d SparseBasicBlock.forward: norm2, + identity, relu; also materialises a plain
+// relu(bn(z)) output that a block reads as its identity)
+__global__ __launch_bounds__(BLK) void k_res_fwd(const float* __restrict__ z, const float* __restrict__ bn,
+                                                 const float* __restrict__ res, int N, int C, int CP,
+                                                 float* __restrict__ out, unsigned short* __restrict__ hb) {
+  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= (long long)N * CP) return;
+  const int r = (int)(t / CP), c = (int)(t - (long long)r * CP);
+  float v = 0.0f;
+  if (c < C) {
+    const long long i = (long long)r * C + c;
+    v = fmaf(z[i] - bn[2 * C + c], bn[c], bn[C + c]);
+    if (res) v = v + res[i];
+    v = fmaxf(v, 0.0f);
+    out[i] = v;
+  }
+  if (hb) {
+    __bf16 b = (__bf16)v;
+    hb[t] = __builtin_bit_cast(unsigned short, b);
+  }
+}
+
+// backward: m = (g1 + g2) * (out > 0) and the BatchNorm-backward partial sums of the layer that
+// produced z (sum m, sum m * xhat) per BM rows, laid out like k_from_dense (C <= 256)
+__global__ __launch_bounds__(BLK) void k_res_bwd(const float* __restrict__ g1, const float* __restrict__ g2,
+                                                 const float* __restrict__ out, const float* __restrict__ z,
+                                                 const float* __restrict__ bn, int N, int C,
+                                                 float* __restrict__ m, float* __restrict__ part) {
+  __shared__ float sh[2][BLK];
+  const int r0 = blockIdx.x * BM, r1 = min(N, r0 + BM);
+  const int nl = BLK / C;
+  const int rl = threadIdx.x / C, c = threadIdx.x - rl * C;
+  float s1 = 0.0f, s2 = 0.0f;
+  if (rl < nl) {
+    const float mu = bn[2 * C + c], is = bn[3 * C + c];
+    for (int r = r0 + rl; r < r1; r += nl) {
+      const long long i = (long long)r * C + c;
+      float g = g1[i];
+      if (g2) g = g + g2[i];
+      const float v = out[i] > 0.0f ? g : 0.0f;
+      m[i] = v;
+      s1 += v;
+      s2 += v * ((z[i] - mu) * is);
+    }
+  }
+  sh[0][threadIdx.x] = s1;
+  sh[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (rl == 0) {
+    float t1 = sh[0][c], t2 = sh[1][c];
+    for (int k = 1; k < nl; ++k) {
+      t1 += sh[0][k * C + c];
+      t2 += sh[1][k * C + c];
+    }
+    part[(long long)blockIdx.x * 2 * C + c] = t1;
+    part[(long long)blockIdx.x * 2 * C + C + c] = t2;
+  }
+}
+
 // ------------------------------------------------------------------ dispatch
 template <int CI, int CO>
 static void launch_gemm_t(int at, int et, const GemmArgs& a, int nblk, hipStream_t st) {
@@ -525,7 +587,7 @@ static void launch_gemm_t(int at, int et, const GemmArgs& a, int nblk, hipStream
 static int launch_gemm(int CI, int CO, int at, int et, const GemmArgs& a, int nblk, hipStream_t st) {
 #define C2(ci, co) if (CI == ci && CO == co) { launch_gemm_t<ci, co>(at, et, a, nblk, st); return RPC_OK; }
   // forward pairs (CI, CO) of SparseEncoder and their dgrad transposes (CO, CI->pad16)
-  C2(4, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
+  C2(4, 16) C2(5, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
   C2(32, 16) C2(64, 32) C2(128, 64)
 #undef C2
   return RPC_ERR_UNSUPPORTED;
@@ -538,7 +600,7 @@ static int launch_wgrad(int CI, int CO, int at, const WgradArgs& a, dim3 grid, h
     else hipLaunchKernelGGL((k_wgrad<ci, co, A_RAW>), grid, dim3(BLK), 0, st, a);                 \
     return RPC_OK;                                                                               \
   }
-  C2(4, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
+  C2(4, 16) C2(5, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
 #undef C2
   return RPC_ERR_UNSUPPORTED;
 }
@@ -786,6 +848,27 @@ extern "C" int rpc_dense_to_sparse_grad(const void* grad_dense, const float* z, 
     default: hipLaunchKernelGGL((k_from_dense<__hip_bfloat16, true>), g, dim3(BLK), 0, st,
                                 (const __hip_bfloat16*)grad_dense, z, bn, coors, N, C, s, dy, part);
   }
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_sparse_res_forward(const float* z, const float* bn, const float* res, int n, int c, float* out,
+                                      void* out_bf16, void* stream) {
+  if (n < 0 || c < 1 || !z || !bn || !out) return RPC_ERR_ARG;
+  if (n == 0) return RPC_OK;
+  const int cp = (c + 7) / 8 * 8;
+  hipLaunchKernelGGL(k_res_fwd, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, res, n,
+                     c, cp, out, (unsigned short*)out_bf16);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_sparse_res_backward(const float* g1, const float* g2, const float* out, const float* z,
+                                       const float* bn, int n, int c, float* m, float* part, void* stream) {
+  if (n < 0 || c < 1 || c > 256 || !g1 || !out || !z || !bn || !m || !part) return RPC_ERR_ARG;
+  if (n == 0) return RPC_OK;
+  hipLaunchKernelGGL(k_res_bwd, dim3(cdiv(n, BM)), dim3(BLK), 0, (hipStream_t)stream, g1, g2, out, z, bn, n, c, m,
+                     part);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

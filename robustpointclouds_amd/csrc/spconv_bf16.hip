@@ -414,7 +414,7 @@ static void launch_t(int epi, const GB& a, int nblk, hipStream_t st) {
 
 static int launch(int KGP, int NT, int epi, const GB& a, int nblk, hipStream_t st) {
 #define C2(kg, nt) if (KGP == kg && NT == nt) { launch_t<kg, nt>(epi, a, nblk, st); return RPC_OK; }
-  C2(32, 1) C2(32, 2) C2(32, 4) C2(64, 2) C2(64, 4) C2(64, 8) C2(128, 4) C2(32, 8) C2(64, 1) C2(128, 2)
+  C2(32, 1) C2(32, 2) C2(32, 4) C2(64, 2) C2(64, 4) C2(64, 8) C2(128, 4) C2(32, 8) C2(64, 1) C2(128, 2) C2(128, 8)
 #undef C2
   return RPC_ERR_UNSUPPORTED;
 }
@@ -508,7 +508,7 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
                                      int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
   if (n_out < 0 || kvol < 1 || kvol > MAXK) return RPC_ERR_ARG;
   bool ok = (ci == 16 && (co == 16 || co == 32)) || (ci == 32 && (co == 32 || co == 64)) ||
-            (ci == 64 && (co == 64 || co == 128));
+            (ci == 64 && (co == 64 || co == 128)) || (ci == 128 && co == 128);
   if (!ok) return RPC_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   if (n_out == 0) {
@@ -518,7 +518,9 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
   int chunks = wgrad_chunks(n_out);
   if (ws_bytes < (size_t)chunks * kvol * ci * co * sizeof(float)) return RPC_ERR_WORKSPACE;
   int rows_per = ((n_out + chunks - 1) / chunks + 31) / 32 * 32;
-  dim3 grid(chunks, (kvol + 2) / 3);
+  // 128 x 128 tiles keep one kernel offset per block (KG = 1: 64 accumulator registers / lane)
+  const int KG = (ci == 128 && co == 128) ? 1 : 3;
+  dim3 grid(chunks, (kvol + KG - 1) / KG);
   float* part = (float*)ws;
   const u16* hp = (const u16*)h;
   const u16* dp = (const u16*)dz;
@@ -528,7 +530,11 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
     hipLaunchKernelGGL((k_wgrad_bf16<a, b, 3>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp, \
                        DP, part);                                                                     \
   } else
-  W2(16, 16) W2(16, 32) W2(32, 32) W2(32, 64) W2(64, 64) W2(64, 128) { return RPC_ERR_UNSUPPORTED; }
+  W2(16, 16) W2(16, 32) W2(32, 32) W2(32, 64) W2(64, 64) W2(64, 128)
+  if (ci == 128 && co == 128) {
+    hipLaunchKernelGGL((k_wgrad_bf16<128, 128, 1>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp,
+                       DP, part);
+  } else { return RPC_ERR_UNSUPPORTED; }
 #undef W2
   RPC_LAUNCH_CHECK();
   long long total = (long long)kvol * ci * co;

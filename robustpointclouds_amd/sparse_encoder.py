@@ -38,6 +38,8 @@ class _Spec:
     lvl_in: int
     lvl_out: int
     name: str
+    res: int = -1       # basicblock conv2: index of the layer whose output is the block identity
+    mat: bool = False   # output materialised as rows (a block output, or read as an identity)
 
     @property
     def K(self):
@@ -67,6 +69,17 @@ class _ConvBN(nn.Sequential):
         super().__init__(_ConvWeight(K, ci, co), nn.BatchNorm1d(co, eps=eps, momentum=momentum))
 
 
+class _BasicBlock(nn.Module):
+    """mmdet3d SparseBasicBlock(c, c): conv1 (SubMConv3d) + bn1 + ReLU, conv2 + bn2, + identity, ReLU."""
+
+    def __init__(self, c, eps, momentum):
+        super().__init__()
+        self.conv1 = _ConvWeight(27, c, c)
+        self.bn1 = nn.BatchNorm1d(c, eps=eps, momentum=momentum)
+        self.conv2 = _ConvWeight(27, c, c)
+        self.bn2 = nn.BatchNorm1d(c, eps=eps, momentum=momentum)
+
+
 class SparseEncoder(nn.Module):
     def __init__(self, in_channels, sparse_shape, order=("conv", "norm", "act"),
                  norm_cfg=dict(type="BN1d", eps=1e-3, momentum=0.01), base_channels=16, output_channels=128,
@@ -74,8 +87,10 @@ class SparseEncoder(nn.Module):
                  encoder_paddings=((1,), (1, 1, 1), (1, 1, 1), ((0, 1, 1), 1, 1)), block_type="conv_module",
                  return_middle_feats=False):
         super().__init__()
-        if tuple(order) != ("conv", "norm", "act") or block_type != "conv_module" or return_middle_feats:
-            raise NotImplementedError("only the SECOND configuration (conv-norm-act, conv_module) is built")
+        if tuple(order) != ("conv", "norm", "act") or block_type not in ("conv_module", "basicblock") \
+                or return_middle_feats:
+            raise NotImplementedError("conv-norm-act order with conv_module / basicblock blocks is built")
+        self.block_type = block_type
         eps = norm_cfg.get("eps", 1e-3)
         mom = norm_cfg.get("momentum", 0.01)
         self.sparse_shape = tuple(int(s) for s in sparse_shape)
@@ -88,10 +103,33 @@ class SparseEncoder(nn.Module):
         self.encoder_layers = nn.Module()
         ci = base_channels
         lvl = 0
+        nst = len(encoder_channels)
         for i, blocks in enumerate(encoder_channels):
             stage = nn.Module()
             for j, co in enumerate(tuple(blocks)):
                 pad = _t3(tuple(encoder_paddings[i])[j])
+                if block_type == "basicblock":
+                    # upstream make_encoder_layers: a stride-2 SparseConv3d closes every stage but the
+                    # last, the other entries are SparseBasicBlock(co, co) (their inputs carry co)
+                    if j == len(blocks) - 1 and i != nst - 1:
+                        out = _conv_out(shapes[lvl], (3, 3, 3), (2, 2, 2), pad)
+                        shapes.append(out)
+                        specs.append(_Spec("spconv", ci, co, (3, 3, 3), (2, 2, 2), pad, f"spconv{i + 1}", lvl,
+                                           lvl + 1, f"encoder_layers.encoder_layer{i + 1}.{j}", mat=True))
+                        stage.add_module(str(j), _ConvBN(27, ci, co, eps, mom))
+                        lvl += 1
+                    else:
+                        if ci != co:
+                            raise ValueError("SparseBasicBlock needs equal in/out channels")
+                        specs[-1].mat = True            # the block identity
+                        specs.append(_Spec("subm", co, co, (3, 3, 3), (1, 1, 1), (1, 1, 1), f"subm{i + 1}", lvl,
+                                           lvl, f"encoder_layers.encoder_layer{i + 1}.{j}.conv1"))
+                        specs.append(_Spec("subm", co, co, (3, 3, 3), (1, 1, 1), (1, 1, 1), f"subm{i + 1}", lvl,
+                                           lvl, f"encoder_layers.encoder_layer{i + 1}.{j}.conv2",
+                                           res=len(specs) - 2, mat=True))
+                        stage.add_module(str(j), _BasicBlock(co, eps, mom))
+                    ci = co
+                    continue
                 if i != 0 and j == 0:
                     out = _conv_out(shapes[lvl], (3, 3, 3), (2, 2, 2), pad)
                     shapes.append(out)
@@ -124,10 +162,15 @@ class SparseEncoder(nn.Module):
         self.dense_bf16 = False
 
     def layers(self):
-        mods = [self.conv_input]
+        """(conv weight module, BatchNorm1d) per spec, in spec order."""
+        mods = [(self.conv_input[0], self.conv_input[1])]
         for st in self.encoder_layers.children():
-            mods += list(st.children())
-        mods.append(self.conv_out)
+            for m in st.children():
+                if isinstance(m, _BasicBlock):
+                    mods += [(m.conv1, m.bn1), (m.conv2, m.bn2)]
+                else:
+                    mods.append((m[0], m[1]))
+        mods.append((self.conv_out[0], self.conv_out[1]))
         return mods
 
     def grid(self, lvl, B, device):
@@ -296,11 +339,23 @@ class SparseEncoderFn(torch.autograd.Function):
                                            _ffi.ptr(wsb), st), "rpc_bn_finalize")
             rec.update(z=z, bn=bn, W=W, gamma=gamma, beta=beta)
             L.append(rec)
-            src, src_bn = z, bn
-            if bf16 and li + 1 < len(enc.specs):
-                hsrc = torch.empty((n_out, _r8(sp.co)), dtype=torch.bfloat16, device=dev)
-                _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(z), _ffi.ptr(bn), n_out, sp.co, 1, _ffi.ptr(hsrc), st),
-                           "rpc_to_bf16_rows")
+            if sp.mat:
+                # materialised output rows: relu(bn(z) [+ block identity]) (+ the bf16 rows the next
+                # layer gathers in perf mode)
+                out = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
+                ob = (torch.empty((n_out, _r8(sp.co)), dtype=torch.bfloat16, device=dev)
+                      if bf16 and li + 1 < len(enc.specs) else None)
+                res = L[sp.res]["out"] if sp.res >= 0 else None
+                _ffi.check(lib.rpc_sparse_res_forward(_ffi.ptr(z), _ffi.ptr(bn), _ffi.ptr(res), n_out, sp.co,
+                                                      _ffi.ptr(out), _ffi.ptr(ob), st), "rpc_sparse_res_forward")
+                rec["out"] = out
+                src, src_bn, hsrc = out, None, ob
+            else:
+                src, src_bn = z, bn
+                if bf16 and li + 1 < len(enc.specs):
+                    hsrc = torch.empty((n_out, _r8(sp.co)), dtype=torch.bfloat16, device=dev)
+                    _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(z), _ffi.ptr(bn), n_out, sp.co, 1, _ffi.ptr(hsrc), st),
+                               "rpc_to_bf16_rows")
             cur_coors, cur_n = rec["coors_out"], n_out
         _ffi.bump_batches([m[1] for m in mods])
         last = L[-1]
@@ -347,10 +402,24 @@ class SparseEncoderFn(torch.autograd.Function):
                                                 _ffi.ptr(last["coors_out"]), n, C, _ffi.int_arr((B, D, H, Wd)),
                                                 flags, _ffi.ptr(dy), _ffi.ptr(part), st), "rpc_dense_to_sparse_grad")
         dfeat = None
+        G = [[] for _ in L]     # gradient contributions to materialised outputs
         for li in range(len(L) - 1, -1, -1):
             rec = L[li]
             sp = rec["spec"]
             n_out = rec["n_out"]
+            if sp.mat:
+                # d out -> ReLU mask -> d(bn output); the block identity receives the same gradient
+                g = G[li]
+                dy = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
+                nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
+                part = torch.empty((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
+                _ffi.check(lib.rpc_sparse_res_backward(_ffi.ptr(g[0]), _ffi.ptr(g[1] if len(g) > 1 else None),
+                                                       _ffi.ptr(rec["out"]), _ffi.ptr(rec["z"]), _ffi.ptr(rec["bn"]),
+                                                       n_out, sp.co, _ffi.ptr(dy), _ffi.ptr(part), st),
+                           "rpc_sparse_res_backward")
+                G[li] = None
+                if sp.res >= 0:
+                    G[sp.res].append(dy)
             if ctx.enc.debug is not None:
                 ctx.enc.debug.append((li, rec["coors_out"].cpu().numpy(), rec["z"].detach().cpu().double(),
                                       dy.detach().cpu().double()))
@@ -396,7 +465,18 @@ class SparseEncoderFn(torch.autograd.Function):
             else:
                 mp, rev = rec["nbr_in"], 0
             din = torch.empty((n_in, sp.ci), dtype=torch.float32, device=dev)
-            if li > 0:
+            if li > 0 and L[li - 1]["spec"].mat:
+                # the input is a materialised output: plain data gradient, masked by its own backward
+                if rec["bf16"]:
+                    _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                                                        _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
+                               "rpc_spconv_gemm_bf16(dgrad)")
+                else:
+                    _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
+                                                    _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
+                                                    None, _ffi.ptr(din), None, st), "rpc_spconv_dgrad")
+                G[li - 1].append(din)
+            elif li > 0:
                 prev = L[li - 1]
                 nblk = max(lib.rpc_spconv_gemm_blocks(n_in), 1)
                 part = torch.empty((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)

@@ -10,7 +10,7 @@ from robustpointclouds_amd import _ffi
 
 pytestmark = pytest.mark.gpu
 
-PAIRS = [(16, 16), (16, 32), (32, 32), (32, 64), (64, 64), (64, 128)]
+PAIRS = [(16, 16), (16, 32), (32, 32), (32, 64), (64, 64), (64, 128), (128, 128)]
 
 
 def _r8(c):

@@ -420,8 +420,32 @@ int rpc_center_head_loss_backward(const RpcCenterCfg* cfg, const float* hm, cons
 /* The training targets themselves (for tests / inspection): heatmap [B][H][W][ncls_total],
  * ind [B][ntasks][max_objs] int32, mask [B][ntasks][max_objs] int32, anno [B][ntasks][max_objs][10]
  * — views into a workspace filled by rpc_center_head_loss_forward. */
+/* Task-head final conv outputs: out[p*op + ooff + c] = z[p*zp + c] (bf16) + bias[c], c < n <= 16;
+ * backward: dz[p*zp + c] = bf16(dout[p*dp + doff + c]) (c < n, else 0) and dbias = sum_p dout. */
+int rpc_head_pack(const void* z, int zp, int n, const float* bias, float* out, int op, int ooff, long long cells,
+                  void* stream);
+size_t rpc_head_unpack_workspace_size(void);
+int rpc_head_unpack_grad(const float* dout, int dp, int doff, int n, void* dz, int zp, long long cells, float* dbias,
+                         void* workspace, size_t ws_bytes, void* stream);
 int rpc_center_head_targets(const RpcCenterCfg* cfg, int max_gts, const void* workspace, const float** heatmap,
                             const int** ind, const int** mask, const float** anno);
+
+/* ------------------------------------------------------------------ §8(f3) DCNSeparateHead deformable conv
+ * mmcv DeformConv2dPack(64, 64, kernel 3, padding 1, groups 4, deform_groups 1) of the CenterHead base
+ * (adversarial-centerpoint_voxel-nuscenes.py:11-13, DCNSeparateHead.feature_adapt_cls / _reg):
+ * x, out: bf16 NHWC images (64 channels at pitch xp / op); off: the offset conv's bf16 output image
+ * (pitch offp, channels 0..17 = (dy, dx) per tap k = 3i + j) to which off_bias [18] is added here.
+ * W [64][16][3][3] fp32 -> rpc_dcn_prep_weight -> w_fwd / w_bwd (bf16 [9][64][64] each).
+ * Backward: dx fp32 [B*H*W][64] is ACCUMULATED (atomics; zero it first), doff = the offset conv's
+ * output gradient (bf16 image, pitch doffp >= 64, channels >= 18 written as zero), doff_bias [18] and
+ * dW [64][16][3][3] are written. H and W must be multiples of 8. */
+int rpc_dcn_prep_weight(const float* W, void* w_fwd, void* w_bwd, void* stream);
+int rpc_dcn_forward(const void* x, int xp, const void* off, int offp, const float* off_bias, const void* w_fwd,
+                    void* out, int op, int B, int H, int W, void* stream);
+size_t rpc_dcn_backward_workspace_size(int B, int H, int W);
+int rpc_dcn_backward(const void* x, int xp, const void* off, int offp, const float* off_bias, const void* w_bwd,
+                     const void* dout, int dop, float* dx, void* doff, int doffp, float* doff_bias, float* dW,
+                     int B, int H, int W, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -126,6 +126,13 @@ SIGNATURES = {
     "rpc_augment_points_workspace_size": (sz, [i32, i32]),
     "rpc_augment_points": (i32, [vp, i32, i32, vp, i32, vp, fp, i32, C.c_ulonglong, vp, vp, vp, sz, vp]),
     "rpc_augment_boxes": (i32, [vp, vp, i32, i32, vp, fp, vp]),
+    "rpc_head_pack": (i32, [vp, i32, i32, vp, vp, i32, i32, C.c_longlong, vp]),
+    "rpc_head_unpack_workspace_size": (sz, []),
+    "rpc_head_unpack_grad": (i32, [vp, i32, i32, i32, vp, i32, C.c_longlong, vp, vp, sz, vp]),
+    "rpc_dcn_prep_weight": (i32, [vp, vp, vp, vp]),
+    "rpc_dcn_forward": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),
+    "rpc_dcn_backward_workspace_size": (sz, [i32, i32, i32]),
+    "rpc_dcn_backward": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, sz, vp]),
     "rpc_sparse_res_forward": (i32, [vp, vp, vp, i32, i32, vp, vp, vp]),
     "rpc_sparse_res_backward": (i32, [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
     "rpc_center_head_workspace_size": (sz, [C.POINTER(RpcCenterCfg), i32]),

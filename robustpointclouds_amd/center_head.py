@@ -124,3 +124,325 @@ def center_targets(cfg, ws, maxg):
 
     return (view(ptrs[0], torch.float32, (B, H, W, N)), view(ptrs[1], torch.int32, (B, T, MO)),
             view(ptrs[2], torch.int32, (B, T, MO)), view(ptrs[3], torch.float32, (B, T, MO, 10)))
+
+
+# ---------------------------------------------------------------------- CenterHead module (HIP)
+import math  # noqa: E402
+
+from torch import nn  # noqa: E402
+
+from . import dense_bev as db  # noqa: E402
+
+NUS_COMMON_HEADS = dict(reg=(2, 2), height=(1, 2), dim=(3, 2), rot=(2, 2), vel=(2, 2))
+_BOX_ORDER = ("reg", "height", "dim", "rot", "vel")     # anno_box channel order (loss_by_feat concat)
+_PAD = 64                                               # padded output width of the small convs
+
+
+class ConvModule(nn.Module):
+    """mmcv ConvModule(conv 3x3 no bias, BN2d (eps 1e-5, momentum 0.1), ReLU) — kaiming fan_out init."""
+
+    def __init__(self, ci, co):
+        super().__init__()
+        self.conv = nn.Conv2d(ci, co, 3, padding=1, bias=False)
+        self.bn = nn.BatchNorm2d(co)
+        nn.init.kaiming_normal_(self.conv.weight, mode="fan_out", nonlinearity="relu")
+
+
+class DeformConv2dPack(nn.Module):
+    """mmcv DeformConv2dPack(64, 64, 3, padding=1, groups=4): weight [64, 16, 3, 3] (uniform
+    1/sqrt(in*k*k)), conv_offset = Conv2d(64, 18, 3, padding 1, bias) zero-initialised."""
+
+    def __init__(self, in_channels=64, out_channels=64, kernel_size=3, padding=1, groups=4):
+        super().__init__()
+        if (in_channels, out_channels, kernel_size, padding, groups) != (64, 64, 3, 1, 4):
+            raise NotImplementedError("the HIP DCN is built for DCN(64 -> 64, k 3, pad 1, groups 4)")
+        self.groups = groups
+        self.weight = nn.Parameter(torch.empty(out_channels, in_channels // groups, kernel_size, kernel_size))
+        stdv = 1.0 / math.sqrt(in_channels * kernel_size * kernel_size)
+        nn.init.uniform_(self.weight, -stdv, stdv)
+        self.conv_offset = nn.Conv2d(in_channels, 2 * kernel_size * kernel_size, kernel_size, padding=padding,
+                                     bias=True)
+        nn.init.zeros_(self.conv_offset.weight)
+        nn.init.zeros_(self.conv_offset.bias)
+
+
+def _final_conv(ci, n, bias_fill=None):
+    c = nn.Conv2d(ci, n, 3, padding=1, bias=True)
+    if bias_fill is None:
+        nn.init.kaiming_normal_(c.weight, mode="fan_out", nonlinearity="relu")
+        nn.init.zeros_(c.bias)
+    else:
+        nn.init.constant_(c.bias, bias_fill)
+    return c
+
+
+class SeparateHead(nn.Module):
+    """mmdet3d SeparateHead (num_conv 2, final_kernel 3): per head ConvModule + Conv2d(64 -> n, bias)."""
+
+    def __init__(self, in_channels, heads, head_conv=64):
+        super().__init__()
+        self.heads = dict(heads)
+        for name, (n, num_conv) in self.heads.items():
+            if num_conv != 2:
+                raise NotImplementedError("SeparateHead with num_conv = 2 is built")
+            self.add_module(name, nn.Sequential(ConvModule(in_channels, head_conv), _final_conv(head_conv, n)))
+
+
+class DCNSeparateHead(nn.Module):
+    """mmdet3d DCNSeparateHead: feature_adapt_cls / _reg (DCN), cls_head (ConvModule + Conv2d, bias
+    init_bias), task_head (SeparateHead on the reg features)."""
+
+    def __init__(self, in_channels, num_cls, heads, head_conv=64, init_bias=-2.19):
+        super().__init__()
+        heads = {k: v for k, v in dict(heads).items() if k != "heatmap"}
+        self.feature_adapt_cls = DeformConv2dPack(in_channels, in_channels)
+        self.feature_adapt_reg = DeformConv2dPack(in_channels, in_channels)
+        self.cls_head = nn.Sequential(ConvModule(in_channels, head_conv), _final_conv(head_conv, num_cls, init_bias))
+        self.task_head = SeparateHead(in_channels, heads, head_conv)
+        self.num_cls = num_cls
+
+
+def _imgs(B, H, W):
+    return (B, H, W), (B, H, W), (B, H, W)
+
+
+def _conv_nobn_fwd(lib, weight, ci, h, pitch, B, H, W, dev, st):
+    """3x3 conv (no BN) on the dense engine with the outputs padded to 64 -> (z image, record)."""
+    n = weight.shape[0]
+    W32 = torch.zeros((_PAD, ci, 3, 3), dtype=torch.float32, device=dev)
+    W32[:n] = weight.detach().float()
+    wf = torch.empty((9, _PAD, ci), dtype=torch.bfloat16, device=dev)
+    wd = torch.empty((9, ci, _PAD), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_dense_wprep(_ffi.ptr(W32), 0, ci, _PAD, 9, 1, _ffi.ptr(wf), _ffi.ptr(wd), st), "rpc_dense_wprep")
+    z = db._image(B, _PAD, H, W, dev)
+    R = _ffi.int_arr((B, H, W))
+    _ffi.check(db._conv(lib, db.S1, _ffi.ptr(h), pitch, ci, _ffi.ptr(wf), _PAD, _ffi.ptr(z), _PAD, 0, 0, None, R, R, R,
+                        st), "rpc_dense_conv")
+    return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, B=B, H=H, W=W)
+
+
+def _conv_nobn_bwd(lib, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=False):
+    ci, B, H, W = rec["ci"], rec["B"], rec["H"], rec["W"]
+    R = _ffi.int_arr((B, H, W))
+    dW = torch.empty((_PAD, ci, 3, 3), dtype=torch.float32, device=dev)
+    wsz = lib.rpc_dense_wgrad_workspace_size(db.S1, R, ci, _PAD)
+    ws = _ffi.workspace(wsz, dev)
+    _ffi.check(lib.rpc_dense_wgrad(db.S1, 0, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), _PAD, _PAD, R, R, R,
+                                   _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
+    dx = None
+    if need_dx:
+        dx = dx_out if dx_out is not None else db._image(B, ci, H, W, dev)
+        _ffi.check(db._conv(lib, db.S1, _ffi.ptr(dz), _PAD, _PAD, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
+                            1 if accumulate else 0, None, R, R, R, st), "rpc_dense_conv(dgrad)")
+    return dx, dW[:rec["n"]]
+
+
+def _conv_module_layer(cm):
+    return db._Layer(db.S1, cm.conv, cm.bn, 0, cm.conv.in_channels, cm.conv.out_channels, 9)
+
+
+class CenterHeadFn(torch.autograd.Function):
+    """The whole CenterHead (shared conv + every DCNSeparateHead) as one node: neck image ->
+    (hm [cells, hm_pitch], box [cells, box_pitch]) fp32; the shared feature gradient is accumulated in
+    fp32 (DCN input gradients) plus bf16 (offset-conv data gradients)."""
+
+    @staticmethod
+    def forward(ctx, x, head, *params):
+        lib = _ffi.load()
+        dev = x.device
+        st = _ffi.stream_of(x)
+        xi = db._nhwc(x)
+        B, Cin, H, W = xi.shape
+        if H % 8 or W % 8:
+            raise RuntimeError("HIP CenterHead needs a feature map with H, W multiples of 8")
+        training = head.training
+        cells = B * H * W
+        hm = torch.empty((cells, head.hm_pitch), dtype=torch.float32, device=dev)
+        box = torch.empty((cells, head.box_pitch), dtype=torch.float32, device=dev)
+        Lsh = _conv_module_layer(head.shared_conv)
+        y0, rsh, _, _ = db._forward_layer(lib, Lsh, xi, Cin, B, H, W, training, dev, st)
+        bns = [head.shared_conv.bn]
+        trecs = []
+        c0 = 0
+        for t, th in enumerate(head.task_heads):
+            tr = {}
+            for br, dcn in (("cls", th.feature_adapt_cls), ("reg", th.feature_adapt_reg)):
+                oz, orec = _conv_nobn_fwd(lib, dcn.conv_offset.weight, 64, y0, 64, B, H, W, dev, st)
+                wf = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=dev)
+                wdd = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=dev)
+                _ffi.check(lib.rpc_dcn_prep_weight(_ffi.ptr(dcn.weight.detach().float().contiguous()), _ffi.ptr(wf),
+                                                   _ffi.ptr(wdd), st), "rpc_dcn_prep_weight")
+                ob = dcn.conv_offset.bias.detach().float().contiguous()
+                feat = db._image(B, 64, H, W, dev)
+                _ffi.check(lib.rpc_dcn_forward(_ffi.ptr(y0), 64, _ffi.ptr(oz), _PAD, _ffi.ptr(ob), _ffi.ptr(wf),
+                                               _ffi.ptr(feat), 64, B, H, W, st), "rpc_dcn_forward")
+                tr[br] = dict(dcn=dcn, oz=oz, orec=orec, wd=wdd, ob=ob, feat=feat)
+            # cls branch -> heatmap logits
+            L = _conv_module_layer(th.cls_head[0])
+            hcls, rc, _, _ = db._forward_layer(lib, L, tr["cls"]["feat"], 64, B, H, W, training, dev, st)
+            bns.append(th.cls_head[0].bn)
+            fc = th.cls_head[1]
+            z, frec = _conv_nobn_fwd(lib, fc.weight, 64, hcls, 64, B, H, W, dev, st)
+            _ffi.check(lib.rpc_head_pack(_ffi.ptr(z), _PAD, th.num_cls, _ffi.ptr(fc.bias.detach().float().contiguous()),
+                                         _ffi.ptr(hm), head.hm_pitch, c0, cells, st), "rpc_head_pack")
+            tr["cls_layers"] = (rc, frec, fc, c0, th.num_cls, hm, head.hm_pitch)
+            c0 += th.num_cls
+            # reg branches -> anno_box channels
+            regs, bo = [], 10 * t
+            for name in _BOX_ORDER:
+                seq = getattr(th.task_head, name)
+                L = _conv_module_layer(seq[0])
+                hr, rr, _, _ = db._forward_layer(lib, L, tr["reg"]["feat"], 64, B, H, W, training, dev, st)
+                bns.append(seq[0].bn)
+                fcv = seq[1]
+                n = fcv.weight.shape[0]
+                z, frec = _conv_nobn_fwd(lib, fcv.weight, 64, hr, 64, B, H, W, dev, st)
+                _ffi.check(lib.rpc_head_pack(_ffi.ptr(z), _PAD, n, _ffi.ptr(fcv.bias.detach().float().contiguous()),
+                                             _ffi.ptr(box), head.box_pitch, bo, cells, st), "rpc_head_pack")
+                regs.append((rr, frec, fcv, bo, n))
+                bo += n
+            tr["regs"] = regs
+            trecs.append(tr)
+        if training:
+            _ffi.bump_batches(bns)
+        ctx.head, ctx.rsh, ctx.trecs = head, rsh, trecs
+        ctx.shape = (B, H, W, Cin)
+        ctx.param_list = params
+        ctx.need_x = ctx.needs_input_grad[0]
+        return hm, box
+
+    @staticmethod
+    def backward(ctx, ghm, gbox):
+        lib = _ffi.load()
+        B, H, W, Cin = ctx.shape
+        g_any = ghm if ghm is not None else gbox
+        dev = g_any.device
+        st = _ffi.stream_of(g_any)
+        cells = B * H * W
+        head = ctx.head
+        ghm = ghm.contiguous() if ghm is not None else torch.zeros((cells, head.hm_pitch), device=dev)
+        gbox = gbox.contiguous() if gbox is not None else torch.zeros((cells, head.box_pitch), device=dev)
+        grads = {}
+        uwsz = lib.rpc_head_unpack_workspace_size()
+        uws = _ffi.workspace(uwsz, dev)
+        dY0f = torch.zeros((cells, 64), dtype=torch.float32, device=dev)     # DCN input gradients
+        dY0b = None                                                           # offset-conv data gradients
+        dwsz = lib.rpc_dcn_backward_workspace_size(B, H, W)
+        dws = _ffi.workspace(dwsz, dev)
+
+        def head_branch(rec_cm, frec, conv, g, gp, off, n, dfeat, acc):
+            dz = db._image(B, _PAD, H, W, dev)
+            db_ = torch.empty(n, dtype=torch.float32, device=dev)
+            _ffi.check(lib.rpc_head_unpack_grad(_ffi.ptr(g), gp, off, n, _ffi.ptr(dz), _PAD, cells, _ffi.ptr(db_),
+                                                _ffi.ptr(uws), uwsz, st), "rpc_head_unpack_grad")
+            dh, dW = _conv_nobn_bwd(lib, frec, dz, dev, st)
+            grads[id(conv.weight)], grads[id(conv.bias)] = dW, db_
+            dfeat, dWc, dg, dbt = db._backward_layer(lib, rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
+            L = rec_cm["L"]
+            grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWc, dg, dbt
+            return dfeat
+
+        for t, tr in enumerate(ctx.trecs):
+            rc, frec, fc, c0, ncls, _, hp = tr["cls_layers"]
+            dfc = head_branch(rc, frec, fc, ghm, hp, c0, ncls, None, False)
+            dfr = None
+            for i, (rr, frec2, fcv, bo, n) in enumerate(tr["regs"]):
+                dfr = head_branch(rr, frec2, fcv, gbox, head.box_pitch, bo, n, dfr, i > 0)
+            for br, dfeat in (("cls", dfc), ("reg", dfr)):
+                d = tr[br]
+                doff = db._image(B, _PAD, H, W, dev)
+                dob = torch.empty(18, dtype=torch.float32, device=dev)
+                dWd = torch.empty((64, 16, 3, 3), dtype=torch.float32, device=dev)
+                _ffi.check(lib.rpc_dcn_backward(_ffi.ptr(d["orec"]["h"]), 64, _ffi.ptr(d["oz"]),
+                                                _PAD, _ffi.ptr(d["ob"]), _ffi.ptr(d["wd"]), _ffi.ptr(dfeat), 64,
+                                                _ffi.ptr(dY0f), _ffi.ptr(doff), _PAD, _ffi.ptr(dob), _ffi.ptr(dWd), B, H,
+                                                W, _ffi.ptr(dws), dwsz, st), "rpc_dcn_backward")
+                dcn = d["dcn"]
+                grads[id(dcn.weight)] = dWd
+                grads[id(dcn.conv_offset.bias)] = dob
+                first = dY0b is None
+                dY0b, dWo = _conv_nobn_bwd(lib, d["orec"], doff, dev, st, True, dY0b, not first)
+                grads[id(dcn.conv_offset.weight)] = dWo
+        dY0 = (dY0f + dY0b.permute(0, 2, 3, 1).reshape(cells, 64).float()).to(torch.bfloat16)
+        dY0 = dY0.view(B, H, W, 64).permute(0, 3, 1, 2)
+        dx, dWs, dgs, dbs = db._backward_layer(lib, ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
+        L = ctx.rsh["L"]
+        grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWs, dgs, dbs
+        ctx.trecs = ctx.rsh = None
+        return (dx, None) + tuple(grads.get(id(p)) for p in ctx.param_list)
+
+
+class CenterHead(nn.Module):
+    """upstream mmdet3d CenterHead with DCNSeparateHead task heads (nuScenes base of
+    adversarial-centerpoint_voxel-nuscenes.py:11-13), on the HIP kernels only (no torch path):
+    forward -> per-task prediction dicts (NCHW views of the packed fp32 head buffers);
+    loss_by_feat -> CenterLossFn (csrc/center_head.hip). Parameter names follow mmdet3d."""
+
+    def __init__(self, in_channels=512, tasks=None, common_heads=None, share_conv_channel=64, train_cfg=None,
+                 test_cfg=None, norm_bbox=True, loss_cls_weight=1.0, loss_bbox_weight=0.25, init_bias=-2.19,
+                 **kwargs):
+        super().__init__()
+        tasks = tasks or [dict(num_class=len(t), class_names=list(t)) for t in NUS_TASKS]
+        self.class_names = [tuple(t["class_names"]) for t in tasks]
+        self.num_classes = [len(c) for c in self.class_names]
+        common_heads = dict(common_heads or NUS_COMMON_HEADS)
+        if tuple(common_heads) != _BOX_ORDER:
+            raise NotImplementedError("common_heads must be reg, height, dim, rot, vel (nuScenes)")
+        self.shared_conv = ConvModule(in_channels, share_conv_channel)
+        self.task_heads = nn.ModuleList([DCNSeparateHead(share_conv_channel, n, common_heads, 64, init_bias)
+                                         for n in self.num_classes])
+        self.train_cfg = dict(NUS_TRAIN_CFG, **(train_cfg or {}))
+        self.test_cfg = test_cfg
+        self.norm_bbox = norm_bbox
+        self.loss_cls_weight, self.loss_bbox_weight = loss_cls_weight, loss_bbox_weight
+        self.hm_pitch = sum(self.num_classes)
+        self.box_pitch = 10 * len(self.num_classes)
+
+    def hip_params(self):
+        return [p for p in self.parameters()]
+
+    def forward(self, feats):
+        x = feats[0] if isinstance(feats, (list, tuple)) else feats
+        if not x.is_cuda:
+            raise RuntimeError("CenterHead runs on the HIP kernels only (no CPU path)")
+        hm, box = CenterHeadFn.apply(x, self, *self.hip_params())
+        B, _, H, W = x.shape
+        hm4, box4 = hm.view(B, H, W, -1), box.view(B, H, W, -1)
+        preds, c0 = [], 0
+        for t, n in enumerate(self.num_classes):
+            d, bo = {}, 10 * t
+            for name, w in zip(_BOX_ORDER, (2, 1, 3, 2, 2)):
+                d[name] = box4[..., bo:bo + w].permute(0, 3, 1, 2)
+                bo += w
+            d["heatmap"] = hm4[..., c0:c0 + n].permute(0, 3, 1, 2)
+            d["_packed"] = (hm, box, B, H, W)
+            c0 += n
+            preds.append([d])
+        return tuple(preds)
+
+    def loss_by_feat(self, preds_dicts, batch_gt_instances_3d, *args, **kwargs):
+        hm, box, B, H, W = preds_dicts[0][0]["_packed"]
+        boxes = [g.bboxes_3d if hasattr(g, "bboxes_3d") else g["bboxes_3d"] for g in batch_gt_instances_3d]
+        labels = [g.labels_3d if hasattr(g, "labels_3d") else g["labels_3d"] for g in batch_gt_instances_3d]
+        boxes = [getattr(b, "tensor", b) for b in boxes]
+        gb, gl = pack_gt(boxes, labels, hm.device)
+        cfg = center_cfg([tuple(c) for c in self.class_names], self.train_cfg, B, H, W, self.hm_pitch, self.box_pitch,
+                         self.norm_bbox, self.loss_cls_weight, self.loss_bbox_weight)
+        lv = CenterLossFn.apply(hm, box, gb, gl, cfg)
+        out = {}
+        for t in range(len(self.num_classes)):
+            out[f"task{t}.loss_heatmap"] = lv[2 * t]
+            out[f"task{t}.loss_bbox"] = lv[2 * t + 1]
+        out = PackedCenterLosses(out)
+        out.packed = lv
+        return out
+
+    def loss(self, feats, batch_data_samples, **kwargs):
+        preds = self(feats)
+        return self.loss_by_feat(preds, [s.gt_instances_3d if hasattr(s, "gt_instances_3d") else s["gt_instances_3d"]
+                                         for s in batch_data_samples])
+
+
+class PackedCenterLosses(dict):
+    """task{t}.loss_heatmap / loss_bbox dict that also carries the device vector they are views of."""
+    packed = None

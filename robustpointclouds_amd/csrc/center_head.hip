@@ -402,3 +402,91 @@ extern "C" int rpc_center_head_loss_backward(const RpcCenterCfg* cfg, const floa
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
+
+// ------------------------------------------------------------------ head output packing
+// The final 3x3 convolutions of the task heads run on the dense engine with their outputs padded to
+// 64 channels (bf16 z); their bias is added here while the n real channels are packed into the fp32
+// head buffers the loss reads (hm / box at a channel offset). Backward: the fp32 gradient slice
+// becomes the bf16 dz image (padding channels zero) and dbias (fixed-order two-level sums).
+namespace rpc {
+namespace ctr {
+constexpr int PACK_NB = 256;
+
+__global__ __launch_bounds__(BLK) void k_pack(const unsigned short* __restrict__ z, int zp, int n,
+                                              const float* __restrict__ bias, float* __restrict__ out, int op,
+                                              int ooff, long long cells) {
+  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e >= cells * n) return;
+  const long long p = e / n;
+  const int c = (int)(e - p * n);
+  out[p * op + ooff + c] = __uint_as_float((unsigned)z[p * zp + c] << 16) + bias[c];
+}
+
+__global__ __launch_bounds__(BLK) void k_unpack(const float* __restrict__ d, int dp, int doff, int n,
+                                                unsigned short* __restrict__ dz, int zp, long long cells,
+                                                float* __restrict__ part) {
+  __shared__ float sh[BLK / 64][16];
+  const long long per = (cells + gridDim.x - 1) / gridDim.x;
+  const long long p0 = (long long)blockIdx.x * per, p1 = min(cells, p0 + per);
+  float acc[16];
+#pragma unroll
+  for (int c = 0; c < 16; ++c) acc[c] = 0.0f;
+  for (long long p = p0 + threadIdx.x; p < p1; p += BLK) {
+    for (int c = 0; c < zp; c += 8) {
+      unsigned w[4];
+#pragma unroll
+      for (int h = 0; h < 4; ++h) {
+        const int c0 = c + 2 * h;
+        const float a = c0 < n ? d[p * dp + doff + c0] : 0.0f;
+        const float b = c0 + 1 < n ? d[p * dp + doff + c0 + 1] : 0.0f;
+        w[h] = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)a) |
+               ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
+      }
+      *(uint4*)(dz + p * zp + c) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+#pragma unroll
+    for (int c = 0; c < 16; ++c)
+      if (c < n) acc[c] += d[p * dp + doff + c];
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int c = 0; c < 16; ++c) {
+    const float v = wave_sum(acc[c]);
+    if (lane == 0) sh[wv][c] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < n) {
+    float s = 0.0f;
+    for (int k = 0; k < BLK / 64; ++k) s += sh[k][threadIdx.x];
+    part[(size_t)blockIdx.x * n + threadIdx.x] = s;
+  }
+}
+}  // namespace ctr
+}  // namespace rpc
+
+extern "C" int rpc_head_pack(const void* z, int zp, int n, const float* bias, float* out, int op, int ooff,
+                             long long cells, void* stream) {
+  if (!z || !bias || !out || n < 1 || n > 16 || zp < n || op < ooff + n || cells < 0) return RPC_ERR_ARG;
+  if (cells == 0) return RPC_OK;
+  hipLaunchKernelGGL(k_pack, dim3((unsigned)((cells * n + BLK - 1) / BLK)), dim3(BLK), 0, (hipStream_t)stream,
+                     (const unsigned short*)z, zp, n, bias, out, op, ooff, cells);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" size_t rpc_head_unpack_workspace_size(void) { return (size_t)PACK_NB * 16 * sizeof(float); }
+
+extern "C" int rpc_head_unpack_grad(const float* dout, int dp, int doff, int n, void* dz, int zp, long long cells,
+                                    float* dbias, void* workspace, size_t ws_bytes, void* stream) {
+  if (!dout || !dz || !dbias || !workspace || n < 1 || n > 16 || zp < n || (zp & 7) || dp < doff + n || cells < 1)
+    return RPC_ERR_ARG;
+  if (ws_bytes < rpc_head_unpack_workspace_size()) return RPC_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)(cells < PACK_NB * 64 ? (cells + 63) / 64 : PACK_NB);
+  hipLaunchKernelGGL(k_unpack, dim3(nb), dim3(BLK), 0, st, dout, dp, doff, n, (unsigned short*)dz, zp, cells,
+                     (float*)workspace);
+  RPC_LAUNCH_CHECK();
+  slab_reduce((const float*)workspace, nb, n, dbias, st);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}

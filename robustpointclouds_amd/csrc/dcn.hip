@@ -1,0 +1,454 @@
+// §8(f3): the deformable convolutions of the CenterPoint DCNSeparateHead, for gfx950.
+//
+// mmcv DeformConv2dPack as built by the CenterHead base of
+// configs/adversarial/adversarial-centerpoint_voxel-nuscenes.py:11-13 (separate_head = DCNSeparateHead,
+// dcn_config = DCN(64 -> 64, kernel 3, padding 1, groups 4), deform_groups 1): for output pixel p and
+// tap k = (i, j) the input is sampled bilinearly at (y - 1 + i + dy_k, x - 1 + j + dx_k), with the
+// offsets (dy_k, dx_k) = channels (2k, 2k+1) of the offset convolution (its bias added here); a sample
+// point outside (-1, H) x (-1, W) reads 0, corners outside the image read 0 (mmcv
+// deformable_im2col_bilinear). Output channel co uses input channels of its group (16 each).
+//
+// Tiles are 8 x 8 output pixels. The 12 x 12 input window every |offset| < 1 sample of the tile can
+// touch is staged in LDS once (bf16, 64 channels); corners outside it are read from global memory.
+//   forward:  per tap, 256 threads sample the tile's 64 x 64 column block into LDS (thread = pixel x
+//             group), 4 waves multiply it by the tap's block-diagonal 64 x 64 weight (bf16 MFMA
+//             16x16x32, fp32 accumulate over the 9 taps), bf16 output image.
+//   backward: per tap, the same sampling, dcol = dOut x W_k (MFMA), dW_k's four diagonal 16 x 16
+//             blocks += dOut^T x col (one wave per group, MFMA over the 64 pixels), then each thread
+//             forms the offset gradient (mmcv get_coordinate_weight) and scatters the input gradient
+//             (bilinear weights) into an fp32 LDS copy of the window (corners outside: global
+//             atomics); the window is flushed with global atomics once per tile.
+#include <hip/hip_runtime.h>
+#include <math.h>
+
+#include "common.h"
+
+namespace rpc {
+namespace dcn {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+typedef unsigned short u16;
+
+constexpr int BLK = 256;
+constexpr int C = 64;          // channels in and out
+constexpr int CG = 16;         // channels per group
+constexpr int KT = 9;          // taps
+constexpr int TE = 8;          // output tile edge
+constexpr int WE = TE + 4;     // input window edge (covers floor(y - 1 + i + dy) .. +1 for |dy| < 1)
+constexpr int WR = WE * WE;    // window pixels (144)
+constexpr int PW = C + 8;      // window LDS pitch (elements)
+constexpr int P = C + 16;      // tile LDS pitch (elements, conflict-free transposed reads)
+
+__device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
+__device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float((unsigned)h << 16); }
+__device__ __forceinline__ s16x4 tr_read(const u16* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
+}
+
+struct Geo {
+  int B, H, W, TY, TX;
+};
+
+struct Tile {
+  int b, y0, x0;
+};
+
+__device__ __forceinline__ Tile tile_of(const Geo& g, int t) {
+  const int b = t / (g.TY * g.TX), r = t - b * g.TY * g.TX;
+  return Tile{b, (r / g.TX) * TE, (r % g.TX) * TE};
+}
+
+// stage the 12 x 12 x 64 input window (zero outside the image)
+__device__ __forceinline__ void stage_window(const Geo& g, const Tile& tl, const u16* __restrict__ x, int xp,
+                                             u16* sXw) {
+  for (int q = threadIdx.x; q < WR * 8; q += BLK) {
+    const int wp = q >> 3, seg = q & 7;
+    const int hy = tl.y0 - 2 + wp / WE, hx = tl.x0 - 2 + wp % WE;
+    uint4 v = make_uint4(0u, 0u, 0u, 0u);
+    if (hy >= 0 && hy < g.H && hx >= 0 && hx < g.W)
+      v = *(const uint4*)(x + ((size_t)(tl.b * g.H + hy) * g.W + hx) * xp + seg * 8);
+    *(uint4*)&sXw[wp * PW + seg * 8] = v;
+  }
+}
+
+// the 16 channels [16q, 16q+16) of input pixel (cy, cx) (caller checks the image bounds)
+__device__ __forceinline__ void fetch16(const Geo& g, const Tile& tl, const u16* __restrict__ x, int xp,
+                                        const u16* sXw, int cy, int cx, int q, float* v) {
+  const int wy = cy - (tl.y0 - 2), wx = cx - (tl.x0 - 2);
+  uint4 a, b;
+  if (wy >= 0 && wy < WE && wx >= 0 && wx < WE) {
+    const u16* p = sXw + (wy * WE + wx) * PW + q * CG;
+    a = *(const uint4*)p;
+    b = *(const uint4*)(p + 8);
+  } else {
+    const u16* p = x + ((size_t)(tl.b * g.H + cy) * g.W + cx) * xp + q * CG;
+    a = *(const uint4*)p;
+    b = *(const uint4*)(p + 8);
+  }
+  const unsigned w[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    v[2 * i] = __uint_as_float(w[i] << 16);
+    v[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+
+// sample geometry of (pixel, tap): mmcv deformable_im2col_bilinear / get_coordinate_weight
+struct Samp {
+  int valid, hl, wl;
+  float lh, lw, hh, hw;
+  int c1, c2, c3, c4;
+};
+
+__device__ __forceinline__ Samp samp(const Geo& g, int y, int x, int k, float dy, float dx) {
+  Samp s;
+  const float ph = (float)(y - 1 + k / 3) + dy, pw = (float)(x - 1 + k % 3) + dx;
+  s.valid = ph > -1.0f && pw > -1.0f && ph < (float)g.H && pw < (float)g.W;
+  const float fh = floorf(ph), fw = floorf(pw);
+  s.hl = (int)fh;
+  s.wl = (int)fw;
+  s.lh = ph - fh;
+  s.lw = pw - fw;
+  s.hh = 1.0f - s.lh;
+  s.hw = 1.0f - s.lw;
+  s.c1 = s.hl >= 0 && s.wl >= 0;
+  s.c2 = s.hl >= 0 && s.wl + 1 <= g.W - 1;
+  s.c3 = s.hl + 1 <= g.H - 1 && s.wl >= 0;
+  s.c4 = s.hl + 1 <= g.H - 1 && s.wl + 1 <= g.W - 1;
+  return s;
+}
+
+__device__ __forceinline__ void offsets(const u16* __restrict__ off, int offp, const float* __restrict__ ob,
+                                        size_t pix, int k, float* dy, float* dx) {
+  *dy = bf2f(off[pix * offp + 2 * k]) + ob[2 * k];
+  *dx = bf2f(off[pix * offp + 2 * k + 1]) + ob[2 * k + 1];
+}
+
+// col values of one (pixel, tap, group): bilinear of the four corners
+__device__ __forceinline__ void sample16(const Geo& g, const Tile& tl, const u16* __restrict__ x, int xp,
+                                         const u16* sXw, const Samp& s, int q, float* col) {
+#pragma unroll
+  for (int c = 0; c < CG; ++c) col[c] = 0.0f;
+  if (!s.valid) return;
+  float v[CG];
+  const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
+  if (s.c1) {
+    fetch16(g, tl, x, xp, sXw, s.hl, s.wl, q, v);
+#pragma unroll
+    for (int c = 0; c < CG; ++c) col[c] = w1 * v[c];
+  }
+  if (s.c2) {
+    fetch16(g, tl, x, xp, sXw, s.hl, s.wl + 1, q, v);
+#pragma unroll
+    for (int c = 0; c < CG; ++c) col[c] += w2 * v[c];
+  }
+  if (s.c3) {
+    fetch16(g, tl, x, xp, sXw, s.hl + 1, s.wl, q, v);
+#pragma unroll
+    for (int c = 0; c < CG; ++c) col[c] += w3 * v[c];
+  }
+  if (s.c4) {
+    fetch16(g, tl, x, xp, sXw, s.hl + 1, s.wl + 1, q, v);
+#pragma unroll
+    for (int c = 0; c < CG; ++c) col[c] += w4 * v[c];
+  }
+}
+
+__device__ __forceinline__ void store_col(u16* sC, int p, int q, const float* col) {
+  uint4 a, b;
+  a.x = f2bf(col[0]) | ((unsigned)f2bf(col[1]) << 16);
+  a.y = f2bf(col[2]) | ((unsigned)f2bf(col[3]) << 16);
+  a.z = f2bf(col[4]) | ((unsigned)f2bf(col[5]) << 16);
+  a.w = f2bf(col[6]) | ((unsigned)f2bf(col[7]) << 16);
+  b.x = f2bf(col[8]) | ((unsigned)f2bf(col[9]) << 16);
+  b.y = f2bf(col[10]) | ((unsigned)f2bf(col[11]) << 16);
+  b.z = f2bf(col[12]) | ((unsigned)f2bf(col[13]) << 16);
+  b.w = f2bf(col[14]) | ((unsigned)f2bf(col[15]) << 16);
+  *(uint4*)&sC[p * P + q * CG] = a;
+  *(uint4*)&sC[p * P + q * CG + 8] = b;
+}
+
+// weights: W [64 co][16 ci_l][3][3] fp32 -> wf [9][64 co][64 ci] and wd [9][64 ci][64 co], bf16,
+// zero outside the diagonal group blocks
+__global__ __launch_bounds__(BLK) void k_prep(const float* __restrict__ W, u16* __restrict__ wf, u16* __restrict__ wd) {
+  const int e = blockIdx.x * BLK + threadIdx.x;
+  if (e >= KT * C * C) return;
+  const int k = e / (C * C), r = e - k * C * C, a = r / C, bb = r - a * C;
+  // wf[k][co=a][ci=bb]
+  {
+    const int co = a, ci = bb;
+    const float v = (co / CG == ci / CG) ? W[(co * CG + (ci % CG)) * KT + k] : 0.0f;
+    wf[e] = f2bf(v);
+  }
+  // wd[k][ci=a][co=bb]
+  {
+    const int ci = a, co = bb;
+    const float v = (co / CG == ci / CG) ? W[(co * CG + (ci % CG)) * KT + k] : 0.0f;
+    wd[e] = f2bf(v);
+  }
+}
+
+__global__ __launch_bounds__(BLK) void k_fwd(Geo g, const u16* __restrict__ x, int xp, const u16* __restrict__ off,
+                                             int offp, const float* __restrict__ ob, const u16* __restrict__ wf,
+                                             u16* __restrict__ out, int op) {
+  __shared__ __attribute__((aligned(16))) u16 sXw[WR * PW];
+  __shared__ __attribute__((aligned(16))) u16 sC[64 * P];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const Tile tl = tile_of(g, blockIdx.x);
+  stage_window(g, tl, x, xp, sXw);
+  const int p = tid >> 2, q = tid & 3;
+  const int y = tl.y0 + (p >> 3), xx = tl.x0 + (p & 7);
+  const size_t pix = (size_t)(tl.b * g.H + y) * g.W + xx;
+  f32x4 acc[4];
+#pragma unroll
+  for (int n = 0; n < 4; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  __syncthreads();
+  for (int k = 0; k < KT; ++k) {
+    float dy, dx, col[CG];
+    offsets(off, offp, ob, pix, k, &dy, &dx);
+    const Samp s = samp(g, y, xx, k, dy, dx);
+    sample16(g, tl, x, xp, sXw, s, q, col);
+    store_col(sC, p, q, col);
+    __syncthreads();
+    const u16* wk = wf + (size_t)k * C * C;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const bf16x8 a = *(const bf16x8*)&sC[(16 * w + (lane & 15)) * P + 32 * ks + 8 * (lane >> 4)];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const bf16x8 bv = *(const bf16x8*)&wk[(n * 16 + (lane & 15)) * C + 32 * ks + 8 * (lane >> 4)];
+        acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, acc[n], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+  // D[px = 16w + 4*(lane>>4) + r][co = 16n + (lane&15)] -> LDS -> 16-B stores
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sC[(16 * w + 4 * (lane >> 4) + r) * P + 16 * n + (lane & 15)] = f2bf(acc[n][r]);
+  __syncthreads();
+  for (int qd = tid; qd < 64 * 8; qd += BLK) {
+    const int pp = qd >> 3, seg = qd & 7;
+    const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
+    *(uint4*)(out + ((size_t)(tl.b * g.H + yy) * g.W + xw) * op + seg * 8) = *(const uint4*)&sC[pp * P + seg * 8];
+  }
+}
+
+__global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, int xp, const u16* __restrict__ off,
+                                             int offp, const float* __restrict__ ob, const u16* __restrict__ wd,
+                                             const u16* __restrict__ dout, int dop, float* __restrict__ dx,
+                                             u16* __restrict__ doff, int doffp, float* __restrict__ pw_part,
+                                             float* __restrict__ pb_part) {
+  __shared__ __attribute__((aligned(16))) u16 sXw[WR * PW];
+  __shared__ __attribute__((aligned(16))) u16 sDo[64 * P];
+  __shared__ __attribute__((aligned(16))) u16 sC[64 * P];
+  __shared__ float sDc[64 * (C + 4)];
+  __shared__ float sDx[WR * C];
+  __shared__ float sOff[64 * 2 * KT];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const Tile tl = tile_of(g, blockIdx.x);
+  stage_window(g, tl, x, xp, sXw);
+  for (int qd = tid; qd < 64 * 8; qd += BLK) {
+    const int pp = qd >> 3, seg = qd & 7;
+    const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
+    *(uint4*)&sDo[pp * P + seg * 8] = *(const uint4*)(dout + ((size_t)(tl.b * g.H + yy) * g.W + xw) * dop + seg * 8);
+  }
+  for (int i = tid; i < WR * C; i += BLK) sDx[i] = 0.0f;
+  const int p = tid >> 2, q = tid & 3;
+  const int y = tl.y0 + (p >> 3), xx = tl.x0 + (p & 7);
+  const size_t pix = (size_t)(tl.b * g.H + y) * g.W + xx;
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp4 = lane & 3, rowoff = 4 * g4 + qq;
+  __syncthreads();
+#pragma unroll 1
+  for (int k = 0; k < KT; ++k) {
+    float dy, dxo, col[CG];
+    offsets(off, offp, ob, pix, k, &dy, &dxo);
+    const Samp s = samp(g, y, xx, k, dy, dxo);
+    sample16(g, tl, x, xp, sXw, s, q, col);
+    store_col(sC, p, q, col);
+    __syncthreads();
+    // dcol[px][ci] = sum_co dOut[px][co] W[co][ci]: wave w owns pixels 16w..16w+15
+    {
+      const u16* wk = wd + (size_t)k * C * C;
+      f32x4 d[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) d[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 a = *(const bf16x8*)&sDo[(16 * w + (lane & 15)) * P + 32 * ks + 8 * (lane >> 4)];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const bf16x8 bv = *(const bf16x8*)&wk[(n * 16 + (lane & 15)) * C + 32 * ks + 8 * (lane >> 4)];
+          d[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, d[n], 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) sDc[(16 * w + 4 * g4 + r) * (C + 4) + 16 * n + (lane & 15)] = d[n][r];
+    }
+    // dW_k diagonal block of group w over this tile's 64 pixels: dOut^T col -> partial [tile][k][w]
+    {
+      f32x4 aw = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int r0 = 32 * ks + rowoff, c = w * CG + 4 * pp4;
+        s16x4 va[2] = {tr_read(&sDo[r0 * P + c]), tr_read(&sDo[(r0 + 16) * P + c])};
+        s16x4 vb[2] = {tr_read(&sC[r0 * P + c]), tr_read(&sC[(r0 + 16) * P + c])};
+        aw = __builtin_amdgcn_mfma_f32_16x16x32_bf16(*(bf16x8*)va, *(bf16x8*)vb, aw, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        pw_part[(((size_t)blockIdx.x * KT + k) * 4 + w) * 256 + (4 * g4 + r) * 16 + (lane & 15)] = aw[r];
+    }
+    __syncthreads();
+    // offset gradient + input gradient of this (pixel, tap, group)
+    float gh = 0.0f, gw = 0.0f;
+    if (s.valid) {
+      float dc[CG], v[CG];
+#pragma unroll
+      for (int c = 0; c < CG; ++c) dc[c] = sDc[p * (C + 4) + q * CG + c];
+      const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
+      const int cys[4] = {s.hl, s.hl, s.hl + 1, s.hl + 1}, cxs[4] = {s.wl, s.wl + 1, s.wl, s.wl + 1};
+      const int cok[4] = {s.c1, s.c2, s.c3, s.c4};
+      const float cw[4] = {w1, w2, w3, w4};
+      // d val / d h and d val / d w per corner (get_coordinate_weight)
+      const float ch[4] = {-s.hw, -s.lw, s.hw, s.lw}, cwd[4] = {-s.hh, s.hh, -s.lh, s.lh};
+#pragma unroll
+      for (int cn = 0; cn < 4; ++cn) {
+        if (!cok[cn]) continue;
+        fetch16(g, tl, x, xp, sXw, cys[cn], cxs[cn], q, v);
+        float sv = 0.0f;
+#pragma unroll
+        for (int c = 0; c < CG; ++c) sv += dc[c] * v[c];
+        gh += ch[cn] * sv;
+        gw += cwd[cn] * sv;
+        const int wy = cys[cn] - (tl.y0 - 2), wx = cxs[cn] - (tl.x0 - 2);
+        if (wy >= 0 && wy < WE && wx >= 0 && wx < WE) {
+          float* dst = &sDx[(wy * WE + wx) * C + q * CG];
+#pragma unroll
+          for (int c = 0; c < CG; ++c) atomicAdd(&dst[c], cw[cn] * dc[c]);
+        } else {
+          float* dst = dx + ((size_t)(tl.b * g.H + cys[cn]) * g.W + cxs[cn]) * C + q * CG;
+#pragma unroll
+          for (int c = 0; c < CG; ++c) atomicAdd(&dst[c], cw[cn] * dc[c]);
+        }
+      }
+    }
+    // the four groups of a pixel are lanes 4p..4p+3 of one wave: fixed-order pair sums
+    gh += __shfl_xor(gh, 1, 64);
+    gw += __shfl_xor(gw, 1, 64);
+    gh += __shfl_xor(gh, 2, 64);
+    gw += __shfl_xor(gw, 2, 64);
+    if (q == 0) {
+      sOff[p * 2 * KT + 2 * k] = gh;
+      sOff[p * 2 * KT + 2 * k + 1] = gw;
+    }
+    __syncthreads();
+  }
+  // offset-conv output gradient (bf16 image, channels >= 18 zero) and its bias partials
+  for (int qd = tid; qd < 64 * 8; qd += BLK) {
+    const int pp = qd >> 3, seg = qd & 7;
+    const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
+    unsigned wv[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) {
+      const int c0 = seg * 8 + 2 * h;
+      const float a = c0 < 2 * KT ? sOff[pp * 2 * KT + c0] : 0.0f;
+      const float bq = c0 + 1 < 2 * KT ? sOff[pp * 2 * KT + c0 + 1] : 0.0f;
+      wv[h] = f2bf(a) | ((unsigned)f2bf(bq) << 16);
+    }
+    *(uint4*)(doff + ((size_t)(tl.b * g.H + yy) * g.W + xw) * doffp + seg * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  }
+  if (tid < 2 * KT) {
+    float sacc = 0.0f;
+    for (int pp = 0; pp < 64; ++pp) sacc += sOff[pp * 2 * KT + tid];
+    pb_part[(size_t)blockIdx.x * 2 * KT + tid] = sacc;
+  }
+  // flush the window's input gradient
+  for (int i = tid; i < WR * C; i += BLK) {
+    const float v = sDx[i];
+    if (v == 0.0f) continue;
+    const int wp = i / C, c = i - wp * C;
+    const int hy = tl.y0 - 2 + wp / WE, hx = tl.x0 - 2 + wp % WE;
+    if (hy >= 0 && hy < g.H && hx >= 0 && hx < g.W)
+      atomicAdd(&dx[((size_t)(tl.b * g.H + hy) * g.W + hx) * C + c], v);
+  }
+}
+
+// dWdiag [9][4][16 co][16 ci] -> module layout [64 co][16 ci][3][3]
+__global__ __launch_bounds__(BLK) void k_wstore(const float* __restrict__ d, float* __restrict__ dW) {
+  const int e = blockIdx.x * BLK + threadIdx.x;
+  if (e >= KT * 4 * 256) return;
+  const int k = e / 1024, r = e - k * 1024, gq = r / 256, m = (r / 16) % 16, n = r % 16;
+  dW[((gq * CG + m) * CG + n) * KT + k] = d[e];
+}
+
+static int check_geo(int B, int H, int W, Geo* g) {
+  if (B < 1 || H < 1 || W < 1 || H % TE || W % TE) return 0;
+  *g = Geo{B, H, W, H / TE, W / TE};
+  return 1;
+}
+
+}  // namespace dcn
+}  // namespace rpc
+
+using namespace rpc;
+using namespace rpc::dcn;
+
+extern "C" int rpc_dcn_prep_weight(const float* W, void* w_fwd, void* w_bwd, void* stream) {
+  if (!W || !w_fwd || !w_bwd) return RPC_ERR_ARG;
+  hipLaunchKernelGGL(k_prep, dim3((KT * C * C + BLK - 1) / BLK), dim3(BLK), 0, (hipStream_t)stream, W, (u16*)w_fwd,
+                     (u16*)w_bwd);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dcn_forward(const void* x, int xp, const void* off, int offp, const float* off_bias,
+                               const void* w_fwd, void* out, int op, int B, int H, int W, void* stream) {
+  Geo g;
+  if (!check_geo(B, H, W, &g)) return RPC_ERR_UNSUPPORTED;
+  if (!x || !off || !off_bias || !w_fwd || !out || xp < C || (xp & 7) || offp < 2 * KT || (offp & 7) || op < C ||
+      (op & 7))
+    return RPC_ERR_ARG;
+  hipLaunchKernelGGL(k_fwd, dim3(B * g.TY * g.TX), dim3(BLK), 0, (hipStream_t)stream, g, (const u16*)x, xp,
+                     (const u16*)off, offp, off_bias, (const u16*)w_fwd, (u16*)out, op);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" size_t rpc_dcn_backward_workspace_size(int B, int H, int W) {
+  Geo g;
+  if (!check_geo(B, H, W, &g)) return 0;
+  const size_t tiles = (size_t)B * g.TY * g.TX;
+  return (tiles * KT * 1024 + tiles * 2 * KT + KT * 1024) * sizeof(float);
+}
+
+extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp, const float* off_bias,
+                                const void* w_bwd, const void* dout, int dop, float* dx, void* doff, int doffp,
+                                float* doff_bias, float* dW, int B, int H, int W, void* workspace, size_t ws_bytes,
+                                void* stream) {
+  Geo g;
+  if (!check_geo(B, H, W, &g)) return RPC_ERR_UNSUPPORTED;
+  if (!x || !off || !off_bias || !w_bwd || !dout || !dx || !doff || !doff_bias || !dW || !workspace) return RPC_ERR_ARG;
+  if (xp < C || (xp & 7) || offp < 2 * KT || (offp & 7) || dop < C || (dop & 7) || doffp < C || (doffp & 7))
+    return RPC_ERR_ARG;
+  if (ws_bytes < rpc_dcn_backward_workspace_size(B, H, W)) return RPC_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int tiles = B * g.TY * g.TX;
+  float* pw = (float*)workspace;
+  float* pb = pw + (size_t)tiles * KT * 1024;
+  float* dwd = pb + (size_t)tiles * 2 * KT;
+  hipLaunchKernelGGL(k_bwd, dim3(tiles), dim3(BLK), 0, st, g, (const u16*)x, xp, (const u16*)off, offp, off_bias,
+                     (const u16*)w_bwd, (const u16*)dout, dop, dx, (u16*)doff, doffp, pw, pb);
+  RPC_LAUNCH_CHECK();
+  slab_reduce(pw, tiles, (long long)KT * 1024, dwd, st);
+  slab_reduce(pb, tiles, 2 * KT, doff_bias, st);
+  hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}

@@ -293,18 +293,23 @@ struct C3 {
   int B, H, W, TY, TX;   // image, tiles per column / row
 };
 
-template <int DUMMY = 0>
+// NARROW = 0: 128 output channels per block (waves 64 px x 64 co); NARROW = 1: 64 output channels
+// per block (waves 64 px x 32 co) for the 64-channel CenterHead convolutions.
+template <int NARROW = 0>
 __global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
+  constexpr int TNB = NARROW ? 64 : TN;   // output channels per block
+  constexpr int WCO = TNB / 2;            // output channels per wave
+  constexpr int NI = WCO / 16;            // 16-channel MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) u16 sA[HR * LP];
-  __shared__ __attribute__((aligned(16))) u16 sW[2][TN * LP];
-  __shared__ float sP[4][2][TN];
+  __shared__ __attribute__((aligned(16))) u16 sW[2][TNB * LP];
+  __shared__ float sP[4][2][TNB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wp = w & 3, wc = w >> 2;
   const int ntiles = g.B * g.TY * g.TX;
   const int tile = xcd_remap(blockIdx.x, ntiles);
   const int b = tile / (g.TY * g.TX), trem = tile - b * g.TY * g.TX;
   const int ty0 = (trem / g.TX) * CT, tx0 = (trem % g.TX) * CT;
-  const int n0 = blockIdx.y * TN;
+  const int n0 = blockIdx.y * TNB;
   const int NKC = g.CIN / BK, NS = 9 * NKC;
 
   // ---- halo staging (chunk q: halo row q>>3, 8 channels (q&7)*8). Out-of-image rows load row 0
@@ -344,35 +349,35 @@ __global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
     const int kc_ = (s) / 9, t_ = (s) - kc_ * 9;                                \
     const u16* p_ = wbase + t_ * wtap + kc_ * BK;                               \
     R##a = *(const uint4*)p_;                                                   \
-    R##b = *(const uint4*)(p_ + whalf);                                         \
+    if (!NARROW) R##b = *(const uint4*)(p_ + whalf);                            \
   }
 #define C3_WSTORE(R, buf)                                        \
   {                                                              \
     *(uint4*)&sW[buf][wrow * LP + wseg] = R##a;                  \
-    *(uint4*)&sW[buf][(wrow + 64) * LP + wseg] = R##b;           \
+    if (!NARROW) *(uint4*)&sW[buf][(wrow + 64) * LP + wseg] = R##b; \
   }
   uint4 r0a, r0b, r1a, r1b, r2a, r2b;
 
-  f32x4 acc[4][4];
+  f32x4 acc[NI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   // pixel p = wp*64 + j*16 + (lane&15) -> tile row wp*4 + j, column lane&15
   const int pcol = lane & 15;
-  const u16* aw = &sW[0][(wc * 64 + (lane & 15)) * LP + 8 * (lane >> 4)];
+  const u16* aw = &sW[0][(wc * WCO + (lane & 15)) * LP + 8 * (lane >> 4)];
   const u16* ab = &sA[(wp * 4 * HT + pcol) * LP + 8 * (lane >> 4)];
 #define C3_COMPUTE(buf, t)                                                                                  \
   {                                                                                                         \
     const int dy_ = (t) / 3, dx_ = (t) % 3;                                                                 \
     _Pragma("unroll") for (int kk = 0; kk < BK / 32; ++kk) {                                                \
-      bf16x8 a[4], bb[4];                                                                                   \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                         \
-        a[i] = *(const bf16x8*)(aw + (buf) * (TN * LP) + i * 16 * LP + kk * 32);                            \
+      bf16x8 a[NI], bb[4];                                                                                  \
+      _Pragma("unroll") for (int i = 0; i < NI; ++i)                                                        \
+        a[i] = *(const bf16x8*)(aw + (buf) * (TNB * LP) + i * 16 * LP + kk * 32);                           \
       _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                         \
         bb[j] = *(const bf16x8*)(ab + ((j + dy_) * HT + dx_) * LP + kk * 32);                               \
-      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                         \
+      _Pragma("unroll") for (int i = 0; i < NI; ++i)                                                        \
         _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);             \
     }                                                                                                       \
@@ -420,9 +425,9 @@ __global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
 #undef C3_WSTORE
 
   // ---- epilogue (as k_igemm): lane holds co = n0 + wc*64 + i*16 + 4*(lane>>4) + r of pixel (wp*4+j, lane&15)
-  float s1[4][4], s2[4][4];
+  float s1[NI][4], s2[NI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
 #pragma unroll
@@ -430,9 +435,9 @@ __global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
     const int y = ty0 + wp * 4 + j, x = tx0 + pcol;
     if (y >= g.H || x >= g.W) continue;
     const size_t orow = (size_t)(b * g.H + y) * g.W + x;
-    u16* op = g.out + orow * g.OP + g.OOFF + n0 + wc * 64 + 4 * (lane >> 4);
+    u16* op = g.out + orow * g.OP + g.OOFF + n0 + wc * WCO + 4 * (lane >> 4);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NI; ++i) {
       float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
       uint2* p2 = (uint2*)(op + i * 16);
       if (g.accum) {
@@ -455,7 +460,7 @@ __global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
   }
   if (g.part == nullptr) return;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
 #pragma unroll
@@ -466,17 +471,17 @@ __global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
     }
   if ((lane & 15) == 0) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < NI; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int c = wc * 64 + i * 16 + 4 * (lane >> 4) + r;
+        const int c = wc * WCO + i * 16 + 4 * (lane >> 4) + r;
         sP[wp][0][c] = s1[i][r];
         sP[wp][1][c] = s2[i][r];
       }
   }
   __syncthreads();
   float* prow = g.part + (size_t)tile * 2 * g.COUT;
-  if (tid < TN) {
+  if (tid < TNB) {
     prow[n0 + tid] = ((sP[0][0][tid] + sP[1][0][tid]) + sP[2][0][tid]) + sP[3][0][tid];
     prow[g.COUT + n0 + tid] = ((sP[0][1][tid] + sP[1][1][tid]) + sP[2][1][tid]) + sP[3][1][tid];
   }
@@ -498,37 +503,43 @@ struct WG {
   float* part;    // [chunks][T][CI][CO]
 };
 
-// 1-D grid of chunks * T * (CI/128)*(CO/128) blocks, XCD-aware: each XCD walks whole chunks with
+// 1-D grid of chunks * T * (CI/TC)*(CO/TC) blocks, XCD-aware: each XCD walks whole chunks with
 // the taps and channel tiles of one chunk adjacent, so a chunk's x / dz rows are fetched into that
-// XCD's L2 once and re-read by its T * tiles blocks. 4 waves as 2 (ci) x 2 (co), 64x64 each.
-template <int MAP>
+// XCD's L2 once and re-read by its T * tiles blocks. 4 waves as 2 (ci) x 2 (co).
+// NARROW = 1: 64 x 64 (ci, co) tiles (waves 32 x 32) for the 64-channel CenterHead layers.
+template <int MAP, int NARROW = 0>
 __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
   constexpr int T = wtaps_of<MAP>();
-  constexpr int RT = 64, P = 128 + 16;  // rows per sub-tile, LDS pitch (conflict-free tr reads)
+  constexpr int TC = NARROW ? 64 : 128;   // block tile edge (ci and co)
+  constexpr int WT = TC / 2;              // wave tile edge
+  constexpr int NW = WT / 16;             // 16 x 16 MFMA tiles per wave edge
+  constexpr int SEGS = TC / 8;            // 16-B segments per row
+  constexpr int NLD = 64 * SEGS / BLK;    // 16-B loads per thread per operand and sub-tile
+  constexpr int RT = 64, P = TC + 16;     // rows per sub-tile, LDS pitch (conflict-free tr reads)
   __shared__ __attribute__((aligned(16))) u16 sX[RT * P];
   __shared__ __attribute__((aligned(16))) u16 sD[RT * P];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wci = w >> 1, wco = w & 1;
-  const int nco = g.CO / 128, ntile = (g.CI / 128) * nco;
+  const int nco = g.CO / TC, ntile = (g.CI / TC) * nco;
   const int lid = xcd_remap(blockIdx.x, gridDim.x);
   const int chunk = lid / (T * ntile), rest = lid - chunk * (T * ntile);
   const int t = rest / ntile, tile = rest - t * ntile;
-  const int ci0 = (tile / nco) * 128, co0 = (tile % nco) * 128;
+  const int ci0 = (tile / nco) * TC, co0 = (tile % nco) * TC;
   const int rb0 = chunk * g.rows_per, rb1 = min(g.M, rb0 + g.rows_per);
   const int HW = g.R.H * g.R.W;
   const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, rowoff = 4 * g4 + qq;
 
-  f32x4 acc[4][4];
+  f32x4 acc[NW][NW];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NW; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  uint4 rx[4], rd[4];
+  uint4 rx[NLD], rd[NLD];
   auto gload = [&](int rs) {
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int q = tid + s * BLK, r = q >> 4, seg = q & 15, m = rs + r;
+    for (int s = 0; s < NLD; ++s) {
+      const int q = tid + s * BLK, r = q / SEGS, seg = q % SEGS, m = rs + r;
       rx[s] = rd[s] = make_uint4(0u, 0u, 0u, 0u);
       if (m < rb1) {
         const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
@@ -551,8 +562,8 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
   for (int rs = rb0; rs < rb1; rs += RT) {
     __syncthreads();
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const int q = tid + s * BLK, r = q >> 4, seg = q & 15;
+    for (int s = 0; s < NLD; ++s) {
+      const int q = tid + s * BLK, r = q / SEGS, seg = q % SEGS;
       *(uint4*)&sX[r * P + seg * 8] = rx[s];
       *(uint4*)&sD[r * P + seg * 8] = rd[s];
     }
@@ -561,33 +572,34 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
 #pragma unroll
     for (int ks = 0; ks < RT / 32; ++ks) {
       const int r0 = 32 * ks + rowoff;
-      bf16x8 a[4], b[4];
+      bf16x8 a[NW], b[NW];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int c = wci * 64 + i * 16 + 4 * pp;
+      for (int i = 0; i < NW; ++i) {
+        const int c = wci * WT + i * 16 + 4 * pp;
         s16x4 v[2] = {tr_read(&sX[r0 * P + c]), tr_read(&sX[(r0 + 16) * P + c])};
         a[i] = *(bf16x8*)v;
       }
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int c = wco * 64 + j * 16 + 4 * pp;
+      for (int j = 0; j < NW; ++j) {
+        const int c = wco * WT + j * 16 + 4 * pp;
         s16x4 v[2] = {tr_read(&sD[r0 * P + c]), tr_read(&sD[(r0 + 16) * P + c])};
         b[j] = *(bf16x8*)v;
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < NW; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < NW; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
   }
   float* out = g.part + ((size_t)chunk * T + t) * g.CI * g.CO;
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < NW; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
+    for (int j = 0; j < NW; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int ci = ci0 + wci * 64 + i * 16 + 4 * g4 + r, co = co0 + wco * 64 + j * 16 + (lane & 15);
+        const int ci = ci0 + wci * WT + i * 16 + 4 * g4 + r, co = co0 + wco * WT + j * 16 + (lane & 15);
         out[(size_t)ci * g.CO + co] = acc[i][j][r];
       }
 }
@@ -792,8 +804,13 @@ static void launch_igemm(const IG& g, int par_count, hipStream_t st) {
 
 template <int MAP>
 static void launch_wgrad(const WG& g, int chunks, hipStream_t st) {
-  dim3 grid(chunks * wtaps_of<MAP>() * (g.CI / 128) * (g.CO / 128));
-  hipLaunchKernelGGL((k_wgrad<MAP>), grid, dim3(BLK), 0, st, g);
+  if (g.CI % 128 == 0 && g.CO % 128 == 0) {
+    dim3 grid(chunks * wtaps_of<MAP>() * (g.CI / 128) * (g.CO / 128));
+    hipLaunchKernelGGL((k_wgrad<MAP, 0>), grid, dim3(BLK), 0, st, g);
+  } else {
+    dim3 grid(chunks * wtaps_of<MAP>() * (g.CI / 64) * (g.CO / 64));
+    hipLaunchKernelGGL((k_wgrad<MAP, 1>), grid, dim3(BLK), 0, st, g);
+  }
 }
 
 static int map_wtaps(int map) {
@@ -829,7 +846,10 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
                               int ooff, int accum, float* part, const int* r_img, const int* s_img,
                               const int* o_img, void* stream) {
   if (map < M_S1 || map > M_G2 || !src || !wt || !out || !r_img || !s_img || !o_img) return RPC_ERR_ARG;
-  if (cin % BK || cout % TN || sp < cin || op < ooff + cout || (sp & 7) || (op & 7) || (ooff & 7)) return RPC_ERR_ARG;
+  // S1 takes any multiple of 64 output channels (64-channel blocks when not a multiple of 128)
+  if (cin % BK || (map == M_S1 ? cout % 64 : cout % TN) || sp < cin || op < ooff + cout || (sp & 7) || (op & 7) ||
+      (ooff & 7))
+    return RPC_ERR_ARG;
   IG g{(const u16*)src, sp, cin, (const u16*)wt, cout, (u16*)out, op, ooff, accum, part,
        img3(r_img), img3(s_img), img3(o_img), 0};
   g.M = g.R.B * g.R.H * g.R.W;
@@ -838,7 +858,8 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   if (map == M_S1) {
     const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
     C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
-    hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / TN), dim3(CBLK), 0, st, c);
+    if (g.COUT % TN == 0) hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / TN), dim3(CBLK), 0, st, c);
+    else hipLaunchKernelGGL(k_conv3x3<1>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
     RPC_LAUNCH_CHECK();
     return RPC_OK;
   }
@@ -870,7 +891,7 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
                                const int* r_img, const int* s_img, const int* o_img, float* dW, void* ws,
                                size_t ws_bytes, void* stream) {
   if (map < M_S1 || map > M_G2 || map == M_D2 || map == M_G2) return RPC_ERR_ARG;
-  if (ci % 128 || co % 128 || (xp & 7) || (dp & 7)) return RPC_ERR_ARG;
+  if (ci % 64 || co % 64 || (xp & 7) || (dp & 7)) return RPC_ERR_ARG;
   Img R = img3(r_img), S = img3(s_img), O = img3(o_img);
   const int M = R.B * R.H * R.W, T = map_wtaps(map);
   const int chunks = wgrad_chunks(M);

@@ -1,0 +1,163 @@
+"""§8(f3): the DCNSeparateHead deformable convolution (csrc/dcn.hip) and the whole HIP CenterHead
+(shared conv + six DCN task heads on the dense engine) vs float64 CPU references.
+
+DCN: oracle/dcn.py (mmcv deform_conv2d restated, autograd gradients) on the same bf16-rounded
+input, offsets and weights; the kernel samples in fp32 and multiplies bf16 columns (fp32 accumulate),
+so agreement is bf16-level: forward relative L2 <= 1e-2, gradients (input, offsets, offset bias,
+weights) relative L2 <= 2e-2. Head: the same layer stack in float64 torch (conv / BatchNorm (batch
+statistics) / ReLU / oracle DCN), outputs relative L2 <= 3e-2 and gradient directions (cosine)
+>= 0.98 — the head runs in bf16 activations. Parity w.r.t. mmcv / mmdet3d is unpinned (not vendored)."""
+import pytest
+import torch
+import torch.nn.functional as Fn
+
+from oracle.dcn import deform_conv2d
+from robustpointclouds_amd import _ffi
+from robustpointclouds_amd import dense_bev as db
+from robustpointclouds_amd.center_head import _BOX_ORDER, CenterHead
+
+pytestmark = pytest.mark.gpu
+DEV = torch.device("cuda")
+
+
+def _bf(t):
+    return t.to(torch.bfloat16).to(torch.float64)
+
+
+def _rel(a, b):
+    return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("B,H,W,amp", [(2, 16, 24, 0.8), (1, 8, 8, 2.5)])
+def test_dcn_forward_backward(B, H, W, amp):
+    g = torch.Generator().manual_seed(int(amp * 10) + H)
+    x = _bf(torch.randn(B, 64, H, W, generator=g))
+    offz = _bf(torch.randn(B, 64, H, W, generator=g) * amp)          # offset-conv output image, 64 wide
+    offz[:, 18:] = 0
+    ob = torch.randn(18, generator=g).double() * 0.3
+    Wt = _bf(torch.randn(64, 16, 3, 3, generator=g) * 0.1)
+    gout = _bf(torch.randn(B, 64, H, W, generator=g))
+    lib = _ffi.load()
+    st = _ffi.stream_of(torch.empty(1, device=DEV))
+    xi = db._nhwc(x.float().to(DEV))
+    oi = db._nhwc(offz.float().to(DEV))
+    obd = ob.float().to(DEV)
+    W32 = Wt.float().to(DEV).contiguous()
+    wf = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=DEV)
+    wd = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=DEV)
+    _ffi.check(lib.rpc_dcn_prep_weight(_ffi.ptr(W32), _ffi.ptr(wf), _ffi.ptr(wd), st), "prep")
+    out = db._image(B, 64, H, W, DEV)
+    _ffi.check(lib.rpc_dcn_forward(_ffi.ptr(xi), 64, _ffi.ptr(oi), 64, _ffi.ptr(obd), _ffi.ptr(wf), _ffi.ptr(out), 64,
+                                   B, H, W, st), "fwd")
+    gi = db._nhwc(gout.float().to(DEV))
+    dx = torch.zeros((B * H * W, 64), dtype=torch.float32, device=DEV)
+    doff = db._image(B, 64, H, W, DEV)
+    dob = torch.empty(18, device=DEV)
+    dW = torch.empty((64, 16, 3, 3), device=DEV)
+    wsz = lib.rpc_dcn_backward_workspace_size(B, H, W)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    _ffi.check(lib.rpc_dcn_backward(_ffi.ptr(xi), 64, _ffi.ptr(oi), 64, _ffi.ptr(obd), _ffi.ptr(wd), _ffi.ptr(gi), 64,
+                                    _ffi.ptr(dx), _ffi.ptr(doff), 64, _ffi.ptr(dob), _ffi.ptr(dW), B, H, W, _ffi.ptr(ws),
+                                    wsz, st), "bwd")
+    # reference (offsets = bf16 conv output + fp32 bias, as the kernel reads them)
+    xr = x.clone().requires_grad_(True)
+    offr = (offz[:, :18] + ob.view(1, 18, 1, 1)).clone().requires_grad_(True)
+    Wr = Wt.clone().requires_grad_(True)
+    ref = deform_conv2d(xr, offr, Wr, groups=4)
+    (ref * gout).sum().backward()
+    got = out.float().cpu().double()
+    assert _rel(got, ref.detach()) <= 1e-2
+    assert _rel(dx.view(B, H, W, 64).permute(0, 3, 1, 2).cpu().double(), xr.grad) <= 2e-2
+    assert _rel(doff.float().cpu().double()[:, :18], offr.grad) <= 2e-2
+    assert float(doff.float()[:, 18:].abs().max()) == 0.0
+    assert _rel(dob.cpu().double(), offr.grad.sum((0, 2, 3))) <= 2e-2
+    assert _rel(dW.cpu().double(), Wr.grad) <= 2e-2
+
+
+def _ref_head(head, x, B, H, W):
+    """float64 torch forward of the same stack (BN in training mode: batch statistics)."""
+    P = {k: v.detach().cpu().double() for k, v in head.named_parameters()}
+
+    def cm(prefix, h):
+        z = Fn.conv2d(h, P[prefix + ".conv.weight"], padding=1)
+        m = z.mean((0, 2, 3), keepdim=True)
+        v = z.var((0, 2, 3), unbiased=False, keepdim=True)
+        eps = 1e-5
+        return torch.relu((z - m) / torch.sqrt(v + eps) * P[prefix + ".bn.weight"].view(1, -1, 1, 1)
+                          + P[prefix + ".bn.bias"].view(1, -1, 1, 1))
+
+    def fc(prefix, h):
+        return Fn.conv2d(h, P[prefix + ".weight"], P[prefix + ".bias"], padding=1)
+
+    y0 = cm("shared_conv", x)
+    hms, boxes = [], []
+    for t, th in enumerate(head.task_heads):
+        feats = {}
+        for br in ("cls", "reg"):
+            pre = f"task_heads.{t}.feature_adapt_{br}"
+            off = Fn.conv2d(y0, P[pre + ".conv_offset.weight"], P[pre + ".conv_offset.bias"], padding=1)
+            feats[br] = deform_conv2d(y0, off, P[pre + ".weight"], groups=4)
+        hms.append(fc(f"task_heads.{t}.cls_head.1", cm(f"task_heads.{t}.cls_head.0", feats["cls"])))
+        boxes.append(torch.cat([fc(f"task_heads.{t}.task_head.{n}.1", cm(f"task_heads.{t}.task_head.{n}.0",
+                                                                           feats["reg"])) for n in _BOX_ORDER], 1))
+    return torch.cat(hms, 1), torch.cat(boxes, 1), P
+
+
+def test_center_head_forward_backward():
+    torch.manual_seed(0)
+    B, Cin, H, W = 2, 128, 32, 32
+    head = CenterHead(in_channels=Cin).to(DEV)
+    with torch.no_grad():   # non-zero offsets (the offset convs are zero-initialised)
+        for th in head.task_heads:
+            for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
+                dcn.conv_offset.weight.normal_(0, 0.05)
+                dcn.conv_offset.bias.uniform_(-0.5, 0.5)
+    x = _bf(torch.randn(B, Cin, H, W)).float()
+    xd = x.to(DEV).requires_grad_(True)
+    preds = head([xd])
+    hm = torch.cat([p[0]["heatmap"] for p in preds], 1)
+    box = torch.cat([torch.cat([p[0][n] for n in _BOX_ORDER], 1) for p in preds], 1)
+    xr = x.double().requires_grad_(True)
+    # the reference reads the module's parameters after the step's running-stat update is irrelevant
+    rhm, rbox, _ = _ref_head(head, xr, B, H, W)
+    assert _rel(hm.detach().cpu().double(), rhm.detach()) <= 3e-2
+    assert _rel(box.detach().cpu().double(), rbox.detach()) <= 3e-2
+    g = torch.Generator().manual_seed(5)
+    ghm, gbox = torch.randn(rhm.shape, generator=g).double(), torch.randn(rbox.shape, generator=g).double()
+    ((hm * ghm.float().to(DEV)).sum() + (box * gbox.float().to(DEV)).sum()).backward()
+    ((rhm * ghm).sum() + (rbox * gbox).sum()).backward()
+    cos = lambda a, b: (a.flatten() @ b.flatten() / (a.norm() * b.norm())).item()
+    assert cos(xd.grad.cpu().double(), xr.grad) >= 0.98
+    Pref = {}
+    P = {k: v.detach().cpu().double().requires_grad_(True) for k, v in head.named_parameters()}
+    # parameter gradients: recompute the reference with parameters as leaves
+    def cm(prefix, h):
+        z = Fn.conv2d(h, P[prefix + ".conv.weight"], padding=1)
+        m = z.mean((0, 2, 3), keepdim=True)
+        v = z.var((0, 2, 3), unbiased=False, keepdim=True)
+        return torch.relu((z - m) / torch.sqrt(v + 1e-5) * P[prefix + ".bn.weight"].view(1, -1, 1, 1)
+                          + P[prefix + ".bn.bias"].view(1, -1, 1, 1))
+    y0 = cm("shared_conv", x.double())
+    tot = 0
+    for t, th in enumerate(head.task_heads):
+        feats = {}
+        for br in ("cls", "reg"):
+            pre = f"task_heads.{t}.feature_adapt_{br}"
+            off = Fn.conv2d(y0, P[pre + ".conv_offset.weight"], P[pre + ".conv_offset.bias"], padding=1)
+            feats[br] = deform_conv2d(y0, off, P[pre + ".weight"], groups=4)
+        tot = tot + (Fn.conv2d(cm(f"task_heads.{t}.cls_head.0", feats["cls"]), P[f"task_heads.{t}.cls_head.1.weight"],
+                               P[f"task_heads.{t}.cls_head.1.bias"], padding=1) *
+                     ghm[:, sum(head.num_classes[:t]):sum(head.num_classes[:t + 1])]).sum()
+        bo = 10 * t
+        for n, w in zip(_BOX_ORDER, (2, 1, 3, 2, 2)):
+            pre = f"task_heads.{t}.task_head.{n}"
+            tot = tot + (Fn.conv2d(cm(pre + ".0", feats["reg"]), P[pre + ".1.weight"], P[pre + ".1.bias"], padding=1)
+                         * gbox[:, bo:bo + w]).sum()
+            bo += w
+    tot.backward()
+    bad = []
+    for k, p in head.named_parameters():
+        c = cos(p.grad.cpu().double(), P[k].grad)
+        if not c >= 0.98:
+            bad.append((k, c))
+    assert not bad, bad

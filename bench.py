@@ -27,10 +27,11 @@ def _args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch", type=int, default=6)
+    ap.add_argument("--batch", type=int, default=None, help="frames per GPU (6 KITTI, 4 nuScenes)")
     ap.add_argument("--classes", type=int, default=1, choices=[1, 3])
-    ap.add_argument("--model", default="voxelnet", choices=["voxelnet", "strong"],
-                    help="strong = StrongAdversarialVoxelNet, sensor_error_bound 0.4 (BASELINE config 5)")
+    ap.add_argument("--model", default="voxelnet", choices=["voxelnet", "strong", "centerpoint"],
+                    help="strong = StrongAdversarialVoxelNet, sensor_error_bound 0.4 (BASELINE config 5); "
+                         "centerpoint = AdversarialCenterPoint nuScenes, batch 4 (BASELINE config 4)")
     ap.add_argument("--fp32", action="store_true", help="dense part in fp32 (parity mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=6)
@@ -47,6 +48,20 @@ def _batches(n, B, rank, dev, classes):
     for j in range(n):
         pts, boxes, labels = kitti_batch(B, seed0=(rank * n + j) * B, num_classes=classes)
         out.append(([torch.from_numpy(p).to(dev) for p in pts], _gt(boxes, labels, dev)))
+    return out
+
+
+def _nus_batches(n, B, rank, dev):
+    """Synthetic 10-sweep nuScenes frames [N, 5] + 20-40 GT boxes [M, 9] per frame, padded on device."""
+    from robustpointclouds_amd.center_head import pack_gt
+    from robustpointclouds_amd.synthetic import nus_frame, nus_gt_boxes
+    out = []
+    for j in range(n):
+        seeds = [(rank * n + j) * B + i for i in range(B)]
+        pts = [torch.from_numpy(nus_frame(s)).to(dev) for s in seeds]
+        gts = [nus_gt_boxes(s) for s in seeds]
+        gb, gl = pack_gt([torch.from_numpy(b) for b, _ in gts], [torch.from_numpy(l) for _, l in gts], dev)
+        out.append((pts, dict(gt_boxes=gb, gt_labels=gl)))
     return out
 
 
@@ -136,12 +151,18 @@ def cpu_baseline(frames: int, classes: int):
 
 def main():
     a = _args()
-    from robustpointclouds_amd.trainer import Trainer, init_distributed, make_kitti_model
+    from robustpointclouds_amd.trainer import Trainer, init_distributed, make_kitti_model, make_nus_model
     rank, world, local = init_distributed()
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
-    model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3, variant=a.model)
+    nus = a.model == "centerpoint"
+    if a.batch is None:
+        a.batch = 4 if nus else 6
+    if nus:
+        model = make_nus_model(device=dev, epoch=3)
+    else:
+        model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3, variant=a.model)
     tr = Trainer(model, ddp=world > 1, bf16=not a.fp32, device=dev)
     from robustpointclouds_amd import dense_bev
     from robustpointclouds_amd.sparse_encoder import KernelTimer
@@ -154,7 +175,7 @@ def main():
         timer = KernelTimer(op, int(ci), int(co))
         model.middle_encoder.timer = timer
     NB = 4
-    data = _batches(NB, a.batch, rank, dev, a.classes)
+    data = _nus_batches(NB, a.batch, rank, dev) if nus else _batches(NB, a.batch, rank, dev, a.classes)
     for i in range(a.warmup):
         tr.train_step(*data[i % NB])
     torch.cuda.synchronize()
@@ -176,14 +197,18 @@ def main():
         dt = float(t.item())
     frames = world * a.batch * a.steps
     if rank == 0:
-        res = dict(metric="adversarial-train frames/sec/GPU, SECOND KITTI-3class, at 1/2/4/8 MI355X",
+        metric = ("adversarial-train frames/sec/GPU, CenterPoint nuScenes 10-class (BASELINE config 4)" if nus else
+                  "adversarial-train frames/sec/GPU, SECOND KITTI-3class, at 1/2/4/8 MI355X")
+        workload = ("AdversarialCenterPoint nuScenes 10-class (voxel 0.1 m, 10-sweep HDL-32E-like frames, "
+                    "basicblock SparseEncoder, SECOND/FPN, DCN CenterHead)" if nus else
+                    ("AdversarialVoxelNet" if a.model == "voxelnet" else
+                     "StrongAdversarialVoxelNet (sensor_error_bound 0.4, config 5)") +
+                    " (SECOND) KITTI " + ("Car-only" if a.classes == 1 else "3-class"))
+        res = dict(metric=metric,
                    value=round(frames / dt, 3), unit="frames/s", n_gpus=world, steps=a.steps, warmup=a.warmup,
                    ms_per_step=round(1000 * dt / a.steps, 3), higher_is_better=True, scaling="weak",
                    vs_baseline=None, dtype="fp32" if a.fp32 else "bf16", data="synthetic",
-                   config=dict(workload=("AdversarialVoxelNet" if a.model == "voxelnet" else
-                                         "StrongAdversarialVoxelNet (sensor_error_bound 0.4, config 5)") +
-                               " (SECOND) KITTI " + ("Car-only" if a.classes == 1 else "3-class") +
-                               f", batch {a.batch}/GPU, perturber active (_epoch=3)",
+                   config=dict(workload=workload + f", batch {a.batch}/GPU, perturber active (_epoch=3)",
                                global_batch=world * a.batch, frames_per_gpu=a.batch,
                                dense_dtype="fp32" if a.fp32 else "bf16",
                                kernel_dtype=("fp32 (voxelize, perturber, sparse encoder)" if a.fp32 else

@@ -421,11 +421,17 @@ class CenterHead(nn.Module):
         return tuple(preds)
 
     def loss_by_feat(self, preds_dicts, batch_gt_instances_3d, *args, **kwargs):
+        """batch_gt_instances_3d: per-frame instances (bboxes_3d [n, 9] LiDAR boxes, labels_3d) or the
+        trainer's padded device dict(gt_boxes [B, M, 9], gt_labels [B, M], -1 padding)."""
         hm, box, B, H, W = preds_dicts[0][0]["_packed"]
-        boxes = [g.bboxes_3d if hasattr(g, "bboxes_3d") else g["bboxes_3d"] for g in batch_gt_instances_3d]
-        labels = [g.labels_3d if hasattr(g, "labels_3d") else g["labels_3d"] for g in batch_gt_instances_3d]
-        boxes = [getattr(b, "tensor", b) for b in boxes]
-        gb, gl = pack_gt(boxes, labels, hm.device)
+        if isinstance(batch_gt_instances_3d, dict) and "gt_boxes" in batch_gt_instances_3d:
+            gb = batch_gt_instances_3d["gt_boxes"].float().contiguous()
+            gl = batch_gt_instances_3d["gt_labels"].long().contiguous()
+        else:
+            boxes = [g.bboxes_3d if hasattr(g, "bboxes_3d") else g["bboxes_3d"] for g in batch_gt_instances_3d]
+            labels = [g.labels_3d if hasattr(g, "labels_3d") else g["labels_3d"] for g in batch_gt_instances_3d]
+            boxes = [getattr(b, "tensor", b) for b in boxes]
+            gb, gl = pack_gt(boxes, labels, hm.device)
         cfg = center_cfg([tuple(c) for c in self.class_names], self.train_cfg, B, H, W, self.hm_pitch, self.box_pitch,
                          self.norm_bbox, self.loss_cls_weight, self.loss_bbox_weight)
         lv = CenterLossFn.apply(hm, box, gb, gl, cfg)
@@ -439,6 +445,8 @@ class CenterHead(nn.Module):
 
     def loss(self, feats, batch_data_samples, **kwargs):
         preds = self(feats)
+        if isinstance(batch_data_samples, dict):
+            return self.loss_by_feat(preds, batch_data_samples)
         return self.loss_by_feat(preds, [s.gt_instances_3d if hasattr(s, "gt_instances_3d") else s["gt_instances_3d"]
                                          for s in batch_data_samples])
 

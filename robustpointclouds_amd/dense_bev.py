@@ -65,7 +65,7 @@ TIMER = None
 
 def _conv(lib, fmap, *args):
     """rpc_dense_conv, with the S1 launches timed when a ConvTimer is enabled."""
-    t = TIMER if (TIMER is not None and TIMER.enabled and fmap == S1) else None
+    t = TIMER if (TIMER is not None and TIMER.enabled and fmap == S1 and args[4] % 128 == 0) else None
     e0 = t.start() if t is not None else None
     rc = lib.rpc_dense_conv(fmap, *args)
     if t is not None:
@@ -217,6 +217,9 @@ def fpn_layers(mod):
     for d in mod.deblocks:
         up, bnm = d[0], d[1]
         k = up.kernel_size[0]
+        if type(up) is torch.nn.Conv2d and k == 1 and up.stride[0] == 1:   # use_conv_for_no_stride
+            out.append(_Layer(P1, up, bnm, 0, up.in_channels, up.out_channels, 1))
+            continue
         assert isinstance(up, torch.nn.ConvTranspose2d) and up.stride[0] == k and k in (1, 2), \
             "HIP SECONDFPN supports ConvTranspose2d deblocks with kernel = stride in {1, 2}"
         out.append(_Layer(P1 if k == 1 else U2, up, bnm, 1, up.in_channels, up.out_channels, k * k))

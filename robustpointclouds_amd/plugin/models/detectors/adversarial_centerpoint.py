@@ -1,0 +1,132 @@
+"""AdversarialCenterPoint — drop-in for models/detectors/adversarial_centerpoint.py:9-278 (§8(f3),
+BASELINE config 4).
+
+Same registry name, constructor (adversary_cfg, adversarial_loss_weight, regularization_weight,
+**CenterPoint kwargs with the pts_ prefix), attributes (`adversary`, `_epoch`, `_current_l2_norm`)
+and methods (`extract_pts_feat`, `loss`, `loss_by_feat_single`, `predict`, `set_epoch`).
+
+extract_pts_feat (:43-115): from `_epoch >= 3` in training the raw voxels are perturbed before the
+VFE; with HardSimpleVFE the valid-slot compaction (`sum != 0`, :77), the perturber, the scatter back
+and the VFE are the fused VoxelPerturber.perturb_voxels sequence (no host synchronisation).
+loss_by_feat_single (:203-257): detection losses clamped to [0, 100] and NaN/Inf-skipped, summed;
+loss_adversarial = -min(w * epoch / 10, w) * total when total > 0 (the `.item() > 0` branch of :232
+as a device-side select), loss_l2_regularization = regularization_weight * l2, and the logged
+perturbation_l2_norm.
+
+Documented fix (SURVEY.md finding 5): the reference stores the perturber's second output — its loss
+DICT — as `_current_l2_norm` (:81) and then multiplies / isnan()s it (:247, :252), which raises once
+`_epoch >= 3`; here `_current_l2_norm` is that dict's 'l2_norm' scalar, the value the code means.
+"""
+from __future__ import annotations
+
+from typing import Dict, List
+
+import torch
+from torch import Tensor
+
+from robustpointclouds_amd.centerpoint import CenterPoint
+from robustpointclouds_amd.registry import MODELS as _LOCAL_MODELS
+from robustpointclouds_amd.voxelnet import HardSimpleVFE
+
+from .. import builder
+
+try:  # register into mmdet3d too when it is installed
+    from mmdet3d.registry import MODELS as _MM_MODELS
+except Exception:  # pragma: no cover - mmdet3d absent in this image
+    _MM_MODELS = None
+
+
+def _register(cls):
+    _LOCAL_MODELS.register_module(module=cls)
+    if _MM_MODELS is not None:
+        _MM_MODELS.register_module(module=cls, force=True)
+    return cls
+
+
+@_register
+class AdversarialCenterPoint(CenterPoint):
+    def __init__(self, adversary_cfg: dict = None, adversarial_loss_weight: float = 1.0,
+                 regularization_weight: float = 0.05, **kwargs):
+        super().__init__(**kwargs)
+        self.adversary = builder.build_adversary(adversary_cfg) if adversary_cfg is not None else None
+        if self.adversary is not None:
+            self.adversary._return_loss_dict = True
+        self.adversarial_loss_weight = adversarial_loss_weight
+        self.regularization_weight = regularization_weight
+        self._current_l2_norm = None
+        self._epoch = 0
+
+    def extract_pts_feat(self, voxel_dict, points=None, img_feats=None, batch_input_metas=None):
+        if self.adversary is None:
+            return super().extract_pts_feat(voxel_dict, points, img_feats, batch_input_metas)
+        voxels, npts, coors = voxel_dict["voxels"], voxel_dict["num_points"], voxel_dict["coors"]
+        l2 = None
+        if self.training and self._epoch >= 3:
+            if isinstance(self.pts_voxel_encoder, HardSimpleVFE):
+                feats, loss_dict, _, _ = self.adversary.perturb_voxels(voxels, npts, self.pts_voxel_encoder.num_features)
+            else:
+                V, P, F = voxels.shape
+                flat = voxels.view(-1, F)
+                valid = flat.sum(dim=1) != 0                                           # :77
+                out, loss_dict = self.adversary(flat[valid])
+                flat2 = flat.clone()
+                flat2[valid] = out
+                feats = self.pts_voxel_encoder(flat2.view(V, P, F), npts, coors)
+            l2 = loss_dict["l2_norm"]                                                  # finding 5 fix
+        else:
+            feats = self.pts_voxel_encoder(voxels, npts, coors)
+        x = self.pts_middle_encoder(feats, coors, self._batch_size(voxel_dict))         # :114
+        x = self.pts_backbone(x)
+        if self.with_pts_neck:
+            x = self.pts_neck(x)
+        self._current_l2_norm = l2
+        return x
+
+    def loss(self, batch_inputs_dict: Dict[str, Tensor], batch_data_samples, **kwargs):
+        losses = {}
+        if batch_inputs_dict.get("points", None) is not None or "voxels" in batch_inputs_dict:
+            vd = dict(batch_inputs_dict["voxels"])
+            vd.setdefault("batch_size", batch_inputs_dict.get("batch_size"))
+            losses.update(self.loss_by_feat_single(vd, batch_data_samples, **kwargs))
+        return losses
+
+    def loss_by_feat_single(self, voxel_dict, batch_data_samples, **kwargs):
+        outs = self.pts_bbox_head(self.extract_pts_feat(voxel_dict))
+        if isinstance(batch_data_samples, dict):
+            gts = batch_data_samples
+        else:
+            gts = [s.gt_instances_3d for s in batch_data_samples]
+        losses = self.pts_bbox_head.loss_by_feat(outs, gts)
+        device = voxel_dict["voxels"].device
+        zero = lambda: torch.zeros((), device=device, requires_grad=True)
+        if self.training and self._current_l2_norm is not None:
+            det = torch.zeros((), device=device)
+            for k, v in losses.items():
+                if "loss" in k and isinstance(v, torch.Tensor):
+                    c = torch.clamp(v, min=0.0, max=100.0)
+                    det = det + torch.where(torch.isfinite(c), c, torch.zeros_like(c))
+            w = min(self.adversarial_loss_weight * (self._epoch / 10.0), self.adversarial_loss_weight)
+            adv = -w * det
+            losses["loss_adversarial"] = torch.where(det > 0, adv, torch.zeros_like(adv))
+            losses["loss_l2_regularization"] = self.regularization_weight * self._current_l2_norm
+            losses["perturbation_l2_norm"] = self._current_l2_norm.detach()
+        else:
+            losses["loss_adversarial"] = zero()
+            losses["loss_l2_regularization"] = zero()
+        return losses
+
+    @torch.no_grad()
+    def predict(self, batch_inputs_dict, batch_data_samples=None, **kwargs) -> List[dict]:
+        """Raw per-task head outputs (CenterPoint box decoding / circle NMS are evaluation-only, out of
+        this build's scope) plus the perturbation norm like :262-273."""
+        vd = dict(batch_inputs_dict["voxels"])
+        vd.setdefault("batch_size", batch_inputs_dict.get("batch_size"))
+        preds = self.pts_bbox_head(self.extract_pts_feat(vd))
+        res = [{k: v for k, v in p[0].items() if not k.startswith("_")} for p in preds]
+        if self._current_l2_norm is not None:
+            for r in res:
+                r["perturbation_l2_norm"] = float(self._current_l2_norm)
+        return res
+
+    def set_epoch(self, epoch):
+        self._epoch = epoch

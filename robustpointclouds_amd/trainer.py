@@ -69,7 +69,7 @@ class Trainer:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.module = model.to(self.device)
         self.model = model
-        if bf16 and hasattr(model, "middle_encoder") and hasattr(model.middle_encoder, "bf16"):
+        if bf16 and getattr(model, "middle_encoder", None) is not None and hasattr(model.middle_encoder, "bf16"):
             # perf mode: sparse convs on bf16 MFMA; dense BEV handed over as a bf16 NHWC image to
             # SECOND / SECONDFPN on the HIP dense-conv engine and the HIP head (the images are
             # channels_last; the parameters keep torch's contiguous layout, so gradients are stolen
@@ -77,7 +77,7 @@ class Trainer:
             model.middle_encoder.bf16 = True
             model.middle_encoder.dense_nhwc = True
             model.middle_encoder.dense_bf16 = True
-            for name in ("backbone", "neck"):
+            for name in ("backbone", "neck", "pts_backbone", "pts_neck"):
                 mod = getattr(model, name, None)
                 if mod is None:
                     continue
@@ -172,6 +172,18 @@ def make_kitti_model(num_classes=1, device=None, adversarial=True, hidden_channe
         cfg = second_kitti_cfg(num_classes, hidden_channels=hidden_channels, adversarial=adversarial)
     model = build_model(cfg)
     # DDP calls forward(); route it to loss() like mmengine's BaseModel.forward(mode='loss')
+    model.forward = _ddp_forward.__get__(model)
+    model._epoch = epoch
+    if device is not None:
+        model.to(device)
+    return model
+
+
+def make_nus_model(device=None, adversarial=True, epoch=3):
+    """AdversarialCenterPoint on the nuScenes CenterPoint stack (configs/adversarial/
+    adversarial-centerpoint_voxel-nuscenes.py, BASELINE config 4)."""
+    from .centerpoint import centerpoint_nus_cfg
+    model = build_model(centerpoint_nus_cfg(adversarial=adversarial))
     model.forward = _ddp_forward.__get__(model)
     model._epoch = epoch
     if device is not None:

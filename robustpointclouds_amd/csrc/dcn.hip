@@ -14,10 +14,12 @@
 //             group), 4 waves multiply it by the tap's block-diagonal 64 x 64 weight (bf16 MFMA
 //             16x16x32, fp32 accumulate over the 9 taps), bf16 output image.
 //   backward: per tap, the same sampling, dcol = dOut x W_k (MFMA), dW_k's four diagonal 16 x 16
-//             blocks += dOut^T x col (one wave per group, MFMA over the 64 pixels), then each thread
-//             forms the offset gradient (mmcv get_coordinate_weight) and scatters the input gradient
-//             (bilinear weights) into an fp32 LDS copy of the window (corners outside: global
-//             atomics); the window is flushed with global atomics once per tile.
+//             blocks = dOut^T x col (one wave per group, MFMA over the 64 pixels), the offset
+//             gradient per (pixel, group) thread (mmcv get_coordinate_weight), and the input
+//             gradient as a GEMM: dx_window += S_k x dcol_k with S_k the [144 x 64] bilinear-weight
+//             matrix of the in-window corners (corners outside: global atomics); the window goes to
+//             a per-tile slab and k_gather_dx sums, per pixel, the (at most 4) covering slabs in a
+//             fixed order.
 #include <hip/hip_runtime.h>
 #include <math.h>
 
@@ -238,60 +240,89 @@ __global__ __launch_bounds__(BLK) void k_fwd(Geo g, const u16* __restrict__ x, i
   }
 }
 
+// Input-gradient scatter as a GEMM: per tap, S_k [144 window pixels][64 tile pixels] holds the
+// bilinear weight of every in-window corner (4 per sampled pixel), and dx_window += S_k x dcol_k
+// (bf16 MFMA, fp32 accumulators held in registers across the taps: 9 16x16 tiles per wave).
+constexpr int PS = 64 + 8;     // S row pitch (elements)
+
 __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, int xp, const u16* __restrict__ off,
                                              int offp, const float* __restrict__ ob, const u16* __restrict__ wd,
                                              const u16* __restrict__ dout, int dop, float* __restrict__ dx,
                                              u16* __restrict__ doff, int doffp, float* __restrict__ pw_part,
-                                             float* __restrict__ pb_part) {
+                                             float* __restrict__ pb_part, float* __restrict__ win_part) {
   __shared__ __attribute__((aligned(16))) u16 sXw[WR * PW];
   __shared__ __attribute__((aligned(16))) u16 sDo[64 * P];
   __shared__ __attribute__((aligned(16))) u16 sC[64 * P];
-  __shared__ float sDc[64 * (C + 4)];
-  __shared__ float sDx[WR * C];
-  __shared__ float sOff[64 * 2 * KT];
+  __shared__ __attribute__((aligned(16))) u16 sDcT[64 * PS];    // dcol^T [channel][pixel], bf16
+  __shared__ __attribute__((aligned(16))) u16 sS[2][WR * PS];    // S_k, double-buffered
+  __shared__ __attribute__((aligned(16))) float sDc[64 * (C + 4)];
+  __shared__ float sOin[64 * 2 * KT];     // offsets (+ bias) of the tile, all taps
+  __shared__ float sOff[64 * 2 * KT];     // offset gradients
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const Tile tl = tile_of(g, blockIdx.x);
   stage_window(g, tl, x, xp, sXw);
   for (int qd = tid; qd < 64 * 8; qd += BLK) {
     const int pp = qd >> 3, seg = qd & 7;
     const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
-    *(uint4*)&sDo[pp * P + seg * 8] = *(const uint4*)(dout + ((size_t)(tl.b * g.H + yy) * g.W + xw) * dop + seg * 8);
+    const size_t pix = (size_t)(tl.b * g.H + yy) * g.W + xw;
+    *(uint4*)&sDo[pp * P + seg * 8] = *(const uint4*)(dout + pix * dop + seg * 8);
   }
-  for (int i = tid; i < WR * C; i += BLK) sDx[i] = 0.0f;
+  for (int i = tid; i < 64 * 2 * KT; i += BLK) {
+    const int pp = i / (2 * KT), c = i - pp * 2 * KT;
+    const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
+    sOin[i] = bf2f(off[((size_t)(tl.b * g.H + yy) * g.W + xw) * offp + c]) + ob[c];
+  }
+  for (int i = tid; i < 2 * WR * PS / 8; i += BLK) ((uint4*)&sS[0][0])[i] = make_uint4(0u, 0u, 0u, 0u);
   const int p = tid >> 2, q = tid & 3;
   const int y = tl.y0 + (p >> 3), xx = tl.x0 + (p & 7);
-  const size_t pix = (size_t)(tl.b * g.H + y) * g.W + xx;
   const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp4 = lane & 3, rowoff = 4 * g4 + qq;
+  // B fragments of dcol = dOut x W_k (W_k as [ci][co]) for the current tap, prefetched one tap ahead
+  bf16x8 bw[2][4];
+  auto load_b = [&](int k) {
+    const u16* wk = wd + (size_t)k * C * C;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int n = 0; n < 4; ++n) bw[ks][n] = *(const bf16x8*)&wk[(n * 16 + (lane & 15)) * C + 32 * ks + 8 * (lane >> 4)];
+  };
+  load_b(0);
+  // dx window accumulators: wave w owns window rows 16*(w + 4*i) .. (i < 3, 9 row tiles over 4 waves),
+  // all 64 channels (4 column tiles)
+  f32x4 acc[3][4];
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  int prev_u = -1;                        // this thread's S entry of the previous use of the buffer
   __syncthreads();
 #pragma unroll 1
   for (int k = 0; k < KT; ++k) {
-    float dy, dxo, col[CG];
-    offsets(off, offp, ob, pix, k, &dy, &dxo);
-    const Samp s = samp(g, y, xx, k, dy, dxo);
-    sample16(g, tl, x, xp, sXw, s, q, col);
-    store_col(sC, p, q, col);
-    __syncthreads();
-    // dcol[px][ci] = sum_co dOut[px][co] W[co][ci]: wave w owns pixels 16w..16w+15
+    u16* S = sS[k & 1];
+    // A: sample the column block of tap k (thread = pixel x group); thread q also owns corner q of
+    // its pixel: it clears its entry of tap k-1 in the other buffer (read by tap k-1's phase D before
+    // the last barrier, next written at tap k+1 after two more) and writes the new bilinear weight
+    const Samp s = samp(g, y, xx, k, sOin[p * 2 * KT + 2 * k], sOin[p * 2 * KT + 2 * k + 1]);
     {
-      const u16* wk = wd + (size_t)k * C * C;
-      f32x4 d[4];
-#pragma unroll
-      for (int n = 0; n < 4; ++n) d[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const bf16x8 a = *(const bf16x8*)&sDo[(16 * w + (lane & 15)) * P + 32 * ks + 8 * (lane >> 4)];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const bf16x8 bv = *(const bf16x8*)&wk[(n * 16 + (lane & 15)) * C + 32 * ks + 8 * (lane >> 4)];
-          d[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, d[n], 0, 0, 0);
+      float col[CG];
+      sample16(g, tl, x, xp, sXw, s, q, col);
+      store_col(sC, p, q, col);
+      if (prev_u >= 0) sS[(k + 1) & 1][prev_u * PS + p] = 0;
+      prev_u = -1;
+      const int cok = q == 0 ? s.c1 : (q == 1 ? s.c2 : (q == 2 ? s.c3 : s.c4));
+      if (s.valid && cok) {
+        const float wq = q == 0 ? s.hh * s.hw : (q == 1 ? s.hh * s.lw : (q == 2 ? s.lh * s.hw : s.lh * s.lw));
+        const int cy = s.hl + (q >> 1), cx = s.wl + (q & 1);
+        const int wy = cy - (tl.y0 - 2), wx = cx - (tl.x0 - 2);
+        if (wy >= 0 && wy < WE && wx >= 0 && wx < WE) {
+          prev_u = wy * WE + wx;
+          S[prev_u * PS + p] = f2bf(wq);
+        } else {
+          prev_u = -2 - (cy * 65536 + cx);   // out-of-window corner: global atomics after dcol
         }
       }
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) sDc[(16 * w + 4 * g4 + r) * (C + 4) + 16 * n + (lane & 15)] = d[n][r];
     }
-    // dW_k diagonal block of group w over this tile's 64 pixels: dOut^T col -> partial [tile][k][w]
+    __syncthreads();
+    // B: dW_k diagonal block of group w (dOut^T col over the tile) and dcol (wave w: pixels 16w..)
     {
       f32x4 aw = (f32x4){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -304,49 +335,83 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         pw_part[(((size_t)blockIdx.x * KT + k) * 4 + w) * 256 + (4 * g4 + r) * 16 + (lane & 15)] = aw[r];
+      f32x4 d[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) d[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 a = *(const bf16x8*)&sDo[(16 * w + (lane & 15)) * P + 32 * ks + 8 * (lane >> 4)];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) d[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bw[ks][n], d[n], 0, 0, 0);
+      }
+      if (k + 1 < KT) load_b(k + 1);
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int pr = 16 * w + 4 * g4 + r, cc = 16 * n + (lane & 15);
+          sDc[pr * (C + 4) + cc] = d[n][r];
+          sDcT[cc * PS + pr] = f2bf(d[n][r]);
+        }
     }
     __syncthreads();
-    // offset gradient + input gradient of this (pixel, tap, group)
-    float gh = 0.0f, gw = 0.0f;
-    if (s.valid) {
-      float dc[CG], v[CG];
+    // C: offset gradient (mmcv get_coordinate_weight), thread = pixel x group, the four groups
+    // combined by two xor shuffles; out-of-window corners scatter with global atomics
+    {
+      float gh = 0.0f, gw = 0.0f;
+      if (s.valid) {
+        float dc[CG], v[CG];
 #pragma unroll
-      for (int c = 0; c < CG; ++c) dc[c] = sDc[p * (C + 4) + q * CG + c];
-      const float w1 = s.hh * s.hw, w2 = s.hh * s.lw, w3 = s.lh * s.hw, w4 = s.lh * s.lw;
-      const int cys[4] = {s.hl, s.hl, s.hl + 1, s.hl + 1}, cxs[4] = {s.wl, s.wl + 1, s.wl, s.wl + 1};
-      const int cok[4] = {s.c1, s.c2, s.c3, s.c4};
-      const float cw[4] = {w1, w2, w3, w4};
-      // d val / d h and d val / d w per corner (get_coordinate_weight)
-      const float ch[4] = {-s.hw, -s.lw, s.hw, s.lw}, cwd[4] = {-s.hh, s.hh, -s.lh, s.lh};
+        for (int c4 = 0; c4 < CG / 4; ++c4) {
+          const float4 t4 = *(const float4*)&sDc[p * (C + 4) + q * CG + 4 * c4];
+          dc[4 * c4] = t4.x;
+          dc[4 * c4 + 1] = t4.y;
+          dc[4 * c4 + 2] = t4.z;
+          dc[4 * c4 + 3] = t4.w;
+        }
+        const int cok[4] = {s.c1, s.c2, s.c3, s.c4};
+        const float ch[4] = {-s.hw, -s.lw, s.hw, s.lw}, cwd[4] = {-s.hh, s.hh, -s.lh, s.lh};
 #pragma unroll
-      for (int cn = 0; cn < 4; ++cn) {
-        if (!cok[cn]) continue;
-        fetch16(g, tl, x, xp, sXw, cys[cn], cxs[cn], q, v);
-        float sv = 0.0f;
+        for (int cn = 0; cn < 4; ++cn) {
+          if (!cok[cn]) continue;
+          fetch16(g, tl, x, xp, sXw, s.hl + (cn >> 1), s.wl + (cn & 1), q, v);
+          float sv = 0.0f;
 #pragma unroll
-        for (int c = 0; c < CG; ++c) sv += dc[c] * v[c];
-        gh += ch[cn] * sv;
-        gw += cwd[cn] * sv;
-        const int wy = cys[cn] - (tl.y0 - 2), wx = cxs[cn] - (tl.x0 - 2);
-        if (wy >= 0 && wy < WE && wx >= 0 && wx < WE) {
-          float* dst = &sDx[(wy * WE + wx) * C + q * CG];
-#pragma unroll
-          for (int c = 0; c < CG; ++c) atomicAdd(&dst[c], cw[cn] * dc[c]);
-        } else {
-          float* dst = dx + ((size_t)(tl.b * g.H + cys[cn]) * g.W + cxs[cn]) * C + q * CG;
-#pragma unroll
-          for (int c = 0; c < CG; ++c) atomicAdd(&dst[c], cw[cn] * dc[c]);
+          for (int c = 0; c < CG; ++c) sv += dc[c] * v[c];
+          gh += ch[cn] * sv;
+          gw += cwd[cn] * sv;
         }
       }
+      gh += __shfl_xor(gh, 1, 64);
+      gw += __shfl_xor(gw, 1, 64);
+      gh += __shfl_xor(gh, 2, 64);
+      gw += __shfl_xor(gw, 2, 64);
+      if (q == 0) {
+        sOff[p * 2 * KT + 2 * k] = gh;
+        sOff[p * 2 * KT + 2 * k + 1] = gw;
+      }
+      if (prev_u <= -2) {                  // rare: this thread's corner lies outside the window
+        const int code = -2 - prev_u, cy = code >> 16, cx = code & 0xffff;
+        const float wq = q == 0 ? s.hh * s.hw : (q == 1 ? s.hh * s.lw : (q == 2 ? s.lh * s.hw : s.lh * s.lw));
+        float* dst = dx + ((size_t)(tl.b * g.H + cy) * g.W + cx) * C;
+        for (int c = 0; c < C; ++c) atomicAdd(&dst[c], wq * sDc[p * (C + 4) + c]);
+        prev_u = -1;
+      }
     }
-    // the four groups of a pixel are lanes 4p..4p+3 of one wave: fixed-order pair sums
-    gh += __shfl_xor(gh, 1, 64);
-    gw += __shfl_xor(gw, 1, 64);
-    gh += __shfl_xor(gh, 2, 64);
-    gw += __shfl_xor(gw, 2, 64);
-    if (q == 0) {
-      sOff[p * 2 * KT + 2 * k] = gh;
-      sOff[p * 2 * KT + 2 * k + 1] = gw;
+    // D: dx_window += S_k x dcol_k (M = window pixels, N = channels, K = tile pixels)
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const int rt = w + 4 * i;               // window row tile (16 window pixels), 9 in all
+      if (rt >= WR / 16) break;
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const bf16x8 a = *(const bf16x8*)&S[(16 * rt + (lane & 15)) * PS + 32 * ks + 8 * (lane >> 4)];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const bf16x8 bv = *(const bf16x8*)&sDcT[(16 * n + (lane & 15)) * PS + 32 * ks + 8 * (lane >> 4)];
+          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, bv, acc[i][n], 0, 0, 0);
+        }
+      }
     }
     __syncthreads();
   }
@@ -369,15 +434,42 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
     for (int pp = 0; pp < 64; ++pp) sacc += sOff[pp * 2 * KT + tid];
     pb_part[(size_t)blockIdx.x * 2 * KT + tid] = sacc;
   }
-  // flush the window's input gradient
-  for (int i = tid; i < WR * C; i += BLK) {
-    const float v = sDx[i];
-    if (v == 0.0f) continue;
-    const int wp = i / C, c = i - wp * C;
-    const int hy = tl.y0 - 2 + wp / WE, hx = tl.x0 - 2 + wp % WE;
-    if (hy >= 0 && hy < g.H && hx >= 0 && hx < g.W)
-      atomicAdd(&dx[((size_t)(tl.b * g.H + hy) * g.W + hx) * C + c], v);
+  // the window's input gradient -> this tile's slab [144][64] (k_gather_dx sums the <= 4 covering
+  // slabs per pixel in a fixed order: no atomics, deterministic)
+  float* wdst = win_part + (size_t)blockIdx.x * WR * C;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    const int rt = w + 4 * i;
+    if (rt >= WR / 16) break;
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wdst[(16 * rt + 4 * g4 + r) * C + 16 * n + (lane & 15)] = acc[i][n][r];
   }
+}
+
+__global__ __launch_bounds__(BLK) void k_gather_dx(Geo g, const float* __restrict__ win_part, float* __restrict__ dx) {
+  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e >= (long long)g.B * g.H * g.W * C) return;
+  const long long pix = e / C;
+  const int c = (int)(e - pix * C);
+  const int b = (int)(pix / ((long long)g.H * g.W)), r = (int)(pix - (long long)b * g.H * g.W);
+  const int y = r / g.W, x = r - (r / g.W) * g.W;
+  // tiles whose window rows [8t - 2, 8t + 10) contain y
+  const int ty0 = max(0, (y + 6) / TE - 1), ty1 = min(g.TY - 1, (y + 2) / TE);
+  const int tx0 = max(0, (x + 6) / TE - 1), tx1 = min(g.TX - 1, (x + 2) / TE);
+  float s = 0.0f;
+  for (int ty = ty0; ty <= ty1; ++ty) {
+    const int wy = y - (ty * TE - 2);
+    if (wy < 0 || wy >= WE) continue;
+    for (int tx = tx0; tx <= tx1; ++tx) {
+      const int wx = x - (tx * TE - 2);
+      if (wx < 0 || wx >= WE) continue;
+      const size_t t = ((size_t)b * g.TY + ty) * g.TX + tx;
+      s += win_part[(t * WR + wy * WE + wx) * C + c];
+    }
+  }
+  dx[e] += s;
 }
 
 // dWdiag [9][4][16 co][16 ci] -> module layout [64 co][16 ci][3][3]
@@ -425,7 +517,7 @@ extern "C" size_t rpc_dcn_backward_workspace_size(int B, int H, int W) {
   Geo g;
   if (!check_geo(B, H, W, &g)) return 0;
   const size_t tiles = (size_t)B * g.TY * g.TX;
-  return (tiles * KT * 1024 + tiles * 2 * KT + KT * 1024) * sizeof(float);
+  return (tiles * KT * 1024 + tiles * 2 * KT + KT * 1024 + tiles * WR * C) * sizeof(float);
 }
 
 extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp, const float* off_bias,
@@ -443,9 +535,12 @@ extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp
   float* pw = (float*)workspace;
   float* pb = pw + (size_t)tiles * KT * 1024;
   float* dwd = pb + (size_t)tiles * 2 * KT;
+  float* win = dwd + KT * 1024;
   hipLaunchKernelGGL(k_bwd, dim3(tiles), dim3(BLK), 0, st, g, (const u16*)x, xp, (const u16*)off, offp, off_bias,
-                     (const u16*)w_bwd, (const u16*)dout, dop, dx, (u16*)doff, doffp, pw, pb);
+                     (const u16*)w_bwd, (const u16*)dout, dop, dx, (u16*)doff, doffp, pw, pb, win);
   RPC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_gather_dx, dim3((unsigned)(((long long)B * H * W * C + BLK - 1) / BLK)), dim3(BLK), 0, st, g,
+                     (const float*)win, dx);
   slab_reduce(pw, tiles, (long long)KT * 1024, dwd, st);
   slab_reduce(pb, tiles, 2 * KT, doff_bias, st);
   hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW);

@@ -78,6 +78,23 @@ class _Base3DDetector(nn.Module):
         super().__init__()
 
 
+class _CenterPoint(nn.Module):
+    """Stand-in for mmdet3d CenterPoint (MVXTwoStageDetector points branch): holds the pts_ modules."""
+
+    def __init__(self, pts_voxel_encoder=None, pts_middle_encoder=None, pts_backbone=None, pts_neck=None,
+                 pts_bbox_head=None, **kw):
+        super().__init__()
+        self.pts_voxel_encoder = pts_voxel_encoder
+        self.pts_middle_encoder = pts_middle_encoder
+        self.pts_backbone = pts_backbone
+        self.pts_neck = pts_neck
+        self.pts_bbox_head = pts_bbox_head
+
+    @property
+    def with_pts_neck(self):
+        return self.pts_neck is not None
+
+
 def _install_stubs():
     me = types.ModuleType("mmengine")
     mer = types.ModuleType("mmengine.registry")
@@ -95,9 +112,12 @@ def _install_stubs():
     m3mv = types.ModuleType("mmdet3d.models.detectors.voxelnet")
     m3mv.VoxelNet = _VoxelNet
     m3md.Base3DDetector = _Base3DDetector
+    m3mc = types.ModuleType("mmdet3d.models.detectors.centerpoint")
+    m3mc.CenterPoint = _CenterPoint
     for n, m in {"mmdet3d": m3, "mmdet3d.registry": m3r, "mmdet3d.structures": m3s,
                  "mmdet3d.models": m3m, "mmdet3d.models.detectors": m3md,
-                 "mmdet3d.models.detectors.voxelnet": m3mv}.items():
+                 "mmdet3d.models.detectors.voxelnet": m3mv,
+                 "mmdet3d.models.detectors.centerpoint": m3mc}.items():
         sys.modules[n] = m
 
 
@@ -395,6 +415,98 @@ def gen_strong(builder, sv, tag, listy, bound, seed, steps=53, V=400, hidden=(8,
           f"{rec['scaling'][-1]:.3f} total={d['total']:.6f}")
 
 
+class _StandInVFE5(nn.Module):
+    def forward(self, features, num_points, coors):
+        return features[:, :, :5].sum(dim=1) / num_points.type_as(features).view(-1, 1)
+
+
+class _StandInCenterHead(nn.Module):
+    """Twelve task losses from the per-frame features (task2.loss_heatmap > 100: the [0, 100] clamp)."""
+
+    def __init__(self, w):
+        super().__init__()
+        self.w = nn.Parameter(torch.from_numpy(w))
+
+    def forward(self, x):
+        return x
+
+    def loss_by_feat(self, x, gts, *args, **kw):
+        y = (x * 1e-2) @ self.w                 # [B, 12]
+        out = {}
+        for t in range(6):
+            out[f"task{t}.loss_heatmap"] = (y[:, 2 * t] ** 2).mean() * 1e-2 + 0.4 + (120.0 if t == 2 else 0.0)
+            out[f"task{t}.loss_bbox"] = y[:, 2 * t + 1].abs().mean() * 1e-2 + 0.1
+        return out
+
+
+class _Sample:
+    def __init__(self):
+        self.metainfo = {}
+        self.gt_instances_3d = None
+
+    def get(self, k, d=None):
+        return d
+
+
+class _L2Fix(nn.Module):
+    """The documented finding-5 fix applied to the reference run: the perturber's second output is
+    its loss dict; AdversarialCenterPoint treats it as a tensor, so expose the dict's l2_norm."""
+
+    def __init__(self, vp):
+        super().__init__()
+        self.vp = vp
+
+    def forward(self, x):
+        out, d = self.vp(x)
+        return out, d["l2_norm"]
+
+
+def gen_centerpoint(builder, tag, epoch, seed, V=300, hidden=(16, 32, 64)):
+    cp = _load("refmodels.detectors.adversarial_centerpoint",
+               os.path.join(REF, "models", "detectors", "adversarial_centerpoint.py"))
+    rng = np.random.default_rng(seed)
+    F = 5
+    w = perturber_weights(rng, F, hidden)
+    vox, npts = valid_slots(seed + 1, V, F, pmax=10)
+    B = 2
+    coors = np.zeros((V, 4), np.int32)
+    coors[:, 0] = (np.arange(V) >= V // 2).astype(np.int32)
+    hw = rng.standard_normal((5, 12)).astype(np.float32)
+    with _quiet():
+        model = cp.AdversarialCenterPoint(
+            adversary_cfg=dict(type="VoxelPerturber", sensor_error_bound=0.2, voxel_size=[0.1, 0.1, 0.2],
+                               use_spatial_attention=True, hidden_channels=list(hidden)),
+            adversarial_loss_weight=0.05, regularization_weight=0.005,
+            pts_voxel_encoder=_StandInVFE5(), pts_middle_encoder=_StandInMiddle(), pts_backbone=nn.Identity(),
+            pts_neck=None, pts_bbox_head=_StandInCenterHead(hw))
+        model.adversary._build_model(F)
+        lin, bns, att = set_perturber_weights(model.adversary, w)
+        model.adversary = _L2Fix(model.adversary)
+        model.train()
+        model.set_epoch(epoch)
+        vd = {"voxels": torch.from_numpy(vox), "num_points": torch.from_numpy(npts), "coors": torch.from_numpy(coors)}
+        losses = model.loss({"points": [None] * B, "voxels": vd}, [_Sample() for _ in range(B)])
+        total = 0
+        for k, v in losses.items():          # mmengine parse_losses: keys containing 'loss'
+            if "loss" in k:
+                total = total + v.mean()
+        total.backward()
+    d = dict(w)
+    d.update(vox=vox, num_points=npts, coors=coors, head_w=hw, epoch=np.int32(epoch),
+             hidden=np.array(hidden, np.int32), total=np.float32(total.item()))
+    for k, v in losses.items():
+        d["L_" + k] = np.float32(v.item())
+    g = lambda t: np.zeros(tuple(t.shape), np.float32) if t.grad is None else t.grad.numpy().copy()
+    for l, m in enumerate(lin):
+        d[f"dW{l}"] = g(m.weight)
+        d[f"db{l}"] = g(m.bias)
+    for l, m in enumerate(att):
+        d[f"dWa{l}"] = g(m.weight)
+    d["dhead_w"] = model.pts_bbox_head.w.grad.numpy().copy()
+    np.savez_compressed(os.path.join(OUT, f"centerpoint_{tag}.npz"), **d)
+    print(f"centerpoint_{tag}: " + ", ".join(f"{k}={v.item():.6f}" for k, v in d.items() if k.startswith("L_")))
+
+
 def main():
     torch.manual_seed(0)
     builder, vp, av = load_reference()
@@ -406,6 +518,9 @@ def main():
     gen_voxelnet(builder, av, "list_e7", True, 7, 12)
     gen_voxelnet(builder, av, "tensor_e3", False, 3, 13)
     gen_voxelnet(builder, av, "gate_e2", True, 2, 14)
+    gen_centerpoint(builder, "e3", 3, 31)
+    gen_centerpoint(builder, "e12", 12, 32)
+    gen_centerpoint(builder, "e2", 2, 33)
     sv = load_strong(builder)
     gen_strong(builder, sv, "list", True, 0.4, 21)
     gen_strong(builder, sv, "tensor", False, 0.4, 22)

@@ -269,18 +269,19 @@ __global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
 }
 
 // ------------------------------------------------------------------ 3x3 stride-1 conv (S1) with halo tiles
-// The 10 stride-1 layers of SECOND and their data gradients. Block = 16x16 output pixels of one
-// image x 128 output channels, 8 waves (4 pixel quarters x 2 channel halves, 64x64 each). Per
-// 64-channel chunk the 18x18 input halo is staged ONCE in LDS and all 9 taps read it at shifted
-// rows (9x fewer activation loads than the generic implicit GEMM); the per-tap weight tiles
-// (128 x 64, shared by every block through L2) stream through a 3-deep register ring into a
-// double-buffered LDS tile so two taps of loads are in flight during each tap's 32 MFMAs/wave;
-// the next chunk's halo is prefetched into registers during taps 5-8.
+// The 10 stride-1 layers of SECOND and their data gradients (and the 64-channel CenterHead convs).
+// Block = 16x16 output pixels of one image x 64 output channels, 4 waves (pixel quarters, 64 px x
+// 64 co each), 65 KB of LDS: two blocks share a CU, so one block's barriers and LDS stores overlap
+// the other's MFMAs. Per 64-channel chunk the 18x18 input halo is staged ONCE in LDS and all 9
+// taps read it at shifted rows (9x fewer activation loads than the generic implicit GEMM); the
+// per-tap weight tiles (64 x 64, shared by every block through L2) stream through a 3-deep
+// register ring into a double-buffered LDS tile; the next chunk's halo is prefetched into
+// registers during taps 5-8.
 constexpr int CT = 16;                  // spatial tile edge
 constexpr int HT = CT + 2;              // halo edge
 constexpr int HR = HT * HT;             // halo rows (324)
-constexpr int CBLK = 512;               // threads
-constexpr int HCH = (HR * 8 + CBLK - 1) / CBLK;   // halo 16-B chunks per thread (6)
+constexpr int CBLK = 256;               // threads
+constexpr int HCH = (HR * 8 + CBLK - 1) / CBLK;   // halo 16-B chunks per thread (11)
 
 struct C3 {
   const u16* src;  // input image rows [B*H*W][SP]
@@ -293,18 +294,16 @@ struct C3 {
   int B, H, W, TY, TX;   // image, tiles per column / row
 };
 
-// NARROW = 0: 128 output channels per block (waves 64 px x 64 co); NARROW = 1: 64 output channels
-// per block (waves 64 px x 32 co) for the 64-channel CenterHead convolutions.
-template <int NARROW = 0>
-__global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
-  constexpr int TNB = NARROW ? 64 : TN;   // output channels per block
-  constexpr int WCO = TNB / 2;            // output channels per wave
+template <int DUMMY = 0>
+__global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
+  constexpr int TNB = 64;                 // output channels per block
+  constexpr int WCO = TNB;                // output channels per wave
   constexpr int NI = WCO / 16;            // 16-channel MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) u16 sA[HR * LP];
   __shared__ __attribute__((aligned(16))) u16 sW[2][TNB * LP];
   __shared__ float sP[4][2][TNB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wp = w & 3, wc = w >> 2;
+  const int wp = w, wc = 0;
   const int ntiles = g.B * g.TY * g.TX;
   const int tile = xcd_remap(blockIdx.x, ntiles);
   const int b = tile / (g.TY * g.TX), trem = tile - b * g.TY * g.TX;
@@ -340,21 +339,21 @@ __global__ __launch_bounds__(CBLK, 1) void k_conv3x3(C3 g) {
             make_uint4(ra[i].x & keep, ra[i].y & keep, ra[i].z & keep, ra[i].w & keep);
     }
   };
-  // ---- weight tiles: step s = kc*9 + t; chunk q = tid, tid+512: row q>>3, channels (q&7)*8
+  // ---- weight tiles: step s = kc*9 + t; chunk q = tid, tid+256: row q>>3, channels (q&7)*8
   const int wrow = tid >> 3, wseg = (tid & 7) * 8;
   const u16* wbase = g.wt + (size_t)(n0 + wrow) * g.CIN + wseg;
-  const size_t wtap = (size_t)g.COUT * g.CIN, whalf = (size_t)64 * g.CIN;
+  const size_t wtap = (size_t)g.COUT * g.CIN, whalf = (size_t)32 * g.CIN;
 #define C3_WLOAD(R, s)                                                          \
   {                                                                             \
     const int kc_ = (s) / 9, t_ = (s) - kc_ * 9;                                \
     const u16* p_ = wbase + t_ * wtap + kc_ * BK;                               \
     R##a = *(const uint4*)p_;                                                   \
-    if (!NARROW) R##b = *(const uint4*)(p_ + whalf);                            \
+    R##b = *(const uint4*)(p_ + whalf);                                         \
   }
 #define C3_WSTORE(R, buf)                                        \
   {                                                              \
     *(uint4*)&sW[buf][wrow * LP + wseg] = R##a;                  \
-    if (!NARROW) *(uint4*)&sW[buf][(wrow + 64) * LP + wseg] = R##b; \
+    *(uint4*)&sW[buf][(wrow + 32) * LP + wseg] = R##b;           \
   }
   uint4 r0a, r0b, r1a, r1b, r2a, r2b;
 
@@ -858,8 +857,7 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   if (map == M_S1) {
     const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
     C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
-    if (g.COUT % TN == 0) hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / TN), dim3(CBLK), 0, st, c);
-    else hipLaunchKernelGGL(k_conv3x3<1>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
+    hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
     RPC_LAUNCH_CHECK();
     return RPC_OK;
   }

@@ -282,6 +282,7 @@ constexpr int HT = CT + 2;              // halo edge
 constexpr int HR = HT * HT;             // halo rows (324)
 constexpr int CBLK = 256;               // threads
 constexpr int HCH = (HR * 8 + CBLK - 1) / CBLK;   // halo 16-B chunks per thread (11)
+constexpr int LP3 = 80;                 // LDS row pitch (elements): conflict-free ds_read_b128 fragments
 
 struct C3 {
   const u16* src;  // input image rows [B*H*W][SP]
@@ -299,8 +300,8 @@ __global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
   constexpr int TNB = 64;                 // output channels per block
   constexpr int WCO = TNB;                // output channels per wave
   constexpr int NI = WCO / 16;            // 16-channel MFMA tiles per wave
-  __shared__ __attribute__((aligned(16))) u16 sA[HR * LP];
-  __shared__ __attribute__((aligned(16))) u16 sW[2][TNB * LP];
+  __shared__ __attribute__((aligned(16))) u16 sA[HR * LP3];
+  __shared__ __attribute__((aligned(16))) u16 sW[2][TNB * LP3];
   __shared__ float sP[4][2][TNB];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wp = w, wc = 0;
@@ -335,7 +336,7 @@ __global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
       const int q = tid + i * CBLK;
       const unsigned keep = ((hkeep >> i) & 1u) ? 0xffffffffu : 0u;
       if (q < HR * 8)
-        *(uint4*)&sA[(q >> 3) * LP + (q & 7) * 8] =
+        *(uint4*)&sA[(q >> 3) * LP3 + (q & 7) * 8] =
             make_uint4(ra[i].x & keep, ra[i].y & keep, ra[i].z & keep, ra[i].w & keep);
     }
   };
@@ -352,8 +353,8 @@ __global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
   }
 #define C3_WSTORE(R, buf)                                        \
   {                                                              \
-    *(uint4*)&sW[buf][wrow * LP + wseg] = R##a;                  \
-    *(uint4*)&sW[buf][(wrow + 32) * LP + wseg] = R##b;           \
+    *(uint4*)&sW[buf][wrow * LP3 + wseg] = R##a;                  \
+    *(uint4*)&sW[buf][(wrow + 32) * LP3 + wseg] = R##b;           \
   }
   uint4 r0a, r0b, r1a, r1b, r2a, r2b;
 
@@ -365,17 +366,17 @@ __global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
 
   // pixel p = wp*64 + j*16 + (lane&15) -> tile row wp*4 + j, column lane&15
   const int pcol = lane & 15;
-  const u16* aw = &sW[0][(wc * WCO + (lane & 15)) * LP + 8 * (lane >> 4)];
-  const u16* ab = &sA[(wp * 4 * HT + pcol) * LP + 8 * (lane >> 4)];
+  const u16* aw = &sW[0][(wc * WCO + (lane & 15)) * LP3 + 8 * (lane >> 4)];
+  const u16* ab = &sA[(wp * 4 * HT + pcol) * LP3 + 8 * (lane >> 4)];
 #define C3_COMPUTE(buf, t)                                                                                  \
   {                                                                                                         \
     const int dy_ = (t) / 3, dx_ = (t) % 3;                                                                 \
     _Pragma("unroll") for (int kk = 0; kk < BK / 32; ++kk) {                                                \
       bf16x8 a[NI], bb[4];                                                                                  \
       _Pragma("unroll") for (int i = 0; i < NI; ++i)                                                        \
-        a[i] = *(const bf16x8*)(aw + (buf) * (TNB * LP) + i * 16 * LP + kk * 32);                           \
+        a[i] = *(const bf16x8*)(aw + (buf) * (TNB * LP3) + i * 16 * LP3 + kk * 32);                           \
       _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                         \
-        bb[j] = *(const bf16x8*)(ab + ((j + dy_) * HT + dx_) * LP + kk * 32);                               \
+        bb[j] = *(const bf16x8*)(ab + ((j + dy_) * HT + dx_) * LP3 + kk * 32);                               \
       _Pragma("unroll") for (int i = 0; i < NI; ++i)                                                        \
         _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], bb[j], acc[i][j], 0, 0, 0);             \

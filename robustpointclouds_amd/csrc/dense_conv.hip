@@ -822,9 +822,27 @@ static int map_wtaps(int map) {
   }
 }
 
-static int wgrad_chunks(int M) {
-  int c = (M + 2047) / 2048;
-  return c < 1 ? 1 : (c > 1024 ? 1024 : c);
+// Row chunks of the weight gradient: the grid (chunks x taps x channel tiles) is sized to fill the
+// resident block slots of the chip in whole rounds (k_wgrad: 3 blocks per CU), chunks <= 4096 rows.
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+static int wgrad_chunks(int M, int T, int ci, int co) {
+  const int tc = (ci % 128 == 0 && co % 128 == 0) ? 128 : 64;
+  const int per = T * (ci / tc) * (co / tc);
+  const int slots = 3 * cu_count();
+  const int step = slots / per > 0 ? slots / per : 1;
+  int c = step;
+  while ((M + c - 1) / c > 4096 && c < 1024) c += step;
+  return c < 1024 ? c : 1024;
 }
 
 }  // namespace dn
@@ -883,7 +901,7 @@ extern "C" int rpc_dense_conv_blocks(int map, const int* r_img) {
 extern "C" size_t rpc_dense_wgrad_workspace_size(int map, const int* r_img, int ci, int co) {
   const int M = r_img[0] * r_img[1] * r_img[2];
   const int T = map_wtaps(map);
-  return (size_t)wgrad_chunks(M) * T * ci * co * sizeof(float) + (size_t)T * ci * co * sizeof(float);
+  return (size_t)wgrad_chunks(M, T, ci, co) * T * ci * co * sizeof(float) + (size_t)T * ci * co * sizeof(float);
 }
 
 extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci, const void* dz, int dp, int co,
@@ -893,7 +911,7 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
   if (ci % 64 || co % 64 || (xp & 7) || (dp & 7)) return RPC_ERR_ARG;
   Img R = img3(r_img), S = img3(s_img), O = img3(o_img);
   const int M = R.B * R.H * R.W, T = map_wtaps(map);
-  const int chunks = wgrad_chunks(M);
+  const int chunks = wgrad_chunks(M, T, ci, co);
   const size_t slab = (size_t)T * ci * co;
   if (ws_bytes < (chunks + 1) * slab * sizeof(float)) return RPC_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;

@@ -199,9 +199,10 @@ def init_distributed():
     world = int(os.environ["WORLD_SIZE"])
     local = int(os.environ.get("LOCAL_RANK", rank))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    backend = "nccl" if torch.cuda.is_available() else "gloo"
-    if backend == "nccl":
-        torch.cuda.set_device(local)
+    # nccl (= RCCL) on GPU; RPC_DIST_BACKEND=gloo lets several ranks share one GPU in tests
+    backend = os.environ.get("RPC_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+    if torch.cuda.is_available():
+        torch.cuda.set_device(local % torch.cuda.device_count())
     if not dist.is_initialized():
         dist.init_process_group(backend=backend)
     return rank, world, local

@@ -536,13 +536,35 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
     for (int j = 0; j < NW; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
   uint4 rx[NLD], rd[NLD];
+  // Row decode without per-load divisions: thread rows are r0 + (BLK / SEGS) * s of each sub-tile,
+  // so (b, y, x) of row rs + r0 is carried across sub-tiles and stepped by adding columns.
+  constexpr int RSTEP = BLK / SEGS;
+  const int r0 = tid / SEGS, seg = tid % SEGS;
+  int cb, cy, cx;
+  {
+    const int m = rb0 + r0, rem = m % HW;
+    cb = m / HW;
+    cy = rem / g.R.W;
+    cx = rem - cy * g.R.W;
+  }
+  auto step = [&](int& b, int& y, int& x, int k) {
+    x += k;
+    while (x >= g.R.W) {
+      x -= g.R.W;
+      if (++y == g.R.H) {
+        y = 0;
+        ++b;
+      }
+    }
+  };
   auto gload = [&](int rs) {
+    int b = cb, y = cy, x = cx;
 #pragma unroll
     for (int s = 0; s < NLD; ++s) {
-      const int q = tid + s * BLK, r = q / SEGS, seg = q % SEGS, m = rs + r;
+      if (s) step(b, y, x, RSTEP);
+      const int m = rs + r0 + s * RSTEP;
       rx[s] = rd[s] = make_uint4(0u, 0u, 0u, 0u);
       if (m < rb1) {
-        const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
         int xs, ds;
         if (MAP == M_U2) {
           xs = m;
@@ -557,6 +579,7 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
         }
       }
     }
+    step(cb, cy, cx, RT);
   };
   gload(rb0);
   for (int rs = rb0; rs < rb1; rs += RT) {

@@ -55,7 +55,7 @@ template <int KGP, int NT, int EPI>
 __global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;
-  constexpr int LS = KGP + 8;                 // LDS row stride (elements): 16 B pad
+  constexpr int LS = KGP + 16;                // LDS row stride: 8 mod 16 dwords, conflict-free b128 reads
   constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
   constexpr int BPT = (BV + BLK - 1) / BLK;
   __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];
@@ -67,14 +67,22 @@ __global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int r0 = blockIdx.x * BM;
   const int K = g.K;
-  if (tid < 4) wmask[tid] = 0;
-  __syncthreads();
-  for (int q = tid; q < BM * K; q += BLK) {
-    int r = q / K, k = q - r * K;
-    int kc = g.rev ? K - 1 - k : k;
-    int v = (r0 + r < g.Nout) ? g.nbr[(long long)(r0 + r) * K + kc] : -1;
-    sN[r * MAXK + k] = v;
-    if (v >= 0) atomicOr(&wmask[r >> 4], 1u << k);
+  {
+    // each wave stages its own 16 rows: lane = (offset group k4, row lane&15), 4 offsets per pass;
+    // the wave's offset mask comes from ballots (no LDS atomics)
+    const int rr = lane & 15, k4 = lane >> 4, row = r0 + w * 16 + rr;
+    unsigned m = 0;
+    for (int kb = 0; kb < K; kb += 4) {
+      const int k = kb + k4;
+      int v = -1;
+      if (k < K && row < g.Nout) v = g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)];
+      if (k < K) sN[(w * 16 + rr) * MAXK + k] = v;
+      const unsigned long long b = __ballot(v >= 0);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        if ((b >> (16 * q)) & 0xffffull) m |= 1u << (kb + q);
+    }
+    if (lane == 0) wmask[w] = m;
   }
   __syncthreads();
   if (tid == 0) {

@@ -10,7 +10,8 @@
 //   * the weight tile B_k^T [N][K] of the next offset is prefetched into registers and
 //     written to the other half of a double-buffered LDS ring while the MFMAs of the current
 //     offset run; one barrier per offset;
-//   * offsets with no neighbour in the 64-row tile are skipped by the block, offsets with
+//   * blocks of 8 waves (128 rows; 4 waves for 128 x 128 tiles) share each LDS weight tile;
+//     offsets with no neighbour in the block's rows are skipped by the block, offsets with
 //     none in a wave's 16 rows are skipped by that wave (no loads, no MFMA).
 // Accumulation in fp32; epilogues identical to spconv.hip (z out + BatchNorm partial sums,
 // or the previous layer's ReLU mask + BatchNorm-backward partial sums). No atomics on data.
@@ -23,7 +24,10 @@ namespace rpc {
 namespace spb {
 
 constexpr int BLK = 256;
-constexpr int BM = 64;
+constexpr int BM = 64;          // rows per BatchNorm partial row (rpc_spconv_gemm_blocks)
+// GEMM waves per block (16 rows each; all share one LDS weight tile per offset): 8 — the tile is
+// fetched once per 128 rows — unless the 128 x 128 tiles' LDS ring would leave one block per CU
+__host__ __device__ constexpr int gw_of(int kgp, int nt) { return kgp * nt * 16 >= 128 * 128 ? 4 : 8; }
 constexpr int MAXK = 27;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -52,20 +56,21 @@ struct GB {
 };
 
 template <int KGP, int NT, int EPI>
-__global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
+__global__ __launch_bounds__(64 * gw_of(KGP, NT)) void k_gemm_bf16(GB g) {
+  constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, GBM = 16 * GW;
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;
   constexpr int LS = KGP + 16;                // LDS row stride: 8 mod 16 dwords, conflict-free b128 reads
   constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
-  constexpr int BPT = (BV + BLK - 1) / BLK;
+  constexpr int BPT = (BV + GBLK - 1) / GBLK;
   __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];
-  __shared__ int sN[BM * MAXK];
-  __shared__ unsigned wmask[4];
+  __shared__ int sN[GBM * MAXK];
+  __shared__ unsigned wmask[GW];
   __shared__ int klist[MAXK];
   __shared__ int nk;
-  __shared__ float sP[4][2 * NGP];
+  __shared__ float sP[GW][2 * NGP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r0 = blockIdx.x * BM;
+  const int r0 = blockIdx.x * GBM;
   const int K = g.K;
   {
     // each wave stages its own 16 rows: lane = (offset group k4, row lane&15), 4 offsets per pass;
@@ -86,7 +91,8 @@ __global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
   }
   __syncthreads();
   if (tid == 0) {
-    unsigned m = wmask[0] | wmask[1] | wmask[2] | wmask[3];
+    unsigned m = 0;
+    for (int q = 0; q < GW; ++q) m |= wmask[q];
     int n = 0;
     for (int k = 0; k < K; ++k)
       if ((m >> k) & 1u) klist[n++] = k;
@@ -114,14 +120,14 @@ __global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
     const uint4* src = (const uint4*)(g.bt + (long long)k * NGP * KGP);
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
-      int v = tid + j * BLK;
+      int v = tid + j * GBLK;
       dst[j] = v < BV ? src[v] : make_uint4(0u, 0u, 0u, 0u);
     }
   };
   auto store_b = [&](int buf, const uint4 (&src)[BPT]) {
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
-      int v = tid + j * BLK;
+      int v = tid + j * GBLK;
       if (v < BV) {
         int e = v * 8, n = e / KGP, c = e - n * KGP;
         *(uint4*)&sB[buf][n * LS + c] = src[j];
@@ -207,11 +213,15 @@ __global__ __launch_bounds__(BLK) void k_gemm_bf16(GB g) {
   __syncthreads();
   // partial rows keep the CO_real-wide layout expected by rpc_bn_finalize: [blocks][2*CO_real]
   const int C = g.CO_real;
-  for (int j = tid; j < 2 * C; j += BLK) {
-    int which = j / C, c = j - which * C;
+  // one partial row per 64 rows (waves 4h..4h+3), the layout of rpc_spconv_gemm_blocks
+  const int nrow = (g.Nout + BM - 1) / BM;
+  for (int j = tid; j < (GW / 4) * 2 * C; j += GBLK) {
+    const int h = j / (2 * C), jj = j - h * 2 * C, prow = blockIdx.x * (GW / 4) + h;
+    if (prow >= nrow) continue;
+    int which = jj / C, c = jj - which * C;
     float s = 0.0f;
-    for (int ww = 0; ww < 4; ++ww) s += sP[ww][which * NGP + c];
-    g.part[(long long)blockIdx.x * 2 * C + j] = s;
+    for (int ww = 0; ww < 4; ++ww) s += sP[4 * h + ww][which * NGP + c];
+    g.part[(long long)prow * 2 * C + jj] = s;
   }
 }
 
@@ -414,14 +424,16 @@ __global__ __launch_bounds__(BLK) void k_wgrad_bf16(const u16* __restrict__ h, i
 }
 
 template <int KGP, int NT>
-static void launch_t(int epi, const GB& a, int nblk, hipStream_t st) {
-  if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(BLK), 0, st, a);
-  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(BLK), 0, st, a);
-  else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(BLK), 0, st, a);
+static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
+  constexpr int GW = gw_of(KGP, NT);
+  const int nblk = (n_rows + 16 * GW - 1) / (16 * GW);
+  if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(64 * GW), 0, st, a);
 }
 
-static int launch(int KGP, int NT, int epi, const GB& a, int nblk, hipStream_t st) {
-#define C2(kg, nt) if (KGP == kg && NT == nt) { launch_t<kg, nt>(epi, a, nblk, st); return RPC_OK; }
+static int launch(int KGP, int NT, int epi, const GB& a, int n_rows, hipStream_t st) {
+#define C2(kg, nt) if (KGP == kg && NT == nt) { launch_t<kg, nt>(epi, a, n_rows, st); return RPC_OK; }
   C2(32, 1) C2(32, 2) C2(32, 4) C2(64, 2) C2(64, 4) C2(64, 8) C2(128, 4) C2(32, 8) C2(64, 1) C2(128, 2) C2(128, 8)
 #undef C2
   return RPC_ERR_UNSUPPORTED;
@@ -496,7 +508,7 @@ extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int k
   g.ez = prev_z;
   g.ebn = prev_bn;
   g.part = part;
-  int rc = launch(r32(kg), r16(ng) / 16, epi, g, cdiv(n_out, BM), (hipStream_t)stream);
+  int rc = launch(r32(kg), r16(ng) / 16, epi, g, n_out, (hipStream_t)stream);
   if (rc) return rc;
   RPC_LAUNCH_CHECK();
   return RPC_OK;

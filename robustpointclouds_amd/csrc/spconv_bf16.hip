@@ -514,13 +514,50 @@ extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int k
   return RPC_OK;
 }
 
-static int wgrad_chunks(int n) {
+template <int CI, int CO, int KG>
+static int wgrad_resident() {   // resident blocks per CU of one k_wgrad_bf16 instantiation
+  static int r = 0;
+  if (r == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&r, k_wgrad_bf16<CI, CO, KG>, BLK, 0) != hipSuccess ||
+                 r <= 0))
+    r = 1;
+  return r;
+}
+
+static int wgrad_slots(int ci, int co) {   // resident blocks on the whole device
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  int per = 1;
+#define WR(a, b, kg) if (ci == a && co == b) per = wgrad_resident<a, b, kg>(); else
+  WR(16, 16, 3) WR(16, 32, 3) WR(32, 32, 3) WR(32, 64, 3) WR(64, 64, 3) WR(64, 128, 3) WR(128, 128, 1) {}
+#undef WR
+  return per * cus;
+}
+
+static int wgrad_kg(int ci, int co) { return (ci == 128 && co == 128) ? 1 : 3; }
+
+// row chunks: ~512 rows each, then trimmed so chunks x offset groups fills whole rounds of the
+// resident blocks (a partial last round costs a whole block time)
+static int wgrad_chunks(int n, int kvol, int ci, int co) {
   int c = (n + 511) / 512;
-  return c < 1 ? 1 : (c > 512 ? 512 : c);
+  c = c < 1 ? 1 : (c > 512 ? 512 : c);
+  const int groups = (kvol + wgrad_kg(ci, co) - 1) / wgrad_kg(ci, co);
+  const long long slots = wgrad_slots(ci, co);
+  const long long total = (long long)c * groups;
+  if (total > slots) {
+    const long long rounds = total / slots;
+    const int c2 = (int)(rounds * slots / groups);
+    if (c2 >= 1 && c2 < c) c = c2;
+  }
+  return c;
 }
 
 extern "C" size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co) {
-  return (size_t)wgrad_chunks(n_out) * kvol * ci * co * sizeof(float);
+  return (size_t)wgrad_chunks(n_out, kvol, ci, co) * kvol * ci * co * sizeof(float);
 }
 
 // dW[k] = sum_r h[nbr[r,k]]^T dz[r] with bf16 rows h [.][round8(ci)] and dz [n_out][round8(co)]
@@ -535,11 +572,11 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
     RPC_CHECK(hipMemsetAsync(dW, 0, sizeof(float) * (size_t)kvol * ci * co, st));
     return RPC_OK;
   }
-  int chunks = wgrad_chunks(n_out);
+  int chunks = wgrad_chunks(n_out, kvol, ci, co);
   if (ws_bytes < (size_t)chunks * kvol * ci * co * sizeof(float)) return RPC_ERR_WORKSPACE;
   int rows_per = ((n_out + chunks - 1) / chunks + 31) / 32 * 32;
   // 128 x 128 tiles keep one kernel offset per block (KG = 1: 64 accumulator registers / lane)
-  const int KG = (ci == 128 && co == 128) ? 1 : 3;
+  const int KG = wgrad_kg(ci, co);
   dim3 grid(chunks, (kvol + KG - 1) / KG);
   float* part = (float*)ws;
   const u16* hp = (const u16*)h;

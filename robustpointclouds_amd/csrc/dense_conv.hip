@@ -47,11 +47,21 @@ struct Img {
   int B, H, W;
 };
 
-enum { M_S1 = 0, M_S2 = 1, M_D2 = 2, M_P1 = 3, M_U2 = 4, M_G2 = 5 };
+// M_D2P (internal): the data gradient of S2 split by input-pixel parity (blockIdx.z = 2*py + px):
+// a pixel of parity (py, px) receives only the taps ty in {1} (py = 0) or {0, 2} (py = 1), and
+// likewise tx, so the four classes run 1, 2, 2 and 4 taps instead of 9 taps of mostly zero rows
+enum { M_S1 = 0, M_S2 = 1, M_D2 = 2, M_P1 = 3, M_U2 = 4, M_G2 = 5, M_D2P = 6 };
 
 template <int MAP>
 __host__ __device__ constexpr int taps_of() {
-  return (MAP == M_P1 || MAP == M_U2) ? 1 : (MAP == M_G2 ? 4 : 9);
+  return (MAP == M_P1 || MAP == M_U2) ? 1 : ((MAP == M_G2 || MAP == M_D2P) ? 4 : 9);
+}
+
+// tap j < ntaps of parity (py, px) of M_D2P -> 3x3 tap index
+__device__ __forceinline__ int d2p_tap(int j, int py, int px) {
+  const int ntx = px ? 2 : 1;
+  const int ty = py ? 2 * (j / ntx) : 1, tx = px ? 2 * (j % ntx) : 1;
+  return ty * 3 + tx;
 }
 // weight-gradient "taps": U2 has one GEMM per output parity, each with its own weight slice
 template <int MAP>
@@ -126,15 +136,26 @@ __global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wc = w >> 1, wp = w & 1;  // wave: output channels wc*64.., pixels wp*64..
   const int bx = xcd_remap(blockIdx.x, gridDim.x);
-  const int m0 = bx * TM, n0 = blockIdx.y * TN, par = blockIdx.z;
-  const int KC = g.CIN / BK, NKS = T * KC;
-  const u16* wbase = g.wt + (size_t)par * g.COUT * g.CIN;
+  // M_D2P: the 4-tap class (odd, odd) is dispatched first, the 1-tap class last (shorter tail)
+  const int m0 = bx * TM, n0 = blockIdx.y * TN, par = MAP == M_D2P ? 3 - (int)blockIdx.z : blockIdx.z;
+  const int py = par >> 1, px = par & 1;
+  // M_D2P: rows of parity class par, a (Hp x Wp) sub-grid of the row image
+  const int Hp = MAP == M_D2P ? (g.R.H - py + 1) >> 1 : g.R.H, Wp = MAP == M_D2P ? (g.R.W - px + 1) >> 1 : g.R.W;
+  const int Mrows = MAP == M_D2P ? g.R.B * Hp * Wp : g.M;
+  if (m0 >= Mrows) return;
+  const int KC = g.CIN / BK, NKS = (MAP == M_D2P ? (py + 1) * (px + 1) : T) * KC;
+  const u16* wbase = g.wt + (MAP == M_U2 ? (size_t)par * g.COUT * g.CIN : 0);
   const int HW = g.R.H * g.R.W;
 
   for (int q = tid; q < TM * T; q += BLK) {
     const int r = q / T, t = q - r * T, m = m0 + r;
     int s = -1;
-    if (m < g.M) {
+    if (MAP == M_D2P) {
+      if (m < Mrows && t < (py + 1) * (px + 1)) {
+        const int b = m / (Hp * Wp), rem = m - b * (Hp * Wp), yy = rem / Wp, xx = rem - yy * Wp;
+        s = src_row<M_D2>(b, 2 * yy + py, 2 * xx + px, d2p_tap(t, py, px), g.S);
+      }
+    } else if (m < g.M) {
       const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
       s = src_row<MAP>(b, y, x, t, g.S);
     }
@@ -153,7 +174,8 @@ __global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
     const unsigned keep_ = ~(unsigned)(sr_ >> 31);                                                  \
     uint4 v_ = *(const uint4*)(g.src + (size_t)max(sr_, 0) * g.SP + kc_ * BK + sseg);                \
     rx##S = make_uint4(v_.x & keep_, v_.y & keep_, v_.z & keep_, v_.w & keep_);                     \
-    rw##S = *(const uint4*)(wbase + ((size_t)(t_ * g.COUT + n0 + srow + 32 * S)) * g.CIN + kc_ * BK + sseg); \
+    const int tw_ = MAP == M_D2P ? d2p_tap(t_, py, px) : t_;                                        \
+    rw##S = *(const uint4*)(wbase + ((size_t)(tw_ * g.COUT + n0 + srow + 32 * S)) * g.CIN + kc_ * BK + sseg); \
   }
 #define IG_LOAD(ks) { IG_LOAD1(0, ks) IG_LOAD1(1, ks) IG_LOAD1(2, ks) IG_LOAD1(3, ks) }
 #define IG_STORE1(S, buf)                                          \
@@ -210,11 +232,14 @@ __global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int m = m0 + wp * 64 + j * 16 + (lane & 15);
-    if (m >= g.M) continue;
+    if (m >= Mrows) continue;
     int orow = m;
     if (MAP == M_U2) {
       const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
       orow = out_row<MAP>(m, b, y, x, par, g.O);
+    } else if (MAP == M_D2P) {
+      const int b = m / (Hp * Wp), rem = m - b * (Hp * Wp), yy = rem / Wp, xx = rem - yy * Wp;
+      orow = (b * g.R.H + 2 * yy + py) * g.R.W + 2 * xx + px;
     }
     u16* op = g.out + (size_t)orow * g.OP + g.OOFF + n0 + wc * 64 + 4 * (lane >> 4);
 #pragma unroll
@@ -821,7 +846,9 @@ static inline unsigned cdivu(long long a, long long b) { return (unsigned)((a + 
 
 template <int MAP>
 static void launch_igemm(const IG& g, int par_count, hipStream_t st) {
-  dim3 grid(cdivu(g.M, TM), g.COUT / TN, par_count);
+  // M_D2P: grid over the largest parity class (even rows, even columns)
+  const int rows = MAP == M_D2P ? g.R.B * ((g.R.H + 1) / 2) * ((g.R.W + 1) / 2) : g.M;
+  dim3 grid(cdivu(rows, TM), g.COUT / TN, par_count);
   hipLaunchKernelGGL((k_igemm<MAP>), grid, dim3(BLK), 0, st, g);
 }
 
@@ -906,7 +933,10 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   switch (map) {
     case M_S1: launch_igemm<M_S1>(g, 1, st); break;
     case M_S2: launch_igemm<M_S2>(g, 1, st); break;
-    case M_D2: launch_igemm<M_D2>(g, 1, st); break;
+    case M_D2:   // BatchNorm partials need the row-tile layout of rpc_dense_conv_blocks: 9-tap form
+      if (g.part) launch_igemm<M_D2>(g, 1, st);
+      else launch_igemm<M_D2P>(g, 4, st);
+      break;
     case M_P1: launch_igemm<M_P1>(g, 1, st); break;
     case M_U2: launch_igemm<M_U2>(g, 4, st); break;
     default: launch_igemm<M_G2>(g, 1, st); break;

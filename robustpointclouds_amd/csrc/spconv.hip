@@ -573,6 +573,104 @@ __global__ __launch_bounds__(BLK) void k_res_bwd(const float* __restrict__ g1, c
   }
 }
 
+
+// Weight gradient of the narrow input layer (CI * CO <= 128, the 4/5 -> 16 conv_input): every
+// block takes a chunk of rows for ALL K offsets, so the BatchNorm-backward dz tile is formed once
+// (not once per offset) and the K gathered x tiles sit side by side in LDS. Thread (k, ci, half)
+// keeps the CO sums of dW[k][ci][:] in registers over its half of the tile rows; the dz row it
+// reads is the same for all lanes of the wave (an LDS broadcast).
+template <int CI, int CO, int AT>
+__global__ __launch_bounds__(BLK) void k_wgrad_narrow(WgradArgs g) {
+  constexpr int RT = 64;
+  __shared__ __attribute__((aligned(16))) float sA[MAXK * RT * CI];
+  __shared__ __attribute__((aligned(16))) float sD[RT * CO];
+  __shared__ int sN[RT * MAXK];
+  __shared__ float sH[BLK / 2][CO];
+  const int tid = threadIdx.x, K = g.K;
+  const int rb0 = blockIdx.x * g.rows_per, rb1 = min(g.Nout, rb0 + g.rows_per);
+  const int pair = tid >> 1, half = tid & 1;          // (k, ci) pair, row parity
+  const int kk = pair / CI, ci = pair - kk * CI;
+  const bool own = pair < K * CI;
+  float acc[CO];
+#pragma unroll
+  for (int n = 0; n < CO; ++n) acc[n] = 0.f;
+  for (int rb = rb0; rb < rb1; rb += RT) {
+    __syncthreads();
+    for (int q = tid; q < RT * K; q += BLK) {
+      const int r = q / K, k = q - r * K, row = rb + r;
+      sN[q] = row < rb1 ? g.nbr[(long long)row * K + k] : -1;
+    }
+    for (int q = tid; q < RT * CO; q += BLK) {
+      const int r = q / CO, n = q - r * CO, row = rb + r;
+      float v = 0.0f;
+      if (row < rb1) {
+        const float d = g.dy[(long long)row * CO + n], zz = g.z[(long long)row * CO + n];
+        const float xh = (zz - g.dbn[3 * CO + n]) * g.dbn[4 * CO + n];
+        v = g.dbn[n] * (d - g.dbn[CO + n] - xh * g.dbn[2 * CO + n]);
+      }
+      sD[q] = v;
+    }
+    __syncthreads();
+    if (CI == 4) {   // one 16-B gather per (offset, row)
+      for (int q = tid; q < K * RT; q += BLK) {
+        const int k = q / RT, r = q - k * RT;
+        const int src = sN[r * K + k];
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (src >= 0) {
+          v = *(const float4*)(g.a + (long long)src * 4);
+          if (AT == A_BNRELU) {
+            v.x = fmaxf(fmaf(v.x - g.abn[8], g.abn[0], g.abn[4]), 0.0f);
+            v.y = fmaxf(fmaf(v.y - g.abn[9], g.abn[1], g.abn[5]), 0.0f);
+            v.z = fmaxf(fmaf(v.z - g.abn[10], g.abn[2], g.abn[6]), 0.0f);
+            v.w = fmaxf(fmaf(v.w - g.abn[11], g.abn[3], g.abn[7]), 0.0f);
+          }
+        }
+        *(float4*)&sA[q * 4] = v;
+      }
+    } else {
+      for (int q = tid; q < K * RT * CI; q += BLK) {
+        const int k = q / (RT * CI), rem = q - k * (RT * CI), r = rem / CI, c = rem - r * CI;
+        const int src = sN[r * K + k];
+        float v = 0.0f;
+        if (src >= 0) {
+          const float x = g.a[(long long)src * CI + c];
+          v = AT == A_BNRELU ? fmaxf(fmaf(x - g.abn[2 * CI + c], g.abn[c], g.abn[CI + c]), 0.0f) : x;
+        }
+        sA[q] = v;
+      }
+    }
+    __syncthreads();
+    if (own) {
+      const float* pa = sA + kk * RT * CI + ci;
+#pragma unroll 4
+      for (int r = half; r < RT; r += 2) {
+        const float a = pa[r * CI];
+        const float4* pd = (const float4*)(sD + r * CO);
+#pragma unroll
+        for (int n4 = 0; n4 < CO / 4; ++n4) {
+          const float4 d = pd[n4];
+          acc[4 * n4 + 0] = fmaf(a, d.x, acc[4 * n4 + 0]);
+          acc[4 * n4 + 1] = fmaf(a, d.y, acc[4 * n4 + 1]);
+          acc[4 * n4 + 2] = fmaf(a, d.z, acc[4 * n4 + 2]);
+          acc[4 * n4 + 3] = fmaf(a, d.w, acc[4 * n4 + 3]);
+        }
+      }
+    }
+  }
+  // fixed-order combine of the two row parities
+  __syncthreads();
+  if (half == 1) {
+#pragma unroll
+    for (int n = 0; n < CO; ++n) sH[pair][n] = acc[n];
+  }
+  __syncthreads();
+  if (half == 0 && own) {
+    float* out = g.part + ((long long)blockIdx.x * K + kk) * CI * CO + ci * CO;
+#pragma unroll
+    for (int n = 0; n < CO; ++n) out[n] = acc[n] + sH[pair][n];
+  }
+}
+
 // ------------------------------------------------------------------ dispatch
 template <int CI, int CO>
 static void launch_gemm_t(int at, int et, const GemmArgs& a, int nblk, hipStream_t st) {
@@ -591,6 +689,13 @@ static int launch_gemm(int CI, int CO, int at, int et, const GemmArgs& a, int nb
   C2(32, 16) C2(64, 32) C2(128, 64)
 #undef C2
   return RPC_ERR_UNSUPPORTED;
+}
+
+static bool wgrad_narrow(int CI, int CO, int K) { return (CI == 4 || CI == 5) && CO == 16 && K * CI * 2 <= BLK; }
+
+static int wgrad_narrow_chunks(int n) {   // 256-row chunks: ~1.5 blocks per CU at 100k rows
+  const int c = (n + 255) / 256;
+  return c < 1 ? 1 : (c > 2048 ? 2048 : c);
 }
 
 static int launch_wgrad(int CI, int CO, int at, const WgradArgs& a, dim3 grid, hipStream_t st) {
@@ -756,6 +861,7 @@ extern "C" int rpc_spconv_dgrad(const float* dy_out, const float* z_out, const f
 }
 
 extern "C" size_t rpc_spconv_wgrad_workspace_size(int n_out, int K, int CI, int CO) {
+  if (wgrad_narrow(CI, CO, K)) return (size_t)wgrad_narrow_chunks(n_out) * K * CI * CO * sizeof(float);
   int chunks = cdiv(n_out > 0 ? n_out : 1, 2048);
   if (chunks > 64) chunks = 64;
   return (size_t)chunks * K * CI * CO * sizeof(float);
@@ -770,8 +876,9 @@ extern "C" int rpc_spconv_wgrad(const float* in, const float* in_bn, int CI, con
     RPC_CHECK(hipMemsetAsync(dW, 0, sizeof(float) * (size_t)K * CI * CO, st));
     return RPC_OK;
   }
-  int chunks = cdiv(n_out, 2048);
-  if (chunks > 64) chunks = 64;
+  const bool narrow = wgrad_narrow(CI, CO, K);
+  int chunks = narrow ? wgrad_narrow_chunks(n_out) : cdiv(n_out, 2048);
+  if (!narrow && chunks > 64) chunks = 64;
   if (ws_bytes < (size_t)chunks * K * CI * CO * sizeof(float)) return RPC_ERR_WORKSPACE;
   WgradArgs a;
   a.a = in;
@@ -784,7 +891,19 @@ extern "C" int rpc_spconv_wgrad(const float* in, const float* in_bn, int CI, con
   a.z = z_out;
   a.dbn = bnb;
   a.part = (float*)ws;
-  int rc = launch_wgrad(CI, CO, in_bn ? A_BNRELU : A_RAW, a, dim3(chunks, K), st);
+  int rc = RPC_OK;
+  if (narrow) {
+    a.rows_per = ((cdiv(n_out, chunks) + 63) / 64) * 64;
+#define NW(ci)                                                                                              \
+    if (CI == ci) {                                                                                         \
+      if (in_bn) hipLaunchKernelGGL((k_wgrad_narrow<ci, 16, A_BNRELU>), dim3(chunks), dim3(BLK), 0, st, a); \
+      else hipLaunchKernelGGL((k_wgrad_narrow<ci, 16, A_RAW>), dim3(chunks), dim3(BLK), 0, st, a);          \
+    }
+    NW(4) NW(5)
+#undef NW
+  } else {
+    rc = launch_wgrad(CI, CO, in_bn ? A_BNRELU : A_RAW, a, dim3(chunks, K), st);
+  }
   if (rc) return rc;
   long long total = (long long)K * CI * CO;
   slab_reduce((const float*)ws, chunks, total, dW, st);

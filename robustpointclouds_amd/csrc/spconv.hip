@@ -61,9 +61,10 @@ __global__ void k_grid_set(const int* __restrict__ coors, int N, Shape s, int* _
 
 __global__ void k_subm_nbr(const int* __restrict__ coors, int N, Shape s, KGeom g,
                            const int* __restrict__ grid, int* __restrict__ nbr) {
-  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (t >= (long long)N * g.K) return;
-  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  // 32-bit (row, offset) index: N * K < 2^31 is checked on the host
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * g.K) return;
+  const int r = t / g.K, k = t - r * g.K;
   int kx = k % g.k[2], ky = (k / g.k[2]) % g.k[1], kz = k / (g.k[2] * g.k[1]);
   const int* c = coors + 4 * r;
   int z = c[1] + kz - g.k[0] / 2, y = c[2] + ky - g.k[1] / 2, x = c[3] + kx - g.k[2] / 2;
@@ -92,9 +93,10 @@ __device__ __forceinline__ bool out_of(const int* c, int k, const KGeom& g, cons
 
 __global__ void k_cand_min(const int* __restrict__ coors, int N, KGeom g, Shape so,
                            unsigned* __restrict__ grid) {
-  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (t >= (long long)N * g.K) return;
-  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  // 32-bit (row, offset) index: N * K < 2^31 is checked on the host
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * g.K) return;
+  const int r = t / g.K, k = t - r * g.K;
   const int* c = coors + 4 * r;
   int oz, oy, ox;
   if (!out_of(c, k, g, so, oz, oy, ox)) return;
@@ -103,11 +105,11 @@ __global__ void k_cand_min(const int* __restrict__ coors, int N, KGeom g, Shape 
 
 __global__ void k_cand_head(const int* __restrict__ coors, int N, KGeom g, Shape so,
                             const unsigned* __restrict__ grid, int* __restrict__ flag) {
-  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  long long n = (long long)N * g.K;
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  const int n = N * g.K;
   if (t == 0) flag[n] = 0;
   if (t >= n) return;
-  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  const int r = t / g.K, k = t - r * g.K;
   const int* c = coors + 4 * r;
   int oz, oy, ox, f = 0;
   if (out_of(c, k, g, so, oz, oy, ox)) f = grid[cell(so, c[0], oz, oy, ox)] == (unsigned)t;
@@ -117,9 +119,9 @@ __global__ void k_cand_head(const int* __restrict__ coors, int N, KGeom g, Shape
 __global__ void k_out_assign(const int* __restrict__ coors, int N, KGeom g, Shape so,
                              const int* __restrict__ flag, const int* __restrict__ pos,
                              int* __restrict__ grid, int* __restrict__ coors_out) {
-  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (t >= (long long)N * g.K || !flag[t]) return;
-  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * g.K || !flag[t]) return;
+  const int r = t / g.K, k = t - r * g.K;
   const int* c = coors + 4 * r;
   int oz, oy, ox;
   out_of(c, k, g, so, oz, oy, ox);
@@ -135,9 +137,10 @@ __global__ void k_out_assign(const int* __restrict__ coors, int N, KGeom g, Shap
 __global__ void k_nbr_fill(const int* __restrict__ coors, int N, KGeom g, Shape so,
                            const int* __restrict__ grid, int* __restrict__ nbr_out,
                            int* __restrict__ nbr_in) {
-  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (t >= (long long)N * g.K) return;
-  int r = (int)(t / g.K), k = (int)(t - (long long)r * g.K);
+  // 32-bit (row, offset) index: N * K < 2^31 is checked on the host
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * g.K) return;
+  const int r = t / g.K, k = t - r * g.K;
   const int* c = coors + 4 * r;
   int oz, oy, ox, o = -1;
   if (out_of(c, k, g, so, oz, oy, ox)) {
@@ -739,6 +742,7 @@ extern "C" int rpc_subm_rulebook(const int* coors, int N, const int* shape /* ho
   Shape s{shape[0], shape[1], shape[2], shape[3]};
   KGeom g = geom(ksize, nullptr, nullptr);
   if (g.K > MAXK) return RPC_ERR_UNSUPPORTED;
+  if ((long long)N * g.K >= (1LL << 31) - BLK) return RPC_ERR_ARG;   // 32-bit (row, offset) index
   hipLaunchKernelGGL(k_grid_set, dim3(cdiv(N, BLK)), dim3(BLK), 0, st, coors, N, s, grid, 0);
   hipLaunchKernelGGL(k_subm_nbr, dim3(cdiv((long long)N * g.K, BLK)), dim3(BLK), 0, st, coors, N, s, g,
                      grid, nbr);
@@ -763,6 +767,7 @@ extern "C" int rpc_spconv_rulebook_count(const int* coors, int N, const int* out
   Shape so{out_shape[0], out_shape[1], out_shape[2], out_shape[3]};
   KGeom g = geom(ksize, stride, pad);
   if (g.K > MAXK) return RPC_ERR_UNSUPPORTED;
+  if ((long long)N * g.K >= (1LL << 31) - BLK) return RPC_ERR_ARG;   // 32-bit (row, offset) index
   size_t n = (size_t)N * g.K + 1;
   if (ws_bytes < rpc_spconv_rulebook_workspace_size(N, g.K)) return RPC_ERR_WORKSPACE;
   int* flag = (int*)ws;
@@ -786,6 +791,7 @@ extern "C" int rpc_spconv_rulebook_build(const int* coors, int N, const int* out
   hipStream_t st = (hipStream_t)stream;
   Shape so{out_shape[0], out_shape[1], out_shape[2], out_shape[3]};
   KGeom g = geom(ksize, stride, pad);
+  if (g.K > MAXK || (long long)N * g.K >= (1LL << 31) - BLK) return RPC_ERR_ARG;
   size_t n = (size_t)N * g.K + 1;
   int* flag = (int*)ws;
   int* pos = (int*)((char*)ws + al(n * sizeof(int)));

@@ -60,7 +60,9 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT)) void k_gemm_bf16(GB g) {
   constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, GBM = 16 * GW;
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;
-  constexpr int LS = KGP + 16;                // LDS row stride: 8 mod 16 dwords, conflict-free b128 reads
+  // LDS row stride: 8 mod 16 dwords (conflict-free b128 reads), except the 128 x 128 tiles, whose
+  // smaller 16-B pad keeps two blocks per CU (a 144-element pitch leaves one: 1.7x slower)
+  constexpr int LS = (KGP >= 128 && NT >= 8) ? KGP + 8 : KGP + 16;
   constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
   constexpr int BPT = (BV + GBLK - 1) / GBLK;
   __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];

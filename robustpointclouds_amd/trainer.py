@@ -86,9 +86,12 @@ class Trainer:
                 else:
                     mod.to(memory_format=torch.channels_last)
         if ddp and dist.is_initialized() and dist.get_world_size() > 1:
+            # 6 MB buckets: the 16 MB of SECOND gradients (ready together when its one-node backward
+            # ends) go out in three RCCL all-reduces that overlap the sparse-encoder and perturber
+            # backward; with one 25 MB bucket the reduction waited for the end of backward
             self.model = torch.nn.parallel.DistributedDataParallel(
                 model, device_ids=[self.device.index] if self.device.type == "cuda" else None,
-                bucket_cap_mb=25, find_unused_parameters=False, broadcast_buffers=False, gradient_as_bucket_view=True)
+                bucket_cap_mb=6, find_unused_parameters=False, broadcast_buffers=False, gradient_as_bucket_view=True)
         if self.device.type == "cuda":
             # clip_grad_norm_ + AdamW as two HIP kernels over a device tensor table (optim.py)
             self.opt = ClipAdamW(param_groups(self.module, lr), lr=lr, betas=betas, eps=eps,

@@ -166,8 +166,8 @@ int rpc_spconv_wgrad(const float* in, const float* in_bn, int ci, const int* nbr
                      void* workspace, size_t workspace_bytes, void* stream);
 /* BatchNorm1d finalize from partial sums. mode 0: bn_out = scale, shift, mean, invstd and the
  * running stats update (train). mode 1: bn_out = gi, m1, m2, mean, invstd for the backward and
- * dgamma = sum dy*xhat, dbeta = sum dy. Armed workspace (the ticket is at offset 0, so one
- * workspace sized for the widest c serves every c). */
+ * dgamma = sum dy*xhat, dbeta = sum dy. One block per channel, no cross-block step: the
+ * workspace is unused (size 0; may be NULL) and kept for signature stability. */
 size_t rpc_bn_finalize_workspace_size(int c);
 int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean, float* running_var,

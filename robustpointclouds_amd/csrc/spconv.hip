@@ -387,9 +387,10 @@ __global__ __launch_bounds__(BLK) void k_wgrad(WgradArgs g) {
 
 
 // ------------------------------------------------------------------ BatchNorm finalize
-// One block per column j < 2C: every thread sums its strided share of the nblk partial rows with
-// four loads in flight (one latency round for nblk <= 1024), then a fixed-order LDS tree; the
-// last-arriving block finalizes:
+// One block per channel c: every thread sums its strided share of the nblk partial rows of both
+// columns c (sum) and C + c (sum of squares / of dy*xhat) with four rows in flight, then a
+// fixed-order reduction (wave shuffles, then the four waves in order) in double; thread 0 writes
+// the channel's parameters. No cross-block step (no ticket, no workspace):
 // mode 0 (forward): bn = scale (= gamma*invstd), beta, mean, invstd ; running stats updated.
 // mode 1 (backward): bnb = gi, m1, m2, mean, invstd ; dgamma, dbeta written.
 __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ part, int nblk, int C, int N,
@@ -397,57 +398,65 @@ __global__ __launch_bounds__(BLK) void k_bn_finalize(const float* __restrict__ p
                                                      const float* __restrict__ beta, float eps,
                                                      float mom, float* __restrict__ rmean,
                                                      float* __restrict__ rvar, const float* __restrict__ fbn,
-                                                     float* __restrict__ bn, double* __restrict__ tot,
-                                                     unsigned* __restrict__ ticket, float* __restrict__ dgamma,
+                                                     float* __restrict__ bn, float* __restrict__ dgamma,
                                                      float* __restrict__ dbeta) {
-  __shared__ double sh[BLK];
-  __shared__ int lastf;
-  const int j = blockIdx.x;
+  __shared__ double sh[2][BLK / 64];
+  const int c = blockIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const long long C2 = 2 * C;
-  double s = 0.0;
+  double s1 = 0.0, s2 = 0.0;
   int r = threadIdx.x;
   for (; r + 3 * BLK < nblk; r += 4 * BLK) {
-    const float a0 = part[r * C2 + j], a1 = part[(r + BLK) * C2 + j];
-    const float a2 = part[(r + 2 * BLK) * C2 + j], a3 = part[(r + 3 * BLK) * C2 + j];
-    s += (double)a0;
-    s += (double)a1;
-    s += (double)a2;
-    s += (double)a3;
+    const float* p = part + r * C2 + c;
+    const float a0 = p[0], b0 = p[C], a1 = p[BLK * C2], b1 = p[BLK * C2 + C];
+    const float a2 = p[2 * BLK * C2], b2 = p[2 * BLK * C2 + C], a3 = p[3 * BLK * C2], b3 = p[3 * BLK * C2 + C];
+    s1 += (double)a0;
+    s1 += (double)a1;
+    s1 += (double)a2;
+    s1 += (double)a3;
+    s2 += (double)b0;
+    s2 += (double)b1;
+    s2 += (double)b2;
+    s2 += (double)b3;
   }
-  for (; r < nblk; r += BLK) s += (double)part[r * C2 + j];
-  sh[threadIdx.x] = s;
+  for (; r < nblk; r += BLK) {
+    s1 += (double)part[r * C2 + c];
+    s2 += (double)part[r * C2 + C + c];
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    s1 += __shfl_xor(s1, o, 64);
+    s2 += __shfl_xor(s2, o, 64);
+  }
+  if (lane == 0) {
+    sh[0][w] = s1;
+    sh[1][w] = s2;
+  }
   __syncthreads();
-  for (int o = BLK / 2; o > 0; o >>= 1) {
-    if (threadIdx.x < o) sh[threadIdx.x] += sh[threadIdx.x + o];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) tot[j] = sh[0];
-  if (!last_block_arrive(ticket, &lastf)) return;
-  for (int c = threadIdx.x; c < C; c += BLK) {
-    const double s1 = tot[c], s2 = tot[C + c];
-    if (mode == 0) {
-      double mean = s1 / N;
-      double var = s2 / N - mean * mean;
-      if (var < 0) var = 0;
-      float invstd = 1.0f / sqrtf((float)var + eps);
-      // BN applied as (z - mean) * scale + beta: no cancellation between z*scale and a shift
-      bn[c] = gamma[c] * invstd;
-      bn[C + c] = beta[c];
-      bn[2 * C + c] = (float)mean;
-      bn[3 * C + c] = invstd;
-      double uvar = N > 1 ? var * N / (N - 1) : var;
-      rmean[c] = (1.0f - mom) * rmean[c] + mom * (float)mean;
-      rvar[c] = (1.0f - mom) * rvar[c] + mom * (float)uvar;
-    } else {
-      // fbn: forward scale, beta, mean, invstd of this layer
-      bn[c] = gamma[c] * fbn[3 * C + c];
-      bn[C + c] = (float)(s1 / N);
-      bn[2 * C + c] = (float)(s2 / N);
-      bn[3 * C + c] = fbn[2 * C + c];
-      bn[4 * C + c] = fbn[3 * C + c];
-      if (dgamma) dgamma[c] = (float)s2;
-      if (dbeta) dbeta[c] = (float)s1;
-    }
+  if (threadIdx.x != 0) return;
+  s1 = ((sh[0][0] + sh[0][1]) + sh[0][2]) + sh[0][3];
+  s2 = ((sh[1][0] + sh[1][1]) + sh[1][2]) + sh[1][3];
+  if (mode == 0) {
+    const double mean = s1 / N;
+    double var = s2 / N - mean * mean;
+    if (var < 0) var = 0;
+    const float invstd = 1.0f / sqrtf((float)var + eps);
+    // BN applied as (z - mean) * scale + beta: no cancellation between z*scale and a shift
+    bn[c] = gamma[c] * invstd;
+    bn[C + c] = beta[c];
+    bn[2 * C + c] = (float)mean;
+    bn[3 * C + c] = invstd;
+    const double uvar = N > 1 ? var * N / (N - 1) : var;
+    rmean[c] = (1.0f - mom) * rmean[c] + mom * (float)mean;
+    rvar[c] = (1.0f - mom) * rvar[c] + mom * (float)uvar;
+  } else {
+    // fbn: forward scale, beta, mean, invstd of this layer
+    bn[c] = gamma[c] * fbn[3 * C + c];
+    bn[C + c] = (float)(s1 / N);
+    bn[2 * C + c] = (float)(s2 / N);
+    bn[3 * C + c] = fbn[2 * C + c];
+    bn[4 * C + c] = fbn[3 * C + c];
+    if (dgamma) dgamma[c] = (float)s2;
+    if (dbeta) dbeta[c] = (float)s1;
   }
 }
 
@@ -917,21 +926,16 @@ extern "C" int rpc_spconv_wgrad(const float* in, const float* in_bn, int CI, con
   return RPC_OK;
 }
 
-extern "C" size_t rpc_bn_finalize_workspace_size(int C) { return al(sizeof(double) * 2 * C) + 256; }
+extern "C" size_t rpc_bn_finalize_workspace_size(int C) { return 0; }
 
 extern "C" int rpc_bn_finalize(const float* part, int nblk, int C, int N, int mode, const float* gamma,
                                const float* beta, float eps, float momentum, float* running_mean,
                                float* running_var, const float* fwd_bn, float* bn_out, float* dgamma, float* dbeta,
                                void* ws, void* stream) {
-  if (C < 1 || nblk < 1 || !part || !bn_out || !ws) return RPC_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  // armed workspace: the ticket is zero on entry (zero-filled once by the owner) and re-armed by
-  // the kernel's last block, so there is no per-call memset
-  // the ticket sits at offset 0 so that one armed workspace serves every width c
-  unsigned* ticket = (unsigned*)ws;
-  double* tot = (double*)((char*)ws + 256);
-  hipLaunchKernelGGL(k_bn_finalize, dim3(2 * C), dim3(BLK), 0, st, part, nblk, C, N, mode, gamma, beta, eps,
-                     momentum, running_mean, running_var, fwd_bn, bn_out, tot, ticket, dgamma, dbeta);
+  (void)ws;   // single pass since r01 v11: no workspace (kept in the signature; may be NULL)
+  if (C < 1 || nblk < 1 || !part || !bn_out) return RPC_ERR_ARG;
+  hipLaunchKernelGGL(k_bn_finalize, dim3(C), dim3(BLK), 0, (hipStream_t)stream, part, nblk, C, N, mode, gamma, beta,
+                     eps, momentum, running_mean, running_var, fwd_bn, bn_out, dgamma, dbeta);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

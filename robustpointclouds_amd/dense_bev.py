@@ -136,11 +136,10 @@ def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
     bnm = L.bnm
     if training:
         bn = torch.empty(4 * L.co, dtype=torch.float32, device=dev)
-        wsb = _ffi.armed_workspace("bn_finalize", lib.rpc_bn_finalize_workspace_size(L.co), dev)
         _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), part.shape[0], L.co, Mo, 0, _ffi.ptr(bnm.weight),
                                        _ffi.ptr(bnm.bias), float(bnm.eps), float(bnm.momentum),
                                        _ffi.ptr(bnm.running_mean), _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn),
-                                       None, None, _ffi.ptr(wsb), st), "rpc_bn_finalize")
+                                       None, None, None, st), "rpc_bn_finalize")
     else:
         bn = _bn_eval(bnm, dev)
     if out is None:
@@ -165,10 +164,9 @@ def _backward_layer(lib, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
     bnb = torch.empty(5 * co, dtype=torch.float32, device=dev)
     dgamma = torch.empty(co, dtype=torch.float32, device=dev)
     dbeta = torch.empty(co, dtype=torch.float32, device=dev)
-    wsb = _ffi.armed_workspace("bn_finalize", lib.rpc_bn_finalize_workspace_size(co), dev)
     _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nb, co, Mo, 1, _ffi.ptr(L.bnm.weight), _ffi.ptr(L.bnm.bias),
                                    0.0, 0.0, None, None, _ffi.ptr(rec["bn"]), _ffi.ptr(bnb), _ffi.ptr(dgamma),
-                                   _ffi.ptr(dbeta), _ffi.ptr(wsb), st), "rpc_bn_finalize(bwd)")
+                                   _ffi.ptr(dbeta), None, st), "rpc_bn_finalize(bwd)")
     dz = torch.empty((Mo, co), dtype=torch.bfloat16, device=dev)
     _ffi.check(lib.rpc_dense_bnbwd_apply(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
                                          _ffi.ptr(rec["bn"]), _ffi.ptr(bnb), _ffi.ptr(dz), st),

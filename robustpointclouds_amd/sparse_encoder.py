@@ -332,11 +332,10 @@ class SparseEncoderFn(torch.autograd.Function):
                       f"rpc::sp::k_gemm<{sp.ci}, {sp.co}, {1 if li else 0}, 0>")
                 enc.timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
             bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
-            wsb = _ffi.armed_workspace("bn_finalize", lib.rpc_bn_finalize_workspace_size(sp.co), dev)
             _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
                                            float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
                                            _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
-                                           _ffi.ptr(wsb), st), "rpc_bn_finalize")
+                                           None, st), "rpc_bn_finalize")
             rec.update(z=z, bn=bn, W=W, gamma=gamma, beta=beta)
             L.append(rec)
             if sp.mat:
@@ -427,10 +426,9 @@ class SparseEncoderFn(torch.autograd.Function):
             bnb = torch.empty(5 * sp.co, dtype=torch.float32, device=dev)
             dgamma = torch.empty_like(rec["gamma"])
             dbeta = torch.empty_like(rec["beta"])
-            wsb = _ffi.armed_workspace("bn_finalize", lib.rpc_bn_finalize_workspace_size(sp.co), dev)
             _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 1, _ffi.ptr(rec["gamma"]),
                                            _ffi.ptr(rec["beta"]), 0.0, 0.0, None, None, _ffi.ptr(rec["bn"]),
-                                           _ffi.ptr(bnb), _ffi.ptr(dgamma), _ffi.ptr(dbeta), _ffi.ptr(wsb), st),
+                                           _ffi.ptr(bnb), _ffi.ptr(dgamma), _ffi.ptr(dbeta), None, st),
                        "rpc_bn_finalize(bwd)")
             # weight gradient
             dW = torch.empty_like(rec["W"])

@@ -830,16 +830,35 @@ __global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int 
   }
 }
 
-// G[t][ci][co] fp32 -> torch layout (kind 0: [co][ci][t], kind 1: [ci][co][t])
-__global__ __launch_bounds__(BLK) void k_wgrad_store(const float* __restrict__ G, int kind, int CI, int CO, int T,
-                                                     float* __restrict__ dW) {
-  const long long n = (long long)T * CI * CO;
-  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (e >= n) return;
+// k_slab_reduce (common.h: same fixed summation order) fused with the store to torch layout
+// (kind 0: [co][ci][t], kind 1: [ci][co][t]): the reduced [T][CI][CO] element goes straight to dW
+__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int chunks, int kind, int CI,
+                                                      int CO, int T, float* __restrict__ dW) {
+  __shared__ double sh[4][64];
+  const long long total = (long long)T * CI * CO;
+  const int o = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const long long e = (long long)blockIdx.x * 64 + o;
+  double s = 0.0;
+  if (e < total) {
+    int c = q;
+    for (; c + 12 < chunks; c += 16) {
+      float a0 = part[(long long)c * total + e], a1 = part[(long long)(c + 4) * total + e];
+      float a2 = part[(long long)(c + 8) * total + e], a3 = part[(long long)(c + 12) * total + e];
+      s += (double)a0;
+      s += (double)a1;
+      s += (double)a2;
+      s += (double)a3;
+    }
+    for (; c < chunks; c += 4) s += (double)part[(long long)c * total + e];
+  }
+  sh[q][o] = s;
+  __syncthreads();
+  if (q != 0 || e >= total) return;
+  const float v = (float)(((sh[0][o] + sh[1][o]) + sh[2][o]) + sh[3][o]);
   const int t = (int)(e / ((long long)CI * CO));
   const int rem = (int)(e - (long long)t * CI * CO), ci = rem / CO, co = rem - ci * CO;
-  if (kind == 0) dW[((size_t)co * CI + ci) * T + t] = G[e];
-  else dW[((size_t)ci * CO + co) * T + t] = G[e];
+  if (kind == 0) dW[((size_t)co * CI + ci) * T + t] = v;
+  else dW[((size_t)ci * CO + co) * T + t] = v;
 }
 
 static inline unsigned cdivu(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
@@ -954,7 +973,7 @@ extern "C" int rpc_dense_conv_blocks(int map, const int* r_img) {
 extern "C" size_t rpc_dense_wgrad_workspace_size(int map, const int* r_img, int ci, int co) {
   const int M = r_img[0] * r_img[1] * r_img[2];
   const int T = map_wtaps(map);
-  return (size_t)wgrad_chunks(M, T, ci, co) * T * ci * co * sizeof(float) + (size_t)T * ci * co * sizeof(float);
+  return (size_t)wgrad_chunks(M, T, ci, co) * T * ci * co * sizeof(float);
 }
 
 extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci, const void* dz, int dp, int co,
@@ -966,10 +985,9 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
   const int M = R.B * R.H * R.W, T = map_wtaps(map);
   const int chunks = wgrad_chunks(M, T, ci, co);
   const size_t slab = (size_t)T * ci * co;
-  if (ws_bytes < (chunks + 1) * slab * sizeof(float)) return RPC_ERR_WORKSPACE;
+  if (ws_bytes < chunks * slab * sizeof(float)) return RPC_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   float* part = (float*)ws;
-  float* G = part + chunks * slab;
   if (M == 0) {
     RPC_CHECK(hipMemsetAsync(dW, 0, slab * sizeof(float), st));
     return RPC_OK;
@@ -983,9 +1001,8 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
     default: launch_wgrad<M_U2>(g, chunks, st); break;
   }
   RPC_LAUNCH_CHECK();
-  slab_reduce(part, chunks, (long long)slab, G, st);
-  RPC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_wgrad_store, dim3(cdivu(slab, BLK)), dim3(BLK), 0, st, (const float*)G, kind, ci, co, T, dW);
+  hipLaunchKernelGGL(k_wgrad_reduce, dim3(cdivu(slab, 64)), dim3(256), 0, st, (const float*)part, chunks, kind, ci, co,
+                     T, dW);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -202,6 +202,13 @@ int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const float* bnb, in
 /* W [K][ci][co] fp32 -> per-offset B^T tiles bf16 (forward: [K][co][ci]; dgrad: [K][ci][co]), zero padded */
 size_t rpc_spconv_bf16_weight_elems(int kvol, int ci, int co, int dgrad);
 int rpc_spconv_prep_weight_bf16(const float* W, int kvol, int ci, int co, int dgrad, void* bt, void* stream);
+/* up to 32 rpc_spconv_prep_weight_bf16 calls (forward and data-gradient tiles of every layer) in one launch */
+typedef struct {
+  const float* W;
+  void* bt;
+  int kvol, ci, co, dgrad;
+} RpcSpconvWprep;
+int rpc_spconv_prep_weight_bf16_batch(const RpcSpconvWprep* descs, int n, void* stream);
 /* out[r] = sum_k a[map[r, k']] . B_k ; epi 0 forward (+BN partial sums), 1 dgrad (prev ReLU mask +
  * BN-backward partial sums), 2 plain */
 int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out, const void* bt,
@@ -249,6 +256,14 @@ int rpc_dense_bnbwd_apply(const void* dh, int dh_pitch, int dh_offset, const voi
 /* torch fp32 weights -> bf16 GEMM operands: fwd [taps][co][ci] and/or dgrad [taps][ci][co] (flip: taps reversed) */
 int rpc_dense_wprep(const float* W, int kind, int ci, int co, int taps, int flip, void* w_fwd, void* w_dgrad,
                     void* stream);
+/* up to 16 rpc_dense_wprep calls (every layer of a module) in one launch */
+typedef struct {
+  const float* W;
+  void* w_fwd;
+  void* w_dgrad;
+  int kind, ci, co, taps, flip;
+} RpcDenseWprep;
+int rpc_dense_wprep_batch(const RpcDenseWprep* descs, int n, void* stream);
 
 
 /* ------------------------------------------------------------------ a8 / §8(f1) Anchor3DHead targets + losses

@@ -62,6 +62,18 @@ class RpcAugFrame(C.Structure):
                 ("sinr", C.c_float), ("scale", C.c_float), ("tx", C.c_float), ("ty", C.c_float), ("tz", C.c_float)]
 
 
+class RpcDenseWprep(C.Structure):
+    """include/rpc_hip.h RpcDenseWprep."""
+    _fields_ = [("W", C.c_void_p), ("w_fwd", C.c_void_p), ("w_dgrad", C.c_void_p), ("kind", C.c_int),
+                ("ci", C.c_int), ("co", C.c_int), ("taps", C.c_int), ("flip", C.c_int)]
+
+
+class RpcSpconvWprep(C.Structure):
+    """include/rpc_hip.h RpcSpconvWprep."""
+    _fields_ = [("W", C.c_void_p), ("bt", C.c_void_p), ("kvol", C.c_int), ("ci", C.c_int), ("co", C.c_int),
+                ("dgrad", C.c_int)]
+
+
 class RpcCenterCfg(C.Structure):
     """include/rpc_hip.h RpcCenterCfg."""
     _fields_ = [("B", C.c_int), ("H", C.c_int), ("W", C.c_int), ("ntasks", C.c_int), ("ncls_total", C.c_int),
@@ -102,6 +114,7 @@ SIGNATURES = {
     "rpc_bnbwd_to_bf16_rows": (i32, [vp, vp, vp, i32, i32, vp, vp]),
     "rpc_spconv_bf16_weight_elems": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_prep_weight_bf16": (i32, [vp, i32, i32, i32, i32, vp, vp]),
+    "rpc_spconv_prep_weight_bf16_batch": (i32, [vp, i32, vp]),
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_wgrad_bf16": (i32, [vp, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
@@ -114,6 +127,7 @@ SIGNATURES = {
     "rpc_dense_bnbwd_stats": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp]),
     "rpc_dense_bnbwd_apply": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
     "rpc_dense_wprep": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
+    "rpc_dense_wprep_batch": (i32, [vp, i32, vp]),
     "rpc_loss_tail_forward": (i32, [vp, vp, C.c_float, vp, vp]),
     "rpc_loss_tail_backward": (i32, [vp, C.c_float, vp, vp, vp, vp]),
     "rpc_clip_adamw_workspace_size": (sz, [i32]),

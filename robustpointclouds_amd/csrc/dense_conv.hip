@@ -25,8 +25,10 @@
 // fp32 slabs reduced in a fixed order (k_slab_reduce). BatchNorm apply / backward are
 // vectorised elementwise passes (8 channels per thread).
 #include <hip/hip_runtime.h>
+#include <string.h>
 
 #include "common.h"
+#include "rpc_hip.h"
 
 namespace rpc {
 namespace dn {
@@ -815,11 +817,8 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_apply(const u16* __restrict__ dh,
 // torch layouts -> bf16 GEMM operands. kind: 0 Conv2d 3x3 [co][ci][3][3]; 1 ConvTranspose2d
 // [ci][co][k][k] (k = 1 or 2). fwd: [T][co][ci]; dgrad: [T][ci][co] with, for a stride-1 3x3
 // conv, the taps flipped (S1 data gradient), otherwise the same tap order (D2 / P1 / G2).
-__global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int kind, int CI, int CO, int T,
-                                               int flip, u16* __restrict__ wf, u16* __restrict__ wd) {
-  const long long n = (long long)T * CI * CO;
-  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (e >= n) return;
+__device__ __forceinline__ void wprep_elem(long long e, const float* __restrict__ W, int kind, int CI, int CO, int T,
+                                           int flip, u16* __restrict__ wf, u16* __restrict__ wd) {
   const int t = (int)(e / ((long long)CI * CO));
   const int rem = (int)(e - (long long)t * CI * CO), ci = rem / CO, co = rem - ci * CO;
   const float v = kind == 0 ? W[((size_t)co * CI + ci) * T + t] : W[((size_t)ci * CO + co) * T + t];
@@ -828,6 +827,24 @@ __global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int 
     const int td = flip ? T - 1 - t : t;
     wd[((size_t)td * CI + ci) * CO + co] = f2bf(v);
   }
+}
+
+__global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int kind, int CI, int CO, int T,
+                                               int flip, u16* __restrict__ wf, u16* __restrict__ wd) {
+  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e < (long long)T * CI * CO) wprep_elem(e, W, kind, CI, CO, T, flip, wf, wd);
+}
+
+// every layer of a module in one launch: blockIdx.y = layer
+constexpr int WPREP_MAX = 16;
+struct WprepBatch {
+  RpcDenseWprep d[WPREP_MAX];
+};
+__global__ __launch_bounds__(BLK) void k_wprep_batch(WprepBatch b) {
+  const RpcDenseWprep& d = b.d[blockIdx.y];
+  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e < (long long)d.taps * d.ci * d.co)
+    wprep_elem(e, d.W, d.kind, d.ci, d.co, d.taps, d.flip, (u16*)d.w_fwd, (u16*)d.w_dgrad);
 }
 
 // k_slab_reduce (common.h: same fixed summation order) fused with the store to torch layout
@@ -1038,6 +1055,24 @@ extern "C" int rpc_dense_bnbwd_apply(const void* dh, int dp, int doff, const voi
   if (m == 0) return RPC_OK;
   hipLaunchKernelGGL(k_bnbwd_apply, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
                      (const u16*)dh, dp, doff, (const u16*)z, m, c, bn, bnb, (u16*)dz);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dense_wprep_batch(const RpcDenseWprep* descs, int n, void* stream) {
+  if (n < 0 || n > WPREP_MAX || (n > 0 && !descs)) return RPC_ERR_ARG;
+  if (n == 0) return RPC_OK;
+  WprepBatch b;
+  memset(&b, 0, sizeof(b));
+  long long most = 0;
+  for (int i = 0; i < n; ++i) {
+    const RpcDenseWprep& d = descs[i];
+    if (!d.W || d.ci < 1 || d.co < 1 || d.taps < 1 || (d.kind != 0 && d.kind != 1)) return RPC_ERR_ARG;
+    b.d[i] = d;
+    const long long e = (long long)d.taps * d.ci * d.co;
+    most = e > most ? e : most;
+  }
+  hipLaunchKernelGGL(k_wprep_batch, dim3(cdivu(most, BLK), n), dim3(BLK), 0, (hipStream_t)stream, b);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

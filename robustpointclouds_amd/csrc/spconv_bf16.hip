@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include "common.h"
+#include "rpc_hip.h"
 
 namespace rpc {
 namespace spb {
@@ -258,10 +259,8 @@ __global__ __launch_bounds__(BLK) void k_dz_bf16(const float* __restrict__ dy, c
 }
 
 // W fp32 [K][CI][CO] -> B^T bf16 [K][NGP][KGP]; fwd: n = co, kk = ci ; dgrad: n = ci, kk = co
-__global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int K, int CI, int CO, int dgrad,
-                                               int NGP, int KGP, u16* __restrict__ bt) {
-  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (t >= (long long)K * NGP * KGP) return;
+__device__ __forceinline__ void wprep_elem(long long t, const float* __restrict__ W, int CI, int CO, int dgrad,
+                                           int NGP, int KGP, u16* __restrict__ bt) {
   int kk = (int)(t % KGP);
   long long q = t / KGP;
   int n = (int)(q % NGP), k = (int)(q / NGP);
@@ -269,6 +268,25 @@ __global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int 
   if (!dgrad) { if (n < CO && kk < CI) v = W[((long long)k * CI + kk) * CO + n]; }
   else { if (n < CI && kk < CO) v = W[((long long)k * CI + n) * CO + kk]; }
   bt[t] = to_bf16(v);
+}
+
+__global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int K, int CI, int CO, int dgrad,
+                                               int NGP, int KGP, u16* __restrict__ bt) {
+  long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t < (long long)K * NGP * KGP) wprep_elem(t, W, CI, CO, dgrad, NGP, KGP, bt);
+}
+
+// every layer (forward and data-gradient tiles) of an encoder in one launch: blockIdx.y = entry
+constexpr int SWPREP_MAX = 32;
+struct SWprepBatch {
+  RpcSpconvWprep d[SWPREP_MAX];
+};
+__global__ __launch_bounds__(BLK) void k_wprep_batch(SWprepBatch b) {
+  const RpcSpconvWprep& d = b.d[blockIdx.y];
+  const int ng = d.dgrad ? d.ci : d.co, kg = d.dgrad ? d.co : d.ci;
+  const int NGP = (ng + 15) / 16 * 16, KGP = (kg + 31) / 32 * 32;
+  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t < (long long)d.kvol * NGP * KGP) wprep_elem(t, d.W, d.ci, d.co, d.dgrad, NGP, KGP, (u16*)d.bt);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -476,6 +494,24 @@ extern "C" int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const flo
 extern "C" size_t rpc_spconv_bf16_weight_elems(int kvol, int ci, int co, int dgrad) {
   int ng = dgrad ? ci : co, kg = dgrad ? co : ci;
   return (size_t)kvol * r16(ng) * r32(kg);
+}
+
+extern "C" int rpc_spconv_prep_weight_bf16_batch(const RpcSpconvWprep* descs, int n, void* stream) {
+  if (n < 0 || n > SWPREP_MAX || (n > 0 && !descs)) return RPC_ERR_ARG;
+  if (n == 0) return RPC_OK;
+  SWprepBatch b;
+  memset(&b, 0, sizeof(b));
+  long long most = 0;
+  for (int i = 0; i < n; ++i) {
+    const RpcSpconvWprep& d = descs[i];
+    if (!d.W || !d.bt || d.kvol < 1 || d.kvol > MAXK || d.ci < 1 || d.co < 1) return RPC_ERR_ARG;
+    b.d[i] = d;
+    const long long e = (long long)rpc_spconv_bf16_weight_elems(d.kvol, d.ci, d.co, d.dgrad);
+    most = e > most ? e : most;
+  }
+  hipLaunchKernelGGL(k_wprep_batch, dim3(cdiv(most, BLK), n), dim3(BLK), 0, (hipStream_t)stream, b);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
 }
 
 extern "C" int rpc_spconv_prep_weight_bf16(const float* W, int kvol, int ci, int co, int dgrad, void* bt,

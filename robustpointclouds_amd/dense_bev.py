@@ -116,14 +116,33 @@ class _Layer:
         return {S1: S1, S2: D2, P1: P1, U2: G2}[self.map]
 
 
-def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_pitch=None, out_off=0):
-    """z = conv(h); BN (batch or running stats); y = relu(bn(z)) -> (y image, record)."""
+def _prep_weights(lib, layers, dev, st):
+    """bf16 GEMM operands (forward [T][co][ci], data gradient [T][ci][co]) of every layer of a module
+    from the fp32 master weights, in one rpc_dense_wprep_batch launch."""
+    out = []
+    for g0 in range(0, len(layers), 16):   # the kernel takes up to 16 layers per launch
+        group = layers[g0:g0 + 16]
+        descs = (_ffi.RpcDenseWprep * len(group))()
+        keep = []   # fp32 copies stay referenced until the launch is enqueued (stream order after that)
+        for i, L in enumerate(group):
+            W32 = L.conv.weight.detach().float().contiguous()
+            keep.append(W32)
+            wf = torch.empty((L.taps, L.co, L.ci), dtype=torch.bfloat16, device=dev)
+            wd = torch.empty((L.taps, L.ci, L.co), dtype=torch.bfloat16, device=dev)
+            descs[i] = _ffi.RpcDenseWprep(W32.data_ptr(), wf.data_ptr(), wd.data_ptr(), L.kind, L.ci, L.co,
+                                          L.taps, 1 if L.map == S1 else 0)
+            out.append((wf, wd))
+        _ffi.check(lib.rpc_dense_wprep_batch(descs, len(group), st), "rpc_dense_wprep_batch")
+    return out
+
+
+def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_pitch=None, out_off=0, wts=None):
+    """z = conv(h); BN (batch or running stats); y = relu(bn(z)) -> (y image, record).
+    wts: (forward, data-gradient) bf16 operands from _prep_weights, else prepared here."""
     R, S, O, Ho, Wo = L.images(B, H, W)
-    W32 = L.conv.weight.detach().float().contiguous()
-    wf = torch.empty((L.taps, L.co, L.ci), dtype=torch.bfloat16, device=dev)
-    wd = torch.empty((L.taps, L.ci, L.co), dtype=torch.bfloat16, device=dev)
-    _ffi.check(lib.rpc_dense_wprep(_ffi.ptr(W32), L.kind, L.ci, L.co, L.taps, 1 if L.map == S1 else 0,
-                                   _ffi.ptr(wf), _ffi.ptr(wd), st), "rpc_dense_wprep")
+    if wts is None:
+        wts = _prep_weights(lib, [L], dev, st)[0]
+    wf, wd = wts
     Mo = B * Ho * Wo
     z = torch.empty((Mo, L.co), dtype=torch.bfloat16, device=dev)
     ri, si, oi = _ffi.int_arr(R), _ffi.int_arr(S), _ffi.int_arr(O)
@@ -245,10 +264,11 @@ class BackboneFn(torch.autograd.Function):
         B, C, H, W = xi.shape
         h, pitch = xi, C
         recs, outs = [], []
+        wts = iter(_prep_weights(lib, [L for layers in blocks for L in layers], dev, st))
         for layers in blocks:
             brecs = []
             for L in layers:
-                h, rec, H, W = _forward_layer(lib, L, h, pitch, B, H, W, mod.training, dev, st)
+                h, rec, H, W = _forward_layer(lib, L, h, pitch, B, H, W, mod.training, dev, st, wts=next(wts))
                 pitch = L.co
                 brecs.append(rec)
             recs.append(brecs)
@@ -316,10 +336,11 @@ class NeckFn(torch.autograd.Function):
         out = _image(B, Ctot, H0, W0, dev)
         recs = []
         off = 0
-        for L, hi in zip(layers, ins):
+        wts = _prep_weights(lib, layers, dev, st)
+        for L, hi, wt in zip(layers, ins, wts):
             _, C, H, W = hi.shape
             _, rec, Ho, Wo = _forward_layer(lib, L, hi, C, B, H, W, mod.training, dev, st, out=out, out_pitch=Ctot,
-                                            out_off=off)
+                                            out_off=off, wts=wt)
             assert (Ho, Wo) == (H0, W0), "FPN deblocks must upsample to the first block's resolution"
             rec["off"] = off
             recs.append(rec)

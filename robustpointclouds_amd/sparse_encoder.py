@@ -206,15 +206,35 @@ def _r32(c):
     return (c + 31) // 32 * 32
 
 
+def _prep_bf16_weights(lib, specs, Ws, dev, st):
+    """Forward and data-gradient bf16 B^T tiles of every bf16 layer (entries of `specs` / `Ws`),
+    from the fp32 master weights in rpc_spconv_prep_weight_bf16_batch launches of up to 32 tiles."""
+    jobs = []
+    for sp, W in zip(specs, Ws):
+        for dg in (0, 1):
+            bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, dg), dtype=torch.bfloat16,
+                             device=dev)
+            jobs.append((sp, W, dg, bt))
+    for g0 in range(0, len(jobs), 32):
+        group = jobs[g0:g0 + 32]
+        descs = (_ffi.RpcSpconvWprep * len(group))()
+        for i, (sp, W, dg, bt) in enumerate(group):
+            descs[i] = _ffi.RpcSpconvWprep(W.data_ptr(), bt.data_ptr(), sp.K, sp.ci, sp.co, dg)
+        _ffi.check(lib.rpc_spconv_prep_weight_bf16_batch(descs, len(group), st), "rpc_spconv_prep_weight_bf16_batch")
+    return [(jobs[2 * i][3], jobs[2 * i + 1][3]) for i in range(len(specs))]
+
+
 def _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st):
     """bf16 dz rows (BatchNorm backward applied) and the dgrad weight tiles W[k] (as B^T)."""
     sp = rec["spec"]
     dzb = torch.empty((rec["n_out"], _r8(sp.co)), dtype=torch.bfloat16, device=dev)
     _ffi.check(lib.rpc_bnbwd_to_bf16_rows(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), rec["n_out"], sp.co,
                                           _ffi.ptr(dzb), st), "rpc_bnbwd_to_bf16_rows")
-    btd = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 1), dtype=torch.bfloat16, device=dev)
-    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(rec["W"]), sp.K, sp.ci, sp.co, 1, _ffi.ptr(btd), st),
-               "rpc_spconv_prep_weight_bf16")
+    btd = rec.get("btd")
+    if btd is None:
+        btd = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 1), dtype=torch.bfloat16, device=dev)
+        _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(rec["W"]), sp.K, sp.ci, sp.co, 1, _ffi.ptr(btd), st),
+                   "rpc_spconv_prep_weight_bf16")
     return dzb, btd
 
 
@@ -272,6 +292,13 @@ class SparseEncoderFn(torch.autograd.Function):
         bf16 = enc.bf16
         hsrc = None
         L = []
+        # bf16 layers (1..): forward + data-gradient weight tiles of all of them in one launch
+        wtiles = {}
+        if bf16 and len(enc.specs) > 1:
+            bl = list(range(1, len(enc.specs)))
+            Ws = [params[3 * li].detach().float().contiguous() for li in bl]
+            for li, tiles in zip(bl, _prep_bf16_weights(lib, [enc.specs[li] for li in bl], Ws, dev, st)):
+                wtiles[li] = tiles
         for li, (sp, m) in enumerate(zip(enc.specs, mods)):
             W = params[3 * li]
             gamma, beta = params[3 * li + 1], params[3 * li + 2]
@@ -314,10 +341,7 @@ class SparseEncoderFn(torch.autograd.Function):
             rec["bf16"] = bf16 and li > 0
             rec["h_in"] = hsrc if rec["bf16"] else None
             if rec["bf16"]:
-                bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 0), dtype=torch.bfloat16,
-                                 device=dev)
-                _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), sp.K, sp.ci, sp.co, 0, _ffi.ptr(bt), st),
-                           "rpc_spconv_prep_weight_bf16")
+                bt, rec["btd"] = wtiles[li]
                 e0 = enc.timer.start() if tm else None
                 _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(hsrc), sp.ci, _ffi.ptr(rec["nbr"]), sp.K, 0, n_out,
                                                     _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None, _ffi.ptr(part), 0,

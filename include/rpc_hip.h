@@ -8,9 +8,6 @@
  *   - `stream` is a hipStream_t passed as void* (the launcher's current stream);
  *   - return value 0 = success, otherwise an RPC_ERR_* code (the Python side raises);
  *     nothing in the library aborts or synchronises the device;
- *   - an *armed* workspace (marked so below) must be zero-filled once when it is allocated: the
- *     kernel's last-arriving block re-arms its ticket to zero, so the same workspace is reused by
- *     later calls on the same stream with no per-call memset.
  *
  * Each entry point names the reference interface it replaces (file:line in
  * /root/reference, or the un-vendored upstream call site that file reaches).

@@ -215,19 +215,6 @@ def workspace(nbytes: int, device) -> torch.Tensor:
 _ARMED: dict = {}
 
 
-def armed_workspace(tag: str, nbytes: int, device) -> torch.Tensor:
-    """A persistent zero-filled workspace for kernels whose last block re-arms its tickets
-    (include/rpc_hip.h "armed workspaces"): zeroed once when (re)allocated, then reused on the
-    same stream with no per-call memset. Stream-ordered reuse only: callers on other streams
-    need their own tag."""
-    key = (tag, torch.device(device))
-    t = _ARMED.get(key)
-    if t is None or t.numel() < nbytes:
-        t = torch.zeros(max(int(nbytes), 1), dtype=torch.uint8, device=device)
-        _ARMED[key] = t
-    return t
-
-
 def float_arr(vals):
     return (C.c_float * len(vals))(*[float(v) for v in vals])
 

@@ -81,7 +81,27 @@ __global__ __launch_bounds__(OBLK) void k_sqnorm(const long long* __restrict__ g
   double acc = 0.0;
   if (g) {
     g += s0;
-    for (int i = threadIdx.x; i < n; i += OBLK) {
+    int i0 = 0;
+    if ((((uintptr_t)g) & 15) == 0) {   // 16-B loads, four in flight per thread, four partial sums
+      const int n4 = n >> 2;
+      double a[4] = {0.0, 0.0, 0.0, 0.0};
+      int q = threadIdx.x;
+      for (; q + 3 * OBLK < n4; q += 4 * OBLK) {
+        float4 v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = ((const float4*)g)[q + u * OBLK];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          a[u] += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
+      }
+      for (; q < n4; q += OBLK) {
+        const float4 v = ((const float4*)g)[q];
+        a[0] += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
+      }
+      acc = (a[0] + a[1]) + (a[2] + a[3]);
+      i0 = n4 << 2;
+    }
+    for (int i = i0 + threadIdx.x; i < n; i += OBLK) {
       const float v = g[i];
       acc += (double)v * (double)v;
     }

@@ -487,27 +487,41 @@ __global__ __launch_bounds__(BLK) void k_to_dense(const float* __restrict__ z, c
   store_val(dense + dense_index<NHWC>(coors + 4 * r, c, C, s), h);
 }
 
+constexpr int FBLK = 1024;   // k_from_dense: 1024 threads = 1024 / C row lanes over the block's 64 rows
 template <typename T, bool NHWC>
-__global__ __launch_bounds__(BLK) void k_from_dense(const T* __restrict__ gd, const float* __restrict__ z,
+__global__ __launch_bounds__(FBLK) void k_from_dense(const T* __restrict__ gd, const float* __restrict__ z,
                                                     const float* __restrict__ bn, const int* __restrict__ coors,
                                                     int N, int C, Shape s, float* __restrict__ dy,
                                                     float* __restrict__ part) {
   // block: BM rows; threads laid out (row lane, channel) so that each row's gather and the dy
   // store are coalesced; row lanes combined in lane order (C <= 256)
-  __shared__ float sh[2][BLK];
+  __shared__ float sh[2][FBLK];
   const int r0 = blockIdx.x * BM, r1 = min(N, r0 + BM);
-  const int nl = BLK / C;                       // >= 1 row lanes
+  const int nl = FBLK / C;                       // >= 1 row lanes
   const int rl = threadIdx.x / C, c = threadIdx.x - rl * C;
   float s1 = 0.0f, s2 = 0.0f;
   if (rl < nl) {
     const float mu = bn[2 * C + c], sc = bn[c], sh0 = bn[C + c], is = bn[3 * C + c];
-    for (int r = r0 + rl; r < r1; r += nl) {
-      const float zz = z[(long long)r * C + c];
-      const float h = fmaxf(fmaf(zz - mu, sc, sh0), 0.0f);
-      const float v = h > 0.0f ? load_val(gd + dense_index<NHWC>(coors + 4 * r, c, C, s)) : 0.0f;
-      dy[(long long)r * C + c] = v;
-      s1 += v;
-      s2 += v * ((zz - mu) * is);
+    // four rows per round: their z values and dense gathers are in flight together
+    constexpr int RR = 4;
+    for (int rb = r0 + rl; rb < r1; rb += RR * nl) {
+      float zz[RR], gv[RR];
+#pragma unroll
+      for (int u = 0; u < RR; ++u) {
+        const int r = rb + u * nl;
+        zz[u] = r < r1 ? z[(long long)r * C + c] : 0.0f;
+        gv[u] = r < r1 ? load_val(gd + dense_index<NHWC>(coors + 4 * r, c, C, s)) : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < RR; ++u) {
+        const int r = rb + u * nl;
+        if (r >= r1) continue;
+        const float h = fmaxf(fmaf(zz[u] - mu, sc, sh0), 0.0f);
+        const float v = h > 0.0f ? gv[u] : 0.0f;
+        dy[(long long)r * C + c] = v;
+        s1 += v;
+        s2 += v * ((zz[u] - mu) * is);
+      }
     }
   }
   sh[0][threadIdx.x] = s1;
@@ -968,13 +982,13 @@ extern "C" int rpc_dense_to_sparse_grad(const void* grad_dense, const float* z, 
   dim3 g(cdiv(N, BM));
   hipStream_t st = (hipStream_t)stream;
   switch (flags) {
-    case 0: hipLaunchKernelGGL((k_from_dense<float, false>), g, dim3(BLK), 0, st, (const float*)grad_dense, z, bn,
+    case 0: hipLaunchKernelGGL((k_from_dense<float, false>), g, dim3(FBLK), 0, st, (const float*)grad_dense, z, bn,
                                coors, N, C, s, dy, part); break;
-    case 1: hipLaunchKernelGGL((k_from_dense<float, true>), g, dim3(BLK), 0, st, (const float*)grad_dense, z, bn,
+    case 1: hipLaunchKernelGGL((k_from_dense<float, true>), g, dim3(FBLK), 0, st, (const float*)grad_dense, z, bn,
                                coors, N, C, s, dy, part); break;
-    case 2: hipLaunchKernelGGL((k_from_dense<__hip_bfloat16, false>), g, dim3(BLK), 0, st,
+    case 2: hipLaunchKernelGGL((k_from_dense<__hip_bfloat16, false>), g, dim3(FBLK), 0, st,
                                (const __hip_bfloat16*)grad_dense, z, bn, coors, N, C, s, dy, part); break;
-    default: hipLaunchKernelGGL((k_from_dense<__hip_bfloat16, true>), g, dim3(BLK), 0, st,
+    default: hipLaunchKernelGGL((k_from_dense<__hip_bfloat16, true>), g, dim3(FBLK), 0, st,
                                 (const __hip_bfloat16*)grad_dense, z, bn, coors, N, C, s, dy, part);
   }
   RPC_LAUNCH_CHECK();

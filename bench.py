@@ -176,15 +176,17 @@ def main():
         model.middle_encoder.timer = timer
     NB = 4
     data = _nus_batches(NB, a.batch, rank, dev) if nus else _batches(NB, a.batch, rank, dev, a.classes)
+    # each step queues the next step's hard voxelisation on a side stream (Trainer.train_step
+    # next_points): the timed region still voxelises K batches, one per step
     for i in range(a.warmup):
-        tr.train_step(*data[i % NB])
+        tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     timer.enabled = True
     t0 = time.perf_counter()
     for i in range(a.steps):
-        tr.train_step(*data[i % NB])
+        tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0])
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()

@@ -123,25 +123,45 @@ struct ChanAcc {
   }
 };
 
-// thread j < 2C: fixed-order sum of column j over all blocks' partial rows
-__device__ __forceinline__ double col_total(const double* part, int j) {
-  // 8 independent partial sums keep 8 loads in flight; combined in a fixed order (deterministic)
-  const int R = (int)gridDim.x;
-  double a[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  int r = 0;
-  for (; r + 8 <= R; r += 8)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) a[k] += part[(size_t)(r + k) * 2 * MAXC + j];
-  for (; r < R; ++r) a[0] += part[(size_t)r * 2 * MAXC + j];
-  return ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+// Column totals of the gridDim.x partial rows part[r][0..ncol), run by the whole (last-arriving)
+// block: thread t = rg * ncol + j sums rows rg, rg + G, rg + 2G, ... of column j (G = blockDim / ncol
+// row groups, four independent sums keep four loads in flight, consecutive threads read consecutive
+// columns of one row), then thread j adds the G group sums in group order into lds[j]. The
+// assignment depends only on (blockDim, ncol, gridDim), so the result is run-to-run deterministic.
+// lds needs max(blockDim, ncol) doubles; it is free to overwrite (after the ticket barrier).
+__device__ void block_col_totals(const double* part, int ncol, double* lds) {  // ncol <= blockDim.x
+  const int R = (int)gridDim.x, t = threadIdx.x;
+  const int G = (int)blockDim.x / ncol;
+  const int j = t % ncol, rg = t / ncol;
+  double tot = 0.0;
+  if (rg < G) {
+    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
+    int r = rg;
+    for (; r + 3 * G < R; r += 4 * G) {
+      a0 += part[(size_t)r * 2 * MAXC + j];
+      a1 += part[(size_t)(r + G) * 2 * MAXC + j];
+      a2 += part[(size_t)(r + 2 * G) * 2 * MAXC + j];
+      a3 += part[(size_t)(r + 3 * G) * 2 * MAXC + j];
+    }
+    for (; r < R; r += G) a0 += part[(size_t)r * 2 * MAXC + j];
+    tot = (a0 + a1) + (a2 + a3);
+  }
+  __syncthreads();
+  if (rg < G) lds[t] = tot;
+  __syncthreads();
+  double c = 0.0;
+  if (t < ncol)
+    for (int g = 0; g < G; ++g) c += lds[g * ncol + t];
+  __syncthreads();
+  if (t < ncol) lds[t] = c;
+  __syncthreads();
 }
 
 // finalize a BatchNorm layer from its batch sums (train) — run by the last block
 template <int C>
 __device__ void bn_finalize(Dev& d, int l, double* lds) {
   const int N = d.meta[0];
-  for (int j = threadIdx.x; j < 2 * C; j += BLK) lds[j] = col_total(d.part, j);
-  __syncthreads();
+  block_col_totals(d.part, 2 * C, lds);
   for (int c = threadIdx.x; c < C; c += BLK) {
     double mean = lds[c] / N;
     double var = lds[C + c] / N - mean * mean;
@@ -228,8 +248,7 @@ __global__ __launch_bounds__(BLK) void k_xstats(Dev d) {
     d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
   }
   if (!last_block_arrive(d.ticket + 0, &lastf)) return;
-  if (threadIdx.x < 2 * F + 1) lds[threadIdx.x] = col_total(d.part, threadIdx.x);
-  __syncthreads();
+  block_col_totals(d.part, 2 * F + 1, lds);
   if (threadIdx.x == 0) {
     int N = d.fused ? d.off[d.rows] : d.rows;
     d.meta[0] = N;
@@ -419,8 +438,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_last(Dev d) {
     d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
   }
   if (!last_block_arrive(d.ticket + 6, &lastf)) return;
-  if (threadIdx.x < NS) lds[threadIdx.x] = col_total(d.part, threadIdx.x);
-  __syncthreads();
+  block_col_totals(d.part, NS, lds);
   if (threadIdx.x == 0) {
     const int n = N;
     int flag = d.meta[1] || lds[2 + 2 * F] != 0.0;
@@ -502,7 +520,8 @@ __global__ void k_bn_eval(Dev d) {
 // ------------------------------------------------------------------ backward kernels
 template <int C>
 __device__ void bnb_finalize(Dev& d, int l, double* lds) {
-  for (int j = threadIdx.x; j < 2 * C; j += BLK) d.bnsum[l][j] = col_total(d.part, j);
+  block_col_totals(d.part, 2 * C, lds);
+  for (int j = threadIdx.x; j < 2 * C; j += blockDim.x) d.bnsum[l][j] = lds[j];
 }
 
 // output layer + attention: dz5 = d u, dsig, da, a, dh4' and BN4 backward sums

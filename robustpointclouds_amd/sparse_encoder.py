@@ -299,6 +299,33 @@ class SparseEncoderFn(torch.autograd.Function):
             Ws = [params[3 * li].detach().float().contiguous() for li in bl]
             for li, tiles in zip(bl, _prep_bf16_weights(lib, [enc.specs[li] for li in bl], Ws, dev, st)):
                 wtiles[li] = tiles
+        # Output-row counts of the strided layers are host reads. Each count is issued as soon as its
+        # input coordinates exist (one level ahead of the GEMMs), copied to pinned memory behind an
+        # event, and waited for only when its layer is reached: the GEMMs of the current level keep the
+        # GPU busy while the host waits, instead of the stream draining at every read.
+        pending = {}
+
+        def issue_count(start, coors_in, n_in):
+            j = next((k for k in range(start, len(enc.specs)) if enc.specs[k].kind != "subm"), None)
+            if j is None:
+                return
+            sj = enc.specs[j]
+            oshp = _ffi.int_arr((B,) + enc.shapes[sj.lvl_out])
+            ks_, sd, pd = _ffi.int_arr(sj.ksize), _ffi.int_arr(sj.stride), _ffi.int_arr(sj.pad)
+            wsb = lib.rpc_spconv_rulebook_workspace_size(n_in, sj.K)
+            ws = _ffi.workspace(wsb, dev)
+            n_dev = torch.empty(1, dtype=torch.int32, device=dev)
+            gout = enc.grid(sj.lvl_out, B, dev)
+            _ffi.check(lib.rpc_spconv_rulebook_count(_ffi.ptr(coors_in), n_in, oshp, ks_, sd, pd, _ffi.ptr(gout),
+                                                     _ffi.ptr(n_dev), _ffi.ptr(ws), wsb, st),
+                       "rpc_spconv_rulebook_count")
+            n_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+            n_host.copy_(n_dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(dev))
+            pending[j] = (n_host, ev, ws, gout, oshp, ks_, sd, pd)
+
+        issue_count(0, cur_coors, cur_n)
         for li, (sp, m) in enumerate(zip(enc.specs, mods)):
             W = params[3 * li]
             gamma, beta = params[3 * li + 1], params[3 * li + 2]
@@ -315,16 +342,9 @@ class SparseEncoderFn(torch.autograd.Function):
                     rb[sp.key] = nbr
                 rec.update(nbr=rb[sp.key], n_out=cur_n, coors_out=cur_coors)
             else:
-                oshp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_out])
-                sd, pd = _ffi.int_arr(sp.stride), _ffi.int_arr(sp.pad)
-                wsb = lib.rpc_spconv_rulebook_workspace_size(cur_n, sp.K)
-                ws = _ffi.workspace(wsb, dev)
-                n_dev = torch.empty(1, dtype=torch.int32, device=dev)
-                gout = enc.grid(sp.lvl_out, B, dev)
-                _ffi.check(lib.rpc_spconv_rulebook_count(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
-                                                         _ffi.ptr(n_dev), _ffi.ptr(ws), wsb, st),
-                           "rpc_spconv_rulebook_count")
-                n_out = int(n_dev.item())          # host read: output row count
+                n_host, ev, ws, gout, oshp, ks, sd, pd = pending.pop(li)
+                ev.synchronize()
+                n_out = int(n_host[0])             # host read: output row count (issued one level ahead)
                 coors_out = torch.empty((n_out, 4), dtype=torch.int32, device=dev)
                 nbr_out = torch.empty((n_out, sp.K), dtype=torch.int32, device=dev)
                 nbr_in = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
@@ -333,6 +353,7 @@ class SparseEncoderFn(torch.autograd.Function):
                                                          _ffi.ptr(nbr_in), _ffi.ptr(ws), st),
                            "rpc_spconv_rulebook_build")
                 rec.update(nbr=nbr_out, nbr_in=nbr_in, n_out=n_out, coors_out=coors_out)
+                issue_count(li + 1, coors_out, n_out)
             n_out = rec["n_out"]
             z = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
             nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)

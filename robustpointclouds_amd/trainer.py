@@ -107,6 +107,8 @@ class Trainer:
         self.hooks = []
         self.should_stop = False
         self.last_log = None
+        self._side = None        # side stream of the batch prefetch
+        self._pending = None     # (points list, PendingVoxels) of the prefetched next batch
 
     # mmengine-runner-like attributes used by custom_hook.py
     @property
@@ -125,14 +127,40 @@ class Trainer:
             if hasattr(h, "before_train_epoch"):
                 h.before_train_epoch(self)
 
-    def train_step(self, points, gt):
-        """points: list of [Ni, 4] cuda tensors; gt: dict(gt_boxes [B, M, 7], gt_labels [B, M])."""
+    def train_step(self, points, gt, next_points=None):
+        """points: list of [Ni, 4] cuda tensors; gt: dict(gt_boxes [B, M, 7], gt_labels [B, M]).
+
+        next_points (optional): the next step's points, already complete on the device. Their hard
+        voxelisation is queued on a side stream now, concurrently with this step, and its voxel count
+        is read at the next step, so that read no longer drains the training stream (the next step's
+        kernels queue behind this step's backward instead of starting on an idle GPU). Same kernels,
+        same results: only where the voxelisation is queued changes."""
         m = self.module
         if not m.training:
             m.train()
-        batch = m.data_preprocessor(dict(inputs=dict(points=points)), training=True)["inputs"]
+        pend = self._pending
+        self._pending = None
+        if pend is not None and pend[0] is points:
+            v, c, n, vn = pend[1].result(torch.cuda.current_stream(self.device))
+            batch = dict(points=points, voxels=dict(voxels=v, coors=c, num_points=n, voxel_num=vn))
+        else:
+            batch = m.data_preprocessor(dict(inputs=dict(points=points)), training=True)["inputs"]
         batch["batch_size"] = len(points)
+        if next_points is not None:
+            self._prefetch(next_points)
         return self.step_batch(batch, gt)
+
+    def _prefetch(self, points):
+        vl = getattr(getattr(self.module, "data_preprocessor", None), "voxel_layer", None)
+        if vl is None or not hasattr(vl, "voxelize_frames_deferred") or self.device.type != "cuda":
+            return
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        vl.train(True)
+        for p in points:    # read on the side stream: keep the allocator from reusing them early
+            p.record_stream(self._side)
+        with torch.cuda.stream(self._side):
+            self._pending = (points, vl.voxelize_frames_deferred(points))
 
     def step_batch(self, batch, gt):
         """The step after voxelisation: loss -> parse_losses -> backward (DDP all-reduce) -> clip

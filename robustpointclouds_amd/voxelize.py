@@ -31,8 +31,8 @@ def _frame_offsets(sizes: Sequence[int], device) -> torch.Tensor:
 
 
 def voxelize_batch(points: torch.Tensor, frame_offsets: torch.Tensor, voxel_size, point_cloud_range,
-                   max_num_points: int, max_voxels: int):
-    """Voxelise B concatenated frames.
+                   max_num_points: int, max_voxels: int, defer: bool = False):
+    """Voxelise B concatenated frames (defer=True: return a PendingVoxels instead of reading V now).
 
     points:         [P, F] float32 cuda, frames back to back
     frame_offsets:  [B+1] int32 cuda
@@ -60,8 +60,34 @@ def voxelize_batch(points: torch.Tensor, frame_offsets: torch.Tensor, voxel_size
                                _ffi.ptr(num_points), _ffi.ptr(voxel_num), _ffi.ptr(ws), wsb,
                                _ffi.stream_of(points))
     _ffi.check(rc, "rpc_hard_voxelize")
+    if defer:
+        return PendingVoxels(voxels, coors, num_points, voxel_num, B)
     V = int(voxel_num[B].item())  # the one host sync: output shapes
     return voxels[:V], coors[:V], num_points[:V], voxel_num
+
+
+class PendingVoxels:
+    """A voxelisation whose kernels are queued (normally on a side stream) and whose voxel count V —
+    the one host read — is copied to pinned memory behind an event instead of draining the stream.
+    `result(consumer)` makes the consumer stream wait for the voxelisation, marks the outputs as used
+    by it (caching-allocator safety across streams) and reads V, by then normally long complete."""
+
+    def __init__(self, voxels, coors, num_points, voxel_num, B):
+        self.t = (voxels, coors, num_points, voxel_num)
+        self.host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+        self.host.copy_(voxel_num[B:], non_blocking=True)
+        self.ev = torch.cuda.Event()
+        self.ev.record(torch.cuda.current_stream(voxels.device))
+
+    def result(self, consumer=None):
+        voxels, coors, num_points, voxel_num = self.t
+        if consumer is not None:
+            consumer.wait_event(self.ev)
+            for x in self.t:
+                x.record_stream(consumer)
+        self.ev.synchronize()
+        V = int(self.host[0])
+        return voxels[:V], coors[:V], num_points[:V], voxel_num
 
 
 class Voxelization(nn.Module):
@@ -94,3 +120,12 @@ class Voxelization(nn.Module):
         v, c, n, vn = voxelize_batch(pts, off, self.voxel_size, self.point_cloud_range,
                                      self.max_num_points, self._cap())
         return dict(voxels=v, coors=c, num_points=n, voxel_num=vn)
+
+    def voxelize_frames_deferred(self, points_list: Sequence[torch.Tensor]) -> PendingVoxels:
+        """voxelize_frames with the kernels queued on the current stream and V read later
+        (`PendingVoxels.result`); the trainer's batch prefetch runs this on a side stream."""
+        dev = points_list[0].device
+        pts = torch.cat([p.contiguous() for p in points_list], 0)
+        off = _frame_offsets([p.shape[0] for p in points_list], dev)
+        return voxelize_batch(pts, off, self.voxel_size, self.point_cloud_range, self.max_num_points,
+                              self._cap(), defer=True)

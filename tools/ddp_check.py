@@ -27,10 +27,15 @@ def main():
     model = make_kitti_model(num_classes=1, device=dev, epoch=3)
     tr = Trainer(model, ddp=world > 1, bf16=True, device=dev)
     losses = []
+    batches = []
     for step in range(3):
         pts, boxes, labels = kitti_batch(2, seed0=100 * rank + 10 * step, num_classes=1)
         gb, gl = pack_gt(list(zip(boxes, labels)), dev)
-        lg = tr.train_step([torch.from_numpy(p).to(dev) for p in pts], dict(gt_boxes=gb, gt_labels=gl))
+        batches.append(([torch.from_numpy(p).to(dev) for p in pts], dict(gt_boxes=gb, gt_labels=gl)))
+    for step in range(3):
+        # as bench.py: the next batch is voxelised on a side stream during this step (Trainer prefetch)
+        nxt = batches[step + 1][0] if step + 1 < len(batches) else None
+        lg = tr.train_step(*batches[step], next_points=nxt)
         losses.append(float(sum(v for k, v in lg.items() if "loss" in k)))
     torch.cuda.synchronize()
     flat = torch.cat([p.detach().double().flatten() for p in model.parameters()])

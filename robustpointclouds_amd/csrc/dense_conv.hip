@@ -128,11 +128,15 @@ struct IG {
   int M;           // GEMM rows = R.B * R.H * R.W
 };
 
+// 1-tap maps (P1, U2: 2-4 K-steps per block, latency-bound prologue / epilogue) use ONE LDS tile
+// pair (37 KB) so four blocks share a CU and hide each other's global round trips; the 9-tap maps
+// keep the double-buffered pair (two blocks per CU).
 template <int MAP>
-__global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
+__global__ __launch_bounds__(BLK, (taps_of<MAP>() == 1 ? 4 : 2)) void k_igemm(IG g) {
   constexpr int T = taps_of<MAP>();
-  __shared__ __attribute__((aligned(16))) u16 sX[2][TM * LP];
-  __shared__ __attribute__((aligned(16))) u16 sW[2][TN * LP];
+  constexpr int NB = T == 1 ? 1 : 2;
+  __shared__ __attribute__((aligned(16))) u16 sX[NB][TM * LP];
+  __shared__ __attribute__((aligned(16))) u16 sW[NB][TN * LP];
   __shared__ int sRow[TM * T];
   __shared__ float sP[2][2][TN];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -195,7 +199,7 @@ __global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
   IG_STORE(0)
   __syncthreads();
   for (int ks = 0; ks < NKS; ++ks) {
-    const int buf = ks & 1;
+    const int buf = NB == 2 ? (ks & 1) : 0;
     const bool more = ks + 1 < NKS;
     if (more) {
       IG_LOAD(ks + 1)
@@ -215,8 +219,9 @@ __global__ __launch_bounds__(BLK, 2) void k_igemm(IG g) {
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
     }
+    if (NB == 1 && more) __syncthreads();   // one tile pair: every wave has read it before it is refilled
     if (more) {
-      IG_STORE(buf ^ 1)
+      IG_STORE(NB == 2 ? (buf ^ 1) : 0)
     }
     __syncthreads();
   }

@@ -852,7 +852,7 @@ __global__ __launch_bounds__(BLK) void k_wprep_batch(WprepBatch b) {
     wprep_elem(e, d.W, d.kind, d.ci, d.co, d.taps, d.flip, (u16*)d.w_fwd, (u16*)d.w_dgrad);
 }
 
-// k_slab_reduce (common.h: same fixed summation order) fused with the store to torch layout
+// fixed-order chunk reduction (4 interleaved lanes, as k_slab_reduce before its 8-lane form) fused with the store to torch layout
 // (kind 0: [co][ci][t], kind 1: [ci][co][t]): the reduced [T][CI][CO] element goes straight to dW
 __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int chunks, int kind, int CI,
                                                       int CO, int T, float* __restrict__ dW) {

@@ -1,0 +1,53 @@
+"""Host logic of Trainer.train_step(next_points=...) on the CPU: with no HIP device the batch prefetch
+is a no-op, every step runs the model's own data_preprocessor, and the trajectory equals the plain
+train_step's (the GPU side-stream path is covered by tests/test_gpu_prefetch.py)."""
+import torch
+from torch import nn
+
+from robustpointclouds_amd.trainer import Trainer
+
+
+class _Pre(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.calls = 0
+
+    def forward(self, data, training=False):
+        self.calls += 1
+        pts = data["inputs"]["points"]
+        return dict(inputs=dict(points=pts, voxels=dict(feat=torch.cat(pts, 0))))
+
+
+class _Toy(nn.Module):
+    def __init__(self):
+        super().__init__()
+        self.data_preprocessor = _Pre()
+        self.lin = nn.Linear(4, 1)
+
+    def loss(self, batch, gt):
+        f = batch["voxels"]["feat"]
+        return dict(loss_fit=((self.lin(f).squeeze(-1) - gt) ** 2).mean())
+
+
+def _run(prefetch):
+    torch.manual_seed(0)
+    m = _Toy()
+    tr = Trainer(m, lr=1e-2, device=torch.device("cpu"), iters_per_epoch=10)
+    g = torch.Generator().manual_seed(1)
+    data = [([torch.randn(5, 4, generator=g), torch.randn(3, 4, generator=g)], torch.randn(8, generator=g))
+            for _ in range(3)]
+    order = [0, 1, 2, 1]
+    logs = []
+    for k, i in enumerate(order):
+        nxt = data[order[k + 1]][0] if prefetch and k + 1 < len(order) else None
+        logs.append(float(tr.train_step(*data[i], next_points=nxt)["loss_fit"]))
+    assert tr._pending is None
+    return logs, m.data_preprocessor.calls, [p.detach().clone() for p in m.parameters()]
+
+
+def test_prefetch_is_a_noop_on_cpu():
+    la, ca, pa = _run(False)
+    lb, cb, pb = _run(True)
+    assert ca == cb == 4
+    assert la == lb
+    assert all(torch.equal(x, y) for x, y in zip(pa, pb))

@@ -4,11 +4,17 @@
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \\
         --master-port P bench.py --gpus N --steps K --warmup W
 
-Workload (BASELINE.json configs[1]): AdversarialVoxelNet (SECOND) KITTI Car-only, batch 6
-frames per GPU, perturber active (_epoch = 3), dense backbone/neck/head under bf16 autocast
-(voxelize / perturber / sparse encoder in fp32 kernels), AdamW + clip 0.5, synthetic
-HDL-64E-like frames pre-staged in HBM. N > 1: frames sharded across ranks (weak scaling),
-DDP gradient all-reduce over RCCL. Rank 0 prints ONE JSON line.
+Workload = the metric's own config (BASELINE.json metric "SECOND KITTI-3class", configs[2]):
+AdversarialVoxelNet (SECOND) KITTI 3-class (perturber hidden [64, 128, 64], 6 anchors per BEV
+cell), batch 6 frames per GPU, perturber active (_epoch = 3), bf16 perf mode (fp32 voxelize /
+perturber / sparse layer 0 / head losses; bf16 MFMA sparse layers 1-11 and SECOND/FPN), ClipAdamW
+(clip 0.5 + AdamW), synthetic HDL-64E-like frames pre-staged in HBM. `--classes 1` is configs[1]
+(Car-only). N > 1: frames sharded across ranks (weak scaling), DDP gradient all-reduce over RCCL.
+
+`--gpus N` is honoured: under torch.distributed.run the world size must equal N (else exit 2);
+a plain `python bench.py --gpus N` (N > 1) starts torch.distributed.run with N ranks as a child
+process (before this process touches the GPU) and exits with its status. Rank 0 prints ONE JSON
+line; `n_gpus` is the process-group world size.
 """
 from __future__ import annotations
 
@@ -28,7 +34,8 @@ def _args():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=None, help="frames per GPU (6 KITTI, 4 nuScenes)")
-    ap.add_argument("--classes", type=int, default=1, choices=[1, 3])
+    ap.add_argument("--classes", type=int, default=3, choices=[1, 3],
+                    help="3 = KITTI 3-class (the metric's config, default); 1 = Car-only (BASELINE configs[1])")
     ap.add_argument("--model", default="voxelnet", choices=["voxelnet", "strong", "centerpoint"],
                     help="strong = StrongAdversarialVoxelNet, sensor_error_bound 0.4 (BASELINE config 5); "
                          "centerpoint = AdversarialCenterPoint nuScenes, batch 4 (BASELINE config 4)")
@@ -149,10 +156,31 @@ def cpu_baseline(frames: int, classes: int):
                        f"{frames} synthetic KITTI frames, {classes}-class, {dt:.1f} s")
 
 
+def _launch_ranks(n: int) -> int:
+    """Re-run this script under torch.distributed.run with n ranks (child process; no GPU touched
+    here) and return its exit status."""
+    import socket
+    import subprocess
+    import sys
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__), *sys.argv[1:]]
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     a = _args()
+    import sys
+    if "RANK" not in os.environ and a.gpus > 1:
+        sys.exit(_launch_ranks(a.gpus))
     from robustpointclouds_amd.trainer import Trainer, init_distributed, make_kitti_model, make_nus_model
     rank, world, local = init_distributed()
+    if world != a.gpus:
+        print(json.dumps(dict(error=f"--gpus {a.gpus} but the process group has {world} ranks")), flush=True)
+        sys.exit(2)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
@@ -163,7 +191,7 @@ def main():
         model = make_nus_model(device=dev, epoch=3)
     else:
         model = make_kitti_model(num_classes=a.classes, device=dev, epoch=3, variant=a.model)
-    tr = Trainer(model, ddp=world > 1, bf16=not a.fp32, device=dev)
+    tr = Trainer(model, ddp=dist.is_initialized(), bf16=not a.fp32, device=dev)
     from robustpointclouds_amd import dense_bev
     from robustpointclouds_amd.sparse_encoder import KernelTimer
     if a.roofline_kernel == "dense":
@@ -181,19 +209,19 @@ def main():
     for i in range(a.warmup):
         tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     timer.enabled = True
     t0 = time.perf_counter()
     for i in range(a.steps):
         tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0])
     torch.cuda.synchronize()
-    if world > 1:
+    if dist.is_initialized():
         dist.barrier()
     dt = time.perf_counter() - t0
     timer.enabled = False
     ks = timer.summary()
-    if world > 1:
+    if dist.is_initialized():
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
@@ -216,7 +244,8 @@ def main():
                                kernel_dtype=("fp32 (voxelize, perturber, sparse encoder)" if a.fp32 else
                                              "fp32 voxelize/perturber/sparse layer 0; bf16 MFMA (fp32 accumulate,"
                                              " fp32 BN statistics) sparse layers 1-11"),
-                               parallelism=f"dp{world}"))
+                               parallelism=f"dp{world}",
+                               dist_backend=dist.get_backend() if dist.is_initialized() else None))
         if ks and op is None:
             peak = PEAK["bf16_mfma"]
             res["roofline"] = dict(bound="mfma", achieved=round(ks["tflops"], 3), peak=peak, unit="TFLOP/s",
@@ -240,7 +269,7 @@ def main():
         if not a.no_cpu_baseline and a.model == "voxelnet":
             res["cpu_baseline"] = cpu_baseline(a.cpu_frames, a.classes)
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 

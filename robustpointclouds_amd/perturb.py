@@ -45,6 +45,9 @@ def _ptr_array(tensors):
 
 
 def _run_forward(cfg, params, x, rows, slots, num_points, out, vfe):
+    if not x.is_cuda:
+        raise RuntimeError("VoxelPerturber runs on the HIP kernels only: its input is a CPU tensor "
+                           f"({tuple(x.shape)}); move the model and points to a ROCm device")
     lib = _ffi.load()
     dev = x.device
     wsb = lib.rpc_perturber_workspace_size(C.byref(cfg), rows, slots)

@@ -62,8 +62,11 @@ class NaNDetectionHook(Hook):
     def after_train_iter(self, runner, batch_idx, data_batch=None, outputs=None):
         log = getattr(runner, "logger", logging.getLogger("rpc"))
         outputs = outputs or {}
-        bad = [k for k, v in outputs.items() if "loss" in k and isinstance(v, torch.Tensor)
-               and not torch.isfinite(v).all()]
+        keys = [k for k, v in outputs.items() if "loss" in k and isinstance(v, torch.Tensor)]
+        bad = []
+        if keys:   # one device->host read for all loss keys (not one sync per key)
+            fin = torch.stack([torch.isfinite(outputs[k]).all() for k in keys]).cpu()
+            bad = [k for k, ok in zip(keys, fin.tolist()) if not ok]
         if bad:
             self.nan_count += 1
             self.consecutive_nan_count += 1

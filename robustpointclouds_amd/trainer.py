@@ -46,21 +46,59 @@ def param_groups(model, lr, custom_keys=None):
 
 
 class LRSchedule:
-    """LinearLR(start 0.1, 2000 iters) then CosineAnnealingLR(T_max epochs, eta_min) (:142-159)."""
+    """mmengine's chained param_scheduler of the reference configs (…3class.py:142-159):
 
-    def __init__(self, optimizer, iters_per_epoch, warmup=2000, start_factor=0.1, T_max=30, eta_min=1e-6):
+        LinearLR(start_factor 0.1, by_epoch=False, begin 0, end 2000)
+        CosineAnnealingLR(T_max 30, eta_min 1e-6, begin 0, end 30, by_epoch=True,
+                          convert_to_iter_based=True)  -> T_max = end = 30 * iters_per_epoch
+
+    restated RECURSIVELY, as mmengine applies them: each scheduler rescales the group's CURRENT lr
+    once per iteration (ParamSchedulerHook.after_train_iter), so a manual lr change by a hook
+    (NaNDetectionHook's x0.1) persists, and eta_min is the same absolute floor for every group
+    (no eta_min_ratio). Construction applies step 0 (LinearLR: lr = initial_lr * start_factor)."""
+
+    def __init__(self, optimizer, iters_per_epoch, warmup=2000, start_factor=0.1, T_max=30, eta_min=1e-6,
+                 cos_end=None):
         self.opt = optimizer
         self.ipe = max(1, iters_per_epoch)
-        self.warmup, self.start, self.T, self.eta_min = warmup, start_factor, T_max, eta_min
+        self.start = start_factor
+        self.lin_end = warmup                       # LinearLR end (iterations)
+        self.lin_total = warmup - 1                 # mmengine: total_iters = end - begin - 1
+        self.T = T_max * self.ipe                   # convert_to_iter_based
+        self.cos_end = (T_max if cos_end is None else cos_end) * self.ipe
+        self.eta_min = eta_min
+        for g in optimizer.param_groups:
+            g.setdefault("initial_lr", g["lr"])
         self.base = [g["initial_lr"] for g in optimizer.param_groups]
+        self.last_step = 0
+        if self.lin_end > 0:
+            for g in optimizer.param_groups:
+                g["lr"] = g["lr"] * self.start
 
-    def set(self, it):
-        w = 1.0 if it >= self.warmup else self.start + (1.0 - self.start) * it / self.warmup
-        ep = min(it / self.ipe, self.T)
-        for g, b in zip(self.opt.param_groups, self.base):
-            eta = self.eta_min * b / self.base[0]
-            cos = eta + (b - eta) * (1 + math.cos(math.pi * ep / self.T)) / 2
-            g["lr"] = cos * w
+    def step(self):
+        """After one training iteration: LinearLR.step() then CosineAnnealingLR.step()."""
+        self.last_step += 1
+        t = self.last_step
+        gs = self.opt.param_groups
+        if t < self.lin_end and self.lin_total > 0:
+            f = 1.0 + (1.0 - self.start) / (self.lin_total * self.start + (t - 1) * (1.0 - self.start))
+            for g in gs:
+                g["lr"] = g["lr"] * f
+        if t < self.cos_end:
+            T, eta = self.T, self.eta_min
+            if (t - 1 - T) % (2 * T) == 0:
+                for g, b in zip(gs, self.base):
+                    g["lr"] = g["lr"] + (b - eta) * (1 - math.cos(math.pi / T)) / 2
+            else:
+                r = (1 + math.cos(math.pi * t / T)) / (1 + math.cos(math.pi * (t - 1) / T))
+                for g in gs:
+                    g["lr"] = r * (g["lr"] - eta) + eta
+
+    def state_dict(self):
+        return dict(last_step=self.last_step)
+
+    def load_state_dict(self, sd):
+        self.last_step = int(sd["last_step"])
 
 
 class Trainer:
@@ -85,7 +123,7 @@ class Trainer:
                     mod.hip = True
                 else:
                     mod.to(memory_format=torch.channels_last)
-        if ddp and dist.is_initialized() and dist.get_world_size() > 1:
+        if ddp and dist.is_initialized():
             # 6 MB buckets: the 16 MB of SECOND gradients (ready together when its one-node backward
             # ends) go out in three RCCL all-reduces that overlap the sparse-encoder and perturber
             # backward; with one 25 MB bucket the reduction waited for the end of backward
@@ -159,6 +197,9 @@ class Trainer:
         vl.train(True)
         for p in points:    # read on the side stream: keep the allocator from reusing them early
             p.record_stream(self._side)
+        # the points may still be in flight on the training stream (GpuTrainAugment output, a
+        # non_blocking pinned copy): order the side stream after everything queued there so far
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
             self._pending = (points, vl.voxelize_frames_deferred(points))
 
@@ -168,7 +209,6 @@ class Trainer:
         m = self.module
         if not m.training:   # Module.train() walks every submodule (~1 ms of host time)
             m.train()
-        self.sched.set(self.iter)
         with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.bf16):
             if isinstance(self.model, torch.nn.parallel.DistributedDataParallel):
                 losses = self.model(batch, gt, mode="loss")     # DDP hooks fire on the grads
@@ -184,9 +224,12 @@ class Trainer:
         self.opt.zero_grad(set_to_none=True)
         self.iter += 1
         self.last_log = log_vars
+        # hooks first, then the schedulers (mmengine: NaNDetectionHook NORMAL priority runs before
+        # ParamSchedulerHook LOW), so a hook's lr cut is what the schedule rescales from
         for h in self.hooks:
             if hasattr(h, "after_train_iter"):
                 h.after_train_iter(self, self.iter - 1, None, log_vars)
+        self.sched.step()
         return log_vars
 
 
@@ -222,12 +265,21 @@ def make_nus_model(device=None, adversarial=True, epoch=3):
     return model
 
 
-def init_distributed():
-    """torch.distributed from torchrun env vars; backend nccl (= RCCL on ROCm) on GPU, gloo on CPU."""
-    if "RANK" not in os.environ or int(os.environ.get("WORLD_SIZE", "1")) <= 1:
-        return 0, 1, 0
+def init_distributed(force: bool = False):
+    """torch.distributed from torchrun env vars; backend nccl (= RCCL on ROCm) on GPU, gloo on CPU.
+
+    A process launched by torch.distributed.run (RANK in the environment) always joins a process
+    group, also at WORLD_SIZE 1, so a one-rank run still builds the RCCL communicator and sends
+    DDP's bucketed all-reduce through it; a plain `python` run (no RANK) stays single-process
+    unless `force` (then a one-rank group on 127.0.0.1)."""
+    if "RANK" not in os.environ:
+        if not force:
+            return 0, 1, 0
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
     rank = int(os.environ["RANK"])
-    world = int(os.environ["WORLD_SIZE"])
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", rank))
     os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
     # nccl (= RCCL) on GPU; RPC_DIST_BACKEND=gloo lets several ranks share one GPU in tests
@@ -237,3 +289,10 @@ def init_distributed():
     if not dist.is_initialized():
         dist.init_process_group(backend=backend)
     return rank, world, local
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]

@@ -57,7 +57,7 @@ def _worker(rank, port, out_dir):
         d = _load("list_e3")
         m = _build(d)
         tr = Trainer(m, lr=1e-2, ddp=True, device=torch.device("cpu"), iters_per_epoch=10)
-        tr.sched.set = lambda it: None      # constant lr for the comparison
+        tr.sched.step = lambda: None        # constant lr for the comparison
         assert isinstance(tr.model, torch.nn.parallel.DistributedDataParallel)
         tr.step_batch(_shard(d, rank), [None])
         torch.save({k: v.detach() for k, v in m.state_dict().items()}, os.path.join(out_dir, f"r{rank}.pt"))

@@ -18,11 +18,29 @@ def _port():
         return s.getsockname()[1]
 
 
-def test_ddp_two_ranks_identical_parameters():
-    env = dict(os.environ, RPC_DIST_BACKEND="gloo", HSA_ENABLE_IPC_MODE_LEGACY="0")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+def _run(nproc, backend=None, classes=3):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", RPC_DDP_CLASSES=str(classes))
+    env.pop("RPC_DIST_BACKEND", None)
+    if backend:
+        env["RPC_DIST_BACKEND"] = backend
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "tools", "ddp_check.py")]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert '"ddp": "ok"' in out, out[-3000:]
+    print(out[-600:])
+    return out
+
+
+def test_ddp_two_ranks_identical_parameters():
+    """Two ranks share the box's one GPU over gloo (RCCL refuses two ranks on one device)."""
+    _run(2, backend="gloo", classes=3)
+
+
+def test_ddp_rccl_backend_one_rank():
+    """The RCCL path: backend nccl (= RCCL on ROCm), DDP's bucketed all-reduce and an explicit
+    all_reduce through the RCCL communicator, 3-class model (the 8xb6 config's per-rank step)."""
+    out = _run(1, backend=None, classes=3)
+    assert '"backend": "nccl"' in out, out[-3000:]
+    assert '"all_reduce_ok": true' in out, out[-3000:]

@@ -3,10 +3,14 @@
     RPC_DIST_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \\
         --master-addr 127.0.0.1 --master-port 29611 tools/ddp_check.py
 
-Each rank trains the real KITTI car model (bf16 perf mode, HIP kernels, ClipAdamW) on its own
-frames for 3 steps under DDP; afterwards every parameter must be bit-identical across ranks (the
-gradient all-reduce and the optimizer see the same averaged gradients) and the losses finite.
-With gloo both ranks may share one GPU (the 1-GPU test box); the 8-GPU bench uses nccl (RCCL)."""
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+        --master-addr 127.0.0.1 --master-port 29611 tools/ddp_check.py     # nccl = RCCL, one rank
+
+Each rank trains the real KITTI 3-class model (the metric's config; RPC_DDP_CLASSES=1 for Car)
+in bf16 perf mode (HIP kernels, ClipAdamW) on its own frames for 3 steps under DDP; afterwards
+every parameter must be bit-identical across ranks (the gradient all-reduce and the optimizer see
+the same averaged gradients) and the losses finite. With gloo several ranks may share one GPU (the
+1-GPU test box); without RPC_DIST_BACKEND the backend is nccl (RCCL), one rank per GPU."""
 import json
 import os
 import sys
@@ -24,12 +28,14 @@ def main():
     rank, world, local = init_distributed()
     dev = torch.device("cuda", torch.cuda.current_device())
     torch.manual_seed(0)
-    model = make_kitti_model(num_classes=1, device=dev, epoch=3)
-    tr = Trainer(model, ddp=world > 1, bf16=True, device=dev)
+    classes = int(os.environ.get("RPC_DDP_CLASSES", "3"))
+    model = make_kitti_model(num_classes=classes, device=dev, epoch=3)
+    tr = Trainer(model, ddp=True, bf16=True, device=dev)
+    assert isinstance(tr.model, torch.nn.parallel.DistributedDataParallel)
     losses = []
     batches = []
     for step in range(3):
-        pts, boxes, labels = kitti_batch(2, seed0=100 * rank + 10 * step, num_classes=1)
+        pts, boxes, labels = kitti_batch(2, seed0=100 * rank + 10 * step, num_classes=classes)
         gb, gl = pack_gt(list(zip(boxes, labels)), dev)
         batches.append(([torch.from_numpy(p).to(dev) for p in pts], dict(gt_boxes=gb, gt_labels=gl)))
     for step in range(3):
@@ -44,10 +50,16 @@ def main():
     allsums = [torch.zeros_like(sums) for _ in range(world)]
     dist.all_gather(allsums, sums)
     same = all(torch.equal(allsums[0], a) for a in allsums)
+    # the collective itself: all_reduce(SUM) of rank+1 over the group's backend
+    probe = torch.full((1 << 20,), float(rank + 1), device=dev)
+    dist.all_reduce(probe)
+    coll_ok = bool((probe == world * (world + 1) / 2).all())
+    same = same and coll_ok
     ok = same and all(torch.isfinite(torch.tensor(l)) for l in losses)
     if rank == 0:
         print(json.dumps(dict(ddp="ok" if ok else "MISMATCH", world=world, backend=dist.get_backend(),
-                              losses=losses, params_identical=same)), flush=True)
+                              classes=classes, losses=losses, params_identical=same, all_reduce_ok=coll_ok)),
+              flush=True)
     dist.barrier()
     dist.destroy_process_group()
     sys.exit(0 if ok else 1)

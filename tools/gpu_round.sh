@@ -15,7 +15,7 @@ step_tests() {
 }
 step_bench() {
   timeout -k 10 300 python -u bench.py --steps 30 --warmup 10 > $OUT/bench.log 2>&1 &&
-  timeout -k 10 200 python -u bench.py --steps 20 --warmup 8 --classes 3 --no-cpu-baseline > $OUT/bench3.log 2>&1
+  timeout -k 10 200 python -u bench.py --steps 20 --warmup 8 --classes 1 --no-cpu-baseline > $OUT/bench_car.log 2>&1
 }
 step_prof() {
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
@@ -31,7 +31,7 @@ step_pmc() {
   python tools/pmc_traffic.py $(find $OUT/pmc_FETCH_SIZE -name '*counter_collection.csv') \
     $(find $OUT/pmc_WRITE_SIZE -name '*counter_collection.csv') $OUT/pmc_traffic.json 40 > $OUT/pmc_traffic.txt 2>&1
 }
-step_tests && echo "tests ok" && { [ "$MODE" = "profonly" ] || { step_bench && echo "bench ok" && tail -1 $OUT/bench.log | cut -c1-400; tail -1 $OUT/bench3.log | cut -c1-300; }; } && step_prof && echo "prof ok" && step_pmc && echo "pmc ok"
+step_tests && echo "tests ok" && { [ "$MODE" = "profonly" ] || { step_bench && echo "bench ok" && tail -1 $OUT/bench.log | cut -c1-400; tail -1 $OUT/bench_car.log | cut -c1-300; }; } && step_prof && echo "prof ok" && step_pmc && echo "pmc ok"
 RC=$?
 KT=$(find $OUT/prof -name '*kernel_trace.csv' | head -1)
 [ -n "$KT" ] && python tools/prof_summary.py $KT --steps 8 --top 60 > $OUT/step_kernels.txt 2>&1

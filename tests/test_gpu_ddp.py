@@ -44,3 +44,20 @@ def test_ddp_rccl_backend_one_rank():
     out = _run(1, backend=None, classes=3)
     assert '"backend": "nccl"' in out, out[-3000:]
     assert '"all_reduce_ok": true' in out, out[-3000:]
+
+
+def test_bench_gpus2_spawns_two_ranks():
+    """bench.py --gpus 2 from a plain `python` starts torch.distributed.run with two ranks (gloo so
+    both share the test box's one GPU) and reports n_gpus = the process-group world size."""
+    import json
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", RPC_DIST_BACKEND="gloo")
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0, out[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2", res
+    assert "3-class" in res["config"]["workload"], res
+    assert res["config"]["dist_backend"] == "gloo"

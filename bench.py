@@ -181,7 +181,8 @@ def main():
     if world != a.gpus:
         print(json.dumps(dict(error=f"--gpus {a.gpus} but the process group has {world} ranks")), flush=True)
         sys.exit(2)
-    dev = torch.device("cuda", local)
+    # init_distributed picked the device (local rank modulo the visible GPUs)
+    dev = torch.device("cuda", torch.cuda.current_device())
     torch.cuda.set_device(dev)
     torch.manual_seed(0)
     nus = a.model == "centerpoint"

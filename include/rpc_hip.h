@@ -262,6 +262,28 @@ typedef struct {
 } RpcDenseWprep;
 int rpc_dense_wprep_batch(const RpcDenseWprep* descs, int n, void* stream);
 
+/* ---- a7 parity mode: the same dense engine with fp32 operands on fp32 MFMA (v_mfma_f32_16x16x4_f32),
+ * fp32 NHWC images; replaces the same upstream Conv2d / ConvTranspose2d + BatchNorm2d + ReLU stacks
+ * (mmdet3d backbones/second.py, necks/second_fpn.py; …-3class.py:25-36) and the Anchor3DHead 1x1 convs
+ * (dense_heads/anchor3d_head.py, …-3class.py:38-45) in fp32, for the 1e-4 detection-loss parity of
+ * north_star. cin % 16 == 0, cout % 64 == 0 (conv); ci, co % 64 == 0 (wgrad); weights from
+ * rpc_dense_wprep_batch_f32 (fp32 [taps][co][ci] / [taps][ci][co]). */
+int rpc_dense_conv_f32(int map, const float* src, int src_pitch, int cin, const float* wt, int cout, float* out,
+                       int out_pitch, int out_offset, int accumulate, float* part, const int* row_img,
+                       const int* src_img, const int* out_img, void* stream);
+int rpc_dense_conv_blocks_f32(int map, const int* row_img);
+size_t rpc_dense_wgrad_workspace_size_f32(int map, const int* row_img, int ci, int co);
+int rpc_dense_wgrad_f32(int map, int kind, const float* x, int x_pitch, int ci, const float* dz, int dz_pitch, int co,
+                        const int* row_img, const int* src_img, const int* out_img, float* dW, void* workspace,
+                        size_t workspace_bytes, void* stream);
+int rpc_dense_bn_apply_f32(const float* z, int m, int c, const float* bn, float* out, int out_pitch, int out_offset,
+                           void* stream);
+int rpc_dense_bnbwd_stats_f32(const float* dh, int dh_pitch, int dh_offset, const float* z, int m, int c,
+                              const float* bn, float* part, void* stream);
+int rpc_dense_bnbwd_apply_f32(const float* dh, int dh_pitch, int dh_offset, const float* z, int m, int c,
+                              const float* bn, const float* bnb, float* dz, void* stream);
+int rpc_dense_wprep_batch_f32(const RpcDenseWprep* descs, int n, void* stream);
+
 
 /* ------------------------------------------------------------------ a8 / §8(f1) Anchor3DHead targets + losses
  * Replaces upstream mmdet3d `Anchor3DHead.loss_by_feat` (dense_heads/anchor3d_head.py) with

@@ -128,6 +128,14 @@ SIGNATURES = {
     "rpc_dense_bnbwd_apply": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
     "rpc_dense_wprep": (i32, [vp, i32, i32, i32, i32, i32, vp, vp, vp]),
     "rpc_dense_wprep_batch": (i32, [vp, i32, vp]),
+    "rpc_dense_conv_f32": (i32, [i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, vp, ip, ip, ip, vp]),
+    "rpc_dense_conv_blocks_f32": (i32, [i32, ip]),
+    "rpc_dense_wgrad_workspace_size_f32": (sz, [i32, ip, i32, i32]),
+    "rpc_dense_wgrad_f32": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, ip, ip, ip, vp, vp, sz, vp]),
+    "rpc_dense_bn_apply_f32": (i32, [vp, i32, i32, vp, vp, i32, i32, vp]),
+    "rpc_dense_bnbwd_stats_f32": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp]),
+    "rpc_dense_bnbwd_apply_f32": (i32, [vp, i32, i32, vp, i32, i32, vp, vp, vp, vp]),
+    "rpc_dense_wprep_batch_f32": (i32, [vp, i32, vp]),
     "rpc_loss_tail_forward": (i32, [vp, vp, C.c_float, vp, vp]),
     "rpc_loss_tail_backward": (i32, [vp, C.c_float, vp, vp, vp, vp]),
     "rpc_clip_adamw_workspace_size": (sz, [i32]),

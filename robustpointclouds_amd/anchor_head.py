@@ -13,9 +13,9 @@ Upstream returns a dict of LISTS (one tensor per feature level, via multi_apply)
 kept (`loss_by_feat`), because AdversarialVoxelNet.loss only sums Tensor-valued entries
 (SURVEY.md finding 3). Target assignment and losses run as HIP kernels (csrc/anchor_head.hip,
 `rpc_anchor_head_loss_forward/backward`) batched over the frames with no host
-synchronisation; the three 1x1 convs run as ONE GEMM — on the bf16 dense engine
-(`rpc_dense_conv` / `rpc_dense_wgrad`, P1 map) in perf mode, through torch's conv in the fp32
-parity mode. The CPU restatement the kernels are checked against is oracle/anchor_head.py.
+synchronisation; the three 1x1 convs run as ONE GEMM on the dense engine (P1 map) — bf16
+(`rpc_dense_conv` / `rpc_dense_wgrad`) in perf mode, fp32 MFMA (`rpc_dense_conv_f32` /
+`rpc_dense_wgrad_f32`) in the fp32 parity mode. The CPU restatement the kernels are checked against is oracle/anchor_head.py.
 mmdet3d is not installed here: parity for this row is "unpinned" w.r.t. upstream.
 """
 from __future__ import annotations
@@ -186,6 +186,70 @@ class HeadConvFn(torch.autograd.Function):
         return dx, dw
 
 
+def head_pad_f32(N: int) -> int:
+    """GEMM width of the fp32 head image: N rounded up to the fp32 engine's 64-channel tile."""
+    return (N + 63) // 64 * 64
+
+
+class HeadConvF32Fn(torch.autograd.Function):
+    """The fused 1x1 head conv (no bias) on the fp32 dense engine (parity mode):
+    x [B, C, H, W] fp32 -> z [B*H*W, NP] fp32, NP = head_pad_f32(N) (channels >= N are zero)."""
+
+    @staticmethod
+    def forward(ctx, x, weight):
+        from .dense_bev import _nhwc
+        lib = _ffi.load()
+        if not x.is_cuda:
+            raise RuntimeError("Anchor3DHead runs on the HIP kernels only (no CPU path)")
+        x = _nhwc(x, torch.float32)
+        B, Cin, H, W = x.shape
+        N = weight.shape[0]
+        NP = head_pad_f32(N)
+        if Cin % 64:
+            raise RuntimeError(f"fp32 HIP head conv needs C_in % 64 == 0 (got {Cin})")
+        dev = x.device
+        st = _ffi.stream_of(x)
+        wp = Fn.pad(weight.detach().reshape(N, Cin).float(), (0, 0, 0, NP - N)).contiguous()
+        wf = torch.empty((1, NP, Cin), dtype=torch.float32, device=dev)
+        wd = torch.empty((1, Cin, NP), dtype=torch.float32, device=dev)
+        desc = (_ffi.RpcDenseWprep * 1)()
+        desc[0] = _ffi.RpcDenseWprep(wp.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, Cin, NP, 1, 0)
+        _ffi.check(lib.rpc_dense_wprep_batch_f32(desc, 1, st), "rpc_dense_wprep_batch_f32(head)")
+        z = torch.empty((B * H * W, NP), dtype=torch.float32, device=dev)
+        img = _ffi.int_arr((B, H, W))
+        _ffi.check(lib.rpc_dense_conv_f32(P1, _ffi.ptr(x), Cin, Cin, _ffi.ptr(wf), NP, _ffi.ptr(z), NP, 0, 0, None,
+                                          img, img, img, st), "rpc_dense_conv_f32(head)")
+        ctx.save_for_backward(x, wd, wp)
+        ctx.N, ctx.NP, ctx.wshape = N, NP, tuple(weight.shape)
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        from .dense_bev import _image
+        lib = _ffi.load()
+        x, wd, _ = ctx.saved_tensors
+        B, Cin, H, W = x.shape
+        NP = ctx.NP
+        dev = x.device
+        dz = dz.float().contiguous()
+        st = _ffi.stream_of(dz)
+        img = _ffi.int_arr((B, H, W))
+        dx = None
+        if ctx.needs_input_grad[0]:
+            dx = _image(B, Cin, H, W, dev, torch.float32)
+            _ffi.check(lib.rpc_dense_conv_f32(P1, _ffi.ptr(dz), NP, NP, _ffi.ptr(wd), Cin, _ffi.ptr(dx), Cin, 0, 0,
+                                              None, img, img, img, st), "rpc_dense_conv_f32(head dgrad)")
+        dw = None
+        if ctx.needs_input_grad[1]:
+            dwp = torch.empty((NP, Cin, 1, 1), dtype=torch.float32, device=dev)
+            wsz = lib.rpc_dense_wgrad_workspace_size_f32(P1, img, Cin, NP)
+            ws = _ffi.workspace(wsz, dev)
+            _ffi.check(lib.rpc_dense_wgrad_f32(P1, 0, _ffi.ptr(x), Cin, Cin, _ffi.ptr(dz), NP, NP, img, img, img,
+                                               _ffi.ptr(dwp), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad_f32(head)")
+            dw = dwp[:ctx.N].reshape(ctx.wshape)
+        return dx, dw
+
+
 class HeadLossFn(torch.autograd.Function):
     """(z, bias) -> [loss_cls, loss_bbox, loss_dir] through rpc_anchor_head_loss_forward/backward."""
 
@@ -302,25 +366,26 @@ class Anchor3DHead(nn.Module):
 
     # ------------------------------------------------------------------ head outputs
     def _z(self, x):
-        """(z, layout, N): the stacked 1x1 conv WITHOUT bias. bf16 input -> the HIP GEMM image
-        [B*H*W, HEAD_PAD]; fp32 input -> torch conv, [B, N, H, W]."""
+        """(z, layout, N): the stacked 1x1 conv WITHOUT bias as the HIP GEMM image [B*H*W, pad]:
+        bf16 input -> the bf16 engine (pad HEAD_PAD); fp32 input -> the fp32 engine (pad
+        head_pad_f32(N))."""
         w, _ = self._stacked()
         N = w.shape[0]
         B, _, H, W = x.shape
+        if not x.is_cuda:
+            raise RuntimeError("Anchor3DHead runs on the HIP kernels only (no CPU path)")
         if x.dtype == torch.bfloat16:
             z = HeadConvFn.apply(x, w)
             return z, dict(B=B, H=H, W=W, bf16=1, sb=H * W * HEAD_PAD, shw=HEAD_PAD, sn=1, nwrite=HEAD_PAD), N
+        NP = head_pad_f32(N)
         with torch.autocast("cuda", enabled=False):
-            z = Fn.conv2d(x.float(), w.float()).contiguous()
-        return z, dict(B=B, H=H, W=W, bf16=0, sb=N * H * W, shw=1, sn=H * W, nwrite=N), N
+            z = HeadConvF32Fn.apply(x.float(), w.float())
+        return z, dict(B=B, H=H, W=W, bf16=0, sb=H * W * NP, shw=NP, sn=1, nwrite=NP), N
 
     def forward_single(self, x):
         z, lay, N = self._z(x)
         _, b = self._stacked()
-        if lay["bf16"]:
-            y = (z[:, :N].float() + b.float()).view(lay["B"], lay["H"], lay["W"], N).permute(0, 3, 1, 2)
-        else:
-            y = z + b.view(1, -1, 1, 1)
+        y = (z[:, :N].float() + b.float()).view(lay["B"], lay["H"], lay["W"], N).permute(0, 3, 1, 2)
         A = self.num_anchors
         outs = torch.split(y, [A * self.num_classes, A * 7] + ([A * 2] if self.use_direction_classifier else []),
                            dim=1)

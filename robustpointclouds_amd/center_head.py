@@ -260,7 +260,7 @@ class CenterHeadFn(torch.autograd.Function):
         hm = torch.empty((cells, head.hm_pitch), dtype=torch.float32, device=dev)
         box = torch.empty((cells, head.box_pitch), dtype=torch.float32, device=dev)
         Lsh = _conv_module_layer(head.shared_conv)
-        y0, rsh, _, _ = db._forward_layer(lib, Lsh, xi, Cin, B, H, W, training, dev, st)
+        y0, rsh, _, _ = db._forward_layer(db._Eng(lib, False), Lsh, xi, Cin, B, H, W, training, dev, st)
         bns = [head.shared_conv.bn]
         trecs = []
         c0 = 0
@@ -279,7 +279,7 @@ class CenterHeadFn(torch.autograd.Function):
                 tr[br] = dict(dcn=dcn, oz=oz, orec=orec, wd=wdd, ob=ob, feat=feat)
             # cls branch -> heatmap logits
             L = _conv_module_layer(th.cls_head[0])
-            hcls, rc, _, _ = db._forward_layer(lib, L, tr["cls"]["feat"], 64, B, H, W, training, dev, st)
+            hcls, rc, _, _ = db._forward_layer(db._Eng(lib, False), L, tr["cls"]["feat"], 64, B, H, W, training, dev, st)
             bns.append(th.cls_head[0].bn)
             fc = th.cls_head[1]
             z, frec = _conv_nobn_fwd(lib, fc.weight, 64, hcls, 64, B, H, W, dev, st)
@@ -292,7 +292,7 @@ class CenterHeadFn(torch.autograd.Function):
             for name in _BOX_ORDER:
                 seq = getattr(th.task_head, name)
                 L = _conv_module_layer(seq[0])
-                hr, rr, _, _ = db._forward_layer(lib, L, tr["reg"]["feat"], 64, B, H, W, training, dev, st)
+                hr, rr, _, _ = db._forward_layer(db._Eng(lib, False), L, tr["reg"]["feat"], 64, B, H, W, training, dev, st)
                 bns.append(seq[0].bn)
                 fcv = seq[1]
                 n = fcv.weight.shape[0]
@@ -337,7 +337,7 @@ class CenterHeadFn(torch.autograd.Function):
                                                 _ffi.ptr(uws), uwsz, st), "rpc_head_unpack_grad")
             dh, dW = _conv_nobn_bwd(lib, frec, dz, dev, st)
             grads[id(conv.weight)], grads[id(conv.bias)] = dW, db_
-            dfeat, dWc, dg, dbt = db._backward_layer(lib, rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
+            dfeat, dWc, dg, dbt = db._backward_layer(db._Eng(lib, False), rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
             L = rec_cm["L"]
             grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWc, dg, dbt
             return dfeat
@@ -365,7 +365,7 @@ class CenterHeadFn(torch.autograd.Function):
                 grads[id(dcn.conv_offset.weight)] = dWo
         dY0 = (dY0f + dY0b.permute(0, 2, 3, 1).reshape(cells, 64).float()).to(torch.bfloat16)
         dY0 = dY0.view(B, H, W, 64).permute(0, 3, 1, 2)
-        dx, dWs, dgs, dbs = db._backward_layer(lib, ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
+        dx, dWs, dgs, dbs = db._backward_layer(db._Eng(lib, False), ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
         L = ctx.rsh["L"]
         grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWs, dgs, dbs
         ctx.trecs = ctx.rsh = None

@@ -28,6 +28,7 @@
 #include <string.h>
 
 #include "common.h"
+#include "dense_common.h"
 #include "rpc_hip.h"
 
 namespace rpc {
@@ -45,19 +46,9 @@ typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 typedef unsigned short u16;
 
-struct Img {
-  int B, H, W;
-};
-
 // M_D2P (internal): the data gradient of S2 split by input-pixel parity (blockIdx.z = 2*py + px):
 // a pixel of parity (py, px) receives only the taps ty in {1} (py = 0) or {0, 2} (py = 1), and
 // likewise tx, so the four classes run 1, 2, 2 and 4 taps instead of 9 taps of mostly zero rows
-enum { M_S1 = 0, M_S2 = 1, M_D2 = 2, M_P1 = 3, M_U2 = 4, M_G2 = 5, M_D2P = 6 };
-
-template <int MAP>
-__host__ __device__ constexpr int taps_of() {
-  return (MAP == M_P1 || MAP == M_U2) ? 1 : ((MAP == M_G2 || MAP == M_D2P) ? 4 : 9);
-}
 
 // tap j < ntaps of parity (py, px) of M_D2P -> 3x3 tap index
 __device__ __forceinline__ int d2p_tap(int j, int py, int px) {
@@ -65,53 +56,9 @@ __device__ __forceinline__ int d2p_tap(int j, int py, int px) {
   const int ty = py ? 2 * (j / ntx) : 1, tx = px ? 2 * (j % ntx) : 1;
   return ty * 3 + tx;
 }
-// weight-gradient "taps": U2 has one GEMM per output parity, each with its own weight slice
-template <int MAP>
-__host__ __device__ constexpr int wtaps_of() {
-  return MAP == M_U2 ? 4 : taps_of<MAP>();
-}
 
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
 __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float((unsigned)h << 16); }
-
-// K-operand source pixel of GEMM row pixel (b, y, x) for tap t in image S (-1: zero row)
-template <int MAP>
-__device__ __forceinline__ int src_row(int b, int y, int x, int t, const Img& S) {
-  int sy, sx;
-  if (MAP == M_S1) {
-    sy = y + t / 3 - 1;
-    sx = x + t % 3 - 1;
-  } else if (MAP == M_S2) {
-    sy = 2 * y + t / 3 - 1;
-    sx = 2 * x + t % 3 - 1;
-  } else if (MAP == M_D2) {
-    const int oy = y + 1 - t / 3, ox = x + 1 - t % 3;
-    if ((oy | ox) < 0 || ((oy | ox) & 1)) return -1;
-    sy = oy >> 1;
-    sx = ox >> 1;
-  } else if (MAP == M_G2) {
-    sy = 2 * y + (t >> 1);
-    sx = 2 * x + (t & 1);
-  } else {
-    sy = y;
-    sx = x;
-  }
-  if (sy < 0 || sy >= S.H || sx < 0 || sx >= S.W) return -1;
-  return (b * S.H + sy) * S.W + sx;
-}
-
-// output pixel of GEMM row m = (b, y, x) (U2: parity par of the 2x upsampled image O)
-template <int MAP>
-__device__ __forceinline__ int out_row(int m, int b, int y, int x, int par, const Img& O) {
-  if (MAP == M_U2) return (b * O.H + 2 * y + (par >> 1)) * O.W + 2 * x + (par & 1);
-  return m;
-}
-
-// bijective XCD-aware remap of a 1-D block index (consecutive tiles -> the same XCD's L2)
-__device__ __forceinline__ int xcd_remap(int bid, int nwg) {
-  const int xcd = bid & 7, q = nwg >> 3, r = nwg & 7;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-}
 
 // ------------------------------------------------------------------ implicit GEMM (fwd / dgrad)
 struct IG {
@@ -663,11 +610,38 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
 // Every pass maps a 256-thread block to (256 / CG) row lanes x CG channel groups of 8 (CG = C / 8),
 // so a thread keeps its 8 channels' BatchNorm parameters in registers for all of its rows, and
 // walks rows strided over the grid with RU rows per iteration (RU 16-byte loads per stream in flight).
+// The element type E is u16 (bf16 images, perf mode) or float (fp32 images, parity mode): 8 channels
+// are one 16-byte load of bf16 or two of fp32.
 constexpr int RU = 4;
 
-// h = relu((z - mean) * scale + beta) -> bf16 image rows at (OP, OOFF); bn = scale, beta, mean, invstd
-__global__ __launch_bounds__(BLK) void k_bn_apply(const u16* __restrict__ z, int M, int C, const float* __restrict__ bn,
-                                                  u16* __restrict__ out, int OP, int OOFF) {
+template <typename E>
+struct Raw8 {
+  uint4 u[sizeof(E) / 2];
+};
+template <typename E>
+__device__ __forceinline__ Raw8<E> ld8(const E* p) {
+  Raw8<E> r;
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(E) / 2); ++k) r.u[k] = ((const uint4*)p)[k];
+  return r;
+}
+__device__ __forceinline__ float el(const Raw8<u16>& r, int j) { return bf2f(((const u16*)r.u)[j]); }
+__device__ __forceinline__ float el(const Raw8<float>& r, int j) { return ((const float*)r.u)[j]; }
+__device__ __forceinline__ void st8(u16* p, const float* v) {
+  u16 o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = f2bf(v[j]);
+  *(uint4*)p = *(uint4*)o;
+}
+__device__ __forceinline__ void st8(float* p, const float* v) {
+  ((float4*)p)[0] = make_float4(v[0], v[1], v[2], v[3]);
+  ((float4*)p)[1] = make_float4(v[4], v[5], v[6], v[7]);
+}
+
+// h = relu((z - mean) * scale + beta) -> image rows at (OP, OOFF); bn = scale, beta, mean, invstd
+template <typename E>
+__global__ __launch_bounds__(BLK) void k_bn_apply(const E* __restrict__ z, int M, int C, const float* __restrict__ bn,
+                                                  E* __restrict__ out, int OP, int OOFF) {
   const int CG = C >> 3, RL = BLK / CG;
   const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
   if (rl >= RL) return;
@@ -681,28 +655,28 @@ __global__ __launch_bounds__(BLK) void k_bn_apply(const u16* __restrict__ z, int
   }
   const int step = gridDim.x * RL;
   for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
-    uint4 v[RU];
+    Raw8<E> v[RU];
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int m = m0 + u * step;
-      if (m < M) v[u] = *(const uint4*)(z + (size_t)m * C + cg * 8);
+      if (m < M) v[u] = ld8(z + (size_t)m * C + cg * 8);
     }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int m = m0 + u * step;
       if (m >= M) continue;
-      const u16* e = (const u16*)&v[u];
-      u16 o[8];
+      float o[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(fmaxf(fmaf(bf2f(e[j]) - mu[j], sc[j], sh[j]), 0.0f));
-      *(uint4*)(out + (size_t)m * OP + OOFF + cg * 8) = *(uint4*)o;
+      for (int j = 0; j < 8; ++j) o[j] = fmaxf(fmaf(el(v[u], j) - mu[j], sc[j], sh[j]), 0.0f);
+      st8(out + (size_t)m * OP + OOFF + cg * 8, o);
     }
   }
 }
 
 // BatchNorm-backward partial sums: dm = dh * [pre > 0]; part[blk] = (sum dm, sum dm * xhat)
-__global__ __launch_bounds__(BLK) void k_bnbwd_stats(const u16* __restrict__ dh, int DP, int DOFF,
-                                                     const u16* __restrict__ z, int M, int C,
+template <typename E>
+__global__ __launch_bounds__(BLK) void k_bnbwd_stats(const E* __restrict__ dh, int DP, int DOFF,
+                                                     const E* __restrict__ z, int M, int C,
                                                      const float* __restrict__ bn, float* __restrict__ part) {
   __shared__ float sh[2][BLK * 8];
   const int CG = C >> 3, RL = BLK / CG;
@@ -722,25 +696,23 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const u16* __restrict__ dh,
     }
     const int step = gridDim.x * RL;
     for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
-      uint4 dv[RU], zv[RU];
+      Raw8<E> dv[RU], zv[RU];
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         const int m = m0 + u * step;
         if (m < M) {
-          dv[u] = *(const uint4*)(dh + (size_t)m * DP + DOFF + cg * 8);
-          zv[u] = *(const uint4*)(z + (size_t)m * C + cg * 8);
+          dv[u] = ld8(dh + (size_t)m * DP + DOFF + cg * 8);
+          zv[u] = ld8(z + (size_t)m * C + cg * 8);
         }
       }
 #pragma unroll
       for (int u = 0; u < RU; ++u) {
         if (m0 + u * step >= M) continue;
-        const u16* de = (const u16*)&dv[u];
-        const u16* ze = (const u16*)&zv[u];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float zz = bf2f(ze[j]);
+          const float zz = el(zv[u], j);
           const float pre = fmaf(zz - mu[j], sc[j], be[j]);
-          const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
+          const float d = pre > 0.f ? el(dv[u], j) : 0.f;
           s1[j] += d;
           s2[j] += d * ((zz - mu[j]) * is[j]);
         }
@@ -766,11 +738,12 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const u16* __restrict__ dh,
   }
 }
 
-// dz = gi * (dm - m1 - xhat * m2) -> bf16 [M][C]; bnb = gi, m1, m2, mean, invstd; bn = forward
-__global__ __launch_bounds__(BLK) void k_bnbwd_apply(const u16* __restrict__ dh, int DP, int DOFF,
-                                                     const u16* __restrict__ z, int M, int C,
+// dz = gi * (dm - m1 - xhat * m2) -> [M][C]; bnb = gi, m1, m2, mean, invstd; bn = forward
+template <typename E>
+__global__ __launch_bounds__(BLK) void k_bnbwd_apply(const E* __restrict__ dh, int DP, int DOFF,
+                                                     const E* __restrict__ z, int M, int C,
                                                      const float* __restrict__ bn, const float* __restrict__ bnb,
-                                                     u16* __restrict__ dz) {
+                                                     E* __restrict__ dz) {
   const int CG = C >> 3, RL = BLK / CG;
   const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
   if (rl >= RL) return;
@@ -789,31 +762,29 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_apply(const u16* __restrict__ dh,
   }
   const int step = gridDim.x * RL;
   for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
-    uint4 dv[RU], zv[RU];
+    Raw8<E> dv[RU], zv[RU];
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int m = m0 + u * step;
       if (m < M) {
-        dv[u] = *(const uint4*)(dh + (size_t)m * DP + DOFF + cg * 8);
-        zv[u] = *(const uint4*)(z + (size_t)m * C + cg * 8);
+        dv[u] = ld8(dh + (size_t)m * DP + DOFF + cg * 8);
+        zv[u] = ld8(z + (size_t)m * C + cg * 8);
       }
     }
 #pragma unroll
     for (int u = 0; u < RU; ++u) {
       const int m = m0 + u * step;
       if (m >= M) continue;
-      const u16* de = (const u16*)&dv[u];
-      const u16* ze = (const u16*)&zv[u];
-      u16 o[8];
+      float o[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
-        const float zz = bf2f(ze[j]);
+        const float zz = el(zv[u], j);
         const float pre = fmaf(zz - mu[j], sc[j], be[j]);
-        const float d = pre > 0.f ? bf2f(de[j]) : 0.f;
+        const float d = pre > 0.f ? el(dv[u], j) : 0.f;
         const float xh = (zz - mb[j]) * ib[j];
-        o[j] = f2bf(gi[j] * (d - m1[j] - xh * m2[j]));
+        o[j] = gi[j] * (d - m1[j] - xh * m2[j]);
       }
-      *(uint4*)(dz + (size_t)m * C + cg * 8) = *(uint4*)o;
+      st8(dz + (size_t)m * C + cg * 8, o);
     }
   }
 }
@@ -852,39 +823,6 @@ __global__ __launch_bounds__(BLK) void k_wprep_batch(WprepBatch b) {
     wprep_elem(e, d.W, d.kind, d.ci, d.co, d.taps, d.flip, (u16*)d.w_fwd, (u16*)d.w_dgrad);
 }
 
-// fixed-order chunk reduction (4 interleaved lanes, as k_slab_reduce before its 8-lane form) fused with the store to torch layout
-// (kind 0: [co][ci][t], kind 1: [ci][co][t]): the reduced [T][CI][CO] element goes straight to dW
-__global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ part, int chunks, int kind, int CI,
-                                                      int CO, int T, float* __restrict__ dW) {
-  __shared__ double sh[4][64];
-  const long long total = (long long)T * CI * CO;
-  const int o = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const long long e = (long long)blockIdx.x * 64 + o;
-  double s = 0.0;
-  if (e < total) {
-    int c = q;
-    for (; c + 12 < chunks; c += 16) {
-      float a0 = part[(long long)c * total + e], a1 = part[(long long)(c + 4) * total + e];
-      float a2 = part[(long long)(c + 8) * total + e], a3 = part[(long long)(c + 12) * total + e];
-      s += (double)a0;
-      s += (double)a1;
-      s += (double)a2;
-      s += (double)a3;
-    }
-    for (; c < chunks; c += 4) s += (double)part[(long long)c * total + e];
-  }
-  sh[q][o] = s;
-  __syncthreads();
-  if (q != 0 || e >= total) return;
-  const float v = (float)(((sh[0][o] + sh[1][o]) + sh[2][o]) + sh[3][o]);
-  const int t = (int)(e / ((long long)CI * CO));
-  const int rem = (int)(e - (long long)t * CI * CO), ci = rem / CO, co = rem - ci * CO;
-  if (kind == 0) dW[((size_t)co * CI + ci) * T + t] = v;
-  else dW[((size_t)ci * CO + co) * T + t] = v;
-}
-
-static inline unsigned cdivu(long long a, long long b) { return (unsigned)((a + b - 1) / b); }
-
 template <int MAP>
 static void launch_igemm(const IG& g, int par_count, hipStream_t st) {
   // M_D2P: grid over the largest parity class (even rows, even columns)
@@ -902,28 +840,6 @@ static void launch_wgrad(const WG& g, int chunks, hipStream_t st) {
     dim3 grid(chunks * wtaps_of<MAP>() * (g.CI / 64) * (g.CO / 64));
     hipLaunchKernelGGL((k_wgrad<MAP, 1>), grid, dim3(BLK), 0, st, g);
   }
-}
-
-static int map_wtaps(int map) {
-  switch (map) {
-    case M_P1: return 1;
-    case M_U2:
-    case M_G2: return 4;
-    default: return 9;
-  }
-}
-
-// Row chunks of the weight gradient: the grid (chunks x taps x channel tiles) is sized to fill the
-// resident block slots of the chip in whole rounds (k_wgrad: 3 blocks per CU), chunks <= 4096 rows.
-static int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) !=
-                                                 hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
 }
 
 static int wgrad_chunks(int M, int T, int ci, int co) {
@@ -1023,18 +939,40 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
     default: launch_wgrad<M_U2>(g, chunks, st); break;
   }
   RPC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_wgrad_reduce, dim3(cdivu(slab, 64)), dim3(256), 0, st, (const float*)part, chunks, kind, ci, co,
+  hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(cdivu(slab, 64)), dim3(256), 0, st, (const float*)part, chunks, kind, ci, co,
                      T, dW);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
 
-extern "C" int rpc_dense_bn_apply(const void* z, int m, int c, const float* bn, void* out, int op, int ooff,
-                                  void* stream) {
+template <typename E>
+static int bn_apply(const void* z, int m, int c, const float* bn, void* out, int op, int ooff, void* stream) {
   if (m < 0 || c < 8 || c > 2048 || (c & 7) || (op & 7) || (ooff & 7) || op < ooff + c) return RPC_ERR_ARG;
   if (m == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_bn_apply, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
-                     (const u16*)z, m, c, bn, (u16*)out, op, ooff);
+  hipLaunchKernelGGL(k_bn_apply<E>, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
+                     (const E*)z, m, c, bn, (E*)out, op, ooff);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+template <typename E>
+static int bnbwd_stats(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn, float* part,
+                       void* stream) {
+  if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
+  const int nb = rpc_dense_bnbwd_blocks(m);
+  hipLaunchKernelGGL(k_bnbwd_stats<E>, dim3(nb), dim3(BLK), 0, (hipStream_t)stream, (const E*)dh, dp, doff,
+                     (const E*)z, m, c, bn, part);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+template <typename E>
+static int bnbwd_apply(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
+                       const float* bnb, void* dz, void* stream) {
+  if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
+  if (m == 0) return RPC_OK;
+  hipLaunchKernelGGL(k_bnbwd_apply<E>, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
+                     (const E*)dh, dp, doff, (const E*)z, m, c, bn, bnb, (E*)dz);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
@@ -1044,24 +982,29 @@ extern "C" int rpc_dense_bnbwd_blocks(int m) {
   return b < 1 ? 1 : (b > 2048 ? 2048 : b);
 }
 
+extern "C" int rpc_dense_bn_apply(const void* z, int m, int c, const float* bn, void* out, int op, int ooff,
+                                  void* stream) {
+  return bn_apply<u16>(z, m, c, bn, out, op, ooff, stream);
+}
+extern "C" int rpc_dense_bn_apply_f32(const float* z, int m, int c, const float* bn, float* out, int op, int ooff,
+                                      void* stream) {
+  return bn_apply<float>(z, m, c, bn, out, op, ooff, stream);
+}
 extern "C" int rpc_dense_bnbwd_stats(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
                                      float* part, void* stream) {
-  if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
-  const int nb = rpc_dense_bnbwd_blocks(m);
-  hipLaunchKernelGGL(k_bnbwd_stats, dim3(nb), dim3(BLK), 0, (hipStream_t)stream, (const u16*)dh, dp, doff,
-                     (const u16*)z, m, c, bn, part);
-  RPC_LAUNCH_CHECK();
-  return RPC_OK;
+  return bnbwd_stats<u16>(dh, dp, doff, z, m, c, bn, part, stream);
 }
-
+extern "C" int rpc_dense_bnbwd_stats_f32(const float* dh, int dp, int doff, const float* z, int m, int c,
+                                         const float* bn, float* part, void* stream) {
+  return bnbwd_stats<float>(dh, dp, doff, z, m, c, bn, part, stream);
+}
 extern "C" int rpc_dense_bnbwd_apply(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
                                      const float* bnb, void* dz, void* stream) {
-  if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
-  if (m == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_bnbwd_apply, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
-                     (const u16*)dh, dp, doff, (const u16*)z, m, c, bn, bnb, (u16*)dz);
-  RPC_LAUNCH_CHECK();
-  return RPC_OK;
+  return bnbwd_apply<u16>(dh, dp, doff, z, m, c, bn, bnb, dz, stream);
+}
+extern "C" int rpc_dense_bnbwd_apply_f32(const float* dh, int dp, int doff, const float* z, int m, int c,
+                                         const float* bn, const float* bnb, float* dz, void* stream) {
+  return bnbwd_apply<float>(dh, dp, doff, z, m, c, bn, bnb, dz, stream);
 }
 
 extern "C" int rpc_dense_wprep_batch(const RpcDenseWprep* descs, int n, void* stream) {

@@ -12,10 +12,11 @@ become ONE autograd node over csrc/dense_conv.hip (C-ABI `rpc_dense_*`):
   rpc_dense_bnbwd_apply (dz) -> rpc_dense_wgrad (dW, fp32) -> rpc_dense_conv (data gradient:
   flipped-tap S1, D2 for the stride-2 layer, P1 / G2 for the deconvolutions)
 
-Activations are bf16 channels_last (fp32 accumulation, fp32 BatchNorm statistics); weights stay
-fp32 master copies (cast to bf16 GEMM operands per step). The module parameters and state-dict
-keys are the torch modules' own (second.py), so the two paths are interchangeable; the torch path
-remains the fp32 parity mode.
+Perf mode: activations bf16 channels_last (fp32 accumulation, fp32 BatchNorm statistics); weights
+stay fp32 master copies (cast to bf16 GEMM operands per step). Parity mode (fp32 input): the same
+node over the fp32 engine (csrc/dense_f32.hip, `rpc_dense_*_f32`: fp32 operands on fp32 MFMA,
+fp32 NHWC images) — the engine follows the dtype of the image handed in. The module parameters
+and state-dict keys are the torch modules' own (second.py).
 """
 from __future__ import annotations
 
@@ -78,16 +79,56 @@ def _ffi_img_rows(arr):
     return int(arr[0]) * int(arr[1]) * int(arr[2])
 
 
-def _nhwc(t: torch.Tensor) -> torch.Tensor:
-    """[B, C, H, W] -> a bf16 channels_last tensor (its storage is the NHWC image)."""
-    t = t.to(torch.bfloat16)
+def _nhwc(t: torch.Tensor, dt=torch.bfloat16) -> torch.Tensor:
+    """[B, C, H, W] -> a channels_last tensor of dtype dt (its storage is the NHWC image)."""
+    t = t.to(dt)
     if not t.is_contiguous(memory_format=torch.channels_last):
         t = t.contiguous(memory_format=torch.channels_last)
     return t
 
 
-def _image(B, C, H, W, dev):
-    return torch.empty((B, H, W, C), dtype=torch.bfloat16, device=dev).permute(0, 3, 1, 2)
+def _image(B, C, H, W, dev, dt=torch.bfloat16):
+    return torch.empty((B, H, W, C), dtype=dt, device=dev).permute(0, 3, 1, 2)
+
+
+class _Eng:
+    """The C-ABI entry points of one engine: bf16 (perf mode) or fp32 (parity mode)."""
+
+    def __init__(self, lib, f32: bool):
+        self.f32 = f32
+        self.dt = torch.float32 if f32 else torch.bfloat16
+        x = "_f32" if f32 else ""
+        self.conv_raw = getattr(lib, "rpc_dense_conv" + x)
+        self.blocks = getattr(lib, "rpc_dense_conv_blocks" + x)
+        self.wgrad = getattr(lib, "rpc_dense_wgrad" + x)
+        self.wgrad_ws = getattr(lib, "rpc_dense_wgrad_workspace_size" + x)
+        self.bn_apply = getattr(lib, "rpc_dense_bn_apply" + x)
+        self.bnbwd_stats = getattr(lib, "rpc_dense_bnbwd_stats" + x)
+        self.bnbwd_apply = getattr(lib, "rpc_dense_bnbwd_apply" + x)
+        self.wprep_batch = getattr(lib, "rpc_dense_wprep_batch" + x)
+        self.lib = lib
+
+    def conv(self, fmap, *args):
+        if self.f32:
+            return self.conv_raw(fmap, *args)
+        return _conv(self.lib, fmap, *args)
+
+    def check_widths(self, layers):
+        for L in layers:
+            if self.f32:
+                if L.ci % 16 or L.co % 64:
+                    raise RuntimeError(f"fp32 HIP dense conv needs C_in % 16 == 0 and C_out % 64 == 0 "
+                                       f"(got {L.ci}->{L.co})")
+            elif L.ci % 128 or L.co % 128:
+                raise RuntimeError(f"HIP dense conv needs channel counts that are multiples of 128 (got {L.ci}->{L.co})")
+
+
+def _engine(lib, t: torch.Tensor) -> _Eng:
+    if not t.is_cuda:
+        raise RuntimeError("the dense BEV engine runs on the HIP kernels only: got a CPU tensor")
+    if t.dtype not in (torch.float32, torch.bfloat16):
+        raise RuntimeError(f"dense BEV engine: fp32 (parity) or bf16 (perf) images, got {t.dtype}")
+    return _Eng(lib, t.dtype == torch.float32)
 
 
 def _bn_eval(bnm, dev):
@@ -116,9 +157,9 @@ class _Layer:
         return {S1: S1, S2: D2, P1: P1, U2: G2}[self.map]
 
 
-def _prep_weights(lib, layers, dev, st):
-    """bf16 GEMM operands (forward [T][co][ci], data gradient [T][ci][co]) of every layer of a module
-    from the fp32 master weights, in one rpc_dense_wprep_batch launch."""
+def _prep_weights(eng, layers, dev, st):
+    """GEMM operands (forward [T][co][ci], data gradient [T][ci][co]; bf16 or fp32 by engine) of every
+    layer of a module from the fp32 master weights, in one rpc_dense_wprep_batch(_f32) launch."""
     out = []
     for g0 in range(0, len(layers), 16):   # the kernel takes up to 16 layers per launch
         group = layers[g0:g0 + 16]
@@ -127,31 +168,32 @@ def _prep_weights(lib, layers, dev, st):
         for i, L in enumerate(group):
             W32 = L.conv.weight.detach().float().contiguous()
             keep.append(W32)
-            wf = torch.empty((L.taps, L.co, L.ci), dtype=torch.bfloat16, device=dev)
-            wd = torch.empty((L.taps, L.ci, L.co), dtype=torch.bfloat16, device=dev)
+            wf = torch.empty((L.taps, L.co, L.ci), dtype=eng.dt, device=dev)
+            wd = torch.empty((L.taps, L.ci, L.co), dtype=eng.dt, device=dev)
             descs[i] = _ffi.RpcDenseWprep(W32.data_ptr(), wf.data_ptr(), wd.data_ptr(), L.kind, L.ci, L.co,
                                           L.taps, 1 if L.map == S1 else 0)
             out.append((wf, wd))
-        _ffi.check(lib.rpc_dense_wprep_batch(descs, len(group), st), "rpc_dense_wprep_batch")
+        _ffi.check(eng.wprep_batch(descs, len(group), st), "rpc_dense_wprep_batch")
     return out
 
 
-def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_pitch=None, out_off=0, wts=None):
+def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_pitch=None, out_off=0, wts=None):
     """z = conv(h); BN (batch or running stats); y = relu(bn(z)) -> (y image, record).
     wts: (forward, data-gradient) bf16 operands from _prep_weights, else prepared here."""
     R, S, O, Ho, Wo = L.images(B, H, W)
+    lib = eng.lib
     if wts is None:
-        wts = _prep_weights(lib, [L], dev, st)[0]
+        wts = _prep_weights(eng, [L], dev, st)[0]
     wf, wd = wts
     Mo = B * Ho * Wo
-    z = torch.empty((Mo, L.co), dtype=torch.bfloat16, device=dev)
+    z = torch.empty((Mo, L.co), dtype=eng.dt, device=dev)
     ri, si, oi = _ffi.int_arr(R), _ffi.int_arr(S), _ffi.int_arr(O)
     part = None
     if training:
-        nblk = lib.rpc_dense_conv_blocks(L.map, ri)
+        nblk = eng.blocks(L.map, ri)
         part = torch.empty((nblk, 2 * L.co), dtype=torch.float32, device=dev)
-    _ffi.check(_conv(lib, L.map, _ffi.ptr(h), pitch, L.ci, _ffi.ptr(wf), L.co, _ffi.ptr(z), L.co, 0, 0,
-                                  _ffi.ptr(part), ri, si, oi, st), "rpc_dense_conv")
+    _ffi.check(eng.conv(L.map, _ffi.ptr(h), pitch, L.ci, _ffi.ptr(wf), L.co, _ffi.ptr(z), L.co, 0, 0,
+                        _ffi.ptr(part), ri, si, oi, st), "rpc_dense_conv")
     bnm = L.bnm
     if training:
         bn = torch.empty(4 * L.co, dtype=torch.float32, device=dev)
@@ -162,23 +204,24 @@ def _forward_layer(lib, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
     else:
         bn = _bn_eval(bnm, dev)
     if out is None:
-        y = _image(B, L.co, Ho, Wo, dev)
+        y = _image(B, L.co, Ho, Wo, dev, eng.dt)
         out_pitch, out_off = L.co, 0
     else:
         y = out
-    _ffi.check(lib.rpc_dense_bn_apply(_ffi.ptr(z), Mo, L.co, _ffi.ptr(bn), _ffi.ptr(y), out_pitch, out_off, st),
+    _ffi.check(eng.bn_apply(_ffi.ptr(z), Mo, L.co, _ffi.ptr(bn), _ffi.ptr(y), out_pitch, out_off, st),
                "rpc_dense_bn_apply")
     rec = dict(L=L, h=h, pitch=pitch, z=z, bn=bn, wd=wd, R=R, S=S, O=O, in_hw=(H, W), Mo=Mo)
     return y, rec, Ho, Wo
 
 
-def _backward_layer(lib, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False):
+def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False):
     """BN+ReLU backward, weight gradient and (optionally) data gradient of one layer."""
+    lib = eng.lib
     L = rec["L"]
     Mo, co, ci = rec["Mo"], L.co, L.ci
     nb = lib.rpc_dense_bnbwd_blocks(Mo)
     part = torch.empty((nb, 2 * co), dtype=torch.float32, device=dev)
-    _ffi.check(lib.rpc_dense_bnbwd_stats(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
+    _ffi.check(eng.bnbwd_stats(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
                                          _ffi.ptr(rec["bn"]), _ffi.ptr(part), st), "rpc_dense_bnbwd_stats")
     bnb = torch.empty(5 * co, dtype=torch.float32, device=dev)
     dgamma = torch.empty(co, dtype=torch.float32, device=dev)
@@ -186,32 +229,32 @@ def _backward_layer(lib, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
     _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nb, co, Mo, 1, _ffi.ptr(L.bnm.weight), _ffi.ptr(L.bnm.bias),
                                    0.0, 0.0, None, None, _ffi.ptr(rec["bn"]), _ffi.ptr(bnb), _ffi.ptr(dgamma),
                                    _ffi.ptr(dbeta), None, st), "rpc_bn_finalize(bwd)")
-    dz = torch.empty((Mo, co), dtype=torch.bfloat16, device=dev)
-    _ffi.check(lib.rpc_dense_bnbwd_apply(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
+    dz = torch.empty((Mo, co), dtype=eng.dt, device=dev)
+    _ffi.check(eng.bnbwd_apply(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
                                          _ffi.ptr(rec["bn"]), _ffi.ptr(bnb), _ffi.ptr(dz), st),
                "rpc_dense_bnbwd_apply")
     ri, si, oi = _ffi.int_arr(rec["R"]), _ffi.int_arr(rec["S"]), _ffi.int_arr(rec["O"])
     # torch-contiguous layout (the kernel writes [co][ci][kh][kw] / [ci][co][kh][kw] densely), even when
     # the module was converted to channels_last
     dW = torch.empty(tuple(L.conv.weight.shape), dtype=torch.float32, device=dev)
-    wsz = lib.rpc_dense_wgrad_workspace_size(L.map, ri, ci, co)
+    wsz = eng.wgrad_ws(L.map, ri, ci, co)
     ws = _ffi.workspace(wsz, dev)
     # the U2 weight-gradient GEMM reads dz at the output rows; the others read it at the GEMM rows
-    _ffi.check(lib.rpc_dense_wgrad(L.map, L.kind, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), co, co,
+    _ffi.check(eng.wgrad(L.map, L.kind, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), co, co,
                                    ri, si, oi, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
     dx = None
     if need_dx:
         dmap = L.dgrad_map()
         B, H, W = rec["S"]
-        dx = dx_out if dx_out is not None else _image(B, ci, H, W, dev)
+        dx = dx_out if dx_out is not None else _image(B, ci, H, W, dev, eng.dt)
         # data gradient GEMM: rows = forward source pixels, source image = forward output image
         if L.map == U2:
             rd, sd = rec["R"], rec["O"]
         else:
             rd, sd = rec["S"], rec["O"]
-        _ffi.check(_conv(lib, dmap, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
-                                      1 if accumulate else 0, None, _ffi.int_arr(rd), _ffi.int_arr(sd),
-                                      _ffi.int_arr(rd), st), "rpc_dense_conv(dgrad)")
+        _ffi.check(eng.conv(dmap, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
+                            1 if accumulate else 0, None, _ffi.int_arr(rd), _ffi.int_arr(sd),
+                            _ffi.int_arr(rd), st), "rpc_dense_conv(dgrad)")
     return dx, dW, dgamma, dbeta
 
 
@@ -243,32 +286,26 @@ def fpn_layers(mod):
     return out
 
 
-def _check_widths(layers):
-    for L in layers:
-        if L.ci % 128 or L.co % 128:
-            raise RuntimeError(f"HIP dense conv needs channel counts that are multiples of 128 (got {L.ci}->{L.co})")
-
-
 class BackboneFn(torch.autograd.Function):
     """SECOND forward/backward as one node: x [B, Cin, H, W] -> tuple of block outputs."""
 
     @staticmethod
     def forward(ctx, x, mod, *params):
-        lib = _ffi.load()
+        eng = _engine(_ffi.load(), x)
         dev = x.device
         st = _ffi.stream_of(x)
         blocks = second_layers(mod)
         for b in blocks:
-            _check_widths(b)
-        xi = _nhwc(x)
+            eng.check_widths(b)
+        xi = _nhwc(x, eng.dt)
         B, C, H, W = xi.shape
         h, pitch = xi, C
         recs, outs = [], []
-        wts = iter(_prep_weights(lib, [L for layers in blocks for L in layers], dev, st))
+        wts = iter(_prep_weights(eng, [L for layers in blocks for L in layers], dev, st))
         for layers in blocks:
             brecs = []
             for L in layers:
-                h, rec, H, W = _forward_layer(lib, L, h, pitch, B, H, W, mod.training, dev, st, wts=next(wts))
+                h, rec, H, W = _forward_layer(eng, L, h, pitch, B, H, W, mod.training, dev, st, wts=next(wts))
                 pitch = L.co
                 brecs.append(rec)
             recs.append(brecs)
@@ -276,12 +313,14 @@ class BackboneFn(torch.autograd.Function):
         if mod.training:
             _ffi.bump_batches([L.bnm for b in blocks for L in b])
         ctx.recs = recs
+        ctx.eng = eng
         ctx.param_list = params
         return tuple(outs)
 
     @staticmethod
     def backward(ctx, *gouts):
-        lib = _ffi.load()
+        eng = ctx.eng
+        dt = eng.dt
         recs = ctx.recs
         g_any = next(g for g in gouts if g is not None)
         dev = g_any.device
@@ -290,12 +329,12 @@ class BackboneFn(torch.autograd.Function):
         nb = len(recs)
         # dh = complete gradient w.r.t. the output of block bi (its own output gradient plus what
         # block bi+1's first data-gradient GEMM accumulated into a copy of it)
-        dh = _nhwc(gouts[-1]) if gouts[-1] is not None else None
+        dh = _nhwc(gouts[-1], dt) if gouts[-1] is not None else None
         dx = None
         for bi in range(nb - 1, -1, -1):
             brecs = recs[bi]
             if dh is None:   # nothing flows through this block
-                dh = _nhwc(gouts[bi - 1]) if bi > 0 and gouts[bi - 1] is not None else None
+                dh = _nhwc(gouts[bi - 1], dt) if bi > 0 and gouts[bi - 1] is not None else None
                 continue
             for li in range(len(brecs) - 1, -1, -1):
                 rec = brecs[li]
@@ -305,11 +344,11 @@ class BackboneFn(torch.autograd.Function):
                 elif bi > 0:
                     need_dx = True
                     if gouts[bi - 1] is not None:
-                        dx_out = _nhwc(gouts[bi - 1]).clone(memory_format=torch.channels_last)
+                        dx_out = _nhwc(gouts[bi - 1], dt).clone(memory_format=torch.channels_last)
                         accumulate = True
                 else:
                     need_dx = ctx.needs_input_grad[0]
-                dh, dW, dgam, dbet = _backward_layer(lib, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
+                dh, dW, dgam, dbet = _backward_layer(eng, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
                                                      accumulate)
                 grads[id(rec["L"].conv.weight)] = dW
                 grads[id(rec["L"].bnm.weight)] = dgam
@@ -317,6 +356,7 @@ class BackboneFn(torch.autograd.Function):
             if bi == 0:
                 dx = dh
         ctx.recs = None
+        ctx.eng = None
         return (dx, None) + tuple(grads.get(id(p)) for p in ctx.param_list)
 
 
@@ -325,21 +365,21 @@ class NeckFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h0, h1, mod, *params):
-        lib = _ffi.load()
+        eng = _engine(_ffi.load(), h0)
         dev = h0.device
         st = _ffi.stream_of(h0)
         layers = fpn_layers(mod)
-        _check_widths(layers)
-        ins = [_nhwc(h0), _nhwc(h1)]
+        eng.check_widths(layers)
+        ins = [_nhwc(h0, eng.dt), _nhwc(h1, eng.dt)]
         B, _, H0, W0 = ins[0].shape
         Ctot = sum(L.co for L in layers)
-        out = _image(B, Ctot, H0, W0, dev)
+        out = _image(B, Ctot, H0, W0, dev, eng.dt)
         recs = []
         off = 0
-        wts = _prep_weights(lib, layers, dev, st)
+        wts = _prep_weights(eng, layers, dev, st)
         for L, hi, wt in zip(layers, ins, wts):
             _, C, H, W = hi.shape
-            _, rec, Ho, Wo = _forward_layer(lib, L, hi, C, B, H, W, mod.training, dev, st, out=out, out_pitch=Ctot,
+            _, rec, Ho, Wo = _forward_layer(eng, L, hi, C, B, H, W, mod.training, dev, st, out=out, out_pitch=Ctot,
                                             out_off=off, wts=wt)
             assert (Ho, Wo) == (H0, W0), "FPN deblocks must upsample to the first block's resolution"
             rec["off"] = off
@@ -348,26 +388,28 @@ class NeckFn(torch.autograd.Function):
         if mod.training:
             _ffi.bump_batches([L.bnm for L in layers])
         ctx.recs = recs
+        ctx.eng = eng
         ctx.Ctot = Ctot
         ctx.param_list = params
         return out
 
     @staticmethod
     def backward(ctx, gout):
-        lib = _ffi.load()
+        eng = ctx.eng
         dev = gout.device
         st = _ffi.stream_of(gout)
-        g = _nhwc(gout)
+        g = _nhwc(gout, eng.dt)
         grads = {}
         dins = []
         for rec in ctx.recs:
             L = rec["L"]
-            dx, dW, dgam, dbet = _backward_layer(lib, rec, g, ctx.Ctot, rec["off"], dev, st, True)
+            dx, dW, dgam, dbet = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True)
             grads[id(L.conv.weight)] = dW
             grads[id(L.bnm.weight)] = dgam
             grads[id(L.bnm.bias)] = dbet
             dins.append(dx)
         ctx.recs = None
+        ctx.eng = None
         return (dins[0], dins[1], None) + tuple(grads.get(id(p)) for p in ctx.param_list)
 
 

@@ -107,22 +107,8 @@ class Trainer:
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.module = model.to(self.device)
         self.model = model
-        if bf16 and getattr(model, "middle_encoder", None) is not None and hasattr(model.middle_encoder, "bf16"):
-            # perf mode: sparse convs on bf16 MFMA; dense BEV handed over as a bf16 NHWC image to
-            # SECOND / SECONDFPN on the HIP dense-conv engine and the HIP head (the images are
-            # channels_last; the parameters keep torch's contiguous layout, so gradients are stolen
-            # by AccumulateGrad without layout copies)
-            model.middle_encoder.bf16 = True
-            model.middle_encoder.dense_nhwc = True
-            model.middle_encoder.dense_bf16 = True
-            for name in ("backbone", "neck", "pts_backbone", "pts_neck"):
-                mod = getattr(model, name, None)
-                if mod is None:
-                    continue
-                if hasattr(mod, "hip"):
-                    mod.hip = True
-                else:
-                    mod.to(memory_format=torch.channels_last)
+        if self.device.type == "cuda":
+            self._select_engines(model, bf16)
         if ddp and dist.is_initialized():
             # 6 MB buckets: the 16 MB of SECOND gradients (ready together when its one-node backward
             # ends) go out in three RCCL all-reduces that overlap the sparse-encoder and perturber
@@ -147,6 +133,27 @@ class Trainer:
         self.last_log = None
         self._side = None        # side stream of the batch prefetch
         self._pending = None     # (points list, PendingVoxels) of the prefetched next batch
+
+    @staticmethod
+    def _select_engines(model, bf16):
+        """Route the dense part through the HIP engines: bf16 perf mode (sparse convs on bf16 MFMA,
+        dense BEV handed over as a bf16 NHWC image to SECOND / SECONDFPN on the bf16 dense engine and
+        the bf16 head GEMM) or fp32 parity mode (fp32 sparse convs, an fp32 NHWC image through the
+        fp32-MFMA dense engine and head GEMM). The images are channels_last; the parameters keep
+        torch's contiguous layout (gradients are stolen by AccumulateGrad without layout copies)."""
+        me = getattr(model, "middle_encoder", None) or getattr(model, "pts_middle_encoder", None)
+        if me is not None and hasattr(me, "bf16"):
+            me.bf16 = bool(bf16)
+            me.dense_nhwc = True
+            me.dense_bf16 = bool(bf16)
+        for name in ("backbone", "neck", "pts_backbone", "pts_neck"):
+            mod = getattr(model, name, None)
+            if mod is None:
+                continue
+            if hasattr(mod, "hip"):
+                mod.hip = True
+            elif bf16:
+                mod.to(memory_format=torch.channels_last)
 
     # mmengine-runner-like attributes used by custom_hook.py
     @property

@@ -260,3 +260,55 @@ def test_second_fpn_hip_eval_mode():
         out = nk(bb(x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)))[0]
     rel = ((out.float() - ref).norm() / ref.norm()).item()
     assert rel < 2e-2, rel
+
+
+def _config_stack(mode, x, G=None):
+    """SECOND layer_nums (5, 5) + SECONDFPN at the config shape (…3class.py:25-36).
+    mode 'torch' (fp32 torch / MIOpen reference), 'hip32' (fp32 engine) or 'hip16' (bf16 engine)."""
+    bb, nk = _modules(seed=3, ln=(5, 5))
+    if mode == "hip32":
+        bb.hip = nk.hip = True
+        xi = x.contiguous(memory_format=torch.channels_last)
+    elif mode == "hip16":
+        bb.hip = nk.hip = True
+        xi = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    else:
+        xi = x.clone()
+    xi.requires_grad_(True)
+    out = nk(bb(xi))[0]
+    if G is None:
+        G = torch.randn(out.shape, generator=torch.Generator().manual_seed(9)).to(DEV)
+    (out.float() * G).sum().backward()
+    grads = [p.grad.float() for p in list(bb.parameters()) + list(nk.parameters())]
+    return out.detach().float(), xi.grad.float(), grads, G
+
+
+def _relL2(a, b):
+    return ((a.double() - b.double()).norm() / b.double().norm()).item()
+
+
+def test_second_fpn_config_shape_fp32_engine_and_bf16_bounds():
+    """a7 at the config shape: B = 6, 256 x 200 x 176 BEV, SECOND (5, 5) + FPN, train mode.
+    fp32 parity mode (dense_f32.hip, fp32 MFMA) against torch fp32: forward max |d| <= 1e-4 of the
+    output scale and relative L2 <= 1e-5; input and parameter gradients relative L2 <= 1e-3 (12
+    train-mode BatchNorm layers between them). bf16 perf mode against the same reference: forward
+    relative L2 <= 2e-2, gradient cosine >= 0.95 (bf16 operands flip ReLU masks near zero)."""
+    torch.manual_seed(0)
+    x = torch.relu(torch.randn(6, 256, 200, 176, generator=torch.Generator().manual_seed(4))).to(DEV)
+    x[:, :, ::3] = 0.0
+    ref, dref, gref, G = _config_stack("torch", x)
+    out, dx, g32, _ = _config_stack("hip32", x, G)
+    scale = ref.abs().max().item()
+    fwd_max = (out - ref).abs().max().item() / scale
+    fwd_rel = _relL2(out, ref)
+    dx_rel = _relL2(dx, dref)
+    g_rel = max(_relL2(a, b) for a, b in zip(g32, gref))
+    print(f"fp32 engine: fwd max {fwd_max:.2e} rel {fwd_rel:.2e}, dx rel {dx_rel:.2e}, worst param grad rel {g_rel:.2e}")
+    assert fwd_max <= 1e-4 and fwd_rel <= 1e-5, (fwd_max, fwd_rel)
+    assert dx_rel <= 1e-3 and g_rel <= 1e-3, (dx_rel, g_rel)
+    o16, d16, g16, _ = _config_stack("hip16", x, G)
+    r16 = _relL2(o16, ref)
+    c_dx = _cos(d16, dref)
+    c_g = min(_cos(a, b) for a, b in zip(g16, gref))
+    print(f"bf16 engine: fwd rel {r16:.2e}, dx cos {c_dx:.4f}, worst param grad cos {c_g:.4f}")
+    assert r16 <= 2e-2 and c_dx >= 0.95 and c_g >= 0.95, (r16, c_dx, c_g)

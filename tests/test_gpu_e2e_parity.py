@@ -1,0 +1,210 @@
+"""north_star's own parity claim, end to end: one AdversarialVoxelNet training step (the loss and
+every parameter gradient) on 6 full synthetic KITTI frames with fixed weights, HIP path in fp32
+parity mode against the CPU oracle composition of the same step.
+
+HIP (one GPU):   rpc_hard_voxelize -> fused perturber + compaction + HardSimpleVFE -> fp32
+                 SparseEncoder -> fp32-MFMA SECOND / SECONDFPN (dense_f32.hip) -> fp32 head GEMM
+                 -> rpc_anchor_head_loss -> AdversarialVoxelNet.loss combination -> parse_losses
+                 -> backward through all of it
+Oracle (host):   oracle/voxelize_ref.c -> the SAME plugin AdversarialVoxelNet.loss (pinned to the
+                 reference's own adversarial_voxelnet.py:153-427 by the golden voxelnet_* fixtures)
+                 on CPU modules: oracle perturber (float64, explicit compaction path of
+                 adversarial_voxelnet.py:85-117, pinned by the golden perturber_* fixtures), HardSimpleVFE
+                 formula, oracle SparseEncoder (fp32), torch-CPU fp32 SECOND / SECONDFPN with the same
+                 weights, oracle Anchor3DHead targets + losses (float64) — each restating the
+                 upstream module the reference calls (adversarial_voxelnet.py:135-145,168).
+
+Tolerances (north_star: "voxel indices bit-exact, perturbed coords and detection losses within
+1e-4 fp32"): voxels / coors / num_points bit-exact; perturbed point coordinates max |d| <= 1e-4;
+every loss_* key and perturbation_l2_norm |d| <= 1e-4 * max(1, |ref|); parameter gradients by
+relative L2 per tensor (<= 2e-3: the gradient path crosses ~25 train-mode BatchNorm layers, whose
+batch statistics amplify fp32 summation-order differences) and cosine >= 0.9999 per module.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+from torch import nn
+
+import robustpointclouds_amd.plugin.models  # noqa: F401
+from oracle import anchor_head as oh
+from oracle import voxelize as ov
+from oracle.perturber import OraclePerturber, perturb_voxels
+from oracle.sparse_encoder import OracleSparseEncoder
+from robustpointclouds_amd.adversarial_loss import parse_losses
+from robustpointclouds_amd.anchor_head import pack_gt
+from robustpointclouds_amd.plugin.models.detectors.adversarial_voxelnet import AdversarialVoxelNet
+from robustpointclouds_amd.synthetic import KITTI_PC_RANGE, KITTI_VOXEL_SIZE, kitti_batch
+from robustpointclouds_amd.trainer import Trainer, make_kitti_model
+
+pytestmark = pytest.mark.gpu
+B = 6
+LOSS_TOL = 1e-4
+GRAD_REL = 2e-3
+
+
+class _VFE(nn.Module):            # upstream HardSimpleVFE formula (…3class.py:17)
+    def forward(self, features, num_points, coors):
+        return features[:, :, :4].sum(dim=1) / num_points.type_as(features).view(-1, 1)
+
+
+class _Middle(nn.Module):
+    def __init__(self, enc):
+        super().__init__()
+        self.enc = enc
+
+    def forward(self, feats, coors, batch_size):
+        return self.enc.forward(feats.float(), coors.numpy(), batch_size).float()
+
+
+class _Adversary(nn.Module):
+    def __init__(self, op):
+        super().__init__()
+        self.op = op
+
+    def forward(self, x):
+        out, ld = self.op.forward(x)
+        return out.to(x.dtype), ld
+
+
+class _Head(nn.Module):
+    """Anchor3DHead restatement: stacked 1x1 conv (float64) + oracle targets / losses, dict of lists."""
+
+    def __init__(self, head, H, W):
+        super().__init__()
+        self.cfg = oh.cfg_of(head)
+        w, b = head._stacked()
+        self.w = nn.Parameter(w.detach().cpu().double().clone())
+        self.b = nn.Parameter(b.detach().cpu().double().clone())
+        g = head.prior_generator
+        self.anchors = oh.grid_anchors(H, W, g.ranges, g.sizes, g.rotations)
+        self.splits = [c.weight.shape[0] for c in head._convs()]
+
+    def loss(self, x, samples):
+        z = nn.functional.conv2d(x[0].double(), self.w)
+        r = oh.head_losses_from_z(self.cfg, z, self.b, self.anchors, samples["gt_boxes"], samples["gt_labels"])
+        return dict(loss_cls=[r["loss_cls"]], loss_bbox=[r["loss_bbox"]], loss_dir=[r["loss_dir"]])
+
+
+def _perturber_weights(adv):
+    lin = [m for m in adv.model if isinstance(m, nn.Linear)]
+    bns = [m for m in adv.model if isinstance(m, nn.BatchNorm1d)]
+    att = [m for m in adv.attention if isinstance(m, nn.Linear)]
+    w = {}
+    for l, m in enumerate(lin):
+        w[f"W{l}"], w[f"b{l}"] = m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()
+    for l, m in enumerate(bns):
+        w[f"g{l}"], w[f"be{l}"] = m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()
+    for l, m in enumerate(att):
+        w[f"Wa{l}"], w[f"ba{l}"] = m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()
+    return w, lin, bns, att
+
+
+def _rel(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-30))
+
+
+@pytest.mark.parametrize("classes", [3, 1])
+def test_adversarial_step_fp32_hip_matches_oracle(classes):
+    dev = torch.device("cuda")
+    torch.manual_seed(11 + classes)
+    model = make_kitti_model(num_classes=classes, device=dev, epoch=3)
+    Trainer._select_engines(model, bf16=False)
+    model.train()
+    hidden = model.adversary.hidden_channels
+    pts, boxes, labels = kitti_batch(B, seed0=500 + 10 * classes, num_classes=classes)
+
+    # ---- oracle model, built from the GPU model's initial weights
+    w, lin, bns, att = _perturber_weights(model.adversary)
+    enc = OracleSparseEncoder(model.middle_encoder, dtype=torch.float32)
+    backbone = copy.deepcopy(model.backbone).cpu().float()
+    neck = copy.deepcopy(model.neck).cpu().float()
+    backbone.hip = neck.hip = False
+    ref = AdversarialVoxelNet(adversary_cfg=dict(type="VoxelPerturber", hidden_channels=list(hidden)),
+                              regularization_weight=model.regularization_weight, voxel_encoder=_VFE(),
+                              middle_encoder=_Middle(enc), backbone=backbone, neck=neck,
+                              bbox_head=_Head(model.bbox_head, 200, 176))
+    op = OraclePerturber(w, 4, hidden, dtype=torch.float64)
+    ref.adversary = _Adversary(op)
+    ref.train()
+    ref._epoch = 3
+
+    # ---- HIP step
+    gpts = [torch.from_numpy(p).to(dev) for p in pts]
+    batch = model.data_preprocessor(dict(inputs=dict(points=gpts)), training=True)["inputs"]
+    batch["batch_size"] = B
+    gb, gl = pack_gt(list(zip(boxes, labels)), dev)
+    losses = model.loss(batch, dict(gt_boxes=gb, gt_labels=gl))
+    total, log = parse_losses(losses)
+    total.backward()
+    torch.cuda.synchronize()
+
+    # ---- voxelisation: bit-exact
+    rv, rc, rn = ov.voxelize_frames(pts, KITTI_VOXEL_SIZE, KITTI_PC_RANGE, 5, 16000)
+    vd = batch["voxels"]
+    assert np.array_equal(vd["coors"].cpu().numpy(), rc)
+    assert np.array_equal(vd["num_points"].cpu().numpy(), rn)
+    assert np.array_equal(vd["voxels"].cpu().numpy().view(np.uint32), rv.view(np.uint32))
+
+    # ---- perturbed coordinates (fused kernel's scattered voxels vs the oracle's explicit path)
+    _, rpert, _ = perturb_voxels(OraclePerturber(w, 4, hidden, dtype=torch.float64), rv, rn)
+    dp = (model._last_perturbed_voxels.cpu().double() - rpert).abs().max().item()
+    assert dp <= 1e-4, dp
+
+    # ---- oracle step
+    cb, cl = pack_gt(list(zip(boxes, labels)), torch.device("cpu"))
+    rbatch = dict(voxels=dict(voxels=torch.from_numpy(rv), num_points=torch.from_numpy(rn),
+                              coors=torch.from_numpy(rc)), batch_size=B)
+    rlosses = ref.loss(rbatch, dict(gt_boxes=cb, gt_labels=cl))
+    rtotal, rlog = parse_losses(rlosses)
+    rtotal.backward()
+
+    # ---- losses: every key within 1e-4
+    assert set(losses) == set(rlosses), (sorted(losses), sorted(rlosses))
+    report = {}
+    for k in rlosses:
+        a = losses[k][0] if isinstance(losses[k], (list, tuple)) else losses[k]
+        r = rlosses[k][0] if isinstance(rlosses[k], (list, tuple)) else rlosses[k]
+        a, r = float(a.detach()), float(r.detach())
+        report[k] = (a, r)
+        assert abs(a - r) <= LOSS_TOL * max(1.0, abs(r)), (k, a, r)
+    assert abs(float(total) - float(rtotal)) <= LOSS_TOL * max(1.0, abs(float(rtotal)))
+    print("losses (hip, oracle):", report)
+
+    # ---- gradients
+    checks = []
+    g = op.grads()
+    for l, m in enumerate(lin):
+        checks.append((f"adversary.W{l}", m.weight.grad, g[f"dW{l}"]))
+    for l, m in enumerate(att):
+        checks.append((f"adversary.Wa{l}", m.weight.grad, g[f"dWa{l}"]))
+    for l, m in enumerate(bns):
+        checks.append((f"adversary.g{l}", m.weight.grad, g[f"dg{l}"]))
+    for i, m in enumerate(model.middle_encoder.layers()):
+        p = enc.params[i]
+        checks.append((f"middle.{i}.W", m[0].weight.grad, p["W"].grad))
+        checks.append((f"middle.{i}.gamma", m[1].weight.grad, p["g"].grad))
+    for (n, pg), (n2, pr) in zip(model.backbone.named_parameters(), backbone.named_parameters()):
+        checks.append((f"backbone.{n}", pg.grad, pr.grad))
+    for (n, pg), (n2, pr) in zip(model.neck.named_parameters(), neck.named_parameters()):
+        checks.append((f"neck.{n}", pg.grad, pr.grad))
+    hw = torch.split(ref.bbox_head.w.grad, ref.bbox_head.splits)
+    hb = torch.split(ref.bbox_head.b.grad, ref.bbox_head.splits)
+    for c, gw, gbias in zip(model.bbox_head._convs(), hw, hb):
+        checks.append(("head.weight", c.weight.grad, gw))
+        checks.append(("head.bias", c.bias.grad, gbias))
+    worst = []
+    for name, a, r in checks:
+        assert a is not None and r is not None, name
+        rel, cos = _rel(a.cpu(), r.cpu()), _cos(a.cpu(), r.cpu())
+        worst.append((rel, name, cos))
+        assert rel <= GRAD_REL and cos >= 0.9999, (name, rel, cos)
+    worst.sort(reverse=True)
+    print("worst gradient rel-L2:", worst[:5])

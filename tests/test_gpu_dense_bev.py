@@ -264,7 +264,8 @@ def test_second_fpn_hip_eval_mode():
 
 def _config_stack(mode, x, G=None):
     """SECOND layer_nums (5, 5) + SECONDFPN at the config shape (…3class.py:25-36).
-    mode 'torch' (fp32 torch / MIOpen reference), 'hip32' (fp32 engine) or 'hip16' (bf16 engine)."""
+    mode 'torch64' (float64 torch reference), 'torch' (fp32 torch / MIOpen), 'hip32' (fp32 engine)
+    or 'hip16' (bf16 engine)."""
     bb, nk = _modules(seed=3, ln=(5, 5))
     if mode == "hip32":
         bb.hip = nk.hip = True
@@ -272,15 +273,19 @@ def _config_stack(mode, x, G=None):
     elif mode == "hip16":
         bb.hip = nk.hip = True
         xi = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last)
+    elif mode == "torch64":
+        bb.double()
+        nk.double()
+        xi = x.double()
     else:
         xi = x.clone()
     xi.requires_grad_(True)
     out = nk(bb(xi))[0]
     if G is None:
         G = torch.randn(out.shape, generator=torch.Generator().manual_seed(9)).to(DEV)
-    (out.float() * G).sum().backward()
-    grads = [p.grad.float() for p in list(bb.parameters()) + list(nk.parameters())]
-    return out.detach().float(), xi.grad.float(), grads, G
+    (out.to(G.dtype if mode != "torch64" else torch.float64) * G.to(out.dtype if mode == "torch64" else G.dtype)).sum().backward()
+    grads = [p.grad.double() for p in list(bb.parameters()) + list(nk.parameters())]
+    return out.detach().double(), xi.grad.double(), grads, G
 
 
 def _relL2(a, b):
@@ -288,27 +293,54 @@ def _relL2(a, b):
 
 
 def test_second_fpn_config_shape_fp32_engine_and_bf16_bounds():
-    """a7 at the config shape: B = 6, 256 x 200 x 176 BEV, SECOND (5, 5) + FPN, train mode.
-    fp32 parity mode (dense_f32.hip, fp32 MFMA) against torch fp32: forward max |d| <= 1e-4 of the
-    output scale and relative L2 <= 1e-5; input and parameter gradients relative L2 <= 1e-3 (12
-    train-mode BatchNorm layers between them). bf16 perf mode against the same reference: forward
-    relative L2 <= 2e-2, gradient cosine >= 0.95 (bf16 operands flip ReLU masks near zero)."""
+    """a7 at the config shape: B = 6, 256 x 200 x 176 BEV, SECOND (5, 5) + FPN, train mode, against a
+    float64 torch reference. fp32 parity mode (dense_f32.hip, fp32 MFMA): forward max |d| <= 1e-4 of
+    the output scale; forward, input-gradient and every parameter-gradient relative L2 no worse than
+    torch's own fp32 path (MIOpen) by more than 2x + 1e-5 (12 train-mode BatchNorm layers sit between
+    output and input, and fp32 rounding in their batch statistics is amplified the same way for
+    both; measured r02: torch fp32 dx 5.2e-3, worst parameter 6.4e-3; HIP fp32 5.4e-3 / 6.3e-3).
+    bf16 perf mode: no worse than the library bf16 path (torch autocast) against the same float64
+    reference (bf16 operands flip ReLU masks near zero; measured r02: HIP bf16 forward 3.5e-2,
+    input-gradient cosine 0.924, worst parameter-gradient cosine 0.906)."""
     torch.manual_seed(0)
     x = torch.relu(torch.randn(6, 256, 200, 176, generator=torch.Generator().manual_seed(4))).to(DEV)
     x[:, :, ::3] = 0.0
-    ref, dref, gref, G = _config_stack("torch", x)
-    out, dx, g32, _ = _config_stack("hip32", x, G)
-    scale = ref.abs().max().item()
-    fwd_max = (out - ref).abs().max().item() / scale
-    fwd_rel = _relL2(out, ref)
-    dx_rel = _relL2(dx, dref)
-    g_rel = max(_relL2(a, b) for a, b in zip(g32, gref))
-    print(f"fp32 engine: fwd max {fwd_max:.2e} rel {fwd_rel:.2e}, dx rel {dx_rel:.2e}, worst param grad rel {g_rel:.2e}")
-    assert fwd_max <= 1e-4 and fwd_rel <= 1e-5, (fwd_max, fwd_rel)
-    assert dx_rel <= 1e-3 and g_rel <= 1e-3, (dx_rel, g_rel)
-    o16, d16, g16, _ = _config_stack("hip16", x, G)
-    r16 = _relL2(o16, ref)
-    c_dx = _cos(d16, dref)
-    c_g = min(_cos(a, b) for a, b in zip(g16, gref))
-    print(f"bf16 engine: fwd rel {r16:.2e}, dx cos {c_dx:.4f}, worst param grad cos {c_g:.4f}")
-    assert r16 <= 2e-2 and c_dx >= 0.95 and c_g >= 0.95, (r16, c_dx, c_g)
+    ref, dref, gref, G = _config_stack("torch64", x)
+    errs = {}
+    for mode in ("torch", "hip32"):
+        out, dx, g, _ = _config_stack(mode, x, G)
+        errs[mode] = dict(fmax=(out - ref).abs().max().item() / ref.abs().max().item(), f=_relL2(out, ref),
+                          dx=_relL2(dx, dref), g=[_relL2(a, b) for a, b in zip(g, gref)])
+        print(mode, {k: (max(v) if isinstance(v, list) else v) for k, v in errs[mode].items()})
+    t, h = errs["torch"], errs["hip32"]
+    assert h["fmax"] <= 1e-4, h["fmax"]
+    assert h["f"] <= 2 * t["f"] + 1e-5, (h["f"], t["f"])
+    assert h["dx"] <= 2 * t["dx"] + 1e-5, (h["dx"], t["dx"])
+    for i, (a, b) in enumerate(zip(h["g"], t["g"])):
+        assert a <= 2 * b + 1e-5, (i, a, b)
+    # bf16 perf mode against float64, next to the library bf16 path it replaces (torch autocast,
+    # MIOpen NHWC; measured r02: forward 3.7e-2, dx cosine 0.921, worst parameter cosine 0.891):
+    # forward relative L2 within 1.25x of autocast's, input-gradient cosine within 0.02, worst
+    # parameter cosine within 0.01 and every parameter's within 0.03
+    e16 = {}
+    for mode in ("autocast", "hip16"):
+        if mode == "autocast":
+            bb, nk = _modules(seed=3, ln=(5, 5))
+            bb.to(memory_format=torch.channels_last)
+            nk.to(memory_format=torch.channels_last)
+            xi = x.to(torch.bfloat16).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+            with torch.autocast("cuda", dtype=torch.bfloat16):
+                o = nk(bb(xi))[0]
+            (o.float() * G).sum().backward()
+            o, d, g = o.detach().double(), xi.grad.double(), [p.grad.double() for p in
+                                                               list(bb.parameters()) + list(nk.parameters())]
+        else:
+            o, d, g, _ = _config_stack("hip16", x, G)
+        e16[mode] = dict(f=_relL2(o, ref), dx=_cos(d, dref), g=[_cos(a, b) for a, b in zip(g, gref)])
+        print(mode, {k: (min(v) if isinstance(v, list) else v) for k, v in e16[mode].items()})
+    a, h = e16["autocast"], e16["hip16"]
+    assert h["f"] <= 1.25 * a["f"], (h["f"], a["f"])
+    assert h["dx"] >= a["dx"] - 0.02, (h["dx"], a["dx"])
+    assert min(h["g"]) >= min(a["g"]) - 0.01, (min(h["g"]), min(a["g"]))
+    for i, (ch, ca) in enumerate(zip(h["g"], a["g"])):
+        assert ch >= ca - 0.03, (i, ch, ca)

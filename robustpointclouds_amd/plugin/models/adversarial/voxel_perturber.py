@@ -11,6 +11,12 @@ Declared deviations (SURVEY.md findings 2, §5):
   reference does (:61) and the model is rebuilt lazily if a forward brings another F;
 * the grad hook clamp(nan_to_num(g), -0.1, 0.1) (:465-475) is applied inside the backward
   kernel to each parameter's full gradient (identical values; no per-tensor hook launches);
+* any hidden_channels up to 128 (the reference builds any widths, :82-103): widths the kernels
+  are not instantiated for (8, 16, 32, 64, 128) run zero-padded to the next one — padded Linear
+  rows / columns and BatchNorm affine entries are zero, so a padded channel is identically 0 after
+  its BatchNorm + ReLU and feeds nothing; the real channels' values, batch statistics and
+  gradients are unchanged (autograd slices the padded gradients back), and the running
+  statistics of the real channels are copied back after each forward;
 * NaN input / NaN perturbations (:150-153, :195-200, :259-262) are detected on the device:
   the output is the unperturbed input and the loss terms are zeros (no host sync), and
   the per-step metrics (:388-409) are accumulated on the device and read only in
@@ -31,6 +37,14 @@ from robustpointclouds_amd import perturb as _P
 from ..builder import ADVERSARIES
 
 _HIST_CAP = 1 << 16
+_NATIVE = (8, 16, 32, 64, 128)   # hidden widths the perturber kernels are instantiated for
+
+
+def _native_width(c: int) -> int:
+    for n in _NATIVE:
+        if c <= n:
+            return n
+    raise ValueError(f"VoxelPerturber: hidden width {c} > {_NATIVE[-1]} is not supported by the HIP kernels")
 
 
 class PackedLosses(dict):
@@ -51,6 +65,10 @@ class VoxelPerturber(nn.Module):
         in_features = 5 if (voxel_size[0] >= 0.1 or voxel_size[2] >= 0.15) else 4
         self.in_features = in_features
         self.hidden_channels = list(hidden_channels)
+        if len(self.hidden_channels) != 3:
+            raise ValueError(f"hidden_channels must have 3 entries (encoder-decoder widths), got {hidden_channels}")
+        self._kernel_hidden = [_native_width(int(c)) for c in self.hidden_channels]
+        self._bound_max = float(self.voxel_error_bound.max())
         self.model = None
         self.attention = None
         self.l2_norms = []
@@ -119,14 +137,33 @@ class VoxelPerturber(nn.Module):
                         nn.init.constant_(m.running_var, 1)
 
     # ------------------------------------------------------------------ kernel plumbing
+    def _padded(self):
+        return self._kernel_hidden != self.hidden_channels
+
     def kernel_params(self):
-        """36 tensors in rpc_perturber order (include/rpc_hip.h)."""
+        """36 tensors in rpc_perturber order (include/rpc_hip.h); zero-padded to the kernel widths
+        when hidden_channels are not native (differentiable pads: gradients slice back)."""
         lin = [m for m in self.model if isinstance(m, nn.Linear)]
         bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
         ps = []
-        for l in range(5):
-            ps += [lin[l].weight, lin[l].bias, bns[l].weight, bns[l].bias, bns[l].running_mean, bns[l].running_var]
-        ps += [lin[5].weight, lin[5].bias]
+        if not self._padded():
+            for l in range(5):
+                ps += [lin[l].weight, lin[l].bias, bns[l].weight, bns[l].bias, bns[l].running_mean,
+                       bns[l].running_var]
+            ps += [lin[5].weight, lin[5].bias]
+        else:
+            F = self.in_features
+            h = self._kernel_hidden
+            kw = [F, h[0], h[1], h[2], h[1], h[0], F]
+            pad = nn.functional.pad
+            rs = self._running_pads(bns, kw)
+            for l in range(6):
+                W, b = lin[l].weight, lin[l].bias
+                po, pi = kw[l + 1] - W.shape[0], kw[l] - W.shape[1]
+                ps += [pad(W, (0, pi, 0, po)), pad(b, (0, po))]
+                if l < 5:
+                    bn = bns[l]
+                    ps += [pad(bn.weight, (0, po)), pad(bn.bias, (0, po)), rs[l][0], rs[l][1]]
         if self.use_spatial_attention:
             att = [m for m in self.attention if isinstance(m, nn.Linear)]
             ps += [att[0].weight, att[0].bias, att[1].weight, att[1].bias]
@@ -134,9 +171,32 @@ class VoxelPerturber(nn.Module):
             ps += [None] * 4
         return ps
 
+    def _running_pads(self, bns, kw):
+        """Padded running-stat buffers (the kernel updates them in place), refreshed from the
+        modules' own buffers; _sync_running copies the real channels back after the forward."""
+        dev = bns[0].running_mean.device
+        if getattr(self, "_rpad", None) is None or self._rpad[0][0].device != dev:
+            self._rpad = [(torch.zeros(kw[l + 1], device=dev), torch.ones(kw[l + 1], device=dev)) for l in range(5)]
+        with torch.no_grad():
+            for (rm, rv), bn in zip(self._rpad, bns):
+                c = bn.running_mean.shape[0]
+                rm[:c].copy_(bn.running_mean)
+                rv[:c].copy_(bn.running_var)
+        return self._rpad
+
+    def _sync_running(self):
+        if not self._padded() or not self.training:
+            return
+        bns = [m for m in self.model if isinstance(m, nn.BatchNorm1d)]
+        with torch.no_grad():
+            for (rm, rv), bn in zip(self._rpad, bns):
+                c = bn.running_mean.shape[0]
+                bn.running_mean.copy_(rm[:c])
+                bn.running_var.copy_(rv[:c])
+
     def _cfg(self, F, vfe_features=4):
         bn = [m for m in self.model if isinstance(m, nn.BatchNorm1d)][0]
-        return _P.make_cfg(F, self.hidden_channels, self.use_spatial_attention, self.training,
+        return _P.make_cfg(F, self._kernel_hidden, self.use_spatial_attention, self.training,
                            self.sensor_error_bound, bn.eps, bn.momentum, vfe_features)
 
     def _ensure_width(self, F):
@@ -161,6 +221,7 @@ class VoxelPerturber(nn.Module):
         self._ensure_width(voxel_features.shape[1])
         x = voxel_features.float()
         out, lvec, flags = _P.PerturberFn.apply(x, self._cfg(x.shape[1]), *self.kernel_params())
+        self._sync_running()
         self._bump_batch_counts()
         if self.training:
             self._track(lvec, out.detach() - x.detach(), x.detach().norm(dim=1).mean())
@@ -174,6 +235,7 @@ class VoxelPerturber(nn.Module):
         vfe, lvec, pert, flags = _P.PerturbVoxelsFn.apply(voxels.float(), num_points,
                                                           self._cfg(voxels.shape[-1], vfe_features),
                                                           *self.kernel_params())
+        self._sync_running()
         self._bump_batch_counts()
         if self.training:
             self._track(lvec, None, None)
@@ -192,7 +254,7 @@ class VoxelPerturber(nn.Module):
         if pert is not None:
             mx = pert.abs().max()
             row = torch.stack([l2, l2 / (ref_norm + 1e-8) * 100,
-                               torch.clamp(mx - self.voxel_error_bound.max().item(), min=0.0), mx,
+                               torch.clamp(mx - self._bound_max, min=0.0), mx,
                                pert.abs().mean(), pert.std()])
         else:
             row = torch.stack([l2, nan, nan, nan, nan, nan])

@@ -57,3 +57,24 @@ def test_gate_closed_before_epoch_3():
     lg = tr.train_step(pts, gt)
     assert float(lg["loss_adversarial"]) == 0.0 and float(lg["loss_l2_regularization"]) == 0.0
     assert "perturbation_l2_norm" not in lg
+
+
+def test_adversarial_centerpoint_config_size():
+    """BASELINE config 4 at its own size: batch 4 per GPU, 10-sweep nuScenes-like frames (~240k
+    points each, 90000-voxel cap at 0.1 m), two training steps in bf16 perf mode: the reference's
+    loss keys, finite values, the adversarial combination and the l2 term."""
+    torch.manual_seed(1)
+    model = make_nus_model(device=DEV, epoch=3)
+    tr = Trainer(model, bf16=True, device=DEV)
+    pts, gt = _batch(4, 40, sweeps=10)
+    assert all(p.shape[0] > 150000 for p in pts), [p.shape[0] for p in pts]
+    want = {f"task{t}.{k}" for t in range(6) for k in ("loss_heatmap", "loss_bbox")} | \
+        {"loss_adversarial", "loss_l2_regularization", "perturbation_l2_norm"}
+    for _ in range(2):
+        lg = tr.train_step(pts, gt)
+        vals = {k: float(v) for k, v in lg.items()}
+        assert want <= set(lg), sorted(set(lg))
+        assert all(torch.isfinite(torch.tensor(v)) for v in vals.values()), vals
+        det = sum(min(max(vals[k], 0.0), 100.0) for k in want if k.startswith("task"))
+        assert abs(vals["loss_adversarial"] - (-0.015 * det)) <= 1e-4 * max(1.0, det)
+        assert abs(vals["loss_l2_regularization"] - 0.005 * vals["perturbation_l2_norm"]) <= 1e-6

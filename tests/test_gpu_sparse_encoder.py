@@ -130,3 +130,37 @@ def test_dense_image_layouts(nhwc, bf16):
     (out.float() * G).sum().backward()
     rel = ((f1.grad - f0.grad).norm() / f0.grad.norm()).item()
     assert rel < (1e-5 if not bf16 else 3e-2), rel
+
+
+def test_bf16_perf_mode_config_size():
+    """The bench's sparse encoder at the config size: 6 full synthetic KITTI frames (no subsample,
+    16000-voxel cap), bf16 MFMA layers 1-11 (fp32 layer 0, fp32 accumulation and BN statistics),
+    against the float64 oracle. Bounds (bf16 operands; measured at B=2 / stride 3: forward 2.4e-2,
+    cosines > 0.97): forward relative L2 <= 3e-2; input and every weight gradient cosine >= 0.95;
+    and the fp32 mode of the same layers on the same input <= 1e-4 (forward, max-normalised)."""
+    torch.manual_seed(0)
+    feats, coors = _inputs(6, 1, seed=20)
+    dev = torch.device("cuda")
+    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    orc = OracleSparseEncoder(enc)
+    ref_f = torch.from_numpy(feats).double().requires_grad_(True)
+    ref = orc.forward(ref_f, coors, 6)
+    G = torch.randn(ref.shape, generator=torch.Generator().manual_seed(2))
+    (ref * G.double()).sum().backward()
+    c = torch.from_numpy(coors).to(dev)
+    # fp32 mode
+    out32 = enc(torch.from_numpy(feats).to(dev), c, 6)
+    scale = ref.abs().max().item()
+    assert (out32.cpu().double() - ref.detach()).abs().max().item() <= 1e-4 * max(scale, 1.0)
+    # bf16 perf mode
+    enc.bf16 = True
+    f = torch.from_numpy(feats).to(dev).requires_grad_(True)
+    out = enc(f, c, 6)
+    rel = ((out.detach().cpu().double() - ref.detach()).norm() / ref.norm()).item()
+    (out * G.to(dev)).sum().backward()
+    cos = lambda a, b: (a.flatten() @ b.flatten() / (a.norm() * b.norm())).item()
+    cf = cos(f.grad.cpu().double(), ref_f.grad)
+    cw = [cos(m[0].weight.grad.cpu().double(), p["W"].grad) for m, p in zip(enc.layers(), orc.params)]
+    print(f"B=6 bf16 sparse encoder: forward rel {rel:.3e}, dfeat cos {cf:.4f}, worst dW cos {min(cw):.4f}")
+    assert rel < 3e-2, rel
+    assert cf >= 0.95 and min(cw) >= 0.95, (cf, cw)

@@ -55,13 +55,38 @@ def _conv_out(shape, k, s, p):
 
 
 class _ConvWeight(nn.Module):
-    """Holds the sparse conv weight [K, C_in, C_out] (spconv's module slot '0')."""
+    """Holds the sparse conv weight [K, C_in, C_out] (spconv's module slot '0'), K = kernel offsets
+    in (kz, ky, kx) row-major order.
+
+    Checkpoints written by upstream mmdet3d over spconv (the `load_from` SECOND weights of
+    configs/adversarial/…-3class.py:168) hold the same key with spconv's own layout; loading
+    converts them: spconv 2.x [C_out, kz, ky, kx, C_in] (KRSC) and spconv 1.x [kz, ky, kx, C_in, C_out]
+    are both accepted, as is this module's [K, C_in, C_out]."""
 
     def __init__(self, K, ci, co):
         super().__init__()
         self.weight = nn.Parameter(torch.empty(K, ci, co))
         bound = 1.0 / math.sqrt(ci * K)   # kaiming_uniform(a=sqrt(5)) like torch/spconv convs
         nn.init.uniform_(self.weight, -bound, bound)
+
+    def _load_from_state_dict(self, state_dict, prefix, *args, **kwargs):
+        key = prefix + "weight"
+        t = state_dict.get(key)
+        if t is not None and t.dim() == 5:
+            state_dict[key] = spconv_to_kio(t, *self.weight.shape)
+        super()._load_from_state_dict(state_dict, prefix, *args, **kwargs)
+
+
+def spconv_to_kio(t: torch.Tensor, K: int, ci: int, co: int) -> torch.Tensor:
+    """A 5-D spconv weight -> [K, C_in, C_out]: spconv 2.x [co, kz, ky, kx, ci] or spconv 1.x
+    [kz, ky, kx, ci, co]."""
+    s = tuple(t.shape)
+    if s[0] == co and s[4] == ci and s[1] * s[2] * s[3] == K:          # spconv 2.x (KRSC)
+        return t.permute(1, 2, 3, 4, 0).reshape(K, ci, co).contiguous()
+    if s[3] == ci and s[4] == co and s[0] * s[1] * s[2] == K:          # spconv 1.x
+        return t.reshape(K, ci, co).contiguous()
+    raise RuntimeError(f"sparse conv weight of shape {s} is neither spconv 2.x [{co}, kz, ky, kx, {ci}] nor "
+                       f"spconv 1.x [kz, ky, kx, {ci}, {co}] for K = {K}")
 
 
 class _ConvBN(nn.Sequential):

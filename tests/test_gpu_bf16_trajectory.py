@@ -14,8 +14,8 @@ from robustpointclouds_amd.trainer import Trainer, make_kitti_model
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 STEPS = 6
-LOSS_REL = 2e-2      # per-step |bf16 - fp32| / |fp32| of loss_cls, loss_bbox, loss_dir and the total
-ADV_COS = 0.98       # cosine of the adversary's parameter change (bf16 vs fp32) after STEPS steps
+LOSS_REL = 2e-2      # (measured r02: 1.05e-2) per-step |bf16 - fp32| / |fp32| of loss_cls, loss_bbox, loss_dir and the total
+ADV_COS = 0.98       # (measured r02: 0.9915) cosine of the adversary's parameter change (bf16 vs fp32) after STEPS steps
 
 
 def _run(bf16, batches):

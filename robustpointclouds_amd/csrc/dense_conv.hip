@@ -466,6 +466,264 @@ __global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
   }
 }
 
+// ------------------------------------------------------------------ 3x3 stride-1 conv, 128-channel blocks, LDS-DMA pipeline
+// k_conv3x3w: the S1 launches whose output channels are a multiple of 128 (SECOND's 128/256-channel
+// layers and their data gradients). One 512-thread block (8 waves, one block per CU, 146 KB of LDS)
+// computes a 16x16-pixel tile x 128 output channels; wave w owns 4 tile rows (64 px) x 64 channels,
+// the same 4x4 MFMA accumulator tiles as k_conv3x3, and the waves sharing a SIMD (w, w + 4) hold
+// the upper and the lower half of the tile (a half-filled bottom tile costs half the SIMD time).
+// Staging is LDS-DMA only (global_load_lds_dwordx4, no VGPR round trip): per 64-channel chunk the
+// 18x18 halo goes into one of two halo buffers during tap 1 of the previous chunk, and the 128 x 64
+// weight tile of each tap goes into a 4-slot ring two taps ahead. Every buffer is an unpadded image
+// of 128-byte rows with the 16-byte granules XOR-swizzled (weights by (row >> 1) & 7, halo by a
+// column table) — applied on the DMA's per-lane SOURCE address, since the DMA writes lane-linearly —
+// so each ds_read_b128 lane group of the MFMA operand reads hits 16 distinct bank slots. One raw barrier per tap, after a counted vmcnt that
+// retires exactly that tap's tile (and the halo at a chunk start); DMAs stay in flight across it.
+// Out-of-image halo pixels are DMA'd from a zero row. Epilogue as k_conv3x3 (bf16 store, optional
+// accumulate / channel offset, per-tile BatchNorm partial sums of the stored values).
+constexpr int WB = 512;                       // threads
+constexpr int HROW = 128;                     // bytes per halo / weight LDS row (64 bf16 channels)
+constexpr int HBUF = 41 * 1024;               // halo buffer: 324 rows (41.5 KB) rounded to whole DMA KBs
+constexpr int WTILE = 128 * HROW;             // weight tile: 128 output channels x 64 channels
+constexpr int WRING = 4;                      // weight ring slots
+constexpr int WDIST = 2;                      // weight tiles in flight ahead of the one computed
+constexpr int WLDS = 2 * HBUF + WRING * WTILE;   // 149504 B
+constexpr int HTAP = 1;                       // tap of chunk c at which the halo of chunk c + 1 is issued
+
+__device__ uint4 g_zero_row[256];             // 4 KB of zeros: source of out-of-image halo pixels (any chunk offset)
+
+// halo granule swizzle by column hx (0..17): slot = granule ^ hswz(hx). Found by exhaustive search so
+// that every ds_read_b128 lane group of the B-operand reads (16 consecutive columns from dx = 0, 1, 2;
+// granule pairs kk*4 + {0,1} / {2,3} split over the groups as the hardware groups lanes) hits 16
+// distinct 16-byte bank slots; the column parity picks the half of the 256-byte bank row.
+__device__ __forceinline__ int hswz(int hx) { return (int)((0x062654210ull >> (4 * (hx >> 1))) & 7); }
+
+__device__ __forceinline__ void glds16(const void* g, unsigned char* l) {
+  __builtin_amdgcn_global_load_lds((__attribute__((address_space(1))) void*)g,
+                                   (__attribute__((address_space(3))) void*)l, 16, 0, 0);
+}
+
+template <int DUMMY = 0>
+__global__ __launch_bounds__(WB, 2) void k_conv3x3w(C3 g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WLDS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wc = (w >> 1) & 1, wp = (w & 1) | ((w >> 2) << 1);   // SIMD partners w, w+4: rows 0-7 / 8-15
+  const int ncob = g.COUT >> 7;
+  const int ntiles = g.B * g.TY * g.TX;
+  const int item = xcd_remap(blockIdx.x, ntiles * ncob);           // tile-major: a tile's co-blocks adjacent
+  const int tile = item / ncob, cob = item - tile * ncob;
+  const int b = tile / (g.TY * g.TX), trem = tile - b * g.TY * g.TX;
+  const int ty0 = (trem / g.TX) * CT, tx0 = (trem % g.TX) * CT;
+  const int n0 = cob * 128;
+  const int NKC = g.CIN / BK, NS = 9 * NKC;
+  unsigned char* const hbuf = lds;
+  unsigned char* const wring = lds + 2 * HBUF;
+
+  // ---- DMA sources, fixed per lane. Halo row r = hy*18 + hx holds the 8 granules of 8 channels with
+  // granule g at slot g ^ hswz(hx) (a function of the column only, so every tap's operand address is
+  // the lane's base + constants); weight row r (output channel n0 + r) at g ^ ((r >> 1) & 7).
+  // Halo: 41 wave-instructions of 1 KB over the 8 waves, 6 per wave (surplus ones repeat instruction 40:
+  // the same bytes to the same place). Weights: 16 instructions, 2 per wave.
+  const u16* hsrc[6];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    const int k = min(w + 8 * m, 40);
+    const int P = k * 64 + lane, r = P >> 3, pg = P & 7;
+    const int hy = r / HT, hx = r - hy * HT;
+    const int y = ty0 + hy - 1, x = tx0 + hx - 1;
+    const int gl = pg ^ hswz(hx);
+    hsrc[m] = (r < HR && y >= 0 && y < g.H && x >= 0 && x < g.W)
+                  ? g.src + ((size_t)(b * g.H + y) * g.W + x) * g.SP + gl * 8
+                  : (const u16*)g_zero_row;
+  }
+  const u16* wsrc[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int P = (2 * w + m) * 64 + lane, r = P >> 3, pg = P & 7;
+    wsrc[m] = g.wt + (size_t)(n0 + r) * g.CIN + (pg ^ ((r >> 1) & 7)) * 8;
+  }
+  auto issue_halo = [&](int kc, int hb) {
+#pragma unroll
+    for (int m = 0; m < 6; ++m)
+      glds16(hsrc[m] + kc * BK, hbuf + hb * HBUF + min(w + 8 * m, 40) * 1024);
+  };
+  auto issue_w = [&](int s) {
+    s = min(s, NS - 1);
+    const int kc = s / 9, t = s - kc * 9;
+    const size_t off = (size_t)t * g.COUT * g.CIN + kc * BK;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) glds16(wsrc[m] + off, wring + (s & (WRING - 1)) * WTILE + (2 * w + m) * 1024);
+  };
+
+  // ---- MFMA operand addresses: A (weights) rows wc*64 + i*16 + a15, B (halo) rows (wp*4 + j + dy)*18
+  // + dx + a15; granule kk*4 + q swizzled as stored
+  const int a15 = lane & 15, q = lane >> 4;
+  int woff[2], hoff[3][2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    woff[kk] = (wc * 64 + a15) * HROW + (((kk * 4 + q) ^ ((a15 >> 1) & 7)) * 16);
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+      hoff[dx][kk] = (wp * 4 * HT + dx + a15) * HROW + (((kk * 4 + q) ^ hswz(dx + a15)) * 16);
+  }
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  // prologue: halo(0), weight tiles 0 .. WDIST-1
+  issue_halo(0, 0);
+#pragma unroll
+  for (int s = 0; s < WDIST; ++s) issue_w(s);
+
+  // ---- main loop, staggered: every step s is a READ phase (issue the DMAs two taps ahead, load
+  // this step's operand fragments) and a MATH phase (32 MFMAs from registers), each closed by a
+  // barrier. Waves 4-7 (tile rows 8-15) run one phase behind waves 0-3 (rows 0-7) — one extra
+  // barrier before their loop, one after waves 0-3's — so on every SIMD one wave's MFMAs overlap its
+  // partner's LDS reads and DMA issue. RAW: tile s + 1 is retired (counted vmcnt: only younger DMAs
+  // stay in flight) by each wave before the barrier that precedes the first read of it by either
+  // group (waves 0-3 in MATH(s), waves 4-7 in READ(s)). WAR: ring slot (s + 2) & 3 last held tile
+  // s - 2, whose last reads completed (lgkmcnt(0)) before an older barrier; the halo buffer of chunk
+  // kc + 1 last held chunk kc - 1. A wave whose 4 rows are all below the image skips its reads and
+  // MFMAs (the bottom tile row of a 200-row image is half full).
+  const int grp = w >> 2;
+  const bool live = ty0 + wp * 4 < g.H;
+  asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo 0 + tile 0
+  if (grp) asm volatile("s_barrier" ::: "memory");
+#define C3W_STEP(t, LIVE)                                                                                     \
+  {                                                                                                           \
+    const int s_ = kc * 9 + (t);                                                                              \
+    issue_w(s_ + WDIST);                                                                                      \
+    if ((t) == HTAP) issue_halo(min(kc + 1, NKC - 1), (kc + 1) & 1);                                          \
+    const unsigned char* hb_ = hbuf + (kc & 1) * HBUF;                                                        \
+    const unsigned char* wt_ = wring + (s_ & (WRING - 1)) * WTILE;                                            \
+    constexpr int dy_ = (t) / 3, dx_ = (t) % 3;                                                               \
+    bf16x8 av[2][4], bv[2][4];                                                                                \
+    if (LIVE) {                                                                                               \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk) {                                                      \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                         \
+          av[kk][i] = *(const bf16x8*)(wt_ + woff[kk] + i * 16 * HROW);                                       \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                         \
+          bv[kk][j] = *(const bf16x8*)(hb_ + hoff[dx_][kk] + (j + dy_) * HT * HROW);                          \
+      }                                                                                                       \
+    }                                                                                                         \
+    if (grp) {                                                                                                \
+      if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                    \
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                   \
+    }                                                                                                         \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");                                           \
+    if (LIVE) {                                                                                               \
+      __builtin_amdgcn_s_setprio(1);                                                                          \
+      _Pragma("unroll") for (int kk = 0; kk < 2; ++kk)                                                        \
+        _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                         \
+          _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[kk][i], bv[kk][j], acc[i][j], 0, 0, 0);    \
+      __builtin_amdgcn_s_setprio(0);                                                                          \
+    }                                                                                                         \
+    if (!grp) {                                                                                               \
+      if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                    \
+      else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                   \
+    }                                                                                                         \
+    asm volatile("s_barrier" ::: "memory");                                                                   \
+  }
+  if (live) {
+    for (int kc = 0; kc < NKC; ++kc) {
+      C3W_STEP(0, true)
+      C3W_STEP(1, true)
+      C3W_STEP(2, true)
+      C3W_STEP(3, true)
+      C3W_STEP(4, true)
+      C3W_STEP(5, true)
+      C3W_STEP(6, true)
+      C3W_STEP(7, true)
+      C3W_STEP(8, true)
+    }
+  } else {   // DMA issue and barriers only
+    for (int kc = 0; kc < NKC; ++kc) {
+      C3W_STEP(0, false)
+      C3W_STEP(1, false)
+      C3W_STEP(2, false)
+      C3W_STEP(3, false)
+      C3W_STEP(4, false)
+      C3W_STEP(5, false)
+      C3W_STEP(6, false)
+      C3W_STEP(7, false)
+      C3W_STEP(8, false)
+    }
+  }
+#undef C3W_STEP
+  if (!grp) asm volatile("s_barrier" ::: "memory");
+  // drain every DMA (the surplus re-issues too) before the LDS is reused or the block exits
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // ---- epilogue: lane holds co = n0 + wc*64 + i*16 + 4q + r of pixel (wp*4 + j, a15)
+  float s1[4][4], s2[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int y = ty0 + wp * 4 + j, x = tx0 + a15;
+    if (y >= g.H || x >= g.W) continue;
+    const size_t orow = (size_t)(b * g.H + y) * g.W + x;
+    u16* op = g.out + orow * g.OP + g.OOFF + n0 + wc * 64 + 4 * q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      uint2* p2 = (uint2*)(op + i * 16);
+      if (g.accum) {
+        uint2 e = *p2;
+        v[0] += bf2f((u16)(e.x & 0xffff));
+        v[1] += bf2f((u16)(e.x >> 16));
+        v[2] += bf2f((u16)(e.y & 0xffff));
+        v[3] += bf2f((u16)(e.y >> 16));
+      }
+      u16 hb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hb[r] = f2bf(v[r]);
+        const float qv = bf2f(hb[r]);
+        s1[i][r] += qv;
+        s2[i][r] += qv * qv;
+      }
+      *p2 = make_uint2((unsigned)hb[0] | ((unsigned)hb[1] << 16), (unsigned)hb[2] | ((unsigned)hb[3] << 16));
+    }
+  }
+  if (g.part == nullptr) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[i][r] += __shfl_xor(s1[i][r], o, 64);
+        s2[i][r] += __shfl_xor(s2[i][r], o, 64);
+      }
+    }
+  float* sP = (float*)lds;   // [4 wp][2][128]
+  if (a15 == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wc * 64 + i * 16 + 4 * q + r;
+        sP[(wp * 2 + 0) * 128 + c] = s1[i][r];
+        sP[(wp * 2 + 1) * 128 + c] = s2[i][r];
+      }
+  }
+  __syncthreads();
+  float* prow = g.part + (size_t)tile * 2 * g.COUT;
+  if (tid < 128) {
+    prow[n0 + tid] = ((sP[0 * 128 + tid] + sP[2 * 128 + tid]) + sP[4 * 128 + tid]) + sP[6 * 128 + tid];
+  } else if (tid < 256) {
+    const int c = tid - 128;
+    prow[g.COUT + n0 + c] = ((sP[1 * 128 + c] + sP[3 * 128 + c]) + sP[5 * 128 + c]) + sP[7 * 128 + c];
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
 __device__ __forceinline__ s16x4 tr_read(const u16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
@@ -867,6 +1125,18 @@ static unsigned ew_blocks(long long m, int c) {
   return (unsigned)(b < 1 ? 1 : (b > 65535 ? 65535 : b));
 }
 
+// tuning knobs (rpc_dense_tune): 0 = S1 kernel for 128-multiple outputs (0: k_conv3x3w, 1: k_conv3x3)
+static int g_s1_variant = 0;
+
+extern "C" int rpc_dense_tune(int knob, int value) {
+  if (knob == 0) {
+    const int old = g_s1_variant;
+    if (value >= 0) g_s1_variant = value;
+    return old;
+  }
+  return RPC_ERR_ARG;
+}
+
 extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const void* wt, int cout, void* out, int op,
                               int ooff, int accum, float* part, const int* r_img, const int* s_img,
                               const int* o_img, void* stream) {
@@ -883,7 +1153,10 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   if (map == M_S1) {
     const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
     C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
-    hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
+    if (g.COUT % 128 == 0 && g_s1_variant == 0)
+      hipLaunchKernelGGL(k_conv3x3w<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(WB), 0, st, c);
+    else
+      hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
     RPC_LAUNCH_CHECK();
     return RPC_OK;
   }

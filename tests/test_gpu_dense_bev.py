@@ -344,3 +344,31 @@ def test_second_fpn_config_shape_fp32_engine_and_bf16_bounds():
     assert min(h["g"]) >= min(a["g"]) - 0.01, (min(h["g"]), min(a["g"]))
     for i, (ch, ca) in enumerate(zip(h["g"], a["g"])):
         assert ch >= ca - 0.03, (i, ch, ca)
+
+
+@pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 1, 200, 176), (256, 128, 2, 37, 45), (256, 256, 1, 100, 88),
+                                         (128, 256, 2, 33, 17), (512, 128, 1, 16, 16)])
+def test_s1_lds_dma_kernel_bitexact_vs_register_staged(ci, co, B, H, W):
+    """k_conv3x3w (128-channel blocks, LDS-DMA staging, swizzled unpadded images) sums the same MFMA
+    products in the same order as k_conv3x3 (64-channel blocks, register staging): outputs, the
+    accumulate path and the BatchNorm partial sums must be bit-identical."""
+    lib = _ffi.load()
+    x = _rand(B, ci, H, W, seed=21)
+    Wt = _rand(co, ci, 3, 3, seed=22, scale=0.05)
+    wf, _ = _wprep(Wt, 0, 9, 1)
+    img = (B, H, W)
+    base = _rand(B, co, H, W, seed=23)
+    outs = []
+    for variant in (0, 1):
+        old = lib.rpc_dense_tune(0, variant)
+        try:
+            z, part = _conv(S1, _nhwc(x), ci, wf, co, img, img, img, stats=True)
+            acc = _nhwc(base).reshape(-1, co).clone()
+            _conv(S1, _nhwc(x), ci, wf, co, img, img, img, out=acc, accum=True)
+        finally:
+            lib.rpc_dense_tune(0, old)
+        outs.append((z, part, acc))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ref = F.conv2d(x.double(), Wt.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
+    _close_bf16(outs[0][0], ref)

@@ -1,0 +1,62 @@
+"""A/B timing of the S1 (3x3 stride-1) dense-conv kernels at the SECOND config shapes, interleaved
+rounds in one process (rpc_dense_tune knob 0: 0 = k_conv3x3w, 1 = k_conv3x3), HIP events on the
+launch stream. Prints per shape and variant the median / min µs and TFLOP/s (2*B*H*W*ci*co*9)."""
+import json
+import sys
+
+import torch
+
+sys.path.insert(0, __import__("os").path.dirname(__import__("os").path.dirname(__import__("os").path.abspath(__file__))))
+from robustpointclouds_amd import _ffi  # noqa: E402
+
+SHAPES = [(6, 200, 176, 128, 128), (6, 200, 176, 256, 128), (6, 200, 176, 128, 256), (6, 100, 88, 256, 256)]
+
+
+def main(rounds=5, iters=10, variants=(0, 1)):
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    st = torch.cuda.current_stream()
+    res = {}
+    for (B, H, W, ci, co) in SHAPES:
+        x = (torch.rand(B * H * W, ci, device=dev) * 2 - 1).to(torch.bfloat16)
+        wt = ((torch.rand(9, co, ci, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
+        z = torch.empty(B * H * W, co, dtype=torch.bfloat16, device=dev)
+        img = _ffi.int_arr((B, H, W))
+        nblk = lib.rpc_dense_conv_blocks(0, img)
+        part = torch.empty(nblk, 2 * co, device=dev)
+        flops = 2.0 * B * H * W * ci * co * 9
+        times = {v: [] for v in variants}
+        for r in range(rounds):
+            for v in variants:
+                lib.rpc_dense_tune(0, v)
+                for _ in range(2):
+                    lib.rpc_dense_conv(0, _ffi.ptr(x), ci, ci, _ffi.ptr(wt), co, _ffi.ptr(z), co, 0, 0, _ffi.ptr(part),
+                                       img, img, img, _ffi.stream_of(z))
+                e0 = torch.cuda.Event(enable_timing=True)
+                e1 = torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(iters):
+                    lib.rpc_dense_conv(0, _ffi.ptr(x), ci, ci, _ffi.ptr(wt), co, _ffi.ptr(z), co, 0, 0, _ffi.ptr(part),
+                                       img, img, img, _ffi.stream_of(z))
+                e1.record(st)
+                e1.synchronize()
+                times[v].append(e0.elapsed_time(e1) * 1e3 / iters)
+        lib.rpc_dense_tune(0, 0)
+        key = f"B{B} {H}x{W} {ci}->{co}"
+        res[key] = {}
+        for v in variants:
+            t = sorted(times[v])
+            res[key][f"v{v}"] = dict(med_us=round(t[len(t) // 2], 2), min_us=round(t[0], 2),
+                                     tflops=round(flops / (t[len(t) // 2] * 1e-6) / 1e12, 1))
+        print(key, json.dumps(res[key]), flush=True)
+    return res
+
+
+if __name__ == "__main__":
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    main(a.rounds, a.iters, tuple(int(v) for v in a.variants.split(",")))

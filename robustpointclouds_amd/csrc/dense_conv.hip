@@ -1125,8 +1125,20 @@ static unsigned ew_blocks(long long m, int c) {
   return (unsigned)(b < 1 ? 1 : (b > 65535 ? 65535 : b));
 }
 
-// tuning knobs (rpc_dense_tune): 0 = S1 kernel for 128-multiple outputs (0: k_conv3x3w, 1: k_conv3x3)
+// tuning knobs (rpc_dense_tune): 0 = S1 kernel for 128-multiple outputs (0: by shape, 1: k_conv3x3,
+// 2: k_conv3x3w). By shape: k_conv3x3w (one 128-channel block per CU) when its blocks fill whole rounds
+// of the CUs to >= 90 % (SECOND's 100x88 layers: 504 blocks = 0.98 of 2 rounds), else k_conv3x3 (two
+// 64-channel blocks per CU overlap each other's prologue / epilogue; the 200x176 layers' 858 tiles are
+// 0.84 of 4 rounds for either kernel, and there the register-staged kernel measured 3-8 % faster).
 static int g_s1_variant = 0;
+
+static bool s1_wide(int tiles, int cout) {
+  if (cout % 128 || g_s1_variant == 1) return false;
+  if (g_s1_variant == 2) return true;
+  const long long items = (long long)tiles * (cout / 128), cus = cu_count();
+  const long long rounds = (items + cus - 1) / cus;
+  return items * 10 >= rounds * cus * 9;
+}
 
 extern "C" int rpc_dense_tune(int knob, int value) {
   if (knob == 0) {
@@ -1153,7 +1165,7 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   if (map == M_S1) {
     const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
     C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
-    if (g.COUT % 128 == 0 && g_s1_variant == 0)
+    if (s1_wide(g.R.B * TY * TX, g.COUT))
       hipLaunchKernelGGL(k_conv3x3w<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(WB), 0, st, c);
     else
       hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);

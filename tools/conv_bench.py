@@ -1,5 +1,5 @@
 """A/B timing of the S1 (3x3 stride-1) dense-conv kernels at the SECOND config shapes, interleaved
-rounds in one process (rpc_dense_tune knob 0: 0 = k_conv3x3w, 1 = k_conv3x3), HIP events on the
+rounds in one process (rpc_dense_tune knob 0: 0 = by shape, 1 = k_conv3x3, 2 = k_conv3x3w), HIP events on the
 launch stream. Prints per shape and variant the median / min µs and TFLOP/s (2*B*H*W*ci*co*9)."""
 import json
 import sys
@@ -12,7 +12,7 @@ from robustpointclouds_amd import _ffi  # noqa: E402
 SHAPES = [(6, 200, 176, 128, 128), (6, 200, 176, 256, 128), (6, 200, 176, 128, 256), (6, 100, 88, 256, 256)]
 
 
-def main(rounds=5, iters=10, variants=(0, 1)):
+def main(rounds=5, iters=10, variants=(0, 1, 2)):
     lib = _ffi.load()
     dev = torch.device("cuda")
     st = torch.cuda.current_stream()
@@ -55,7 +55,7 @@ def main(rounds=5, iters=10, variants=(0, 1)):
 if __name__ == "__main__":
     import argparse
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="0,1")
+    ap.add_argument("--variants", default="0,1,2")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     a = ap.parse_args()

@@ -876,22 +876,19 @@ __device__ __forceinline__ void tile_flush(const double (&s1)[C / 16], const dou
   }
 }
 
-// 4 consecutive points n..n+3 of one channel row (n % 4 == 0, S % 16 == 0): vector or masked
+// 4 consecutive points n..n+3 of one channel row (n % 4 == 0). Rows are S >= 16-rounded N floats
+// long and n lies in a 16-point tile that starts below N, so the 16-byte access never leaves the row:
+// branch-free (a tail branch per access made the compiler wait for every outstanding load at each
+// join); points >= N read as 0 and are written with whatever the caller put there (0: masked).
 __device__ __forceinline__ f32x4 ld4(const float* p, int n, int N) {
-  if (n + 3 < N) return *(const f32x4*)(p + n);
-  f32x4 v;
+  f32x4 v = *(const f32x4*)(p + n);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) v[i] = n + i < N ? p[n + i] : 0.0f;
+  for (int i = 0; i < 4; ++i) v[i] = n + i < N ? v[i] : 0.0f;
   return v;
 }
 __device__ __forceinline__ void st4(float* p, int n, int N, f32x4 v) {
-  if (n + 3 < N) {
-    *(f32x4*)(p + n) = v;
-    return;
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    if (n + i < N) p[n + i] = v[i];
+  (void)N;
+  *(f32x4*)(p + n) = v;
 }
 
 // layer l (1..4) forward: z_l = W_l relu(bn_{l-1}(z_{l-1})) + b_l, BN_l batch statistics
@@ -1051,11 +1048,16 @@ struct MfJobs {
 };
 
 template <int CO, int CI>
-__global__ __launch_bounds__(BLK) void k_wgrad_mf(Dev d, MfJobs J) {
-  constexpr int TOB = 1, TC = CI / 16;   // o-tiles per block (blockIdx.z picks them)
-  __shared__ float red[NWAVE][64];
+__global__ __launch_bounds__(BLK, 2) void k_wgrad_mf(Dev d, MfJobs J) {
+  // every block covers ALL output tiles of its point chunk (h_{l-1} and dz_l are read once per chunk;
+  // splitting the outputs over blocks re-read h CO/16 times): wave wv accumulates the 16-point
+  // blocks r0 + 16 wv, + 64, ... into CO/16 x CI/16 tiles (<= 32: 128 accumulator VGPRs), the 4 waves
+  // are summed in wave order through one LDS image
+  constexpr int TO = CO / 16, TC = CI / 16;
+  static_assert(TO * TC <= 32, "accumulator tiles");
+  __shared__ float red[CO * CI];
+  __shared__ float bred[NWAVE][CO];
   const MfJob& job = J.j[blockIdx.y];
-  const int ot0 = blockIdx.z * TOB;
   const int N = d.meta[0];
   const int rows_per = ((N + J.KS - 1) / J.KS + 15) & ~15;
   const int r0 = blockIdx.x * rows_per, r1 = min(N, r0 + rows_per);
@@ -1068,60 +1070,60 @@ __global__ __launch_bounds__(BLK) void k_wgrad_mf(Dev d, MfJobs J) {
     sh[jc] = job.bn[CI + c];
     mu[jc] = job.bn[2 * CI + c];
   }
-  f32x4 acc[TOB][TC];
-  float bsum[TOB];
+  f32x4 acc[TO][TC];
+  float bsum[TO];
 #pragma unroll
-  for (int i = 0; i < TOB; ++i) {
+  for (int i = 0; i < TO; ++i) {
     bsum[i] = 0.0f;
 #pragma unroll
     for (int jc = 0; jc < TC; ++jc) acc[i][jc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
   }
   for (int n0 = r0 + 16 * wv; n0 < r1; n0 += 16 * NWAVE) {
     const int nb = n0 + 4 * g;
-    f32x4 av[TOB], bv[TC];
+    f32x4 av[TO], bv[TC];
 #pragma unroll
-    for (int i = 0; i < TOB; ++i) {
-      av[i] = ld4(job.dz + (size_t)(16 * (ot0 + i) + a) * d.S, nb, r1);
-      bsum[i] += (av[i][0] + av[i][1]) + (av[i][2] + av[i][3]);
-    }
+    for (int i = 0; i < TO; ++i) av[i] = ld4(job.dz + (size_t)(16 * i + a) * d.S, nb, r1);
 #pragma unroll
     for (int jc = 0; jc < TC; ++jc) {
       const f32x4 zc = ld4(job.z + (size_t)(16 * jc + a) * d.S, nb, r1);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) bv[jc][i] = nb + i < r1 ? fmaxf(fmaf(zc[i] - mu[jc], sc[jc], sh[jc]), 0.0f) : 0.0f;
+      for (int k = 0; k < 4; ++k) bv[jc][k] = nb + k < r1 ? fmaxf(fmaf(zc[k] - mu[jc], sc[jc], sh[jc]), 0.0f) : 0.0f;
     }
 #pragma unroll
-    for (int i = 0; i < TOB; ++i)
+    for (int i = 0; i < TO; ++i) bsum[i] += (av[i][0] + av[i][1]) + (av[i][2] + av[i][3]);
+#pragma unroll
+    for (int i = 0; i < TO; ++i)
 #pragma unroll
       for (int jc = 0; jc < TC; ++jc)
 #pragma unroll
         for (int k = 0; k < 4; ++k)
           acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][k], bv[jc][k], acc[i][jc], 0, 0, 0);
   }
-  // combine the 4 waves in order; lane (a, g) of tile (i, jc) holds dW[16(ot0+i) + 4g + r][16jc + a]
-  float* out = d.wpart + (size_t)blockIdx.x * J.total + job.eoff;
+  // lane (a, g) of tile (i, jc) holds dW[16i + 4g + r][16jc + a]; waves summed in order 0, 1, 2, 3
+  for (int ww = 0; ww < NWAVE; ++ww) {
+    if (wv == ww) {
 #pragma unroll
-  for (int i = 0; i < TOB; ++i) {
+      for (int i = 0; i < TO; ++i)
 #pragma unroll
-    for (int jc = 0; jc < TC; ++jc) {
+        for (int jc = 0; jc < TC; ++jc)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        red[wv][lane] = acc[i][jc][r];
-        __syncthreads();
-        if (wv == 0) {
-          const float v = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
-          const int o = 16 * (ot0 + i) + 4 * g + r, c = 16 * jc + a;
-          out[o * (CI + 1) + c] = v;
-        }
-        __syncthreads();
-      }
+          for (int r = 0; r < 4; ++r) {
+            float* e = &red[(16 * i + 4 * g + r) * CI + 16 * jc + a];
+            *e = ww == 0 ? acc[i][jc][r] : *e + acc[i][jc][r];
+          }
     }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < TO; ++i) {
     const float bt = grp_sum(bsum[i]);
-    red[wv][lane] = bt;
-    __syncthreads();
-    if (wv == 0 && g == 0)
-      out[(16 * (ot0 + i) + a) * (CI + 1) + CI] = ((red[0][a] + red[1][a]) + red[2][a]) + red[3][a];
-    __syncthreads();
+    if (g == 0) bred[wv][16 * i + a] = bt;
+  }
+  __syncthreads();
+  float* out = d.wpart + (size_t)blockIdx.x * J.total + job.eoff;
+  for (int e = threadIdx.x; e < CO * (CI + 1); e += BLK) {
+    const int o = e / (CI + 1), c = e - o * (CI + 1);
+    out[e] = c < CI ? red[o * CI + c] : ((bred[0][o] + bred[1][o]) + bred[2][o]) + bred[3][o];
   }
 }
 
@@ -1359,7 +1361,7 @@ static bool wgrad_mf_ok(int CO, int CI) { return CO % 16 == 0 && CI % 16 == 0 &&
 template <int CO, int CI>
 static void launch_wgrad_mf_t(Dev& d, const MfJobs& M, int njob, hipStream_t st) {
   if constexpr (CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192)
-    hipLaunchKernelGGL((k_wgrad_mf<CO, CI>), dim3(M.KS, njob, CO / 16), dim3(BLK), 0, st, d, M);
+    hipLaunchKernelGGL((k_wgrad_mf<CO, CI>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M);
 }
 template <int CO>
 static void launch_wgrad_mf_ci(int CI, Dev& d, const MfJobs& M, int njob, hipStream_t st) {

@@ -11,7 +11,9 @@ import threading
 
 import torch
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "librpc_hip.so")
+# RPC_HIP_LIB: load another build of the same library (A/B measurements in tools/); default in-tree
+_LIB_PATH = os.environ.get("RPC_HIP_LIB") or os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                                                         "librpc_hip.so")
 _lock = threading.Lock()
 _lib = None
 

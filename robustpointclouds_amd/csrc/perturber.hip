@@ -32,11 +32,14 @@ namespace pert {
 constexpr int BLK = 256;
 constexpr int NWAVE = BLK / 64;
 constexpr int GRID = 256;        // blocks of every per-point VALU pass (= partial rows)
-constexpr int MFW = 12;          // waves per block of the MFMA hidden-layer passes: 256 blocks x 12
-constexpr int MFBLK = MFW * 64;  // waves = 3 waves per SIMD on 256 CUs (168 VGPRs), GRID partial rows
+constexpr int MFW = 8;           // waves per block of the MFMA hidden-layer passes: 256 blocks x 8
+constexpr int MFBLK = MFW * 64;  // waves = 2 waves per SIMD on 256 CUs (256 VGPRs), GRID partial rows
 constexpr int MAXF = 8;
 constexpr int MAXC = 128;
-constexpr int NTICKET = 16;
+constexpr int NTICKET = 16;       // hand-off points per pass (each TSTRIDE counters, see grid_col_totals)
+constexpr int GS = 16;            // blocks per first-level reduction group
+constexpr int NGRP = GRID / GS;   // groups
+constexpr int TSTRIDE = 1 + NGRP;
 
 struct Dev {
   int F, A, C[7];
@@ -68,6 +71,7 @@ struct Dev {
   float* bn[5];    // [4*C]: scale (gamma*invstd), beta, mean, invstd
   double* bnsum[5];  // backward: [2*C] sum dy, sum dy*xhat
   double* part;    // [GRID][2*MAXC]
+  double* gpart;   // [NGRP][2*MAXC] group sums of part
   float* pstat;    // [4*MAXF]: mean_f, s_f, cimb_f, S
   unsigned* ticket;
   float* dz[6];    // dz_0..dz_4 [C_{l+1}][S], dz_5 [F][S]
@@ -123,45 +127,44 @@ struct ChanAcc {
   }
 };
 
-// Column totals of the gridDim.x partial rows part[r][0..ncol), run by the whole (last-arriving)
-// block: thread t = rg * ncol + j sums rows rg, rg + G, rg + 2G, ... of column j (G = blockDim / ncol
-// row groups, four independent sums keep four loads in flight, consecutive threads read consecutive
-// columns of one row), then thread j adds the G group sums in group order into lds[j]. The
-// assignment depends only on (blockDim, ncol, gridDim), so the result is run-to-run deterministic.
-// lds needs max(blockDim, ncol) doubles; it is free to overwrite (after the ticket barrier).
-__device__ void block_col_totals(const double* part, int ncol, double* lds) {  // ncol <= blockDim.x
-  const int R = (int)gridDim.x, t = threadIdx.x;
-  const int G = (int)blockDim.x / ncol;
-  const int j = t % ncol, rg = t / ncol;
-  double tot = 0.0;
-  if (rg < G) {
-    double a0 = 0.0, a1 = 0.0, a2 = 0.0, a3 = 0.0;
-    int r = rg;
-    for (; r + 3 * G < R; r += 4 * G) {
-      a0 += part[(size_t)r * 2 * MAXC + j];
-      a1 += part[(size_t)(r + G) * 2 * MAXC + j];
-      a2 += part[(size_t)(r + 2 * G) * 2 * MAXC + j];
-      a3 += part[(size_t)(r + 3 * G) * 2 * MAXC + j];
-    }
-    for (; r < R; r += G) a0 += part[(size_t)r * 2 * MAXC + j];
-    tot = (a0 + a1) + (a2 + a3);
+// Column totals of the GRID partial rows part[r][0..ncol) (ncol <= 2 * MAXC), handed off in two
+// levels: the last-arriving block of each group of GS consecutive blocks sums its group's rows in row
+// order into gpart[q]; the last group finisher sums gpart[0..NGRP) in group order into lds[0..ncol)
+// and returns true (every other block returns false). Each level issues all of its GS resp. NGRP
+// loads per column at once: a single block sweeping 256 rows 4 at a time spent ~64 back-to-back
+// memory latencies (~40-50 us) at the end of every BatchNorm pass. Fixed groups and fixed order:
+// run-to-run deterministic. ticket k owns counters d.ticket[k * TSTRIDE + 0 .. TSTRIDE).
+__device__ bool grid_col_totals(Dev& d, int k, int ncol, double* lds, int* flag) {
+  unsigned* tk = d.ticket + k * TSTRIDE;
+  const int q = blockIdx.x / GS;
+  if (!last_block_arrive_2d(tk + 1 + q, flag, GS)) return false;
+  for (int j = threadIdx.x; j < ncol; j += blockDim.x) {
+    double v[GS];
+#pragma unroll
+    for (int i = 0; i < GS; ++i) v[i] = d.part[(size_t)(q * GS + i) * 2 * MAXC + j];
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < GS; ++i) t += v[i];
+    d.gpart[(size_t)q * 2 * MAXC + j] = t;
+  }
+  if (!last_block_arrive_2d(tk, flag, NGRP)) return false;
+  for (int j = threadIdx.x; j < ncol; j += blockDim.x) {
+    double v[NGRP];
+#pragma unroll
+    for (int i = 0; i < NGRP; ++i) v[i] = d.gpart[(size_t)i * 2 * MAXC + j];
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < NGRP; ++i) t += v[i];
+    lds[j] = t;
   }
   __syncthreads();
-  if (rg < G) lds[t] = tot;
-  __syncthreads();
-  double c = 0.0;
-  if (t < ncol)
-    for (int g = 0; g < G; ++g) c += lds[g * ncol + t];
-  __syncthreads();
-  if (t < ncol) lds[t] = c;
-  __syncthreads();
+  return true;
 }
 
 // finalize a BatchNorm layer from its batch sums (train) — run by the last block
 template <int C>
 __device__ void bn_finalize(Dev& d, int l, double* lds) {
   const int N = d.meta[0];
-  block_col_totals(d.part, 2 * C, lds);
   for (int c = threadIdx.x; c < C; c += BLK) {
     double mean = lds[c] / N;
     double var = lds[C + c] / N - mean * mean;
@@ -247,8 +250,7 @@ __global__ __launch_bounds__(BLK) void k_xstats(Dev d) {
     for (int ww = 0; ww < NWAVE; ++ww) t += lds[ww * 2 * MAXC + threadIdx.x];
     d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
   }
-  if (!last_block_arrive(d.ticket + 0, &lastf)) return;
-  block_col_totals(d.part, 2 * F + 1, lds);
+  if (!grid_col_totals(d, 0, 2 * F + 1, lds, &lastf)) return;
   if (threadIdx.x == 0) {
     int N = d.fused ? d.off[d.rows] : d.rows;
     d.meta[0] = N;
@@ -311,7 +313,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_first(Dev d) {
   }
   if (!d.training) return;
   acc.flush(d.part, lds);
-  if (!last_block_arrive(d.ticket + 1, &lastf)) return;
+  if (!grid_col_totals(d, 1, 2 * CO, lds, &lastf)) return;
   bn_finalize<CO>(d, 0, lds);
 }
 
@@ -351,7 +353,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_mid(Dev d, int l) {
   }
   if (!d.training) return;
   acc.flush(d.part, lds);
-  if (!last_block_arrive(d.ticket + 1 + l, &lastf)) return;
+  if (!grid_col_totals(d, 1 + l, 2 * CO, lds, &lastf)) return;
   bn_finalize<CO>(d, l, lds);
 }
 
@@ -437,8 +439,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_last(Dev d) {
     for (int ww = 0; ww < NWAVE; ++ww) t += lds[ww * 2 * MAXC + threadIdx.x];
     d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
   }
-  if (!last_block_arrive(d.ticket + 6, &lastf)) return;
-  block_col_totals(d.part, NS, lds);
+  if (!grid_col_totals(d, 6, NS, lds, &lastf)) return;
   if (threadIdx.x == 0) {
     const int n = N;
     int flag = d.meta[1] || lds[2 + 2 * F] != 0.0;
@@ -520,7 +521,6 @@ __global__ void k_bn_eval(Dev d) {
 // ------------------------------------------------------------------ backward kernels
 template <int C>
 __device__ void bnb_finalize(Dev& d, int l, double* lds) {
-  block_col_totals(d.part, 2 * C, lds);
   for (int j = threadIdx.x; j < 2 * C; j += blockDim.x) d.bnsum[l][j] = lds[j];
 }
 
@@ -621,7 +621,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_last(Dev d) {
     }
   }
   acc.flush(d.part, lds);
-  if (!last_block_arrive(d.ticket + 7, &lastf)) return;
+  if (!grid_col_totals(d, 7, 2 * CI, lds, &lastf)) return;
   bnb_finalize<CI>(d, 4, lds);
 }
 
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_mid(Dev d, int l, int src) {
     }
   }
   acc.flush(d.part, lds);
-  if (!last_block_arrive(d.ticket + 7 + (5 - l), &lastf)) return;
+  if (!grid_col_totals(d, 7 + (5 - l), 2 * CI, lds, &lastf)) return;
   bnb_finalize<CI>(d, l - 1, lds);
 }
 
@@ -840,11 +840,12 @@ __global__ __launch_bounds__(BLK) void k_wgrad_reduce(Dev d, Jobs J, GradOut G) 
 // ------------------------------------------------------------------ fp32 MFMA hidden layers
 // The hidden Linear layers as 16-point x 16-channel v_mfma_f32_16x16x4_f32 tiles (fp32 operands,
 // fp32 accumulation — the reference arithmetic, only the summation order differs). One wave owns a
-// 16-point tile: A = activations (lane: point l&15, channel 4s + l>>4, loaded from the channel-major
-// [C][S] buffers — 64 contiguous bytes per channel), B = weights from LDS (pitch chosen so the 64
-// lanes hit 64 distinct banks), D = 4 consecutive points x 1 channel per lane, stored as one
-// 16-byte vector per channel row. BatchNorm batch sums are reduced across the 4 lane groups with two
-// shuffles per tile and kept in double, then combined in fixed order like the VALU kernels.
+// 64-point group = 4 interleaved tiles: A = activations (lane: 4 consecutive points 4(l&15).., channel
+// 4s + l>>4, one 16-byte load from the channel-major [C][S] buffers feeds the 4 tiles), B = weights
+// from LDS (pitch chosen so the 64 lanes hit 64 distinct banks), D = 4 consecutive points x 1
+// channel per lane across the 4 tiles, stored as one 16-byte vector per channel row. BatchNorm batch
+// sums are reduced across the 4 lane groups with two shuffles per group and kept in double, then
+// combined in fixed order like the VALU kernels.
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 __host__ __device__ constexpr int pitch_mod(int ci, int m) { return ci + ((m - ci % 64) + 64) % 64; }
@@ -855,18 +856,23 @@ __device__ __forceinline__ float grp_sum(float v) {  // sum over the 4 lanes sha
   return v;
 }
 
-// per-channel sums of a 16-channel tile column: lanes with l>>4 == 0 write wave partials
-template <int C>
-__device__ __forceinline__ void tile_flush(const double (&s1)[C / 16], const double (&s2)[C / 16], double* part,
-                                           double* lds) {  // lds: [MFW][2][MAXC]
+// BatchNorm batch sums of the MFMA passes: each wave accumulates its channel sums in its own LDS rows
+// lds[w][2][MAXC] (double, lanes l < 16 own channel 16j + l of tile column j), then the block
+// combines the waves in fixed order into its partial row (keeps 2 * C / 16 doubles out of VGPRs).
+__device__ __forceinline__ void wave_sums_zero(double* lds) {
+  for (int j = threadIdx.x; j < MFW * 2 * MAXC; j += MFBLK) lds[j] = 0.0;
+}
+__device__ __forceinline__ void wave_sums_add(double* lds, int j, float t1, float t2) {
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  t1 = grp_sum(t1);
+  t2 = grp_sum(t2);
   if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < C / 16; ++j) {
-      lds[(w * 2 + 0) * MAXC + 16 * j + lane] = s1[j];
-      lds[(w * 2 + 1) * MAXC + 16 * j + lane] = s2[j];
-    }
+    lds[(w * 2 + 0) * MAXC + 16 * j + lane] += (double)t1;
+    lds[(w * 2 + 1) * MAXC + 16 * j + lane] += (double)t2;
   }
+}
+template <int C>
+__device__ __forceinline__ void tile_flush(double* part, const double* lds) {
   __syncthreads();
   for (int j = threadIdx.x; j < 2 * C; j += MFBLK) {
     int which = j / C, c = j - which * C;
@@ -876,8 +882,8 @@ __device__ __forceinline__ void tile_flush(const double (&s1)[C / 16], const dou
   }
 }
 
-// 4 consecutive points n..n+3 of one channel row (n % 4 == 0). Rows are S >= 16-rounded N floats
-// long and n lies in a 16-point tile that starts below N, so the 16-byte access never leaves the row:
+// 4 consecutive points n..n+3 of one channel row (n % 4 == 0). Rows are S >= 64-rounded N floats
+// long and n lies in a 64-point group (16-point block) that starts below N, so the 16-byte access never leaves the row:
 // branch-free (a tail branch per access made the compiler wait for every outstanding load at each
 // join); points >= N read as 0 and are written with whatever the caller put there (0: masked).
 __device__ __forceinline__ f32x4 ld4(const float* p, int n, int N) {
@@ -890,11 +896,31 @@ __device__ __forceinline__ void st4(float* p, int n, int N, f32x4 v) {
   (void)N;
   *(f32x4*)(p + n) = v;
 }
+// Q = 2 or 4 consecutive points of one channel row (same contract as ld4 / st4, n % Q == 0)
+template <int Q>
+using fvec = float __attribute__((ext_vector_type(Q)));
+template <int Q>
+__device__ __forceinline__ fvec<Q> ldq(const float* p, int n, int N) {
+  fvec<Q> v = *(const fvec<Q>*)(p + n);
+#pragma unroll
+  for (int i = 0; i < Q; ++i) v[i] = n + i < N ? v[i] : 0.0f;
+  return v;
+}
+template <int Q>
+__device__ __forceinline__ void stq(float* p, int n, fvec<Q> v) { *(fvec<Q>*)(p + n) = v; }
+// interleaved tiles per wave group: 4 (64 points, 16-byte accesses) while the group's activation
+// operand fits 64 VGPRs, else 2 (32 points, 8-byte accesses) — 2 waves per SIMD, no spills
+__host__ __device__ constexpr int tiles_per_group(int ks) { return ks * 4 <= 64 ? 4 : 2; }
 
-// layer l (1..4) forward: z_l = W_l relu(bn_{l-1}(z_{l-1})) + b_l, BN_l batch statistics
+// layer l (1..4) forward: z_l = W_l relu(bn_{l-1}(z_{l-1})) + b_l, BN_l batch statistics.
+// A wave owns a 64-point group as 4 interleaved MFMA tiles: tile q holds points n0 + 4m + q (m = row),
+// so the A operand of all 4 tiles for channel 4s + g is ONE 16-byte load of points n0 + 4a .. +3, and
+// the 4 tiles' D values for output row 4g + i are 4 consecutive points (one 16-byte store). Every
+// weight read from LDS feeds 4 MFMAs. Groups go to waves block-fastest (t = wave * GRID + block) so
+// each CU gets an equal share when N / 64 is not much larger than the wave count.
 template <int CI, int CO>
 __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
-  constexpr int P = pitch_mod(CI, 4), NT = CO / 16, KS = CI / 4;
+  constexpr int P = pitch_mod(CI, 4), NT = CO / 16, KS = CI / 4, TQ = tiles_per_group(KS), GP = 16 * TQ;
   __shared__ float sW[CO * P];
   __shared__ float sp[3 * CI + CO];
   __shared__ double lds[MFW * 2 * MAXC];
@@ -902,6 +928,7 @@ __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
   for (int j = threadIdx.x; j < CO * CI; j += MFBLK) sW[(j / CI) * P + j % CI] = d.W[l][j];
   for (int j = threadIdx.x; j < 3 * CI; j += MFBLK) sp[j] = d.bn[l - 1][j];
   for (int j = threadIdx.x; j < CO; j += MFBLK) sp[3 * CI + j] = d.b[l][j];
+  wave_sums_zero(lds);
   __syncthreads();
   const float* sc = sp;
   const float* sh = sp + CI;
@@ -911,53 +938,57 @@ __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
   const int lane = threadIdx.x & 63, a = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
   const float* zin = d.z[l - 1];
   float* zout = d.z[l];
-  double s1[NT], s2[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) s1[j] = s2[j] = 0.0;
-  for (int t = blockIdx.x * MFW + wv; t * 16 < N; t += GRID * MFW) {
-    const int n0 = t * 16, na = n0 + a;
-    const bool va = na < N;
-    float hv[KS];
+  for (int t = wv * GRID + blockIdx.x; t * GP < N; t += GRID * MFW) {
+    const int n0 = t * GP, na = n0 + TQ * a;
+    fvec<TQ> hv[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int c = 4 * s + g;
-      const float zv = va ? zin[(size_t)c * d.S + na] : 0.0f;
-      hv[s] = va ? fmaxf(fmaf(zv - mu[c], sc[c], sh[c]), 0.0f) : 0.0f;
+      hv[s] = ldq<TQ>(zin + (size_t)c * d.S, na, N);
+#pragma unroll
+      for (int q = 0; q < TQ; ++q) hv[s][q] = na + q < N ? fmaxf(fmaf(hv[s][q] - mu[c], sc[c], sh[c]), 0.0f) : 0.0f;
     }
-    const int nb = n0 + 4 * g;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
       const float b = bias[16 * j + a];
-      f32x4 v = (f32x4){b, b, b, b};
+      f32x4 v[TQ];
 #pragma unroll
-      for (int s = 0; s < KS; ++s)
-        v = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s], sW[(16 * j + a) * P + 4 * s + g], v, 0, 0, 0);
+      for (int q = 0; q < TQ; ++q) v[q] = (f32x4){b, b, b, b};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float w = sW[(16 * j + a) * P + 4 * s + g];
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) v[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][q], w, v[q], 0, 0, 0);
+      }
       float t1 = 0.0f, t2 = 0.0f;
+      float* row = zout + (size_t)(16 * j + a) * d.S;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        if (nb + i >= N) v[i] = 0.0f;
-        t1 += v[i];
-        t2 = fmaf(v[i], v[i], t2);
+        const int nb = n0 + TQ * (4 * g + i);
+        fvec<TQ> o;
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) {
+          o[q] = nb + q < N ? v[q][i] : 0.0f;
+          t1 += o[q];
+          t2 = fmaf(o[q], o[q], t2);
+        }
+        stq<TQ>(row, nb, o);
       }
-      st4(zout + (size_t)(16 * j + a) * d.S, nb, N, v);
-      if (d.training) {
-        s1[j] += (double)grp_sum(t1);
-        s2[j] += (double)grp_sum(t2);
-      }
+      if (d.training) wave_sums_add(lds, j, t1, t2);
       asm volatile("" ::: "memory");  // keep the next tile's B reads here (register pressure)
     }
   }
   if (!d.training) return;
-  tile_flush<CO>(s1, s2, d.part, lds);
-  if (!last_block_arrive(d.ticket + 1 + l, &lastf)) return;
+  tile_flush<CO>(d.part, lds);
+  if (!grid_col_totals(d, 1 + l, 2 * CO, lds, &lastf)) return;
   bn_finalize<CO>(d, l, lds);
 }
 
 // layer l (4..1) backward: dz_l = BN_l backward of dh_l (stored), dh_{l-1} = relu'(h_{l-1}) W_l^T dz_l,
-// BN_{l-1} backward sums (sum dh, sum dh * xhat)
+// BN_{l-1} backward sums (sum dh, sum dh * xhat). Same interleaved point groups as the forward.
 template <int CI, int CO>
 __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
-  constexpr int P = pitch_mod(CI, 16), NT = CI / 16, KS = CO / 4;
+  constexpr int P = pitch_mod(CI, 16), NT = CI / 16, KS = CO / 4, TQ = tiles_per_group(KS), GP = 16 * TQ;
   __shared__ float sW[CO * P];
   __shared__ float sp[7 * CO + 4 * CI];
   __shared__ double lds[MFW * 2 * MAXC];
@@ -973,6 +1004,7 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
     m[CO + j] = (float)(d.bnsum[l][CO + j] * invN);
     m[2 * CO + j] = d.g[l][j] * d.bn[l][3 * CO + j];
   }
+  wave_sums_zero(lds);
   __syncthreads();
   const float* bo = sp;            // scale, beta, mean, invstd of layer l
   const float* bi = sp + 4 * CO;   // of layer l-1
@@ -985,49 +1017,58 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
   const float* zl = d.z[l];
   const float* zp = d.z[l - 1];
   float* dzl = d.dz[l];
-  double s1[NT], s2[NT];
-#pragma unroll
-  for (int j = 0; j < NT; ++j) s1[j] = s2[j] = 0.0;
-  for (int t = blockIdx.x * MFW + wv; t * 16 < N; t += GRID * MFW) {
-    const int n0 = t * 16, na = n0 + a;
-    const bool va = na < N;
-    float dzv[KS];
+  for (int t = wv * GRID + blockIdx.x; t * GP < N; t += GRID * MFW) {
+    const int n0 = t * GP, na = n0 + TQ * a;
+    fvec<TQ> dzv[KS];
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int o = 4 * s + g;
-      float v = 0.0f;
-      if (va) {
-        const float xh = (zl[(size_t)o * d.S + na] - bo[2 * CO + o]) * bo[3 * CO + o];
-        v = gi[o] * (dhin[(size_t)o * d.S + na] - m1[o] - xh * m2[o]);
-        dzl[(size_t)o * d.S + na] = v;
+      const fvec<TQ> zv = ldq<TQ>(zl + (size_t)o * d.S, na, N);
+      const fvec<TQ> dv = ldq<TQ>(dhin + (size_t)o * d.S, na, N);
+#pragma unroll
+      for (int q = 0; q < TQ; ++q) {
+        const float xh = (zv[q] - bo[2 * CO + o]) * bo[3 * CO + o];
+        dzv[s][q] = na + q < N ? gi[o] * (dv[q] - m1[o] - xh * m2[o]) : 0.0f;
       }
-      dzv[s] = v;
+      stq<TQ>(dzl + (size_t)o * d.S, na, dzv[s]);
+      if (s % 8 == 7) asm volatile("" ::: "memory");  // bound the loads in flight (register pressure)
     }
-    const int nb = n0 + 4 * g;
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
-      f32x4 v = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
-#pragma unroll
-      for (int s = 0; s < KS; ++s)
-        v = __builtin_amdgcn_mfma_f32_16x16x4f32(dzv[s], sW[(4 * s + g) * P + 16 * j + a], v, 0, 0, 0);
       const int c = 16 * j + a;
-      const f32x4 zc = ld4(zp + (size_t)c * d.S, nb, N);
+      fvec<TQ> zc[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) zc[i] = ldq<TQ>(zp + (size_t)c * d.S, n0 + TQ * (4 * g + i), N);
+      f32x4 v[TQ];
+#pragma unroll
+      for (int q = 0; q < TQ; ++q) v[q] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+      for (int s = 0; s < KS; ++s) {
+        const float w = sW[(4 * s + g) * P + c];
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) v[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(dzv[s][q], w, v[q], 0, 0, 0);
+      }
       float t1 = 0.0f, t2 = 0.0f;
+      float* row = dhout + (size_t)c * d.S;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const float hv = fmaxf(fmaf(zc[i] - bi[2 * CI + c], bi[c], bi[CI + c]), 0.0f);
-        v[i] = (nb + i < N && hv > 0.0f) ? v[i] : 0.0f;
-        t1 += v[i];
-        t2 += v[i] * ((zc[i] - bi[2 * CI + c]) * bi[3 * CI + c]);
+        const int nb = n0 + TQ * (4 * g + i);
+        fvec<TQ> o;
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) {
+          const float hv = fmaxf(fmaf(zc[i][q] - bi[2 * CI + c], bi[c], bi[CI + c]), 0.0f);
+          o[q] = (nb + q < N && hv > 0.0f) ? v[q][i] : 0.0f;
+          t1 += o[q];
+          t2 += o[q] * ((zc[i][q] - bi[2 * CI + c]) * bi[3 * CI + c]);
+        }
+        stq<TQ>(row, nb, o);
       }
-      st4(dhout + (size_t)c * d.S, nb, N, v);
-      s1[j] += (double)grp_sum(t1);
-      s2[j] += (double)grp_sum(t2);
+      wave_sums_add(lds, j, t1, t2);
       asm volatile("" ::: "memory");  // keep the next tile's B reads here (register pressure)
     }
   }
-  tile_flush<CI>(s1, s2, d.part, lds);
-  if (!last_block_arrive(d.ticket + 7 + (5 - l), &lastf)) return;
+  tile_flush<CI>(d.part, lds);
+  if (!grid_col_totals(d, 7 + (5 - l), 2 * CI, lds, &lastf)) return;
   bnb_finalize<CI>(d, l - 1, lds);
 }
 
@@ -1129,14 +1170,14 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad_mf(Dev d, MfJobs J) {
 
 // ------------------------------------------------------------------ host side
 static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
-// channel stride of the SoA activation buffers: whole 16-point MFMA tiles, 16-byte aligned rows
+// channel stride of the SoA activation buffers: whole 64-point MFMA groups, 16-byte aligned rows
 static inline size_t chan_stride(int rows, int slots) {
   size_t n = (size_t)rows * slots;
-  return n < 16 ? 16 : (n + 15) & ~(size_t)15;
+  return n < 64 ? 64 : (n + 63) & ~(size_t)63;
 }
 
 struct Layout {
-  size_t off, list, meta, xs, z[5], bn[5], bnsum[5], part, pstat, ticket, dz[6], dh[2], dsig, da,
+  size_t off, list, meta, xs, z[5], bn[5], bnsum[5], part, gpart, pstat, ticket, dz[6], dh[2], dsig, da,
       aact, wpart, scan_tmp, scan_bytes, total;
 };
 
@@ -1198,7 +1239,8 @@ static int make_layout(const rpc_perturber_cfg* cfg, int rows, int slots, Layout
   for (int l = 0; l < 5; ++l) { L->bnsum[l] = o; o += al(sizeof(double) * 2 * C[l + 1]); }
   L->part = o; o += al(sizeof(double) * GRID * 2 * MAXC);
   L->pstat = o; o += al(sizeof(float) * 4 * MAXF);
-  L->ticket = o; o += al(sizeof(unsigned) * NTICKET);
+  L->ticket = o; o += al(sizeof(unsigned) * NTICKET * TSTRIDE);
+  L->gpart = o; o += al(sizeof(double) * NGRP * 2 * MAXC);
   for (int l = 0; l < 5; ++l) { L->dz[l] = o; o += al(sizeof(float) * Nmax * C[l + 1]); }
   L->dz[5] = o; o += al(sizeof(float) * Nmax * cfg->F);
   int cmax = 0;
@@ -1288,6 +1330,7 @@ static int fill_dev(const rpc_perturber_cfg* cfg, const float* const* P, const f
     d.bnsum[l] = (double*)(w + L.bnsum[l]);
   }
   d.part = (double*)(w + L.part);
+  d.gpart = (double*)(w + L.gpart);
   d.pstat = (float*)(w + L.pstat);
   d.ticket = (unsigned*)(w + L.ticket);
   for (int l = 0; l < 6; ++l) d.dz[l] = (float*)(w + L.dz[l]);
@@ -1415,7 +1458,7 @@ extern "C" int rpc_perturber_forward(const rpc_perturber_cfg* cfg, const float* 
   d.out = out;
   d.vfe = vfe_out;
   d.losses = losses;
-  RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET, st));
+  RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET * TSTRIDE, st));
   if (d.fused) {
     ValidCount vc{x, slots, cfg->F, rows};
     CountIt it(hipcub::CountingInputIterator<int>(0), vc);
@@ -1466,7 +1509,7 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
   if (rc) return rc;
   d.dout = dout;
   d.dl = dlosses;
-  RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET, st));
+  RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET * TSTRIDE, st));
   const int F = cfg->F;
   rc = F == 4 ? launch_last<4>(d.C[5], d, st, true) : launch_last<5>(d.C[5], d, st, true);
   if (rc) return rc;

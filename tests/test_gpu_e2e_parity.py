@@ -16,12 +16,17 @@ Oracle (host):   oracle/voxelize_ref.c -> the SAME plugin AdversarialVoxelNet.lo
 
 Tolerances (north_star: "voxel indices bit-exact, perturbed coords and detection losses within
 1e-4 fp32"): voxels / coors / num_points bit-exact; perturbed point coordinates max |d| <= 1e-4;
-every loss_* key and perturbation_l2_norm |d| <= 1e-4 * max(1, |ref|); parameter gradients by
-relative L2 per tensor <= 1e-2 and cosine >= 0.9999: the gradient path crosses ~25 train-mode
-BatchNorm layers, whose batch statistics amplify fp32 summation-order differences — torch's own fp32
-SECOND/FPN is 5-6e-3 (relative L2) from a float64 evaluation at this shape
-(tests/test_gpu_dense_bev.py::test_second_fpn_config_shape_fp32_engine_and_bf16_bounds), and the
-oracle's dense part is torch fp32 too.
+every loss_* key and perturbation_l2_norm |d| <= 1e-4 * max(1, |ref|). Parameter gradients: the
+gradient path crosses ~25 train-mode BatchNorm layers, whose batch statistics amplify fp32
+summation-order differences — torch's own fp32 SECOND/FPN is 5-6e-3 (relative L2) from a float64
+evaluation at this shape (tests/test_gpu_dense_bev.py::test_second_fpn_config_shape_fp32_engine_and_bf16_bounds),
+so two correct fp32 evaluations (HIP, and the fp32 oracle whose dense part is torch fp32) differ by
+up to ~1e-2 depending on how their rounding happens to correlate. The oracle composition is
+therefore also run with float64 sparse encoder / SECOND / FPN, and each parameter gradient must be
+(a) within relative L2 2e-2, cosine >= 0.9998 of the fp32 oracle and (b) within relative L2 1e-2 of
+the float64 oracle, with the mean over all gradient tensors <= 2e-3 — as close to the exact step as
+an fp32 evaluation of it gets (the fp32 oracle itself: mean 4.8e-3 / max 1.2e-2 for 3 classes,
+2.3e-4 / 1.1e-3 for Car; HIP: 1.7e-3 / 5.7e-3 and 4.6e-4 / 2.6e-3, profiles/r02_e2e_parity_fp32.log).
 """
 import copy
 
@@ -44,7 +49,9 @@ from robustpointclouds_amd.trainer import Trainer, make_kitti_model
 pytestmark = pytest.mark.gpu
 B = 6
 LOSS_TOL = 1e-4
-GRAD_REL = 1e-2
+GRAD_REL = 2e-2
+GRAD_F64_MAX = 1e-2
+GRAD_F64_MEAN = 2e-3
 
 
 class _VFE(nn.Module):            # upstream HardSimpleVFE formula (…3class.py:17)
@@ -53,12 +60,12 @@ class _VFE(nn.Module):            # upstream HardSimpleVFE formula (…3class.py
 
 
 class _Middle(nn.Module):
-    def __init__(self, enc):
+    def __init__(self, enc, dtype):
         super().__init__()
-        self.enc = enc
+        self.enc, self.dtype = enc, dtype
 
     def forward(self, feats, coors, batch_size):
-        return self.enc.forward(feats.float(), coors.numpy(), batch_size).float()
+        return self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size).to(self.dtype)
 
 
 class _Adversary(nn.Module):
@@ -114,6 +121,65 @@ def _cos(a, b):
     return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-30))
 
 
+class _Oracle:
+    """The oracle composition of the step at one dtype for the sparse encoder / SECOND / FPN (the
+    perturber and head restatements are float64 in both)."""
+
+    def __init__(self, model, hidden, w, dtype):
+        self.dtype = dtype
+        self.enc = OracleSparseEncoder(model.middle_encoder, dtype=dtype)
+        self.backbone = copy.deepcopy(model.backbone).cpu().to(dtype)
+        self.neck = copy.deepcopy(model.neck).cpu().to(dtype)
+        self.backbone.hip = self.neck.hip = False
+        self.ref = AdversarialVoxelNet(adversary_cfg=dict(type="VoxelPerturber", hidden_channels=list(hidden)),
+                                       regularization_weight=model.regularization_weight, voxel_encoder=_VFE(),
+                                       middle_encoder=_Middle(self.enc, dtype), backbone=self.backbone,
+                                       neck=self.neck, bbox_head=_Head(model.bbox_head, 200, 176))
+        self.op = OraclePerturber(w, 4, hidden, dtype=torch.float64)
+        self.ref.adversary = _Adversary(self.op)
+        self.ref.train()
+        self.ref._epoch = 3
+
+    def step(self, rv, rn, rc, cb, cl, B):
+        rbatch = dict(voxels=dict(voxels=torch.from_numpy(rv).to(self.dtype), num_points=torch.from_numpy(rn),
+                                  coors=torch.from_numpy(rc)), batch_size=B)
+        self.losses = self.ref.loss(rbatch, dict(gt_boxes=cb, gt_labels=cl))
+        self.total, _ = parse_losses(self.losses)
+        self.total.backward()
+
+    def grads(self, nlin, natt, nbn):
+        out = []
+        g = self.op.grads()
+        out += [g[f"dW{l}"] for l in range(nlin)] + [g[f"dWa{l}"] for l in range(natt)]
+        out += [g[f"dg{l}"] for l in range(nbn)]
+        for p in self.enc.params:
+            out += [p["W"].grad, p["g"].grad]
+        out += [p.grad for p in self.backbone.parameters()] + [p.grad for p in self.neck.parameters()]
+        hw = torch.split(self.ref.bbox_head.w.grad, self.ref.bbox_head.splits)
+        hb = torch.split(self.ref.bbox_head.b.grad, self.ref.bbox_head.splits)
+        for gw, gbias in zip(hw, hb):
+            out += [gw, gbias]
+        return out
+
+
+def _hip_grads(model):
+    """(name, grad) in the order of _Oracle.grads()."""
+    adv = model.adversary
+    lin = [m for m in adv.model if isinstance(m, nn.Linear)]
+    bns = [m for m in adv.model if isinstance(m, nn.BatchNorm1d)]
+    att = [m for m in adv.attention if isinstance(m, nn.Linear)]
+    out = [(f"adversary.W{l}", m.weight.grad) for l, m in enumerate(lin)]
+    out += [(f"adversary.Wa{l}", m.weight.grad) for l, m in enumerate(att)]
+    out += [(f"adversary.g{l}", m.weight.grad) for l, m in enumerate(bns)]
+    for i, m in enumerate(model.middle_encoder.layers()):
+        out += [(f"middle.{i}.W", m[0].weight.grad), (f"middle.{i}.gamma", m[1].weight.grad)]
+    out += [(f"backbone.{n}", p.grad) for n, p in model.backbone.named_parameters()]
+    out += [(f"neck.{n}", p.grad) for n, p in model.neck.named_parameters()]
+    for c in model.bbox_head._convs():
+        out += [("head.weight", c.weight.grad), ("head.bias", c.bias.grad)]
+    return out
+
+
 @pytest.mark.parametrize("classes", [3, 1])
 def test_adversarial_step_fp32_hip_matches_oracle(classes):
     dev = torch.device("cuda")
@@ -124,20 +190,10 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
     hidden = model.adversary.hidden_channels
     pts, boxes, labels = kitti_batch(B, seed0=500 + 10 * classes, num_classes=classes)
 
-    # ---- oracle model, built from the GPU model's initial weights
-    w, lin, bns, att = _perturber_weights(model.adversary)
-    enc = OracleSparseEncoder(model.middle_encoder, dtype=torch.float32)
-    backbone = copy.deepcopy(model.backbone).cpu().float()
-    neck = copy.deepcopy(model.neck).cpu().float()
-    backbone.hip = neck.hip = False
-    ref = AdversarialVoxelNet(adversary_cfg=dict(type="VoxelPerturber", hidden_channels=list(hidden)),
-                              regularization_weight=model.regularization_weight, voxel_encoder=_VFE(),
-                              middle_encoder=_Middle(enc), backbone=backbone, neck=neck,
-                              bbox_head=_Head(model.bbox_head, 200, 176))
-    op = OraclePerturber(w, 4, hidden, dtype=torch.float64)
-    ref.adversary = _Adversary(op)
-    ref.train()
-    ref._epoch = 3
+    # ---- oracle models (fp32 and float64), built from the GPU model's initial weights
+    w = _perturber_weights(model.adversary)[0]
+    o32 = _Oracle(model, hidden, w, torch.float32)
+    o64 = _Oracle(model, hidden, w, torch.float64)
 
     # ---- HIP step
     gpts = [torch.from_numpy(p).to(dev) for p in pts]
@@ -161,15 +217,13 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
     dp = (model._last_perturbed_voxels.cpu().double() - rpert).abs().max().item()
     assert dp <= 1e-4, dp
 
-    # ---- oracle step
+    # ---- oracle steps
     cb, cl = pack_gt(list(zip(boxes, labels)), torch.device("cpu"))
-    rbatch = dict(voxels=dict(voxels=torch.from_numpy(rv), num_points=torch.from_numpy(rn),
-                              coors=torch.from_numpy(rc)), batch_size=B)
-    rlosses = ref.loss(rbatch, dict(gt_boxes=cb, gt_labels=cl))
-    rtotal, rlog = parse_losses(rlosses)
-    rtotal.backward()
+    o32.step(rv, rn, rc, cb, cl, B)
+    o64.step(rv, rn, rc, cb, cl, B)
+    rlosses, rtotal = o32.losses, o32.total
 
-    # ---- losses: every key within 1e-4
+    # ---- losses: every key within 1e-4 of the fp32 oracle
     assert set(losses) == set(rlosses), (sorted(losses), sorted(rlosses))
     report = {}
     for k in rlosses:
@@ -181,34 +235,26 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
     assert abs(float(total) - float(rtotal)) <= LOSS_TOL * max(1.0, abs(float(rtotal)))
     print("losses (hip, oracle):", report)
 
-    # ---- gradients
-    checks = []
-    g = op.grads()
-    for l, m in enumerate(lin):
-        checks.append((f"adversary.W{l}", m.weight.grad, g[f"dW{l}"]))
-    for l, m in enumerate(att):
-        checks.append((f"adversary.Wa{l}", m.weight.grad, g[f"dWa{l}"]))
-    for l, m in enumerate(bns):
-        checks.append((f"adversary.g{l}", m.weight.grad, g[f"dg{l}"]))
-    for i, m in enumerate(model.middle_encoder.layers()):
-        p = enc.params[i]
-        checks.append((f"middle.{i}.W", m[0].weight.grad, p["W"].grad))
-        checks.append((f"middle.{i}.gamma", m[1].weight.grad, p["g"].grad))
-    for (n, pg), (n2, pr) in zip(model.backbone.named_parameters(), backbone.named_parameters()):
-        checks.append((f"backbone.{n}", pg.grad, pr.grad))
-    for (n, pg), (n2, pr) in zip(model.neck.named_parameters(), neck.named_parameters()):
-        checks.append((f"neck.{n}", pg.grad, pr.grad))
-    hw = torch.split(ref.bbox_head.w.grad, ref.bbox_head.splits)
-    hb = torch.split(ref.bbox_head.b.grad, ref.bbox_head.splits)
-    for c, gw, gbias in zip(model.bbox_head._convs(), hw, hb):
-        checks.append(("head.weight", c.weight.grad, gw))
-        checks.append(("head.bias", c.bias.grad, gbias))
+    # ---- gradients: against the fp32 oracle, and no further from the float64 oracle than it is
+    _, lin, bns, att = _perturber_weights(model.adversary)
+    hg = _hip_grads(model)
+    g32, g64 = o32.grads(len(lin), len(att), len(bns)), o64.grads(len(lin), len(att), len(bns))
+    assert len(hg) == len(g32) == len(g64)
     worst = []
-    for name, a, r in checks:
-        assert a is not None and r is not None, name
-        rel, cos = _rel(a.cpu(), r.cpu()), _cos(a.cpu(), r.cpu())
-        worst.append((rel, name, cos))
+    for (name, a), r, r64 in zip(hg, g32, g64):
+        assert a is not None and r is not None and r64 is not None, name
+        a = a.cpu()
+        rel, cos = _rel(a, r.cpu()), _cos(a, r.cpu())
+        e_hip, e_ora = _rel(a, r64), _rel(r.cpu(), r64)
+        worst.append((rel, name, cos, e_hip, e_ora))
     worst.sort(reverse=True)
-    print("worst gradient rel-L2:", worst[:6])
-    for rel, name, cos in worst:
-        assert rel <= GRAD_REL and cos >= 0.9999, (name, rel, cos)
+    print("worst gradient rel-L2 (vs fp32 oracle, cos, hip vs f64, fp32 oracle vs f64):", worst[:6])
+    ora_level = max(w[4] for w in worst)
+    mean_hip = sum(w[3] for w in worst) / len(worst)
+    mean_ora = sum(w[4] for w in worst) / len(worst)
+    print(f"vs float64: hip mean {mean_hip:.2e} max {max(w[3] for w in worst):.2e}; "
+          f"fp32 oracle mean {mean_ora:.2e} max {ora_level:.2e}")
+    for rel, name, cos, e_hip, e_ora in worst:
+        assert rel <= GRAD_REL and cos >= 0.9998, (name, rel, cos)
+        assert e_hip <= GRAD_F64_MAX, (name, e_hip, e_ora)
+    assert mean_hip <= GRAD_F64_MEAN, (mean_hip, mean_ora)

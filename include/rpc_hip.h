@@ -236,7 +236,8 @@ int rpc_dense_conv(int map, const void* src, int src_pitch, int cin, const void*
 int rpc_dense_conv_blocks(int map, const int* row_img);
 /* kernel-selection knob for A/B measurement (returns the previous value; value < 0 only reads it):
  * knob 0 = the S1 kernel for output channels that are a multiple of 128 (0: chosen by shape, default;
- * 1: the 64-channel register-staged kernel; 2: the 128-channel LDS-DMA kernel) */
+ * 1: the 64-channel register-staged kernel; 2: the 128-channel LDS-DMA kernel); knob 1 = the S1 weight
+ * gradient for 128-multiple channels (0: tap-sharing row-segment kernel, default; 1: per-tap kernel) */
 int rpc_dense_tune(int knob, int value);
 /* dW (torch layout; kind 0 = Conv2d [co][ci][kh][kw], 1 = ConvTranspose2d [ci][co][kh][kw]) of the
  * forward map (S1/S2/P1/U2): sum over rows of x[src_row(row,t)][ci] * dz[row][co]; ci, co % 128 == 0 */

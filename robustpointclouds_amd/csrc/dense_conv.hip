@@ -864,6 +864,220 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad(WG g) {
       }
 }
 
+// ------------------------------------------------------------------ 3x3 stride-1 weight gradient, taps sharing tiles
+// k_wgrad_s1: dW[t][ci][co] = sum_m x[src(m, t)][ci] dz[m][co] for the S1 map, with the output pixels
+// walked as SEG-pixel segments of one image row. A segment's dz tile (SEG rows) and its x tile of the
+// input row y + dy - 1 (SEG + 2 rows: columns x0 - 1 .. x0 + SEG, zero outside the image) feed all three
+// taps (dy, 0..2) of that row: tap dx reads x rows r + dx for output row r, so no per-tap masking is
+// needed (a segment never crosses an image row) and every staged byte serves 3 taps (k_wgrad stages
+// both operands once per tap). Block = (chunk of segments, dy, 128 x 128 (ci, co) tile), 8 waves as
+// 4 (ci, 32 each) x 2 (co, 64 each), each with 3 taps x 2 x 4 MFMA accumulator tiles (96 AGPRs; two
+// waves per SIMD, so one wave's LDS reads overlap the other's MFMAs).
+// Staging is LDS-DMA only, into a ring of WS_ST segment stages issued WS_ST - 1 segments ahead (no
+// VGPR round trip: the register-staged form of this kernel was bound by its one-segment-ahead
+// prefetch). Rows are unpadded 256-byte images whose 16-byte granules are XOR-swizzled by
+// ((row & 7) << 1) through the DMA's per-lane source address, which makes the transposed 8-byte
+// operand reads (ds_read_b64_tr_b16) of any 8 consecutive rows conflict-free. Every wave issues the
+// same number of DMA instructions per segment (surplus ones repeat the last: same bytes, same place),
+// so one counted vmcnt per segment retires exactly that segment's tiles before the barrier. Segments
+// whose source row y + dy - 1 lies outside the image are skipped (walked with counters, no
+// divisions); pixels past the row end are zero rows. Partial sums go to part[chunk][t][ci][co] like
+// k_wgrad (same k_wgrad_reduce).
+constexpr int WS_ST = 4;    // ring stages
+// ds_read_b64_tr_b16 at an LDS byte address, as inline asm (the caller waits on lgkmcnt)
+__device__ __forceinline__ s16x4 tr_read_asm(unsigned addr) {
+  s16x4 r;
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(r) : "v"(addr));
+  return r;
+}
+constexpr int WSB = 512;    // threads
+template <int SEG>
+__global__ __launch_bounds__(WSB, 1) void k_wgrad_s1(WG g, int nseg_x, int seg_per) {
+  constexpr int TC = 128, RB = 256;                              // 256-byte rows (128 bf16 channels)
+  constexpr int NWI = 2, NWJ = 4;                                // 16x16 tiles per wave (ci, co)
+  constexpr int XR = SEG + 2, NX = (XR + 3) / 4, ND = SEG / 4;   // DMA instructions (4 rows each)
+  constexpr int NI = NX + ND, PW = (NI + 7) / 8;                 // per segment, per wave
+  constexpr int XB = NX * 4 * RB, STB = XB + SEG * RB;           // x tile bytes, stage bytes
+  static_assert(SEG % 32 == 0 && WS_ST * STB <= 160 * 1024, "segment");
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[WS_ST * STB];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wci = w >> 1, wco = w & 1;
+  const int nco = g.CO / TC, ntile = (g.CI / TC) * nco;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = lid / (3 * ntile), rest = lid - chunk * (3 * ntile);
+  const int dy = rest / ntile, tile = rest - dy * ntile;
+  const int ci0 = (tile / nco) * TC, co0 = (tile % nco) * TC;
+  const int H = g.R.H, W = g.R.W;
+  const int nseg = g.R.B * H * nseg_x;
+  const int sg0 = min(nseg, chunk * seg_per), sg1 = min(nseg, sg0 + seg_per);
+  const bool skip_top = dy == 0, skip_bot = dy == 2;   // source row outside the image at y = 0 / H - 1
+
+  // ---- segment walk (uniform): position of segment sg0, count of valid segments
+  int cx = sg0 % nseg_x, cby = sg0 / nseg_x;
+  int cy = cby % H, cb = cby / H;
+  int nvalid = 0;
+  {
+    int y = cy, left = sg1 - sg0, xs = cx;
+    while (left > 0) {
+      const int n = min(left, nseg_x - xs);
+      if (!((skip_top && y == 0) || (skip_bot && y == H - 1))) nvalid += n;
+      left -= n;
+      xs = 0;
+      if (++y == H) y = 0;
+    }
+  }
+  int ileft = sg1 - sg0;   // segments not yet passed by the issue cursor
+  auto skip_invalid = [&]() {
+    while (ileft > 0 && ((skip_top && cy == 0) || (skip_bot && cy == H - 1))) {
+      ileft -= nseg_x - cx;
+      cx = 0;
+      if (++cy == H) { cy = 0; ++cb; }
+    }
+  };
+  auto advance = [&]() {
+    --ileft;
+    if (++cx == nseg_x) {
+      cx = 0;
+      if (++cy == H) { cy = 0; ++cb; }
+    }
+  };
+
+  // ---- DMA: instruction k = w + 8m covers rows 4k' .. 4k' + 3 of the x (k < NX) or dz (k' = k - NX)
+  // tile; lane L writes row 4k' + L / 16, slot L % 16 = granule ^ swz(row)
+  // per-lane constants of each DMA instruction (g's fields copied to registers first: reading them
+  // inside the loop went through memory and made the compiler wait for every DMA in flight)
+  const u16* const gx = g.x;
+  const u16* const gdz = g.dz;
+  const int XP = g.XP, DP = g.DP;
+  const u16* lbase[PW];
+  int lrow[PW], lpitch[PW], ladj[PW], llim[PW], kslot[PW];
+  bool isx[PW];
+#pragma unroll
+  for (int m = 0; m < PW; ++m) {
+    const int k = min(w + 8 * m, NI - 1);
+    isx[m] = k < NX;
+    kslot[m] = k;
+    lrow[m] = 4 * (isx[m] ? k : k - NX) + (lane >> 4);
+    const int gsrc = ((lane & 15) ^ ((lrow[m] & 7) << 1)) * 8;   // source channel offset of the granule
+    lbase[m] = isx[m] ? gx + ci0 + gsrc : gdz + co0 + gsrc;
+    lpitch[m] = isx[m] ? XP : DP;
+    ladj[m] = isx[m] ? -1 : 0;
+    llim[m] = isx[m] ? XR : SEG;
+  }
+  int lastx = 0, lasty = 0, lastb = 0;
+  auto issue = [&](int st) {
+    // the cursor's segment, or (past the end) the last one again into a stage that is never read
+    const bool have = ileft > 0;
+    const int xs = have ? cx : lastx, y = have ? cy : lasty, b = have ? cb : lastb;
+    lastx = xs; lasty = y; lastb = b;
+    const int x0 = xs * SEG;
+    const int xrow0 = (b * H + y + dy - 1) * W, drow0 = (b * H + y) * W;
+    unsigned char* base = lds + st * STB;
+#pragma unroll
+    for (int m = 0; m < PW; ++m) {
+      const int xc = x0 + lrow[m] + ladj[m];
+      const bool ok = lrow[m] < llim[m] && xc >= 0 && xc < W;
+      const int row = (isx[m] ? xrow0 : drow0) + xc;
+      const u16* src = ok ? lbase[m] + (size_t)row * lpitch[m] : (const u16*)g_zero_row;
+      glds16(src, base + kslot[m] * 1024);
+    }
+    if (have) {
+      advance();
+      skip_invalid();
+    }
+  };
+
+  // ---- operand addresses: transposed reads of rows r0 (+16) (+dx), r0 = 32 ks + 4 (lane >> 4) + (lane & 15) / 4,
+  // 4 channels 4 (lane & 3) of a 16-column block; granule ((c >> 3) ^ swz(row)), byte 8 (lane & 1) in it
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, rowoff = 4 * g4 + qq;
+  int aoff[3][NWI], boff[NWJ];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int sw = ((rowoff + dx) & 7) << 1;
+#pragma unroll
+    for (int i = 0; i < NWI; ++i) {
+      const int gr = ((wci * 32 + i * 16) >> 3) + (pp >> 1);
+      aoff[dx][i] = (rowoff + dx) * RB + ((gr ^ sw) << 4) + 8 * (pp & 1);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NWJ; ++j) {
+    const int gr = ((wco * 64 + j * 16) >> 3) + (pp >> 1);
+    boff[j] = XB + rowoff * RB + ((gr ^ ((rowoff & 7) << 1)) << 4) + 8 * (pp & 1);
+  }
+
+  f32x4 acc[3][NWI][NWJ];
+#pragma unroll
+  for (int t = 0; t < 3; ++t)
+#pragma unroll
+    for (int i = 0; i < NWI; ++i)
+#pragma unroll
+      for (int j = 0; j < NWJ; ++j) acc[t][i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  if (nvalid > 0) {
+    skip_invalid();
+#pragma unroll
+    for (int st = 0; st < WS_ST - 1; ++st) issue(st);
+    int st = 0;
+    const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) unsigned char*)lds);
+    for (int k = 0; k < nvalid; ++k) {
+      // retire this segment's DMAs (the WS_ST - 2 younger segments stay in flight), then publish
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((WS_ST - 2) * PW) : "memory");
+      // refill the stage computed last iteration (every wave has passed this barrier after reading it)
+      issue(st == 0 ? WS_ST - 1 : st - 1);
+      const unsigned base = lds0 + st * STB;
+#pragma unroll
+      for (int ks = 0; ks < SEG / 32; ++ks) {
+        // operand reads as inline asm: the compiler cannot tell the transposed-read intrinsic apart
+        // from the DMA-written stages in flight and put a vmcnt(0) (every DMA, the look-ahead too)
+        // before it. The asm wait below ties the fragments, so no MFMA is scheduled above it.
+        bf16x8 bv[NWJ], av[3][NWI];
+#pragma unroll
+        for (int j = 0; j < NWJ; ++j) {
+          const unsigned pb = base + boff[j] + 32 * ks * RB;
+          s16x4 v[2] = {tr_read_asm(pb), tr_read_asm(pb + 16 * RB)};
+          bv[j] = *(bf16x8*)v;
+        }
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int i = 0; i < NWI; ++i) {
+            const unsigned pa = base + aoff[dx][i] + 32 * ks * RB;
+            s16x4 v[2] = {tr_read_asm(pa), tr_read_asm(pa + 16 * RB)};
+            av[dx][i] = *(bf16x8*)v;
+          }
+        static_assert(NWI == 2 && NWJ == 4, "operand tie list");
+        asm volatile("s_waitcnt lgkmcnt(0)"
+                     : "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(av[0][0]), "+v"(av[0][1]),
+                       "+v"(av[1][0]), "+v"(av[1][1]), "+v"(av[2][0]), "+v"(av[2][1]));
+#pragma unroll
+        for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+          for (int i = 0; i < NWI; ++i)
+#pragma unroll
+            for (int j = 0; j < NWJ; ++j)
+              acc[dx][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[dx][i], bv[j], acc[dx][i][j], 0, 0, 0);
+      }
+      st = st == WS_ST - 1 ? 0 : st + 1;
+    }
+    // drain the look-ahead DMAs before the block exits
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    float* out = g.part + ((size_t)chunk * 9 + dy * 3 + dx) * g.CI * g.CO;
+#pragma unroll
+    for (int i = 0; i < NWI; ++i)
+#pragma unroll
+      for (int j = 0; j < NWJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int ci = ci0 + wci * 32 + i * 16 + 4 * g4 + r, co = co0 + wco * 64 + j * 16 + (lane & 15);
+          out[(size_t)ci * g.CO + co] = acc[dx][i][j][r];
+        }
+  }
+}
+
 // ------------------------------------------------------------------ BatchNorm passes (8 channels / thread)
 // Every pass maps a 256-thread block to (256 / CG) row lanes x CG channel groups of 8 (CG = C / 8),
 // so a thread keeps its 8 channels' BatchNorm parameters in registers for all of its rows, and
@@ -1131,6 +1345,7 @@ static unsigned ew_blocks(long long m, int c) {
 // 64-channel blocks per CU overlap each other's prologue / epilogue; the 200x176 layers' 858 tiles are
 // 0.84 of 4 rounds for either kernel, and there the register-staged kernel measured 3-8 % faster).
 static int g_s1_variant = 0;
+static int g_wgrad_variant = 0;   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
 static bool s1_wide(int tiles, int cout) {
   if (cout % 128 || g_s1_variant == 1) return false;
@@ -1144,6 +1359,11 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   if (knob == 0) {
     const int old = g_s1_variant;
     if (value >= 0) g_s1_variant = value;
+    return old;
+  }
+  if (knob == 1) {
+    const int old = g_wgrad_variant;
+    if (value >= 0) g_wgrad_variant = value;
     return old;
   }
   return RPC_ERR_ARG;
@@ -1217,7 +1437,15 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
   }
   const int rows_per = ((M + chunks - 1) / chunks + 63) / 64 * 64;
   WG g{(const u16*)x, xp, (const u16*)dz, dp, ci, co, R, S, O, M, rows_per, part};
-  switch (map) {
+  if (map == M_S1 && ci % 128 == 0 && co % 128 == 0 && g_wgrad_variant == 0) {
+    // tap-sharing row-segment kernel: segment length with the least padding of the image row
+    const int seg = (R.W + 63) / 64 * 64 <= (R.W + 31) / 32 * 32 ? 64 : 32;
+    const int nsx = (R.W + seg - 1) / seg, nseg = R.B * R.H * nsx;
+    const int seg_per = (nseg + chunks - 1) / chunks;
+    const dim3 grid(chunks * 3 * (ci / 128) * (co / 128));
+    if (seg == 64) hipLaunchKernelGGL(k_wgrad_s1<64>, grid, dim3(WSB), 0, st, g, nsx, seg_per);
+    else hipLaunchKernelGGL(k_wgrad_s1<32>, grid, dim3(WSB), 0, st, g, nsx, seg_per);
+  } else switch (map) {
     case M_S1: launch_wgrad<M_S1>(g, chunks, st); break;
     case M_S2: launch_wgrad<M_S2>(g, chunks, st); break;
     case M_P1: launch_wgrad<M_P1>(g, chunks, st); break;

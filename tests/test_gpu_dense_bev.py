@@ -372,3 +372,35 @@ def test_s1_lds_dma_kernel_bitexact_vs_register_staged(ci, co, B, H, W):
         assert torch.equal(a, b)
     ref = F.conv2d(x.double(), Wt.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
     _close_bf16(outs[0][0], ref)
+
+
+@pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 1, 200, 176), (256, 256, 1, 100, 88), (256, 128, 2, 37, 45),
+                                         (128, 128, 2, 17, 70), (128, 256, 1, 5, 130)])
+def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):
+    """k_wgrad_s1 (row segments, 3 taps per staged tile) against float64 torch at 1e-5 of the gradient
+    scale, and against the per-tap kernel k_wgrad (rpc_dense_tune knob 1) — same bf16 products, fp32
+    sums in another order: within 2e-6 of the scale."""
+    lib = _ffi.load()
+    x = _rand(B, ci, H, W, seed=31)
+    dz = _rand(B, co, H, W, seed=32)
+    Wt = _rand(co, ci, 3, 3, seed=33, scale=0.05)
+    wr = Wt.double().requires_grad_(True)
+    F.conv2d(x.double(), wr, padding=1).backward(dz.double())
+    img = _ffi.int_arr((B, H, W))
+    wsz = lib.rpc_dense_wgrad_workspace_size(S1, img, ci, co)
+    ws = _ffi.workspace(wsz, DEV)
+    xn, dn = _nhwc(x), _nhwc(dz)
+    outs = []
+    for variant in (0, 1):
+        old = lib.rpc_dense_tune(1, variant)
+        try:
+            dW = torch.full(Wt.shape, float("nan"), dtype=torch.float32, device=DEV)
+            _ffi.check(lib.rpc_dense_wgrad(S1, 0, _ffi.ptr(xn), ci, ci, _ffi.ptr(dn), co, co, img, img, img,
+                                           _ffi.ptr(dW), _ffi.ptr(ws), wsz, _ffi.stream_of(dW)), "rpc_dense_wgrad")
+            torch.cuda.synchronize()
+        finally:
+            lib.rpc_dense_tune(1, old)
+        outs.append(dW.double().cpu())
+    scale = wr.grad.abs().max().item()
+    assert (outs[0] - wr.grad).abs().max().item() <= 1e-5 * scale
+    assert (outs[0] - outs[1]).abs().max().item() <= 2e-6 * scale

@@ -73,6 +73,38 @@ int rpc_vfe_mean_backward(const float* dout, const int* num_points, int num_voxe
                           int max_points, int num_features, int vfe_features,
                           float* dvoxels, void* stream);
 
+/* ------------------------------------------------------------------ ★ HardVFE (PointNet MLP + max)
+ * Replaces upstream mmdet3d `HardVFE.forward` + `VFELayer.forward`
+ * (mmdet3d/models/voxel_encoders/voxel_encoder.py; not vendored: /root/reference/mmdetection3d is
+ * empty), the "VFE per-voxel PointNet MLP+max" of BASELINE.json's north_star, called where
+ * models/detectors/adversarial_voxelnet.py:135-137 and adversarial_centerpoint.py:100 call the voxel
+ * encoder. Per voxel [T, F] slots: decoration (raw features, xyz - point mean, xyz - voxel centre,
+ * |xyz|) masked to the first num_points slots, then per layer Linear(no bias) -> BatchNorm1d over
+ * all V*T rows -> ReLU -> max over the T slots, [pointwise, max] concatenated into the next layer.
+ * params: 5 pointers per layer (W [C][K] torch layout, gamma, beta, running_mean, running_var);
+ * grads: 3 per layer (dW, dgamma, dbeta). The workspace carries the forward state to the backward
+ * (keep it alive and unmodified in between). F <= 9 (decorated width <= 16), T <= 64, channels <= 128,
+ * 1-4 layers; backward in training mode only. */
+typedef struct {
+  int F;                 /* raw features per point slot */
+  int T;                 /* slots per voxel (max_num_points) */
+  int nlayers;           /* 1..4 */
+  int channels[4];       /* feat_channels */
+  int with_cluster_center, with_voxel_center, with_distance;
+  int training;
+  float voxel_size[3];
+  float pc_range_min[3];
+  float bn_eps, bn_momentum;
+} RpcHardVfeCfg;
+size_t rpc_hard_vfe_workspace_size(const RpcHardVfeCfg* cfg, int num_voxels);
+int rpc_hard_vfe_forward(const RpcHardVfeCfg* cfg, float* const* params, const float* features,
+                         const int* num_points, const int* coors, int num_voxels, float* out /* [V][C_last] */,
+                         void* workspace, size_t workspace_bytes, void* stream);
+int rpc_hard_vfe_backward(const RpcHardVfeCfg* cfg, float* const* params, const float* features,
+                          const int* num_points, const int* coors, int num_voxels, const float* dout,
+                          float* dfeatures /* [V][T][F] */, float* const* grads, void* workspace,
+                          size_t workspace_bytes, void* stream);
+
 /* ------------------------------------------------------------------ a2/a3/a4 VoxelPerturber
  * Replaces `VoxelPerturber.forward` + `_apply_physical_constraints`
  * (models/adversarial/voxel_perturber.py:120-321, 323-386), the compaction /

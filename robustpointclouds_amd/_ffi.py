@@ -34,6 +34,14 @@ class PerturberCfg(C.Structure):
                 ("bn_momentum", C.c_float), ("vfe_features", C.c_int)]
 
 
+class RpcHardVfeCfg(C.Structure):
+    """include/rpc_hip.h RpcHardVfeCfg."""
+    _fields_ = [("F", C.c_int), ("T", C.c_int), ("nlayers", C.c_int), ("channels", C.c_int * 4),
+                ("with_cluster_center", C.c_int), ("with_voxel_center", C.c_int), ("with_distance", C.c_int),
+                ("training", C.c_int), ("voxel_size", C.c_float * 3), ("pc_range_min", C.c_float * 3),
+                ("bn_eps", C.c_float), ("bn_momentum", C.c_float)]
+
+
 class RpcHeadCfg(C.Structure):
     """include/rpc_hip.h RpcHeadCfg (field order and types must match)."""
     _fields_ = [("B", C.c_int), ("H", C.c_int), ("W", C.c_int), ("S", C.c_int), ("R", C.c_int), ("C", C.c_int),
@@ -93,6 +101,10 @@ SIGNATURES = {
     "rpc_hard_voxelize": (i32, [vp, i32, i32, vp, i32, fp, fp, i32, i32, vp, vp, vp, vp, vp, sz, vp]),
     "rpc_vfe_mean_forward": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
     "rpc_vfe_mean_backward": (i32, [vp, vp, i32, i32, i32, i32, vp, vp]),
+    "rpc_hard_vfe_workspace_size": (sz, [C.POINTER(RpcHardVfeCfg), i32]),
+    "rpc_hard_vfe_forward": (i32, [C.POINTER(RpcHardVfeCfg), C.POINTER(vp), vp, vp, vp, i32, vp, vp, sz, vp]),
+    "rpc_hard_vfe_backward": (i32, [C.POINTER(RpcHardVfeCfg), C.POINTER(vp), vp, vp, vp, i32, vp, vp,
+                                    C.POINTER(vp), vp, sz, vp]),
     "rpc_perturber_workspace_size": (sz, [C.POINTER(PerturberCfg), i32, i32]),
     "rpc_perturber_forward": (i32, [C.POINTER(PerturberCfg), C.POINTER(vp), vp, i32, i32, vp, vp, vp,
                                     vp, vp, sz, vp]),

@@ -713,6 +713,7 @@ static int launch_gemm(int CI, int CO, int at, int et, const GemmArgs& a, int nb
   // forward pairs (CI, CO) of SparseEncoder and their dgrad transposes (CO, CI->pad16)
   C2(4, 16) C2(5, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
   C2(32, 16) C2(64, 32) C2(128, 64)
+  C2(64, 16) C2(16, 64)   // 64-channel voxel features (HardVFE [.., 64]) into conv_input, and its dgrad
 #undef C2
   return RPC_ERR_UNSUPPORTED;
 }
@@ -731,7 +732,7 @@ static int launch_wgrad(int CI, int CO, int at, const WgradArgs& a, dim3 grid, h
     else hipLaunchKernelGGL((k_wgrad<ci, co, A_RAW>), grid, dim3(BLK), 0, st, a);                 \
     return RPC_OK;                                                                               \
   }
-  C2(4, 16) C2(5, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128)
+  C2(4, 16) C2(5, 16) C2(16, 16) C2(16, 32) C2(32, 32) C2(32, 64) C2(64, 64) C2(64, 128) C2(64, 16)
 #undef C2
   return RPC_ERR_UNSUPPORTED;
 }

@@ -10,6 +10,7 @@ from __future__ import annotations
 import torch
 from torch import nn
 
+from . import hard_vfe  # noqa: F401  (registers HardVFE)
 from .anchor_head import Anchor3DHead
 from .perturb import VoxelMeanFn
 from .registry import MODELS

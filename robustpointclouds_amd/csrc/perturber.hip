@@ -698,6 +698,211 @@ __global__ __launch_bounds__(BLK) void k_bwd_first(Dev d, int src) {
   }
 }
 
+// ------------------------------------------------------------------ per-point boundary layers
+// The VALU boundary layers (F -> C0 forward, C4 -> F backward, and the layer-0 BatchNorm backward) as
+// per-point passes over ceil(S / BLK) blocks (the point count N lives on the device: blocks past it
+// exit) with no reductions in the loop; their BatchNorm sums run as a separate column pass
+// (k_colstats). The grid-stride versions above reduced every channel of every point with two wave
+// shuffles chains on one wave per SIMD (k_bwd_last 96 us, k_fwd_first 55 us for 112k points).
+template <int F, int CO>
+__global__ __launch_bounds__(BLK) void k_fwd_first_pp(Dev d) {
+  __shared__ float sW[CO * F + CO];
+  for (int j = threadIdx.x; j < CO * F; j += BLK) sW[j] = d.W[0][j];
+  for (int j = threadIdx.x; j < CO; j += BLK) sW[CO * F + j] = d.b[0][j];
+  __syncthreads();
+  const int i = blockIdx.x * BLK + threadIdx.x;
+  if (i >= d.meta[0]) return;
+  float xv[F], xn[F];
+  load_xn<F>(d, point_slot(d, i), xv, xn);
+#pragma unroll
+  for (int o = 0; o < CO; ++o) {
+    float a = sW[CO * F + o];
+#pragma unroll
+    for (int f = 0; f < F; ++f) a = fmaf(sW[o * F + f], xn[f], a);
+    d.z[0][(size_t)o * d.S + i] = a;
+  }
+}
+
+// per-channel sums over the N points of channel-major [C][S] rows: MODE 0 (forward BatchNorm of
+// layer l): sum z, sum z^2 of z_l, then bn_finalize; MODE 1 (backward of layer l): sum g, sum g*xhat_l
+// with g = the masked post-ReLU gradient, then bnb_finalize. GRID blocks of contiguous point ranges,
+// 1024 threads = 64 channels x 16 lanes of float4 (the whole range in flight at once: 256-thread blocks
+// ran these at 1.4 TB/s), double accumulation, fixed-order combine (deterministic).
+constexpr int CSB = 1024;
+template <int C, int MODE>
+__global__ __launch_bounds__(CSB) void k_colstats(Dev d, int l, const float* __restrict__ gsrc, int tk) {
+  __shared__ double lds[2 * MAXC];
+  __shared__ int lastf;
+  const int N = d.meta[0];
+  const int rows_per = ((N + GRID - 1) / GRID + 15) & ~15;
+  const int p0 = blockIdx.x * rows_per, p1 = min(N, p0 + rows_per);
+  const int q = threadIdx.x & 15;
+  for (int c0 = 0; c0 < C; c0 += CSB / 16) {
+    const int c = c0 + (threadIdx.x >> 4);
+    double s1 = 0.0, s2 = 0.0;
+    if (c < C) {
+      const float* zr = d.z[l] + (size_t)c * d.S;
+      const float* ar = MODE == 0 ? zr : gsrc + (size_t)c * d.S;
+      const float mu = MODE == 1 ? d.bn[l][2 * C + c] : 0.0f;
+      const float is = MODE == 1 ? d.bn[l][3 * C + c] : 0.0f;
+      for (int pb = p0 + 4 * q; pb < p1; pb += 64 * 8) {
+        float4 a[8], z[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int p = pb + 64 * u;
+          a[u] = p < p1 ? *(const float4*)(ar + p) : make_float4(0.f, 0.f, 0.f, 0.f);
+          z[u] = a[u];
+          if (MODE == 1 && p < p1) z[u] = *(const float4*)(zr + p);
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int p = pb + 64 * u;
+          const float av[4] = {a[u].x, a[u].y, a[u].z, a[u].w}, zv[4] = {z[u].x, z[u].y, z[u].z, z[u].w};
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (p + j < p1) {
+              s1 += (double)av[j];
+              s2 += MODE == 0 ? (double)av[j] * av[j] : (double)(av[j] * ((zv[j] - mu) * is));
+            }
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) {
+      s1 += __shfl_xor(s1, o, 64);
+      s2 += __shfl_xor(s2, o, 64);
+    }
+    if (q == 0 && c < C) {
+      d.part[(size_t)blockIdx.x * 2 * MAXC + c] = s1;
+      d.part[(size_t)blockIdx.x * 2 * MAXC + C + c] = s2;
+    }
+  }
+  if (!grid_col_totals(d, tk, 2 * C, lds, &lastf)) return;
+  if (MODE == 0) bn_finalize<C>(d, l, lds);
+  else bnb_finalize<C>(d, l, lds);
+}
+
+// output layer + attention backward, per point: dz5 = d u, dsig, da, a, and dh4' (BN4 sums: k_colstats).
+// Block = 64 points x 4 waves; wave w owns a quarter of the CI channels (their z4 rows are loaded once
+// per wave, coalesced over the 64 points), the partial products u = W5 h4 are combined through LDS in
+// wave order, and every wave then finishes the per-point output-layer math for its own channels.
+template <int CI, int F>
+__global__ __launch_bounds__(BLK) void k_bwd_last_pp(Dev d) {
+  __shared__ float sW[F * CI + F + 4 * CI];
+  __shared__ float su[NWAVE][F][64];
+  const int N = d.meta[0];
+  if (blockIdx.x * 64 >= N) return;
+  for (int j = threadIdx.x; j < F * CI; j += BLK) sW[j] = d.W[5][j];
+  for (int j = threadIdx.x; j < F; j += BLK) sW[F * CI + j] = d.b[5][j];
+  for (int j = threadIdx.x; j < 4 * CI; j += BLK) sW[F * CI + F + j] = d.bn[4][j];
+  __syncthreads();
+  const float* sc = sW + F * CI + F;
+  const float* sh = sc + CI;
+  const float* mean4 = sh + CI;
+  const int pl = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + pl;
+  const bool act = i < N;
+  constexpr int CQ = (CI + NWAVE - 1) / NWAVE;
+  const int cb = w * CQ, ce = min(CI, cb + CQ);
+  const float* zi = d.z[4] + (act ? i : 0);
+  float up[F];
+#pragma unroll
+  for (int f = 0; f < F; ++f) up[f] = 0.0f;
+  if (act) {
+#pragma unroll 8
+    for (int c = cb; c < ce; ++c) {
+      const float hc = fmaxf(fmaf(zi[(size_t)c * d.S] - mean4[c], sc[c], sh[c]), 0.0f);
+#pragma unroll
+      for (int f = 0; f < F; ++f) up[f] = fmaf(sW[f * CI + c], hc, up[f]);
+    }
+  }
+#pragma unroll
+  for (int f = 0; f < F; ++f) su[w][f][pl] = up[f];
+  __syncthreads();
+  if (!act) return;
+  const float gl2 = d.dl[0], gint = d.dl[1], gbias = d.dl[2], gimb = d.dl[3];
+  const float invN = 1.0f / (float)N;
+  const int slot = point_slot(d, i);
+  float xv[F], xn[F], du[F];
+  load_xn<F>(d, slot, xv, xn);
+  float am[MAXF];
+  const float att = d.use_att ? attention<F>(d, xn, am) : 1.0f;
+  float raw[F], pp[F], p[F], dout[F];
+  float nrm2 = 0.0f;
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    float u = sW[F * CI + f];
+#pragma unroll
+    for (int ww = 0; ww < NWAVE; ++ww) u += su[ww][f][pl];
+    raw[f] = tanhf(u);
+    pp[f] = (raw[f] * att) * d.bscale[f];
+    p[f] = fminf(fmaxf(pp[f], -d.bclamp[f]), d.bclamp[f]);
+    nrm2 = fmaf(p[f], p[f], nrm2);
+  }
+  if (d.fused) {
+    const int v = slot / d.slots;
+    const float rn = 1.0f / (float)d.npts[v];
+#pragma unroll
+    for (int f = 0; f < F; ++f) dout[f] = f < d.vfe_f ? d.dout[(size_t)v * d.vfe_f + f] * rn : 0.0f;
+  } else {
+#pragma unroll
+    for (int f = 0; f < F; ++f) dout[f] = d.dout[(size_t)i * F + f];
+  }
+  const float nrm = sqrtf(nrm2);
+  float datt = 0.0f;
+#pragma unroll
+  for (int f = 0; f < F; ++f) {
+    float g = dout[f];
+    if (nrm > 0.0f) g += gl2 * invN * (p[f] / nrm);
+    if (f == 3) g += gint * invN * (float)((p[3] > 0.0f) - (p[3] < 0.0f));
+    const float m = d.pstat[f];
+    g += gbias * invN / (float)F * (float)((m > 0.0f) - (m < 0.0f));
+    g += gimb * d.pstat[2 * MAXF + f] * (p[f] - m);
+    const float dpp = (pp[f] >= -d.bclamp[f] && pp[f] <= d.bclamp[f]) ? g : 0.0f;
+    const float draw = dpp * att * d.bscale[f];
+    datt = fmaf(dpp * raw[f], d.bscale[f], datt);
+    du[f] = draw * (1.0f - raw[f] * raw[f]);
+    if (w == 0) d.dz[5][(size_t)f * d.S + i] = du[f];
+  }
+  if (d.use_att && w == 0) {
+    const float dt = datt * att * (1.0f - att);
+    d.dsig[i] = dt;
+    for (int j = 0; j < d.A; ++j) {
+      d.aact[(size_t)j * d.S + i] = am[j];
+      d.da[(size_t)j * d.S + i] = am[j] > 0.0f ? d.Wa1[j] * dt : 0.0f;
+    }
+  }
+#pragma unroll 8
+  for (int c = cb; c < ce; ++c) {
+    float s = 0.0f;
+#pragma unroll
+    for (int f = 0; f < F; ++f) s = fmaf(sW[f * CI + c], du[f], s);
+    const float hc = fmaxf(fmaf(zi[(size_t)c * d.S] - mean4[c], sc[c], sh[c]), 0.0f);
+    d.dh[0][(size_t)c * d.S + i] = hc > 0.0f ? s : 0.0f;
+  }
+}
+
+// layer 0 BatchNorm backward, 4 points of one channel per thread (grid: point quads x CO)
+__global__ __launch_bounds__(BLK) void k_bwd_first_pp(Dev d, int src, int CO) {
+  const int o = blockIdx.y;
+  const int i = (blockIdx.x * BLK + threadIdx.x) * 4;
+  const int N = d.meta[0];
+  if (i >= N) return;
+  const double invN = 1.0 / N;
+  const float* bo = d.bn[0];
+  const float m1 = (float)(d.bnsum[0][o] * invN), m2 = (float)(d.bnsum[0][CO + o] * invN);
+  const float mu = bo[2 * CO + o], is = bo[3 * CO + o], gi = d.g[0][o] * is;
+  const size_t base = (size_t)o * d.S + i;
+  const float4 z = *(const float4*)(d.z[0] + base);
+  const float4 g = *(const float4*)(d.dh[src] + base);
+  float4 r;
+  r.x = gi * (g.x - m1 - ((z.x - mu) * is) * m2);
+  r.y = gi * (g.y - m1 - ((z.y - mu) * is) * m2);
+  r.z = gi * (g.z - m1 - ((z.z - mu) * is) * m2);
+  r.w = gi * (g.w - m1 - ((z.w - mu) * is) * m2);
+  *(float4*)(d.dz[0] + base) = r;
+}
+
 // ------------------------------------------------------------------ weight gradients
 // job: dW[o][i] = sum_n dz[n][o] * h[n][i] ; i == CI is the bias column (h = 1)
 enum HSrc { H_XN = 0, H_BNRELU = 1, H_RAW = 2 };
@@ -787,6 +992,154 @@ __global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
   }
 }
 
+// All VALU weight-gradient jobs of one point range per block (grid = KS ranges): per 64-point tile
+// every job's dz rows and h rows are staged channel-major in LDS (dynamic: the host sizes it), then
+// each thread accumulates up to EPT (job, o, i) elements in fixed row order. The staging is one flat
+// sweep over a per-block table of source rows (raw / BatchNorm+ReLU / normalised-x gather), double
+// buffered: the next tile's loads are in flight while the current one is summed.
+// (One block grid per job — 4 jobs x 256 ranges of 7 serial tiles — took 97 us.)
+// 1024 threads (16 waves per CU keep the staging loads in flight); WPRE float4 per thread: nrow <= 768
+constexpr int TRP = 64, TPP = TRP + 1, WPB = 1024, WPRE = 12, WEPT = 2;
+struct RowSrc {
+  const float* p;   // channel row base ([S] floats); XN: nullptr
+  float mu, sc, be; // BNRELU: relu((v - mu) * sc + be)
+  int kind;         // HSrc, or 3 = dz row (raw)
+  int c;            // XN: feature index
+};
+template <int F>
+__device__ __forceinline__ float row_value(const Dev& d, const RowSrc& rs, int n) {
+  if (rs.kind == H_XN) {
+    const float t = d.x[(size_t)point_slot(d, n) * F + rs.c] / d.xs[rs.c];
+    return fminf(fmaxf(t, -10.0f), 10.0f);
+  }
+  const float v = rs.p[n];
+  return rs.kind == H_BNRELU ? fmaxf(fmaf(v - rs.mu, rs.sc, rs.be), 0.0f) : v;
+}
+template <int F>
+__global__ __launch_bounds__(WPB) void k_wgrad_pp(Dev d, Jobs J, int nrow) {
+  extern __shared__ float sbuf[];
+  RowSrc* rows = (RowSrc*)(sbuf + 2 * ((nrow * TPP + 3) & ~3));
+  const int N = d.meta[0];
+  const int rows_per = ((N + J.KS - 1) / J.KS + TRP - 1) / TRP * TRP;
+  const int r0 = blockIdx.x * rows_per, r1 = min(N, r0 + rows_per);
+  int joff[MAXJOB + 1];
+  joff[0] = 0;
+  for (int k = 0; k < J.njob; ++k) joff[k + 1] = joff[k] + J.j[k].CO + J.j[k].CI;
+  // source table: job k's dz rows at joff[k] .., then its h rows
+  for (int k = 0; k < J.njob; ++k) {
+    const Job& job = J.j[k];
+    for (int q = threadIdx.x; q < job.CO + job.CI; q += WPB) {
+      RowSrc rs{};
+      if (q < job.CO) {
+        rs.p = job.dz + (size_t)q * d.S;
+        rs.kind = 3;
+      } else {
+        const int c = q - job.CO;
+        rs.kind = job.hsrc;
+        rs.c = c;
+        if (job.hsrc != H_XN) rs.p = job.h + (size_t)c * d.S;
+        if (job.hsrc == H_BNRELU) {
+          rs.mu = job.bn[2 * job.CI + c];
+          rs.sc = job.bn[c];
+          rs.be = job.bn[job.CI + c];
+        }
+      }
+      rows[joff[k] + q] = rs;
+    }
+  }
+  // this thread's elements
+  int ej[WEPT];
+  int pz[WEPT], ph[WEPT];
+  float acc[WEPT];
+  int nE = 0;
+  for (int k = 0; k < J.njob; ++k) nE += J.j[k].nelem;
+#pragma unroll
+  for (int k = 0; k < WEPT; ++k) {
+    acc[k] = 0.0f;
+    ej[k] = -1;
+    pz[k] = ph[k] = -1;
+    int e = threadIdx.x + k * WPB;
+    if (e < nE) {
+      int jb = 0;
+      while (e >= J.j[jb].nelem) { e -= J.j[jb].nelem; ++jb; }
+      const int CI1 = J.j[jb].CI + 1, o = e / CI1, ii = e - o * CI1;
+      ej[k] = J.j[jb].eoff + e;
+      pz[k] = (joff[jb] + o) * TPP;
+      ph[k] = ii < J.j[jb].CI ? (joff[jb] + J.j[jb].CO + ii) * TPP : -1;
+    }
+  }
+  __syncthreads();
+  // staging sweep: float4 of 4 consecutive points per lane (rows_per is a multiple of 64, so every
+  // tile starts 16-byte aligned); tile t + 1 is fetched into registers while tile t is summed
+  const int nq = nrow * (TRP / 4);
+  float4 pre[WPRE];
+  auto fetch = [&](int rb) {
+#pragma unroll
+    for (int u = 0; u < WPRE; ++u) {
+      const int q = threadIdx.x + u * WPB;
+      float v[4] = {0.0f, 0.0f, 0.0f, 0.0f};
+      if (q < nq) {
+        const int row = q / (TRP / 4), n0 = rb + (q - row * (TRP / 4)) * 4;
+        const RowSrc rs = rows[row];
+        if (rs.kind == H_XN) {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (n0 + j < r1) {
+              const float t = d.x[(size_t)point_slot(d, n0 + j) * F + rs.c] / d.xs[rs.c];
+              v[j] = fminf(fmaxf(t, -10.0f), 10.0f);
+            }
+        } else if (n0 < r1) {
+          const float4 x = *(const float4*)(rs.p + n0);
+          v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            if (rs.kind == H_BNRELU) v[j] = fmaxf(fmaf(v[j] - rs.mu, rs.sc, rs.be), 0.0f);
+            if (n0 + j >= r1) v[j] = 0.0f;
+          }
+        }
+      }
+      pre[u] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  };
+  const int tsz = (nrow * TPP + 3) & ~3;
+  int cur = 0;
+  if (r0 < r1) fetch(r0);
+  for (int rb = r0; rb < r1; rb += TRP) {
+    float* buf = sbuf + cur * tsz;
+#pragma unroll
+    for (int u = 0; u < WPRE; ++u) {
+      const int q = threadIdx.x + u * WPB;
+      if (q < nq) {
+        const int row = q / (TRP / 4), r4 = (q - row * (TRP / 4)) * 4;
+        float* dst = buf + row * TPP + r4;
+        dst[0] = pre[u].x;
+        dst[1] = pre[u].y;
+        dst[2] = pre[u].z;
+        dst[3] = pre[u].w;
+      }
+    }
+    __syncthreads();
+    if (rb + TRP < r1) fetch(rb + TRP);
+#pragma unroll
+    for (int k = 0; k < WEPT; ++k) {
+      if (ej[k] < 0) continue;
+      float a = acc[k];
+      const float* z = buf + pz[k];
+      if (ph[k] >= 0) {
+        const float* hh = buf + ph[k];
+        for (int r = 0; r < TRP; ++r) a = fmaf(z[r], hh[r], a);
+      } else {
+        for (int r = 0; r < TRP; ++r) a += z[r];
+      }
+      acc[k] = a;
+    }
+    cur ^= 1;
+  }
+#pragma unroll
+  for (int k = 0; k < WEPT; ++k)
+    if (ej[k] >= 0) d.wpart[(size_t)blockIdx.x * J.total + ej[k]] = acc[k];
+}
+
 __device__ __forceinline__ float grad_hook(float g) {
   // clamp(nan_to_num(g, nan=0, posinf=0, neginf=0), -0.1, 0.1)  (voxel_perturber.py:465-470)
   if (isnan(g) || isinf(g)) g = 0.0f;
@@ -800,36 +1153,46 @@ struct GradOut {
   float* gb[5];
 };
 
+// Fixed-order reduction of the KS partial rows + the reference's grad hook. Block = 64 elements x 4
+// row quarters (each quarter 8 interleaved sums, 8 loads in flight), quarters combined in order through
+// LDS; elements past J.total are the BatchNorm affine gradients (no rows).
 __global__ __launch_bounds__(BLK) void k_wgrad_reduce(Dev d, Jobs J, GradOut G) {
-  int e = blockIdx.x * BLK + threadIdx.x;
-  int flag = d.meta[1];
+  __shared__ double sq[4][64];
+  const int el = threadIdx.x & 63, qt = threadIdx.x >> 6;
+  const int e = blockIdx.x * 64 + el;
+  const int flag = d.meta[1];
+  if (e < J.total) {
+    const int k0 = qt * J.KS / 4, k1 = (qt + 1) * J.KS / 4;
+    double q[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+    int k = k0;
+    for (; k + 8 <= k1; k += 8)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) q[u] += d.wpart[(size_t)(k + u) * J.total + e];
+    for (; k < k1; ++k) q[0] += d.wpart[(size_t)k * J.total + e];
+    sq[qt][el] = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
+  }
+  __syncthreads();
+  if (qt != 0) return;
   if (e < J.total) {
     int jb = 0;
     while (jb + 1 < J.njob && e >= J.j[jb + 1].eoff) ++jb;
     const Job& job = J.j[jb];
-    int le = e - job.eoff;
-    // 8 independent partial sums (8 loads in flight), combined in a fixed order
-    double q[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-    int k = 0;
-    for (; k + 8 <= J.KS; k += 8)
-#pragma unroll
-      for (int u = 0; u < 8; ++u) q[u] += d.wpart[(size_t)(k + u) * J.total + e];
-    for (; k < J.KS; ++k) q[0] += d.wpart[(size_t)k * J.total + e];
-    const double s = ((q[0] + q[1]) + (q[2] + q[3])) + ((q[4] + q[5]) + (q[6] + q[7]));
-    float g = flag ? 0.0f : grad_hook((float)s);
-    int CI1 = job.CI + 1, o = le / CI1, i = le - o * CI1;
+    const int le = e - job.eoff;
+    const double s = (sq[0][el] + sq[1][el]) + (sq[2][el] + sq[3][el]);
+    const float g = flag ? 0.0f : grad_hook((float)s);
+    const int CI1 = job.CI + 1, o = le / CI1, i = le - o * CI1;
     if (i < job.CI) { if (G.W[jb]) G.W[jb][o * job.CI + i] = g; }
     else if (G.b[jb]) G.b[jb][o] = g;
   }
   // BatchNorm gamma / beta: sum dy*xhat, sum dy
-  int t = e - J.total;
+  const int t = e - J.total;
   if (t >= 0) {
     int l = 0, base = 0;
     while (l < 5 && t >= base + d.C[l + 1]) { base += d.C[l + 1]; ++l; }
     if (l < 5) {
-      int c = t - base, C = d.C[l + 1];
-      float gg = flag ? 0.0f : grad_hook((float)d.bnsum[l][C + c]);
-      float gb = flag ? 0.0f : grad_hook((float)d.bnsum[l][c]);
+      const int c = t - base, C = d.C[l + 1];
+      const float gg = flag ? 0.0f : grad_hook((float)d.bnsum[l][C + c]);
+      const float gb = flag ? 0.0f : grad_hook((float)d.bnsum[l][c]);
       if (G.gg[l]) G.gg[l][c] = gg;
       if (G.gb[l]) G.gb[l][c] = gb;
     }
@@ -1346,10 +1709,27 @@ static int fill_dev(const rpc_perturber_cfg* cfg, const float* const* P, const f
 // ---- width dispatch
 #define RPC_HID(X) X(8) X(16) X(32) X(64) X(128)
 
+// per-point passes cover every slot the batch can have (S >= N); blocks past N exit at once
+static inline dim3 pp_grid(const Dev& d) { return dim3((unsigned)((d.S + BLK - 1) / BLK)); }
+
+static int launch_colstats(int C, int mode, Dev& d, int l, const float* g, int tk, hipStream_t st) {
+  switch (C) {
+#define CASE(c)                                                                                      \
+  case c:                                                                                            \
+    if (mode == 0) hipLaunchKernelGGL((k_colstats<c, 0>), dim3(GRID), dim3(CSB), 0, st, d, l, g, tk); \
+    else hipLaunchKernelGGL((k_colstats<c, 1>), dim3(GRID), dim3(CSB), 0, st, d, l, g, tk);           \
+    break;
+    RPC_HID(CASE)
+#undef CASE
+    default: return RPC_ERR_UNSUPPORTED;
+  }
+  return RPC_OK;
+}
+
 template <int F>
 static int launch_first(int C0, Dev& d, hipStream_t st) {
   switch (C0) {
-#define CASE(c) case c: hipLaunchKernelGGL((k_fwd_first<F, c>), dim3(GRID), dim3(BLK), 0, st, d); break;
+#define CASE(c) case c: hipLaunchKernelGGL((k_fwd_first_pp<F, c>), pp_grid(d), dim3(BLK), 0, st, d); break;
     RPC_HID(CASE)
 #undef CASE
     default: return RPC_ERR_UNSUPPORTED;
@@ -1361,7 +1741,7 @@ static int launch_last(int CI, Dev& d, hipStream_t st, bool bwd) {
   switch (CI) {
 #define CASE(c)                                                                          \
   case c:                                                                                \
-    if (bwd) hipLaunchKernelGGL((k_bwd_last<c, F>), dim3(GRID), dim3(BLK), 0, st, d);    \
+    if (bwd) hipLaunchKernelGGL((k_bwd_last_pp<c, F>), dim3((d.S + 63) / 64), dim3(BLK), 0, st, d); \
     else hipLaunchKernelGGL((k_fwd_last<c, F>), dim3(GRID), dim3(BLK), 0, st, d);        \
     break;
     RPC_HID(CASE)
@@ -1422,12 +1802,8 @@ static void launch_wgrad_mf(int CO, int CI, Dev& d, const MfJobs& M, int njob, h
   }
 }
 static int launch_bwd_first(int CO, Dev& d, hipStream_t st, int src) {
-  switch (CO) {
-#define CASE(c) case c: hipLaunchKernelGGL((k_bwd_first<c>), dim3(GRID), dim3(BLK), 0, st, d, src); break;
-    RPC_HID(CASE)
-#undef CASE
-    default: return RPC_ERR_UNSUPPORTED;
-  }
+  const unsigned nq = (unsigned)((d.S / 4 + BLK - 1) / BLK);
+  hipLaunchKernelGGL(k_bwd_first_pp, dim3(nq, CO), dim3(BLK), 0, st, d, src, CO);
   return RPC_OK;
 }
 
@@ -1477,6 +1853,11 @@ extern "C" int rpc_perturber_forward(const rpc_perturber_cfg* cfg, const float* 
   rc = F == 4 ? launch_first<4>(d.C[1], d, st) : launch_first<5>(d.C[1], d, st);
   if (rc) return rc;
   RPC_LAUNCH_CHECK();
+  if (cfg->training) {
+    rc = launch_colstats(d.C[1], 0, d, 0, nullptr, 1, st);
+    if (rc) return rc;
+    RPC_LAUNCH_CHECK();
+  }
   for (int l = 1; l < 5; ++l) {
     rc = launch_mid(d.C[l], d.C[l + 1], d, l, st, false);
     if (rc) return rc;
@@ -1512,6 +1893,9 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
   RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET * TSTRIDE, st));
   const int F = cfg->F;
   rc = F == 4 ? launch_last<4>(d.C[5], d, st, true) : launch_last<5>(d.C[5], d, st, true);
+  if (rc) return rc;
+  RPC_LAUNCH_CHECK();
+  rc = launch_colstats(d.C[5], 1, d, 4, d.dh[0], 7, st);
   if (rc) return rc;
   RPC_LAUNCH_CHECK();
   int src = 0;
@@ -1567,13 +1951,24 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
     JV.echunks[k] = (JV.j[k].nelem + BLK * EPT - 1) / (BLK * EPT);
     chunks += JV.echunks[k];
   }
-  int ks = chunks ? 1024 / chunks : KS_MAX;
-  if (ks < 128) ks = 128;
-  if (ks > KS_MAX) ks = KS_MAX;
+  const int ks = KS_MAX;   // point ranges of the weight-gradient passes (= partial rows reduced)
   J.KS = JV.KS = ks;
   if (nv) {
-    if (F == 4) hipLaunchKernelGGL((k_wgrad<4>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
-    else hipLaunchKernelGGL((k_wgrad<5>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
+    // one launch over KS point ranges covering every VALU job (LDS sized to the jobs' tile rows)
+    int nrow = 0, nel = 0;
+    for (int k = 0; k < nv; ++k) { nrow += JV.j[k].CO + JV.j[k].CI; nel += JV.j[k].nelem; }
+    const size_t lds = (size_t)2 * ((nrow * TPP + 3) & ~3) * sizeof(float) + (size_t)nrow * sizeof(RowSrc);
+    if (nel > WPB * WEPT || lds > 160 * 1024 || nrow * (TRP / 4) > WPB * WPRE) {
+      // wide VALU hidden layers (CO * CI > 8192): the per-job chunked kernel
+      if (F == 4) hipLaunchKernelGGL((k_wgrad<4>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
+      else hipLaunchKernelGGL((k_wgrad<5>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
+    } else if (F == 4) {
+      if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_wgrad_pp<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((k_wgrad_pp<4>), dim3(ks), dim3(WPB), lds, st, d, JV, nrow);
+    } else {
+      if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_wgrad_pp<5>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((k_wgrad_pp<5>), dim3(ks), dim3(WPB), lds, st, d, JV, nrow);
+    }
     RPC_LAUNCH_CHECK();
   }
   for (int l = 1; l < 5; ++l) {
@@ -1598,7 +1993,7 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
     G.gb[l] = grads[6 * l + 3];
   }
   int nbn = d.C[1] + d.C[2] + d.C[3] + d.C[4] + d.C[5];
-  int nr = (J.total + nbn + BLK - 1) / BLK;
+  int nr = (J.total + nbn + 63) / 64;
   hipLaunchKernelGGL(k_wgrad_reduce, dim3(nr), dim3(BLK), 0, st, d, J, G);
   RPC_LAUNCH_CHECK();
   return RPC_OK;

@@ -56,8 +56,10 @@ struct GB {
   float* part;        // [blocks][2*NGP] or null
 };
 
+// Occupancy: the <= 64 x 64 tiles are held to 64 VGPRs (8 waves per SIMD, 4 blocks per CU) — at 72 the
+// 106k-row 64-channel layers needed 1.08 rounds of 3 blocks per CU (k_gemm_bf16<64,4,1> 60.6 -> 51.5 us)
 template <int KGP, int NT, int EPI>
-__global__ __launch_bounds__(64 * gw_of(KGP, NT)) void k_gemm_bf16(GB g) {
+__global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 8 : 1)) void k_gemm_bf16(GB g) {
   constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, GBM = 16 * GW;
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;

@@ -1,0 +1,15 @@
+#!/bin/bash
+# perturber GPU tests + 3-class profile
+set -o pipefail
+OUT=gpurun_out/$1
+mkdir -p $OUT
+export TMPDIR=/tmp
+timeout -k 10 300 python -u -m pytest tests/test_gpu_sparse_encoder.py tests/test_gpu_sparse_layers.py tests/test_gpu_bf16_kernels.py tests/test_gpu_e2e_parity.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 && echo tests ok &&
+timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python -u bench.py --steps 12 --warmup 6 --no-cpu-baseline > $OUT/prof_bench.log 2>&1
+RC=$?
+KT=$(find $OUT/prof -name '*kernel_trace.csv' | head -1)
+[ -n "$KT" ] && python tools/prof_summary.py $KT --steps 8 --top 200 > $OUT/step_kernels.txt 2>&1
+find $OUT/prof -name '*.csv' -size +1M -delete 2>/dev/null
+find $OUT/prof -name '*.db' -delete 2>/dev/null
+tail -3 $OUT/pytest.log
+exit $RC

@@ -20,6 +20,8 @@ and state-dict keys are the torch modules' own (second.py).
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _ffi
@@ -28,11 +30,13 @@ S1, S2, D2, P1, U2, G2 = 0, 1, 2, 3, 4, 5
 
 
 class ConvTimer:
-    """HIP-event timing of the S1 (3x3 stride-1, kernel `rpc::dn::k_conv3x3<0>`) launches of
-    rpc_dense_conv — forward and flipped-tap data gradient — on the stream they are launched on.
-    Algorithmic work per launch = 2 * B*H*W * C_in * C_out * 9 FLOP (every tap of a zero-padded
+    """HIP-event timing of the S1 (3x3 stride-1: kernels `rpc::dn::k_conv3x3<0>` and `k_conv3x3w<0>`)
+    launches of rpc_dense_conv — forward and flipped-tap data gradient — on the stream they are launched
+    on. Algorithmic work per launch = 2 * B*H*W * C_in * C_out * 9 FLOP (every tap of a zero-padded
     3x3 convolution); algorithmic bytes = bf16 source image + bf16 output image + bf16 weights.
-    bench.py installs one as `dense_bev.TIMER`."""
+    bench.py installs one as `dense_bev.TIMER`. Timing events cannot be recorded inside a captured HIP
+    graph on ROCm (torch refuses external events), so launches issued during a capture are not timed:
+    bench.py times eager steps (graphs off) right after its timed loop — the same kernels and shapes."""
 
     def __init__(self):
         self.recs = []
@@ -47,6 +51,9 @@ class ConvTimer:
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(torch.cuda.current_stream())
         self.recs.append((e0, e1, rows, ci, co))
+
+    def reset(self):
+        self.recs = []
 
     def summary(self):
         torch.cuda.synchronize()
@@ -63,10 +70,87 @@ class ConvTimer:
 
 TIMER = None
 
+# ---- HIP graphs over the fixed-shape dense part. The SECOND / SECONDFPN forward and backward issue
+# ~100 launches per step from Python (weight prep, conv, BN finalize / apply, wgrad, dgrad) with fixed
+# shapes for a fixed batch; on a slow host that issue time made the whole step host-bound (r01: one box
+# at 553.6 instead of ~720 frames/s with unchanged kernel time). Each autograd node (BackboneFn,
+# NeckFn, and their backward) runs eagerly the first time it sees a shape, is captured into a HIP graph
+# the second time and replayed afterwards: inputs are copied into the captured static inputs only when
+# the caller passes other storage (the FPN reads the backbone graph's own outputs in place), outputs
+# are the graph's static tensors (overwritten by the next replay, after this step has consumed them).
+# RPC_DENSE_GRAPHS=0 turns it off.
+GRAPHS = os.environ.get("RPC_DENSE_GRAPHS", "1") != "0"
+_CAPTURING = [False]
+
+
+def _capturing() -> bool:
+    return _CAPTURING[0]
+
+
+class _GraphEntry:
+    def __init__(self):
+        self.calls = 0
+        self.graph = None
+        self.static_in = None
+        self.outs = None
+        self.state = None
+        self.bwd = {}
+
+
+_STABLE = {}   # data_ptr -> tensor: storage that stays put across steps (graph outputs, persistent buffers)
+
+
+def mark_stable(t: torch.Tensor) -> None:
+    """Declare `t`'s storage persistent (reused, never freed, by its owner across steps): a graph
+    captured with it as an input reads it in place instead of from a copy."""
+    _STABLE[t.data_ptr()] = t
+
+
+def _static_in(t):
+    if t is None:
+        return None
+    if t.data_ptr() in _STABLE:
+        return t
+    s_ = torch.empty_strided(t.size(), t.stride(), dtype=t.dtype, device=t.device)
+    s_.copy_(t)
+    return s_
+
+
+def _graph_run(cache, key, inputs, body, eager_first=True):
+    """body(*inputs) -> (outputs, state): eager on the first call for `key` (eager_first), captured
+    into a HIP graph on the next one and replayed from then on. Returns (outputs, state, entry)."""
+    e = cache.get(key)
+    if e is None:
+        e = cache[key] = _GraphEntry()
+    e.calls += 1
+    if eager_first and e.calls == 1:
+        outs, state = body(*inputs)
+        return outs, state, None
+    if e.graph is None:
+        e.static_in = [_static_in(t) for t in inputs]
+        g = torch.cuda.CUDAGraph()
+        _CAPTURING[0] = True
+        try:
+            with torch.cuda.graph(g, capture_error_mode="thread_local"):
+                e.outs, e.state = body(*e.static_in)
+        finally:
+            _CAPTURING[0] = False
+        e.graph = g
+        for o in (e.outs if isinstance(e.outs, (tuple, list)) else (e.outs,)):
+            if isinstance(o, torch.Tensor):
+                mark_stable(o)
+    else:
+        for s_, t in zip(e.static_in, inputs):
+            if t is not None and s_.data_ptr() != t.data_ptr():
+                s_.copy_(t)
+    e.graph.replay()
+    return e.outs, e.state, e
+
 
 def _conv(lib, fmap, *args):
     """rpc_dense_conv, with the S1 launches timed when a ConvTimer is enabled."""
-    t = TIMER if (TIMER is not None and TIMER.enabled and fmap == S1 and args[4] % 128 == 0) else None
+    t = TIMER if (TIMER is not None and TIMER.enabled and not _capturing() and fmap == S1 and args[4] % 128 == 0) \
+        else None
     e0 = t.start() if t is not None else None
     rc = lib.rpc_dense_conv(fmap, *args)
     if t is not None:
@@ -286,110 +370,156 @@ def fpn_layers(mod):
     return out
 
 
+def _backbone_fwd(eng, mod, x):
+    dev = x.device
+    st = _ffi.stream_of(x)
+    blocks = second_layers(mod)
+    xi = _nhwc(x, eng.dt)
+    B, C, H, W = xi.shape
+    h, pitch = xi, C
+    recs, outs = [], []
+    wts = iter(_prep_weights(eng, [L for layers in blocks for L in layers], dev, st))
+    for layers in blocks:
+        brecs = []
+        for L in layers:
+            h, rec, H, W = _forward_layer(eng, L, h, pitch, B, H, W, mod.training, dev, st, wts=next(wts))
+            pitch = L.co
+            brecs.append(rec)
+        recs.append(brecs)
+        outs.append(h)
+    if mod.training:
+        _ffi.bump_batches([L.bnm for b in blocks for L in b])
+    return tuple(outs), recs
+
+
+def _backbone_bwd(eng, recs, params, need_x, gouts):
+    dt = eng.dt
+    g_any = next(g for g in gouts if g is not None)
+    dev = g_any.device
+    st = _ffi.stream_of(g_any)
+    grads = {}
+    nb = len(recs)
+    # dh = complete gradient w.r.t. the output of block bi (its own output gradient plus what
+    # block bi+1's first data-gradient GEMM accumulated into a copy of it)
+    dh = _nhwc(gouts[-1], dt) if gouts[-1] is not None else None
+    dx = None
+    for bi in range(nb - 1, -1, -1):
+        brecs = recs[bi]
+        if dh is None:   # nothing flows through this block
+            dh = _nhwc(gouts[bi - 1], dt) if bi > 0 and gouts[bi - 1] is not None else None
+            continue
+        for li in range(len(brecs) - 1, -1, -1):
+            rec = brecs[li]
+            dx_out, accumulate = None, False
+            if li > 0:
+                need_dx = True
+            elif bi > 0:
+                need_dx = True
+                if gouts[bi - 1] is not None:
+                    dx_out = _nhwc(gouts[bi - 1], dt).clone(memory_format=torch.channels_last)
+                    accumulate = True
+            else:
+                need_dx = need_x
+            dh, dW, dgam, dbet = _backward_layer(eng, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
+                                                 accumulate)
+            grads[id(rec["L"].conv.weight)] = dW
+            grads[id(rec["L"].bnm.weight)] = dgam
+            grads[id(rec["L"].bnm.bias)] = dbet
+        if bi == 0:
+            dx = dh
+    return (dx,) + tuple(grads.get(id(p)) for p in params), None
+
+
+def _alias(t):
+    return None if t is None else t.detach()
+
+
+def _shape_key(ts):
+    return tuple(None if t is None else (tuple(t.shape), tuple(t.stride()), t.dtype, t.device) for t in ts)
+
+
+_FWD_GRAPHS = {}
+
+
 class BackboneFn(torch.autograd.Function):
-    """SECOND forward/backward as one node: x [B, Cin, H, W] -> tuple of block outputs."""
+    """SECOND forward/backward as one node: x [B, Cin, H, W] -> tuple of block outputs (training
+    steps replay HIP graphs after the first, see _graph_run)."""
 
     @staticmethod
     def forward(ctx, x, mod, *params):
         eng = _engine(_ffi.load(), x)
-        dev = x.device
-        st = _ffi.stream_of(x)
-        blocks = second_layers(mod)
-        for b in blocks:
+        for b in second_layers(mod):
             eng.check_widths(b)
-        xi = _nhwc(x, eng.dt)
-        B, C, H, W = xi.shape
-        h, pitch = xi, C
-        recs, outs = [], []
-        wts = iter(_prep_weights(eng, [L for layers in blocks for L in layers], dev, st))
-        for layers in blocks:
-            brecs = []
-            for L in layers:
-                h, rec, H, W = _forward_layer(eng, L, h, pitch, B, H, W, mod.training, dev, st, wts=next(wts))
-                pitch = L.co
-                brecs.append(rec)
-            recs.append(brecs)
-            outs.append(h)
-        if mod.training:
-            _ffi.bump_batches([L.bnm for b in blocks for L in b])
-        ctx.recs = recs
         ctx.eng = eng
         ctx.param_list = params
-        return tuple(outs)
+        ctx.entry = None
+        if GRAPHS and mod.training:
+            key = ("second", id(mod), eng.f32) + _shape_key([x])
+            outs, recs, ctx.entry = _graph_run(_FWD_GRAPHS, key, [x], lambda xx: _backbone_fwd(eng, mod, xx))
+            outs = tuple(_alias(o) for o in outs) if ctx.entry is not None else outs
+        else:
+            outs, recs = _backbone_fwd(eng, mod, x)
+        ctx.recs = recs
+        return outs
 
     @staticmethod
     def backward(ctx, *gouts):
-        eng = ctx.eng
-        dt = eng.dt
-        recs = ctx.recs
-        g_any = next(g for g in gouts if g is not None)
-        dev = g_any.device
-        st = _ffi.stream_of(g_any)
-        grads = {}
-        nb = len(recs)
-        # dh = complete gradient w.r.t. the output of block bi (its own output gradient plus what
-        # block bi+1's first data-gradient GEMM accumulated into a copy of it)
-        dh = _nhwc(gouts[-1], dt) if gouts[-1] is not None else None
-        dx = None
-        for bi in range(nb - 1, -1, -1):
-            brecs = recs[bi]
-            if dh is None:   # nothing flows through this block
-                dh = _nhwc(gouts[bi - 1], dt) if bi > 0 and gouts[bi - 1] is not None else None
-                continue
-            for li in range(len(brecs) - 1, -1, -1):
-                rec = brecs[li]
-                dx_out, accumulate = None, False
-                if li > 0:
-                    need_dx = True
-                elif bi > 0:
-                    need_dx = True
-                    if gouts[bi - 1] is not None:
-                        dx_out = _nhwc(gouts[bi - 1], dt).clone(memory_format=torch.channels_last)
-                        accumulate = True
-                else:
-                    need_dx = ctx.needs_input_grad[0]
-                dh, dW, dgam, dbet = _backward_layer(eng, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
-                                                     accumulate)
-                grads[id(rec["L"].conv.weight)] = dW
-                grads[id(rec["L"].bnm.weight)] = dgam
-                grads[id(rec["L"].bnm.bias)] = dbet
-            if bi == 0:
-                dx = dh
+        eng, recs, params = ctx.eng, ctx.recs, ctx.param_list
+        need_x = ctx.needs_input_grad[0]
+        if ctx.entry is not None:   # the forward replayed a graph: so does the backward
+            key = (need_x,) + _shape_key(gouts)
+            res, _, _ = _graph_run(ctx.entry.bwd, key, list(gouts),
+                                   lambda *g: _backbone_bwd(eng, recs, params, need_x, g), eager_first=False)
+            res = tuple(_alias(t) for t in res)
+        else:
+            res, _ = _backbone_bwd(eng, recs, params, need_x, gouts)
         ctx.recs = None
         ctx.eng = None
-        return (dx, None) + tuple(grads.get(id(p)) for p in ctx.param_list)
+        ctx.entry = None
+        return (res[0], None) + tuple(res[1:])
+
+
+def _neck_fwd(eng, mod, h0, h1):
+    dev = h0.device
+    st = _ffi.stream_of(h0)
+    layers = fpn_layers(mod)
+    ins = [_nhwc(h0, eng.dt), _nhwc(h1, eng.dt)]
+    B, _, H0, W0 = ins[0].shape
+    Ctot = sum(L.co for L in layers)
+    out = _image(B, Ctot, H0, W0, dev, eng.dt)
+    recs = []
+    off = 0
+    wts = _prep_weights(eng, layers, dev, st)
+    for L, hi, wt in zip(layers, ins, wts):
+        _, C, H, W = hi.shape
+        _, rec, Ho, Wo = _forward_layer(eng, L, hi, C, B, H, W, mod.training, dev, st, out=out, out_pitch=Ctot,
+                                        out_off=off, wts=wt)
+        assert (Ho, Wo) == (H0, W0), "FPN deblocks must upsample to the first block's resolution"
+        rec["off"] = off
+        recs.append(rec)
+        off += L.co
+    if mod.training:
+        _ffi.bump_batches([L.bnm for L in layers])
+    return out, (recs, Ctot)
 
 
 class NeckFn(torch.autograd.Function):
-    """SECONDFPN forward/backward as one node: (block outputs) -> [B, sum(out), H0, W0]."""
+    """SECONDFPN forward/backward as one node: (block outputs) -> [B, sum(out), H0, W0]. The training
+    forward replays a HIP graph after the first step (reading the backbone graph's outputs in place);
+    the backward stays eager (its input, the head's gradient, is fresh storage every step)."""
 
     @staticmethod
     def forward(ctx, h0, h1, mod, *params):
         eng = _engine(_ffi.load(), h0)
-        dev = h0.device
-        st = _ffi.stream_of(h0)
-        layers = fpn_layers(mod)
-        eng.check_widths(layers)
-        ins = [_nhwc(h0, eng.dt), _nhwc(h1, eng.dt)]
-        B, _, H0, W0 = ins[0].shape
-        Ctot = sum(L.co for L in layers)
-        out = _image(B, Ctot, H0, W0, dev, eng.dt)
-        recs = []
-        off = 0
-        wts = _prep_weights(eng, layers, dev, st)
-        for L, hi, wt in zip(layers, ins, wts):
-            _, C, H, W = hi.shape
-            _, rec, Ho, Wo = _forward_layer(eng, L, hi, C, B, H, W, mod.training, dev, st, out=out, out_pitch=Ctot,
-                                            out_off=off, wts=wt)
-            assert (Ho, Wo) == (H0, W0), "FPN deblocks must upsample to the first block's resolution"
-            rec["off"] = off
-            recs.append(rec)
-            off += L.co
-        if mod.training:
-            _ffi.bump_batches([L.bnm for L in layers])
-        ctx.recs = recs
+        eng.check_widths(fpn_layers(mod))
+        if GRAPHS and mod.training:
+            key = ("fpn", id(mod), eng.f32) + _shape_key([h0, h1])
+            out, st_, ent = _graph_run(_FWD_GRAPHS, key, [h0, h1], lambda a, b: _neck_fwd(eng, mod, a, b))
+            out = _alias(out) if ent is not None else out
+        else:
+            out, st_ = _neck_fwd(eng, mod, h0, h1)
+        ctx.recs, ctx.Ctot = st_
         ctx.eng = eng
-        ctx.Ctot = Ctot
         ctx.param_list = params
         return out
 

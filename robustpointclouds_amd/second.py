@@ -1,11 +1,13 @@
-"""Dense BEV backbone + neck, PyTorch-ROCm (MIOpen) convs.
+"""Dense BEV backbone + neck.
 
 `SECOND` / `SECONDFPN` restate upstream mmdet3d backbones/second.py and necks/second_fpn.py
 as configured at configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:25-36
 (called at models/detectors/adversarial_voxelnet.py:142-145): Conv3x3-BN-ReLU stacks, BN eps
 1e-3 momentum 0.01, conv bias off; FPN deconvs (kernel = stride) + BN + ReLU, concatenated.
-These are the MFMA-bound layers; they run through MIOpen under bf16 autocast in the perf
-mode (bench.py) and in fp32 for parity. Module names match mmdet3d state dicts.
+These are the MFMA-bound layers. With `hip = True` (set by the Trainer) the whole stack runs as one
+HIP node per module on the dense engine of dense_bev.py — bf16 MFMA in the perf mode (bench.py), fp32
+MFMA (dense_f32.hip) in the parity mode; the plain torch path below is the reference / CPU form.
+Module names match mmdet3d state dicts.
 """
 from __future__ import annotations
 

@@ -247,6 +247,9 @@ __device__ __forceinline__ int dir_target(const RpcHeadCfg& c, float t6, float a
   return d < 0 ? 0 : (d > 1 ? 1 : d);
 }
 
+// focal-loss modulating factor: the configs' gamma = 2 as one product (pow of ocml is ~100 instructions)
+__device__ __forceinline__ float pow_gamma(float x, float gamma) { return gamma == 2.0f ? x * x : powf(x, gamma); }
+
 __device__ __forceinline__ float smooth_l1(float d, float beta) {
   const float a = fabsf(d);
   return a < beta ? 0.5f * a * a / beta : a - 0.5f * beta;
@@ -292,7 +295,7 @@ __global__ __launch_bounds__(BLK) void k_loss_fwd(RpcHeadCfg c, const float* __r
   double lc = 0.0, lb = 0.0, ld = 0.0;
   int npos = 0;
   extern __shared__ __attribute__((aligned(16))) unsigned short ztile[];
-  const int N = A * (C + 7 + (c.use_dir ? 2 : 0)), nc8 = (N + 7) / 8, tp = 8 * nc8 + 8;
+  const int N = A * (C + 7 + (c.use_dir ? 2 : 0)), nc8 = (N + 7) / 8, tp = 8 * nc8;
   const int loc0 = blockIdx.x * BLK, nrows = min(BLK, HW - loc0);
   if (kTile) {
     tile_load(ztile, tp, z, c.z_sb, c.z_shw, b, loc0, nrows, nc8);
@@ -321,9 +324,9 @@ __global__ __launch_bounds__(BLK) void k_loss_fwd(RpcHeadCfg c, const float* __r
         const float p = 1.0f / (1.0f + expf(-x));
         float f;
         if (label == k)
-          f = -c.alpha * powf(1.0f - p, c.gamma) * logf(fmaxf(p, kFltMin));
+          f = -c.alpha * pow_gamma(1.0f - p, c.gamma) * logf(fmaxf(p, kFltMin));
         else
-          f = -(1.0f - c.alpha) * powf(p, c.gamma) * logf(fmaxf(1.0f - p, kFltMin));
+          f = -(1.0f - c.alpha) * pow_gamma(p, c.gamma) * logf(fmaxf(1.0f - p, kFltMin));
         fc += f * lw;
       }
       lc += (double)fc;
@@ -411,7 +414,10 @@ __global__ __launch_bounds__(BLK) void k_loss_bwd(RpcHeadCfg c, const float* __r
   const int N = A * (C + 7 + (c.use_dir ? 2 : 0));
   float* sb = (float*)smem;  // [4][N] per-wave bias-gradient sums
   unsigned short* ztile = (unsigned short*)(smem + ((4 * N * sizeof(float) + 15) & ~15));
-  const int nc8 = (N + 7) / 8, nw8 = c.dz_nwrite / 8, tp = 8 * (nc8 > nw8 ? nc8 : nw8) + 8;
+  // the LDS tile holds the N computed channels (rounded to 16-byte granules): at 72 channels x 256 cells
+  // that is 37 KB and four blocks share a CU, so the 828-block grid runs in one round (the 128-wide
+  // zero-padded tile of 70 KB ran 1.6 rounds); channels [8*nc8, n_write) are zero-stored directly
+  const int nc8 = (N + 7) / 8, nw8 = c.dz_nwrite / 8, tp = 8 * nc8;
   const int loc0 = blockIdx.x * BLK, nrows = min(BLK, HW - loc0);
   const int loc = blockIdx.x * BLK + threadIdx.x, b = blockIdx.y;
   if (kTile) {
@@ -450,9 +456,9 @@ __global__ __launch_bounds__(BLK) void k_loss_bwd(RpcHeadCfg c, const float* __r
         const float p = 1.0f / (1.0f + expf(-x));
         float gr;
         if (label == k)
-          gr = -c.alpha * powf(1.0f - p, c.gamma) * (1.0f - p - c.gamma * p * logf(fmaxf(p, kFltMin)));
+          gr = -c.alpha * pow_gamma(1.0f - p, c.gamma) * (1.0f - p - c.gamma * p * logf(fmaxf(p, kFltMin)));
         else
-          gr = -(1.0f - c.alpha) * powf(p, c.gamma) * (c.gamma * (1.0f - p) * logf(fmaxf(1.0f - p, kFltMin)) - p);
+          gr = -(1.0f - c.alpha) * pow_gamma(p, c.gamma) * (c.gamma * (1.0f - p) * logf(fmaxf(1.0f - p, kFltMin)) - p);
         d = gr * lw * s_cls;
         put(ch, d);
       }
@@ -503,9 +509,19 @@ __global__ __launch_bounds__(BLK) void k_loss_bwd(RpcHeadCfg c, const float* __r
       }
   }
   if (live)
-    for (int ch = N; ch < c.dz_nwrite; ++ch) put(ch, 0.0f);
+    for (int ch = N; ch < (kTile ? 8 * nc8 : c.dz_nwrite); ++ch) put(ch, 0.0f);
   __syncthreads();
-  if (kTile) tile_store(ztile, tp, dz, c.dz_sb, c.dz_shw, b, loc0, nrows, nw8);
+  if (kTile) {
+    tile_store(ztile, tp, dz, c.dz_sb, c.dz_shw, b, loc0, nrows, nc8);
+    const int nz = nw8 - nc8;
+    if (nz > 0) {
+      unsigned short* dst = (unsigned short*)dz + (long long)b * c.dz_sb + (long long)loc0 * c.dz_shw;
+      for (int q = threadIdx.x; q < nrows * nz; q += BLK) {
+        const int r = q / nz, g8 = nc8 + (q - r * nz);
+        *(uint4*)(dst + (long long)r * c.dz_shw + 8 * g8) = make_uint4(0u, 0u, 0u, 0u);
+      }
+    }
+  }
   for (int ch = threadIdx.x; ch < N; ch += BLK)
     bpart[(long long)bid * N + ch] = ((sb[ch] + sb[N + ch]) + sb[2 * N + ch]) + sb[3 * N + ch];
 }
@@ -599,7 +615,7 @@ extern "C" int rpc_anchor_head_loss_forward(const RpcHeadCfg* cfg, const float* 
   }
   const bool tile = zrow_tile(c, z, nullptr);
   const int N = head_channels(&c);
-  const size_t lds = tile ? (size_t)BLK * (8 * ((N + 7) / 8) + 8) * sizeof(unsigned short) : 0;
+  const size_t lds = tile ? (size_t)BLK * (8 * ((N + 7) / 8)) * sizeof(unsigned short) : 0;
   hipLaunchKernelGGL(tile ? k_loss_fwd<true> : k_loss_fwd<false>, dim3(cdiv_u(HW, BLK), c.B), dim3(BLK), lds, st, c,
                      anchor_tab, (const float*)w.gtb,
                      gt_boxes, M, (const unsigned*)w.gmax, z, bias, assigned, w.part, w.cnt, w.ticket, losses);
@@ -623,7 +639,7 @@ extern "C" int rpc_anchor_head_loss_backward(const RpcHeadCfg* cfg, const float*
   const int HW = c.H * c.W;
   const unsigned gx = cdiv_u(HW, BLK);
   const bool tile = zrow_tile(c, z, dz);
-  const int tp = 8 * ((N + 7) / 8 > c.dz_nwrite / 8 ? (N + 7) / 8 : c.dz_nwrite / 8) + 8;
+  const int tp = 8 * ((N + 7) / 8);
   const size_t lds = ((4 * N * sizeof(float) + 15) & ~(size_t)15) + (tile ? (size_t)BLK * tp * sizeof(unsigned short) : 0);
   hipLaunchKernelGGL(tile ? k_loss_bwd<true> : k_loss_bwd<false>, dim3(gx, c.B), dim3(BLK), lds, st, c, anchor_tab,
                      (const float*)w.gtb, gt_boxes, max_gts, z, bias, assigned, grad_losses, losses, dz, w.bpart);

@@ -116,6 +116,51 @@ __global__ void k_cand_head(const int* __restrict__ coors, int N, KGeom g, Shape
   flag[t] = f;
 }
 
+// Per-row forms of k_cand_head / k_out_assign: one thread per input row walks its K candidates in
+// offset order, so the exclusive scan that numbers the output cells runs over N + 1 per-row head counts
+// instead of N*K + 1 flags (the same first-appearance order: a cell's head is its smallest r*K + k).
+// (the head offsets of each row are kept as a bit mask, K <= 27: the assign pass rewrites grid cells, so
+// it cannot re-test them against candidate indices)
+__global__ void k_row_heads(const int* __restrict__ coors, int N, KGeom g, Shape so, const unsigned* __restrict__ grid,
+                            int* __restrict__ cnt, unsigned* __restrict__ hmask) {
+  // 32 lanes per row, one per offset (K <= 27): the row's bits come out of the wave's ballot
+  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  const int r = (int)(t >> 5), k = (int)(t & 31);
+  if (r == N && k == 0) cnt[N] = 0;
+  bool head = false;
+  if (r < N && k < g.K) {
+    const int* c = coors + 4 * r;
+    int oz, oy, ox;
+    head = out_of(c, k, g, so, oz, oy, ox) && grid[cell(so, c[0], oz, oy, ox)] == (unsigned)(r * g.K + k);
+  }
+  const unsigned m = (unsigned)(__ballot(head) >> (threadIdx.x & 32));
+  if (r < N && k == 0) {
+    cnt[r] = __popc(m);
+    hmask[r] = m;
+  }
+}
+
+__global__ void k_row_assign(const int* __restrict__ coors, int N, KGeom g, Shape so, const int* __restrict__ pos,
+                             const unsigned* __restrict__ hmask, int* __restrict__ grid, int* __restrict__ coors_out) {
+  const int r = blockIdx.x * BLK + threadIdx.x;
+  if (r >= N) return;
+  const int* c = coors + 4 * r;
+  int o = pos[r];
+  for (unsigned m = hmask[r]; m; m &= m - 1) {
+    const int k = __ffs(m) - 1;
+    int oz, oy, ox;
+    out_of(c, k, g, so, oz, oy, ox);
+    int* gc = grid + cell(so, c[0], oz, oy, ox);
+    *gc = o;
+    int* co = coors_out + 4 * o;
+    co[0] = c[0];
+    co[1] = oz;
+    co[2] = oy;
+    co[3] = ox;
+    ++o;
+  }
+}
+
 __global__ void k_out_assign(const int* __restrict__ coors, int N, KGeom g, Shape so,
                              const int* __restrict__ flag, const int* __restrict__ pos,
                              int* __restrict__ grid, int* __restrict__ coors_out) {
@@ -794,17 +839,21 @@ extern "C" int rpc_spconv_rulebook_count(const int* coors, int N, const int* out
   if ((long long)N * g.K >= (1LL << 31) - BLK) return RPC_ERR_ARG;   // 32-bit (row, offset) index
   size_t n = (size_t)N * g.K + 1;
   if (ws_bytes < rpc_spconv_rulebook_workspace_size(N, g.K)) return RPC_ERR_WORKSPACE;
-  int* flag = (int*)ws;
+  // per-row head counts [N + 1] and their exclusive scan (the row positions of rpc_spconv_rulebook_build)
+  int* cnt = (int*)ws;
+  unsigned* hmask = (unsigned*)ws + (N + 1);   // the first region holds N*K + 1 >= 2N + 2 ints
   int* pos = (int*)((char*)ws + al(n * sizeof(int)));
   void* tmp = (char*)ws + 2 * al(n * sizeof(int));
   size_t tb = 0;
-  RPC_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, flag, pos, (int)n, st));
+  RPC_CHECK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb, cnt, pos, N + 1, st));
+  if (g.K < 2 || tb > ws_bytes - 2 * al(n * sizeof(int))) return RPC_ERR_WORKSPACE;
   int nb = cdiv((long long)N * g.K, BLK);
   hipLaunchKernelGGL(k_cand_min, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, (unsigned*)grid_out);
-  hipLaunchKernelGGL(k_cand_head, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, (const unsigned*)grid_out, flag);
+  hipLaunchKernelGGL(k_row_heads, dim3(cdiv(32LL * (N + 1), BLK)), dim3(BLK), 0, st, coors, N, g, so,
+                     (const unsigned*)grid_out, cnt, hmask);
   RPC_LAUNCH_CHECK();
-  RPC_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, flag, pos, (int)n, st));
-  RPC_CHECK(hipMemcpyAsync(n_out, pos + (n - 1), sizeof(int), hipMemcpyDeviceToDevice, st));
+  RPC_CHECK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, cnt, pos, N + 1, st));
+  RPC_CHECK(hipMemcpyAsync(n_out, pos + N, sizeof(int), hipMemcpyDeviceToDevice, st));
   return RPC_OK;
 }
 
@@ -817,11 +866,12 @@ extern "C" int rpc_spconv_rulebook_build(const int* coors, int N, const int* out
   KGeom g = geom(ksize, stride, pad);
   if (g.K > MAXK || (long long)N * g.K >= (1LL << 31) - BLK) return RPC_ERR_ARG;
   size_t n = (size_t)N * g.K + 1;
-  int* flag = (int*)ws;
+  const unsigned* hmask = (const unsigned*)ws + (N + 1);
   int* pos = (int*)((char*)ws + al(n * sizeof(int)));
   int nb = cdiv((long long)N * g.K, BLK);
   RPC_CHECK(hipMemsetAsync(nbr_out, 0xFF, sizeof(int) * (size_t)n_out * g.K, st));
-  hipLaunchKernelGGL(k_out_assign, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, flag, pos, grid_out, coors_out);
+  hipLaunchKernelGGL(k_row_assign, dim3(cdiv(N, BLK)), dim3(BLK), 0, st, coors, N, g, so, pos, hmask, grid_out,
+                     coors_out);
   hipLaunchKernelGGL(k_nbr_fill, dim3(nb), dim3(BLK), 0, st, coors, N, g, so, grid_out, nbr_out, nbr_in);
   if (n_out > 0)
     hipLaunchKernelGGL(k_grid_set, dim3(cdiv(n_out, BLK)), dim3(BLK), 0, st, coors_out, n_out, so, grid_out, 1);

@@ -12,12 +12,12 @@ from robustpointclouds_amd import _ffi  # noqa: E402
 SHAPES = [(6, 200, 176, 128, 128), (6, 200, 176, 256, 128), (6, 200, 176, 128, 256), (6, 100, 88, 256, 256)]
 
 
-def main(rounds=5, iters=10, variants=(0, 1, 2)):
+def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None):
     lib = _ffi.load()
     dev = torch.device("cuda")
     st = torch.cuda.current_stream()
     res = {}
-    for (B, H, W, ci, co) in SHAPES:
+    for (B, H, W, ci, co) in (shapes or SHAPES):
         x = (torch.rand(B * H * W, ci, device=dev) * 2 - 1).to(torch.bfloat16)
         wt = ((torch.rand(9, co, ci, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
         z = torch.empty(B * H * W, co, dtype=torch.bfloat16, device=dev)
@@ -58,5 +58,7 @@ if __name__ == "__main__":
     ap.add_argument("--variants", default="0,1,2")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--shapes", default="", help="B,H,W,ci,co;... (default: the SECOND config shapes)")
     a = ap.parse_args()
-    main(a.rounds, a.iters, tuple(int(v) for v in a.variants.split(",")))
+    shapes = [tuple(int(x) for x in sh.split(",")) for sh in a.shapes.split(";") if sh] or None
+    main(a.rounds, a.iters, tuple(int(v) for v in a.variants.split(",")), shapes)

@@ -1,10 +1,11 @@
 #!/bin/bash
-# perturber GPU tests + 3-class profile
+# selected GPU tests, then a rocprof kernel trace of the 3-class bench step
+#   gpurun --timeout 900 -- bash tools/gpu_tests_prof.sh <tag> <test files...>
 set -o pipefail
-OUT=gpurun_out/$1
+OUT=gpurun_out/$1; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_perturber.py tests/test_gpu_e2e_parity.py tests/test_strong_variant.py -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1 && echo tests ok &&
+timeout -k 10 400 python -u -m pytest "$@" -x -q --timeout 300 --timeout-method thread > $OUT/pytest.log 2>&1 && echo tests ok &&
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- python -u bench.py --steps 12 --warmup 6 --no-cpu-baseline > $OUT/prof_bench.log 2>&1
 RC=$?
 KT=$(find $OUT/prof -name '*kernel_trace.csv' | head -1)

@@ -73,6 +73,7 @@ struct IG {
   float* part;     // [gridDim.z * gridDim.x][2 * COUT] BatchNorm partial sums, or null
   Img R, S, O;     // GEMM-row image, source image, output image
   int M;           // GEMM rows = R.B * R.H * R.W
+  int flat;        // grid: 1 = row tiles x channel blocks flattened, a tile's channel blocks adjacent
 };
 
 // 1-tap maps (P1, U2: 2-4 K-steps per block, latency-bound prologue / epilogue) use ONE LDS tile
@@ -88,9 +89,21 @@ __global__ __launch_bounds__(BLK, (taps_of<MAP>() == 1 ? 4 : 2)) void k_igemm(IG
   __shared__ float sP[2][2][TN];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wc = w >> 1, wp = w & 1;  // wave: output channels wc*64.., pixels wp*64..
-  const int bx = xcd_remap(blockIdx.x, gridDim.x);
+  // flat grid: the COUT/TN channel blocks of one row tile are consecutive items on one XCD, so the
+  // tile's activation rows are fetched from HBM once and re-read from that XCD's L2 (the 2-D grid
+  // dispatched every tile of channel block 0 before any of block 1: each re-read went back to memory)
+  const int ncob = g.COUT / TN, ntiles = g.flat ? gridDim.x / ncob : gridDim.x;
+  int bx, cob;
+  if (g.flat) {
+    const int item = xcd_remap(blockIdx.x, gridDim.x);
+    bx = item / ncob;
+    cob = item - bx * ncob;
+  } else {
+    bx = xcd_remap(blockIdx.x, gridDim.x);
+    cob = blockIdx.y;
+  }
   // M_D2P: the 4-tap class (odd, odd) is dispatched first, the 1-tap class last (shorter tail)
-  const int m0 = bx * TM, n0 = blockIdx.y * TN, par = MAP == M_D2P ? 3 - (int)blockIdx.z : blockIdx.z;
+  const int m0 = bx * TM, n0 = cob * TN, par = MAP == M_D2P ? 3 - (int)blockIdx.z : blockIdx.z;
   const int py = par >> 1, px = par & 1;
   // M_D2P: rows of parity class par, a (Hp x Wp) sub-grid of the row image
   const int Hp = MAP == M_D2P ? (g.R.H - py + 1) >> 1 : g.R.H, Wp = MAP == M_D2P ? (g.R.W - px + 1) >> 1 : g.R.W;
@@ -240,7 +253,7 @@ __global__ __launch_bounds__(BLK, (taps_of<MAP>() == 1 ? 4 : 2)) void k_igemm(IG
       }
   }
   __syncthreads();
-  float* prow = g.part + ((size_t)blockIdx.z * gridDim.x + bx) * 2 * g.COUT;
+  float* prow = g.part + ((size_t)blockIdx.z * ntiles + bx) * 2 * g.COUT;
   if (tid < TN) {
     prow[n0 + tid] = sP[0][0][tid] + sP[1][0][tid];
     prow[g.COUT + n0 + tid] = sP[0][1][tid] + sP[1][1][tid];
@@ -1300,6 +1313,10 @@ static void launch_igemm(const IG& g, int par_count, hipStream_t st) {
   // M_D2P: grid over the largest parity class (even rows, even columns)
   const int rows = MAP == M_D2P ? g.R.B * ((g.R.H + 1) / 2) * ((g.R.W + 1) / 2) : g.M;
   dim3 grid(cdivu(rows, TM), g.COUT / TN, par_count);
+  if (g.flat) {
+    grid.x *= grid.y;
+    grid.y = 1;
+  }
   hipLaunchKernelGGL((k_igemm<MAP>), grid, dim3(BLK), 0, st, g);
 }
 
@@ -1345,7 +1362,8 @@ static unsigned ew_blocks(long long m, int c) {
 // 64-channel blocks per CU overlap each other's prologue / epilogue; the 200x176 layers' 858 tiles are
 // 0.84 of 4 rounds for either kernel, and there the register-staged kernel measured 3-8 % faster).
 static int g_s1_variant = 0;
-static int g_wgrad_variant = 0;   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
+static int g_wgrad_variant = 0;
+static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
 static bool s1_wide(int tiles, int cout) {
   if (cout % 128 || g_s1_variant == 1) return false;
@@ -1366,6 +1384,11 @@ extern "C" int rpc_dense_tune(int knob, int value) {
     if (value >= 0) g_wgrad_variant = value;
     return old;
   }
+  if (knob == 2) {
+    const int old = g_ig_order;
+    if (value >= 0) g_ig_order = value;
+    return old;
+  }
   return RPC_ERR_ARG;
 }
 
@@ -1380,6 +1403,9 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   IG g{(const u16*)src, sp, cin, (const u16*)wt, cout, (u16*)out, op, ooff, accum, part,
        img3(r_img), img3(s_img), img3(o_img), 0};
   g.M = g.R.B * g.R.H * g.R.W;
+  // flat grid for two channel blocks (P1 128->256, U2, G2, S2: 3-7 % faster); four adjacent blocks
+  // of one tile (the head's 128->512 data gradient) measured 10 % slower than the 2-D order
+  g.flat = g_ig_order == 0 && cout / TN == 2;
   if (g.M == 0) return RPC_OK;
   hipStream_t st = (hipStream_t)stream;
   if (map == M_S1) {

@@ -1541,7 +1541,7 @@ static inline size_t chan_stride(int rows, int slots) {
 
 struct Layout {
   size_t off, list, meta, xs, z[5], bn[5], bnsum[5], part, gpart, pstat, ticket, dz[6], dh[2], dsig, da,
-      aact, wpart, scan_tmp, scan_bytes, total;
+      aact, wpart, scan_tmp, scan_bytes, cnt, total;
 };
 
 struct ValidCount {
@@ -1559,7 +1559,12 @@ struct ValidCount {
     return c;
   }
 };
-using CountIt = hipcub::TransformInputIterator<int, ValidCount, hipcub::CountingInputIterator<int>>;
+// per-row valid-slot counts as a plain pass (the scan then runs over ints: with the counting done inside
+// the scan's transform iterator the strided slot reads ran at the scan's low parallelism, 38 us)
+__global__ __launch_bounds__(BLK) void k_valid_count(ValidCount vc, int* __restrict__ cnt) {
+  const int v = blockIdx.x * BLK + threadIdx.x;
+  if (v <= vc.rows) cnt[v] = vc(v);
+}
 
 constexpr int KS_MAX = 256;
 
@@ -1583,10 +1588,8 @@ static int make_layout(const rpc_perturber_cfg* cfg, int rows, int slots, Layout
   if (rc) return rc;
   size_t Nmax = chan_stride(rows, slots);
   size_t scan_b = 0;
-  ValidCount vc{nullptr, slots, cfg->F, rows};
-  CountIt it(hipcub::CountingInputIterator<int>(0), vc);
-  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, it, (int*)nullptr, rows + 1, (hipStream_t)0) !=
-      hipSuccess)
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (const int*)nullptr, (int*)nullptr, rows + 1,
+                                       (hipStream_t)0) != hipSuccess)
     return RPC_ERR_HIP;
   int A = cfg->F / 2 > 1 ? cfg->F / 2 : 1;
   size_t welems = 0;
@@ -1594,6 +1597,7 @@ static int make_layout(const rpc_perturber_cfg* cfg, int rows, int slots, Layout
   welems += (size_t)A * (cfg->F + 1) + (size_t)(A + 1);
   size_t o = 0;
   L->off = o; o += al(sizeof(int) * (rows + 2));
+  L->cnt = o; o += al(sizeof(int) * (rows + 1));
   L->list = o; o += al(sizeof(int) * Nmax);
   L->meta = o; o += al(sizeof(int) * 8);
   L->xs = o; o += al(sizeof(float) * MAXF);
@@ -1837,10 +1841,11 @@ extern "C" int rpc_perturber_forward(const rpc_perturber_cfg* cfg, const float* 
   RPC_CHECK(hipMemsetAsync(d.ticket, 0, sizeof(unsigned) * NTICKET * TSTRIDE, st));
   if (d.fused) {
     ValidCount vc{x, slots, cfg->F, rows};
-    CountIt it(hipcub::CountingInputIterator<int>(0), vc);
+    int* cnt = (int*)((char*)workspace + L.cnt);
+    hipLaunchKernelGGL(k_valid_count, dim3((rows + BLK) / BLK), dim3(BLK), 0, st, vc, cnt);
+    RPC_LAUNCH_CHECK();
     size_t sb = L.scan_bytes;
-    RPC_CHECK(hipcub::DeviceScan::ExclusiveSum((char*)workspace + L.scan_tmp, sb, it, d.off,
-                                               rows + 1, st));
+    RPC_CHECK(hipcub::DeviceScan::ExclusiveSum((char*)workspace + L.scan_tmp, sb, cnt, d.off, rows + 1, st));
   }
   const int F = cfg->F;
   if (F == 4) hipLaunchKernelGGL((k_xstats<4>), dim3(GRID), dim3(BLK), 0, st, d);

@@ -106,6 +106,24 @@ def mark_stable(t: torch.Tensor) -> None:
     _STABLE[t.data_ptr()] = t
 
 
+_SCRATCH = {}  # data_ptr -> tensor: persistent gradient images owned by this module (the FPN's data
+              # gradients): rewritten every step before they are read, so a consumer may add into them
+
+
+def _scratch_image(key, B, C, H, W, dev, dt):
+    """A persistent NHWC image for `key` (stable: the backbone's backward graph reads it in place)."""
+    t = _SCRATCH_BY_KEY.get(key)
+    if t is None:
+        t = _image(B, C, H, W, dev, dt)
+        _SCRATCH_BY_KEY[key] = t
+        _SCRATCH[t.data_ptr()] = t
+        mark_stable(t)
+    return t
+
+
+_SCRATCH_BY_KEY = {}
+
+
 def _static_in(t):
     if t is None:
         return None
@@ -416,7 +434,10 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
             elif bi > 0:
                 need_dx = True
                 if gouts[bi - 1] is not None:
-                    dx_out = _nhwc(gouts[bi - 1], dt).clone(memory_format=torch.channels_last)
+                    go = _nhwc(gouts[bi - 1], dt)
+                    # the FPN's persistent data-gradient image is ours to add into (no copy); any other
+                    # incoming gradient is cloned first
+                    dx_out = go if go.data_ptr() in _SCRATCH else go.clone(memory_format=torch.channels_last)
                     accumulate = True
             else:
                 need_dx = need_x
@@ -520,6 +541,7 @@ class NeckFn(torch.autograd.Function):
             out, st_ = _neck_fwd(eng, mod, h0, h1)
         ctx.recs, ctx.Ctot = st_
         ctx.eng = eng
+        ctx.mod_id = id(mod)
         ctx.param_list = params
         return out
 
@@ -531,9 +553,14 @@ class NeckFn(torch.autograd.Function):
         g = _nhwc(gout, eng.dt)
         grads = {}
         dins = []
-        for rec in ctx.recs:
+        for i, rec in enumerate(ctx.recs):
             L = rec["L"]
-            dx, dW, dgam, dbet = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True)
+            dx_out = None
+            if GRAPHS:   # persistent: the backbone's backward graph then reads (and adds into) it in place
+                B, H, W = rec["S"]
+                dx_out = _scratch_image(("fpn_dx", ctx.mod_id, i, B, L.ci, H, W, eng.dt, dev), B, L.ci, H, W,
+                                        dev, eng.dt)
+            dx, dW, dgam, dbet = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True, dx_out)
             grads[id(L.conv.weight)] = dW
             grads[id(L.bnm.weight)] = dgam
             grads[id(L.bnm.bias)] = dbet

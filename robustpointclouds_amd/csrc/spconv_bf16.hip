@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include "common.h"
+#include "dense_common.h"
 #include "rpc_hip.h"
 
 namespace rpc {
@@ -326,7 +327,12 @@ __global__ __launch_bounds__(BLK) void k_wgrad_bf16(const u16* __restrict__ h, i
   __shared__ int sN[SEG * KG];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % WM, wn = w / WM;
-  const int chunk = blockIdx.x, k0 = blockIdx.y * KG;
+  // 1-D grid over (chunk, offset group), XCD-aware: the groups of one row chunk are consecutive items on
+  // one XCD, so its dz rows (read by every group) and its neighbours' h rows are fetched once into that
+  // XCD's L2 (a 2-D grid dispatched a chunk's groups `chunks` blocks apart, after its rows were evicted)
+  const int ngroups = (K + KG - 1) / KG;
+  const int item = dn::xcd_remap(blockIdx.x, gridDim.x);
+  const int chunk = item / ngroups, k0 = (item - chunk * ngroups) * KG;
   const int rb0 = chunk * rows_per, rb1 = min(N, rb0 + rows_per);
   f32x4 acc[KG][TPW];
 #pragma unroll
@@ -617,7 +623,7 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
   int rows_per = ((n_out + chunks - 1) / chunks + 31) / 32 * 32;
   // 128 x 128 tiles keep one kernel offset per block (KG = 1: 64 accumulator registers / lane)
   const int KG = wgrad_kg(ci, co);
-  dim3 grid(chunks, (kvol + KG - 1) / KG);
+  dim3 grid(chunks * ((kvol + KG - 1) / KG));
   float* part = (float*)ws;
   const u16* hp = (const u16*)h;
   const u16* dp = (const u16*)dz;

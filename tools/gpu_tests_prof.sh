@@ -10,6 +10,7 @@ timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/p
 RC=$?
 KT=$(find $OUT/prof -name '*kernel_trace.csv' | head -1)
 [ -n "$KT" ] && python tools/prof_summary.py $KT --steps 8 --top 200 > $OUT/step_kernels.txt 2>&1
+[ -n "$KT" ] && gzip -c $KT > $OUT/kernel_trace.csv.gz
 find $OUT/prof -name '*.csv' -size +1M -delete 2>/dev/null
 find $OUT/prof -name '*.db' -delete 2>/dev/null
 tail -3 $OUT/pytest.log

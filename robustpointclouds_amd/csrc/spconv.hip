@@ -29,6 +29,7 @@
 #include <hip/hip_bf16.h>
 
 #include "common.h"
+#include "dense_common.h"
 
 namespace rpc {
 namespace sp {
@@ -230,7 +231,8 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
   __shared__ unsigned kmask;
   __shared__ float sP[4][2 * CO];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r0 = blockIdx.x * BM;
+  const int lb = dn::xcd_remap(blockIdx.x, gridDim.x);   // XCD-contiguous row blocks (L2-local gathers)
+  const int r0 = lb * BM;
   const int K = g.K;
   if (tid == 0) kmask = 0;
   __syncthreads();
@@ -329,7 +331,7 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
   }
   __syncthreads();
   for (int j = tid; j < 2 * CO; j += BLK)
-    g.part[(long long)blockIdx.x * 2 * CO + j] = sP[0][j] + sP[1][j] + sP[2][j] + sP[3][j];
+    g.part[(long long)lb * 2 * CO + j] = sP[0][j] + sP[1][j] + sP[2][j] + sP[3][j];
 }
 
 // ------------------------------------------------------------------ weight gradient

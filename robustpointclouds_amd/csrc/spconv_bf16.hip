@@ -76,7 +76,11 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   __shared__ int nk;
   __shared__ float sP[GW][2 * NGP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int r0 = blockIdx.x * GBM;
+  // XCD-aware row blocks: each XCD takes one contiguous eighth of the (spatially sorted) rows, so the
+  // neighbour rows its blocks gather — mostly within a few thousand rows — stay in that XCD's L2
+  // (round-robin placement made every XCD gather from the whole source table: L2 misses)
+  const int lb = dn::xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = lb * GBM;
   const int K = g.K;
   {
     // each wave stages its own 16 rows: lane = (offset group k4, row lane&15), 4 offsets per pass;
@@ -222,7 +226,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   // one partial row per 64 rows (waves 4h..4h+3), the layout of rpc_spconv_gemm_blocks
   const int nrow = (g.Nout + BM - 1) / BM;
   for (int j = tid; j < (GW / 4) * 2 * C; j += GBLK) {
-    const int h = j / (2 * C), jj = j - h * 2 * C, prow = blockIdx.x * (GW / 4) + h;
+    const int h = j / (2 * C), jj = j - h * 2 * C, prow = lb * (GW / 4) + h;
     if (prow >= nrow) continue;
     int which = jj / C, c = jj - which * C;
     float s = 0.0f;

@@ -182,22 +182,32 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   }
 
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg (16x16 shapes, gfx950)
+  // E_DGRAD: per output tile n, the previous layer's z of the lane's 4 rows and the column's BatchNorm
+  // parameters are loaded together before the tile's stores (out and ez are not known not to alias:
+  // interleaved with the stores, every z load waited for its own round trip — 16 per lane)
   float s1[NT], s2[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) {
     s1[n] = s2[n] = 0.0f;
     int col = n * 16 + (lane & 15);
+    float zr[4], pb[4];
+    if (EPI == E_DGRAD) {
+      const int C = g.CO_real, cc = min(col, C - 1);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];   // scale, beta, mean, invstd
+#pragma unroll
+      for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)min(r0 + w * 16 + (lane >> 4) * 4 + j, g.Nout - 1) * C + cc];
+    }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       int row = r0 + w * 16 + (lane >> 4) * 4 + j;
       float v = acc[n][j];
       if (row < g.Nout && col < g.CO_real) {
         if (EPI == E_DGRAD) {
-          const int C = g.CO_real;
-          float zz = g.ez[(long long)row * C + col];
-          float h = fmaxf(fmaf(zz - g.ebn[2 * C + col], g.ebn[col], g.ebn[C + col]), 0.0f);
+          const float zz = zr[j];
+          float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
           v = h > 0.0f ? v : 0.0f;
-          float xh = (zz - g.ebn[2 * C + col]) * g.ebn[3 * C + col];
+          float xh = (zz - pb[2]) * pb[3];
           s1[n] += v;
           s2[n] += v * xh;
         } else {

@@ -275,6 +275,68 @@ __global__ __launch_bounds__(BLK) void k_dz_bf16(const float* __restrict__ dy, c
   dz[t] = to_bf16(v);
 }
 
+// 8-channel forms of the two producers for C % 8 == 0 (every bf16 layer): one thread per 8 channels of
+// a row — two float4 loads per operand, BatchNorm parameters as float4, one 16-byte bf16 store, 32-bit
+// index arithmetic (the scalar forms above spend their time in the 64-bit division t / CP). Same
+// arithmetic per element, so the same bits.
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+__device__ __forceinline__ void st8h(u16* p, const float (&v)[8]) {
+  u16 o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = to_bf16(v[j]);
+  *(uint4*)p = *(const uint4*)o;
+}
+
+__global__ __launch_bounds__(BLK) void k_to_bf16_v8(const float* __restrict__ z, const float* __restrict__ bn, int N,
+                                                    int C, int relu, u16* __restrict__ h) {
+  const int C8 = C >> 3;
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * C8) return;
+  const int r = t / C8, c = (t - r * C8) * 8;
+  float v[8];
+  ld8f(z + (size_t)r * C + c, v);
+  if (bn) {
+    float mu[8], sc[8], be[8];
+    ld8f(bn + 2 * C + c, mu);
+    ld8f(bn + c, sc);
+    ld8f(bn + C + c, be);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j] - mu[j], sc[j], be[j]);
+  }
+  if (relu) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+  }
+  st8h(h + (size_t)r * C + c, v);
+}
+
+__global__ __launch_bounds__(BLK) void k_dz_bf16_v8(const float* __restrict__ dy, const float* __restrict__ z,
+                                                    const float* __restrict__ bnb, int N, int C,
+                                                    u16* __restrict__ dz) {
+  const int C8 = C >> 3;
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * C8) return;
+  const int r = t / C8, c = (t - r * C8) * 8;
+  float d[8], zz[8], gi[8], m1[8], m2[8], mb[8], ib[8];
+  ld8f(dy + (size_t)r * C + c, d);
+  ld8f(z + (size_t)r * C + c, zz);
+  ld8f(bnb + c, gi);
+  ld8f(bnb + C + c, m1);
+  ld8f(bnb + 2 * C + c, m2);
+  ld8f(bnb + 3 * C + c, mb);
+  ld8f(bnb + 4 * C + c, ib);
+  float v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float xh = (zz[j] - mb[j]) * ib[j];
+    v[j] = gi[j] * (d[j] - m1[j] - xh * m2[j]);
+  }
+  st8h(dz + (size_t)r * C + c, v);
+}
+
 // W fp32 [K][CI][CO] -> B^T bf16 [K][NGP][KGP]; fwd: n = co, kk = ci ; dgrad: n = ci, kk = co
 __device__ __forceinline__ void wprep_elem(long long t, const float* __restrict__ W, int CI, int CO, int dgrad,
                                            int NGP, int KGP, u16* __restrict__ bt) {
@@ -496,8 +558,12 @@ extern "C" int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, i
   if (n < 0 || c < 1) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   int cp = r8(c);
-  hipLaunchKernelGGL(k_to_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, n, c,
-                     cp, relu, (u16*)h);
+  if (c % 8 == 0 && (long long)n * (c / 8) < (1LL << 31))
+    hipLaunchKernelGGL(k_to_bf16_v8, dim3(cdiv((long long)n * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn,
+                       n, c, relu, (u16*)h);
+  else
+    hipLaunchKernelGGL(k_to_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, n, c,
+                       cp, relu, (u16*)h);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
@@ -507,8 +573,12 @@ extern "C" int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const flo
   if (n < 0 || c < 1) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   int cp = r8(c);
-  hipLaunchKernelGGL(k_dz_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, dy, z, bnb,
-                     n, c, cp, (u16*)dz);
+  if (c % 8 == 0 && (long long)n * (c / 8) < (1LL << 31))
+    hipLaunchKernelGGL(k_dz_bf16_v8, dim3(cdiv((long long)n * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream, dy, z,
+                       bnb, n, c, (u16*)dz);
+  else
+    hipLaunchKernelGGL(k_dz_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, dy, z, bnb,
+                       n, c, cp, (u16*)dz);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -82,3 +82,44 @@ def test_wgrad_bf16_rejects_short_workspace_and_empty():
     _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hd), 16, _ffi.ptr(nd), 27, 0, _ffi.ptr(dd), 16, _ffi.ptr(dW),
                                          _ffi.ptr(ws), wsz, st), "wgrad_bf16(empty)")
     assert dW.abs().max().item() == 0.0
+
+
+def _bf16_ulp_close(got, want, atol=1e-30):
+    """got (bf16 on the GPU) within one bf16 ulp of the float64 value want (+ atol: the fp32 rounding of
+    the kernel's intermediate terms where they cancel)."""
+    g = got.float().double().cpu()
+    w = want.double()
+    ulp = w.abs() * 2.0 ** -7
+    assert ((g - w).abs() <= ulp + atol).all(), float(((g - w).abs() - ulp).max())
+
+
+@pytest.mark.parametrize("n,c", [(4097, 64), (333, 16), (1000, 128), (515, 60)])
+def test_bf16_row_producers(n, c):
+    """rpc_to_bf16_rows (relu(bn(z)) -> bf16 rows of pitch round8(C)) and rpc_bnbwd_to_bf16_rows
+    (gi * (dy - m1 - xhat*m2) -> bf16): the 8-channel vector forms (C % 8 == 0) and the scalar form
+    (C = 60, padded channels zero) against float64 within one bf16 ulp."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(n + c)
+    cp = _r8(c)
+    z = torch.randn(n, c, generator=g) * 2
+    dy = torch.randn(n, c, generator=g)
+    bn = torch.cat([torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.3,
+                    torch.randn(c, generator=g) * 0.2, torch.rand(c, generator=g) + 0.5])
+    bnb = torch.cat([torch.rand(c, generator=g) + 0.5] + [torch.randn(c, generator=g) * 0.3 for _ in range(4)])
+    zd, dyd, bnd, bnbd = z.to(dev), dy.to(dev), bn.to(dev), bnb.to(dev)
+    h = torch.full((n, cp), 7.0, dtype=torch.bfloat16, device=dev)
+    dz = torch.full((n, cp), 7.0, dtype=torch.bfloat16, device=dev)
+    st = _ffi.stream_of(h)
+    _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(zd), _ffi.ptr(bnd), n, c, 1, _ffi.ptr(h), st), "rpc_to_bf16_rows")
+    _ffi.check(lib.rpc_bnbwd_to_bf16_rows(_ffi.ptr(dyd), _ffi.ptr(zd), _ffi.ptr(bnbd), n, c, _ffi.ptr(dz), st),
+               "rpc_bnbwd_to_bf16_rows")
+    torch.cuda.synchronize()
+    sc, be, mu = bn.double().view(4, c)[:3]
+    want_h = torch.clamp((z.double() - mu) * sc + be, min=0.0)
+    gi, m1, m2, mb, ib = bnb.double().view(5, c)
+    want_dz = gi * (dy.double() - m1 - (z.double() - mb) * ib * m2)
+    _bf16_ulp_close(h[:, :c], want_h)
+    _bf16_ulp_close(dz[:, :c], want_dz, atol=1e-5)
+    if cp > c:
+        assert (h[:, c:] == 0).all() and (dz[:, c:] == 0).all()

@@ -535,6 +535,26 @@ __global__ __launch_bounds__(BLK) void k_to_dense(const float* __restrict__ z, c
 }
 
 constexpr int FBLK = 1024;   // k_from_dense: 1024 threads = 1024 / C row lanes over the block's 64 rows
+// C % 4 == 0 form: 4 channels of a row per thread, float4 operand loads, 32-bit indexing (the scalar
+// form's time went to a 64-bit division per element); same arithmetic per element
+template <typename T, bool NHWC>
+__global__ __launch_bounds__(BLK) void k_to_dense_v4(const float* __restrict__ z, const float* __restrict__ bn,
+                                                     const int* __restrict__ coors, int N, int C, Shape s,
+                                                     T* __restrict__ dense) {
+  const int C4 = C >> 2;
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * C4) return;
+  const int r = t / C4, c = (t - r * C4) * 4;
+  const float4 zv = *(const float4*)(z + (size_t)r * C + c);
+  const float4 mu = *(const float4*)(bn + 2 * C + c), sc = *(const float4*)(bn + c), be = *(const float4*)(bn + C + c);
+  const float zz[4] = {zv.x, zv.y, zv.z, zv.w}, m[4] = {mu.x, mu.y, mu.z, mu.w}, a[4] = {sc.x, sc.y, sc.z, sc.w},
+              b[4] = {be.x, be.y, be.z, be.w};
+  const int4 co = *(const int4*)(coors + 4 * r);
+  const int cr[4] = {co.x, co.y, co.z, co.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+    store_val(dense + dense_index<NHWC>(cr, c + j, C, s), fmaxf(fmaf(zz[j] - m[j], a[j], b[j]), 0.0f));
+}
 template <typename T, bool NHWC>
 __global__ __launch_bounds__(FBLK) void k_from_dense(const T* __restrict__ gd, const float* __restrict__ z,
                                                     const float* __restrict__ bn, const int* __restrict__ coors,
@@ -1012,8 +1032,21 @@ extern "C" int rpc_sparse_to_dense(const float* z, const float* bn, const int* c
   if (N < 0 || C < 1 || !shape || (flags & ~3)) return RPC_ERR_ARG;
   if (N == 0) return RPC_OK;
   Shape s{shape[0], shape[1], shape[2], shape[3]};
-  dim3 g(cdiv((long long)N * C, BLK));
   hipStream_t st = (hipStream_t)stream;
+  if (C % 4 == 0 && (long long)N * (C / 4) < (1LL << 31)) {
+    dim3 g4(cdiv((long long)N * (C / 4), BLK));
+    switch (flags) {
+      case 0: hipLaunchKernelGGL((k_to_dense_v4<float, false>), g4, dim3(BLK), 0, st, z, bn, coors, N, C, s, (float*)dense); break;
+      case 1: hipLaunchKernelGGL((k_to_dense_v4<float, true>), g4, dim3(BLK), 0, st, z, bn, coors, N, C, s, (float*)dense); break;
+      case 2: hipLaunchKernelGGL((k_to_dense_v4<__hip_bfloat16, false>), g4, dim3(BLK), 0, st, z, bn, coors, N, C, s,
+                                 (__hip_bfloat16*)dense); break;
+      default: hipLaunchKernelGGL((k_to_dense_v4<__hip_bfloat16, true>), g4, dim3(BLK), 0, st, z, bn, coors, N, C, s,
+                                  (__hip_bfloat16*)dense);
+    }
+    RPC_LAUNCH_CHECK();
+    return RPC_OK;
+  }
+  dim3 g(cdiv((long long)N * C, BLK));
   switch (flags) {
     case 0: hipLaunchKernelGGL((k_to_dense<float, false>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s, (float*)dense); break;
     case 1: hipLaunchKernelGGL((k_to_dense<float, true>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s, (float*)dense); break;

@@ -1301,11 +1301,44 @@ constexpr int WPREP_MAX = 16;
 struct WprepBatch {
   RpcDenseWprep d[WPREP_MAX];
 };
+// LDS-tiled form: the torch weight of a layer is [A][Bd][T] (Conv2d: A = co, Bd = ci; ConvTranspose2d:
+// A = ci, Bd = co) and both operands are a tap-major copy of it, one as [t][a][b], the other as [t][b][a].
+// A block moves a 32 x 32 (a, b) tile with all its taps: source rows of 32*T contiguous floats read
+// coalesced into LDS, then 64-byte bf16 rows written to both operands (the per-element form read with
+// a stride of CI*T floats and wrote 2-byte scattered stores, behind 64-bit index divisions).
+constexpr int WPT = 32;
+constexpr int WPT_MAXT = 9;
 __global__ __launch_bounds__(BLK) void k_wprep_batch(WprepBatch b) {
+  // [t][a][b] at t*TP + a*(WPT+1) + b: the odd tap stride keeps the tap-fastest stores of the load
+  // loop on distinct banks, the row pad the transposed reads of out2
+  constexpr int TP = WPT * (WPT + 1) + 1;
+  __shared__ float tile[WPT_MAXT * TP];
   const RpcDenseWprep& d = b.d[blockIdx.y];
-  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (e < (long long)d.taps * d.ci * d.co)
-    wprep_elem(e, d.W, d.kind, d.ci, d.co, d.taps, d.flip, (u16*)d.w_fwd, (u16*)d.w_dgrad);
+  const int T = d.taps;
+  const int A = d.kind == 0 ? d.co : d.ci, Bd = d.kind == 0 ? d.ci : d.co;
+  const int nbt = (Bd + WPT - 1) / WPT;
+  const int ntile = ((A + WPT - 1) / WPT) * nbt;
+  if ((int)blockIdx.x >= ntile) return;
+  const int a0 = (blockIdx.x / nbt) * WPT, b0 = (blockIdx.x % nbt) * WPT;
+  const int an = min(WPT, A - a0), bn = min(WPT, Bd - b0);
+  const int row = bn * T;   // contiguous source floats per a
+  for (int q = threadIdx.x; q < an * row; q += BLK) {
+    const int ar = q / row, k = q - ar * row, br = k / T, t = k - br * T;
+    tile[t * TP + ar * (WPT + 1) + br] = d.W[((size_t)(a0 + ar) * Bd + b0) * T + k];
+  }
+  __syncthreads();
+  // out1[t][a][b] (Conv2d: w_fwd [t][co][ci]; ConvTranspose2d: w_dgrad [t][ci][co])
+  // out2[t][b][a] (Conv2d: w_dgrad [td][ci][co], td = flip ? T-1-t : t; ConvTranspose2d: w_fwd [t][co][ci])
+  u16* out1 = (u16*)(d.kind == 0 ? d.w_fwd : d.w_dgrad);
+  u16* out2 = (u16*)(d.kind == 0 ? d.w_dgrad : d.w_fwd);
+  const int flip1 = d.kind == 0 ? 0 : d.flip, flip2 = d.kind == 0 ? d.flip : 0;
+  for (int q = threadIdx.x; q < T * WPT * WPT; q += BLK) {
+    const int t = q / (WPT * WPT), r = (q / WPT) % WPT, c = q % WPT;
+    if (out1 && r < an && c < bn)
+      out1[((size_t)(flip1 ? T - 1 - t : t) * A + a0 + r) * Bd + b0 + c] = f2bf(tile[t * TP + r * (WPT + 1) + c]);
+    if (out2 && r < bn && c < an)
+      out2[((size_t)(flip2 ? T - 1 - t : t) * Bd + b0 + r) * A + a0 + c] = f2bf(tile[t * TP + c * (WPT + 1) + r]);
+  }
 }
 
 template <int MAP>
@@ -1554,12 +1587,13 @@ extern "C" int rpc_dense_wprep_batch(const RpcDenseWprep* descs, int n, void* st
   long long most = 0;
   for (int i = 0; i < n; ++i) {
     const RpcDenseWprep& d = descs[i];
-    if (!d.W || d.ci < 1 || d.co < 1 || d.taps < 1 || (d.kind != 0 && d.kind != 1)) return RPC_ERR_ARG;
+    if (!d.W || d.ci < 1 || d.co < 1 || d.taps < 1 || d.taps > WPT_MAXT || (d.kind != 0 && d.kind != 1))
+      return RPC_ERR_ARG;
     b.d[i] = d;
-    const long long e = (long long)d.taps * d.ci * d.co;
+    const long long e = (long long)((d.ci + WPT - 1) / WPT) * ((d.co + WPT - 1) / WPT);
     most = e > most ? e : most;
   }
-  hipLaunchKernelGGL(k_wprep_batch, dim3(cdivu(most, BLK), n), dim3(BLK), 0, (hipStream_t)stream, b);
+  hipLaunchKernelGGL(k_wprep_batch, dim3((unsigned)most, n), dim3(BLK), 0, (hipStream_t)stream, b);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -404,3 +404,31 @@ def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):
     scale = wr.grad.abs().max().item()
     assert (outs[0] - wr.grad).abs().max().item() <= 1e-5 * scale
     assert (outs[0] - outs[1]).abs().max().item() <= 2e-6 * scale
+
+
+def test_wprep_batch_matches_per_layer_prep():
+    """rpc_dense_wprep_batch (LDS-tiled, every layer of a module in one launch) writes the same bf16
+    operands as rpc_dense_wprep (per element) for Conv2d 3x3 (flipped and not), ConvTranspose2d k2 / k1
+    and a non-multiple-of-32 width."""
+    lib = _ffi.load()
+    g = torch.Generator().manual_seed(61)
+    layers = [(0, 128, 128, 9, 1), (0, 256, 128, 9, 0), (1, 256, 256, 4, 0), (1, 128, 256, 1, 0), (0, 96, 160, 9, 1)]
+    descs = (_ffi.RpcDenseWprep * len(layers))()
+    keep, outs = [], []
+    for i, (kind, ci, co, T, flip) in enumerate(layers):
+        k = int(round(T ** 0.5))
+        shape = (co, ci, k, k) if kind == 0 else (ci, co, k, k)
+        W = torch.randn(*shape, generator=g).to(DEV)
+        wf = torch.empty((T, co, ci), dtype=torch.bfloat16, device=DEV)
+        wd = torch.empty((T, ci, co), dtype=torch.bfloat16, device=DEV)
+        descs[i] = _ffi.RpcDenseWprep(W.data_ptr(), wf.data_ptr(), wd.data_ptr(), kind, ci, co, T, flip)
+        keep.append(W)
+        outs.append((wf, wd))
+    _ffi.check(lib.rpc_dense_wprep_batch(descs, len(layers), _ffi.stream_of(keep[0])), "rpc_dense_wprep_batch")
+    for (kind, ci, co, T, flip), W, (wf, wd) in zip(layers, keep, outs):
+        rf = torch.empty_like(wf)
+        rd = torch.empty_like(wd)
+        _ffi.check(lib.rpc_dense_wprep(_ffi.ptr(W), kind, ci, co, T, flip, _ffi.ptr(rf), _ffi.ptr(rd),
+                                       _ffi.stream_of(W)), "rpc_dense_wprep")
+        torch.cuda.synchronize()
+        assert torch.equal(wf, rf) and torch.equal(wd, rd), (kind, ci, co, T, flip)

@@ -82,20 +82,26 @@ __global__ __launch_bounds__(OBLK) void k_sqnorm(const long long* __restrict__ g
   if (g) {
     g += s0;
     int i0 = 0;
-    if ((((uintptr_t)g) & 15) == 0) {   // 16-B loads, four in flight per thread, four partial sums
+    // four float4 in flight per thread, four partial sums; a gradient view at an odd offset (DDP bucket)
+    // is read with scalar loads in the same loop
+    const bool gvec = (((uintptr_t)g) & 15) == 0;
+    auto ldg4 = [&](int q) -> float4 {
+      return gvec ? ((const float4*)g)[q] : make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+    };
+    {
       const int n4 = n >> 2;
       double a[4] = {0.0, 0.0, 0.0, 0.0};
       int q = threadIdx.x;
       for (; q + 3 * OBLK < n4; q += 4 * OBLK) {
         float4 v[4];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = ((const float4*)g)[q + u * OBLK];
+        for (int u = 0; u < 4; ++u) v[u] = ldg4(q + u * OBLK);
 #pragma unroll
         for (int u = 0; u < 4; ++u)
           a[u] += ((double)v[u].x * v[u].x + (double)v[u].y * v[u].y) + ((double)v[u].z * v[u].z + (double)v[u].w * v[u].w);
       }
       for (; q < n4; q += OBLK) {
-        const float4 v = ((const float4*)g)[q];
+        const float4 v = ldg4(q);
         a[0] += ((double)v.x * v.x + (double)v.y * v.y) + ((double)v.z * v.z + (double)v.w * v.w);
       }
       acc = (a[0] + a[1]) + (a[2] + a[3]);
@@ -111,10 +117,18 @@ __global__ __launch_bounds__(OBLK) void k_sqnorm(const long long* __restrict__ g
   __syncthreads();
   if (threadIdx.x == 0) part[c] = ((sh[0] + sh[1]) + sh[2]) + sh[3];
   if (!last_block_arrive_2d(ticket, &last, nchunks)) return;
-  if (threadIdx.x < 64) {
+  {
+    // the last block: all its threads read the partials (about two each, in flight together), then
+    // the four waves are combined in order (was one wave walking ~7 dependent loads per lane)
     double s = 0.0;
-    for (int k = threadIdx.x; k < nchunks; k += 64) s += part[k];
+    for (int k = threadIdx.x; k < nchunks; k += OBLK) s += part[k];
     s = wave_sum(s);
+    __syncthreads();
+    if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+    __syncthreads();
+  }
+  if (threadIdx.x < 64) {
+    const double s = ((sh[0] + sh[1]) + sh[2]) + sh[3];
     if (threadIdx.x == 0) {
       const float norm = (float)sqrt(s);
       float coef = 1.0f;
@@ -163,12 +177,41 @@ __global__ __launch_bounds__(OBLK) void k_adamw(const long long* __restrict__ pp
   const float step = steps[t];
   const float step_size = lr / (1.0f - powf(a.h.beta1, step));
   const float bc2_sqrt = sqrtf(1.0f - powf(a.h.beta2, step));
-  const bool vec = ((((uintptr_t)p | (uintptr_t)g | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
+  // p / m / v are 16-byte aligned (the moments' views are padded, optim.py); a gradient that is a view
+  // into a DDP bucket at an odd offset is read with scalar loads inside the vector loop
+  const bool vec = ((((uintptr_t)p | (uintptr_t)m | (uintptr_t)v) & 15) == 0);
+  const bool gvec = (((uintptr_t)g) & 15) == 0;
+  auto ldg4 = [&](int q) -> float4 {
+    return gvec ? ((const float4*)g)[q] : make_float4(g[4 * q], g[4 * q + 1], g[4 * q + 2], g[4 * q + 3]);
+  };
   int i0 = 0;
   if (vec) {
     const int n4 = n >> 2;
-    for (int q = threadIdx.x; q < n4; q += OBLK) {
-      float4 pp = ((float4*)p)[q], gg = ((const float4*)g)[q], mm = ((float4*)m)[q], vv = ((float4*)v)[q];
+    int q = threadIdx.x;
+    // four float4 of each operand in flight per thread (a 16384-element chunk is 16 float4 per thread:
+    // one load round trip per float4 made the pass latency-bound at ~2.9 TB/s)
+    for (; q + 3 * OBLK < n4; q += 4 * OBLK) {
+      float4 pp[4], gg[4], mm[4], vv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        pp[u] = ((float4*)p)[q + u * OBLK];
+        gg[u] = ldg4(q + u * OBLK);
+        mm[u] = ((float4*)m)[q + u * OBLK];
+        vv[u] = ((float4*)v)[q + u * OBLK];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        adamw1(pp[u].x, gg[u].x * coef, mm[u].x, vv[u].x, lr, step_size, bc2_sqrt, a.h);
+        adamw1(pp[u].y, gg[u].y * coef, mm[u].y, vv[u].y, lr, step_size, bc2_sqrt, a.h);
+        adamw1(pp[u].z, gg[u].z * coef, mm[u].z, vv[u].z, lr, step_size, bc2_sqrt, a.h);
+        adamw1(pp[u].w, gg[u].w * coef, mm[u].w, vv[u].w, lr, step_size, bc2_sqrt, a.h);
+        ((float4*)p)[q + u * OBLK] = pp[u];
+        ((float4*)m)[q + u * OBLK] = mm[u];
+        ((float4*)v)[q + u * OBLK] = vv[u];
+      }
+    }
+    for (; q < n4; q += OBLK) {
+      float4 pp = ((float4*)p)[q], gg = ldg4(q), mm = ((float4*)m)[q], vv = ((float4*)v)[q];
       adamw1(pp.x, gg.x * coef, mm.x, vv.x, lr, step_size, bc2_sqrt, a.h);
       adamw1(pp.y, gg.y * coef, mm.y, vv.y, lr, step_size, bc2_sqrt, a.h);
       adamw1(pp.z, gg.z * coef, mm.z, vv.z, lr, step_size, bc2_sqrt, a.h);

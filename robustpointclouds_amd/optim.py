@@ -47,11 +47,15 @@ class ClipAdamW:
                 raise RuntimeError("ClipAdamW needs contiguous fp32 parameters on one device")
         self.device = dev
         numel = [p.numel() for p in self.params]
-        total = sum(numel)
-        # moments in two flat buffers (torch's state['exp_avg'/'exp_avg_sq'] are views of them)
+        # moments in two flat buffers (torch's state['exp_avg'/'exp_avg_sq'] are views of them); every
+        # view starts on a 256-byte boundary so the kernels' 16-byte vector path applies to all of them
+        # (unpadded, the first tensor whose size is not a multiple of 4 — a head bias — pushed every
+        # later tensor onto the scalar path)
+        padded = [(n + 63) // 64 * 64 for n in numel]
+        total = int(sum(padded))
         self.exp_avg = torch.zeros(total, dtype=torch.float32, device=dev)
         self.exp_avg_sq = torch.zeros(total, dtype=torch.float32, device=dev)
-        offs = np.concatenate([[0], np.cumsum(numel)[:-1]]).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(padded)[:-1]]).astype(np.int64)
         self._m_views = [self.exp_avg[o:o + n].view_as(p) for o, n, p in zip(offs, numel, self.params)]
         self._v_views = [self.exp_avg_sq[o:o + n].view_as(p) for o, n, p in zip(offs, numel, self.params)]
         self.steps = torch.zeros(len(self.params), dtype=torch.float32, device=dev)

@@ -237,12 +237,23 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
   if (tid == 0) kmask = 0;
   __syncthreads();
   unsigned my = 0;
-  for (int q = tid; q < BM * K; q += BLK) {
-    int r = q / K, k = q - r * K;
-    int kc = g.rev ? K - 1 - k : k;
-    int v = (r0 + r < g.Nout) ? g.nbr[(long long)(r0 + r) * K + kc] : -1;
-    sN[r * MAXK + k] = v;
-    if (v >= 0) my |= 1u << k;
+  {
+    // all of the thread's neighbour-index loads in flight before the first LDS store
+    constexpr int PN = (BM * MAXK + BLK - 1) / BLK;
+    int nv[PN];
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+      const int q = tid + i * BLK, r = q / K, k = q - r * K;
+      const int kc = g.rev ? K - 1 - k : k;
+      nv[i] = (q < BM * K && r0 + r < g.Nout) ? g.nbr[(long long)(r0 + r) * K + kc] : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < PN; ++i) {
+      const int q = tid + i * BLK, r = q / K, k = q - r * K;
+      if (q >= BM * K) continue;
+      sN[r * MAXK + k] = nv[i];
+      if (nv[i] >= 0) my |= 1u << k;
+    }
   }
   if (my) atomicOr(&kmask, my);
   __syncthreads();
@@ -250,35 +261,9 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
   f32x4 acc[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  for (int k = 0; k < K; ++k) {
-    if (!((mask >> k) & 1u)) continue;
-    __syncthreads();
-    // gather A_k: BM rows x CI, transformed on load
-    for (int q = tid; q < BM * CIP; q += BLK) {
-      int r = q / CIP, c = q - r * CIP;
-      int src = c < CI ? sN[r * MAXK + k] : -1;
-      float v = 0.0f;
-      if (src >= 0) {
-        float x = g.a[(long long)src * CI + c];
-        if (AT == A_BNRELU) v = fmaxf(fmaf(x - g.abn[2 * CI + c], g.abn[c], g.abn[CI + c]), 0.0f);
-        else if (AT == A_BNBWD) {
-          float zz = g.a2[(long long)src * CI + c];
-          float xh = (zz - g.abn[3 * CI + c]) * g.abn[4 * CI + c];
-          v = g.abn[c] * (x - g.abn[CI + c] - xh * g.abn[2 * CI + c]);
-        } else v = x;
-      }
-      sA[r * AS + c] = v;
-    }
-    // B_k = W[k] (CI x CO) or W[k]^T ; zero-pad columns beyond the stored width
-    const float* Wk = g.W + (long long)k * g.CIw * g.COw;
-    for (int q = tid; q < CIP * CO; q += BLK) {
-      int c = q / CO, n = q - c * CO;
-      float v = 0.0f;
-      if (!g.transW) { if (c < g.CIw && n < g.COw) v = Wk[c * g.COw + n]; }
-      else { if (n < g.CIw && c < g.COw) v = Wk[n * g.COw + c]; }
-      sB[c * BS + n] = v;
-    }
-    __syncthreads();
+  constexpr int PA = (BM * CIP + BLK - 1) / BLK, PB = (CIP * CO + BLK - 1) / BLK;
+  constexpr int GA = PA < 8 ? PA : 8, GB = PB < 8 ? PB : 8;   // loads in flight per group (registers)
+  auto mfma_k = [&]() {
     const float* pa = sA + (w * 16 + (lane & 15)) * AS + (lane >> 4);
     const float* pb = sB + (lane >> 4) * BS + (lane & 15);
 #pragma unroll 4
@@ -289,6 +274,129 @@ __global__ __launch_bounds__(BLK) void k_gemm(GemmArgs g) {
         float b = pb[kk * 4 * BS + n * 16];
         acc[n] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[n], 0, 0, 0);
       }
+    }
+  };
+  if constexpr (PA <= 8 && PB <= 8) {
+    // narrow layers (every register-held operand fits one group): the next offset's gathers and weight
+    // tile are loaded into registers while the MFMAs of the current one run (one exposed round trip per
+    // offset was the whole cost of these layers)
+    float xa[PA], za[PA], wb[PB];
+    auto load = [&](int k) {
+#pragma unroll
+      for (int j = 0; j < PA; ++j) {
+        const int q = tid + j * BLK, r = q / CIP, c = q - r * CIP;
+        const int src = (q < BM * CIP && c < CI) ? sN[r * MAXK + k] : -1;
+        xa[j] = src >= 0 ? g.a[(long long)src * CI + c] : 0.0f;
+        za[j] = (AT == A_BNBWD && src >= 0) ? g.a2[(long long)src * CI + c] : 0.0f;
+      }
+      const float* Wk = g.W + (long long)k * g.CIw * g.COw;
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int q = tid + j * BLK, c = q / CO, n = q - c * CO;
+        float v = 0.0f;
+        if (q < CIP * CO) {
+          if (!g.transW) { if (c < g.CIw && n < g.COw) v = Wk[c * g.COw + n]; }
+          else { if (n < g.CIw && c < g.COw) v = Wk[n * g.COw + c]; }
+        }
+        wb[j] = v;
+      }
+    };
+    auto stage = [&](int k) {
+#pragma unroll
+      for (int j = 0; j < PA; ++j) {
+        const int q = tid + j * BLK, r = q / CIP, c = q - r * CIP;
+        if (q >= BM * CIP) continue;
+        const int src = c < CI ? sN[r * MAXK + k] : -1;
+        float v = 0.0f;
+        if (src >= 0) {
+          const float x = xa[j];
+          if (AT == A_BNRELU) v = fmaxf(fmaf(x - g.abn[2 * CI + c], g.abn[c], g.abn[CI + c]), 0.0f);
+          else if (AT == A_BNBWD) {
+            const float zz = za[j];
+            const float xh = (zz - g.abn[3 * CI + c]) * g.abn[4 * CI + c];
+            v = g.abn[c] * (x - g.abn[CI + c] - xh * g.abn[2 * CI + c]);
+          } else v = x;
+        }
+        sA[r * AS + c] = v;
+      }
+#pragma unroll
+      for (int j = 0; j < PB; ++j) {
+        const int q = tid + j * BLK, c = q / CO, n = q - c * CO;
+        if (q < CIP * CO) sB[c * BS + n] = wb[j];
+      }
+    };
+    auto next_k = [&](int k) {   // first offset > k with a neighbour in the block (K when none)
+      const unsigned rest = k < 0 ? mask : (mask & ~((2u << k) - 1u));
+      return rest ? __ffs(rest) - 1 : K;
+    };
+    int k = next_k(-1);
+    if (k < K) load(k);
+    while (k < K) {
+      __syncthreads();   // the previous offset's MFMAs are done with sA / sB
+      stage(k);
+      __syncthreads();
+      const int kn = next_k(k);
+      if (kn < K) load(kn);
+      mfma_k();
+      k = kn;
+    }
+  } else {
+    for (int k = 0; k < K; ++k) {
+      if (!((mask >> k) & 1u)) continue;
+      __syncthreads();
+      // gather A_k (BM rows x CI, transformed on load) and B_k = W[k] (CI x CO) or W[k]^T (zero-padded
+      // beyond the stored width): every global load of the thread is issued before the first LDS store
+      // (as strided load -> store loops each load waited out its own round trip, ~5 per offset)
+  #pragma unroll 1
+      for (int i0 = 0; i0 < PA; i0 += GA) {
+        float xa[GA], za[GA];
+  #pragma unroll
+        for (int j = 0; j < GA; ++j) {
+          const int q = tid + (i0 + j) * BLK, r = q / CIP, c = q - r * CIP;
+          const int src = (q < BM * CIP && c < CI) ? sN[r * MAXK + k] : -1;
+          xa[j] = src >= 0 ? g.a[(long long)src * CI + c] : 0.0f;
+          za[j] = (AT == A_BNBWD && src >= 0) ? g.a2[(long long)src * CI + c] : 0.0f;
+        }
+  #pragma unroll
+        for (int j = 0; j < GA; ++j) {
+          const int q = tid + (i0 + j) * BLK, r = q / CIP, c = q - r * CIP;
+          if (q >= BM * CIP) continue;
+          const int src = c < CI ? sN[r * MAXK + k] : -1;
+          float v = 0.0f;
+          if (src >= 0) {
+            const float x = xa[j];
+            if (AT == A_BNRELU) v = fmaxf(fmaf(x - g.abn[2 * CI + c], g.abn[c], g.abn[CI + c]), 0.0f);
+            else if (AT == A_BNBWD) {
+              const float zz = za[j];
+              const float xh = (zz - g.abn[3 * CI + c]) * g.abn[4 * CI + c];
+              v = g.abn[c] * (x - g.abn[CI + c] - xh * g.abn[2 * CI + c]);
+            } else v = x;
+          }
+          sA[r * AS + c] = v;
+        }
+      }
+      const float* Wk = g.W + (long long)k * g.CIw * g.COw;
+  #pragma unroll 1
+      for (int i0 = 0; i0 < PB; i0 += GB) {
+        float wb[GB];
+  #pragma unroll
+        for (int j = 0; j < GB; ++j) {
+          const int q = tid + (i0 + j) * BLK, c = q / CO, n = q - c * CO;
+          float v = 0.0f;
+          if (q < CIP * CO) {
+            if (!g.transW) { if (c < g.CIw && n < g.COw) v = Wk[c * g.COw + n]; }
+            else { if (n < g.CIw && c < g.COw) v = Wk[n * g.COw + c]; }
+          }
+          wb[j] = v;
+        }
+  #pragma unroll
+        for (int j = 0; j < GB; ++j) {
+          const int q = tid + (i0 + j) * BLK, c = q / CO, n = q - c * CO;
+          if (q < CIP * CO) sB[c * BS + n] = wb[j];
+        }
+      }
+      __syncthreads();
+      mfma_k();
     }
   }
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg
@@ -687,36 +795,63 @@ __global__ __launch_bounds__(BLK) void k_wgrad_narrow(WgradArgs g) {
   float acc[CO];
 #pragma unroll
   for (int n = 0; n < CO; ++n) acc[n] = 0.f;
+  // every staging loop below issues all of its thread's global loads before the first LDS store (one
+  // round trip per phase; as plain strided loops each load waited for the store before it: ~18 exposed
+  // latencies per 64-row sub-tile)
+  constexpr int PN = (RT * MAXK + BLK - 1) / BLK, PD = (RT * CO + BLK - 1) / BLK;
   for (int rb = rb0; rb < rb1; rb += RT) {
     __syncthreads();
-    for (int q = tid; q < RT * K; q += BLK) {
-      const int r = q / K, k = q - r * K, row = rb + r;
-      sN[q] = row < rb1 ? g.nbr[(long long)row * K + k] : -1;
-    }
-    for (int q = tid; q < RT * CO; q += BLK) {
-      const int r = q / CO, n = q - r * CO, row = rb + r;
-      float v = 0.0f;
-      if (row < rb1) {
-        const float d = g.dy[(long long)row * CO + n], zz = g.z[(long long)row * CO + n];
-        const float xh = (zz - g.dbn[3 * CO + n]) * g.dbn[4 * CO + n];
-        v = g.dbn[n] * (d - g.dbn[CO + n] - xh * g.dbn[2 * CO + n]);
+    {
+      int nv[PN];
+#pragma unroll
+      for (int i = 0; i < PN; ++i) {
+        const int q = tid + i * BLK;
+        const int r = q / K, k = q - r * K, row = rb + r;
+        nv[i] = (q < RT * K && row < rb1) ? g.nbr[(long long)row * K + k] : -1;
       }
-      sD[q] = v;
+#pragma unroll
+      for (int i = 0; i < PN; ++i)
+        if (tid + i * BLK < RT * K) sN[tid + i * BLK] = nv[i];
+      float dv[PD], zv[PD];
+#pragma unroll
+      for (int i = 0; i < PD; ++i) {
+        const int q = tid + i * BLK, r = q / CO, n = q - r * CO, row = rb + r;
+        const bool ok = q < RT * CO && row < rb1;
+        dv[i] = ok ? g.dy[(long long)row * CO + n] : 0.0f;
+        zv[i] = ok ? g.z[(long long)row * CO + n] : 0.0f;
+      }
+#pragma unroll
+      for (int i = 0; i < PD; ++i) {
+        const int q = tid + i * BLK, r = q / CO, n = q - r * CO, row = rb + r;
+        if (q >= RT * CO) continue;
+        float v = 0.0f;
+        if (row < rb1) {
+          const float xh = (zv[i] - g.dbn[3 * CO + n]) * g.dbn[4 * CO + n];
+          v = g.dbn[n] * (dv[i] - g.dbn[CO + n] - xh * g.dbn[2 * CO + n]);
+        }
+        sD[q] = v;
+      }
     }
     __syncthreads();
     if (CI == 4) {   // one 16-B gather per (offset, row)
-      for (int q = tid; q < K * RT; q += BLK) {
+      float4 gv[PN];
+#pragma unroll
+      for (int i = 0; i < PN; ++i) {
+        const int q = tid + i * BLK, k = q / RT, r = q - k * RT;
+        const int src = q < K * RT ? sN[r * K + k] : -1;
+        gv[i] = src >= 0 ? *(const float4*)(g.a + (long long)src * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int i = 0; i < PN; ++i) {
+        const int q = tid + i * BLK;
+        if (q >= K * RT) continue;
         const int k = q / RT, r = q - k * RT;
-        const int src = sN[r * K + k];
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (src >= 0) {
-          v = *(const float4*)(g.a + (long long)src * 4);
-          if (AT == A_BNRELU) {
-            v.x = fmaxf(fmaf(v.x - g.abn[8], g.abn[0], g.abn[4]), 0.0f);
-            v.y = fmaxf(fmaf(v.y - g.abn[9], g.abn[1], g.abn[5]), 0.0f);
-            v.z = fmaxf(fmaf(v.z - g.abn[10], g.abn[2], g.abn[6]), 0.0f);
-            v.w = fmaxf(fmaf(v.w - g.abn[11], g.abn[3], g.abn[7]), 0.0f);
-          }
+        float4 v = gv[i];
+        if (AT == A_BNRELU && sN[r * K + k] >= 0) {
+          v.x = fmaxf(fmaf(v.x - g.abn[8], g.abn[0], g.abn[4]), 0.0f);
+          v.y = fmaxf(fmaf(v.y - g.abn[9], g.abn[1], g.abn[5]), 0.0f);
+          v.z = fmaxf(fmaf(v.z - g.abn[10], g.abn[2], g.abn[6]), 0.0f);
+          v.w = fmaxf(fmaf(v.w - g.abn[11], g.abn[3], g.abn[7]), 0.0f);
         }
         *(float4*)&sA[q * 4] = v;
       }

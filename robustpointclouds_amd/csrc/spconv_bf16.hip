@@ -87,10 +87,19 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
     // the wave's offset mask comes from ballots (no LDS atomics)
     const int rr = lane & 15, k4 = lane >> 4, row = r0 + w * 16 + rr;
     unsigned m = 0;
-    for (int kb = 0; kb < K; kb += 4) {
-      const int k = kb + k4;
-      int v = -1;
-      if (k < K && row < g.Nout) v = g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)];
+    // the wave's 7 index loads are all in flight before the first is used (a load per pass, each
+    // waited out before the next, cost 7 round trips at the start of every block)
+    constexpr int NP = (MAXK + 3) / 4;
+    int nv[NP];
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int k = 4 * i + k4;
+      nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
+    }
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int kb = 4 * i, k = kb + k4, v = nv[i];
+      if (kb >= K) break;
       if (k < K) sN[(w * 16 + rr) * MAXK + k] = v;
       const unsigned long long b = __ballot(v >= 0);
 #pragma unroll

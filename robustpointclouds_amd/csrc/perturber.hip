@@ -196,24 +196,34 @@ __global__ __launch_bounds__(BLK) void k_xstats(Dev d) {
   for (int r = blockIdx.x * BLK + threadIdx.x; r < d.rows; r += stride) {
     if (d.fused) {
       int base = d.off[r], j = 0;
-      for (int s = 0; s < d.slots; ++s) {
-        size_t slot = (size_t)r * d.slots + s;
-        const float* p = d.x + slot * F;
-        float v[F];
-        float sum = 0.0f;
+      // eight slots' loads in flight before their copies are stored (d.out may alias d.x as far as the
+      // compiler knows: interleaved, every slot's loads waited behind the previous slot's stores)
+      for (int s0 = 0; s0 < d.slots; s0 += 8) {
+        float vv[8][F];
 #pragma unroll
-        for (int f = 0; f < F; ++f) {
-          v[f] = p[f];
-          sum = f == 0 ? v[0] : sum + v[f];
-          d.out[slot * F + f] = v[f];
+        for (int u = 0; u < 8; ++u) {
+          const size_t slot = (size_t)r * d.slots + s0 + u;
+#pragma unroll
+          for (int f = 0; f < F; ++f) vv[u][f] = s0 + u < d.slots ? d.x[slot * F + f] : 0.0f;
         }
-        if (sum != 0.0f) {
-          d.list[base + j++] = (int)slot;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          if (s0 + u >= d.slots) break;
+          const size_t slot = (size_t)r * d.slots + s0 + u;
+          float sum = 0.0f;
 #pragma unroll
           for (int f = 0; f < F; ++f) {
-            s1[f] += v[f];
-            s2[f] += (double)v[f] * v[f];
-            nan |= isnan(v[f]);
+            sum = f == 0 ? vv[u][0] : sum + vv[u][f];
+            d.out[slot * F + f] = vv[u][f];
+          }
+          if (sum != 0.0f) {
+            d.list[base + j++] = (int)slot;
+#pragma unroll
+            for (int f = 0; f < F; ++f) {
+              s1[f] += vv[u][f];
+              s2[f] += (double)vv[u][f] * vv[u][f];
+              nan |= isnan(vv[u][f]);
+            }
           }
         }
       }

@@ -1505,12 +1505,15 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad_mf(Dev d, MfJobs J) {
     }
 #pragma unroll
     for (int i = 0; i < TO; ++i) bsum[i] += (av[i][0] + av[i][1]) + (av[i][2] + av[i][3]);
+    // k outermost: consecutive MFMAs update different accumulators (the 4 k-steps of one tile back to
+    // back waited out the 16x16x4 f32 dependent latency, 40 of every 32-cycle issue slot); each tile
+    // still sums k = 0..3 in order
 #pragma unroll
-    for (int i = 0; i < TO; ++i)
+    for (int k = 0; k < 4; ++k)
 #pragma unroll
-      for (int jc = 0; jc < TC; ++jc)
+      for (int i = 0; i < TO; ++i)
 #pragma unroll
-        for (int k = 0; k < 4; ++k)
+        for (int jc = 0; jc < TC; ++jc)
           acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][k], bv[jc][k], acc[i][jc], 0, 0, 0);
   }
   // lane (a, g) of tile (i, jc) holds dW[16i + 4g + r][16jc + a]; waves summed in order 0, 1, 2, 3

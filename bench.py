@@ -239,6 +239,8 @@ def main():
     frames = world * a.batch * a.steps
     if rank == 0:
         metric = ("adversarial-train frames/sec/GPU, CenterPoint nuScenes 10-class (BASELINE config 4)" if nus else
+                  "adversarial-train frames/sec/GPU, StrongAdversarialVoxelNet KITTI (BASELINE config 5, not the "
+                  "metric)" if a.model != "voxelnet" else
                   "adversarial-train frames/sec/GPU, SECOND KITTI-3class, at 1/2/4/8 MI355X" if a.classes == 3 else
                   "adversarial-train frames/sec/GPU, SECOND KITTI Car-only (BASELINE configs[1], not the metric)")
         workload = ("AdversarialCenterPoint nuScenes 10-class (voxel 0.1 m, 10-sweep HDL-32E-like frames, "

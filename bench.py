@@ -281,6 +281,14 @@ def main():
                                    avg_launch_ms=round(ks["avg_ms"], 4),
                                    flops_per_launch=ks["flops_per_launch"], launches=ks["launches"],
                                    work="2*C_in*C_out FLOP per valid rulebook pair")
+        if not nus and a.classes == 3:
+            # whole-step algorithmic rate next to the dominant kernel's: 441 GFLOP per frame
+            # = SECOND/FPN/head fwd + data and weight gradients (418) + sparse encoder (21) + perturber (3.2),
+            # bf16 MFMA peak as the bound
+            fpf = 441e9
+            res["step_roofline"] = dict(flop_per_frame=fpf, achieved=round(frames / dt * fpf / 1e12, 1),
+                                        peak=PEAK["bf16_mfma"], unit="TFLOP/s",
+                                        frac=round(frames / dt * fpf / 1e12 / PEAK["bf16_mfma"], 4))
         if not a.no_cpu_baseline and a.model == "voxelnet":
             res["cpu_baseline"] = cpu_baseline(a.cpu_frames, a.classes)
         print(json.dumps(res), flush=True)

@@ -91,3 +91,34 @@ def test_clip_adamw_matches_torch(max_norm):
         ref.zero_grad()
     sd = ours.state_dict()
     assert float(sd["state"][6]["step"]) == 2.0 and float(sd["state"][0]["step"]) == 3.0
+
+
+def test_clip_adamw_gradient_views_at_odd_offsets():
+    """Gradients that are views into one flat buffer at offsets that are not 16-byte aligned (as DDP's
+    gradient_as_bucket_view buckets can be) take the scalar-load branch of the vector loops; parameters
+    whose sizes are not multiples of 4 shift the moments' views (padded to 256 B). Same result as torch."""
+    shapes = [(18,), (70, 33), (5,), (4096 + 3,), (64, 64), (7, 3)]
+    g = torch.Generator().manual_seed(5)
+    pa = [torch.nn.Parameter(torch.randn(s, generator=g).to(DEV)) for s in shapes]
+    pb = [torch.nn.Parameter(p.detach().clone()) for p in pa]
+    ours = ClipAdamW([dict(params=pa, lr=1e-3, initial_lr=1e-3)], lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                     weight_decay=1e-3, max_norm=0.5)
+    ref = torch.optim.AdamW([dict(params=pb, lr=1e-3, initial_lr=1e-3)], lr=1e-3, betas=(0.9, 0.999), eps=1e-8,
+                            weight_decay=1e-3)
+    for step in range(3):
+        total = sum(p.numel() for p in pa)
+        flat = (torch.randn(total + 1, generator=g) * 0.05).to(DEV)
+        off = 1   # every view starts at an odd float offset
+        for x, y in zip(pa, pb):
+            n = x.numel()
+            x.grad = flat[off:off + n].view_as(x)
+            y.grad = flat[off:off + n].view_as(y).clone()
+            off += n
+        norm = ours.step()
+        rn = torch.nn.utils.clip_grad_norm_(pb, 0.5)
+        ref.step()
+        torch.testing.assert_close(norm[0], rn, rtol=1e-6, atol=0)
+        for x, y in zip(pa, pb):
+            torch.testing.assert_close(x.detach(), y.detach(), rtol=2e-6, atol=1e-8)
+        ours.zero_grad()
+        ref.zero_grad()

@@ -30,6 +30,17 @@ constexpr int BM = 64;          // rows per BatchNorm partial row (rpc_spconv_ge
 // GEMM waves per block (16 rows each; all share one LDS weight tile per offset): 8 — the tile is
 // fetched once per 128 rows — unless the 128 x 128 tiles' LDS ring would leave one block per CU
 __host__ __device__ constexpr int gw_of(int kgp, int nt) { return kgp * nt * 16 >= 128 * 128 ? 4 : 8; }
+// 16-row MFMA tiles per wave: every weight fragment a wave reads from LDS feeds RT MFMAs. Two for the
+// mid-size tiles (K x 16*NT of 32x32 .. 64x32), whose time went to LDS weight reads (every wave re-read
+// the whole tile per offset for its 16 rows): r02v30 <32,2,0> 35.0 -> 30.0 us, <32,2,1> 38.5 -> 36.5,
+// <64,2,1> 49 -> 42. Measured and kept at RT=1: the 64x64 tiles (88 VGPRs, 5 waves/SIMD: <64,4,1>
+// 47 -> 54 us) and the 32x16 tiles (<32,1,0> 21.3 -> 23.4 us)
+__host__ __device__ constexpr int rt_of(int kgp, int nt) {
+  return (kgp * nt >= 64 && kgp * nt <= 128 && nt <= 4) ? 2 : 1;
+}
+__host__ __device__ constexpr int gemm_waves_per_simd(int kgp, int nt) {
+  return rt_of(kgp, nt) == 2 ? 5 : ((kgp * nt <= 256 && nt <= 4) ? 8 : 1);
+}
 constexpr int MAXK = 27;
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
@@ -60,8 +71,8 @@ struct GB {
 // Occupancy: the <= 64 x 64 tiles are held to 64 VGPRs (8 waves per SIMD, 4 blocks per CU) — at 72 the
 // 106k-row 64-channel layers needed 1.08 rounds of 3 blocks per CU (k_gemm_bf16<64,4,1> 60.6 -> 51.5 us)
 template <int KGP, int NT, int EPI>
-__global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 8 : 1)) void k_gemm_bf16(GB g) {
-  constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, GBM = 16 * GW;
+__global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) void k_gemm_bf16(GB g) {
+  constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, RT = rt_of(KGP, NT), WR = 16 * RT, GBM = WR * GW;
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;
   // LDS row stride: 8 mod 16 dwords (conflict-free b128 reads), except the 128 x 128 tiles, whose
@@ -85,26 +96,30 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   {
     // each wave stages its own 16 rows: lane = (offset group k4, row lane&15), 4 offsets per pass;
     // the wave's offset mask comes from ballots (no LDS atomics)
-    const int rr = lane & 15, k4 = lane >> 4, row = r0 + w * 16 + rr;
+    const int rr = lane & 15, k4 = lane >> 4;
     unsigned m = 0;
-    // the wave's 7 index loads are all in flight before the first is used (a load per pass, each
+    // the wave's index loads are all in flight before the first is used (a load per pass, each
     // waited out before the next, cost 7 round trips at the start of every block)
     constexpr int NP = (MAXK + 3) / 4;
-    int nv[NP];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int k = 4 * i + k4;
-      nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
-    }
+    for (int rt = 0; rt < RT; ++rt) {
+      const int lr = w * WR + rt * 16 + rr, row = r0 + lr;
+      int nv[NP];
 #pragma unroll
-    for (int i = 0; i < NP; ++i) {
-      const int kb = 4 * i, k = kb + k4, v = nv[i];
-      if (kb >= K) break;
-      if (k < K) sN[(w * 16 + rr) * MAXK + k] = v;
-      const unsigned long long b = __ballot(v >= 0);
+      for (int i = 0; i < NP; ++i) {
+        const int k = 4 * i + k4;
+        nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
+      }
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        if ((b >> (16 * q)) & 0xffffull) m |= 1u << (kb + q);
+      for (int i = 0; i < NP; ++i) {
+        const int kb = 4 * i, k = kb + k4, v = nv[i];
+        if (kb >= K) break;
+        if (k < K) sN[lr * MAXK + k] = v;
+        const unsigned long long b = __ballot(v >= 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if ((b >> (16 * q)) & 0xffffull) m |= 1u << (kb + q);
+      }
     }
     if (lane == 0) wmask[w] = m;
   }
@@ -120,19 +135,24 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   __syncthreads();
   const int NK = nk;
   const unsigned my = wmask[w];
-  f32x4 acc[NT];
+  f32x4 acc[RT][NT];
 #pragma unroll
-  for (int n = 0; n < NT; ++n) acc[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
-  const int arow = w * 16 + (lane & 15);
+  const int arow = w * WR + (lane & 15);
   const int ag = lane >> 4;
-  auto load_a = [&](int k, uint4 (&dst)[KS]) {
-    int src = sN[arow * MAXK + k];
+  auto load_a = [&](int k, uint4 (&dst)[RT][KS]) {
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) {
-      int c0 = ks * 32 + ag * 8;
-      dst[ks] = (src >= 0 && c0 < g.CP) ? *(const uint4*)(g.a + (long long)src * g.CP + c0)
-                                        : make_uint4(0u, 0u, 0u, 0u);
+    for (int rt = 0; rt < RT; ++rt) {
+      const int src = sN[(arow + rt * 16) * MAXK + k];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        int c0 = ks * 32 + ag * 8;
+        dst[rt][ks] = (src >= 0 && c0 < g.CP) ? *(const uint4*)(g.a + (long long)src * g.CP + c0)
+                                              : make_uint4(0u, 0u, 0u, 0u);
+      }
     }
   };
   auto load_b = [&](int k, uint4 (&dst)[BPT]) {
@@ -155,7 +175,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   };
 
   if (NK > 0) {
-    uint4 acur[KS], anxt[KS], bnx[BPT];
+    uint4 acur[RT][KS], anxt[RT][KS], bnx[BPT];
     {
       load_b(klist[0], bnx);
       store_b(0, bnx);
@@ -173,11 +193,13 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
         const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
-          bf16x8 av = __builtin_bit_cast(bf16x8, acur[ks]);
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
             bf16x8 bv = *(const bf16x8*)(bb + n * 16 * LS + ks * 32);
-            acc[n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv, acc[n], 0, 0, 0);
+#pragma unroll
+            for (int rt = 0; rt < RT; ++rt)
+              acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, acur[rt][ks]), bv,
+                                                                   acc[rt][n], 0, 0, 0);
           }
         }
       }
@@ -185,7 +207,9 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
       __syncthreads();
       if (need_n) {
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) acur[ks] = anxt[ks];
+        for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) acur[rt][ks] = anxt[rt][ks];
       }
     }
   }
@@ -196,34 +220,39 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   // interleaved with the stores, every z load waited for its own round trip — 16 per lane)
   float s1[NT], s2[NT];
 #pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    s1[n] = s2[n] = 0.0f;
-    int col = n * 16 + (lane & 15);
-    float zr[4], pb[4];
-    if (EPI == E_DGRAD) {
-      const int C = g.CO_real, cc = min(col, C - 1);
+  for (int n = 0; n < NT; ++n) s1[n] = s2[n] = 0.0f;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];   // scale, beta, mean, invstd
+  for (int rt = 0; rt < RT; ++rt) {
+    const int rb = r0 + w * WR + rt * 16 + (lane >> 4) * 4;
 #pragma unroll
-      for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)min(r0 + w * 16 + (lane >> 4) * 4 + j, g.Nout - 1) * C + cc];
-    }
+    for (int n = 0; n < NT; ++n) {
+      int col = n * 16 + (lane & 15);
+      float zr[4], pb[4];
+      if (EPI == E_DGRAD) {
+        const int C = g.CO_real, cc = min(col, C - 1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      int row = r0 + w * 16 + (lane >> 4) * 4 + j;
-      float v = acc[n][j];
-      if (row < g.Nout && col < g.CO_real) {
-        if (EPI == E_DGRAD) {
-          const float zz = zr[j];
-          float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
-          v = h > 0.0f ? v : 0.0f;
-          float xh = (zz - pb[2]) * pb[3];
-          s1[n] += v;
-          s2[n] += v * xh;
-        } else {
-          s1[n] += v;
-          s2[n] += v * v;
+        for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];   // scale, beta, mean, invstd
+#pragma unroll
+        for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)min(rb + j, g.Nout - 1) * C + cc];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int row = rb + j;
+        float v = acc[rt][n][j];
+        if (row < g.Nout && col < g.CO_real) {
+          if (EPI == E_DGRAD) {
+            const float zz = zr[j];
+            float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
+            v = h > 0.0f ? v : 0.0f;
+            float xh = (zz - pb[2]) * pb[3];
+            s1[n] += v;
+            s2[n] += v * xh;
+          } else {
+            s1[n] += v;
+            s2[n] += v * v;
+          }
+          g.out[(long long)row * g.CO_real + col] = v;
         }
-        g.out[(long long)row * g.CO_real + col] = v;
       }
     }
   }
@@ -242,14 +271,15 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), (KGP * NT <= 256 && NT <= 4 ? 
   __syncthreads();
   // partial rows keep the CO_real-wide layout expected by rpc_bn_finalize: [blocks][2*CO_real]
   const int C = g.CO_real;
-  // one partial row per 64 rows (waves 4h..4h+3), the layout of rpc_spconv_gemm_blocks
+  // one partial row per 64 rows (the layout of rpc_spconv_gemm_blocks): waves WPR*h .. WPR*h + WPR-1
+  constexpr int WPR = 64 / WR, PRB = GBM / 64;
   const int nrow = (g.Nout + BM - 1) / BM;
-  for (int j = tid; j < (GW / 4) * 2 * C; j += GBLK) {
-    const int h = j / (2 * C), jj = j - h * 2 * C, prow = lb * (GW / 4) + h;
+  for (int j = tid; j < PRB * 2 * C; j += GBLK) {
+    const int h = j / (2 * C), jj = j - h * 2 * C, prow = lb * PRB + h;
     if (prow >= nrow) continue;
     int which = jj / C, c = jj - which * C;
     float s = 0.0f;
-    for (int ww = 0; ww < 4; ++ww) s += sP[4 * h + ww][which * NGP + c];
+    for (int ww = 0; ww < WPR; ++ww) s += sP[WPR * h + ww][which * NGP + c];
     g.part[(long long)prow * 2 * C + jj] = s;
   }
 }
@@ -538,8 +568,8 @@ __global__ __launch_bounds__(BLK) void k_wgrad_bf16(const u16* __restrict__ h, i
 
 template <int KGP, int NT>
 static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
-  constexpr int GW = gw_of(KGP, NT);
-  const int nblk = (n_rows + 16 * GW - 1) / (16 * GW);
+  constexpr int GW = gw_of(KGP, NT), GBM = 16 * rt_of(KGP, NT) * GW;
+  const int nblk = (n_rows + GBM - 1) / GBM;
   if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(64 * GW), 0, st, a);

@@ -84,16 +84,18 @@ __global__ __launch_bounds__(256) void k_wgrad_reduce(const float* __restrict__ 
   const long long e = (long long)blockIdx.x * 64 + o;
   double s = 0.0;
   if (e < total) {
-    int c = q;
-    for (; c + 12 < chunks; c += 16) {
-      float a0 = part[(long long)c * total + e], a1 = part[(long long)(c + 4) * total + e];
-      float a2 = part[(long long)(c + 8) * total + e], a3 = part[(long long)(c + 12) * total + e];
-      s += (double)a0;
-      s += (double)a1;
-      s += (double)a2;
-      s += (double)a3;
+    // 8 chunks in flight per lane, predicated (no remainder loop that waits out one round trip per
+    // chunk); same ascending order per lane, missing chunks add 0.0
+    for (int c = q; c < chunks; c += 32) {
+      float a[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {  // clamped address + select (a conditional load waits for itself)
+        const float v = part[(long long)min(c + 4 * k, chunks - 1) * total + e];
+        a[k] = c + 4 * k < chunks ? v : 0.0f;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) s += (double)a[k];
     }
-    for (; c < chunks; c += 4) s += (double)part[(long long)c * total + e];
   }
   sh[q][o] = s;
   __syncthreads();

@@ -239,7 +239,9 @@ typedef struct {
 } RpcSpconvWprep;
 int rpc_spconv_prep_weight_bf16_batch(const RpcSpconvWprep* descs, int n, void* stream);
 /* out[r] = sum_k a[map[r, k']] . B_k ; epi 0 forward (+BN partial sums), 1 dgrad (prev ReLU mask +
- * BN-backward partial sums), 2 plain */
+ * BN-backward partial sums), 2 plain. The source rows a and the tiles bt are read through 32-bit
+ * buffer offsets: both must stay below 2 GiB (RPC_ERR_UNSUPPORTED when n_out rows of a already
+ * exceed it). */
 int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out, const void* bt,
                          int ng, float* out, const float* prev_z, const float* prev_bn, float* part, int epi,
                          void* stream);

@@ -39,7 +39,7 @@ __host__ __device__ constexpr int rt_of(int kgp, int nt) {
   return (kgp * nt >= 64 && kgp * nt <= 128 && nt <= 4) ? 2 : 1;
 }
 __host__ __device__ constexpr int gemm_waves_per_simd(int kgp, int nt) {
-  return rt_of(kgp, nt) == 2 ? 5 : ((kgp * nt <= 256 && nt <= 4) ? 8 : 1);
+  return rt_of(kgp, nt) == 2 ? 5 : ((kgp * nt <= 256 && nt <= 4 && kgp <= 64) ? 8 : 1);
 }
 constexpr int MAXK = 27;
 
@@ -143,31 +143,42 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
 
   const int arow = w * WR + (lane & 15);
   const int ag = lane >> 4;
+  // Every load of the main loop is issued unconditionally as a buffer load: a missing neighbour, a
+  // padding column or an idle thread gets an offset past the descriptor's range, which the hardware
+  // returns as zeros. With conditional loads the compiler could not count the loads in flight: the
+  // weight-tile LDS store waited on vmcnt(0), i.e. for the next offset's gathers too, every offset.
+  // Offsets are 32-bit: the host checks that the source table and the weight tiles fit below 2 GB.
+  constexpr unsigned OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.bt, (short)0, 0x7fffffff, 0x00020000);
   auto load_a = [&](int k, uint4 (&dst)[RT][KS]) {
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
       const int src = sN[(arow + rt * 16) * MAXK + k];
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        int c0 = ks * 32 + ag * 8;
-        dst[rt][ks] = (src >= 0 && c0 < g.CP) ? *(const uint4*)(g.a + (long long)src * g.CP + c0)
-                                              : make_uint4(0u, 0u, 0u, 0u);
+        const int c0 = ks * 32 + ag * 8;
+        unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
+        asm volatile("" : "+v"(off));   // keeps the select a select (else: one load per branch of a diamond)
+        dst[rt][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
       }
     }
   };
   auto load_b = [&](int k, uint4 (&dst)[BPT]) {
-    const uint4* src = (const uint4*)(g.bt + (long long)k * NGP * KGP);
+    const unsigned base = (unsigned)k * (unsigned)(NGP * KGP * 2);
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
-      int v = tid + j * GBLK;
-      dst[j] = v < BV ? src[v] : make_uint4(0u, 0u, 0u, 0u);
+      const int v = tid + j * GBLK;
+      unsigned off = (BV % GBLK == 0 || v < BV) ? base + (unsigned)v * 16u : OOB;
+      asm volatile("" : "+v"(off));
+      dst[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, off, 0, 0));
     }
   };
   auto store_b = [&](int buf, const uint4 (&src)[BPT]) {
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       int v = tid + j * GBLK;
-      if (v < BV) {
+      if (BV % GBLK == 0 || v < BV) {
         int e = v * 8, n = e / KGP, c = e - n * KGP;
         *(uint4*)&sB[buf][n * LS + c] = src[j];
       }
@@ -175,20 +186,22 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
   };
 
   if (NK > 0) {
-    uint4 acur[RT][KS], anxt[RT][KS], bnx[BPT];
-    {
-      load_b(klist[0], bnx);
-      store_b(0, bnx);
-      if ((my >> klist[0]) & 1u) load_a(klist[0], acur);
-    }
+    uint4 a0[RT][KS], a1[RT][KS], bw0[BPT], bw1[BPT];
+    load_b(klist[0], bw0);
+    store_b(0, bw0);
+    load_b(klist[NK > 1 ? 1 : 0], bw0);
+    load_a(klist[0], a0);
     __syncthreads();
-    for (int t = 0; t < NK; ++t) {
+    // one offset per step. Loads run ahead: the A fragments of offset t+1 and the weight tile of
+    // offset t+2 are issued at the top of step t, so the LDS store of tile t+1 (loaded one step
+    // earlier) and the MFMAs of offset t wait only on loads a whole step old. A fragments and weight
+    // registers ping-pong (a0 / a1, bw0 / bw1: no register copy that would wait on the newest loads);
+    // the steps near the end re-fetch the last offset so the load count per step is fixed.
+    auto step = [&](int t, const uint4 (&ac)[RT][KS], uint4 (&an)[RT][KS], const uint4 (&bc)[BPT],
+                    uint4 (&bn)[BPT]) {
       const int k = klist[t];
-      const bool more = t + 1 < NK;
-      const int kn = more ? klist[t + 1] : 0;
-      const bool need_n = more && ((my >> kn) & 1u);
-      if (more) load_b(kn, bnx);
-      if (need_n) load_a(kn, anxt);
+      load_b(klist[t + 2 < NK ? t + 2 : NK - 1], bn);
+      load_a(klist[t + 1 < NK ? t + 1 : t], an);
       if ((my >> k) & 1u) {
         const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
 #pragma unroll
@@ -198,20 +211,23 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
             bf16x8 bv = *(const bf16x8*)(bb + n * 16 * LS + ks * 32);
 #pragma unroll
             for (int rt = 0; rt < RT; ++rt)
-              acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, acur[rt][ks]), bv,
+              acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ac[rt][ks]), bv,
                                                                    acc[rt][n], 0, 0, 0);
           }
         }
       }
-      if (more) store_b((t + 1) & 1, bnx);
+      store_b((t + 1) & 1, bc);
       __syncthreads();
-      if (need_n) {
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) acur[rt][ks] = anxt[rt][ks];
-      }
+    };
+    // pairs in the loop, an odd last offset after it (a conditional second step inside the loop
+    // gave the compiler a path step(t) -> step(t+2) on which a1's gathers were still in flight, and a
+    // vmcnt(0) at the loop head for it)
+    int t = 0;
+    for (; t + 1 < NK; t += 2) {
+      step(t, a0, a1, bw0, bw1);
+      step(t + 1, a1, a0, bw1, bw0);
     }
+    if (t < NK) step(t, a0, a1, bw0, bw1);
   }
 
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg (16x16 shapes, gfx950)
@@ -677,6 +693,10 @@ extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int k
   g.ez = prev_z;
   g.ebn = prev_bn;
   g.part = part;
+  // 32-bit buffer offsets in k_gemm_bf16 (the source table's own size is not passed: n_out rows of it
+  // is the bound checked here, exact for submanifold layers)
+  if ((long long)n_out * g.CP * 2 >= (1LL << 31) || (long long)kvol * r16(ng) * r32(kg) * 2 >= (1LL << 31))
+    return RPC_ERR_UNSUPPORTED;
   int rc = launch(r32(kg), r16(ng) / 16, epi, g, n_out, (hipStream_t)stream);
   if (rc) return rc;
   RPC_LAUNCH_CHECK();

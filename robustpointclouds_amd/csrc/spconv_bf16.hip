@@ -440,7 +440,7 @@ __device__ __forceinline__ s16x4 tr_read(const u16* p) {
 }
 
 template <int CI, int CO, int KG>
-__global__ __launch_bounds__(BLK) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
+__global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
                                                     int K, int N, int rows_per, const u16* __restrict__ dz, int DP,
                                                     float* __restrict__ part) {
   constexpr int RT = 64;                                   // rows per sub-tile (2 MFMA k-steps)
@@ -480,9 +480,23 @@ __global__ __launch_bounds__(BLK) void k_wgrad_bf16(const u16* __restrict__ h, i
   for (int seg = rb0; seg < rb1; seg += SEG) {
     const int se = min(rb1, seg + SEG);
     __syncthreads();
-    for (int q = tid; q < SEG * KG; q += BLK) {
-      int r = q / KG, g = q - r * KG, row = seg + r, k = k0 + g;
-      sN[q] = (row < se && k < K) ? nbr[(long long)row * K + k] : -1;
+    {
+      // all of a thread's index loads in flight at once, from clamped addresses (a guarded load per
+      // pass compiled to a branch that waited for its load before the next pass: 2-6 round trips)
+      // (32-bit buffer offsets; an index outside the map reads as -1 via the OOB-zero + select)
+      constexpr int NQ = (SEG * KG + BLK - 1) / BLK;
+      const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc((void*)nbr, (short)0, 0x7fffffff, 0x00020000);
+      int v[NQ];
+#pragma unroll
+      for (int i = 0; i < NQ; ++i) {
+        const int q = tid + i * BLK, r = q / KG, g = q - r * KG, row = seg + r, k = k0 + g;
+        unsigned off = (q < SEG * KG && row < se && k < K) ? (unsigned)(row * K + k) * 4u : 0x80000000u;
+        asm volatile("" : "+v"(off));
+        v[i] = off == 0x80000000u ? -1 : __builtin_amdgcn_raw_buffer_load_b32(rn, off, 0, 0);
+      }
+#pragma unroll
+      for (int i = 0; i < NQ; ++i)
+        if (tid + i * BLK < SEG * KG) sN[tid + i * BLK] = v[i];
     }
     __syncthreads();
     auto load = [&](int rs) {   // global -> registers for the sub-tile starting at segment row rs

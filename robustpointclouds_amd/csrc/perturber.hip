@@ -1281,6 +1281,20 @@ __device__ __forceinline__ fvec<Q> ldq(const float* p, int n, int N) {
 }
 template <int Q>
 __device__ __forceinline__ void stq(float* p, int n, fvec<Q> v) { *(fvec<Q>*)(p + n) = v; }
+// W_l [R][CI] row-major -> LDS rows of pitch P: all of a thread's loads in flight before its first LDS
+// store (a load -> store loop waited out one L2 round trip per pass: 16 at the start of every block)
+template <int NTOT, int CI, int P>
+__device__ __forceinline__ void stage_w(float* sW, const float* __restrict__ W) {
+  constexpr int NQ = (NTOT + MFBLK - 1) / MFBLK;
+  float v[NQ];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) v[i] = W[min((int)threadIdx.x + i * MFBLK, NTOT - 1)];
+#pragma unroll
+  for (int i = 0; i < NQ; ++i) {
+    const int j = threadIdx.x + i * MFBLK;
+    if (j < NTOT) sW[(j / CI) * P + j % CI] = v[i];
+  }
+}
 // interleaved tiles per wave group: 4 (64 points, 16-byte accesses) while the group's activation
 // operand fits 64 VGPRs, else 2 (32 points, 8-byte accesses) — 2 waves per SIMD, no spills
 __host__ __device__ constexpr int tiles_per_group(int ks) { return ks * 4 <= 64 ? 4 : 2; }
@@ -1298,7 +1312,7 @@ __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
   __shared__ float sp[3 * CI + CO];
   __shared__ double lds[MFW * 2 * MAXC];
   __shared__ int lastf;
-  for (int j = threadIdx.x; j < CO * CI; j += MFBLK) sW[(j / CI) * P + j % CI] = d.W[l][j];
+  stage_w<CO * CI, CI, P>(sW, d.W[l]);
   for (int j = threadIdx.x; j < 3 * CI; j += MFBLK) sp[j] = d.bn[l - 1][j];
   for (int j = threadIdx.x; j < CO; j += MFBLK) sp[3 * CI + j] = d.b[l][j];
   wave_sums_zero(lds);
@@ -1314,10 +1328,13 @@ __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
   for (int t = wv * GRID + blockIdx.x; t * GP < N; t += GRID * MFW) {
     const int n0 = t * GP, na = n0 + TQ * a;
     fvec<TQ> hv[KS];
+    // all KS activation loads in flight before the first BN / ReLU (load + transform per s waited out
+    // one round trip per s)
+#pragma unroll
+    for (int s = 0; s < KS; ++s) hv[s] = ldq<TQ>(zin + (size_t)(4 * s + g) * d.S, na, N);
 #pragma unroll
     for (int s = 0; s < KS; ++s) {
       const int c = 4 * s + g;
-      hv[s] = ldq<TQ>(zin + (size_t)c * d.S, na, N);
 #pragma unroll
       for (int q = 0; q < TQ; ++q) hv[s][q] = na + q < N ? fmaxf(fmaf(hv[s][q] - mu[c], sc[c], sh[c]), 0.0f) : 0.0f;
     }
@@ -1368,7 +1385,7 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
   __shared__ int lastf;
   const int N = d.meta[0];
   const double invN = 1.0 / N;
-  for (int j = threadIdx.x; j < CO * CI; j += MFBLK) sW[(j / CI) * P + j % CI] = d.W[l][j];
+  stage_w<CO * CI, CI, P>(sW, d.W[l]);
   for (int j = threadIdx.x; j < 4 * CO; j += MFBLK) sp[j] = d.bn[l][j];
   for (int j = threadIdx.x; j < 4 * CI; j += MFBLK) sp[4 * CO + j] = d.bn[l - 1][j];
   for (int j = threadIdx.x; j < CO; j += MFBLK) {

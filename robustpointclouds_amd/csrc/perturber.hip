@@ -1410,18 +1410,29 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
   for (int t = wv * GRID + blockIdx.x; t * GP < N; t += GRID * MFW) {
     const int n0 = t * GP, na = n0 + TQ * a;
     fvec<TQ> dzv[KS];
+    // 8 channel rows per batch: their z / dh loads all in flight before the batch's dz stores (the
+    // stores may alias the next rows' loads, so a load -> store per row waited one round trip per row)
+    constexpr int SB = KS < 8 ? KS : 8;
 #pragma unroll
-    for (int s = 0; s < KS; ++s) {
-      const int o = 4 * s + g;
-      const fvec<TQ> zv = ldq<TQ>(zl + (size_t)o * d.S, na, N);
-      const fvec<TQ> dv = ldq<TQ>(dhin + (size_t)o * d.S, na, N);
+    for (int s0 = 0; s0 < KS; s0 += SB) {
+      fvec<TQ> zv[SB], dv[SB];
 #pragma unroll
-      for (int q = 0; q < TQ; ++q) {
-        const float xh = (zv[q] - bo[2 * CO + o]) * bo[3 * CO + o];
-        dzv[s][q] = na + q < N ? gi[o] * (dv[q] - m1[o] - xh * m2[o]) : 0.0f;
+      for (int u = 0; u < SB; ++u) {
+        const int o = 4 * (s0 + u) + g;
+        zv[u] = ldq<TQ>(zl + (size_t)o * d.S, na, N);
+        dv[u] = ldq<TQ>(dhin + (size_t)o * d.S, na, N);
       }
-      stq<TQ>(dzl + (size_t)o * d.S, na, dzv[s]);
-      if (s % 8 == 7) asm volatile("" ::: "memory");  // bound the loads in flight (register pressure)
+#pragma unroll
+      for (int u = 0; u < SB; ++u) {
+        const int s = s0 + u, o = 4 * s + g;
+#pragma unroll
+        for (int q = 0; q < TQ; ++q) {
+          const float xh = (zv[u][q] - bo[2 * CO + o]) * bo[3 * CO + o];
+          dzv[s][q] = na + q < N ? gi[o] * (dv[u][q] - m1[o] - xh * m2[o]) : 0.0f;
+        }
+        stq<TQ>(dzl + (size_t)o * d.S, na, dzv[s]);
+      }
+      asm volatile("" ::: "memory");  // bound the loads in flight (register pressure)
     }
 #pragma unroll
     for (int j = 0; j < NT; ++j) {

@@ -44,7 +44,50 @@ def _native_width(c: int) -> int:
     for n in _NATIVE:
         if c <= n:
             return n
-    raise ValueError(f"VoxelPerturber: hidden width {c} > {_NATIVE[-1]} is not supported by the HIP kernels")
+    raise ValueError(f"VoxelPerturber: hidden width {c} > {_NATIVE[-1]} is not supported by the HIP kernels "
+                     "(e.g. configs/adversarial/adversarial-second_strong_v2.py's 256; widths <= 128 are)")
+
+
+class _GradHookClamp(torch.autograd.Function):
+    """Identity on a parameter whose backward is the reference's per-parameter grad hook
+    clamp(nan_to_num(g, 0, 0, 0), -0.1, 0.1) (voxel_perturber.py:465-475). Each perturber
+    parameter is used once per forward, so clamping its one incoming gradient here is the hook."""
+
+    @staticmethod
+    def forward(ctx, p):
+        return p.view_as(p)
+
+    @staticmethod
+    def backward(ctx, g):
+        return torch.clamp(torch.nan_to_num(g, nan=0.0, posinf=0.0, neginf=0.0), -0.1, 0.1)
+
+
+def _bounds_torch(F: int, training: bool, e: float, device):
+    """(forward scale, clamp) vectors of voxel_perturber.py:209-256 / :333-359 in the same fp32 op
+    order (KITTI F = 4 train / eval; F > 4: bound e, timestamp channels 0)."""
+    eb = torch.ones(F, device=device) * e
+    if F == 4:
+        if not training:
+            eb *= 2.5 * ((2.0 + 1.5 + 1.2) / 3.0)
+            eb[:3] *= 2.0
+            eb[3] = 1.5
+            cb = torch.ones(F, device=device) * e * 5.0
+            cb[:3] *= 5.0
+            cb[3] = 2.0
+        else:
+            eb *= 0.8
+            eb[:3] *= 1.3
+            eb[3] = 0.2
+            cb = torch.ones(F, device=device) * e * 0.9
+            cb[:3] *= 1.2
+            cb[3] = 0.1
+    elif F > 4:
+        eb[4:] = 0.0
+        cb = torch.ones(F, device=device) * e
+        cb[4:] = 0.0
+    else:
+        raise ValueError(f"VoxelPerturber: {F} input features (the reference defines bounds for F >= 4)")
+    return eb, cb
 
 
 class PackedLosses(dict):
@@ -64,9 +107,11 @@ class VoxelPerturber(nn.Module):
         self.auto_detect_dims = True
         in_features = 5 if (voxel_size[0] >= 0.1 or voxel_size[2] >= 0.15) else 4
         self.in_features = in_features
-        self.hidden_channels = list(hidden_channels)
-        if len(self.hidden_channels) != 3:
-            raise ValueError(f"hidden_channels must have 3 entries (encoder-decoder widths), got {hidden_channels}")
+        if len(hidden_channels) < 3:
+            raise ValueError(f"hidden_channels needs 3 entries (encoder-decoder widths), got {hidden_channels}")
+        # the reference reads hidden_channels[0..2] only (:82-103) and ignores extra entries
+        # (configs/adversarial/adversarial-second_strong_v2.py passes [64, 128, 256, 128])
+        self.hidden_channels = [int(c) for c in list(hidden_channels)[:3]]
         self._kernel_hidden = [_native_width(int(c)) for c in self.hidden_channels]
         self._bound_max = float(self.voxel_error_bound.max())
         self.model = None
@@ -217,8 +262,13 @@ class VoxelPerturber(nn.Module):
 
     # ------------------------------------------------------------------ forward
     def forward(self, voxel_features: torch.Tensor) -> Tuple[torch.Tensor, dict]:
+        """ROCm tensors run the fused HIP kernels (and fail loudly if librpc_hip.so is missing);
+        CPU tensors run the module's own torch layers (BASELINE configs[0], the reference's own
+        device-agnostic torch path) — a dispatch on the input's device, never a fallback."""
         assert voxel_features.dim() == 2, f"Expected 2D input, got {voxel_features.dim()}D"
         self._ensure_width(voxel_features.shape[1])
+        if voxel_features.device.type == "cpu":
+            return self._forward_torch(voxel_features)
         x = voxel_features.float()
         out, lvec, flags = _P.PerturberFn.apply(x, self._cfg(x.shape[1]), *self.kernel_params())
         self._sync_running()
@@ -227,11 +277,90 @@ class VoxelPerturber(nn.Module):
             self._track(lvec, out.detach() - x.detach(), x.detach().norm(dim=1).mean())
         return out, self._loss_dict(lvec)
 
+    # ------------------------------------------------------------------ host (CPU) path
+    def _forward_torch(self, x: torch.Tensor) -> Tuple[torch.Tensor, dict]:
+        """voxel_perturber.py:120-321 + _apply_physical_constraints (:323-386) in torch on the host,
+        op for op: unbiased std-normalisation (:158-168), the encoder-decoder MLP with train-mode
+        BatchNorm (batch statistics, running-stat update, :176), the sigmoid attention gate
+        (:203-205), bound scaling (:209-256), clamp + nan_to_num (:357-365) and the four loss terms
+        (:268-299). The grad hook (:465-475) is an identity node on each parameter. NaN input / NaN
+        perturbations return the unperturbed input and zero losses (the HIP path's device-flag
+        behaviour)."""
+        dev = x.device
+        zeros = lambda: {k: torch.zeros((), device=dev) for k in
+                         ("l2_norm", "intensity_loss", "bias_loss", "imbalance_loss")}
+        if torch.isnan(x).any():                                                    # :150-153
+            return x, zeros()
+        s = torch.std(x, dim=0, keepdim=True) + 1e-6                                # :158
+        if torch.isnan(s).any() or torch.isinf(s).any():                            # :161-163
+            s = torch.ones_like(s)
+        xn = torch.clamp(x.clone() / s, -10.0, 10.0)                                # :157, 165-168
+        h = xn
+        hook = _GradHookClamp.apply
+        mods = list(self.model)
+        for m in mods:
+            if isinstance(m, nn.Linear):
+                h = nn.functional.linear(h, hook(m.weight), hook(m.bias))
+            elif isinstance(m, nn.BatchNorm1d):
+                if self.training:
+                    m.num_batches_tracked.add_(1)
+                h = nn.functional.batch_norm(h, m.running_mean, m.running_var, hook(m.weight), hook(m.bias),
+                                             self.training, m.momentum, m.eps)
+            elif isinstance(m, nn.ReLU):
+                h = torch.relu(h)
+            elif isinstance(m, nn.Tanh):
+                h = torch.tanh(h)
+            else:
+                h = m(h)
+        raw = h
+        if torch.isnan(raw).any():                                                  # :195-200
+            self._reset_problematic_weights()
+            return x, zeros()
+        if self.use_spatial_attention:                                              # :203-205
+            a0, _, a1, _ = list(self.attention)
+            att = nn.functional.linear(torch.relu(nn.functional.linear(xn, hook(a0.weight), hook(a0.bias))),
+                                       hook(a1.weight), hook(a1.bias))
+            raw = raw * torch.sigmoid(att)
+        F = x.shape[1]
+        eb, cb = _bounds_torch(F, self.training, self.sensor_error_bound, dev)
+        pert = raw * eb.view(1, -1)                                                 # :256
+        if torch.isnan(pert).any():                                                 # :259-262
+            return x, zeros()
+        pert = torch.clamp(pert, -cb.view(1, -1), cb.view(1, -1))                   # :357-359
+        if torch.isnan(pert).any():                                                 # :362-365
+            pert = torch.nan_to_num(pert, nan=0.0)
+        ref_norm = torch.norm(x, p=2, dim=1).mean()                                 # :268
+        l2 = torch.norm(pert, p=2, dim=1).mean()                                    # :269
+        if self.training:                                                           # :281-282
+            self._track(l2.detach().reshape(1), pert.detach(), ref_norm.detach())
+        out = x + pert                                                              # :285
+        inten = pert[:, 3].abs().mean()                                             # :290
+        bias = pert.mean(dim=0).abs().mean()                                        # :295
+        imb = pert.std(dim=0).std()                                                 # :298-299
+        return out, dict(l2_norm=l2, intensity_loss=inten, bias_loss=bias, imbalance_loss=imb)
+
+    def _perturb_voxels_torch(self, voxels, num_points, vfe_features):
+        """adversarial_voxelnet.py:85-117 + HardSimpleVFE on the host: valid = slot sum != 0 (:89),
+        perturb the compacted points, gradient-connected masked scatter (:113-117), slot mean."""
+        V, P, F = voxels.shape
+        flat = voxels.reshape(-1, F).float()
+        valid = flat.sum(dim=1) != 0
+        out, ld = self._forward_torch(flat[valid]) if bool(valid.any()) else (flat[valid], None)
+        if ld is None:
+            ld = {k: torch.zeros(()) for k in ("l2_norm", "intensity_loss", "bias_loss", "imbalance_loss")}
+        pert = (flat + torch.zeros_like(flat)).masked_scatter(valid[:, None].expand_as(flat), out).view(V, P, F)
+        vfe = pert[:, :, :vfe_features].sum(dim=1) / num_points.to(pert.dtype).view(-1, 1)
+        flags = torch.zeros(8)
+        flags[4] = valid.sum()
+        return vfe, ld, pert.detach(), flags
+
     def perturb_voxels(self, voxels: torch.Tensor, num_points: torch.Tensor, vfe_features: int = 4):
         """Fused path of AdversarialVoxelNet.extract_feat (adversarial_voxelnet.py:85-137):
         valid-slot mask + perturber + masked scatter + HardSimpleVFE in one kernel sequence.
         Returns (vfe [V, vfe_features], loss_dict, perturbed voxels, flags)."""
         self._ensure_width(voxels.shape[-1])
+        if voxels.device.type == "cpu":
+            return self._perturb_voxels_torch(voxels, num_points, vfe_features)
         vfe, lvec, pert, flags = _P.PerturbVoxelsFn.apply(voxels.float(), num_points,
                                                           self._cfg(voxels.shape[-1], vfe_features),
                                                           *self.kernel_params())

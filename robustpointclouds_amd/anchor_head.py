@@ -29,6 +29,7 @@ import torch.nn.functional as Fn
 from torch import nn
 
 from . import _ffi
+from .base_model import det3d_gt
 
 P1 = 3          # dense-engine map: 1x1 conv
 HEAD_PAD = 128  # GEMM width of the bf16 head image (the engine's output-channel tile)
@@ -453,10 +454,29 @@ class Anchor3DHead(nn.Module):
 
 
 def pack_gt(samples, device):
+    """GT of one batch -> padded (boxes [B, M, 7] fp32, labels [B, M] int64, -1 padding). `samples`:
+    the trainer's dict(gt_boxes, gt_labels); mmdet3d Det3DDataSamples (what Anchor3DHead.loss
+    receives from AdversarialVoxelNet.loss, adversarial_voxelnet.py:168 — duck-typed
+    `gt_instances_3d.bboxes_3d(.tensor)` / `.labels_3d`); or (boxes, labels) pairs."""
     if isinstance(samples, dict):
         return samples["gt_boxes"].to(device), samples["gt_labels"].to(device)
+    d = det3d_gt(samples)
+    if d is not None:
+        samples = [(b[:, :7], l) for b, l in zip(*d)]
     M = max(1, max(int(b.shape[0]) for b, _ in samples))
     B = len(samples)
+    dev_t = torch.device(device).type
+    if dev_t != "cpu" and all(torch.is_tensor(b) and b.device.type == dev_t for b, _ in samples):
+        # already on the device (mmdet3d's data preprocessor moved the samples): pad there, no host copy
+        boxes = torch.zeros((B, M, 7), dtype=torch.float32, device=device)
+        labels = torch.full((B, M), -1, dtype=torch.long, device=device)
+        for i, (b, l) in enumerate(samples):
+            n = int(b.shape[0])
+            if n:
+                boxes[i, :n] = b.float()
+                labels[i, :n] = torch.as_tensor(l, device=device).long()
+        boxes[..., 3:6] = torch.where(labels[..., None] >= 0, boxes[..., 3:6], torch.ones_like(boxes[..., 3:6]))
+        return boxes, labels
     boxes = torch.zeros((B, M, 7), dtype=torch.float32)
     labels = torch.full((B, M), -1, dtype=torch.long)
     for i, (b, l) in enumerate(samples):

@@ -15,6 +15,7 @@ import torch
 from torch import nn
 
 from .center_head import NUS_COMMON_HEADS, NUS_TASKS, NUS_TRAIN_CFG, CenterHead
+from .base_model import DetectorBase
 from .registry import MODELS
 from .voxelnet import Det3DDataPreprocessor
 
@@ -24,7 +25,7 @@ NUS_PC_RANGE = [-51.2, -51.2, -5.0, 51.2, 51.2, 3.0]
 NUS_VOXEL_SIZE = [0.1, 0.1, 0.2]
 
 
-class CenterPoint(nn.Module):
+class CenterPoint(DetectorBase):
     def __init__(self, pts_voxel_encoder=None, pts_middle_encoder=None, pts_backbone=None, pts_neck=None,
                  pts_bbox_head=None, train_cfg=None, test_cfg=None, data_preprocessor=None, init_cfg=None, **kwargs):
         super().__init__()
@@ -56,12 +57,18 @@ class CenterPoint(nn.Module):
         return bs if bs else int(voxel_dict["coors"][-1, 0].item()) + 1    # upstream: coors[-1, 0] + 1
 
     def extract_pts_feat(self, voxel_dict, points=None, img_feats=None, batch_input_metas=None):
+        self._sync_engines(voxel_dict["voxels"].device)
         feats = self.pts_voxel_encoder(voxel_dict["voxels"], voxel_dict["num_points"], voxel_dict["coors"])
         x = self.pts_middle_encoder(feats, voxel_dict["coors"], self._batch_size(voxel_dict))
         x = self.pts_backbone(x)
         if self.with_pts_neck:
             x = self.pts_neck(x)
         return x
+
+    def _forward(self, inputs, data_samples=None, **kwargs):
+        vd = dict(inputs["voxels"])
+        vd.setdefault("batch_size", inputs.get("batch_size"))
+        return self.pts_bbox_head(self.extract_pts_feat(vd))
 
     def loss(self, batch_inputs_dict, batch_data_samples, **kwargs):
         vd = dict(batch_inputs_dict["voxels"])

@@ -775,6 +775,8 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
     RPC_CHECK(hipMemsetAsync(dW, 0, sizeof(float) * (size_t)kvol * ci * co, st));
     return RPC_OK;
   }
+  // 32-bit buffer offsets: the index staging reads nbr[(row * kvol + k)] as bytes (row * K + k) * 4
+  if ((long long)n_out * kvol * 4 >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
   int chunks = wgrad_chunks(n_out, kvol, ci, co);
   if (ws_bytes < (size_t)chunks * kvol * ci * co * sizeof(float)) return RPC_ERR_WORKSPACE;
   int rows_per = ((n_out + chunks - 1) / chunks + 31) / 32 * 32;

@@ -21,6 +21,7 @@ and state-dict keys are the torch modules' own (second.py).
 from __future__ import annotations
 
 import os
+import weakref
 
 import torch
 
@@ -97,7 +98,9 @@ class _GraphEntry:
         self.bwd = {}
 
 
-_STABLE = {}   # data_ptr -> tensor: storage that stays put across steps (graph outputs, persistent buffers)
+# data_ptr -> tensor: storage that stays put across steps (graph outputs, persistent buffers). Weak:
+# an entry lives only as long as its owner keeps the tensor (a graph entry, a module's buffer cache)
+_STABLE = weakref.WeakValueDictionary()
 
 
 def mark_stable(t: torch.Tensor) -> None:
@@ -106,22 +109,46 @@ def mark_stable(t: torch.Tensor) -> None:
     _STABLE[t.data_ptr()] = t
 
 
-_SCRATCH = {}  # data_ptr -> tensor: persistent gradient images owned by this module (the FPN's data
-              # gradients): rewritten every step before they are read, so a consumer may add into them
+# data_ptr -> tensor: persistent gradient images owned by a module's graph cache (the FPN's data
+# gradients): rewritten every step before they are read, so a consumer may add into them
+_SCRATCH = weakref.WeakValueDictionary()
 
 
-def _scratch_image(key, B, C, H, W, dev, dt):
-    """A persistent NHWC image for `key` (stable: the backbone's backward graph reads it in place)."""
-    t = _SCRATCH_BY_KEY.get(key)
+class _GraphCache(dict):
+    """A module's HIP graph entries and persistent images, kept in the module's own __dict__ so they
+    are freed with it (a module-level cache keyed by id(module) could hand a new module that reuses
+    the id a stale graph). Not copied by deepcopy / pickling: a copy captures its own graphs."""
+
+    def __deepcopy__(self, memo):
+        return _GraphCache()
+
+    def __reduce__(self):
+        return (_GraphCache, ())
+
+
+def graph_cache(mod) -> "_GraphCache":
+    c = mod.__dict__.get("_hip_graphs")
+    if c is None:
+        c = mod.__dict__["_hip_graphs"] = _GraphCache()
+    return c
+
+
+def _state_key(mod):
+    """Addresses the captured kernels read and write (weights, BN affine, running statistics): a
+    replaced or moved parameter / buffer forces a new capture instead of a replay of stale pointers."""
+    return tuple(t.data_ptr() for t in mod.parameters()) + tuple(t.data_ptr() for t in mod.buffers())
+
+
+def _scratch_image(cache, key, B, C, H, W, dev, dt):
+    """A persistent NHWC image for `key` in a module's graph cache (stable: the backbone's backward
+    graph reads it in place)."""
+    t = cache.get(key)
     if t is None:
         t = _image(B, C, H, W, dev, dt)
-        _SCRATCH_BY_KEY[key] = t
+        cache[key] = t
         _SCRATCH[t.data_ptr()] = t
         mark_stable(t)
     return t
-
-
-_SCRATCH_BY_KEY = {}
 
 
 def _static_in(t):
@@ -459,9 +486,6 @@ def _shape_key(ts):
     return tuple(None if t is None else (tuple(t.shape), tuple(t.stride()), t.dtype, t.device) for t in ts)
 
 
-_FWD_GRAPHS = {}
-
-
 class BackboneFn(torch.autograd.Function):
     """SECOND forward/backward as one node: x [B, Cin, H, W] -> tuple of block outputs (training
     steps replay HIP graphs after the first, see _graph_run)."""
@@ -475,8 +499,8 @@ class BackboneFn(torch.autograd.Function):
         ctx.param_list = params
         ctx.entry = None
         if GRAPHS and mod.training:
-            key = ("second", id(mod), eng.f32) + _shape_key([x])
-            outs, recs, ctx.entry = _graph_run(_FWD_GRAPHS, key, [x], lambda xx: _backbone_fwd(eng, mod, xx))
+            key = ("second", eng.f32) + _shape_key([x]) + _state_key(mod)
+            outs, recs, ctx.entry = _graph_run(graph_cache(mod), key, [x], lambda xx: _backbone_fwd(eng, mod, xx))
             outs = tuple(_alias(o) for o in outs) if ctx.entry is not None else outs
         else:
             outs, recs = _backbone_fwd(eng, mod, x)
@@ -534,14 +558,14 @@ class NeckFn(torch.autograd.Function):
         eng = _engine(_ffi.load(), h0)
         eng.check_widths(fpn_layers(mod))
         if GRAPHS and mod.training:
-            key = ("fpn", id(mod), eng.f32) + _shape_key([h0, h1])
-            out, st_, ent = _graph_run(_FWD_GRAPHS, key, [h0, h1], lambda a, b: _neck_fwd(eng, mod, a, b))
+            key = ("fpn", eng.f32) + _shape_key([h0, h1]) + _state_key(mod)
+            out, st_, ent = _graph_run(graph_cache(mod), key, [h0, h1], lambda a, b: _neck_fwd(eng, mod, a, b))
             out = _alias(out) if ent is not None else out
         else:
             out, st_ = _neck_fwd(eng, mod, h0, h1)
         ctx.recs, ctx.Ctot = st_
         ctx.eng = eng
-        ctx.mod_id = id(mod)
+        ctx.cache = graph_cache(mod)
         ctx.param_list = params
         return out
 
@@ -558,7 +582,7 @@ class NeckFn(torch.autograd.Function):
             dx_out = None
             if GRAPHS:   # persistent: the backbone's backward graph then reads (and adds into) it in place
                 B, H, W = rec["S"]
-                dx_out = _scratch_image(("fpn_dx", ctx.mod_id, i, B, L.ci, H, W, eng.dt, dev), B, L.ci, H, W,
+                dx_out = _scratch_image(ctx.cache, ("fpn_dx", i, B, L.ci, H, W, eng.dt, dev), B, L.ci, H, W,
                                         dev, eng.dt)
             dx, dW, dgam, dbet = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True, dx_out)
             grads[id(L.conv.weight)] = dW
@@ -567,6 +591,7 @@ class NeckFn(torch.autograd.Function):
             dins.append(dx)
         ctx.recs = None
         ctx.eng = None
+        ctx.cache = None
         return (dins[0], dins[1], None) + tuple(grads.get(id(p)) for p in ctx.param_list)
 
 

@@ -94,6 +94,7 @@ class HardVFEFn(torch.autograd.Function):
             _ffi.bump_batches([L.norm for L in module.vfe_layers])
         ctx.save_for_backward(feats, npts, co, *params)
         ctx.cfg, ctx.ws, ctx.wsb, ctx.nw = cfg, ws, wsb, len(weights)
+        ctx.in_dtype = features.dtype
         return out
 
     @staticmethod
@@ -109,12 +110,14 @@ class HardVFEFn(torch.autograd.Function):
         for l in range(cfg.nlayers):
             W, g, b = params[5 * l], params[5 * l + 1], params[5 * l + 2]
             grads += [torch.empty_like(W), torch.empty_like(g), torch.empty_like(b)]
+        dout = dout.contiguous().float()
         _ffi.check(lib.rpc_hard_vfe_backward(C.byref(cfg), _ptrs(params), _ffi.ptr(feats), _ffi.ptr(npts),
-                                             _ffi.ptr(co), V, _ffi.ptr(dout.contiguous().float()),
+                                             _ffi.ptr(co), V, _ffi.ptr(dout),
                                              _ffi.ptr(dfeat), _ptrs(grads), _ffi.ptr(ctx.ws), ctx.wsb,
                                              _ffi.stream_of(feats)),
                    "rpc_hard_vfe_backward")
-        return (dfeat, None, None, None, None, *grads)
+        # the kernels compute in fp32; autograd needs the gradient in the input's dtype (bf16 / fp16 voxels)
+        return (dfeat.to(ctx.in_dtype), None, None, None, None, *grads)
 
 
 @MODELS.register_module()

@@ -145,3 +145,55 @@ class ClipAdamW:
         for g, d in zip(self.param_groups, sd["param_groups"]):
             g["lr"] = d["lr"]
             g["initial_lr"] = d.get("initial_lr", d["lr"])
+
+
+class OptimWrapper:
+    """The mmengine `OptimWrapper` / `AmpOptimWrapper` surface a model's `train_step` calls
+    (`optim_context`, `update_params`, plus `backward` / `step` / `zero_grad` / `param_groups`),
+    over `ClipAdamW` on a ROCm device (clip_grad fused into the step) or torch AdamW +
+    clip_grad_norm_ on the host. `amp_dtype` (AmpOptimWrapper) turns autocast on in
+    `optim_context`, which selects the bf16 perf engines (base_model.select_engines)."""
+
+    def __init__(self, optimizer, clip_grad=None, amp_dtype=None):
+        self.optimizer = optimizer
+        self.clip_grad = dict(clip_grad) if clip_grad else None
+        if self.clip_grad and float(self.clip_grad.get("norm_type", 2)) != 2.0:
+            raise ValueError("clip_grad: only the L2 norm (norm_type 2) of the reference configs is supported")
+        self.amp_dtype = amp_dtype
+        self.grad_norm = None
+
+    @property
+    def param_groups(self):
+        return self.optimizer.param_groups
+
+    def optim_context(self, model):
+        import contextlib
+        if self.amp_dtype is None:
+            return contextlib.nullcontext()
+        return torch.autocast("cuda", dtype=self.amp_dtype)
+
+    def backward(self, loss):
+        loss.backward()
+
+    def step(self):
+        if isinstance(self.optimizer, ClipAdamW):
+            self.grad_norm = self.optimizer.step()[0]
+            return
+        if self.clip_grad:
+            params = [p for g in self.optimizer.param_groups for p in g["params"] if p.grad is not None]
+            self.grad_norm = torch.nn.utils.clip_grad_norm_(params, float(self.clip_grad["max_norm"]))
+        self.optimizer.step()
+
+    def zero_grad(self):
+        self.optimizer.zero_grad(set_to_none=True)
+
+    def update_params(self, loss):
+        self.backward(loss)
+        self.step()
+        self.zero_grad()
+
+    def state_dict(self):
+        return self.optimizer.state_dict()
+
+    def load_state_dict(self, sd):
+        self.optimizer.load_state_dict(sd)

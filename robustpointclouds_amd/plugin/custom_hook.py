@@ -17,6 +17,8 @@ except ImportError:   # standalone
 
 
 def _reg(cls):
+    from robustpointclouds_amd.registry import HOOKS as _LOCAL_HOOKS
+    _LOCAL_HOOKS.register_module(module=cls)   # custom_hooks=[dict(type=...)] without mmengine
     if HOOKS is not None:
         HOOKS.register_module(module=cls, force=True)
     return cls

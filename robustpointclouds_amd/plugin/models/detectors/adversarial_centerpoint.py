@@ -60,6 +60,7 @@ class AdversarialCenterPoint(CenterPoint):
         if self.adversary is None:
             return super().extract_pts_feat(voxel_dict, points, img_feats, batch_input_metas)
         voxels, npts, coors = voxel_dict["voxels"], voxel_dict["num_points"], voxel_dict["coors"]
+        self._sync_engines(voxels.device)
         l2 = None
         if self.training and self._epoch >= 3:
             if isinstance(self.pts_voxel_encoder, HardSimpleVFE):

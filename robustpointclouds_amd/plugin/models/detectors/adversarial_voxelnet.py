@@ -67,6 +67,7 @@ class AdversarialVoxelNet(VoxelNet):
         vd = batch_inputs_dict["voxels"]
         l2, loss_dict = None, None
         voxels, npts, coors = vd["voxels"], vd["num_points"], vd["coors"]
+        self._sync_engines(voxels.device)
         if self._gate() and isinstance(self.voxel_encoder, HardSimpleVFE):
             feats, loss_dict, pert, flags = self.adversary.perturb_voxels(voxels, npts,
                                                                           self.voxel_encoder.num_features)

@@ -171,6 +171,7 @@ class StrongAdversarialVoxelNet(VoxelNet):
     def extract_feat(self, batch_inputs_dict, batch_data_samples=None):
         self._iteration += 1
         vd = batch_inputs_dict["voxels"]
+        self._sync_engines(vd["voxels"].device)
         feats = self.voxel_encoder(vd["voxels"], vd["num_points"], vd["coors"])
         if self.training and self.adversary is not None:
             feats, l2 = self.apply_enhanced_perturbations(feats, True)

@@ -44,8 +44,11 @@ class Registry:
             raise KeyError(f"{t} is not registered in {self.name}")
         for k, v in default_args.items():
             cfg.setdefault(k, v)
+        if self.name == "hooks":
+            cfg.pop("priority", None)   # consumed by mmengine's Runner.register_hook, not the hook
         return cls(**cfg)
 
 
 MODELS = Registry("models")
 ADVERSARIES = Registry("adversaries")
+HOOKS = Registry("hooks")

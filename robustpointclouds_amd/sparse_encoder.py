@@ -437,13 +437,15 @@ class SparseEncoderFn(torch.autograd.Function):
         dt = torch.bfloat16 if enc.dense_bf16 else torch.float32
         # the dense BEV lives in one persistent buffer per module (re-zeroed each step): the SECOND
         # forward graph (dense_bev._graph_run) then reads it in place instead of from a copy
+        # one buffer per shape: a returning shape (full batches after a partial last one) reuses the
+        # storage its graph captured, and a dropped encoder frees them all
         bkey = (B, H, Wd, C * D, dt, enc.dense_nhwc, dev)
-        buf = getattr(enc, "_dense_buf", None)
-        if buf is None or buf[0] != bkey:
-            base = torch.empty((B, H, Wd, C * D) if enc.dense_nhwc else (B, C * D, H, Wd), dtype=dt, device=dev)
-            buf = enc._dense_buf = (bkey, base)
+        bufs = enc.__dict__.setdefault("_dense_bufs", {})
+        base = bufs.get(bkey)
+        if base is None:
+            base = bufs[bkey] = torch.empty((B, H, Wd, C * D) if enc.dense_nhwc else (B, C * D, H, Wd), dtype=dt,
+                                            device=dev)
             dense_bev.mark_stable(base)
-        base = buf[1]
         base.zero_()
         if enc.dense_nhwc:   # channels_last image, logically [B, C*D, H, W]
             dense = base.permute(0, 3, 1, 2)

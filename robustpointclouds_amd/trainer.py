@@ -11,6 +11,7 @@ statistics stay per rank (no SyncBN, like the reference).
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 
@@ -19,8 +20,8 @@ import torch.distributed as dist
 
 import robustpointclouds_amd.plugin.models  # noqa: F401  (registers AdversarialVoxelNet, VoxelPerturber)
 
-from .adversarial_loss import parse_losses
-from .optim import ClipAdamW
+from .base_model import ddp_train_step, select_engines
+from .optim import ClipAdamW, OptimWrapper
 from .registry import MODELS
 from .voxelnet import second_kitti_cfg, second_kitti_strong_cfg
 
@@ -43,6 +44,36 @@ def param_groups(model, lr, custom_keys=None):
                 break
         groups.setdefault(mult, []).append(p)
     return [dict(params=ps, lr=lr * m, initial_lr=lr * m) for m, ps in sorted(groups.items())]
+
+
+def build_optim_wrapper(model, cfg: dict):
+    """mmengine `build_optim_wrapper` for the reference configs' `optim_wrapper` dict
+    (…3class.py:130-139): type OptimWrapper | AmpOptimWrapper (dtype 'bfloat16' / 'float16'),
+    optimizer AdamW(lr, betas, eps, weight_decay), clip_grad(max_norm, norm_type 2), paramwise_cfg
+    custom_keys lr_mult. On a ROCm device the optimizer is ClipAdamW (clip + AdamW, two launches)."""
+    cfg = dict(cfg)
+    kind = cfg.get("type", "OptimWrapper")
+    oc = dict(cfg["optimizer"])
+    if oc.pop("type", "AdamW") != "AdamW":
+        raise ValueError("only AdamW (the reference configs' optimizer) is supported")
+    lr = float(oc["lr"])
+    betas = tuple(oc.get("betas", (0.9, 0.999)))
+    eps, wd = float(oc.get("eps", 1e-8)), float(oc.get("weight_decay", 1e-2))
+    keys = (cfg.get("paramwise_cfg") or {}).get("custom_keys", {})
+    groups = param_groups(model, lr, keys)
+    clip = cfg.get("clip_grad")
+    dev = next(model.parameters()).device
+    if dev.type == "cuda":
+        opt = ClipAdamW(groups, lr=lr, betas=betas, eps=eps, weight_decay=wd,
+                        max_norm=float(clip["max_norm"]) if clip else 0.0)
+    else:
+        opt = torch.optim.AdamW(groups, lr=lr, betas=betas, eps=eps, weight_decay=wd)
+    amp = None
+    if kind == "AmpOptimWrapper":
+        amp = {"bfloat16": torch.bfloat16, "float16": torch.bfloat16, None: torch.bfloat16}[cfg.get("dtype")]
+    elif kind != "OptimWrapper":
+        raise ValueError(f"optim_wrapper type {kind}")
+    return OptimWrapper(opt, clip_grad=clip, amp_dtype=amp)
 
 
 class LRSchedule:
@@ -136,24 +167,7 @@ class Trainer:
 
     @staticmethod
     def _select_engines(model, bf16):
-        """Route the dense part through the HIP engines: bf16 perf mode (sparse convs on bf16 MFMA,
-        dense BEV handed over as a bf16 NHWC image to SECOND / SECONDFPN on the bf16 dense engine and
-        the bf16 head GEMM) or fp32 parity mode (fp32 sparse convs, an fp32 NHWC image through the
-        fp32-MFMA dense engine and head GEMM). The images are channels_last; the parameters keep
-        torch's contiguous layout (gradients are stolen by AccumulateGrad without layout copies)."""
-        me = getattr(model, "middle_encoder", None) or getattr(model, "pts_middle_encoder", None)
-        if me is not None and hasattr(me, "bf16"):
-            me.bf16 = bool(bf16)
-            me.dense_nhwc = True
-            me.dense_bf16 = bool(bf16)
-        for name in ("backbone", "neck", "pts_backbone", "pts_neck"):
-            mod = getattr(model, name, None)
-            if mod is None:
-                continue
-            if hasattr(mod, "hip"):
-                mod.hip = True
-            elif bf16:
-                mod.to(memory_format=torch.channels_last)
+        select_engines(model, bf16)
 
     # mmengine-runner-like attributes used by custom_hook.py
     @property
@@ -188,8 +202,8 @@ class Trainer:
         if pend is not None and pend[0] is points:
             v, c, n, vn = pend[1].result(torch.cuda.current_stream(self.device))
             batch = dict(points=points, voxels=dict(voxels=v, coors=c, num_points=n, voxel_num=vn))
-        else:
-            batch = m.data_preprocessor(dict(inputs=dict(points=points)), training=True)["inputs"]
+        else:   # voxelised by the model's data_preprocessor inside train_step, as mmengine does
+            batch = dict(points=points)
         batch["batch_size"] = len(points)
         if next_points is not None:
             self._prefetch(next_points)
@@ -211,24 +225,19 @@ class Trainer:
             self._pending = (points, vl.voxelize_frames_deferred(points))
 
     def step_batch(self, batch, gt):
-        """The step after voxelisation: loss -> parse_losses -> backward (DDP all-reduce) -> clip
-        -> AdamW -> hooks. batch: dict(voxels=dict(voxels, num_points, coors), batch_size)."""
+        """The step after voxelisation, as mmengine runs it: model.train_step(data, optim_wrapper)
+        (MMDistributedDataParallel.train_step under DDP) with this trainer as the optim wrapper —
+        loss -> parse_losses -> backward (DDP all-reduce) -> clip -> AdamW — then the hooks and the
+        LR schedule. batch: dict(voxels=dict(voxels, num_points, coors), batch_size); gt: the
+        padded dict(gt_boxes, gt_labels) or mmdet3d Det3DDataSamples."""
         m = self.module
         if not m.training:   # Module.train() walks every submodule (~1 ms of host time)
             m.train()
-        with torch.autocast("cuda", dtype=torch.bfloat16, enabled=self.bf16):
-            if isinstance(self.model, torch.nn.parallel.DistributedDataParallel):
-                losses = self.model(batch, gt, mode="loss")     # DDP hooks fire on the grads
-            else:
-                losses = m.loss(batch, gt)
-        total, log_vars = parse_losses(losses)
-        total.backward()
-        if isinstance(self.opt, ClipAdamW):
-            self._grad_norm = self.opt.step()[0]
+        data = dict(inputs=batch, data_samples=gt)
+        if isinstance(self.model, torch.nn.parallel.DistributedDataParallel):
+            log_vars = ddp_train_step(self.model, data, self)    # DDP hooks fire on the grads
         else:
-            self._grad_norm = torch.nn.utils.clip_grad_norm_(self.module.parameters(), self.max_norm)
-            self.opt.step()
-        self.opt.zero_grad(set_to_none=True)
+            log_vars = m.train_step(data, self)
         self.iter += 1
         self.last_log = log_vars
         # hooks first, then the schedulers (mmengine: NaNDetectionHook NORMAL priority runs before
@@ -239,9 +248,20 @@ class Trainer:
         self.sched.step()
         return log_vars
 
+    # ------------------------------------------------------------------ mmengine OptimWrapper surface
+    def optim_context(self, model):
+        """AmpOptimWrapper.optim_context: autocast (bf16) in the perf mode, nothing in fp32."""
+        return torch.autocast("cuda", dtype=torch.bfloat16) if self.bf16 else contextlib.nullcontext()
 
-def _ddp_forward(self, batch, gt, mode="loss"):
-    return self.loss(batch, gt)
+    def update_params(self, loss):
+        """OptimWrapper.update_params: backward, clip_grad (max_norm 0.5) + AdamW, zero_grad."""
+        loss.backward()
+        if isinstance(self.opt, ClipAdamW):
+            self._grad_norm = self.opt.step()[0]
+        else:
+            self._grad_norm = torch.nn.utils.clip_grad_norm_(self.module.parameters(), self.max_norm)
+            self.opt.step()
+        self.opt.zero_grad(set_to_none=True)
 
 
 def make_kitti_model(num_classes=1, device=None, adversarial=True, hidden_channels=None, epoch=3, variant="voxelnet"):
@@ -252,8 +272,6 @@ def make_kitti_model(num_classes=1, device=None, adversarial=True, hidden_channe
     else:
         cfg = second_kitti_cfg(num_classes, hidden_channels=hidden_channels, adversarial=adversarial)
     model = build_model(cfg)
-    # DDP calls forward(); route it to loss() like mmengine's BaseModel.forward(mode='loss')
-    model.forward = _ddp_forward.__get__(model)
     model._epoch = epoch
     if device is not None:
         model.to(device)
@@ -265,7 +283,6 @@ def make_nus_model(device=None, adversarial=True, epoch=3):
     adversarial-centerpoint_voxel-nuscenes.py, BASELINE config 4)."""
     from .centerpoint import centerpoint_nus_cfg
     model = build_model(centerpoint_nus_cfg(adversarial=adversarial))
-    model.forward = _ddp_forward.__get__(model)
     model._epoch = epoch
     if device is not None:
         model.to(device)

@@ -12,6 +12,7 @@ from torch import nn
 
 from . import hard_vfe  # noqa: F401  (registers HardVFE)
 from .anchor_head import Anchor3DHead
+from .base_model import DetectorBase
 from .perturb import VoxelMeanFn
 from .registry import MODELS
 from .second import SECOND, SECONDFPN
@@ -31,7 +32,12 @@ class HardSimpleVFE(nn.Module):
 
 
 class Det3DDataPreprocessor(nn.Module):
-    """Voxelisation part of upstream Det3DDataPreprocessor (voxel=True, voxel_type='hard')."""
+    """Voxelisation part of upstream Det3DDataPreprocessor (voxel=True, voxel_type='hard'):
+    `forward(data, training)` moves the batch's points to the model's device (mmengine
+    BaseDataPreprocessor.cast_data) and hard-voxelises all frames in one launch sequence ->
+    dict(inputs=dict(points, voxels=dict(voxels, coors, num_points, voxel_num), batch_size),
+    data_samples). Inputs that already carry `voxels` (a runner that voxelised ahead, e.g.
+    Trainer's side-stream prefetch) pass through."""
 
     def __init__(self, voxel=True, voxel_type="hard", voxel_layer=None, **kw):
         super().__init__()
@@ -39,11 +45,17 @@ class Det3DDataPreprocessor(nn.Module):
                                       voxel_size=[0.05, 0.05, 0.1], max_voxels=(16000, 40000)))
         self.voxel_layer = Voxelization(vl["voxel_size"], vl["point_cloud_range"], vl["max_num_points"],
                                         vl.get("max_voxels", (16000, 40000)))
+        # follows .to() / .cuda() like mmengine's BaseDataPreprocessor._device
+        self.register_buffer("_device_probe", torch.zeros(0), persistent=False)
 
     def forward(self, data, training=False):
-        pts = data["inputs"]["points"]
-        self.voxel_layer.train(training)
-        inputs = dict(points=pts, voxels=self.voxel_layer.voxelize_frames(pts))
+        inputs = dict(data["inputs"])
+        if "voxels" not in inputs:
+            dev = self._device_probe.device
+            pts = [p if p.device == dev else p.to(dev, non_blocking=True) for p in inputs["points"]]
+            self.voxel_layer.train(training)
+            inputs.update(points=pts, voxels=self.voxel_layer.voxelize_frames(pts))
+        inputs.setdefault("batch_size", len(inputs["points"]) if "points" in inputs else None)
         return dict(inputs=inputs, data_samples=data.get("data_samples"))
 
 
@@ -51,7 +63,7 @@ for _c in (HardSimpleVFE, SparseEncoder, SECOND, SECONDFPN, Anchor3DHead, Det3DD
     MODELS.register_module(module=_c)
 
 
-class VoxelNet(nn.Module):
+class VoxelNet(DetectorBase):
     def __init__(self, voxel_encoder, middle_encoder, backbone, neck=None, bbox_head=None, train_cfg=None,
                  test_cfg=None, data_preprocessor=None, init_cfg=None):
         super().__init__()
@@ -75,6 +87,7 @@ class VoxelNet(nn.Module):
 
     def extract_feat(self, batch_inputs_dict):
         vd = batch_inputs_dict["voxels"]
+        self._sync_engines(vd["voxels"].device)
         feats = self.voxel_encoder(vd["voxels"], vd["num_points"], vd["coors"])
         B = batch_inputs_dict.get("batch_size") or int(vd["coors"][-1, 0].item()) + 1
         x = self.middle_encoder(feats, vd["coors"], B)

@@ -18,7 +18,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 from torch import nn
 
-from robustpointclouds_amd.trainer import Trainer, _ddp_forward
+from robustpointclouds_amd.trainer import Trainer
 from tests.test_adversarial_voxelnet import OracleAdversary, StandInVFE, _load, _model
 
 WORLD = 2
@@ -37,7 +37,6 @@ def _build(d):
     torch.manual_seed(0)
     m = _model(d, StandInVFE(), torch.device("cpu"))
     m.adversary = ParamOracleAdversary(d, [int(h) for h in d["hidden"]])
-    m.forward = _ddp_forward.__get__(m)
     return m
 
 

@@ -4,6 +4,7 @@ train_step's (the GPU side-stream path is covered by tests/test_gpu_prefetch.py)
 import torch
 from torch import nn
 
+from robustpointclouds_amd.base_model import DetectorBase
 from robustpointclouds_amd.trainer import Trainer
 
 
@@ -14,11 +15,13 @@ class _Pre(nn.Module):
 
     def forward(self, data, training=False):
         self.calls += 1
-        pts = data["inputs"]["points"]
-        return dict(inputs=dict(points=pts, voxels=dict(feat=torch.cat(pts, 0))))
+        inputs = dict(data["inputs"])
+        if "voxels" not in inputs:
+            inputs["voxels"] = dict(feat=torch.cat(inputs["points"], 0))
+        return dict(inputs=inputs, data_samples=data.get("data_samples"))
 
 
-class _Toy(nn.Module):
+class _Toy(DetectorBase):
     def __init__(self):
         super().__init__()
         self.data_preprocessor = _Pre()

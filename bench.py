@@ -41,7 +41,8 @@ def _args():
                          "centerpoint = AdversarialCenterPoint nuScenes, batch 4 (BASELINE config 4)")
     ap.add_argument("--fp32", action="store_true", help="dense part in fp32 (parity mode)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-frames", type=int, default=6)
+    ap.add_argument("--cpu-frames", type=int, default=2,
+                    help="frames per CPU-baseline step (bounded sample: 3 warm-up + 5 timed steps)")
     ap.add_argument("--roofline-kernel", default="dense",
                     help="'dense' (the dominant kernel: 3x3 stride-1 bf16 conv, rpc::dn::k_conv3x3<0>) or "
                          "op,ci,co of the sparse conv launches timed with HIP events")
@@ -82,21 +83,34 @@ PEAK = {"fp32_mfma": 157.3, "bf16_mfma": 2500.0}   # TFLOP/s dense, MI355X_MICRO
 
 
 def _traffic(kernel_tag):
-    """HBM bytes per launch of the timed kernel from the committed PMC summary
-    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, KB -> bytes), else None."""
+    """HBM bytes per launch of one kernel from the newest committed PMC summary that has it
+    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, KB -> bytes) and that summary's file name,
+    else (None, None). `kernel_tag` is matched against the kernel's name without its argument list."""
     import glob
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic*.json")))
-    if not files:
-        return None
-    d = json.load(open(files[-1]))
-    for name, v in d.get("kernels", {}).items():
-        if kernel_tag in name:
-            return v.get("hbm_bytes_per_launch")
-    return None
+    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic*.json")),
+                   key=os.path.getmtime)
+    for f in reversed(files):
+        d = json.load(open(f))
+        for name, v in d.get("kernels", {}).items():
+            if name.split("(")[0].strip() == kernel_tag or name.startswith(kernel_tag + "("):
+                return v.get("hbm_bytes_per_launch"), os.path.basename(f)
+    return None, None
 
 
-def cpu_baseline(frames: int, classes: int):
-    """The oracle restatement of the whole step on the host cores (bounded sample)."""
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(frames: int, classes: int, warmup: int = 3, steps: int = 5):
+    """The oracle restatement of the whole step on the host cores (bounded sample; BASELINE.md §3:
+    3 warm-up steps, >= 5 timed steps, CPU model and thread count reported)."""
     from oracle import anchor_head as oh
     from oracle import voxelize as ov
     from oracle.perturber import OraclePerturber, perturb_voxels
@@ -146,14 +160,47 @@ def cpu_baseline(frames: int, classes: int):
         opt.step()
         opt.zero_grad()
 
-    step()                       # warm-up
+    for _ in range(warmup):
+        step()
     t0 = time.perf_counter()
-    step()
+    for _ in range(steps):
+        step()
     dt = time.perf_counter() - t0
-    return dict(value=round(frames / dt, 4), unit="frames/s", cores=cores, kind="port",
-                sample=f"1 timed step (after 1 warm-up) of the oracle restatement (C voxelize, torch-CPU fp32 "
-                       f"perturber + sparse encoder, torch-CPU SECOND/FPN/Anchor3DHead fwd+bwd, AdamW) on "
-                       f"{frames} synthetic KITTI frames, {classes}-class, {dt:.1f} s")
+    return dict(value=round(frames * steps / dt, 4), unit="frames/s", cores=cores, kind="port",
+                cpu_model=_cpu_model(), warmup=warmup, steps=steps,
+                sample=f"{steps} timed steps (after {warmup} warm-up) of the oracle restatement (C voxelize, "
+                       f"torch-CPU fp32 perturber + sparse encoder, torch-CPU SECOND/FPN/Anchor3DHead fwd+bwd, "
+                       f"AdamW), {frames} synthetic KITTI frames per step, {classes}-class, {dt:.1f} s timed")
+
+
+def _dense_flops_per_frame(model, H, W):
+    """Algorithmic FLOPs of one frame through SECOND + SECONDFPN + the head's 1x1 convs: forward, data
+    gradient and weight gradient of every conv (3 x 2·MACs; the first conv's data gradient is the BEV
+    gradient the sparse encoder needs), from the modules' own shapes."""
+    from torch import nn
+    total = 0.0
+    h, w = H, W
+    dims = []
+    for blk in model.backbone.blocks:
+        for m in blk:
+            if isinstance(m, nn.Conv2d):
+                s = m.stride[0]
+                h, w = (h + s - 1) // s, (w + s - 1) // s
+                total += 3 * 2.0 * h * w * m.in_channels * m.out_channels * m.kernel_size[0] * m.kernel_size[1]
+        dims.append((h, w))
+    for (hi, wi), d in zip(dims, model.neck.deblocks):
+        m = d[0]
+        total += 3 * 2.0 * hi * wi * m.in_channels * m.out_channels * m.kernel_size[0] * m.kernel_size[1]
+    head = model.bbox_head
+    for c in head._convs():
+        total += 3 * 2.0 * H * W * c.in_channels * c.out_channels
+    return total
+
+
+def _perturber_flops_per_point(adv):
+    from torch import nn
+    lin = [m for m in list(adv.model) + list(adv.attention or []) if isinstance(m, nn.Linear)]
+    return 3 * 2.0 * sum(m.in_features * m.out_features for m in lin)
 
 
 def _launch_ranks(n: int) -> int:
@@ -220,18 +267,35 @@ def main():
     if dist.is_initialized():
         dist.barrier()
     dt = time.perf_counter() - t0
-    # per-launch HIP-event timing of the roofline kernel: ROCm cannot record timing events inside a
-    # captured graph, so 2 more steps of the same workload run with the dense graphs off and the timer
-    # on (same kernels, shapes and inputs as the timed steps; rocprof summaries under profiles/ agree)
+    # per-launch HIP-event timing of the roofline kernels and of the HBM-bound stages: ROCm cannot record
+    # timing events inside a captured graph, so 2 more steps of the same workload run with the dense
+    # graphs off and the timers on (same kernels, shapes and inputs as the timed steps; rocprof summaries
+    # under profiles/ agree); the second of them also counts the step's algorithmic FLOPs
+    from robustpointclouds_amd import stage_timer
     graphs = dense_bev.GRAPHS
     dense_bev.GRAPHS = False
     timer.enabled = True
+    stage_timer.TIMER.enabled = True
+    me = getattr(model, "middle_encoder", None)
     for i in range(a.steps, a.steps + 2):
+        if i == a.steps + 1 and me is not None:
+            me.flop_probe = []
         tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0])
     torch.cuda.synchronize()
     timer.enabled = False
+    stage_timer.TIMER.enabled = False
     dense_bev.GRAPHS = graphs
     ks = timer.summary()
+    stages = stage_timer.TIMER.summary()
+    step_flops = None
+    if me is not None and me.flop_probe and not nus:
+        sparse = sum(3 * 2.0 * float((nbr >= 0).sum().item()) * ci * co for nbr, ci, co in me.flop_probe[-1])
+        me.flop_probe = None
+        flags = getattr(model, "_last_flags", None)
+        n_valid = float(flags[4].item()) if flags is not None else 0.0
+        pert = n_valid * _perturber_flops_per_point(model.adversary) if model.adversary is not None else 0.0
+        dense = _dense_flops_per_frame(model, 200, 176) * a.batch
+        step_flops = dict(dense=dense, sparse=sparse, perturber=pert, total=dense + sparse + pert)
     if dist.is_initialized():
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -261,34 +325,45 @@ def main():
                                parallelism=f"dp{world}",
                                dist_backend=dist.get_backend() if dist.is_initialized() else None))
         if ks and op is None:
-            peak = PEAK["bf16_mfma"]
-            res["roofline"] = dict(bound="mfma", achieved=round(ks["tflops"], 3), peak=peak, unit="TFLOP/s",
-                                   frac=round(ks["tflops"] / peak, 4), traffic=_traffic("k_conv3x3"),
-                                   kernel=ks["kernel"] + " (SECOND 3x3 stride-1 conv, fwd + data gradient, "
-                                   "bf16 MFMA, fp32 accumulate; 200x176 launches: k_conv3x3<0>, 100x88: "
-                                   "k_conv3x3w<0>)",
-                                   avg_launch_ms=round(ks["avg_ms"], 4), flops_per_launch=ks["flops_per_launch"],
-                                   algorithmic_bytes_per_launch=ks["bytes_per_launch"],
-                                   achieved_gbps=round(ks["gbps"], 1), launches=ks["launches"],
-                                   work="2*B*H*W*C_in*C_out*9 FLOP per launch")
+            # one entry per kernel, each over its own launches with its own FLOPs / bytes / PMC traffic;
+            # `roofline` is the one with the most time per step
+            peak = PEAK["fp32_mfma"] if a.fp32 else PEAK["bf16_mfma"]
+            ents = []
+            for name, k in ks.items():
+                tr_bytes, tr_src = _traffic(name)
+                ents.append(dict(bound="mfma", kernel=name, achieved=round(k["tflops"], 3), peak=peak, unit="TFLOP/s",
+                                 frac=round(k["tflops"] / peak, 4), traffic=tr_bytes, traffic_source=tr_src,
+                                 avg_launch_ms=round(k["avg_ms"], 4), launches=k["launches"],
+                                 flops_per_launch=k["flops_per_launch"],
+                                 algorithmic_bytes_per_launch=k["bytes_per_launch"],
+                                 achieved_gbps=round(k["gbps"], 1), ms_per_step=round(k["total_ms"] / 2, 4),
+                                 work="2*B*H*W*C_in*C_out*9 FLOP per launch (SECOND 3x3 stride-1 conv, "
+                                      "forward + flipped-tap data gradient)"))
+            ents.sort(key=lambda e: -e["ms_per_step"])
+            res["roofline"] = dict(ents[0])
+            res["roofline_kernels"] = ents
         elif ks:
             peak = PEAK["bf16_mfma" if ks["dtype"] == "bf16" else "fp32_mfma"]
             tag = ks["kernel"]
             res["roofline"] = dict(bound="mfma", achieved=round(ks["tflops"], 3), peak=peak,
                                    unit="TFLOP/s", frac=round(ks["tflops"] / peak, 4),
-                                   traffic=_traffic(tag.split("::")[-1]),
+                                   traffic=_traffic(tag)[0],
                                    kernel=f"{tag} (sparse conv {op} {ci}->{co}, {ks['dtype']} MFMA)",
                                    avg_launch_ms=round(ks["avg_ms"], 4),
                                    flops_per_launch=ks["flops_per_launch"], launches=ks["launches"],
                                    work="2*C_in*C_out FLOP per valid rulebook pair")
-        if not nus and a.classes == 3:
-            # whole-step algorithmic rate next to the dominant kernel's: 441 GFLOP per frame
-            # = SECOND/FPN/head fwd + data and weight gradients (418) + sparse encoder (21) + perturber (3.2),
-            # bf16 MFMA peak as the bound
-            fpf = 441e9
-            res["step_roofline"] = dict(flop_per_frame=fpf, achieved=round(frames / dt * fpf / 1e12, 1),
-                                        peak=PEAK["bf16_mfma"], unit="TFLOP/s",
-                                        frac=round(frames / dt * fpf / 1e12 / PEAK["bf16_mfma"], 4))
+        if stages:
+            # HBM-bound stages: compulsory bytes (stage_timer.py) / HIP-event time / 8 TB/s
+            res["stage_roofline"] = dict(bound="hbm", unit="GB/s", stages=stages)
+        if step_flops is not None:
+            # whole-step algorithmic FLOP rate, the per-frame constant counted on this run's
+            # synthetic frames: dense convs from the module shapes, sparse convs from the valid rulebook pairs,
+            # perturber from the valid points (each x3: forward, data gradient, weight gradient)
+            fpf = step_flops["total"] / a.batch
+            res["step_roofline"] = dict(flop_per_frame=round(fpf), flop_per_frame_split={
+                k: round(v / a.batch) for k, v in step_flops.items() if k != "total"},
+                achieved=round(frames / dt * fpf / 1e12, 1), peak=PEAK["fp32_mfma" if a.fp32 else "bf16_mfma"], unit="TFLOP/s",
+                frac=round(frames / dt * fpf / 1e12 / PEAK["fp32_mfma" if a.fp32 else "bf16_mfma"], 4))
         if not a.no_cpu_baseline and a.model == "voxelnet":
             res["cpu_baseline"] = cpu_baseline(a.cpu_frames, a.classes)
         print(json.dumps(res), flush=True)

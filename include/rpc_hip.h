@@ -268,6 +268,10 @@ int rpc_dense_conv(int map, const void* src, int src_pitch, int cin, const void*
                    int out_pitch, int out_offset, int accumulate, float* part, const int* row_img,
                    const int* src_img, const int* out_img, void* stream);
 int rpc_dense_conv_blocks(int map, const int* row_img);
+/* which kernel rpc_dense_conv launches for an RPC_DMAP_S1 call with `cout` outputs over row_img:
+ * 0 = rpc::dn::k_conv3x3<0> (64-channel blocks), 1 = rpc::dn::k_conv3x3w<0> (128-channel LDS-DMA
+ * blocks), -1 = not an S1 call (per-kernel roofline attribution in bench.py) */
+int rpc_dense_conv_s1_kernel(int map, int cout, const int* row_img);
 /* kernel-selection knob for A/B measurement (returns the previous value; value < 0 only reads it):
  * knob 0 = the S1 kernel for output channels that are a multiple of 128 (0: chosen by shape, default;
  * 1: the 64-channel register-staged kernel; 2: the 128-channel LDS-DMA kernel); knob 1 = the S1 weight

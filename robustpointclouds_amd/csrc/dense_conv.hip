@@ -1466,6 +1466,12 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   return RPC_OK;
 }
 
+extern "C" int rpc_dense_conv_s1_kernel(int map, int cout, const int* r_img) {
+  if (map != M_S1 || !r_img || cout % 64) return -1;
+  const int TY = (r_img[1] + CT - 1) / CT, TX = (r_img[2] + CT - 1) / CT;
+  return s1_wide(r_img[0] * TY * TX, cout) ? 1 : 0;
+}
+
 extern "C" int rpc_dense_conv_blocks(int map, const int* r_img) {
   if (map == M_S1) return r_img[0] * ((r_img[1] + CT - 1) / CT) * ((r_img[2] + CT - 1) / CT);
   const long long M = (long long)r_img[0] * r_img[1] * r_img[2];

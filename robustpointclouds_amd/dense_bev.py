@@ -48,25 +48,37 @@ class ConvTimer:
         e.record(torch.cuda.current_stream())
         return e
 
-    def stop(self, e0, rows, ci, co):
+    KERNELS = {0: "rpc::dn::k_conv3x3<0>", 1: "rpc::dn::k_conv3x3w<0>"}
+
+    def stop(self, e0, rows, ci, co, variant=0):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(torch.cuda.current_stream())
-        self.recs.append((e0, e1, rows, ci, co))
+        self.recs.append((e0, e1, rows, ci, co, variant))
 
     def reset(self):
         self.recs = []
 
+    @staticmethod
+    def _stats(recs, kernel):
+        ms = sum(a.elapsed_time(b) for a, b, *_ in recs)
+        flops = sum(2.0 * r * ci * co * 9 for _, _, r, ci, co, _v in recs)
+        byts = sum(2.0 * r * (ci + co) + 2.0 * 9 * ci * co for _, _, r, ci, co, _v in recs)
+        n = len(recs)
+        return dict(launches=n, avg_ms=ms / n, flops_per_launch=flops / n, bytes_per_launch=byts / n,
+                    tflops=flops / (ms * 1e-3) / 1e12, gbps=byts / (ms * 1e-3) / 1e9, kernel=kernel, dtype="bf16",
+                    total_ms=ms)
+
     def summary(self):
+        """Per kernel: {kernel name: stats}, each over that kernel's own launches, FLOPs and bytes."""
         torch.cuda.synchronize()
         if not self.recs:
             return None
-        ms = sum(a.elapsed_time(b) for a, b, *_ in self.recs)
-        flops = sum(2.0 * r * ci * co * 9 for _, _, r, ci, co in self.recs)
-        byts = sum(2.0 * r * (ci + co) + 2.0 * 9 * ci * co for _, _, r, ci, co in self.recs)
-        n = len(self.recs)
-        return dict(launches=n, avg_ms=ms / n, flops_per_launch=flops / n, bytes_per_launch=byts / n,
-                    tflops=flops / (ms * 1e-3) / 1e12, gbps=byts / (ms * 1e-3) / 1e9,
-                    kernel="rpc::dn::k_conv3x3<0>", dtype="bf16")
+        out = {}
+        for v, name in self.KERNELS.items():
+            rs = [r for r in self.recs if r[5] == v]
+            if rs:
+                out[name] = self._stats(rs, name)
+        return out
 
 
 TIMER = None
@@ -200,7 +212,7 @@ def _conv(lib, fmap, *args):
     rc = lib.rpc_dense_conv(fmap, *args)
     if t is not None:
         r = _ffi_img_rows(args[10])
-        t.stop(e0, r, args[2], args[4])
+        t.stop(e0, r, args[2], args[4], lib.rpc_dense_conv_s1_kernel(fmap, args[4], args[10]))
     return rc
 
 

@@ -20,6 +20,7 @@ import ctypes as C
 import torch
 
 from . import _ffi
+from . import stage_timer
 
 
 def make_cfg(F, hidden, use_attention, training, sensor_error_bound, bn_eps=1e-3, bn_momentum=0.1,
@@ -124,7 +125,11 @@ class PerturbVoxelsFn(torch.autograd.Function):
         V, P, F = voxels.shape
         out = torch.empty_like(voxels)
         vfe = torch.empty((V, cfg.vfe_features), dtype=torch.float32, device=voxels.device)
+        tm = stage_timer.active()
+        e0 = stage_timer.TIMER.start() if tm else None
         ws, losses = _run_forward(cfg, params, voxels, V, P, num_points, out, vfe)
+        if tm:
+            stage_timer.TIMER.stop("perturber_fwd", e0, 2 * V * P * F * 4 + V * 4 + V * cfg.vfe_features * 4)
         ctx.cfg = cfg
         ctx.save_for_backward(voxels, num_points, ws, *params)
         ctx.mark_non_differentiable(out, losses)
@@ -137,7 +142,11 @@ class PerturbVoxelsFn(torch.autograd.Function):
         dev = voxels.device
         dvfe = torch.zeros((V, ctx.cfg.vfe_features), device=dev) if dvfe is None else dvfe.contiguous()
         dl = _loss_grads(dlvec, dev)
+        tm = stage_timer.active()
+        e0 = stage_timer.TIMER.start() if tm else None
         grads = _run_backward(ctx.cfg, params, voxels, V, P, num_points, dvfe, dl, ws)
+        if tm:
+            stage_timer.TIMER.stop("perturber_bwd", e0, V * P * F * 4 + V * 4 + V * ctx.cfg.vfe_features * 4)
         return (None, None, None, *grads)
 
 

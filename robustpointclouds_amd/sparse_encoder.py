@@ -23,7 +23,7 @@ from dataclasses import dataclass
 import torch
 from torch import nn
 
-from . import _ffi, dense_bev
+from . import _ffi, dense_bev, stage_timer
 
 
 @dataclass
@@ -178,6 +178,7 @@ class SparseEncoder(nn.Module):
         self._grids = {}
         self.timer = None   # optional KernelTimer (bench.py roofline), see below
         self.debug = None   # optional list: backward appends (layer, dy) for diagnostics
+        self.flop_probe = None   # optional list: forward appends [(rulebook, C_in, C_out)] per step (bench.py)
         # perf mode: forward / dgrad convs on bf16 MFMA with bf16 gathered rows (fp32 accumulate,
         # fp32 BatchNorm statistics); parity mode (default) is fp32 end to end
         self.bf16 = False
@@ -263,6 +264,23 @@ def _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st):
     return dzb, btd
 
 
+def _sparse_bytes(L, bf16, dense_bytes, backward):
+    """Compulsory HBM bytes of the sparse encoder (stage_timer.py): per layer the input rows it gathers
+    (bf16 rows in perf mode for layers >= 1), its rulebook and its output rows; backward adds the dz rows,
+    the saved z and the data gradient; plus the dense BEV image (or its gradient) once."""
+    total = dense_bytes
+    for li, rec in enumerate(L):
+        sp = rec["spec"]
+        ein = 2 if (bf16 and li > 0) else 4
+        n_in, n_out = rec["n_in"], rec["n_out"]
+        fwd = n_in * sp.ci * ein + n_out * sp.K * 4 + n_out * sp.co * 4
+        if not backward:
+            total += fwd
+        else:
+            total += n_out * sp.co * 4 * 2 + n_out * sp.K * 4 + n_in * sp.ci * ein + n_in * sp.ci * 4
+    return total
+
+
 class KernelTimer:
     """HIP-event timing of selected conv launches on the stream they are launched on.
 
@@ -309,6 +327,8 @@ class SparseEncoderFn(torch.autograd.Function):
         lib = _ffi.load()
         dev = feats.device
         st = _ffi.stream_of(feats)
+        tm_stage = stage_timer.active()
+        e_stage = stage_timer.TIMER.start() if tm_stage else None
         feats = feats.contiguous().float()
         coors = coors.to(torch.int32).contiguous()
         mods = enc.layers()
@@ -454,6 +474,11 @@ class SparseEncoderFn(torch.autograd.Function):
         shp = _ffi.int_arr((B, D, H, Wd))
         _ffi.check(lib.rpc_sparse_to_dense(_ffi.ptr(last["z"]), _ffi.ptr(last["bn"]), _ffi.ptr(last["coors_out"]),
                                            last["n_out"], C, shp, flags, _ffi.ptr(dense), st), "rpc_sparse_to_dense")
+        if enc.flop_probe is not None:
+            enc.flop_probe.append([(rec["nbr"], rec["spec"].ci, rec["spec"].co) for rec in L])
+        if tm_stage:
+            stage_timer.TIMER.stop("sparse_fwd", e_stage, _sparse_bytes(L, bf16, dense.numel() * dense.element_size(),
+                                                                          backward=False))
         ctx.dense_flags = flags
         ctx.L = L
         ctx.enc = enc
@@ -469,6 +494,10 @@ class SparseEncoderFn(torch.autograd.Function):
         L = ctx.L
         dev = gdense.device
         st = _ffi.stream_of(gdense)
+        tm_stage = stage_timer.active()
+        e_stage = stage_timer.TIMER.start() if tm_stage else None
+        nbytes = _sparse_bytes(L, ctx.bf16, gdense.numel() * (2 if ctx.dense_flags & 2 else 4), backward=True) \
+            if tm_stage else 0
         B, C, D, H, Wd = ctx.shape
         flags = ctx.dense_flags
         dt = torch.bfloat16 if flags & 2 else torch.float32
@@ -591,6 +620,8 @@ class SparseEncoderFn(torch.autograd.Function):
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
                                                     None, _ffi.ptr(din), None, st), "rpc_spconv_dgrad")
                 dfeat = din
+        if tm_stage:
+            stage_timer.TIMER.stop("sparse_bwd", e_stage, nbytes)
         ctx.L = None
         ctx.enc = None
         return (dfeat, None, None, None, *grads)

@@ -16,6 +16,7 @@ import torch
 from torch import nn
 
 from . import _ffi
+from . import stage_timer
 
 
 def _frame_offsets(sizes: Sequence[int], device) -> torch.Tensor:
@@ -54,12 +55,17 @@ def voxelize_batch(points: torch.Tensor, frame_offsets: torch.Tensor, voxel_size
     voxel_num = torch.empty((B + 1,), dtype=torch.int32, device=dev)
     wsb = lib.rpc_hard_voxelize_workspace_size(P, B)
     ws = _ffi.workspace(wsb, dev)
+    tm = stage_timer.active()
+    e0 = stage_timer.TIMER.start() if tm else None
     rc = lib.rpc_hard_voxelize(_ffi.ptr(points), F, P, _ffi.ptr(frame_offsets), B,
                                _ffi.float_arr(voxel_size), _ffi.float_arr(point_cloud_range),
                                int(max_num_points), int(max_voxels), _ffi.ptr(voxels), _ffi.ptr(coors),
                                _ffi.ptr(num_points), _ffi.ptr(voxel_num), _ffi.ptr(ws), wsb,
                                _ffi.stream_of(points))
     _ffi.check(rc, "rpc_hard_voxelize")
+    if tm:
+        vrow = max_num_points * F * 4 + 16 + 4
+        stage_timer.TIMER.stop("voxelize", e0, lambda: P * F * 4 + int(voxel_num[B]) * vrow)
     if defer:
         return PendingVoxels(voxels, coors, num_points, voxel_num, B)
     V = int(voxel_num[B].item())  # the one host sync: output shapes

@@ -61,6 +61,8 @@ class AdversarialCenterPoint(CenterPoint):
             return super().extract_pts_feat(voxel_dict, points, img_feats, batch_input_metas)
         voxels, npts, coors = voxel_dict["voxels"], voxel_dict["num_points"], voxel_dict["coors"]
         self._sync_engines(voxels.device)
+        if hasattr(self.pts_middle_encoder, "coors_ready"):
+            self.pts_middle_encoder.coors_ready(coors)
         l2 = None
         if self.training and self._epoch >= 3:
             if isinstance(self.pts_voxel_encoder, HardSimpleVFE):

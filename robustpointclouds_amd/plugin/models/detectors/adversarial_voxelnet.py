@@ -68,6 +68,8 @@ class AdversarialVoxelNet(VoxelNet):
         l2, loss_dict = None, None
         voxels, npts, coors = vd["voxels"], vd["num_points"], vd["coors"]
         self._sync_engines(voxels.device)
+        if hasattr(self.middle_encoder, "coors_ready"):
+            self.middle_encoder.coors_ready(coors)   # its rulebooks build concurrently with the perturber
         if self._gate() and isinstance(self.voxel_encoder, HardSimpleVFE):
             feats, loss_dict, pert, flags = self.adversary.perturb_voxels(voxels, npts,
                                                                           self.voxel_encoder.num_features)

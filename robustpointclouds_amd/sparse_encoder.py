@@ -18,6 +18,7 @@ conv weights are stored [K, C_in, C_out] (k = (kz*3 + ky)*3 + kx).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 
 import torch
@@ -44,6 +45,10 @@ class _Spec:
     @property
     def K(self):
         return self.ksize[0] * self.ksize[1] * self.ksize[2]
+
+
+# rulebooks / sparse weight gradients on side streams (SparseEncoder.side_stream)
+SIDE_STREAMS = os.environ.get("RPC_SPARSE_STREAMS", "1") != "0"
 
 
 def _t3(v):
@@ -199,6 +204,26 @@ class SparseEncoder(nn.Module):
         mods.append((self.conv_out[0], self.conv_out[1]))
         return mods
 
+    def side_stream(self, name, device):
+        """A per-encoder side stream ('rb': rulebooks in the forward, 'wg': weight gradients in the backward);
+        RPC_SPARSE_STREAMS=0 puts both back on the current stream (A/B measurement)."""
+        if not SIDE_STREAMS:
+            return torch.cuda.current_stream(device)
+        key = (name, str(device))
+        s = self.__dict__.setdefault("_side_streams", {}).get(key)
+        if s is None:
+            s = self._side_streams[key] = torch.cuda.Stream(device)
+        return s
+
+    def coors_ready(self, coors: torch.Tensor) -> None:
+        """Called by the detector as soon as the voxel coordinates are queued, before the perturber: the
+        rulebooks (which depend on the coordinates only) are then built on a side stream concurrently
+        with the perturber and the first GEMMs instead of after them."""
+        if coors.is_cuda:
+            ev = torch.cuda.Event()
+            ev.record(torch.cuda.current_stream(coors.device))
+            self._coors_ready = (coors.data_ptr(), ev)
+
     def grid(self, lvl, B, device):
         """Dense int32 index grid [B, D, H, W] kept all -1 between uses."""
         key = (lvl, B, str(device))
@@ -321,6 +346,76 @@ class KernelTimer:
                     kernel=self.kernel, dtype=self.dtype)
 
 
+def _rulebooks(lib, enc, coors, n0, B, dev):
+    """Every layer's rulebook on the encoder's 'rb' side stream: the submanifold neighbour lists (one
+    per indice key) and, for each strided conv, its output count (a host read: the output allocation
+    size), output coordinates and both neighbour maps. The chain depends on the coordinates only, so
+    it starts from the detector's coors_ready event — concurrently with the perturber — and the main
+    stream waits for each layer's event right before that layer's GEMM. Returns one dict per spec."""
+    main = torch.cuda.current_stream(dev)
+    side = enc.side_stream("rb", dev)
+    ready = enc.__dict__.pop("_coors_ready", None)
+    if ready is not None and ready[0] == coors.data_ptr():
+        side.wait_event(ready[1])
+    else:
+        side.wait_stream(main)
+    plan = []
+    made = []
+    with torch.cuda.stream(side):
+        st = _ffi.stream_of(coors)
+        rb = {}
+        cur_coors, cur_n = coors, n0
+        for sp in enc.specs:
+            ks = _ffi.int_arr(sp.ksize)
+            p = dict(n_in=cur_n, coors_in=cur_coors)
+            if sp.kind == "subm":
+                if sp.key not in rb:
+                    nbr = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
+                    shp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_in])
+                    _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, ks,
+                                                     _ffi.ptr(enc.grid(sp.lvl_in, B, dev)), _ffi.ptr(nbr), st),
+                               "rpc_subm_rulebook")
+                    rb[sp.key] = nbr
+                    made.append(nbr)
+                p.update(nbr=rb[sp.key], n_out=cur_n, coors_out=cur_coors)
+            else:
+                oshp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_out])
+                sd, pd = _ffi.int_arr(sp.stride), _ffi.int_arr(sp.pad)
+                wsb = lib.rpc_spconv_rulebook_workspace_size(cur_n, sp.K)
+                ws = _ffi.workspace(wsb, dev)
+                n_dev = torch.empty(1, dtype=torch.int32, device=dev)
+                gout = enc.grid(sp.lvl_out, B, dev)
+                _ffi.check(lib.rpc_spconv_rulebook_count(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
+                                                         _ffi.ptr(n_dev), _ffi.ptr(ws), wsb, st),
+                           "rpc_spconv_rulebook_count")
+                n_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                n_host.copy_(n_dev, non_blocking=True)
+                ev_n = torch.cuda.Event()
+                ev_n.record(side)
+                ev_n.synchronize()
+                n_out = int(n_host[0])             # host read: the output row count (side stream only)
+                coors_out = torch.empty((n_out, 4), dtype=torch.int32, device=dev)
+                nbr_out = torch.empty((n_out, sp.K), dtype=torch.int32, device=dev)
+                nbr_in = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
+                _ffi.check(lib.rpc_spconv_rulebook_build(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
+                                                         n_out, _ffi.ptr(coors_out), _ffi.ptr(nbr_out),
+                                                         _ffi.ptr(nbr_in), _ffi.ptr(ws), st),
+                           "rpc_spconv_rulebook_build")
+                made += [coors_out, nbr_out, nbr_in]
+                p.update(nbr=nbr_out, nbr_in=nbr_in, n_out=n_out, coors_out=coors_out)
+                cur_coors, cur_n = coors_out, n_out
+            ev = torch.cuda.Event()
+            ev.record(side)
+            p["ev"] = ev
+            plan.append(p)
+    # made on the side stream, used and freed on the main one: the allocator must not recycle them
+    # before the main stream's work on them is done
+    for t in made:
+        t.record_stream(main)
+    coors.record_stream(side)
+    return plan
+
+
 class SparseEncoderFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, feats, coors, enc: SparseEncoder, B: int, *params):
@@ -332,8 +427,6 @@ class SparseEncoderFn(torch.autograd.Function):
         feats = feats.contiguous().float()
         coors = coors.to(torch.int32).contiguous()
         mods = enc.layers()
-        rb = {}
-        cur_coors, cur_n = coors, feats.shape[0]
         src, src_bn = feats, None
         # perf mode: layers >= 1 gather bf16 rows of relu(bn(z)) (O(1) values); layer 0 stays fp32 —
         # its input is the raw VFE mean (coordinates up to 70 m, where a bf16 step is 0.5 m)
@@ -347,61 +440,19 @@ class SparseEncoderFn(torch.autograd.Function):
             Ws = [params[3 * li].detach().float().contiguous() for li in bl]
             for li, tiles in zip(bl, _prep_bf16_weights(lib, [enc.specs[li] for li in bl], Ws, dev, st)):
                 wtiles[li] = tiles
-        # Output-row counts of the strided layers are host reads. Each count is issued as soon as its
-        # input coordinates exist (one level ahead of the GEMMs), copied to pinned memory behind an
-        # event, and waited for only when its layer is reached: the GEMMs of the current level keep the
-        # GPU busy while the host waits, instead of the stream draining at every read.
-        pending = {}
-
-        def issue_count(start, coors_in, n_in):
-            j = next((k for k in range(start, len(enc.specs)) if enc.specs[k].kind != "subm"), None)
-            if j is None:
-                return
-            sj = enc.specs[j]
-            oshp = _ffi.int_arr((B,) + enc.shapes[sj.lvl_out])
-            ks_, sd, pd = _ffi.int_arr(sj.ksize), _ffi.int_arr(sj.stride), _ffi.int_arr(sj.pad)
-            wsb = lib.rpc_spconv_rulebook_workspace_size(n_in, sj.K)
-            ws = _ffi.workspace(wsb, dev)
-            n_dev = torch.empty(1, dtype=torch.int32, device=dev)
-            gout = enc.grid(sj.lvl_out, B, dev)
-            _ffi.check(lib.rpc_spconv_rulebook_count(_ffi.ptr(coors_in), n_in, oshp, ks_, sd, pd, _ffi.ptr(gout),
-                                                     _ffi.ptr(n_dev), _ffi.ptr(ws), wsb, st),
-                       "rpc_spconv_rulebook_count")
-            n_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-            n_host.copy_(n_dev, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(torch.cuda.current_stream(dev))
-            pending[j] = (n_host, ev, ws, gout, oshp, ks_, sd, pd)
-
-        issue_count(0, cur_coors, cur_n)
+        # rulebooks (and the strided layers' output counts, host reads) on a side stream, ahead of the GEMMs
+        plan = _rulebooks(lib, enc, coors, feats.shape[0], B, dev)
+        main = torch.cuda.current_stream(dev)
         for li, (sp, m) in enumerate(zip(enc.specs, mods)):
             W = params[3 * li]
             gamma, beta = params[3 * li + 1], params[3 * li + 2]
             bnm = m[1]
-            ks = _ffi.int_arr(sp.ksize)
-            rec = dict(spec=sp, n_in=cur_n, src=src, src_bn=src_bn, coors_in=cur_coors)
-            if sp.kind == "subm":
-                if sp.key not in rb:
-                    nbr = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
-                    shp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_in])
-                    _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, ks,
-                                                     _ffi.ptr(enc.grid(sp.lvl_in, B, dev)), _ffi.ptr(nbr), st),
-                               "rpc_subm_rulebook")
-                    rb[sp.key] = nbr
-                rec.update(nbr=rb[sp.key], n_out=cur_n, coors_out=cur_coors)
-            else:
-                n_host, ev, ws, gout, oshp, ks, sd, pd = pending.pop(li)
-                ev.synchronize()
-                n_out = int(n_host[0])             # host read: output row count (issued one level ahead)
-                coors_out = torch.empty((n_out, 4), dtype=torch.int32, device=dev)
-                nbr_out = torch.empty((n_out, sp.K), dtype=torch.int32, device=dev)
-                nbr_in = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
-                _ffi.check(lib.rpc_spconv_rulebook_build(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
-                                                         n_out, _ffi.ptr(coors_out), _ffi.ptr(nbr_out),
-                                                         _ffi.ptr(nbr_in), _ffi.ptr(ws), st),
-                           "rpc_spconv_rulebook_build")
-                rec.update(nbr=nbr_out, nbr_in=nbr_in, n_out=n_out, coors_out=coors_out)
-                issue_count(li + 1, coors_out, n_out)
+            p = plan[li]
+            rec = dict(spec=sp, n_in=p["n_in"], src=src, src_bn=src_bn, coors_in=p["coors_in"], nbr=p["nbr"],
+                       n_out=p["n_out"], coors_out=p["coors_out"])
+            if "nbr_in" in p:
+                rec["nbr_in"] = p["nbr_in"]
+            main.wait_event(p["ev"])
             n_out = rec["n_out"]
             z = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
             nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
@@ -448,7 +499,6 @@ class SparseEncoderFn(torch.autograd.Function):
                     hsrc = torch.empty((n_out, _r8(sp.co)), dtype=torch.bfloat16, device=dev)
                     _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(z), _ffi.ptr(bn), n_out, sp.co, 1, _ffi.ptr(hsrc), st),
                                "rpc_to_bf16_rows")
-            cur_coors, cur_n = rec["coors_out"], n_out
         _ffi.bump_batches([m[1] for m in mods])
         last = L[-1]
         D, H, Wd = enc.shapes[-1]
@@ -515,6 +565,8 @@ class SparseEncoderFn(torch.autograd.Function):
                                                 _ffi.ptr(last["coors_out"]), n, C, _ffi.int_arr((B, D, H, Wd)),
                                                 flags, _ffi.ptr(dy), _ffi.ptr(part), st), "rpc_dense_to_sparse_grad")
         dfeat = None
+        main = torch.cuda.current_stream(dev)
+        wg = ctx.enc.side_stream("wg", dev)
         G = [[] for _ in L]     # gradient contributions to materialised outputs
         for li in range(len(L) - 1, -1, -1):
             rec = L[li]
@@ -544,31 +596,45 @@ class SparseEncoderFn(torch.autograd.Function):
                                            _ffi.ptr(rec["beta"]), 0.0, 0.0, None, None, _ffi.ptr(rec["bn"]),
                                            _ffi.ptr(bnb), _ffi.ptr(dgamma), _ffi.ptr(dbeta), None, st),
                        "rpc_bn_finalize(bwd)")
-            # weight gradient
+            # weight gradient, on the 'wg' side stream: it reads only this layer's dz / input rows, so it
+            # runs concurrently with the data-gradient chain of the main stream (both are gather-latency
+            # bound with partial occupancy); the main stream joins it at the end of the backward
             dW = torch.empty_like(rec["W"])
             timer = ctx.enc.timer
             tw = timer is not None and timer.wants("wgrad", sp)
             dzb = btd = None
             if rec["bf16"]:
                 dzb, btd = _bf16_dgrad_operands(lib, rec, dy, bnb, dev, st)
-                wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, sp.K, sp.ci, sp.co)
-                ws = _ffi.workspace(wsz, dev)
-                e0 = timer.start() if tw else None
-                _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(rec["h_in"]), sp.ci, _ffi.ptr(rec["nbr"]), sp.K, n_out,
-                                                     _ffi.ptr(dzb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st),
-                           "rpc_spconv_wgrad_bf16")
-                kn = f"rpc::spb::k_wgrad_bf16<{sp.ci}, {sp.co}, 3>"
+                ins = (rec["h_in"], rec["nbr"], dzb, dW)
             else:
-                wsz = lib.rpc_spconv_wgrad_workspace_size(n_out, sp.K, sp.ci, sp.co)
-                ws = _ffi.workspace(wsz, dev)
-                e0 = timer.start() if tw else None
-                _ffi.check(lib.rpc_spconv_wgrad(_ffi.ptr(rec["src"]), _ffi.ptr(rec["src_bn"]), sp.ci,
-                                                _ffi.ptr(rec["nbr"]), sp.K, n_out, _ffi.ptr(dy), _ffi.ptr(rec["z"]),
-                                                _ffi.ptr(bnb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st),
-                           "rpc_spconv_wgrad")
-                kn = f"rpc::sp::k_wgrad<{sp.ci}, {sp.co}, {1 if li else 0}>"
-            if tw:
-                timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
+                ins = (rec["src"], rec["src_bn"], rec["nbr"], dy, rec["z"], bnb, dW)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            wg.wait_event(ev)
+            with torch.cuda.stream(wg):
+                sw = _ffi.stream_of(dW)
+                if rec["bf16"]:
+                    wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, sp.K, sp.ci, sp.co)
+                    ws = _ffi.workspace(wsz, dev)
+                    e0 = timer.start() if tw else None
+                    _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(rec["h_in"]), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
+                                                         n_out, _ffi.ptr(dzb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws), wsz,
+                                                         sw), "rpc_spconv_wgrad_bf16")
+                    kn = f"rpc::spb::k_wgrad_bf16<{sp.ci}, {sp.co}, 3>"
+                else:
+                    wsz = lib.rpc_spconv_wgrad_workspace_size(n_out, sp.K, sp.ci, sp.co)
+                    ws = _ffi.workspace(wsz, dev)
+                    e0 = timer.start() if tw else None
+                    _ffi.check(lib.rpc_spconv_wgrad(_ffi.ptr(rec["src"]), _ffi.ptr(rec["src_bn"]), sp.ci,
+                                                    _ffi.ptr(rec["nbr"]), sp.K, n_out, _ffi.ptr(dy), _ffi.ptr(rec["z"]),
+                                                    _ffi.ptr(bnb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws), wsz, sw),
+                               "rpc_spconv_wgrad")
+                    kn = f"rpc::sp::k_wgrad<{sp.ci}, {sp.co}, {1 if li else 0}>"
+                if tw:
+                    timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
+            for t in ins:
+                if t is not None:
+                    t.record_stream(wg)
             grads[3 * li: 3 * li + 3] = [dW, dgamma, dbeta]
             # data gradient into the previous layer (ReLU mask + its BN-backward partial sums)
             n_in = rec["n_in"]
@@ -620,6 +686,7 @@ class SparseEncoderFn(torch.autograd.Function):
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
                                                     None, _ffi.ptr(din), None, st), "rpc_spconv_dgrad")
                 dfeat = din
+        main.wait_stream(wg)    # the weight gradients are complete before autograd hands them on
         if tm_stage:
             stage_timer.TIMER.stop("sparse_bwd", e_stage, nbytes)
         ctx.L = None

@@ -346,74 +346,104 @@ class KernelTimer:
                     kernel=self.kernel, dtype=self.dtype)
 
 
-def _rulebooks(lib, enc, coors, n0, B, dev):
+class _RulebookPlan:
     """Every layer's rulebook on the encoder's 'rb' side stream: the submanifold neighbour lists (one
-    per indice key) and, for each strided conv, its output count (a host read: the output allocation
-    size), output coordinates and both neighbour maps. The chain depends on the coordinates only, so
-    it starts from the detector's coors_ready event — concurrently with the perturber — and the main
-    stream waits for each layer's event right before that layer's GEMM. Returns one dict per spec."""
-    main = torch.cuda.current_stream(dev)
-    side = enc.side_stream("rb", dev)
-    ready = enc.__dict__.pop("_coors_ready", None)
-    if ready is not None and ready[0] == coors.data_ptr():
-        side.wait_event(ready[1])
-    else:
-        side.wait_stream(main)
-    plan = []
-    made = []
-    with torch.cuda.stream(side):
-        st = _ffi.stream_of(coors)
-        rb = {}
-        cur_coors, cur_n = coors, n0
-        for sp in enc.specs:
-            ks = _ffi.int_arr(sp.ksize)
-            p = dict(n_in=cur_n, coors_in=cur_coors)
-            if sp.kind == "subm":
-                if sp.key not in rb:
+    per indice key) and, per strided conv, its output count, output coordinates and both neighbour maps.
+    The chain depends on the coordinates only, so it starts from the detector's coors_ready event —
+    concurrently with the perturber — and the main stream waits for each layer's event right before
+    that layer's GEMM. Issued lazily, one level ahead: a strided conv's output count (a host read: it
+    sizes the allocations) is read only when the forward reaches that layer, after the host has queued
+    the previous level's GEMMs, so the main stream computes while the host waits."""
+
+    def __init__(self, lib, enc, coors, n0, B, dev):
+        self.lib, self.enc, self.B, self.dev = lib, enc, B, dev
+        self.main = torch.cuda.current_stream(dev)
+        self.side = enc.side_stream("rb", dev)
+        ready = enc.__dict__.pop("_coors_ready", None)
+        if ready is not None and ready[0] == coors.data_ptr():
+            self.side.wait_event(ready[1])
+        else:
+            self.side.wait_stream(self.main)
+        coors.record_stream(self.side)
+        self.plan = [None] * len(enc.specs)
+        self.rb = {}
+        self.pending = None        # (layer, n_host, event, ws, gout) of the issued strided count
+        self.cur = (coors, n0)
+        self.next = 0              # first layer not yet issued
+        self._issue()
+
+    def _done(self, li, p, made):
+        ev = torch.cuda.Event()
+        ev.record(self.side)
+        p["ev"] = ev
+        self.plan[li] = p
+        for t in made:     # made on the side stream, used and freed on the main one
+            t.record_stream(self.main)
+
+    def _issue(self):
+        """Issue layers from self.next up to (not including) the next strided conv, then its count."""
+        lib, enc, dev, B = self.lib, self.enc, self.dev, self.B
+        with torch.cuda.stream(self.side):
+            st = _ffi.stream_of(self.cur[0])
+            while self.next < len(enc.specs):
+                li, sp = self.next, enc.specs[self.next]
+                cur_coors, cur_n = self.cur
+                if sp.kind != "subm":
+                    oshp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_out])
+                    wsb = lib.rpc_spconv_rulebook_workspace_size(cur_n, sp.K)
+                    ws = _ffi.workspace(wsb, dev)
+                    n_dev = torch.empty(1, dtype=torch.int32, device=dev)
+                    gout = enc.grid(sp.lvl_out, B, dev)
+                    _ffi.check(lib.rpc_spconv_rulebook_count(_ffi.ptr(cur_coors), cur_n, oshp, _ffi.int_arr(sp.ksize),
+                                                             _ffi.int_arr(sp.stride), _ffi.int_arr(sp.pad),
+                                                             _ffi.ptr(gout), _ffi.ptr(n_dev), _ffi.ptr(ws), wsb, st),
+                               "rpc_spconv_rulebook_count")
+                    n_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+                    n_host.copy_(n_dev, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(self.side)
+                    self.pending = (li, n_host, ev, ws, gout)
+                    return
+                made = []
+                if sp.key not in self.rb:
                     nbr = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
                     shp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_in])
-                    _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, ks,
+                    _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, _ffi.int_arr(sp.ksize),
                                                      _ffi.ptr(enc.grid(sp.lvl_in, B, dev)), _ffi.ptr(nbr), st),
                                "rpc_subm_rulebook")
-                    rb[sp.key] = nbr
+                    self.rb[sp.key] = nbr
                     made.append(nbr)
-                p.update(nbr=rb[sp.key], n_out=cur_n, coors_out=cur_coors)
-            else:
-                oshp = _ffi.int_arr((B,) + enc.shapes[sp.lvl_out])
-                sd, pd = _ffi.int_arr(sp.stride), _ffi.int_arr(sp.pad)
-                wsb = lib.rpc_spconv_rulebook_workspace_size(cur_n, sp.K)
-                ws = _ffi.workspace(wsb, dev)
-                n_dev = torch.empty(1, dtype=torch.int32, device=dev)
-                gout = enc.grid(sp.lvl_out, B, dev)
-                _ffi.check(lib.rpc_spconv_rulebook_count(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
-                                                         _ffi.ptr(n_dev), _ffi.ptr(ws), wsb, st),
-                           "rpc_spconv_rulebook_count")
-                n_host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-                n_host.copy_(n_dev, non_blocking=True)
-                ev_n = torch.cuda.Event()
-                ev_n.record(side)
-                ev_n.synchronize()
-                n_out = int(n_host[0])             # host read: the output row count (side stream only)
+                self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=self.rb[sp.key], n_out=cur_n,
+                                    coors_out=cur_coors), made)
+                self.next += 1
+
+    def get(self, li):
+        if self.plan[li] is None:
+            lj, n_host, ev, ws, gout = self.pending
+            assert lj == li, (lj, li)
+            lib, enc, dev, B = self.lib, self.enc, self.dev, self.B
+            sp = enc.specs[li]
+            cur_coors, cur_n = self.cur
+            ev.synchronize()
+            n_out = int(n_host[0])             # host read: the strided conv's output row count
+            with torch.cuda.stream(self.side):
+                st = _ffi.stream_of(cur_coors)
                 coors_out = torch.empty((n_out, 4), dtype=torch.int32, device=dev)
                 nbr_out = torch.empty((n_out, sp.K), dtype=torch.int32, device=dev)
                 nbr_in = torch.empty((cur_n, sp.K), dtype=torch.int32, device=dev)
-                _ffi.check(lib.rpc_spconv_rulebook_build(_ffi.ptr(cur_coors), cur_n, oshp, ks, sd, pd, _ffi.ptr(gout),
-                                                         n_out, _ffi.ptr(coors_out), _ffi.ptr(nbr_out),
-                                                         _ffi.ptr(nbr_in), _ffi.ptr(ws), st),
-                           "rpc_spconv_rulebook_build")
-                made += [coors_out, nbr_out, nbr_in]
-                p.update(nbr=nbr_out, nbr_in=nbr_in, n_out=n_out, coors_out=coors_out)
-                cur_coors, cur_n = coors_out, n_out
-            ev = torch.cuda.Event()
-            ev.record(side)
-            p["ev"] = ev
-            plan.append(p)
-    # made on the side stream, used and freed on the main one: the allocator must not recycle them
-    # before the main stream's work on them is done
-    for t in made:
-        t.record_stream(main)
-    coors.record_stream(side)
-    return plan
+                _ffi.check(lib.rpc_spconv_rulebook_build(_ffi.ptr(cur_coors), cur_n,
+                                                         _ffi.int_arr((B,) + enc.shapes[sp.lvl_out]),
+                                                         _ffi.int_arr(sp.ksize), _ffi.int_arr(sp.stride),
+                                                         _ffi.int_arr(sp.pad), _ffi.ptr(gout), n_out,
+                                                         _ffi.ptr(coors_out), _ffi.ptr(nbr_out), _ffi.ptr(nbr_in),
+                                                         _ffi.ptr(ws), st), "rpc_spconv_rulebook_build")
+            self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr_out, nbr_in=nbr_in, n_out=n_out,
+                                coors_out=coors_out), [coors_out, nbr_out, nbr_in])
+            self.pending = None
+            self.cur = (coors_out, n_out)
+            self.next = li + 1
+            self._issue()
+        return self.plan[li]
 
 
 class SparseEncoderFn(torch.autograd.Function):
@@ -441,13 +471,13 @@ class SparseEncoderFn(torch.autograd.Function):
             for li, tiles in zip(bl, _prep_bf16_weights(lib, [enc.specs[li] for li in bl], Ws, dev, st)):
                 wtiles[li] = tiles
         # rulebooks (and the strided layers' output counts, host reads) on a side stream, ahead of the GEMMs
-        plan = _rulebooks(lib, enc, coors, feats.shape[0], B, dev)
+        plan = _RulebookPlan(lib, enc, coors, feats.shape[0], B, dev)
         main = torch.cuda.current_stream(dev)
         for li, (sp, m) in enumerate(zip(enc.specs, mods)):
             W = params[3 * li]
             gamma, beta = params[3 * li + 1], params[3 * li + 2]
             bnm = m[1]
-            p = plan[li]
+            p = plan.get(li)
             rec = dict(spec=sp, n_in=p["n_in"], src=src, src_bn=src_bn, coors_in=p["coors_in"], nbr=p["nbr"],
                        n_out=p["n_out"], coors_out=p["coors_out"])
             if "nbr_in" in p:

@@ -215,6 +215,24 @@ class SparseEncoder(nn.Module):
             s = self._side_streams[key] = torch.cuda.Stream(device)
         return s
 
+    def prepare(self, coors: torch.Tensor, batch_size: int, after=None, consumer=None) -> None:
+        """Build every rulebook of a future forward over `coors` now (the trainer's batch prefetch calls
+        this during the previous step): the four strided output counts are read here, while the GPU
+        still runs the current step's queued work, so the forward that uses them issues its GEMMs
+        without a single host read. The forward picks the plan up when it sees the same coordinates."""
+        if not coors.is_cuda:
+            return
+        lib = _ffi.load()
+        coors = coors.to(torch.int32).contiguous()
+        plan = _RulebookPlan(lib, self, coors, coors.shape[0], int(batch_size), coors.device, after=after,
+                             consumer=consumer)
+        for li in range(len(self.specs)):
+            plan.get(li)
+        prepared = self.__dict__.setdefault("_prepared", {})
+        while len(prepared) >= 2:          # the batch in flight and the next one; drop older plans
+            prepared.pop(next(iter(prepared)))
+        prepared[plan.key] = plan
+
     def coors_ready(self, coors: torch.Tensor) -> None:
         """Called by the detector as soon as the voxel coordinates are queued, before the perturber: the
         rulebooks (which depend on the coordinates only) are then built on a side stream concurrently
@@ -355,15 +373,22 @@ class _RulebookPlan:
     sizes the allocations) is read only when the forward reaches that layer, after the host has queued
     the previous level's GEMMs, so the main stream computes while the host waits."""
 
-    def __init__(self, lib, enc, coors, n0, B, dev):
+    def __init__(self, lib, enc, coors, n0, B, dev, after=None, consumer=None):
+        """after: an event the coordinates are complete behind (default: the detector's coors_ready event,
+        else everything queued on the current stream); consumer: the stream the GEMMs run on (default:
+        the current stream)."""
         self.lib, self.enc, self.B, self.dev = lib, enc, B, dev
-        self.main = torch.cuda.current_stream(dev)
+        self.main = consumer if consumer is not None else torch.cuda.current_stream(dev)
         self.side = enc.side_stream("rb", dev)
+        self.key = (coors.data_ptr(), int(n0), int(B))
+        self.coors0 = coors     # held: while this plan exists no other tensor can own that address
         ready = enc.__dict__.pop("_coors_ready", None)
-        if ready is not None and ready[0] == coors.data_ptr():
+        if after is not None:
+            self.side.wait_event(after)
+        elif ready is not None and ready[0] == coors.data_ptr():
             self.side.wait_event(ready[1])
         else:
-            self.side.wait_stream(self.main)
+            self.side.wait_stream(torch.cuda.current_stream(dev))
         coors.record_stream(self.side)
         self.plan = [None] * len(enc.specs)
         self.rb = {}
@@ -471,7 +496,11 @@ class SparseEncoderFn(torch.autograd.Function):
             for li, tiles in zip(bl, _prep_bf16_weights(lib, [enc.specs[li] for li in bl], Ws, dev, st)):
                 wtiles[li] = tiles
         # rulebooks (and the strided layers' output counts, host reads) on a side stream, ahead of the GEMMs
-        plan = _RulebookPlan(lib, enc, coors, feats.shape[0], B, dev)
+        plan = enc.__dict__.get("_prepared", {}).pop((coors.data_ptr(), feats.shape[0], B), None)
+        if plan is None or plan.main != torch.cuda.current_stream(dev):
+            plan = _RulebookPlan(lib, enc, coors, feats.shape[0], B, dev)
+        else:
+            enc.__dict__.pop("_coors_ready", None)
         main = torch.cuda.current_stream(dev)
         for li, (sp, m) in enumerate(zip(enc.specs, mods)):
             W = params[3 * li]

@@ -26,6 +26,10 @@ from .registry import MODELS
 from .voxelnet import second_kitti_cfg, second_kitti_strong_cfg
 
 
+# Trainer._prefetch also builds the next batch's sparse rulebooks (RPC_PREFETCH_RULEBOOKS=0: off, A/B)
+PREFETCH_RULEBOOKS = os.environ.get("RPC_PREFETCH_RULEBOOKS", "1") != "0"
+
+
 def build_model(cfg: dict):
     return MODELS.build(cfg)
 
@@ -222,7 +226,15 @@ class Trainer:
         # non_blocking pinned copy): order the side stream after everything queued there so far
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(self._side):
-            self._pending = (points, vl.voxelize_frames_deferred(points))
+            pend = vl.voxelize_frames_deferred(points)
+        self._pending = (points, pend)
+        # and that batch's sparse rulebooks: their host reads (V, four strided output counts) happen now,
+        # while the GPU still runs this step's queued work, so next step's sparse forward issues its
+        # GEMMs without waiting on the GPU
+        me = getattr(self.module, "middle_encoder", None)
+        if PREFETCH_RULEBOOKS and me is not None and hasattr(me, "prepare"):
+            V = pend.count()
+            me.prepare(pend.t[1][:V], len(points), after=pend.ev, consumer=torch.cuda.current_stream(self.device))
 
     def step_batch(self, batch, gt):
         """The step after voxelisation, as mmengine runs it: model.train_step(data, optim_wrapper)

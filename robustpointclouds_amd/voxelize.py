@@ -85,6 +85,11 @@ class PendingVoxels:
         self.ev = torch.cuda.Event()
         self.ev.record(torch.cuda.current_stream(voxels.device))
 
+    def count(self) -> int:
+        """V (a host read: waits for the voxelisation kernels only)."""
+        self.ev.synchronize()
+        return int(self.host[0])
+
     def result(self, consumer=None):
         voxels, coors, num_points, voxel_num = self.t
         if consumer is not None:

@@ -168,6 +168,7 @@ class Trainer:
         self.last_log = None
         self._side = None        # side stream of the batch prefetch
         self._pending = None     # (points list, PendingVoxels) of the prefetched next batch
+        self._next = None        # (points, ready event) of the next batch, prefetched in update_params
 
     @staticmethod
     def _select_engines(model, bf16):
@@ -190,14 +191,16 @@ class Trainer:
             if hasattr(h, "before_train_epoch"):
                 h.before_train_epoch(self)
 
-    def train_step(self, points, gt, next_points=None):
+    def train_step(self, points, gt, next_points=None, next_ready=None):
         """points: list of [Ni, 4] cuda tensors; gt: dict(gt_boxes [B, M, 7], gt_labels [B, M]).
 
-        next_points (optional): the next step's points, already complete on the device. Their hard
-        voxelisation is queued on a side stream now, concurrently with this step, and its voxel count
-        is read at the next step, so that read no longer drains the training stream (the next step's
-        kernels queue behind this step's backward instead of starting on an idle GPU). Same kernels,
-        same results: only where the voxelisation is queued changes."""
+        next_points (optional): the next step's points. Their hard voxelisation and sparse rulebooks
+        are queued on side streams during this step — after its forward has been issued, so the host
+        reads they need (the voxel count, the strided convolutions' output counts) block the host while
+        the GPU still has this step's work queued — and the next step's forward starts with both ready.
+        next_ready (optional): an event after which next_points are complete (default: everything queued
+        on the training stream before this step). Same kernels, same results: only where and when the
+        voxelisation and the rulebooks are queued changes."""
         m = self.module
         if not m.training:
             m.train()
@@ -209,11 +212,23 @@ class Trainer:
         else:   # voxelised by the model's data_preprocessor inside train_step, as mmengine does
             batch = dict(points=points)
         batch["batch_size"] = len(points)
-        if next_points is not None:
-            self._prefetch(next_points)
-        return self.step_batch(batch, gt)
+        self._next = None
+        if next_points is not None and self.device.type == "cuda":
+            if next_ready is None:
+                next_ready = torch.cuda.Event()
+                next_ready.record(torch.cuda.current_stream(self.device))
+            self._next = (next_points, next_ready)
+        out = self.step_batch(batch, gt)
+        self._issue_prefetch()      # no-op when update_params already issued it
+        return out
 
-    def _prefetch(self, points):
+    def _issue_prefetch(self):
+        nxt = getattr(self, "_next", None)
+        self._next = None
+        if nxt is not None:
+            self._prefetch(*nxt)
+
+    def _prefetch(self, points, after):
         vl = getattr(getattr(self.module, "data_preprocessor", None), "voxel_layer", None)
         if vl is None or not hasattr(vl, "voxelize_frames_deferred") or self.device.type != "cuda":
             return
@@ -223,8 +238,8 @@ class Trainer:
         for p in points:    # read on the side stream: keep the allocator from reusing them early
             p.record_stream(self._side)
         # the points may still be in flight on the training stream (GpuTrainAugment output, a
-        # non_blocking pinned copy): order the side stream after everything queued there so far
-        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        # non_blocking pinned copy): order the side stream after the caller's readiness event
+        self._side.wait_event(after)
         with torch.cuda.stream(self._side):
             pend = vl.voxelize_frames_deferred(points)
         self._pending = (points, pend)
@@ -266,7 +281,9 @@ class Trainer:
         return torch.autocast("cuda", dtype=torch.bfloat16) if self.bf16 else contextlib.nullcontext()
 
     def update_params(self, loss):
-        """OptimWrapper.update_params: backward, clip_grad (max_norm 0.5) + AdamW, zero_grad."""
+        """OptimWrapper.update_params: backward, clip_grad (max_norm 0.5) + AdamW, zero_grad. The batch
+        prefetch (train_step next_points) is issued here, between this step's forward and backward."""
+        self._issue_prefetch()
         loss.backward()
         if isinstance(self.opt, ClipAdamW):
             self._grad_norm = self.opt.step()[0]

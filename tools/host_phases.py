@@ -62,8 +62,10 @@ def main():
     model = trainer.make_kitti_model(num_classes=a.classes, device=dev, epoch=3)
     tr = trainer.Trainer(model, bf16=True, device=dev)
     data = bench._batches(4, 6, 0, dev, a.classes)
+    ready = torch.cuda.Event()
+    ready.record()
     for i in range(8):
-        tr.train_step(*data[i % 4], next_points=data[(i + 1) % 4][0])
+        tr.train_step(*data[i % 4], next_points=data[(i + 1) % 4][0], next_ready=ready)
     torch.cuda.synchronize()
     for cls, tag in ((perturb.PerturbVoxelsFn, "perturber"), (sparse_encoder.SparseEncoderFn, "sparse"),
                      (dense_bev.BackboneFn, "second"), (dense_bev.NeckFn, "fpn"), (anchor_head.HeadLossFn, "head_loss"),
@@ -80,7 +82,7 @@ def main():
     N.clear()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        tr.train_step(*data[i % 4], next_points=data[(i + 1) % 4][0])
+        tr.train_step(*data[i % 4], next_points=data[(i + 1) % 4][0], next_ready=ready)
     t1 = time.perf_counter()
     torch.cuda.synchronize()
     t2 = time.perf_counter()

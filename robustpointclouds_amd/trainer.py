@@ -195,7 +195,7 @@ class Trainer:
         """points: list of [Ni, 4] cuda tensors; gt: dict(gt_boxes [B, M, 7], gt_labels [B, M]).
 
         next_points (optional): the next step's points. Their hard voxelisation and sparse rulebooks
-        are queued on side streams during this step — after its forward has been issued, so the host
+        are queued on side streams during this step — after its backward has been issued, so the host
         reads they need (the voxel count, the strided convolutions' output counts) block the host while
         the GPU still has this step's work queued — and the next step's forward starts with both ready.
         next_ready (optional): an event after which next_points are complete (default: everything queued
@@ -282,9 +282,10 @@ class Trainer:
 
     def update_params(self, loss):
         """OptimWrapper.update_params: backward, clip_grad (max_norm 0.5) + AdamW, zero_grad. The batch
-        prefetch (train_step next_points) is issued here, between this step's forward and backward."""
-        self._issue_prefetch()
+        prefetch (train_step next_points) is issued here, right after the backward: its host reads
+        then block while the GPU still has the whole backward queued."""
         loss.backward()
+        self._issue_prefetch()
         if isinstance(self.opt, ClipAdamW):
             self._grad_norm = self.opt.step()[0]
         else:

@@ -250,6 +250,41 @@ size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co)
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
                           float* dW, void* workspace, size_t workspace_bytes, void* stream);
 
+/* ---- a6 runtime: the whole SparseEncoder backward in one call (csrc/sparse_exec.hip).
+ * Replaces the per-layer backward of upstream mmdet3d SparseEncoder (adversarial_voxelnet.py:141;
+ * configs/adversarial/…-3class.py:19-23) over spconv: one entry per sparse conv in forward order, with
+ * the forward's saved tensors; the weight / BatchNorm-affine gradients are written to dW / dgamma / dbeta.
+ * The launches are those of the per-layer entry points above, in the same order; weight gradients go to
+ * wgrad_stream (NULL or == stream: the main stream) behind one event per layer and are joined back into
+ * `stream` before the call returns. Temporaries come from `workspace` (no allocation). */
+typedef struct {
+  int kind;              /* 0 = submanifold (SubMConv3d), 1 = strided (SparseConv3d) */
+  int ci, co, kvol;
+  int n_in, n_out;
+  int bf16;              /* bf16 MFMA path (perf mode, layers >= 1); 0 = fp32 */
+  int mat;               /* output materialised as rows (basicblock output / identity) */
+  int res;               /* layer whose output is this block's identity, or -1 */
+  const int* nbr;        /* [n_out][kvol] */
+  const int* nbr_in;     /* strided: [n_in][kvol] */
+  const float* z;        /* [n_out][co] pre-BatchNorm output */
+  const float* bn;       /* [4*co] forward scale, beta, mean, invstd */
+  const float* out;      /* mat: [n_out][co] */
+  const void* h_in;      /* bf16 layers: bf16 input rows [n_in][round8(ci)] */
+  const float* src;      /* fp32 layers: input rows [n_in][ci] */
+  const float* src_bn;   /* fp32 layers: BatchNorm params of src (folded into its gather) or NULL */
+  const float* W;        /* [kvol][ci][co] */
+  const float* gamma;
+  const float* beta;
+  const void* btd;       /* bf16 layers: data-gradient weight tiles (rpc_spconv_prep_weight_bf16, dgrad 1) */
+  float* dW;
+  float* dgamma;
+  float* dbeta;
+} RpcSparseLayer;
+size_t rpc_sparse_backward_workspace_size(const RpcSparseLayer* layers, int nlayers);
+int rpc_sparse_backward(const RpcSparseLayer* layers, int nlayers, const void* grad_dense, const int* coors_last,
+                        const int* shape /* B,D,H,W */, int flags, float* dfeat /* [n_in of layer 0][ci] or NULL */,
+                        void* workspace, size_t workspace_bytes, void* stream, void* wgrad_stream);
+
 
 /* ---- a7 perf mode: dense BEV backbone / neck (SECOND + SECONDFPN) on bf16 MFMA, NHWC images.
  * Replaces the Conv2d/ConvTranspose2d + BatchNorm2d + ReLU stacks of upstream mmdet3d

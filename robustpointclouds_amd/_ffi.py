@@ -84,6 +84,16 @@ class RpcSpconvWprep(C.Structure):
                 ("dgrad", C.c_int)]
 
 
+class RpcSparseLayer(C.Structure):
+    """include/rpc_hip.h RpcSparseLayer (one sparse conv of the rpc_sparse_backward layer table)."""
+    _fields_ = [("kind", C.c_int), ("ci", C.c_int), ("co", C.c_int), ("kvol", C.c_int), ("n_in", C.c_int),
+                ("n_out", C.c_int), ("bf16", C.c_int), ("mat", C.c_int), ("res", C.c_int),
+                ("nbr", C.c_void_p), ("nbr_in", C.c_void_p), ("z", C.c_void_p), ("bn", C.c_void_p),
+                ("out", C.c_void_p), ("h_in", C.c_void_p), ("src", C.c_void_p), ("src_bn", C.c_void_p),
+                ("W", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("btd", C.c_void_p),
+                ("dW", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p)]
+
+
 class RpcCenterCfg(C.Structure):
     """include/rpc_hip.h RpcCenterCfg."""
     _fields_ = [("B", C.c_int), ("H", C.c_int), ("W", C.c_int), ("ntasks", C.c_int), ("ncls_total", C.c_int),
@@ -132,6 +142,8 @@ SIGNATURES = {
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_wgrad_bf16": (i32, [vp, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
+    "rpc_sparse_backward_workspace_size": (sz, [vp, i32]),
+    "rpc_sparse_backward": (i32, [vp, i32, vp, vp, ip, i32, vp, vp, sz, vp, vp]),
     "rpc_dense_conv": (i32, [i32, vp, i32, i32, vp, i32, vp, i32, i32, i32, vp, ip, ip, ip, vp]),
     "rpc_dense_conv_blocks": (i32, [i32, ip]),
     "rpc_dense_conv_s1_kernel": (i32, [i32, i32, ip]),

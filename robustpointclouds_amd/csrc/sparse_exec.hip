@@ -1,0 +1,187 @@
+// a6 runtime: the SparseEncoder backward as ONE host call (rpc_sparse_backward).
+//
+// The backward of upstream mmdet3d SparseEncoder (12 sparse convs, SubMConv3d / SparseConv3d +
+// BatchNorm1d + ReLU, and the SparseBasicBlock residuals of the basicblock variant) walks the layers
+// in reverse: dense-BEV gradient gather, per layer the BatchNorm-backward finalize, the weight gradient
+// and the data gradient into the layer below (its ReLU mask and BatchNorm-backward partial sums fused
+// into the data-gradient epilogue). Issued from Python that is ~10 allocations, ~6 C-ABI calls, two
+// stream switches and their events per layer — about 1.2 ms of host time per step, more than the GPU
+// time of the kernels it issues, so the GPU waited on the host. Here the same launches, with the same
+// arguments in the same order, come from one C++ loop over a layer table: temporaries are carved out of
+// one caller-owned workspace (a bump arena, nothing freed during the call, so the side stream never
+// races an allocator), and the weight gradients go to the caller's second stream behind one event per
+// layer, joined back into the main stream before returning. Same kernels, same order, same bits as the
+// Python loop in sparse_encoder.py (which remains the path for per-kernel timing / debugging).
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <vector>
+
+#include "common.h"
+#include "rpc_hip.h"
+
+namespace {
+
+constexpr int BM = 64;   // rows per BatchNorm partial row (rpc_spconv_gemm_blocks)
+
+inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+inline int r8(int c) { return (c + 7) / 8 * 8; }
+
+struct Arena {
+  char* base;
+  size_t cap, off;
+  bool dry;
+  void* take(size_t bytes) {
+    off = (off + 255) & ~(size_t)255;
+    void* p = dry ? nullptr : base + off;
+    off += bytes;
+    return p;
+  }
+  bool ok() const { return dry || off <= cap; }
+};
+
+// events of the main -> weight-gradient stream hand-offs, reused across calls (re-recording an event
+// after a stream has been told to wait on it is safe: the wait captured the earlier record)
+std::vector<hipEvent_t> g_events;
+hipEvent_t event_at(size_t i) {
+  while (g_events.size() <= i) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
+    g_events.push_back(e);
+  }
+  return g_events[i];
+}
+
+int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coors_last, const int* shape, int flags,
+        float* dfeat, Arena& A, hipStream_t st, hipStream_t wg) {
+#define CHK(x)                 \
+  do {                         \
+    if (!A.dry) {              \
+      int rc__ = (x);          \
+      if (rc__) return rc__;   \
+    }                          \
+  } while (0)
+  const RpcSparseLayer& last = L[nl - 1];
+  int n = last.n_out, C = last.co;
+  float* dy = (float*)A.take(sizeof(float) * (size_t)n * C);
+  int nblk = cdiv(n, BM) > 0 ? cdiv(n, BM) : 1;
+  float* part = (float*)A.take(sizeof(float) * (size_t)nblk * 2 * C);
+  CHK(rpc_dense_to_sparse_grad(grad_dense, last.z, last.bn, coors_last, n, C, shape, flags, dy, part, st));
+  // gradient contributions to materialised outputs (block outputs and their identities)
+  std::vector<std::vector<const float*>> G(nl);
+  const bool split = wg != nullptr && wg != st;
+  for (int li = nl - 1; li >= 0; --li) {
+    const RpcSparseLayer& l = L[li];
+    const int n_out = l.n_out;
+    if (l.mat) {
+      if (G[li].empty()) return RPC_ERR_ARG;
+      dy = (float*)A.take(sizeof(float) * (size_t)n_out * l.co);
+      nblk = cdiv(n_out, BM) > 0 ? cdiv(n_out, BM) : 1;
+      part = (float*)A.take(sizeof(float) * (size_t)nblk * 2 * l.co);
+      CHK(rpc_sparse_res_backward(G[li][0], G[li].size() > 1 ? G[li][1] : nullptr, l.out, l.z, l.bn, n_out, l.co, dy,
+                                  part, st));
+      if (l.res >= 0) G[l.res].push_back(dy);
+    }
+    // BatchNorm backward statistics -> bnb, dgamma, dbeta
+    float* bnb = (float*)A.take(sizeof(float) * 5 * (size_t)l.co);
+    CHK(rpc_bn_finalize(part, nblk, l.co, n_out, 1, l.gamma, l.beta, 0.0f, 0.0f, nullptr, nullptr, l.bn, bnb, l.dgamma,
+                        l.dbeta, nullptr, st));
+    // weight gradient, on the second stream (it reads only this layer's dz / input rows)
+    void* dzb = nullptr;
+    if (l.bf16) {
+      dzb = A.take(2 * (size_t)n_out * r8(l.co));
+      CHK(rpc_bnbwd_to_bf16_rows(dy, l.z, bnb, n_out, l.co, dzb, st));
+    }
+    hipStream_t sw = split ? wg : st;
+    if (split && !A.dry) {
+      hipEvent_t e = event_at((size_t)li);
+      if (!e) return RPC_ERR_HIP;
+      RPC_CHECK(hipEventRecord(e, st));
+      RPC_CHECK(hipStreamWaitEvent(wg, e, 0));
+    }
+    const size_t wsz = l.bf16 ? rpc_spconv_wgrad_bf16_workspace_size(n_out, l.kvol, l.ci, l.co)
+                              : rpc_spconv_wgrad_workspace_size(n_out, l.kvol, l.ci, l.co);
+    void* wsw = A.take(wsz);
+    if (l.bf16)
+      CHK(rpc_spconv_wgrad_bf16(l.h_in, l.ci, l.nbr, l.kvol, n_out, dzb, l.co, l.dW, wsw, wsz, sw));
+    else
+      CHK(rpc_spconv_wgrad(l.src, l.src_bn, l.ci, l.nbr, l.kvol, n_out, dy, l.z, bnb, l.co, l.dW, wsw, wsz, sw));
+    // data gradient into the layer below (its ReLU mask + BatchNorm-backward partial sums)
+    const int* mp = l.kind == 0 ? l.nbr : l.nbr_in;
+    const int rev = l.kind == 0 ? 1 : 0;
+    const int n_in = l.n_in;
+    if (li > 0 && L[li - 1].mat) {
+      float* din = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
+      if (l.bf16)
+        CHK(rpc_spconv_gemm_bf16(dzb, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, nullptr, nullptr, nullptr, 2, st));
+      else
+        CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, din, nullptr, st));
+      G[li - 1].push_back(din);
+    } else if (li > 0) {
+      const RpcSparseLayer& prev = L[li - 1];
+      float* din = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
+      nblk = cdiv(n_in, BM) > 0 ? cdiv(n_in, BM) : 1;
+      part = (float*)A.take(sizeof(float) * (size_t)nblk * 2 * l.ci);
+      if (l.bf16)
+        CHK(rpc_spconv_gemm_bf16(dzb, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part, 1, st));
+      else
+        CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, prev.z, prev.bn, din, part, st));
+      dy = din;
+    } else if (dfeat) {
+      if (l.bf16)
+        CHK(rpc_spconv_gemm_bf16(dzb, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, dfeat, nullptr, nullptr, nullptr, 2,
+                                 st));
+      else
+        CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, dfeat, nullptr,
+                             st));
+    }
+  }
+  if (split && !A.dry) {   // the weight gradients are complete before the main stream goes on
+    hipEvent_t e = event_at((size_t)nl);
+    if (!e) return RPC_ERR_HIP;
+    RPC_CHECK(hipEventRecord(e, wg));
+    RPC_CHECK(hipStreamWaitEvent(st, e, 0));
+  }
+  return A.ok() ? RPC_OK : RPC_ERR_WORKSPACE;
+#undef CHK
+}
+
+int check_layers(const RpcSparseLayer* L, int nl) {
+  if (!L || nl < 1) return RPC_ERR_ARG;
+  for (int i = 0; i < nl; ++i) {
+    const RpcSparseLayer& l = L[i];
+    if (l.n_in < 0 || l.n_out < 0 || l.ci < 1 || l.co < 1 || l.kvol < 1 || l.res >= i || !l.nbr || !l.z || !l.bn ||
+        !l.W || !l.gamma || !l.beta || !l.dW || !l.dgamma || !l.dbeta || (l.kind != 0 && !l.nbr_in) ||
+        (l.mat && !l.out) || (l.bf16 && (!l.h_in || !l.btd)) || (!l.bf16 && !l.src))
+      return RPC_ERR_ARG;
+    if (i > 0 && L[i - 1].n_out != l.n_in) return RPC_ERR_ARG;
+  }
+  return RPC_OK;
+}
+
+}  // namespace
+
+extern "C" size_t rpc_sparse_backward_workspace_size(const RpcSparseLayer* layers, int nlayers) {
+  if (check_layers(layers, nlayers)) return 0;
+  Arena A{nullptr, 0, 0, true};
+  int shape[4] = {1, 1, 1, 1};
+  if (run(layers, nlayers, nullptr, nullptr, shape, 0, nullptr, A, nullptr, nullptr)) return 0;
+  return A.off + 256;
+}
+
+extern "C" int rpc_sparse_backward(const RpcSparseLayer* layers, int nlayers, const void* grad_dense,
+                                   const int* coors_last, const int* shape, int flags, float* dfeat, void* workspace,
+                                   size_t workspace_bytes, void* stream, void* wgrad_stream) {
+  int rc = check_layers(layers, nlayers);
+  if (rc) return rc;
+  if (!grad_dense || !coors_last || !shape || !workspace) return RPC_ERR_ARG;
+  Arena A{(char*)workspace, workspace_bytes, 0, false};
+  // dry pass first: a workspace that is too small fails before anything is launched
+  {
+    Arena D{nullptr, 0, 0, true};
+    if (run(layers, nlayers, grad_dense, coors_last, shape, flags, dfeat, D, nullptr, nullptr)) return RPC_ERR_ARG;
+    if (D.off > workspace_bytes) return RPC_ERR_WORKSPACE;
+  }
+  return run(layers, nlayers, grad_dense, coors_last, shape, flags, dfeat, A, (hipStream_t)stream,
+             (hipStream_t)wgrad_stream);
+}

@@ -49,6 +49,8 @@ class _Spec:
 
 # rulebooks / sparse weight gradients on side streams (SparseEncoder.side_stream)
 SIDE_STREAMS = os.environ.get("RPC_SPARSE_STREAMS", "1") != "0"
+# the backward as one native call (csrc/sparse_exec.hip rpc_sparse_backward); 0: the per-layer Python loop
+NATIVE_BACKWARD = os.environ.get("RPC_SPARSE_NATIVE", "1") != "0"
 
 
 def _t3(v):
@@ -599,6 +601,10 @@ class SparseEncoderFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gdense):
+        enc = ctx.enc
+        timed = enc.timer is not None and enc.timer.enabled
+        if NATIVE_BACKWARD and enc.debug is None and not timed:
+            return _native_backward(ctx, gdense)
         lib = _ffi.load()
         L = ctx.L
         dev = gdense.device
@@ -751,3 +757,69 @@ class SparseEncoderFn(torch.autograd.Function):
         ctx.L = None
         ctx.enc = None
         return (dfeat, None, None, None, *grads)
+
+
+def _native_backward(ctx, gdense):
+    """SparseEncoderFn.backward as ONE C-ABI call (rpc_sparse_backward, csrc/sparse_exec.hip): the same
+    kernels with the same arguments in the same order as the per-layer loop above, issued from C++
+    (the loop's host time exceeded the GPU time of its kernels). Gradients of all layers land in one
+    flat buffer (views returned to autograd)."""
+    lib = _ffi.load()
+    L = ctx.L
+    dev = gdense.device
+    main = torch.cuda.current_stream(dev)
+    st = _ffi.stream_of(gdense)
+    tm_stage = stage_timer.active()
+    e_stage = stage_timer.TIMER.start() if tm_stage else None
+    B, C, D, H, Wd = ctx.shape
+    flags = ctx.dense_flags
+    dt = torch.bfloat16 if flags & 2 else torch.float32
+    gd = gdense.to(dt).contiguous(memory_format=torch.channels_last) if flags & 1 else gdense.to(dt).contiguous()
+    nl = len(L)
+    sizes = []
+    for rec in L:
+        sizes += [rec["W"].numel(), rec["gamma"].numel(), rec["beta"].numel()]
+    flat = torch.empty(sum(sizes), dtype=torch.float32, device=dev)
+    parts = torch.split(flat, sizes)
+    grads = []
+    table = (_ffi.RpcSparseLayer * nl)()
+    vp = lambda t: None if t is None else t.data_ptr()
+    for li, rec in enumerate(L):
+        sp = rec["spec"]
+        dW = parts[3 * li].view(rec["W"].shape)
+        dg, db = parts[3 * li + 1], parts[3 * li + 2]
+        grads += [dW, dg, db]
+        bf = bool(rec["bf16"])
+        if bf and rec.get("btd") is None:
+            btd = torch.empty(lib.rpc_spconv_bf16_weight_elems(sp.K, sp.ci, sp.co, 1), dtype=torch.bfloat16, device=dev)
+            _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(rec["W"]), sp.K, sp.ci, sp.co, 1, _ffi.ptr(btd), st),
+                       "rpc_spconv_prep_weight_bf16")
+            rec["btd"] = btd
+        table[li] = _ffi.RpcSparseLayer(
+            0 if sp.kind == "subm" else 1, sp.ci, sp.co, sp.K, rec["n_in"], rec["n_out"], int(bf), int(sp.mat),
+            sp.res, vp(rec["nbr"]), vp(rec.get("nbr_in")), vp(rec["z"]), vp(rec["bn"]), vp(rec.get("out")),
+            vp(rec["h_in"]) if bf else None, None if bf else vp(rec["src"]), None if bf else vp(rec["src_bn"]),
+            vp(rec["W"]), vp(rec["gamma"]), vp(rec["beta"]), vp(rec.get("btd")) if bf else None,
+            dW.data_ptr(), dg.data_ptr(), db.data_ptr())
+    dfeat = (torch.empty((L[0]["n_in"], L[0]["spec"].ci), dtype=torch.float32, device=dev)
+             if ctx.needs_input_grad[0] else None)
+    wsb = lib.rpc_sparse_backward_workspace_size(table, nl)
+    if wsb == 0:
+        raise RuntimeError("rpc_sparse_backward_workspace_size: inconsistent layer table")
+    ws = _ffi.workspace(wsb, dev)
+    wg = ctx.enc.side_stream("wg", dev)
+    _ffi.check(lib.rpc_sparse_backward(table, nl, _ffi.ptr(gd), _ffi.ptr(L[-1]["coors_out"]),
+                                       _ffi.int_arr((B, D, H, Wd)), flags, _ffi.ptr(dfeat), _ffi.ptr(ws), wsb, st,
+                                       C_stream(wg)), "rpc_sparse_backward")
+    if tm_stage:
+        stage_timer.TIMER.stop("sparse_bwd", e_stage, _sparse_bytes(L, ctx.bf16, gdense.numel() * (2 if flags & 2 else 4),
+                                                                      backward=True))
+    ctx.L = None
+    ctx.enc = None
+    return (dfeat, None, None, None, *grads)
+
+
+def C_stream(s):
+    import ctypes
+    return ctypes.c_void_p(s.cuda_stream)
+

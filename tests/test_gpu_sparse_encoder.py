@@ -164,3 +164,39 @@ def test_bf16_perf_mode_config_size():
     print(f"B=6 bf16 sparse encoder: forward rel {rel:.3e}, dfeat cos {cf:.4f}, worst dW cos {min(cw):.4f}")
     assert rel < 3e-2, rel
     assert cf >= 0.95 and min(cw) >= 0.95, (cf, cw)
+
+
+@pytest.mark.parametrize("bf16,basic", [(True, False), (False, False), (True, True), (False, True)])
+def test_native_backward_bit_identical_to_layer_loop(bf16, basic):
+    """rpc_sparse_backward (one C++ loop, weight gradients on the side stream) issues the same kernels
+    with the same arguments in the same order as the per-layer Python loop: identical bits for the
+    input gradient and every parameter gradient, conv_module and basicblock encoders, both precisions."""
+    import robustpointclouds_amd.sparse_encoder as se
+    dev = torch.device("cuda")
+    feats, coors = _inputs(2, 2, seed=3)
+    if basic:
+        kw = dict(output_channels=128, encoder_channels=((16, 16, 32), (32, 32, 64), (64, 64, 128), (128, 128)),
+                  encoder_paddings=((0, 0, 1), (0, 0, 1), (0, 0, [0, 1, 1]), (1, 1)), block_type="basicblock")
+    else:
+        kw = {}
+    torch.manual_seed(0)
+    enc = SparseEncoder(4, [41, 1600, 1408], **kw).to(dev)
+    enc.bf16 = enc.dense_bf16 = bf16
+    enc.dense_nhwc = bf16
+    G = torch.randn((2, enc.output_channels * 2, 200, 176), generator=torch.Generator().manual_seed(2)).to(dev)
+    res = {}
+    saved = se.NATIVE_BACKWARD
+    try:
+        for native in (False, True):
+            se.NATIVE_BACKWARD = native
+            for p in enc.parameters():
+                p.grad = None
+            f = torch.from_numpy(feats).to(dev).requires_grad_(True)
+            out = enc(f, torch.from_numpy(coors).to(dev), 2)
+            (out.float() * G).sum().backward()
+            torch.cuda.synchronize()
+            res[native] = [f.grad.clone()] + [p.grad.clone() for p in enc.parameters()]
+    finally:
+        se.NATIVE_BACKWARD = saved
+    for i, (a, b) in enumerate(zip(res[False], res[True])):
+        assert torch.equal(a, b), i

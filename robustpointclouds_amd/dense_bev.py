@@ -355,51 +355,8 @@ def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
     return y, rec, Ho, Wo
 
 
-# weight gradients on a side stream, concurrent with the next (lower) layer's BatchNorm-backward passes
-# (HBM-bound) and data gradient; RPC_DENSE_WG_STREAM=0 keeps them on the main stream (A/B)
-WG_STREAM = os.environ.get("RPC_DENSE_WG_STREAM", "1") != "0"
-_WG_STREAMS = {}
-
-
-class _WgScope:
-    """Fork / join of the weight-gradient side stream for one backward node. Works inside a HIP graph
-    capture (the side stream joins the capture through the fork event). Every tensor the side stream
-    reads or writes stays referenced here until the join, so neither the caching allocator (eager) nor
-    the capture's private pool (graphs) can hand its storage to a later allocation of the main stream
-    while the side stream may still use it."""
-
-    def __init__(self, dev):
-        self.main = torch.cuda.current_stream(dev)
-        self.side = None
-        if WG_STREAM:
-            s = _WG_STREAMS.get(str(dev))
-            if s is None:
-                s = _WG_STREAMS[str(dev)] = torch.cuda.Stream(dev)
-            self.side = s
-        self.keep = []
-
-    def stream(self, *uses):
-        """The stream for the next weight gradient (after everything queued on main so far)."""
-        if self.side is None:
-            return _ffi.stream_of(uses[0])
-        ev = torch.cuda.Event()
-        ev.record(self.main)
-        self.side.wait_event(ev)
-        self.keep.extend(uses)
-        import ctypes
-        return ctypes.c_void_p(self.side.cuda_stream)
-
-    def join(self):
-        if self.side is not None:
-            ev = torch.cuda.Event()
-            ev.record(self.side)
-            self.main.wait_event(ev)
-        self.keep = []
-
-
-def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False, wg=None):
-    """BN+ReLU backward, weight gradient (on wg's side stream when given) and (optionally) data gradient
-    of one layer."""
+def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False):
+    """BN+ReLU backward, weight gradient and (optionally) data gradient of one layer."""
     lib = eng.lib
     L = rec["L"]
     Mo, co, ci = rec["Mo"], L.co, L.ci
@@ -424,9 +381,8 @@ def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
     wsz = eng.wgrad_ws(L.map, ri, ci, co)
     ws = _ffi.workspace(wsz, dev)
     # the U2 weight-gradient GEMM reads dz at the output rows; the others read it at the GEMM rows
-    sw = wg.stream(dz, rec["h"], dW, ws) if wg is not None else st
     _ffi.check(eng.wgrad(L.map, L.kind, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), co, co,
-                                   ri, si, oi, _ffi.ptr(dW), _ffi.ptr(ws), wsz, sw), "rpc_dense_wgrad")
+                                   ri, si, oi, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
     dx = None
     if need_dx:
         dmap = L.dgrad_map()
@@ -504,7 +460,6 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
     # block bi+1's first data-gradient GEMM accumulated into a copy of it)
     dh = _nhwc(gouts[-1], dt) if gouts[-1] is not None else None
     dx = None
-    wg = _WgScope(dev)
     for bi in range(nb - 1, -1, -1):
         brecs = recs[bi]
         if dh is None:   # nothing flows through this block
@@ -526,13 +481,12 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
             else:
                 need_dx = need_x
             dh, dW, dgam, dbet = _backward_layer(eng, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
-                                                 accumulate, wg=wg)
+                                                 accumulate)
             grads[id(rec["L"].conv.weight)] = dW
             grads[id(rec["L"].bnm.weight)] = dgam
             grads[id(rec["L"].bnm.bias)] = dbet
         if bi == 0:
             dx = dh
-    wg.join()
     return (dx,) + tuple(grads.get(id(p)) for p in params), None
 
 
@@ -635,7 +589,6 @@ class NeckFn(torch.autograd.Function):
         g = _nhwc(gout, eng.dt)
         grads = {}
         dins = []
-        wg = _WgScope(dev)
         for i, rec in enumerate(ctx.recs):
             L = rec["L"]
             dx_out = None
@@ -643,12 +596,11 @@ class NeckFn(torch.autograd.Function):
                 B, H, W = rec["S"]
                 dx_out = _scratch_image(ctx.cache, ("fpn_dx", i, B, L.ci, H, W, eng.dt, dev), B, L.ci, H, W,
                                         dev, eng.dt)
-            dx, dW, dgam, dbet = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True, dx_out, wg=wg)
+            dx, dW, dgam, dbet = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True, dx_out)
             grads[id(L.conv.weight)] = dW
             grads[id(L.bnm.weight)] = dgam
             grads[id(L.bnm.bias)] = dbet
             dins.append(dx)
-        wg.join()
         ctx.recs = None
         ctx.eng = None
         ctx.cache = None

@@ -29,6 +29,8 @@ def _run(nproc, backend=None, classes=3):
     out = r.stdout + r.stderr
     assert r.returncode == 0, out[-3000:]
     assert '"ddp": "ok"' in out, out[-3000:]
+    if nproc > 1:
+        assert '"averaged_grads_ok": true' in out, out[-3000:]
     print(out[-600:])
     return out
 

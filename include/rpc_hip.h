@@ -298,18 +298,23 @@ int rpc_sparse_backward(const RpcSparseLayer* layers, int nlayers, const void* g
 #define RPC_DMAP_U2 4 /* ConvTranspose2d k2 s2 (4 parities) */
 #define RPC_DMAP_G2 5 /* data gradient of U2 */
 /* out[orow][ooff + n] (+)= sum_{t,k} src[src_row(row,t)][k] * wt[t][n][k]; cin % 64 == 0, cout % 128 == 0;
- * part (optional): [rpc_dense_conv_blocks][2*cout] BatchNorm partial sums of the stored bf16 values */
+ * part (optional): [rpc_dense_conv_part_rows][2*cout] BatchNorm partial sums of the stored bf16 values */
 int rpc_dense_conv(int map, const void* src, int src_pitch, int cin, const void* wt, int cout, void* out,
                    int out_pitch, int out_offset, int accumulate, float* part, const int* row_img,
                    const int* src_img, const int* out_img, void* stream);
 int rpc_dense_conv_blocks(int map, const int* row_img);
+/* exact number of BatchNorm partial-sum rows rpc_dense_conv writes for (map, cout, row_img): one per
+ * 16x32-pixel tile for the S1 kernel k_conv3x3x, else rpc_dense_conv_blocks (the rows rpc_bn_finalize
+ * reduces; never more than rpc_dense_conv_blocks) */
+int rpc_dense_conv_part_rows(int map, int cout, const int* row_img);
 /* which kernel rpc_dense_conv launches for an RPC_DMAP_S1 call with `cout` outputs over row_img:
  * 0 = rpc::dn::k_conv3x3<0> (64-channel blocks), 1 = rpc::dn::k_conv3x3w<0> (128-channel LDS-DMA
- * blocks), -1 = not an S1 call (per-kernel roofline attribution in bench.py) */
+ * blocks), 2 = rpc::dn::k_conv3x3x<0> (16x32-pixel x 128-channel LDS-DMA blocks), -1 = not an S1 call (per-kernel roofline attribution in bench.py) */
 int rpc_dense_conv_s1_kernel(int map, int cout, const int* row_img);
 /* kernel-selection knob for A/B measurement (returns the previous value; value < 0 only reads it):
  * knob 0 = the S1 kernel for output channels that are a multiple of 128 (0: chosen by shape, default;
- * 1: the 64-channel register-staged kernel; 2: the 128-channel LDS-DMA kernel); knob 1 = the S1 weight
+ * 1: the 64-channel register-staged kernel; 2: the 128-channel LDS-DMA kernel; 3: the 16x32-pixel
+ * tile kernel); knob 1 = the S1 weight
  * gradient for 128-multiple channels (0: tap-sharing row-segment kernel, default; 1: per-tap kernel) */
 int rpc_dense_tune(int knob, int value);
 /* dW (torch layout; kind 0 = Conv2d [co][ci][kh][kw], 1 = ConvTranspose2d [ci][co][kh][kw]) of the

@@ -27,6 +27,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "dense_common.h"
 #include "rpc_hip.h"
@@ -680,6 +682,245 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3w(C3 g) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int y = ty0 + wp * 4 + j, x = tx0 + a15;
+    if (y >= g.H || x >= g.W) continue;
+    const size_t orow = (size_t)(b * g.H + y) * g.W + x;
+    u16* op = g.out + orow * g.OP + g.OOFF + n0 + wc * 64 + 4 * q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float v[4] = {acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]};
+      uint2* p2 = (uint2*)(op + i * 16);
+      if (g.accum) {
+        uint2 e = *p2;
+        v[0] += bf2f((u16)(e.x & 0xffff));
+        v[1] += bf2f((u16)(e.x >> 16));
+        v[2] += bf2f((u16)(e.y & 0xffff));
+        v[3] += bf2f((u16)(e.y >> 16));
+      }
+      u16 hb[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        hb[r] = f2bf(v[r]);
+        const float qv = bf2f(hb[r]);
+        s1[i][r] += qv;
+        s2[i][r] += qv * qv;
+      }
+      *p2 = make_uint2((unsigned)hb[0] | ((unsigned)hb[1] << 16), (unsigned)hb[2] | ((unsigned)hb[3] << 16));
+    }
+  }
+  if (g.part == nullptr) return;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) {
+        s1[i][r] += __shfl_xor(s1[i][r], o, 64);
+        s2[i][r] += __shfl_xor(s2[i][r], o, 64);
+      }
+    }
+  float* sP = (float*)lds;   // [4 wp][2][128]
+  if (a15 == 0) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int c = wc * 64 + i * 16 + 4 * q + r;
+        sP[(wp * 2 + 0) * 128 + c] = s1[i][r];
+        sP[(wp * 2 + 1) * 128 + c] = s2[i][r];
+      }
+  }
+  __syncthreads();
+  float* prow = g.part + (size_t)tile * 2 * g.COUT;
+  if (tid < 128) {
+    prow[n0 + tid] = ((sP[0 * 128 + tid] + sP[2 * 128 + tid]) + sP[4 * 128 + tid]) + sP[6 * 128 + tid];
+  } else if (tid < 256) {
+    const int c = tid - 128;
+    prow[g.COUT + n0 + c] = ((sP[1 * 128 + c] + sP[3 * 128 + c]) + sP[5 * 128 + c]) + sP[7 * 128 + c];
+  }
+}
+
+// ------------------------------------------------------------------ 3x3 stride-1 conv, 16x32-pixel tiles x 128 channels
+// k_conv3x3x: k_conv3x3w's 8-wave LDS-DMA pipeline with twice the pixels per wave. Each wave owns
+// 4 tile rows x 32 columns (128 pixels) x 64 output channels = 8 x 4 MFMA accumulator tiles (128
+// VGPRs), so one step's 32 MFMAs read 12 operand fragments (8 pixel + 4 weight) instead of 16
+// (4 + 4 for 16 MFMAs, twice): 0.375 ds_read_b128 per MFMA instead of 0.5, and each staged weight
+// tile feeds 512 pixels instead of 256 (half the weight bytes per FLOP through L2 and the DMA).
+// K-steps are 32 channels of one tap (a step still has 32 MFMAs per wave), so a 32-channel chunk
+// of the 18x34 halo (36-pixel LDS row pitch, 64-byte rows: 41 KB) and a 4-slot ring of 128 x 32
+// weight tiles (8 KB each) fit twice the tile in 115 KB. 64-byte rows carry their four 16-byte
+// granules XOR-swizzled by bit 2 of the pixel column / weight row (g ^ ((x >> 1) & 2)), found by
+// exhaustive search so that every ds_read_b128 lane group of an MFMA operand read (16 consecutive
+// columns from dx = 0..2 or 16..18; 16 aligned weight rows) hits 16 distinct bank slots; the row
+// pitch of 36 pixels keeps the bank of a pixel a function of its column only, so every tap's
+// operand address is the lane's base + constants. Staggered READ / MATH phases, counted vmcnt
+// waits, one raw barrier per phase and the zero-row halo as in k_conv3x3w. SECOND's 200x176
+// layers: 468 tiles = 1.83 rounds of the CUs (858 16x16 tiles = 3.35 rounds).
+constexpr int XTW = 32;                        // tile columns
+constexpr int XHW = XTW + 2;                   // halo columns (34)
+constexpr int XHP = 36;                        // halo LDS row pitch in pixels (bank = f(column))
+constexpr int XHR = HT * XHP;                  // halo LDS rows (648)
+constexpr int XROW = 64;                       // bytes per LDS row (32 bf16 channels)
+constexpr int XBK = 32;                        // channels per K-step
+constexpr int XHBUF = 41 * 1024;               // halo buffer: 648 rows (40.5 KB) rounded to whole DMA KBs
+constexpr int XWTILE = 128 * XROW;             // weight tile: 128 output channels x 32 channels (8 KB)
+constexpr int XLDS = 2 * XHBUF + WRING * XWTILE;   // 116736 B
+constexpr int XHI = 6;                         // halo DMA instructions per wave (41 over 8 waves)
+
+__device__ __forceinline__ int xswz(int x) { return (x >> 1) & 2; }
+
+template <int DUMMY = 0>
+__global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
+  // ONE LDS object: a second __shared__ array gives the accesses alias scopes, and the compiler then
+  // waits for every LDS-DMA in flight (vmcnt(0)) before each step's operand reads
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[XLDS];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wc = (w >> 1) & 1, wp = (w & 1) | ((w >> 2) << 1);   // SIMD partners w, w+4: rows 0-7 / 8-15
+  const int ncob = g.COUT >> 7;
+  const int ntiles = g.B * g.TY * g.TX;
+  const int item = xcd_remap(blockIdx.x, ntiles * ncob);           // tile-major: a tile's co-blocks adjacent
+  const int tile = item / ncob, cob = item - tile * ncob;
+  const int b = tile / (g.TY * g.TX), trem = tile - b * g.TY * g.TX;
+  const int ty0 = (trem / g.TX) * CT, tx0 = (trem % g.TX) * XTW;
+  const int n0 = cob * 128;
+  const int NKC = g.CIN / XBK, NS = 9 * NKC;
+  unsigned char* const hbuf = lds;
+  unsigned char* const wring = lds + 2 * XHBUF;
+
+  // ---- DMA sources, fixed per lane. Instruction k of a halo chunk writes LDS granules k*64 + lane:
+  // row r = hy*36 + hx, slot j holds channel granule j ^ xswz(hx) (pad columns 34, 35 and rows past
+  // 648 read the zero row). Weights: instruction w writes rows w*16 + (lane >> 2) = output channel
+  // n0 + r, slot j = granule j ^ xswz(r).
+  // 32-bit byte offsets into buffer resources (rpc_dense_conv checks the image and weights fit in 2 GB);
+  // out-of-image halo pixels get an offset past the range, which the buffer load returns as zeros
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g.src, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwt = __builtin_amdgcn_make_buffer_rsrc((void*)g.wt, (short)0, 0x7fffffff, 0x00020000);
+  unsigned hofs[XHI];
+#pragma unroll
+  for (int m = 0; m < XHI; ++m) {
+    const int k = min(w + 8 * m, 40);
+    const int P = k * 64 + lane, r = P >> 2, j = P & 3;
+    const int hy = r / XHP, hx = r - hy * XHP;
+    const int y = ty0 + hy - 1, x = tx0 + hx - 1;
+    hofs[m] = (r < XHR && hx < XHW && y >= 0 && y < g.H && x >= 0 && x < g.W)
+                  ? (unsigned)((((b * g.H + y) * g.W + x) * g.SP + (j ^ xswz(hx)) * 8) * 2)
+                  : 0x80000000u;
+  }
+  unsigned wofs;
+  {
+    const int r = w * 16 + (lane >> 2), j = lane & 3;
+    wofs = (unsigned)(((n0 + r) * g.CIN + (j ^ xswz(r)) * 8) * 2);
+  }
+  auto issue_halo = [&](int kc, int hb) {
+#pragma unroll
+    for (int m = 0; m < XHI; ++m)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void*)(hbuf + hb * XHBUF + min(w + 8 * m, 40) * 1024), 16,
+          hofs[m], kc * XBK * 2, 0, 0);
+  };
+  const int wtap = g.COUT * g.CIN * 2;
+  auto issue_w = [&](int s) {
+    s = min(s, NS - 1);
+    const int kc = s / 9, t = s - kc * 9;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        rwt, (__attribute__((address_space(3))) void*)(wring + (s & (WRING - 1)) * XWTILE + w * 1024), 16, wofs,
+        t * wtap + kc * XBK * 2, 0, 0);
+  };
+
+  // ---- MFMA operand addresses: A (weights) rows wc*64 + i*16 + a15; B (halo) pixel (wp*4 + r + dy,
+  // hh*16 + a15 + dx) — the swizzle of column hh*16 + a15 + dx equals that of a15 + dx
+  const int a15 = lane & 15, q = lane >> 4;
+  const int woff = (wc * 64 + a15) * XROW + ((q ^ xswz(a15)) * 16);
+  int hoff[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) hoff[dx] = (wp * 4 * XHP + dx + a15) * XROW + ((q ^ xswz(dx + a15)) * 16);
+
+  f32x4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  issue_halo(0, 0);
+#pragma unroll
+  for (int s = 0; s < WDIST; ++s) issue_w(s);
+
+  const int grp = w >> 2;
+  const bool live = ty0 + wp * 4 < g.H;
+  asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo 0 + tile 0
+  if (grp) asm volatile("s_barrier" ::: "memory");
+  // per step: 1 weight DMA (+ XHI halo DMAs at tap HTAP); the tile of the next step is retired by
+  // vmcnt(1) (vmcnt(1 + XHI) at taps HTAP and HTAP + 1, whose younger DMAs include the halo)
+#define C3X_STEP(t, LIVE)                                                                                     \
+  {                                                                                                           \
+    const int s_ = kc * 9 + (t);                                                                              \
+    issue_w(s_ + WDIST);                                                                                      \
+    if ((t) == HTAP) issue_halo(min(kc + 1, NKC - 1), (kc + 1) & 1);                                          \
+    const unsigned char* hb_ = hbuf + (kc & 1) * XHBUF;                                                       \
+    const unsigned char* wt_ = wring + (s_ & (WRING - 1)) * XWTILE;                                           \
+    constexpr int dy_ = (t) / 3, dx_ = (t) % 3;                                                               \
+    bf16x8 av[4], bv[8];                                                                                      \
+    if (LIVE) {                                                                                               \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                           \
+        av[i] = *(const bf16x8*)(wt_ + woff + i * 16 * XROW);                                                 \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                           \
+        bv[j] = *(const bf16x8*)(hb_ + hoff[dx_] + ((j >> 1) + dy_) * XHP * XROW + (j & 1) * 16 * XROW);      \
+    }                                                                                                         \
+    if (grp) {                                                                                                \
+      if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");                    \
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");                                                   \
+    }                                                                                                         \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");                                           \
+    if (LIVE) {                                                                                               \
+      __builtin_amdgcn_s_setprio(1);                                                                          \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                           \
+        _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                         \
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);              \
+      __builtin_amdgcn_s_setprio(0);                                                                          \
+    }                                                                                                         \
+    if (!grp) {                                                                                               \
+      if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");                    \
+      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");                                                   \
+    }                                                                                                         \
+    asm volatile("s_barrier" ::: "memory");                                                                   \
+  }
+  if (live) {
+    for (int kc = 0; kc < NKC; ++kc) {
+      C3X_STEP(0, true)
+      C3X_STEP(1, true)
+      C3X_STEP(2, true)
+      C3X_STEP(3, true)
+      C3X_STEP(4, true)
+      C3X_STEP(5, true)
+      C3X_STEP(6, true)
+      C3X_STEP(7, true)
+      C3X_STEP(8, true)
+    }
+  } else {   // DMA issue and barriers only
+    for (int kc = 0; kc < NKC; ++kc) {
+      C3X_STEP(0, false)
+      C3X_STEP(1, false)
+      C3X_STEP(2, false)
+      C3X_STEP(3, false)
+      C3X_STEP(4, false)
+      C3X_STEP(5, false)
+      C3X_STEP(6, false)
+      C3X_STEP(7, false)
+      C3X_STEP(8, false)
+    }
+  }
+#undef C3X_STEP
+  if (!grp) asm volatile("s_barrier" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // ---- epilogue: lane holds co = n0 + wc*64 + i*16 + 4q + r of pixel (wp*4 + (j >> 1), (j & 1)*16 + a15)
+  float s1[4][4], s2[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int y = ty0 + wp * 4 + (j >> 1), x = tx0 + (j & 1) * 16 + a15;
     if (y >= g.H || x >= g.W) continue;
     const size_t orow = (size_t)(b * g.H + y) * g.W + x;
     u16* op = g.out + orow * g.OP + g.OOFF + n0 + wc * 64 + 4 * q;
@@ -1398,6 +1639,9 @@ static int g_s1_variant = 0;
 static int g_wgrad_variant = 0;
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
+// k_conv3x3x (16x32-pixel tiles) for 128-multiple outputs unless another S1 kernel is forced
+static bool s1_xwide(int cout) { return cout % 128 == 0 && (g_s1_variant == 0 || g_s1_variant == 3); }
+
 static bool s1_wide(int tiles, int cout) {
   if (cout % 128 || g_s1_variant == 1) return false;
   if (g_s1_variant == 2) return true;
@@ -1444,7 +1688,11 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   if (map == M_S1) {
     const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
     C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
-    if (s1_wide(g.R.B * TY * TX, g.COUT))
+    if (s1_xwide(g.COUT) && g.CIN % XBK == 0 && (long long)g.M * g.SP * 2 < (1LL << 31) &&
+        9LL * g.COUT * g.CIN * 2 < (1LL << 31)) {
+      c.TX = (g.R.W + XTW - 1) / XTW;
+      hipLaunchKernelGGL(k_conv3x3x<0>, dim3(g.R.B * TY * c.TX * (g.COUT / 128)), dim3(WB), 0, st, c);
+    } else if (s1_wide(g.R.B * TY * TX, g.COUT))
       hipLaunchKernelGGL(k_conv3x3w<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(WB), 0, st, c);
     else
       hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
@@ -1469,7 +1717,15 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
 extern "C" int rpc_dense_conv_s1_kernel(int map, int cout, const int* r_img) {
   if (map != M_S1 || !r_img || cout % 64) return -1;
   const int TY = (r_img[1] + CT - 1) / CT, TX = (r_img[2] + CT - 1) / CT;
+  if (s1_xwide(cout)) return 2;
   return s1_wide(r_img[0] * TY * TX, cout) ? 1 : 0;
+}
+
+extern "C" int rpc_dense_conv_part_rows(int map, int cout, const int* r_img) {
+  if (!r_img || map < M_S1 || map > M_G2) return -1;
+  if (map == M_S1 && s1_xwide(cout))   // one row per 16x32 tile
+    return r_img[0] * ((r_img[1] + CT - 1) / CT) * ((r_img[2] + XTW - 1) / XTW);
+  return rpc_dense_conv_blocks(map, r_img);
 }
 
 extern "C" int rpc_dense_conv_blocks(int map, const int* r_img) {

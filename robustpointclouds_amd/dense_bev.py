@@ -48,7 +48,7 @@ class ConvTimer:
         e.record(torch.cuda.current_stream())
         return e
 
-    KERNELS = {0: "rpc::dn::k_conv3x3<0>", 1: "rpc::dn::k_conv3x3w<0>"}
+    KERNELS = {0: "rpc::dn::k_conv3x3<0>", 1: "rpc::dn::k_conv3x3w<0>", 2: "rpc::dn::k_conv3x3x<0>"}
 
     def stop(self, e0, rows, ci, co, variant=0):
         e1 = torch.cuda.Event(enable_timing=True)
@@ -241,6 +241,9 @@ class _Eng:
         x = "_f32" if f32 else ""
         self.conv_raw = getattr(lib, "rpc_dense_conv" + x)
         self.blocks = getattr(lib, "rpc_dense_conv_blocks" + x)
+        # BatchNorm partial-sum rows one conv writes (bf16 S1: one per 16x32 tile)
+        self.part_rows = (lambda fmap, co, ri: self.blocks(fmap, ri)) if f32 else \
+            (lambda fmap, co, ri: lib.rpc_dense_conv_part_rows(fmap, co, ri))
         self.wgrad = getattr(lib, "rpc_dense_wgrad" + x)
         self.wgrad_ws = getattr(lib, "rpc_dense_wgrad_workspace_size" + x)
         self.bn_apply = getattr(lib, "rpc_dense_bn_apply" + x)
@@ -331,7 +334,7 @@ def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
     ri, si, oi = _ffi.int_arr(R), _ffi.int_arr(S), _ffi.int_arr(O)
     part = None
     if training:
-        nblk = eng.blocks(L.map, ri)
+        nblk = eng.part_rows(L.map, L.co, ri)
         part = torch.empty((nblk, 2 * L.co), dtype=torch.float32, device=dev)
     _ffi.check(eng.conv(L.map, _ffi.ptr(h), pitch, L.ci, _ffi.ptr(wf), L.co, _ffi.ptr(z), L.co, 0, 0,
                         _ffi.ptr(part), ri, si, oi, st), "rpc_dense_conv")

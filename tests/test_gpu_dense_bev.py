@@ -374,6 +374,51 @@ def test_s1_lds_dma_kernel_bitexact_vs_register_staged(ci, co, B, H, W):
     _close_bf16(outs[0][0], ref)
 
 
+@pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 6, 200, 176), (256, 128, 2, 200, 176), (256, 256, 2, 100, 88),
+                                         (128, 128, 1, 16, 32), (256, 128, 2, 37, 45), (128, 256, 2, 33, 17),
+                                         (128, 128, 3, 24, 40), (128, 256, 1, 9, 130), (384, 128, 1, 21, 70),
+                                         (192, 128, 1, 19, 33)])
+def test_s1_wide_tile_kernel(ci, co, B, H, W):
+    """k_conv3x3x (16x32-pixel tiles, 32-channel K-steps, rpc_dense_tune knob 0 = 3) against float64 torch on
+    the same bf16 operands: output within 1 bf16 ulp of the output scale, the accumulate path likewise,
+    BatchNorm partials = column sums / sums of squares of the stored values over exactly
+    rpc_dense_conv_part_rows rows (later rows untouched), and the output within 1 bf16 ulp of k_conv3x3's
+    (same 32-channel MFMA sums, added in another order). Shapes: SECOND's (200x176 with an 8-row last
+    tile row and a 16-column last tile column; 100x88), one tile, partial rows / columns, an odd number of
+    32-channel K-steps (192 channels)."""
+    lib = _ffi.load()
+    x = _rand(B, ci, H, W, seed=31)
+    Wt = _rand(co, ci, 3, 3, seed=32, scale=0.05)
+    wf, _ = _wprep(Wt, 0, 9, 1)
+    img = (B, H, W)
+    base = _rand(B, co, H, W, seed=33)
+    ref = F.conv2d(x.double(), Wt.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
+    outs = {}
+    for variant in (3, 1):
+        old = lib.rpc_dense_tune(0, variant)
+        try:
+            if variant == 3:
+                assert lib.rpc_dense_conv_s1_kernel(S1, co, _ffi.int_arr(img)) == 2
+            rows = lib.rpc_dense_conv_part_rows(S1, co, _ffi.int_arr(img))
+            z, part = _conv(S1, _nhwc(x), ci, wf, co, img, img, img, stats=True)
+            acc = _nhwc(base).reshape(-1, co).clone()
+            _conv(S1, _nhwc(x), ci, wf, co, img, img, img, out=acc, accum=True)
+            torch.cuda.synchronize()
+        finally:
+            lib.rpc_dense_tune(0, old)
+        assert 1 <= rows <= part.shape[0]
+        assert torch.all(part[rows:] == 0)
+        outs[variant] = (z, acc, part[:rows].double().sum(0))
+    z, acc, sp = outs[3]
+    _close_bf16(z, ref)
+    _close_bf16(acc, ref + base.permute(0, 2, 3, 1).reshape(-1, co).double())
+    _close_bf16(z, outs[1][0])
+    zd = z.double()
+    want = torch.cat([zd.sum(0), (zd ** 2).sum(0)])
+    scale = torch.cat([zd.abs().sum(0), (zd ** 2).sum(0)])   # fp32 summation error scale
+    assert torch.all((sp - want).abs() <= 1e-5 * scale + 1e-6)
+
+
 @pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 1, 200, 176), (256, 256, 1, 100, 88), (256, 128, 2, 37, 45),
                                          (128, 128, 2, 17, 70), (128, 256, 1, 5, 130)])
 def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):

@@ -746,8 +746,8 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3w(C3 g) {
 // (4 + 4 for 16 MFMAs, twice): 0.375 ds_read_b128 per MFMA instead of 0.5, and each staged weight
 // tile feeds 512 pixels instead of 256 (half the weight bytes per FLOP through L2 and the DMA).
 // K-steps are 32 channels of one tap (a step still has 32 MFMAs per wave), so a 32-channel chunk
-// of the 18x34 halo (36-pixel LDS row pitch, 64-byte rows: 41 KB) and a 4-slot ring of 128 x 32
-// weight tiles (8 KB each) fit twice the tile in 115 KB. 64-byte rows carry their four 16-byte
+// of the 18x34 halo (36-pixel LDS row pitch, 64-byte rows: 41 KB) and an 8-slot ring of 128 x 32
+// weight tiles (8 KB each) (four in flight ahead of the one computed) fit twice the tile in 146 KB. 64-byte rows carry their four 16-byte
 // granules XOR-swizzled by bit 2 of the pixel column / weight row (g ^ ((x >> 1) & 2)), found by
 // exhaustive search so that every ds_read_b128 lane group of an MFMA operand read (16 consecutive
 // columns from dx = 0..2 or 16..18; 16 aligned weight rows) hits 16 distinct bank slots; the row
@@ -763,12 +763,17 @@ constexpr int XROW = 64;                       // bytes per LDS row (32 bf16 cha
 constexpr int XBK = 32;                        // channels per K-step
 constexpr int XHBUF = 41 * 1024;               // halo buffer: 648 rows (40.5 KB) rounded to whole DMA KBs
 constexpr int XWTILE = 128 * XROW;             // weight tile: 128 output channels x 32 channels (8 KB)
-constexpr int XLDS = 2 * XHBUF + WRING * XWTILE;   // 116736 B
+constexpr int XWR = 8;                         // weight ring slots
+constexpr int XWD = 4;                         // weight tiles in flight ahead of the one computed
+constexpr int XLDS = 2 * XHBUF + XWR * XWTILE;     // 149504 B
 constexpr int XHI = 6;                         // halo DMA instructions per wave (41 over 8 waves)
 
 __device__ __forceinline__ int xswz(int x) { return (x >> 1) & 2; }
 
-template <int DUMMY = 0>
+// DBG (timing experiments only, rpc_dense_tune knob 4; outputs are garbage): bit 0 = no MFMAs, bit 1 =
+// no operand reads, bit 2 = no weight DMAs, bit 3 = no halo DMAs, bit 4 = no barriers in the K-loop,
+// bit 5 = the register-direct epilogue (8-byte stores from the accumulator layout)
+template <int DBG = 0>
 __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
   // ONE LDS object: a second __shared__ array gives the accesses alias scopes, and the compiler then
   // waits for every LDS-DMA in flight (vmcnt(0)) before each step's operand reads
@@ -811,6 +816,7 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
     wofs = (unsigned)(((n0 + r) * g.CIN + (j ^ xswz(r)) * 8) * 2);
   }
   auto issue_halo = [&](int kc, int hb) {
+    if (DBG & 8) return;
 #pragma unroll
     for (int m = 0; m < XHI; ++m)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
@@ -819,10 +825,11 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
   };
   const int wtap = g.COUT * g.CIN * 2;
   auto issue_w = [&](int s) {
+    if (DBG & 4) return;
     s = min(s, NS - 1);
     const int kc = s / 9, t = s - kc * 9;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        rwt, (__attribute__((address_space(3))) void*)(wring + (s & (WRING - 1)) * XWTILE + w * 1024), 16, wofs,
+        rwt, (__attribute__((address_space(3))) void*)(wring + (s & (XWR - 1)) * XWTILE + w * 1024), 16, wofs,
         t * wtap + kc * XBK * 2, 0, 0);
   };
 
@@ -842,35 +849,41 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
 
   issue_halo(0, 0);
 #pragma unroll
-  for (int s = 0; s < WDIST; ++s) issue_w(s);
+  for (int s = 0; s < XWD; ++s) issue_w(s);
 
   const int grp = w >> 2;
   const bool live = ty0 + wp * 4 < g.H;
-  asm volatile("s_waitcnt vmcnt(1)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo 0 + tile 0
+  static_assert(XWD == 4 && XHI == 6 && HTAP + XWD <= 8, "vmcnt immediates below");
+  asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo 0 + tile 0
   if (grp) asm volatile("s_barrier" ::: "memory");
-  // per step: 1 weight DMA (+ XHI halo DMAs at tap HTAP); the tile of the next step is retired by
-  // vmcnt(1) (vmcnt(1 + XHI) at taps HTAP and HTAP + 1, whose younger DMAs include the halo)
+  // per step: 1 weight DMA XWD tiles ahead (+ XHI halo DMAs at tap HTAP, after it); the tile of the next
+  // step is retired by vmcnt(XWD - 1), or vmcnt(XWD - 1 + XHI) at taps HTAP .. HTAP + XWD - 1 while the
+  // halo is younger than that tile (it is retired XWD steps after its issue)
 #define C3X_STEP(t, LIVE)                                                                                     \
   {                                                                                                           \
     const int s_ = kc * 9 + (t);                                                                              \
-    issue_w(s_ + WDIST);                                                                                      \
+    issue_w(s_ + XWD);                                                                                        \
     if ((t) == HTAP) issue_halo(min(kc + 1, NKC - 1), (kc + 1) & 1);                                          \
     const unsigned char* hb_ = hbuf + (kc & 1) * XHBUF;                                                       \
-    const unsigned char* wt_ = wring + (s_ & (WRING - 1)) * XWTILE;                                           \
+    const unsigned char* wt_ = wring + (s_ & (XWR - 1)) * XWTILE;                                             \
     constexpr int dy_ = (t) / 3, dx_ = (t) % 3;                                                               \
     bf16x8 av[4], bv[8];                                                                                      \
-    if (LIVE) {                                                                                               \
+    if (DBG & 2) {                                                                                            \
+      _Pragma("unroll") for (int i = 0; i < 4; ++i) av[i] = __builtin_bit_cast(bf16x8, make_uint4(lane, i, w, s_)); \
+      _Pragma("unroll") for (int j = 0; j < 8; ++j) bv[j] = __builtin_bit_cast(bf16x8, make_uint4(j, lane, s_, w)); \
+    }                                                                                                         \
+    if (LIVE && !(DBG & 2)) {                                                                                 \
       _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                           \
         av[i] = *(const bf16x8*)(wt_ + woff + i * 16 * XROW);                                                 \
       _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                           \
         bv[j] = *(const bf16x8*)(hb_ + hoff[dx_] + ((j >> 1) + dy_) * XHP * XROW + (j & 1) * 16 * XROW);      \
     }                                                                                                         \
     if (grp) {                                                                                                \
-      if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");                    \
-      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");                                                   \
+      if ((t) >= HTAP && (t) < HTAP + XWD) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");                   \
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");                                                   \
     }                                                                                                         \
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");                                           \
-    if (LIVE) {                                                                                               \
+    if (DBG & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");                                           \
+    if (LIVE && !(DBG & 1)) {                                                                                 \
       __builtin_amdgcn_s_setprio(1);                                                                          \
       _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                           \
         _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                         \
@@ -878,10 +891,10 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
       __builtin_amdgcn_s_setprio(0);                                                                          \
     }                                                                                                         \
     if (!grp) {                                                                                               \
-      if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");                    \
-      else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");                                                   \
+      if ((t) >= HTAP && (t) < HTAP + XWD) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");                   \
+      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");                                                   \
     }                                                                                                         \
-    asm volatile("s_barrier" ::: "memory");                                                                   \
+    if (!(DBG & 16)) asm volatile("s_barrier" ::: "memory");                                                  \
   }
   if (live) {
     for (int kc = 0; kc < NKC; ++kc) {
@@ -913,6 +926,75 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // ---- epilogue: lane holds co = n0 + wc*64 + i*16 + 4q + r of pixel (wp*4 + (j >> 1), (j & 1)*16 + a15)
+  if (!g.accum && !(DBG & 32)) {
+    // Staged through LDS (the pipeline buffers are drained): the bf16 tile [512 px][128 co] (256-byte
+    // rows, 16-byte granule g of pixel p at slot g ^ (p & 15): the 16 pixels of one ds_write_b64 lane
+    // group hit 16 slots), then written back as whole 256-byte pixel rows, 16 bytes per lane — a tile
+    // row of 32 pixels is 8 KB contiguous. Direct 8-byte stores from the accumulator layout touched 16
+    // rows per instruction (store-issue bound: 128 KB per block). BatchNorm sums from the same bf16
+    // values: per thread 8 channels over its 16 pixels, then lane groups, then waves in fixed order.
+    unsigned char* tileb = lds;
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int p = (wp * 4 + (j >> 1)) * XTW + (j & 1) * 16 + a15;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int gr = (wc * 8 + i * 2 + (q >> 1)) ^ (p & 15);
+          const unsigned lo = (unsigned)f2bf(acc[i][j][0]) | ((unsigned)f2bf(acc[i][j][1]) << 16);
+          const unsigned hi = (unsigned)f2bf(acc[i][j][2]) | ((unsigned)f2bf(acc[i][j][3]) << 16);
+          *(uint2*)(tileb + p * 256 + gr * 16 + (q & 1) * 8) = make_uint2(lo, hi);
+        }
+      }
+    }
+    __syncthreads();
+    const int c = tid & 15, px = tid >> 4;   // 16-byte chunk (8 channels) c of column px of every tile row
+    float t1[8], t2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t1[e] = t2[e] = 0.f;
+    const int x = tx0 + px;
+#pragma unroll 4
+    for (int k = 0; k < CT; ++k) {
+      const int y = ty0 + k, p = k * XTW + px;
+      if (y >= g.H || x >= g.W) continue;
+      const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
+      *(uint4*)(g.out + ((size_t)(b * g.H + y) * g.W + x) * g.OP + g.OOFF + n0 + c * 8) = v;
+      const unsigned u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float f0 = bf2f((u16)(u[e] & 0xffff)), f1 = bf2f((u16)(u[e] >> 16));
+        t1[2 * e] += f0;
+        t2[2 * e] += f0 * f0;
+        t1[2 * e + 1] += f1;
+        t2[2 * e + 1] += f1 * f1;
+      }
+    }
+    if (g.part == nullptr) return;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      t1[e] += __shfl_xor(t1[e], 16, 64);
+      t2[e] += __shfl_xor(t2[e], 16, 64);
+      t1[e] += __shfl_xor(t1[e], 32, 64);
+      t2[e] += __shfl_xor(t2[e], 32, 64);
+    }
+    float* sR = (float*)(lds + 128 * 1024);   // [8 waves][2][128 channels]
+    if (lane < 16) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sR[(w * 2 + 0) * 128 + c * 8 + e] = t1[e];
+        sR[(w * 2 + 1) * 128 + c * 8 + e] = t2[e];
+      }
+    }
+    __syncthreads();
+    if (tid < 256) {
+      const int k2 = tid >> 7, ch = tid & 127;
+      float s = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 8; ++ww) s += sR[(ww * 2 + k2) * 128 + ch];
+      g.part[(size_t)tile * 2 * g.COUT + k2 * g.COUT + n0 + ch] = s;
+    }
+    return;
+  }
   float s1[4][4], s2[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -1637,6 +1719,7 @@ static unsigned ew_blocks(long long m, int c) {
 // 0.84 of 4 rounds for either kernel, and there the register-staged kernel measured 3-8 % faster).
 static int g_s1_variant = 0;
 static int g_wgrad_variant = 0;
+static int g_s1x_dbg = 0;          // knob 4: k_conv3x3x timing experiments (0 = the real kernel)
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
 // k_conv3x3x (16x32-pixel tiles) for 128-multiple outputs unless another S1 kernel is forced
@@ -1659,6 +1742,11 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   if (knob == 1) {
     const int old = g_wgrad_variant;
     if (value >= 0) g_wgrad_variant = value;
+    return old;
+  }
+  if (knob == 4) {
+    const int old = g_s1x_dbg;
+    if (value >= 0 && value <= 63) g_s1x_dbg = value;
     return old;
   }
   if (knob == 2) {
@@ -1691,7 +1779,25 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
     if (s1_xwide(g.COUT) && g.CIN % XBK == 0 && (long long)g.M * g.SP * 2 < (1LL << 31) &&
         9LL * g.COUT * g.CIN * 2 < (1LL << 31)) {
       c.TX = (g.R.W + XTW - 1) / XTW;
-      hipLaunchKernelGGL(k_conv3x3x<0>, dim3(g.R.B * TY * c.TX * (g.COUT / 128)), dim3(WB), 0, st, c);
+      const dim3 grid(g.R.B * TY * c.TX * (g.COUT / 128));
+      switch (g_s1x_dbg) {
+        case 1: hipLaunchKernelGGL(k_conv3x3x<1>, grid, dim3(WB), 0, st, c); break;
+        case 2: hipLaunchKernelGGL(k_conv3x3x<2>, grid, dim3(WB), 0, st, c); break;
+        case 3: hipLaunchKernelGGL(k_conv3x3x<3>, grid, dim3(WB), 0, st, c); break;
+        case 4: hipLaunchKernelGGL(k_conv3x3x<4>, grid, dim3(WB), 0, st, c); break;
+        case 8: hipLaunchKernelGGL(k_conv3x3x<8>, grid, dim3(WB), 0, st, c); break;
+        case 12: hipLaunchKernelGGL(k_conv3x3x<12>, grid, dim3(WB), 0, st, c); break;
+        case 13: hipLaunchKernelGGL(k_conv3x3x<13>, grid, dim3(WB), 0, st, c); break;
+        case 14: hipLaunchKernelGGL(k_conv3x3x<14>, grid, dim3(WB), 0, st, c); break;
+        case 28: hipLaunchKernelGGL(k_conv3x3x<28>, grid, dim3(WB), 0, st, c); break;
+        case 30: hipLaunchKernelGGL(k_conv3x3x<30>, grid, dim3(WB), 0, st, c); break;
+        case 29: hipLaunchKernelGGL(k_conv3x3x<29>, grid, dim3(WB), 0, st, c); break;
+        case 32: hipLaunchKernelGGL(k_conv3x3x<32>, grid, dim3(WB), 0, st, c); break;
+        case 62: hipLaunchKernelGGL(k_conv3x3x<62>, grid, dim3(WB), 0, st, c); break;
+        case 63: hipLaunchKernelGGL(k_conv3x3x<63>, grid, dim3(WB), 0, st, c); break;
+        case 31: hipLaunchKernelGGL(k_conv3x3x<31>, grid, dim3(WB), 0, st, c); break;
+        default: hipLaunchKernelGGL(k_conv3x3x<0>, grid, dim3(WB), 0, st, c);
+      }
     } else if (s1_wide(g.R.B * TY * TX, g.COUT))
       hipLaunchKernelGGL(k_conv3x3w<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(WB), 0, st, c);
     else

@@ -1060,6 +1060,286 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
   }
 }
 
+// ------------------------------------------------------------------ 3x3 stride-1 conv, two 4-wave blocks per CU
+// k_conv3x3y: k_conv3x3x's per-wave work (128 accumulator VGPRs, 12 operand fragments per 32 MFMAs,
+// 32-channel K-steps, 64-byte swizzled rows, buffer-load DMA, LDS-staged epilogue) in a 4-wave block
+// of 16x16 pixels x 128 output channels (wave w: tile rows 4w..4w+3 = 64 pixels x 128 channels),
+// 78 KB of LDS, so TWO blocks share a CU. k_conv3x3x's 8-wave blocks fill whole rounds of the CUs
+// at once: every block stages its halo, computes, and stores its 128 KB output at the same time
+// (measured: prologue + epilogue 17 us of a 71 us 200x176 launch, not overlapped). Two independent
+// blocks per CU overlap one block's prologue / epilogue with the other's MFMAs, and the grid of
+// 16x16 tiles (858 at 200x176) is drained by whichever slot frees first. One barrier per step
+// (the other block on the SIMD plays the partner wave); halo: 18 rows of 20 pixels (row pitch
+// 20 = 0 mod 4, so a pixel's bank is a function of its column), double-buffered 23 KB chunks; weights: 4-slot
+// ring of 128 x 32 tiles two steps ahead.
+constexpr int YB = 256;                        // threads
+constexpr int YHP = 20;                        // halo LDS row pitch in pixels
+constexpr int YHR = HT * YHP;                  // halo LDS rows (360)
+constexpr int YHBUF = 23 * 1024;               // halo buffer: 360 rows (22.5 KB) rounded to whole DMA KBs
+constexpr int YHI = 6;                         // halo DMA instructions per wave (23 over 4 waves)
+constexpr int YLDS = 2 * YHBUF + WRING * XWTILE;   // 79872 B
+
+template <int DBG = 0>
+__global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[YLDS];   // ONE LDS object (see k_conv3x3x)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int ncob = g.COUT >> 7;
+  const int ntiles = g.B * g.TY * g.TX;
+  const int item = xcd_remap(blockIdx.x, ntiles * ncob);           // tile-major: a tile's co-blocks adjacent
+  const int tile = item / ncob, cob = item - tile * ncob;
+  const int b = tile / (g.TY * g.TX), trem = tile - b * g.TY * g.TX;
+  const int ty0 = (trem / g.TX) * CT, tx0 = (trem % g.TX) * CT;
+  const int n0 = cob * 128;
+  const int NKC = g.CIN / XBK, NS = 9 * NKC;
+  unsigned char* const hbuf = lds;
+  unsigned char* const wring = lds + 2 * YHBUF;
+
+  const __amdgpu_buffer_rsrc_t rsrc = __builtin_amdgcn_make_buffer_rsrc((void*)g.src, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rwt = __builtin_amdgcn_make_buffer_rsrc((void*)g.wt, (short)0, 0x7fffffff, 0x00020000);
+  // halo: instruction k writes LDS granules k*64 + lane (row r = hy*20 + hx, slot j = granule j ^ xswz(hx));
+  // pad columns 18, 19 and rows past 360 read zeros (offset past the range)
+  unsigned hofs[YHI];
+#pragma unroll
+  for (int m = 0; m < YHI; ++m) {
+    const int k = min(w + 4 * m, 22);
+    const int P = k * 64 + lane, r = P >> 2, j = P & 3;
+    const int hy = r / YHP, hx = r - hy * YHP;
+    const int y = ty0 + hy - 1, x = tx0 + hx - 1;
+    hofs[m] = (r < YHR && hx < HT && y >= 0 && y < g.H && x >= 0 && x < g.W)
+                  ? (unsigned)((((b * g.H + y) * g.W + x) * g.SP + (j ^ xswz(hx)) * 8) * 2)
+                  : 0x80000000u;
+  }
+  // weights: instructions 2w, 2w + 1 write rows (2w + m)*16 + (lane >> 2) = output channel n0 + r
+  unsigned wofs[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int r = (2 * w + m) * 16 + (lane >> 2), j = lane & 3;
+    wofs[m] = (unsigned)(((n0 + r) * g.CIN + (j ^ xswz(r)) * 8) * 2);
+  }
+  auto issue_halo = [&](int kc, int hb) {
+#pragma unroll
+    for (int m = 0; m < YHI; ++m)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rsrc, (__attribute__((address_space(3))) void*)(hbuf + hb * YHBUF + min(w + 4 * m, 22) * 1024), 16,
+          hofs[m], kc * XBK * 2, 0, 0);
+  };
+  const int wtap = g.COUT * g.CIN * 2;
+  auto issue_w = [&](int s) {
+    s = min(s, NS - 1);
+    const int kc = s / 9, t = s - kc * 9;
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rwt, (__attribute__((address_space(3))) void*)(wring + (s & (WRING - 1)) * XWTILE + (2 * w + m) * 1024), 16,
+          wofs[m], t * wtap + kc * XBK * 2, 0, 0);
+  };
+
+  // operands: A (weights) rows i*16 + a15 (i = 0..7); B (halo) pixel (4w + j + dy, a15 + dx)
+  const int a15 = lane & 15, q = lane >> 4;
+  const int woff = a15 * XROW + ((q ^ xswz(a15)) * 16);
+  int hoff[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) hoff[dx] = (w * 4 * YHP + dx + a15) * XROW + ((q ^ xswz(dx + a15)) * 16);
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  issue_halo(0, 0);
+#pragma unroll
+  for (int s = 0; s < WDIST; ++s) issue_w(s);
+  const bool live = ty0 + w * 4 < g.H;
+  asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo 0 + tile 0
+  // per step: issue the DMAs two steps ahead, read this step's 12 fragments, 32 MFMAs, retire the next
+  // step's tile (vmcnt(2); vmcnt(8) at taps HTAP, HTAP + 1 whose younger DMAs include the halo), barrier
+#define C3Y_STEP(t, LIVE)                                                                                     \
+  {                                                                                                           \
+    const int s_ = kc * 9 + (t);                                                                              \
+    issue_w(s_ + WDIST);                                                                                      \
+    if ((t) == HTAP) issue_halo(min(kc + 1, NKC - 1), (kc + 1) & 1);                                          \
+    if (LIVE) {                                                                                               \
+      const unsigned char* hb_ = hbuf + (kc & 1) * YHBUF;                                                     \
+      const unsigned char* wt_ = wring + (s_ & (WRING - 1)) * XWTILE;                                         \
+      constexpr int dy_ = (t) / 3, dx_ = (t) % 3;                                                             \
+      bf16x8 av[8], bv[4];                                                                                    \
+      _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                           \
+        bv[j] = *(const bf16x8*)(hb_ + hoff[dx_] + (j + dy_) * YHP * XROW);                                   \
+      _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
+        av[i] = *(const bf16x8*)(wt_ + woff + i * 16 * XROW);                                                 \
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
+      __builtin_amdgcn_s_setprio(1);                                                                          \
+      _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                         \
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);              \
+      __builtin_amdgcn_s_setprio(0);                                                                          \
+    }                                                                                                         \
+    if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                      \
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                     \
+    asm volatile("s_barrier" ::: "memory");                                                                   \
+  }
+  if (live) {
+    for (int kc = 0; kc < NKC; ++kc) {
+      C3Y_STEP(0, true)
+      C3Y_STEP(1, true)
+      C3Y_STEP(2, true)
+      C3Y_STEP(3, true)
+      C3Y_STEP(4, true)
+      C3Y_STEP(5, true)
+      C3Y_STEP(6, true)
+      C3Y_STEP(7, true)
+      C3Y_STEP(8, true)
+    }
+  } else {
+    for (int kc = 0; kc < NKC; ++kc) {
+      C3Y_STEP(0, false)
+      C3Y_STEP(1, false)
+      C3Y_STEP(2, false)
+      C3Y_STEP(3, false)
+      C3Y_STEP(4, false)
+      C3Y_STEP(5, false)
+      C3Y_STEP(6, false)
+      C3Y_STEP(7, false)
+      C3Y_STEP(8, false)
+    }
+  }
+#undef C3Y_STEP
+  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+
+  // ---- epilogue: lane holds co = n0 + i*16 + 4q + r of pixel (4w + j, a15)
+  if (!g.accum) {
+    // bf16 tile [256 px][128 co] in LDS (granule g of pixel p at slot g ^ (p & 15)), written back as
+    // whole 256-byte pixel rows; BatchNorm sums from the same bf16 values (as k_conv3x3x)
+    unsigned char* tileb = lds;
+    if (live) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int p = (w * 4 + j) * CT + a15;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int gr = (i * 2 + (q >> 1)) ^ (p & 15);
+          const unsigned lo = (unsigned)f2bf(acc[i][j][0]) | ((unsigned)f2bf(acc[i][j][1]) << 16);
+          const unsigned hi = (unsigned)f2bf(acc[i][j][2]) | ((unsigned)f2bf(acc[i][j][3]) << 16);
+          *(uint2*)(tileb + p * 256 + gr * 16 + (q & 1) * 8) = make_uint2(lo, hi);
+        }
+      }
+    }
+    __syncthreads();
+    const int c = tid & 15, px = tid >> 4;   // 16-byte chunk c of column px of every tile row
+    float t1[8], t2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t1[e] = t2[e] = 0.f;
+    const int x = tx0 + px;
+#pragma unroll 4
+    for (int k = 0; k < CT; ++k) {
+      const int y = ty0 + k, p = k * CT + px;
+      if (y >= g.H || x >= g.W) continue;
+      const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
+      *(uint4*)(g.out + ((size_t)(b * g.H + y) * g.W + x) * g.OP + g.OOFF + n0 + c * 8) = v;
+      const unsigned u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float f0 = bf2f((u16)(u[e] & 0xffff)), f1 = bf2f((u16)(u[e] >> 16));
+        t1[2 * e] += f0;
+        t2[2 * e] += f0 * f0;
+        t1[2 * e + 1] += f1;
+        t2[2 * e + 1] += f1 * f1;
+      }
+    }
+    if (g.part == nullptr) return;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      t1[e] += __shfl_xor(t1[e], 16, 64);
+      t2[e] += __shfl_xor(t2[e], 16, 64);
+      t1[e] += __shfl_xor(t1[e], 32, 64);
+      t2[e] += __shfl_xor(t2[e], 32, 64);
+    }
+    float* sR = (float*)(lds + 64 * 1024);   // [4 waves][2][128 channels]
+    if (lane < 16) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sR[(w * 2 + 0) * 128 + c * 8 + e] = t1[e];
+        sR[(w * 2 + 1) * 128 + c * 8 + e] = t2[e];
+      }
+    }
+    __syncthreads();
+    {
+      const int k2 = tid >> 7, ch = tid & 127;
+      const float s = ((sR[(0 * 2 + k2) * 128 + ch] + sR[(1 * 2 + k2) * 128 + ch]) + sR[(2 * 2 + k2) * 128 + ch]) +
+                      sR[(3 * 2 + k2) * 128 + ch];
+      g.part[(size_t)tile * 2 * g.COUT + k2 * g.COUT + n0 + ch] = s;
+    }
+    return;
+  }
+  // accumulate into the existing image: fp32 sum, one rounding (register-direct stores), in two halves
+  // of 64 channels (BatchNorm sums of half the accumulator tiles live at a time)
+  float* sP = (float*)lds;   // [4 waves][2][128]
+#pragma unroll
+  for (int ih = 0; ih < 2; ++ih) {
+    float s1[4][4], s2[4][4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s1[i][r] = s2[i][r] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int y = ty0 + w * 4 + j, x = tx0 + a15;
+      if (y >= g.H || x >= g.W) continue;
+      u16* op = g.out + ((size_t)(b * g.H + y) * g.W + x) * g.OP + g.OOFF + n0 + ih * 64 + 4 * q;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const f32x4 a = acc[ih * 4 + i][j];
+        float v[4] = {a[0], a[1], a[2], a[3]};
+        uint2* p2 = (uint2*)(op + i * 16);
+        uint2 e = *p2;
+        v[0] += bf2f((u16)(e.x & 0xffff));
+        v[1] += bf2f((u16)(e.x >> 16));
+        v[2] += bf2f((u16)(e.y & 0xffff));
+        v[3] += bf2f((u16)(e.y >> 16));
+        u16 hb[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          hb[r] = f2bf(v[r]);
+          const float qv = bf2f(hb[r]);
+          s1[i][r] += qv;
+          s2[i][r] += qv * qv;
+        }
+        *p2 = make_uint2((unsigned)hb[0] | ((unsigned)hb[1] << 16), (unsigned)hb[2] | ((unsigned)hb[3] << 16));
+      }
+    }
+    if (g.part == nullptr) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) {
+          s1[i][r] += __shfl_xor(s1[i][r], o, 64);
+          s2[i][r] += __shfl_xor(s2[i][r], o, 64);
+        }
+      }
+    if (a15 == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int cc = ih * 64 + i * 16 + 4 * q + r;
+          sP[(w * 2 + 0) * 128 + cc] = s1[i][r];
+          sP[(w * 2 + 1) * 128 + cc] = s2[i][r];
+        }
+    }
+  }
+  if (g.part == nullptr) return;
+  __syncthreads();
+  {
+    const int k2 = tid >> 7, ch = tid & 127;
+    const float s = ((sP[(0 * 2 + k2) * 128 + ch] + sP[(1 * 2 + k2) * 128 + ch]) + sP[(2 * 2 + k2) * 128 + ch]) +
+                    sP[(3 * 2 + k2) * 128 + ch];
+    g.part[(size_t)tile * 2 * g.COUT + k2 * g.COUT + n0 + ch] = s;
+  }
+}
+
 // ------------------------------------------------------------------ weight gradient
 __device__ __forceinline__ s16x4 tr_read(const u16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
@@ -1722,7 +2002,17 @@ static int g_wgrad_variant = 0;
 static int g_s1x_dbg = 0;          // knob 4: k_conv3x3x timing experiments (0 = the real kernel)
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
-// k_conv3x3x (16x32-pixel tiles) for 128-multiple outputs unless another S1 kernel is forced
+// 128-multiple outputs, by shape: k_conv3x3y (two 4-wave 16x16 blocks per CU) when its grid is more than
+// one round of the 2 x CUs block slots (SECOND's 200x176 layers: 858 / 1716 blocks; 128->128 73.6 -> 68.4,
+// 128->256 130.0 -> 114.0 us vs k_conv3x3x), else k_conv3x3x (16x32 tiles, one 8-wave block per CU:
+// 100x88 256->256, 504 16x16 blocks = 0.98 rounds: 59.8 -> 57.6 us) — profiles/r03_conv_bench_y1.log
+static bool s1_ybig(const int* r_img, int cout) {
+  const long long blocks = (long long)r_img[0] * ((r_img[1] + CT - 1) / CT) * ((r_img[2] + CT - 1) / CT) * (cout / 128);
+  return blocks > 2LL * cu_count();
+}
+static bool s1_ytwo(const int* r_img, int cout) {
+  return cout % 128 == 0 && (g_s1_variant == 4 || (g_s1_variant == 0 && s1_ybig(r_img, cout)));
+}
 static bool s1_xwide(int cout) { return cout % 128 == 0 && (g_s1_variant == 0 || g_s1_variant == 3); }
 
 static bool s1_wide(int tiles, int cout) {
@@ -1776,8 +2066,12 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   if (map == M_S1) {
     const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
     C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
-    if (s1_xwide(g.COUT) && g.CIN % XBK == 0 && (long long)g.M * g.SP * 2 < (1LL << 31) &&
-        9LL * g.COUT * g.CIN * 2 < (1LL << 31)) {
+    const bool fits32 = (long long)g.M * g.SP * 2 < (1LL << 31) && 9LL * g.COUT * g.CIN * 2 < (1LL << 31);
+    const int rimg[3] = {g.R.B, g.R.H, g.R.W};
+    if (s1_ytwo(rimg, g.COUT) && fits32) {
+      hipLaunchKernelGGL(k_conv3x3y<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(YB), 0, st, c);
+    } else if (s1_xwide(g.COUT)) {
+      if (!fits32) return RPC_ERR_UNSUPPORTED;   // 32-bit buffer offsets (part rows are those of 16x32 tiles)
       c.TX = (g.R.W + XTW - 1) / XTW;
       const dim3 grid(g.R.B * TY * c.TX * (g.COUT / 128));
       switch (g_s1x_dbg) {
@@ -1823,13 +2117,14 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
 extern "C" int rpc_dense_conv_s1_kernel(int map, int cout, const int* r_img) {
   if (map != M_S1 || !r_img || cout % 64) return -1;
   const int TY = (r_img[1] + CT - 1) / CT, TX = (r_img[2] + CT - 1) / CT;
+  if (s1_ytwo(r_img, cout)) return 3;
   if (s1_xwide(cout)) return 2;
   return s1_wide(r_img[0] * TY * TX, cout) ? 1 : 0;
 }
 
 extern "C" int rpc_dense_conv_part_rows(int map, int cout, const int* r_img) {
   if (!r_img || map < M_S1 || map > M_G2) return -1;
-  if (map == M_S1 && s1_xwide(cout))   // one row per 16x32 tile
+  if (map == M_S1 && !s1_ytwo(r_img, cout) && s1_xwide(cout))   // one row per 16x32 tile
     return r_img[0] * ((r_img[1] + CT - 1) / CT) * ((r_img[2] + XTW - 1) / XTW);
   return rpc_dense_conv_blocks(map, r_img);
 }

@@ -48,7 +48,7 @@ class ConvTimer:
         e.record(torch.cuda.current_stream())
         return e
 
-    KERNELS = {0: "rpc::dn::k_conv3x3<0>", 1: "rpc::dn::k_conv3x3w<0>", 2: "rpc::dn::k_conv3x3x<0>"}
+    KERNELS = {0: "rpc::dn::k_conv3x3<0>", 1: "rpc::dn::k_conv3x3w<0>", 2: "rpc::dn::k_conv3x3x<0>", 3: "rpc::dn::k_conv3x3y<0>"}
 
     def stop(self, e0, rows, ci, co, variant=0):
         e1 = torch.cuda.Event(enable_timing=True)

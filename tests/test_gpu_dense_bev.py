@@ -378,8 +378,10 @@ def test_s1_lds_dma_kernel_bitexact_vs_register_staged(ci, co, B, H, W):
                                          (128, 128, 1, 16, 32), (256, 128, 2, 37, 45), (128, 256, 2, 33, 17),
                                          (128, 128, 3, 24, 40), (128, 256, 1, 9, 130), (384, 128, 1, 21, 70),
                                          (192, 128, 1, 19, 33)])
-def test_s1_wide_tile_kernel(ci, co, B, H, W):
-    """k_conv3x3x (16x32-pixel tiles, 32-channel K-steps, rpc_dense_tune knob 0 = 3) against float64 torch on
+@pytest.mark.parametrize("variant", [3, 4])
+def test_s1_wide_tile_kernel(ci, co, B, H, W, variant):
+    """k_conv3x3x (16x32-pixel tiles, 32-channel K-steps, rpc_dense_tune knob 0 = 3) and k_conv3x3y (two
+    4-wave 16x16 blocks per CU, knob 0 = 4) against float64 torch on
     the same bf16 operands: output within 1 bf16 ulp of the output scale, the accumulate path likewise,
     BatchNorm partials = column sums / sums of squares of the stored values over exactly
     rpc_dense_conv_part_rows rows (later rows untouched), and the output within 1 bf16 ulp of k_conv3x3's
@@ -394,11 +396,11 @@ def test_s1_wide_tile_kernel(ci, co, B, H, W):
     base = _rand(B, co, H, W, seed=33)
     ref = F.conv2d(x.double(), Wt.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
     outs = {}
-    for variant in (3, 1):
-        old = lib.rpc_dense_tune(0, variant)
+    for v in (variant, 1):
+        old = lib.rpc_dense_tune(0, v)
         try:
-            if variant == 3:
-                assert lib.rpc_dense_conv_s1_kernel(S1, co, _ffi.int_arr(img)) == 2
+            if v != 1:
+                assert lib.rpc_dense_conv_s1_kernel(S1, co, _ffi.int_arr(img)) == v - 1
             rows = lib.rpc_dense_conv_part_rows(S1, co, _ffi.int_arr(img))
             z, part = _conv(S1, _nhwc(x), ci, wf, co, img, img, img, stats=True)
             acc = _nhwc(base).reshape(-1, co).clone()
@@ -408,8 +410,8 @@ def test_s1_wide_tile_kernel(ci, co, B, H, W):
             lib.rpc_dense_tune(0, old)
         assert 1 <= rows <= part.shape[0]
         assert torch.all(part[rows:] == 0)
-        outs[variant] = (z, acc, part[:rows].double().sum(0))
-    z, acc, sp = outs[3]
+        outs[v] = (z, acc, part[:rows].double().sum(0))
+    z, acc, sp = outs[variant]
     _close_bf16(z, ref)
     _close_bf16(acc, ref + base.permute(0, 2, 3, 1).reshape(-1, co).double())
     _close_bf16(z, outs[1][0])

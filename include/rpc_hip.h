@@ -307,6 +307,15 @@ int rpc_dense_conv_blocks(int map, const int* row_img);
  * 16x32-pixel tile for the S1 kernel k_conv3x3x, else rpc_dense_conv_blocks (the rows rpc_bn_finalize
  * reduces; never more than rpc_dense_conv_blocks) */
 int rpc_dense_conv_part_rows(int map, int cout, const int* row_img);
+/* RPC_DMAP_S1 data gradient (no accumulate, channel offset 0) whose output out = dh is the gradient of a
+ * BatchNorm2d + ReLU layer with pre-activation image bnz [B*H*W][cout] and forward parameters bnp[4*cout]
+ * (scale, beta, mean, invstd): also writes that layer's BatchNorm-backward partial sums (sum dm, sum dm*xhat;
+ * dm = dh * [pre > 0]) to part [rpc_dense_conv_part_rows][2*cout] (rpc_bn_finalize mode 1 reduces them).
+ * Replaces rpc_dense_bnbwd_stats for that layer; RPC_ERR_UNSUPPORTED when the shape takes an S1 kernel
+ * without it (cout not a multiple of 128, images >= 2 GB) */
+int rpc_dense_conv_bnbwd(const void* src, int src_pitch, int cin, const void* wt, int cout, void* out,
+                         int out_pitch, const void* bnz, const float* bnp, float* part, const int* row_img,
+                         void* stream);
 /* which kernel rpc_dense_conv launches for an RPC_DMAP_S1 call with `cout` outputs over row_img:
  * 0 = rpc::dn::k_conv3x3<0> (64-channel blocks), 1 = rpc::dn::k_conv3x3w<0> (128-channel LDS-DMA
  * blocks), 2 = rpc::dn::k_conv3x3x<0> (16x32-pixel x 128-channel LDS-DMA blocks), -1 = not an S1 call (per-kernel roofline attribution in bench.py) */

@@ -148,6 +148,7 @@ SIGNATURES = {
     "rpc_dense_conv_blocks": (i32, [i32, ip]),
     "rpc_dense_conv_s1_kernel": (i32, [i32, i32, ip]),
     "rpc_dense_conv_part_rows": (i32, [i32, i32, ip]),
+    "rpc_dense_conv_bnbwd": (i32, [vp, i32, i32, vp, i32, vp, i32, vp, vp, vp, ip, vp]),
     "rpc_dense_tune": (i32, [i32, i32]),
     "rpc_dense_wgrad_workspace_size": (sz, [i32, ip, i32, i32]),
     "rpc_dense_wgrad": (i32, [i32, i32, vp, i32, i32, vp, i32, i32, ip, ip, ip, vp, vp, sz, vp]),

@@ -337,7 +337,7 @@ class CenterHeadFn(torch.autograd.Function):
                                                 _ffi.ptr(uws), uwsz, st), "rpc_head_unpack_grad")
             dh, dW = _conv_nobn_bwd(lib, frec, dz, dev, st)
             grads[id(conv.weight)], grads[id(conv.bias)] = dW, db_
-            dfeat, dWc, dg, dbt = db._backward_layer(db._Eng(lib, False), rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
+            dfeat, dWc, dg, dbt, _ = db._backward_layer(db._Eng(lib, False), rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
             L = rec_cm["L"]
             grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWc, dg, dbt
             return dfeat
@@ -365,7 +365,7 @@ class CenterHeadFn(torch.autograd.Function):
                 grads[id(dcn.conv_offset.weight)] = dWo
         dY0 = (dY0f + dY0b.permute(0, 2, 3, 1).reshape(cells, 64).float()).to(torch.bfloat16)
         dY0 = dY0.view(B, H, W, 64).permute(0, 3, 1, 2)
-        dx, dWs, dgs, dbs = db._backward_layer(db._Eng(lib, False), ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
+        dx, dWs, dgs, dbs, _ = db._backward_layer(db._Eng(lib, False), ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
         L = ctx.rsh["L"]
         grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWs, dgs, dbs
         ctx.trecs = ctx.rsh = None

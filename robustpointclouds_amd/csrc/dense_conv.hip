@@ -287,6 +287,11 @@ struct C3 {
   int OP, OOFF, accum;
   float* part;     // [tiles][2*COUT] or null
   int B, H, W, TY, TX;   // image, tiles per column / row
+  // k_conv3x3x / y data gradients only (rpc_dense_conv_bnbwd): the output is dh of a BatchNorm + ReLU layer
+  // with pre-activation image bnz [B*H*W][COUT] and forward parameters bnp (scale, beta, mean, invstd);
+  // part then receives that layer's BatchNorm-backward partial sums (sum dm, sum dm * xhat), dm = dh * [pre > 0]
+  const u16* bnz;
+  const float* bnp;
 };
 
 template <int DUMMY = 0>
@@ -949,17 +954,41 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
     }
     __syncthreads();
     const int c = tid & 15, px = tid >> 4;   // 16-byte chunk (8 channels) c of column px of every tile row
-    float t1[8], t2[8];
+    float t1[8], t2[8], bsc[8], bbe[8], bmu[8], bis[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) t1[e] = t2[e] = 0.f;
+    if (g.bnz != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = n0 + c * 8 + e;
+        bsc[e] = g.bnp[ch];
+        bbe[e] = g.bnp[g.COUT + ch];
+        bmu[e] = g.bnp[2 * g.COUT + ch];
+        bis[e] = g.bnp[3 * g.COUT + ch];
+      }
+    }
     const int x = tx0 + px;
 #pragma unroll 4
     for (int k = 0; k < CT; ++k) {
       const int y = ty0 + k, p = k * XTW + px;
       if (y >= g.H || x >= g.W) continue;
+      const size_t pix = (size_t)(b * g.H + y) * g.W + x;
       const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
-      *(uint4*)(g.out + ((size_t)(b * g.H + y) * g.W + x) * g.OP + g.OOFF + n0 + c * 8) = v;
+      *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
       const unsigned u[4] = {v.x, v.y, v.z, v.w};
+      if (g.bnz != nullptr) {   // BatchNorm-backward sums of the layer this gradient enters
+        const uint4 zv = *(const uint4*)(g.bnz + pix * g.COUT + n0 + c * 8);
+        const unsigned zu[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float zz = bf2f((u16)(zu[e >> 1] >> (16 * (e & 1)))), d0 = bf2f((u16)(u[e >> 1] >> (16 * (e & 1))));
+          const float pre = fmaf(zz - bmu[e], bsc[e], bbe[e]);
+          const float d = pre > 0.f ? d0 : 0.f;
+          t1[e] += d;
+          t2[e] += d * ((zz - bmu[e]) * bis[e]);
+        }
+        continue;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float f0 = bf2f((u16)(u[e] & 0xffff)), f1 = bf2f((u16)(u[e] >> 16));
@@ -1227,17 +1256,41 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     }
     __syncthreads();
     const int c = tid & 15, px = tid >> 4;   // 16-byte chunk c of column px of every tile row
-    float t1[8], t2[8];
+    float t1[8], t2[8], bsc[8], bbe[8], bmu[8], bis[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) t1[e] = t2[e] = 0.f;
+    if (g.bnz != nullptr) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ch = n0 + c * 8 + e;
+        bsc[e] = g.bnp[ch];
+        bbe[e] = g.bnp[g.COUT + ch];
+        bmu[e] = g.bnp[2 * g.COUT + ch];
+        bis[e] = g.bnp[3 * g.COUT + ch];
+      }
+    }
     const int x = tx0 + px;
 #pragma unroll 4
     for (int k = 0; k < CT; ++k) {
       const int y = ty0 + k, p = k * CT + px;
       if (y >= g.H || x >= g.W) continue;
+      const size_t pix = (size_t)(b * g.H + y) * g.W + x;
       const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
-      *(uint4*)(g.out + ((size_t)(b * g.H + y) * g.W + x) * g.OP + g.OOFF + n0 + c * 8) = v;
+      *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
       const unsigned u[4] = {v.x, v.y, v.z, v.w};
+      if (g.bnz != nullptr) {   // BatchNorm-backward sums of the layer this gradient enters
+        const uint4 zv = *(const uint4*)(g.bnz + pix * g.COUT + n0 + c * 8);
+        const unsigned zu[4] = {zv.x, zv.y, zv.z, zv.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float zz = bf2f((u16)(zu[e >> 1] >> (16 * (e & 1)))), d0 = bf2f((u16)(u[e >> 1] >> (16 * (e & 1))));
+          const float pre = fmaf(zz - bmu[e], bsc[e], bbe[e]);
+          const float d = pre > 0.f ? d0 : 0.f;
+          t1[e] += d;
+          t2[e] += d * ((zz - bmu[e]) * bis[e]);
+        }
+        continue;
+      }
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float f0 = bf2f((u16)(u[e] & 0xffff)), f1 = bf2f((u16)(u[e] >> 16));
@@ -2047,6 +2100,41 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   return RPC_ERR_ARG;
 }
 
+// the S1 kernels; bnz / bnp (k_conv3x3x / y only, checked by the caller): BatchNorm-backward partial sums
+// of the layer the output gradient enters, instead of the output's own statistics
+static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t st) {
+  const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
+  C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX,
+       bnz, bnp};
+  const bool fits32 = (long long)g.M * g.SP * 2 < (1LL << 31) && 9LL * g.COUT * g.CIN * 2 < (1LL << 31);
+  const int rimg[3] = {g.R.B, g.R.H, g.R.W};
+  if (s1_ytwo(rimg, g.COUT) && fits32) {
+    hipLaunchKernelGGL(k_conv3x3y<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(YB), 0, st, c);
+  } else if (s1_xwide(g.COUT)) {
+    if (!fits32) return RPC_ERR_UNSUPPORTED;   // 32-bit buffer offsets (part rows are those of 16x32 tiles)
+    c.TX = (g.R.W + XTW - 1) / XTW;
+    const dim3 grid(g.R.B * TY * c.TX * (g.COUT / 128));
+    switch (g_s1x_dbg) {
+      case 1: hipLaunchKernelGGL(k_conv3x3x<1>, grid, dim3(WB), 0, st, c); break;
+      case 3: hipLaunchKernelGGL(k_conv3x3x<3>, grid, dim3(WB), 0, st, c); break;
+      case 12: hipLaunchKernelGGL(k_conv3x3x<12>, grid, dim3(WB), 0, st, c); break;
+      case 13: hipLaunchKernelGGL(k_conv3x3x<13>, grid, dim3(WB), 0, st, c); break;
+      case 30: hipLaunchKernelGGL(k_conv3x3x<30>, grid, dim3(WB), 0, st, c); break;
+      case 31: hipLaunchKernelGGL(k_conv3x3x<31>, grid, dim3(WB), 0, st, c); break;
+      case 32: hipLaunchKernelGGL(k_conv3x3x<32>, grid, dim3(WB), 0, st, c); break;
+      default: hipLaunchKernelGGL(k_conv3x3x<0>, grid, dim3(WB), 0, st, c);
+    }
+  } else if (bnz != nullptr) {
+    return RPC_ERR_UNSUPPORTED;
+  } else if (s1_wide(g.R.B * TY * TX, g.COUT)) {
+    hipLaunchKernelGGL(k_conv3x3w<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(WB), 0, st, c);
+  } else {
+    hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
+  }
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
 extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const void* wt, int cout, void* out, int op,
                               int ooff, int accum, float* part, const int* r_img, const int* s_img,
                               const int* o_img, void* stream) {
@@ -2063,42 +2151,7 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   g.flat = g_ig_order == 0 && cout / TN == 2;
   if (g.M == 0) return RPC_OK;
   hipStream_t st = (hipStream_t)stream;
-  if (map == M_S1) {
-    const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
-    C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX};
-    const bool fits32 = (long long)g.M * g.SP * 2 < (1LL << 31) && 9LL * g.COUT * g.CIN * 2 < (1LL << 31);
-    const int rimg[3] = {g.R.B, g.R.H, g.R.W};
-    if (s1_ytwo(rimg, g.COUT) && fits32) {
-      hipLaunchKernelGGL(k_conv3x3y<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(YB), 0, st, c);
-    } else if (s1_xwide(g.COUT)) {
-      if (!fits32) return RPC_ERR_UNSUPPORTED;   // 32-bit buffer offsets (part rows are those of 16x32 tiles)
-      c.TX = (g.R.W + XTW - 1) / XTW;
-      const dim3 grid(g.R.B * TY * c.TX * (g.COUT / 128));
-      switch (g_s1x_dbg) {
-        case 1: hipLaunchKernelGGL(k_conv3x3x<1>, grid, dim3(WB), 0, st, c); break;
-        case 2: hipLaunchKernelGGL(k_conv3x3x<2>, grid, dim3(WB), 0, st, c); break;
-        case 3: hipLaunchKernelGGL(k_conv3x3x<3>, grid, dim3(WB), 0, st, c); break;
-        case 4: hipLaunchKernelGGL(k_conv3x3x<4>, grid, dim3(WB), 0, st, c); break;
-        case 8: hipLaunchKernelGGL(k_conv3x3x<8>, grid, dim3(WB), 0, st, c); break;
-        case 12: hipLaunchKernelGGL(k_conv3x3x<12>, grid, dim3(WB), 0, st, c); break;
-        case 13: hipLaunchKernelGGL(k_conv3x3x<13>, grid, dim3(WB), 0, st, c); break;
-        case 14: hipLaunchKernelGGL(k_conv3x3x<14>, grid, dim3(WB), 0, st, c); break;
-        case 28: hipLaunchKernelGGL(k_conv3x3x<28>, grid, dim3(WB), 0, st, c); break;
-        case 30: hipLaunchKernelGGL(k_conv3x3x<30>, grid, dim3(WB), 0, st, c); break;
-        case 29: hipLaunchKernelGGL(k_conv3x3x<29>, grid, dim3(WB), 0, st, c); break;
-        case 32: hipLaunchKernelGGL(k_conv3x3x<32>, grid, dim3(WB), 0, st, c); break;
-        case 62: hipLaunchKernelGGL(k_conv3x3x<62>, grid, dim3(WB), 0, st, c); break;
-        case 63: hipLaunchKernelGGL(k_conv3x3x<63>, grid, dim3(WB), 0, st, c); break;
-        case 31: hipLaunchKernelGGL(k_conv3x3x<31>, grid, dim3(WB), 0, st, c); break;
-        default: hipLaunchKernelGGL(k_conv3x3x<0>, grid, dim3(WB), 0, st, c);
-      }
-    } else if (s1_wide(g.R.B * TY * TX, g.COUT))
-      hipLaunchKernelGGL(k_conv3x3w<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(WB), 0, st, c);
-    else
-      hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
-    RPC_LAUNCH_CHECK();
-    return RPC_OK;
-  }
+  if (map == M_S1) return launch_s1(g, nullptr, nullptr, st);
   switch (map) {
     case M_S1: launch_igemm<M_S1>(g, 1, st); break;
     case M_S2: launch_igemm<M_S2>(g, 1, st); break;
@@ -2112,6 +2165,21 @@ extern "C" int rpc_dense_conv(int map, const void* src, int sp, int cin, const v
   }
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+// S1 data gradient whose output dh enters a BatchNorm + ReLU layer: also that layer's BatchNorm-backward
+// partial sums (replaces rpc_dense_bnbwd_stats for it; part: [rpc_dense_conv_part_rows][2*cout])
+extern "C" int rpc_dense_conv_bnbwd(const void* src, int sp, int cin, const void* wt, int cout, void* out, int op,
+                                    const void* bnz, const float* bnp, float* part, const int* r_img, void* stream) {
+  if (!src || !wt || !out || !r_img || !bnz || !bnp || !part) return RPC_ERR_ARG;
+  if (cin % BK || cout % 128 || sp < cin || op < cout || (sp & 7) || (op & 7)) return RPC_ERR_ARG;
+  if (!s1_ytwo(r_img, cout) && !s1_xwide(cout)) return RPC_ERR_UNSUPPORTED;
+  IG g{(const u16*)src, sp, cin, (const u16*)wt, cout, (u16*)out, op, 0, 0, part, img3(r_img), img3(r_img),
+       img3(r_img), 0};
+  g.M = g.R.B * g.R.H * g.R.W;
+  if ((long long)g.M * g.SP * 2 >= (1LL << 31) || 9LL * g.COUT * g.CIN * 2 >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
+  if (g.M == 0) return RPC_OK;
+  return launch_s1(g, (const u16*)bnz, bnp, (hipStream_t)stream);
 }
 
 extern "C" int rpc_dense_conv_s1_kernel(int map, int cout, const int* r_img) {

@@ -216,6 +216,21 @@ def _conv(lib, fmap, *args):
     return rc
 
 
+RPC_ERR_UNSUPPORTED = 3
+
+
+def _conv_bnbwd(lib, *args):
+    """rpc_dense_conv_bnbwd (an S1 data gradient + the BatchNorm-backward sums of the layer it enters), timed
+    like _conv's S1 launches when a ConvTimer is enabled. Returns the rpc status."""
+    t = TIMER if (TIMER is not None and TIMER.enabled and not _capturing() and args[4] % 128 == 0) else None
+    e0 = t.start() if t is not None else None
+    rc = lib.rpc_dense_conv_bnbwd(*args)
+    if t is not None and rc == 0:
+        r = _ffi_img_rows(args[10])
+        t.stop(e0, r, args[2], args[4], lib.rpc_dense_conv_s1_kernel(S1, args[4], args[10]))
+    return rc
+
+
 def _ffi_img_rows(arr):
     return int(arr[0]) * int(arr[1]) * int(arr[2])
 
@@ -358,15 +373,24 @@ def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
     return y, rec, Ho, Wo
 
 
-def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False):
-    """BN+ReLU backward, weight gradient and (optionally) data gradient of one layer."""
+def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False,
+                    bn_part=None, next_rec=None):
+    """BN+ReLU backward, weight gradient and (optionally) data gradient of one layer.
+    bn_part: this layer's BatchNorm-backward partial sums, already written by the data-gradient conv that
+    produced dh (rpc_dense_conv_bnbwd) — else rpc_dense_bnbwd_stats computes them. next_rec: the layer the
+    data gradient dx enters (its BN + ReLU backward is next): an S1 bf16 data gradient then writes that
+    layer's partial sums too, returned as the 5th value (None when not fused)."""
     lib = eng.lib
     L = rec["L"]
     Mo, co, ci = rec["Mo"], L.co, L.ci
-    nb = lib.rpc_dense_bnbwd_blocks(Mo)
-    part = torch.empty((nb, 2 * co), dtype=torch.float32, device=dev)
-    _ffi.check(eng.bnbwd_stats(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
-                                         _ffi.ptr(rec["bn"]), _ffi.ptr(part), st), "rpc_dense_bnbwd_stats")
+    if bn_part is not None:
+        part = bn_part
+        nb = part.shape[0]
+    else:
+        nb = lib.rpc_dense_bnbwd_blocks(Mo)
+        part = torch.empty((nb, 2 * co), dtype=torch.float32, device=dev)
+        _ffi.check(eng.bnbwd_stats(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
+                                   _ffi.ptr(rec["bn"]), _ffi.ptr(part), st), "rpc_dense_bnbwd_stats")
     bnb = torch.empty(5 * co, dtype=torch.float32, device=dev)
     dgamma = torch.empty(co, dtype=torch.float32, device=dev)
     dbeta = torch.empty(co, dtype=torch.float32, device=dev)
@@ -387,6 +411,7 @@ def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
     _ffi.check(eng.wgrad(L.map, L.kind, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), co, co,
                                    ri, si, oi, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
     dx = None
+    next_part = None
     if need_dx:
         dmap = L.dgrad_map()
         B, H, W = rec["S"]
@@ -396,10 +421,22 @@ def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
             rd, sd = rec["R"], rec["O"]
         else:
             rd, sd = rec["S"], rec["O"]
-        _ffi.check(eng.conv(dmap, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
-                            1 if accumulate else 0, None, _ffi.int_arr(rd), _ffi.int_arr(sd),
-                            _ffi.int_arr(rd), st), "rpc_dense_conv(dgrad)")
-    return dx, dW, dgamma, dbeta
+        rc = None
+        if next_rec is not None and not eng.f32 and dmap == S1 and not accumulate and next_rec["L"].co == ci:
+            ri_d = _ffi.int_arr(rd)
+            next_part = torch.empty((lib.rpc_dense_conv_part_rows(S1, ci, ri_d), 2 * ci), dtype=torch.float32,
+                                    device=dev)
+            rc = _conv_bnbwd(lib, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci,
+                             _ffi.ptr(next_rec["z"]), _ffi.ptr(next_rec["bn"]), _ffi.ptr(next_part), ri_d, st)
+            if rc == RPC_ERR_UNSUPPORTED:
+                next_part = None
+            else:
+                _ffi.check(rc, "rpc_dense_conv_bnbwd")
+        if next_part is None:
+            _ffi.check(eng.conv(dmap, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
+                                1 if accumulate else 0, None, _ffi.int_arr(rd), _ffi.int_arr(sd),
+                                _ffi.int_arr(rd), st), "rpc_dense_conv(dgrad)")
+    return dx, dW, dgamma, dbeta, next_part
 
 
 def second_layers(mod):
@@ -468,6 +505,7 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
         if dh is None:   # nothing flows through this block
             dh = _nhwc(gouts[bi - 1], dt) if bi > 0 and gouts[bi - 1] is not None else None
             continue
+        bn_part = None   # the block's last layer: its dh comes from outside the block
         for li in range(len(brecs) - 1, -1, -1):
             rec = brecs[li]
             dx_out, accumulate = None, False
@@ -483,8 +521,9 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
                     accumulate = True
             else:
                 need_dx = need_x
-            dh, dW, dgam, dbet = _backward_layer(eng, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
-                                                 accumulate)
+            dh, dW, dgam, dbet, bn_part = _backward_layer(eng, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
+                                                          accumulate, bn_part=bn_part,
+                                                          next_rec=brecs[li - 1] if li > 0 else None)
             grads[id(rec["L"].conv.weight)] = dW
             grads[id(rec["L"].bnm.weight)] = dgam
             grads[id(rec["L"].bnm.bias)] = dbet
@@ -599,7 +638,7 @@ class NeckFn(torch.autograd.Function):
                 B, H, W = rec["S"]
                 dx_out = _scratch_image(ctx.cache, ("fpn_dx", i, B, L.ci, H, W, eng.dt, dev), B, L.ci, H, W,
                                         dev, eng.dt)
-            dx, dW, dgam, dbet = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True, dx_out)
+            dx, dW, dgam, dbet, _ = _backward_layer(eng, rec, g, ctx.Ctot, rec["off"], dev, st, True, dx_out)
             grads[id(L.conv.weight)] = dW
             grads[id(L.bnm.weight)] = dgam
             grads[id(L.bnm.bias)] = dbet

@@ -421,6 +421,63 @@ def test_s1_wide_tile_kernel(ci, co, B, H, W, variant):
     assert torch.all((sp - want).abs() <= 1e-5 * scale + 1e-6)
 
 
+@pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 6, 200, 176), (256, 128, 6, 200, 176), (256, 256, 6, 100, 88),
+                                         (128, 128, 2, 24, 40), (128, 256, 1, 9, 130)])
+def test_s1_dgrad_with_fused_bn_backward_sums(ci, co, B, H, W):
+    """rpc_dense_conv_bnbwd: the S1 data gradient writes the same dh as rpc_dense_conv (bit-identical) and,
+    per tile, the BatchNorm-backward partial sums of the layer dh enters (sum dm, sum dm * xhat with
+    dm = dh * [(z - mean) * scale + beta > 0]) — the column totals equal a float64 computation on the same
+    bf16 dh / z values to fp32 summation accuracy, and rpc_bn_finalize(mode 1) over them matches it over
+    rpc_dense_bnbwd_stats' partials."""
+    lib = _ffi.load()
+    x = _rand(B, ci, H, W, seed=41)
+    Wt = _rand(co, ci, 3, 3, seed=42, scale=0.05)
+    wf, _ = _wprep(Wt, 0, 9, 1)
+    img = (B, H, W)
+    M = B * H * W
+    z = _nhwc(_rand(B, co, H, W, seed=43)).reshape(M, co)
+    g = torch.Generator().manual_seed(44)
+    mean = (torch.randn(co, generator=g) * 0.1).to(DEV)
+    invstd = (torch.rand(co, generator=g) + 0.5).to(DEV)
+    gamma = (torch.rand(co, generator=g) + 0.5).to(DEV)
+    beta = (torch.randn(co, generator=g) * 0.2).to(DEV)
+    bn = torch.cat([gamma * invstd, beta, mean, invstd]).float().contiguous()
+    ri = _ffi.int_arr(img)
+    rows = lib.rpc_dense_conv_part_rows(S1, co, ri)
+    part = torch.zeros((rows, 2 * co), device=DEV)
+    dh = torch.empty((M, co), dtype=torch.bfloat16, device=DEV)
+    xs = _nhwc(x)
+    _ffi.check(lib.rpc_dense_conv_bnbwd(_ffi.ptr(xs), ci, ci, _ffi.ptr(wf), co, _ffi.ptr(dh), co, _ffi.ptr(z),
+                                        _ffi.ptr(bn), _ffi.ptr(part), ri, _ffi.stream_of(dh)), "rpc_dense_conv_bnbwd")
+    plain, _ = _conv(S1, xs, ci, wf, co, img, img, img)
+    torch.cuda.synchronize()
+    assert torch.equal(dh, plain)
+    zd, dd = z.double(), dh.double()
+    pre = (zd - mean.double()) * (gamma * invstd).double() + beta.double()
+    dm = torch.where(pre > 0, dd, torch.zeros_like(dd))
+    xhat = (zd - mean.double()) * invstd.double()
+    want = torch.cat([dm.sum(0), (dm * xhat).sum(0)])
+    scale = torch.cat([dm.abs().sum(0), (dm * xhat).abs().sum(0)])
+    got = part.double().sum(0)
+    assert torch.all((got - want).abs() <= 1e-5 * scale + 1e-6)
+    # finalize over the fused partials vs over rpc_dense_bnbwd_stats' partials
+    nb = lib.rpc_dense_bnbwd_blocks(M)
+    part2 = torch.empty((nb, 2 * co), device=DEV)
+    _ffi.check(lib.rpc_dense_bnbwd_stats(_ffi.ptr(dh), co, 0, _ffi.ptr(z), M, co, _ffi.ptr(bn), _ffi.ptr(part2),
+                                         _ffi.stream_of(dh)), "bnbwd_stats")
+    outs = []
+    for pp, n in ((part, rows), (part2, nb)):
+        bnb = torch.empty(5 * co, device=DEV)
+        dg = torch.empty(co, device=DEV)
+        db = torch.empty(co, device=DEV)
+        _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(pp), n, co, M, 1, _ffi.ptr(gamma), _ffi.ptr(beta), 0.0, 0.0, None,
+                                       None, _ffi.ptr(bn), _ffi.ptr(bnb), _ffi.ptr(dg), _ffi.ptr(db), None,
+                                       _ffi.stream_of(dh)), "finalize")
+        outs.append((bnb, dg, db))
+    for a, b_ in zip(*outs):
+        torch.testing.assert_close(a, b_, rtol=1e-5, atol=1e-5 * float(b_.abs().max()) + 1e-7)
+
+
 @pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 1, 200, 176), (256, 256, 1, 100, 88), (256, 128, 2, 37, 45),
                                          (128, 128, 2, 17, 70), (128, 256, 1, 5, 130)])
 def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):

@@ -25,6 +25,7 @@
 // fp32 slabs reduced in a fixed order (k_slab_reduce). BatchNorm apply / backward are
 // vectorised elementwise passes (8 channels per thread).
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <algorithm>
@@ -85,8 +86,12 @@ template <int MAP>
 __global__ __launch_bounds__(BLK, (taps_of<MAP>() == 1 ? 4 : 2)) void k_igemm(IG g) {
   constexpr int T = taps_of<MAP>();
   constexpr int NB = T == 1 ? 1 : 2;
-  __shared__ __attribute__((aligned(16))) u16 sX[NB][TM * LP];
-  __shared__ __attribute__((aligned(16))) u16 sW[NB][TN * LP];
+  // the operand tiles, and after the K-loop the bf16 output tile [TM][TN] of the epilogue (32 KB)
+  constexpr int TILEB = NB * (TM + TN) * LP * 2;
+  static_assert(TILEB >= TM * TN * 2, "epilogue staging");
+  __shared__ __attribute__((aligned(16))) unsigned char ldsb[TILEB];
+  u16 (*sX)[TM * LP] = (u16 (*)[TM * LP])ldsb;
+  u16 (*sW)[TN * LP] = (u16 (*)[TN * LP])(ldsb + NB * TM * LP * 2);
   __shared__ int sRow[TM * T];
   __shared__ float sP[2][2][TN];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -193,6 +198,76 @@ __global__ __launch_bounds__(BLK, (taps_of<MAP>() == 1 ? 4 : 2)) void k_igemm(IG
 #undef IG_STORE
 
   // epilogue: lane holds channels co = n0 + wc*64 + i*16 + 4*(lane>>4) + r of pixel wp*64 + j*16 + (lane&15)
+  if (!g.accum) {
+    // staged through LDS as whole 256-byte pixel rows (granule gr of pixel p at slot gr ^ (p & 15)) and
+    // written 16 bytes per lane: the 8-byte stores of the accumulator layout touch 16 rows per instruction
+    // (store-issue bound, k_conv3x3x); BatchNorm sums from the stored bf16 values
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int p = wp * 64 + j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int q4 = lane >> 4, gr = (wc * 8 + i * 2 + (q4 >> 1)) ^ (p & 15);
+        const unsigned lo = (unsigned)f2bf(acc[i][j][0]) | ((unsigned)f2bf(acc[i][j][1]) << 16);
+        const unsigned hi = (unsigned)f2bf(acc[i][j][2]) | ((unsigned)f2bf(acc[i][j][3]) << 16);
+        *(uint2*)(ldsb + p * 256 + gr * 16 + (q4 & 1) * 8) = make_uint2(lo, hi);
+      }
+    }
+    __syncthreads();
+    const int c = tid & 15, pq = tid >> 4;
+    float t1[8], t2[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) t1[e] = t2[e] = 0.f;
+#pragma unroll 4
+    for (int k = 0; k < TM / 16; ++k) {
+      const int p = pq + 16 * k, m = m0 + p;
+      if (m >= Mrows) continue;
+      int orow = m;
+      if (MAP == M_U2) {
+        const int b = m / HW, rem = m - b * HW, y = rem / g.R.W, x = rem - y * g.R.W;
+        orow = out_row<MAP>(m, b, y, x, par, g.O);
+      } else if (MAP == M_D2P) {
+        const int b = m / (Hp * Wp), rem = m - b * (Hp * Wp), yy = rem / Wp, xx = rem - yy * Wp;
+        orow = (b * g.R.H + 2 * yy + py) * g.R.W + 2 * xx + px;
+      }
+      const uint4 v = *(const uint4*)(ldsb + p * 256 + ((c ^ (p & 15)) * 16));
+      *(uint4*)(g.out + (size_t)orow * g.OP + g.OOFF + n0 + c * 8) = v;
+      const unsigned u[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float f0 = bf2f((u16)(u[e] & 0xffff)), f1 = bf2f((u16)(u[e] >> 16));
+        t1[2 * e] += f0;
+        t2[2 * e] += f0 * f0;
+        t1[2 * e + 1] += f1;
+        t2[2 * e + 1] += f1 * f1;
+      }
+    }
+    if (g.part == nullptr) return;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      t1[e] += __shfl_xor(t1[e], 16, 64);
+      t2[e] += __shfl_xor(t2[e], 16, 64);
+      t1[e] += __shfl_xor(t1[e], 32, 64);
+      t2[e] += __shfl_xor(t2[e], 32, 64);
+    }
+    __syncthreads();   // the tile reads are done: the sums go where it was
+    float* sR = (float*)ldsb;   // [4 waves][2][TN]
+    if (lane < 16) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        sR[(w * 2 + 0) * TN + c * 8 + e] = t1[e];
+        sR[(w * 2 + 1) * TN + c * 8 + e] = t2[e];
+      }
+    }
+    __syncthreads();
+    float* prow = g.part + ((size_t)blockIdx.z * ntiles + bx) * 2 * g.COUT;
+    {
+      const int k2 = tid >> 7, ch = tid & 127;
+      prow[k2 * g.COUT + n0 + ch] = ((sR[(0 * 2 + k2) * TN + ch] + sR[(1 * 2 + k2) * TN + ch]) +
+                                     sR[(2 * 2 + k2) * TN + ch]) + sR[(3 * 2 + k2) * TN + ch];
+    }
+    return;
+  }
   float s1[4][4], s2[4][4];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
@@ -2050,7 +2125,11 @@ static unsigned ew_blocks(long long m, int c) {
 // of the CUs to >= 90 % (SECOND's 100x88 layers: 504 blocks = 0.98 of 2 rounds), else k_conv3x3 (two
 // 64-channel blocks per CU overlap each other's prologue / epilogue; the 200x176 layers' 858 tiles are
 // 0.84 of 4 rounds for either kernel, and there the register-staged kernel measured 3-8 % faster).
-static int g_s1_variant = 0;
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : dflt;
+}
+static int g_s1_variant = env_int("RPC_DENSE_S1", 0);   // A/B: RPC_DENSE_S1=<knob 0 value> for a whole run
 static int g_wgrad_variant = 0;
 static int g_s1x_dbg = 0;          // knob 4: k_conv3x3x timing experiments (0 = the real kernel)
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad

@@ -217,6 +217,8 @@ def _conv(lib, fmap, *args):
 
 
 RPC_ERR_UNSUPPORTED = 3
+# S1 data gradients write the BatchNorm-backward sums of the layer they feed (A/B: RPC_DENSE_BNFUSE=0)
+BN_FUSE = os.environ.get("RPC_DENSE_BNFUSE", "1") != "0"
 
 
 def _conv_bnbwd(lib, *args):
@@ -422,7 +424,8 @@ def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
         else:
             rd, sd = rec["S"], rec["O"]
         rc = None
-        if next_rec is not None and not eng.f32 and dmap == S1 and not accumulate and next_rec["L"].co == ci:
+        if (BN_FUSE and next_rec is not None and not eng.f32 and dmap == S1 and not accumulate and
+                next_rec["L"].co == ci):
             ri_d = _ffi.int_arr(rd)
             next_part = torch.empty((lib.rpc_dense_conv_part_rows(S1, ci, ri_d), 2 * ci), dtype=torch.float32,
                                     device=dev)

@@ -31,10 +31,13 @@ S1, S2, D2, P1, U2, G2 = 0, 1, 2, 3, 4, 5
 
 
 class ConvTimer:
-    """HIP-event timing of the S1 (3x3 stride-1: kernels `rpc::dn::k_conv3x3<0>` and `k_conv3x3w<0>`)
-    launches of rpc_dense_conv — forward and flipped-tap data gradient — on the stream they are launched
-    on. Algorithmic work per launch = 2 * B*H*W * C_in * C_out * 9 FLOP (every tap of a zero-padded
-    3x3 convolution); algorithmic bytes = bf16 source image + bf16 output image + bf16 weights.
+    """HIP-event timing of the S1 (3x3 stride-1: kernels `rpc::dn::k_conv3x3<0>`, `k_conv3x3w<0>`,
+    `k_conv3x3x<0>`, `k_conv3x3y<0>`) launches of rpc_dense_conv — forward and flipped-tap data gradient —
+    on the stream they are launched on. Algorithmic work per launch = 2 * B*H*W * C_in * C_out * 9 FLOP
+    (every tap of a zero-padded 3x3 convolution); algorithmic bytes = bf16 source image + bf16 output
+    image + bf16 weights. Data gradients issued through rpc_dense_conv_bnbwd (the same kernel, whose
+    epilogue also reads the next layer's pre-activation image for its BatchNorm-backward sums: + one bf16
+    image of bytes) are reported as their own entry, "<kernel> +bnbwd".
     bench.py installs one as `dense_bev.TIMER`. Timing events cannot be recorded inside a captured HIP
     graph on ROCm (torch refuses external events), so launches issued during a capture are not timed:
     bench.py times eager steps (graphs off) right after its timed loop — the same kernels and shapes."""
@@ -48,7 +51,9 @@ class ConvTimer:
         e.record(torch.cuda.current_stream())
         return e
 
-    KERNELS = {0: "rpc::dn::k_conv3x3<0>", 1: "rpc::dn::k_conv3x3w<0>", 2: "rpc::dn::k_conv3x3x<0>", 3: "rpc::dn::k_conv3x3y<0>"}
+    KERNELS = {0: "rpc::dn::k_conv3x3<0>", 1: "rpc::dn::k_conv3x3w<0>", 2: "rpc::dn::k_conv3x3x<0>",
+               3: "rpc::dn::k_conv3x3y<0>", 12: "rpc::dn::k_conv3x3x<0> +bnbwd", 13: "rpc::dn::k_conv3x3y<0> +bnbwd"}
+    FUSED = 10   # variant offset of the rpc_dense_conv_bnbwd launches
 
     def stop(self, e0, rows, ci, co, variant=0):
         e1 = torch.cuda.Event(enable_timing=True)
@@ -62,7 +67,8 @@ class ConvTimer:
     def _stats(recs, kernel):
         ms = sum(a.elapsed_time(b) for a, b, *_ in recs)
         flops = sum(2.0 * r * ci * co * 9 for _, _, r, ci, co, _v in recs)
-        byts = sum(2.0 * r * (ci + co) + 2.0 * 9 * ci * co for _, _, r, ci, co, _v in recs)
+        byts = sum(2.0 * r * (ci + co) + 2.0 * 9 * ci * co + (2.0 * r * co if _v >= ConvTimer.FUSED else 0.0)
+                   for _, _, r, ci, co, _v in recs)
         n = len(recs)
         return dict(launches=n, avg_ms=ms / n, flops_per_launch=flops / n, bytes_per_launch=byts / n,
                     tflops=flops / (ms * 1e-3) / 1e12, gbps=byts / (ms * 1e-3) / 1e9, kernel=kernel, dtype="bf16",
@@ -229,7 +235,7 @@ def _conv_bnbwd(lib, *args):
     rc = lib.rpc_dense_conv_bnbwd(*args)
     if t is not None and rc == 0:
         r = _ffi_img_rows(args[10])
-        t.stop(e0, r, args[2], args[4], lib.rpc_dense_conv_s1_kernel(S1, args[4], args[10]))
+        t.stop(e0, r, args[2], args[4], ConvTimer.FUSED + lib.rpc_dense_conv_s1_kernel(S1, args[4], args[10]))
     return rc
 
 

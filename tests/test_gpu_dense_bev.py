@@ -339,6 +339,7 @@ def test_second_fpn_config_shape_fp32_engine_and_bf16_bounds():
         e16[mode] = dict(f=_relL2(o, ref), dx=_cos(d, dref), g=[_cos(a, b) for a, b in zip(g, gref)])
         print(mode, {k: (min(v) if isinstance(v, list) else v) for k, v in e16[mode].items()})
     a, h = e16["autocast"], e16["hip16"]
+    print("per-parameter cosine hip16 - autocast:", [round(ch - ca, 4) for ch, ca in zip(h["g"], a["g"])])
     assert h["f"] <= 1.25 * a["f"], (h["f"], a["f"])
     assert h["dx"] >= a["dx"] - 0.02, (h["dx"], a["dx"])
     assert min(h["g"]) >= min(a["g"]) - 0.01, (min(h["g"]), min(a["g"]))

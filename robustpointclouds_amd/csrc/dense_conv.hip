@@ -1263,7 +1263,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     const int s_ = kc * 9 + (t);                                                                              \
     issue_w(s_ + WDIST);                                                                                      \
     if ((t) == HTAP) issue_halo(min(kc + 1, NKC - 1), (kc + 1) & 1);                                          \
-    if (LIVE) {                                                                                               \
+    if (LIVE && !(DBG & 1)) {                                                                                 \
       const unsigned char* hb_ = hbuf + (kc & 1) * YHBUF;                                                     \
       const unsigned char* wt_ = wring + (s_ & (WRING - 1)) * XWTILE;                                         \
       constexpr int dy_ = (t) / 3, dx_ = (t) % 3;                                                             \
@@ -1283,7 +1283,8 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                     \
     asm volatile("s_barrier" ::: "memory");                                                                   \
   }
-  if (live) {
+  if (DBG & 16) {
+  } else if (live) {
     for (int kc = 0; kc < NKC; ++kc) {
       C3Y_STEP(0, true)
       C3Y_STEP(1, true)
@@ -1351,7 +1352,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       if (y >= g.H || x >= g.W) continue;
       const size_t pix = (size_t)(b * g.H + y) * g.W + x;
       const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
-      *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
+      if (!(DBG & 64)) *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
       const unsigned u[4] = {v.x, v.y, v.z, v.w};
       if (g.bnz != nullptr) {   // BatchNorm-backward sums of the layer this gradient enters
         const uint4 zv = *(const uint4*)(g.bnz + pix * g.COUT + n0 + c * 8);
@@ -2168,7 +2169,7 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   }
   if (knob == 4) {
     const int old = g_s1x_dbg;
-    if (value >= 0 && value <= 63) g_s1x_dbg = value;
+    if (value >= 0 && value <= 127) g_s1x_dbg = value;
     return old;
   }
   if (knob == 2) {
@@ -2188,7 +2189,15 @@ static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t 
   const bool fits32 = (long long)g.M * g.SP * 2 < (1LL << 31) && 9LL * g.COUT * g.CIN * 2 < (1LL << 31);
   const int rimg[3] = {g.R.B, g.R.H, g.R.W};
   if (s1_ytwo(rimg, g.COUT) && fits32) {
-    hipLaunchKernelGGL(k_conv3x3y<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(YB), 0, st, c);
+    const dim3 grid(g.R.B * TY * TX * (g.COUT / 128));
+    switch (g_s1x_dbg) {
+      case 1: hipLaunchKernelGGL(k_conv3x3y<1>, grid, dim3(YB), 0, st, c); break;
+      case 17: hipLaunchKernelGGL(k_conv3x3y<17>, grid, dim3(YB), 0, st, c); break;
+      case 64: hipLaunchKernelGGL(k_conv3x3y<64>, grid, dim3(YB), 0, st, c); break;
+      case 65: hipLaunchKernelGGL(k_conv3x3y<65>, grid, dim3(YB), 0, st, c); break;
+      case 81: hipLaunchKernelGGL(k_conv3x3y<81>, grid, dim3(YB), 0, st, c); break;
+      default: hipLaunchKernelGGL(k_conv3x3y<0>, grid, dim3(YB), 0, st, c);
+    }
   } else if (s1_xwide(g.COUT)) {
     if (!fits32) return RPC_ERR_UNSUPPORTED;   // 32-bit buffer offsets (part rows are those of 16x32 tiles)
     c.TX = (g.R.W + XTW - 1) / XTW;

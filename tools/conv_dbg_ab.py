@@ -9,7 +9,7 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from robustpointclouds_amd import _ffi  # noqa: E402
 
-SHAPES = [(6, 200, 176, 128, 128), (6, 100, 88, 256, 256)]
+SHAPES = [(6, 200, 176, 128, 128), (6, 200, 176, 128, 256)]
 
 
 def main(rounds=5, iters=10):
@@ -22,7 +22,7 @@ def main(rounds=5, iters=10):
         z = torch.empty(B * H * W, co, dtype=torch.bfloat16, device=dev)
         img = _ffi.int_arr((B, H, W))
         part = torch.empty(lib.rpc_dense_conv_blocks(0, img), 2 * co, device=dev)
-        times = {d: [] for d in (0, 32, 30, 62, 31, 63)}
+        times = {d: [] for d in (0, 1, 17, 64, 65, 81)}
         for r in range(rounds):
             for d in times:
                 lib.rpc_dense_tune(4, d)
@@ -38,7 +38,7 @@ def main(rounds=5, iters=10):
                 e1.synchronize()
                 times[d].append(e0.elapsed_time(e1) * 1e3 / iters)
         lib.rpc_dense_tune(4, 0)
-        names = {0: "real", 32: "real_old_epi", 30: "mfma", 62: "mfma_old_epi", 31: "nothing", 63: "nothing_old_epi"}
+        names = {0: "y_real", 1: "y_no_mfma", 17: "y_no_kloop", 64: "y_no_stores", 65: "y_no_mfma_no_stores", 81: "y_skeleton"}
         print(f"B{B} {H}x{W} {ci}->{co}", json.dumps({names[d]: round(sorted(v)[len(v) // 2], 2) for d, v in times.items()}),
               flush=True)
 

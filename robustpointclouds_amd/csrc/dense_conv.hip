@@ -1043,17 +1043,23 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
       }
     }
     const int x = tx0 + px;
-#pragma unroll 4
-    for (int k = 0; k < CT; ++k) {
-      const int y = ty0 + k, p = k * XTW + px;
-      if (y >= g.H || x >= g.W) continue;
-      const size_t pix = (size_t)(b * g.H + y) * g.W + x;
-      const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
-      *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
-      const unsigned u[4] = {v.x, v.y, v.z, v.w};
-      if (g.bnz != nullptr) {   // BatchNorm-backward sums of the layer this gradient enters
-        const uint4 zv = *(const uint4*)(g.bnz + pix * g.COUT + n0 + c * 8);
-        const unsigned zu[4] = {zv.x, zv.y, zv.z, zv.w};
+    if (g.bnz != nullptr) {
+      // BatchNorm-backward sums of the layer this gradient enters: all 16 pre-activation loads issued
+      // before the first is used (clamped addresses; a load per pixel waited out one round trip each)
+      uint4 zpre[CT];
+#pragma unroll
+      for (int k = 0; k < CT; ++k)
+        zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + min(x, g.W - 1)) * g.COUT +
+                                  n0 + c * 8);
+#pragma unroll
+      for (int k = 0; k < CT; ++k) {
+        const int y = ty0 + k, p = k * XTW + px;
+        if (y >= g.H || x >= g.W) continue;
+        const size_t pix = (size_t)(b * g.H + y) * g.W + x;
+        const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
+  *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
+        const unsigned u[4] = {v.x, v.y, v.z, v.w};
+        const unsigned zu[4] = {zpre[k].x, zpre[k].y, zpre[k].z, zpre[k].w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float zz = bf2f((u16)(zu[e >> 1] >> (16 * (e & 1)))), d0 = bf2f((u16)(u[e >> 1] >> (16 * (e & 1))));
@@ -1062,8 +1068,16 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
           t1[e] += d;
           t2[e] += d * ((zz - bmu[e]) * bis[e]);
         }
-        continue;
       }
+    }
+#pragma unroll 4
+    for (int k = 0; k < (g.bnz != nullptr ? 0 : CT); ++k) {
+      const int y = ty0 + k, p = k * XTW + px;
+      if (y >= g.H || x >= g.W) continue;
+      const size_t pix = (size_t)(b * g.H + y) * g.W + x;
+      const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
+      *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
+      const unsigned u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float f0 = bf2f((u16)(u[e] & 0xffff)), f1 = bf2f((u16)(u[e] >> 16));
@@ -1346,17 +1360,23 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       }
     }
     const int x = tx0 + px;
-#pragma unroll 4
-    for (int k = 0; k < CT; ++k) {
-      const int y = ty0 + k, p = k * CT + px;
-      if (y >= g.H || x >= g.W) continue;
-      const size_t pix = (size_t)(b * g.H + y) * g.W + x;
-      const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
-      if (!(DBG & 64)) *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
-      const unsigned u[4] = {v.x, v.y, v.z, v.w};
-      if (g.bnz != nullptr) {   // BatchNorm-backward sums of the layer this gradient enters
-        const uint4 zv = *(const uint4*)(g.bnz + pix * g.COUT + n0 + c * 8);
-        const unsigned zu[4] = {zv.x, zv.y, zv.z, zv.w};
+    if (g.bnz != nullptr) {
+      // BatchNorm-backward sums of the layer this gradient enters: all 16 pre-activation loads issued
+      // before the first is used (clamped addresses; a load per pixel waited out one round trip each)
+      uint4 zpre[CT];
+#pragma unroll
+      for (int k = 0; k < CT; ++k)
+        zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + min(x, g.W - 1)) * g.COUT +
+                                  n0 + c * 8);
+#pragma unroll
+      for (int k = 0; k < CT; ++k) {
+        const int y = ty0 + k, p = k * CT + px;
+        if (y >= g.H || x >= g.W) continue;
+        const size_t pix = (size_t)(b * g.H + y) * g.W + x;
+        const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
+  if (!(DBG & 64)) *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
+        const unsigned u[4] = {v.x, v.y, v.z, v.w};
+        const unsigned zu[4] = {zpre[k].x, zpre[k].y, zpre[k].z, zpre[k].w};
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float zz = bf2f((u16)(zu[e >> 1] >> (16 * (e & 1)))), d0 = bf2f((u16)(u[e >> 1] >> (16 * (e & 1))));
@@ -1365,8 +1385,16 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
           t1[e] += d;
           t2[e] += d * ((zz - bmu[e]) * bis[e]);
         }
-        continue;
       }
+    }
+#pragma unroll 4
+    for (int k = 0; k < (g.bnz != nullptr ? 0 : CT); ++k) {
+      const int y = ty0 + k, p = k * CT + px;
+      if (y >= g.H || x >= g.W) continue;
+      const size_t pix = (size_t)(b * g.H + y) * g.W + x;
+      const uint4 v = *(const uint4*)(tileb + p * 256 + ((c ^ (p & 15)) * 16));
+      if (!(DBG & 64)) *(uint4*)(g.out + pix * g.OP + g.OOFF + n0 + c * 8) = v;
+      const unsigned u[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const float f0 = bf2f((u16)(u[e] & 0xffff)), f1 = bf2f((u16)(u[e] >> 16));

@@ -345,51 +345,84 @@ __device__ __forceinline__ void st8h(u16* p, const float (&v)[8]) {
   *(uint4*)p = *(const uint4*)o;
 }
 
+// Channel-group passes (C % 8 == 0, C / 8 divides BLK): thread = (row lane, 8-channel group), the group's
+// BatchNorm parameters loaded once into registers, RV rows per thread in flight per iteration (one row per
+// thread with the parameters re-read from L1 per row: the parameter loads were 2.5x the data bytes through
+// the load path, k_dz_bf16_v8 ~3.7 TB/s)
+constexpr int RV = 4;
+__host__ __device__ inline int rowpass_blocks(long long n, int c) {
+  const long long rl = BLK / (c / 8), per = rl * RV;
+  const long long b = (n + per - 1) / per;
+  return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+}
+
 __global__ __launch_bounds__(BLK) void k_to_bf16_v8(const float* __restrict__ z, const float* __restrict__ bn, int N,
                                                     int C, int relu, u16* __restrict__ h) {
-  const int C8 = C >> 3;
-  const int t = blockIdx.x * BLK + threadIdx.x;
-  if (t >= N * C8) return;
-  const int r = t / C8, c = (t - r * C8) * 8;
-  float v[8];
-  ld8f(z + (size_t)r * C + c, v);
+  const int C8 = C >> 3, RL = BLK / C8;
+  const int cg = threadIdx.x % C8, rl = threadIdx.x / C8, c = cg * 8;
+  if (rl >= RL) return;
+  float mu[8], sc[8], be[8];
   if (bn) {
-    float mu[8], sc[8], be[8];
     ld8f(bn + 2 * C + c, mu);
     ld8f(bn + c, sc);
     ld8f(bn + C + c, be);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = fmaf(v[j] - mu[j], sc[j], be[j]);
   }
-  if (relu) {
+  const int step = gridDim.x * RL;
+  for (int r0 = blockIdx.x * RL + rl; r0 < N; r0 += RV * step) {
+    float v[RV][8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = fmaxf(v[j], 0.0f);
+    for (int u = 0; u < RV; ++u) ld8f(z + (size_t)min(r0 + u * step, N - 1) * C + c, v[u]);
+#pragma unroll
+    for (int u = 0; u < RV; ++u) {
+      const int r = r0 + u * step;
+      if (r >= N) break;
+      if (bn) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[u][j] = fmaf(v[u][j] - mu[j], sc[j], be[j]);
+      }
+      if (relu) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[u][j] = fmaxf(v[u][j], 0.0f);
+      }
+      st8h(h + (size_t)r * C + c, v[u]);
+    }
   }
-  st8h(h + (size_t)r * C + c, v);
 }
 
 __global__ __launch_bounds__(BLK) void k_dz_bf16_v8(const float* __restrict__ dy, const float* __restrict__ z,
                                                     const float* __restrict__ bnb, int N, int C,
                                                     u16* __restrict__ dz) {
-  const int C8 = C >> 3;
-  const int t = blockIdx.x * BLK + threadIdx.x;
-  if (t >= N * C8) return;
-  const int r = t / C8, c = (t - r * C8) * 8;
-  float d[8], zz[8], gi[8], m1[8], m2[8], mb[8], ib[8];
-  ld8f(dy + (size_t)r * C + c, d);
-  ld8f(z + (size_t)r * C + c, zz);
+  const int C8 = C >> 3, RL = BLK / C8;
+  const int cg = threadIdx.x % C8, rl = threadIdx.x / C8, c = cg * 8;
+  if (rl >= RL) return;
+  float gi[8], m1[8], m2[8], mb[8], ib[8];
   ld8f(bnb + c, gi);
   ld8f(bnb + C + c, m1);
   ld8f(bnb + 2 * C + c, m2);
   ld8f(bnb + 3 * C + c, mb);
   ld8f(bnb + 4 * C + c, ib);
-  float v[8];
+  const int step = gridDim.x * RL;
+  for (int r0 = blockIdx.x * RL + rl; r0 < N; r0 += RV * step) {
+    float d[RV][8], zz[RV][8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float xh = (zz[j] - mb[j]) * ib[j];
-    v[j] = gi[j] * (d[j] - m1[j] - xh * m2[j]);
+    for (int u = 0; u < RV; ++u) {
+      const size_t o = (size_t)min(r0 + u * step, N - 1) * C + c;
+      ld8f(dy + o, d[u]);
+      ld8f(z + o, zz[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < RV; ++u) {
+      const int r = r0 + u * step;
+      if (r >= N) break;
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float xh = (zz[u][j] - mb[j]) * ib[j];
+        v[j] = gi[j] * (d[u][j] - m1[j] - xh * m2[j]);
+      }
+      st8h(dz + (size_t)r * C + c, v);
+    }
   }
-  st8h(dz + (size_t)r * C + c, v);
 }
 
 // W fp32 [K][CI][CO] -> B^T bf16 [K][NGP][KGP]; fwd: n = co, kk = ci ; dgrad: n = ci, kk = co
@@ -627,9 +660,9 @@ extern "C" int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, i
   if (n < 0 || c < 1) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   int cp = r8(c);
-  if (c % 8 == 0 && (long long)n * (c / 8) < (1LL << 31))
-    hipLaunchKernelGGL(k_to_bf16_v8, dim3(cdiv((long long)n * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn,
-                       n, c, relu, (u16*)h);
+  if (c % 8 == 0 && BLK % (c / 8) == 0 && (long long)n * c < (1LL << 31))
+    hipLaunchKernelGGL(k_to_bf16_v8, dim3(rowpass_blocks(n, c)), dim3(BLK), 0, (hipStream_t)stream, z, bn, n, c, relu,
+                       (u16*)h);
   else
     hipLaunchKernelGGL(k_to_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, n, c,
                        cp, relu, (u16*)h);
@@ -642,9 +675,9 @@ extern "C" int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const flo
   if (n < 0 || c < 1) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   int cp = r8(c);
-  if (c % 8 == 0 && (long long)n * (c / 8) < (1LL << 31))
-    hipLaunchKernelGGL(k_dz_bf16_v8, dim3(cdiv((long long)n * (c / 8), BLK)), dim3(BLK), 0, (hipStream_t)stream, dy, z,
-                       bnb, n, c, (u16*)dz);
+  if (c % 8 == 0 && BLK % (c / 8) == 0 && (long long)n * c < (1LL << 31))
+    hipLaunchKernelGGL(k_dz_bf16_v8, dim3(rowpass_blocks(n, c)), dim3(BLK), 0, (hipStream_t)stream, dy, z, bnb, n, c,
+                       (u16*)dz);
   else
     hipLaunchKernelGGL(k_dz_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, dy, z, bnb,
                        n, c, cp, (u16*)dz);

@@ -93,7 +93,7 @@ def _bf16_ulp_close(got, want, atol=1e-30):
     assert ((g - w).abs() <= ulp + atol).all(), float(((g - w).abs() - ulp).max())
 
 
-@pytest.mark.parametrize("n,c", [(4097, 64), (333, 16), (1000, 128), (515, 60)])
+@pytest.mark.parametrize("n,c", [(4097, 64), (333, 16), (1000, 128), (515, 60), (600001, 64), (70001, 128)])
 def test_bf16_row_producers(n, c):
     """rpc_to_bf16_rows (relu(bn(z)) -> bf16 rows of pitch round8(C)) and rpc_bnbwd_to_bf16_rows
     (gi * (dy - m1 - xhat*m2) -> bf16): the 8-channel vector forms (C % 8 == 0) and the scalar form
@@ -119,7 +119,7 @@ def test_bf16_row_producers(n, c):
     want_h = torch.clamp((z.double() - mu) * sc + be, min=0.0)
     gi, m1, m2, mb, ib = bnb.double().view(5, c)
     want_dz = gi * (dy.double() - m1 - (z.double() - mb) * ib * m2)
-    _bf16_ulp_close(h[:, :c], want_h)
+    _bf16_ulp_close(h[:, :c], want_h, atol=1e-6)   # relu(x) with x within fp32 rounding of 0
     _bf16_ulp_close(dz[:, :c], want_dz, atol=1e-5)
     if cp > c:
         assert (h[:, c:] == 0).all() and (dz[:, c:] == 0).all()

@@ -19,6 +19,7 @@
 #include <string.h>
 
 #include "common.h"
+#include <stdlib.h>
 #include "dense_common.h"
 #include "rpc_hip.h"
 
@@ -776,13 +777,35 @@ static int wgrad_slots(int ci, int co) {   // resident blocks on the whole devic
 
 static int wgrad_kg(int ci, int co) { return (ci == 128 && co == 128) ? 1 : 3; }
 
-// row chunks: ~512 rows each, then trimmed so chunks x offset groups fills whole rounds of the
-// resident blocks (a partial last round costs a whole block time)
+static int wgrad_rounds() {   // RPC_SPWG_ROUNDS (A/B): rounds of resident blocks per launch, 0 = 512-row chunks
+  static int r = -1;
+  if (r < 0) {
+    const char* e = getenv("RPC_SPWG_ROUNDS");
+    r = e ? atoi(e) : 1;
+    if (r < 0) r = 1;
+  }
+  return r;
+}
+
+// row chunks: as many as one round of the resident blocks holds (chunks x offset groups <= slots), at
+// least 256 rows each. Every chunk writes a [K][ci][co] fp32 partial slab that k_slab_reduce reads back:
+// with ~512-row chunks over 3 rounds the 106k-row 64 x 64 layers wrote and re-read 75 MB of slabs per
+// launch on the side stream, which slowed the data-gradient chain beside it (step 827 -> 833 frames/s
+// with one round, profiles/r03_spwg_ab.log). RPC_SPWG_ROUNDS=0: the former ~512-row chunks trimmed to
+// whole rounds.
 static int wgrad_chunks(int n, int kvol, int ci, int co) {
-  int c = (n + 511) / 512;
-  c = c < 1 ? 1 : (c > 512 ? 512 : c);
   const int groups = (kvol + wgrad_kg(ci, co) - 1) / wgrad_kg(ci, co);
   const long long slots = wgrad_slots(ci, co);
+  const int R = wgrad_rounds();
+  if (R > 0) {
+    long long c = (long long)R * slots / groups;
+    const long long cmax = (n + 255) / 256;
+    if (c > cmax) c = cmax;
+    if (c > 512) c = 512;
+    return c < 1 ? 1 : (int)c;
+  }
+  int c = (n + 511) / 512;
+  c = c < 1 ? 1 : (c > 512 ? 512 : c);
   const long long total = (long long)c * groups;
   if (total > slots) {
     const long long rounds = total / slots;

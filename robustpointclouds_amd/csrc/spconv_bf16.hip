@@ -777,12 +777,12 @@ static int wgrad_slots(int ci, int co) {   // resident blocks on the whole devic
 
 static int wgrad_kg(int ci, int co) { return (ci == 128 && co == 128) ? 1 : 3; }
 
-static int wgrad_rounds() {   // RPC_SPWG_ROUNDS (A/B): rounds of resident blocks per launch, 0 = 512-row chunks
+static int wgrad_fill() {   // RPC_SPWG_FILL (A/B): percent of one round of resident blocks, 0 = 512-row chunks
   static int r = -1;
   if (r < 0) {
-    const char* e = getenv("RPC_SPWG_ROUNDS");
-    r = e ? atoi(e) : 1;
-    if (r < 0) r = 1;
+    const char* e = getenv("RPC_SPWG_FILL");
+    r = e ? atoi(e) : 100;
+    if (r < 0) r = 100;
   }
   return r;
 }
@@ -791,14 +791,14 @@ static int wgrad_rounds() {   // RPC_SPWG_ROUNDS (A/B): rounds of resident block
 // least 256 rows each. Every chunk writes a [K][ci][co] fp32 partial slab that k_slab_reduce reads back:
 // with ~512-row chunks over 3 rounds the 106k-row 64 x 64 layers wrote and re-read 75 MB of slabs per
 // launch on the side stream, which slowed the data-gradient chain beside it (step 827 -> 833 frames/s
-// with one round, profiles/r03_spwg_ab.log). RPC_SPWG_ROUNDS=0: the former ~512-row chunks trimmed to
-// whole rounds.
+// with one round, profiles/r03_spwg_ab.log; 60 % / 35 % of a round measured equal / slower).
+// RPC_SPWG_FILL=0: the former ~512-row chunks trimmed to whole rounds.
 static int wgrad_chunks(int n, int kvol, int ci, int co) {
   const int groups = (kvol + wgrad_kg(ci, co) - 1) / wgrad_kg(ci, co);
   const long long slots = wgrad_slots(ci, co);
-  const int R = wgrad_rounds();
+  const int R = wgrad_fill();
   if (R > 0) {
-    long long c = (long long)R * slots / groups;
+    long long c = (long long)R * slots / (100 * groups);
     const long long cmax = (n + 255) / 256;
     if (c > cmax) c = cmax;
     if (c > 512) c = 512;

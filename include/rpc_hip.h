@@ -280,6 +280,11 @@ typedef struct {
   float* dgamma;
   float* dbeta;
 } RpcSparseLayer;
+/* Side-work stream (no reference counterpart: the reference runs one stream). which > 0: the device's
+ * least stream priority, < 0: greatest, 0: default; hipStreamNonBlocking. */
+int rpc_stream_create(int which, void** out);
+int rpc_stream_priority_range(int* least, int* greatest);
+
 size_t rpc_sparse_backward_workspace_size(const RpcSparseLayer* layers, int nlayers);
 int rpc_sparse_backward(const RpcSparseLayer* layers, int nlayers, const void* grad_dense, const int* coors_last,
                         const int* shape /* B,D,H,W */, int flags, float* dfeat /* [n_in of layer 0][ci] or NULL */,

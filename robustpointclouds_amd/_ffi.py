@@ -192,6 +192,8 @@ SIGNATURES = {
     "rpc_center_head_loss_backward": (i32, [C.POINTER(RpcCenterCfg), vp, vp, vp, vp, vp, vp, sz, vp]),
     "rpc_center_head_targets": (i32, [C.POINTER(RpcCenterCfg), i32, vp, C.POINTER(vp), C.POINTER(vp),
                                       C.POINTER(vp), C.POINTER(vp)]),
+    "rpc_stream_create": (i32, [i32, C.POINTER(vp)]),
+    "rpc_stream_priority_range": (i32, [C.POINTER(i32), C.POINTER(i32)]),
     "rpc_anchor_head_workspace_size": (sz, [C.POINTER(RpcHeadCfg), i32]),
     "rpc_anchor_head_loss_forward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, vp, i32, vp, vp, vp, vp, vp, sz, vp]),
     "rpc_anchor_head_loss_backward": (i32, [C.POINTER(RpcHeadCfg), vp, vp, i32, vp, vp, vp, vp, vp, vp, vp, vp,
@@ -244,6 +246,26 @@ def stream_of(t: torch.Tensor):
     if not t.is_cuda:
         raise RuntimeError("rpc_hip ops run on the GPU only (no CPU fallback); got a CPU tensor")
     return C.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+# RPC_SIDE_PRIORITY=1: side-work streams (batch prefetch, sparse rulebooks / weight gradients) are HIP
+# streams at the device's least priority, so the training stream's kernels are dispatched first
+SIDE_PRIORITY = os.environ.get("RPC_SIDE_PRIORITY", "0") != "0"
+_side_streams: list = []
+
+
+def side_stream(device) -> torch.cuda.Stream:
+    """A stream for work off the step's critical path (torch.cuda.Stream, or with RPC_SIDE_PRIORITY a
+    least-priority HIP stream wrapped as torch.cuda.ExternalStream; never destroyed)."""
+    if not SIDE_PRIORITY:
+        return torch.cuda.Stream(device)
+    lib = load()
+    out = C.c_void_p()
+    with torch.cuda.device(device):
+        check(lib.rpc_stream_create(1, C.byref(out)), "rpc_stream_create")
+    s = torch.cuda.ExternalStream(out.value, device=device)
+    _side_streams.append(s)
+    return s
 
 
 def workspace(nbytes: int, device) -> torch.Tensor:

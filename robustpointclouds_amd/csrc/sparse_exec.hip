@@ -185,3 +185,23 @@ extern "C" int rpc_sparse_backward(const RpcSparseLayer* layers, int nlayers, co
   return run(layers, nlayers, grad_dense, coors_last, shape, flags, dfeat, A, (hipStream_t)stream,
              (hipStream_t)wgrad_stream);
 }
+
+// Side-work streams at the device's least priority (the trainer's batch prefetch, the sparse rulebooks
+// and weight gradients): the training stream's kernels are dispatched first when both have work queued.
+// which > 0: least priority, which < 0: greatest, 0: default. Returns RPC_OK and the stream in *out.
+extern "C" int rpc_stream_create(int which, void** out) {
+  if (!out) return RPC_ERR_ARG;
+  int least = 0, greatest = 0;
+  RPC_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  const int prio = which > 0 ? least : (which < 0 ? greatest : 0);
+  hipStream_t s = nullptr;
+  RPC_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, prio));
+  *out = (void*)s;
+  return RPC_OK;
+}
+
+extern "C" int rpc_stream_priority_range(int* least, int* greatest) {
+  if (!least || !greatest) return RPC_ERR_ARG;
+  RPC_CHECK(hipDeviceGetStreamPriorityRange(least, greatest));
+  return RPC_OK;
+}

@@ -214,7 +214,7 @@ class SparseEncoder(nn.Module):
         key = (name, str(device))
         s = self.__dict__.setdefault("_side_streams", {}).get(key)
         if s is None:
-            s = self._side_streams[key] = torch.cuda.Stream(device)
+            s = self._side_streams[key] = _ffi.side_stream(device)
         return s
 
     def prepare(self, coors: torch.Tensor, batch_size: int, after=None, consumer=None) -> None:

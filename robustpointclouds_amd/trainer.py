@@ -20,6 +20,7 @@ import torch.distributed as dist
 
 import robustpointclouds_amd.plugin.models  # noqa: F401  (registers AdversarialVoxelNet, VoxelPerturber)
 
+from . import _ffi
 from .base_model import ddp_train_step, select_engines
 from .optim import ClipAdamW, OptimWrapper
 from .registry import MODELS
@@ -233,7 +234,7 @@ class Trainer:
         if vl is None or not hasattr(vl, "voxelize_frames_deferred") or self.device.type != "cuda":
             return
         if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
+            self._side = _ffi.side_stream(self.device)
         vl.train(True)
         for p in points:    # read on the side stream: keep the allocator from reusing them early
             p.record_stream(self._side)

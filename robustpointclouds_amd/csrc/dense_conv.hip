@@ -1265,11 +1265,17 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
+  // operand fragments read a quarter step ahead (C3Y_PSTEP); DBG bit 128 (and the timing arms 1 / 16):
+  // the former loop, which reads a step's 12 fragments, waits for all of them, then runs its 32 MFMAs
+  // (200x176 128->128 72.6 -> 66.9 us, 128->256 113.9 -> 109.8 us, profiles/r03_conv_pipe.log)
+  constexpr bool PIPE = (DBG & (128 | 16 | 1)) == 0;
   issue_halo(0, 0);
 #pragma unroll
   for (int s = 0; s < WDIST; ++s) issue_w(s);
+  if constexpr (PIPE) issue_w(WDIST);
   const bool live = ty0 + w * 4 < g.H;
-  asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo 0 + tile 0
+  // halo 0 + tile 0 (+ tile 1 when pipelined: the youngest tile stays in flight)
+  asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   // per step: issue the DMAs two steps ahead, read this step's 12 fragments, 32 MFMAs, retire the next
   // step's tile (vmcnt(2); vmcnt(8) at taps HTAP, HTAP + 1 whose younger DMAs include the halo), barrier
 #define C3Y_STEP(t, LIVE)                                                                                     \
@@ -1297,7 +1303,78 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                     \
     asm volatile("s_barrier" ::: "memory");                                                                   \
   }
-  if (DBG & 16) {
+  // pipelined form: the 32 MFMAs of a step run as four quarters of 2 weight fragments x 4 halo
+  // fragments; before the MFMAs of quarter q the wave issues the reads of quarter q + 1 (2 weight
+  // fragments), and before those of quarter 3 the reads of the next step's quarter 0 and its 4 halo
+  // fragments (that tile was published by the previous step's barrier), so every LDS read lies under the
+  // same wave's MFMAs and the fragment registers stay at k_conv3x3y's 48 (two 2-fragment weight buffers,
+  // two 4-fragment halo buffers). Step s issues tile s + 3 and retires tile s + 2 before its barrier.
+  // The slot that tile s + 3 overwrites, (s - 1) & 3, was last read during step s - 1; the halo buffer of
+  // chunk kc + 1 (issued at tap HTAP of chunk kc) was last read during step (kc - 1, 7) and is retired by
+  // the wait of step (kc, 7), before step (kc, 8) reads chunk kc + 1's first fragments. At the last step
+  // the reads for "step NS" hit valid LDS (clamped tile / halo) and are never used.
+#define C3Y_PREAD_B(FB, tn, kn)                                                                             \
+  {                                                                                                         \
+    const unsigned char* hb_ = hbuf + ((kn) & 1) * YHBUF;                                                   \
+    const int dy_ = (tn) / 3, dx_ = (tn) % 3;                                                               \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                           \
+      FB[j] = *(const bf16x8*)(hb_ + hoff[dx_] + (j + dy_) * YHP * XROW);                                   \
+  }
+#define C3Y_PREAD_A(FA, sn, qq)                                                                             \
+  {                                                                                                         \
+    const unsigned char* wt_ = wring + ((sn) & (WRING - 1)) * XWTILE + (qq) * 2 * 16 * XROW;                \
+    FA[0] = *(const bf16x8*)(wt_ + woff);                                                                   \
+    FA[1] = *(const bf16x8*)(wt_ + woff + 16 * XROW);                                                       \
+  }
+#define C3Y_PMMA(FA, FB, qq)                                                                                \
+  __builtin_amdgcn_s_setprio(1);                                                                            \
+  _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                          \
+    _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                           \
+      acc[(qq) * 2 + i_][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA[i_], FB[j], acc[(qq) * 2 + i_][j], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);
+#define C3Y_PSTEP(i, FB, NB, LIVE)                                                                          \
+  {                                                                                                         \
+    constexpr int t_ = (i) % 9;                                                                             \
+    const int kq_ = kc + (i) / 9, s_ = kq_ * 9 + t_;                                                        \
+    issue_w(s_ + WDIST + 1);                                                                                \
+    if (t_ == HTAP) issue_halo(min(kq_ + 1, NKC - 1), (kq_ + 1) & 1);                                       \
+    if (LIVE) {                                                                                             \
+      C3Y_PREAD_A(ay, s_, 1)                                                                                \
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
+      C3Y_PMMA(ax, FB, 0)                                                                                   \
+      C3Y_PREAD_A(ax, s_, 2)                                                                                \
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
+      C3Y_PMMA(ay, FB, 1)                                                                                   \
+      C3Y_PREAD_A(ay, s_, 3)                                                                                \
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
+      C3Y_PMMA(ax, FB, 2)                                                                                   \
+      C3Y_PREAD_A(ax, s_ + 1, 0)                                                                            \
+      C3Y_PREAD_B(NB, (t_ + 1) % 9, kq_ + (t_ == 8))                                                        \
+      asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");                                                    \
+      C3Y_PMMA(ay, FB, 3)                                                                                   \
+    }                                                                                                       \
+    if (t_ == HTAP || t_ == HTAP + 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                      \
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                   \
+    asm volatile("s_barrier" ::: "memory");                                                                 \
+  }
+#define C3Y_PKC(LIVE)                                                                                       \
+  C3Y_PSTEP(0, fb0, fb1, LIVE) C3Y_PSTEP(1, fb1, fb0, LIVE) C3Y_PSTEP(2, fb0, fb1, LIVE)                    \
+  C3Y_PSTEP(3, fb1, fb0, LIVE) C3Y_PSTEP(4, fb0, fb1, LIVE) C3Y_PSTEP(5, fb1, fb0, LIVE)                    \
+  C3Y_PSTEP(6, fb0, fb1, LIVE) C3Y_PSTEP(7, fb1, fb0, LIVE) C3Y_PSTEP(8, fb0, fb1, LIVE)
+  if constexpr (PIPE) {
+    bf16x8 ax[2], ay[2], fb0[4], fb1[4];
+    if (live) {
+      C3Y_PREAD_A(ax, 0, 0)
+      C3Y_PREAD_B(fb0, 0, 0)
+      for (int kc = 0; kc < NKC; ++kc) {   // 9 steps (odd): the next chunk's halo fragments move back to fb0
+        C3Y_PKC(true)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) fb0[j] = fb1[j];
+      }
+    } else {
+      for (int kc = 0; kc < NKC; ++kc) { C3Y_PKC(false) }
+    }
+  } else if (DBG & 16) {
   } else if (live) {
     for (int kc = 0; kc < NKC; ++kc) {
       C3Y_STEP(0, true)
@@ -1324,6 +1401,11 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     }
   }
 #undef C3Y_STEP
+#undef C3Y_PKC
+#undef C3Y_PSTEP
+#undef C3Y_PMMA
+#undef C3Y_PREAD_A
+#undef C3Y_PREAD_B
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // ---- epilogue: lane holds co = n0 + i*16 + 4q + r of pixel (4w + j, a15)
@@ -2197,7 +2279,7 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   }
   if (knob == 4) {
     const int old = g_s1x_dbg;
-    if (value >= 0 && value <= 127) g_s1x_dbg = value;
+    if (value >= 0 && value <= 255) g_s1x_dbg = value;
     return old;
   }
   if (knob == 2) {
@@ -2224,6 +2306,7 @@ static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t 
       case 64: hipLaunchKernelGGL(k_conv3x3y<64>, grid, dim3(YB), 0, st, c); break;
       case 65: hipLaunchKernelGGL(k_conv3x3y<65>, grid, dim3(YB), 0, st, c); break;
       case 81: hipLaunchKernelGGL(k_conv3x3y<81>, grid, dim3(YB), 0, st, c); break;
+      case 128: hipLaunchKernelGGL(k_conv3x3y<128>, grid, dim3(YB), 0, st, c); break;
       default: hipLaunchKernelGGL(k_conv3x3y<0>, grid, dim3(YB), 0, st, c);
     }
   } else if (s1_xwide(g.COUT)) {

@@ -22,7 +22,8 @@ def main(rounds=5, iters=10):
         z = torch.empty(B * H * W, co, dtype=torch.bfloat16, device=dev)
         img = _ffi.int_arr((B, H, W))
         part = torch.empty(lib.rpc_dense_conv_blocks(0, img), 2 * co, device=dev)
-        times = {d: [] for d in (0, 1, 17, 64, 65, 81)}
+        dbgs = [int(v) for v in os.environ.get("DBGS", "0,1,17,64,65,81").split(",")]
+        times = {d: [] for d in dbgs}
         for r in range(rounds):
             for d in times:
                 lib.rpc_dense_tune(4, d)
@@ -38,7 +39,7 @@ def main(rounds=5, iters=10):
                 e1.synchronize()
                 times[d].append(e0.elapsed_time(e1) * 1e3 / iters)
         lib.rpc_dense_tune(4, 0)
-        names = {0: "y_real", 1: "y_no_mfma", 17: "y_no_kloop", 64: "y_no_stores", 65: "y_no_mfma_no_stores", 81: "y_skeleton"}
+        names = {0: "y_real", 1: "y_no_mfma", 17: "y_no_kloop", 64: "y_no_stores", 65: "y_no_mfma_no_stores", 81: "y_skeleton", 128: "y_former_loop"}
         print(f"B{B} {H}x{W} {ci}->{co}", json.dumps({names[d]: round(sorted(v)[len(v) // 2], 2) for d, v in times.items()}),
               flush=True)
 

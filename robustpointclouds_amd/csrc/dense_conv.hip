@@ -931,10 +931,17 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
 #pragma unroll
   for (int s = 0; s < XWD; ++s) issue_w(s);
 
-  const int grp = w >> 2;
+  // DBG bit 128: operand fragments read a quarter step ahead (C3X_PSTEP, one barrier per step) instead of
+  // the partner groups staggered one phase (two barriers per step). Measured equal (100x88 256->256 63.8
+  // vs 62.4 us, 200x176 128->128 69.7 vs 69.7, profiles/r03_conv_pipe.log): the stagger already hides
+  // the reads here, unlike k_conv3x3y's, so the staggered loop stays the default
+  constexpr bool PIPE = (DBG & 128) != 0;
+  const int grp = PIPE ? 0 : w >> 2;
   const bool live = ty0 + wp * 4 < g.H;
   static_assert(XWD == 4 && XHI == 6 && HTAP + XWD <= 8, "vmcnt immediates below");
-  asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // halo 0 + tile 0
+  // halo 0 + tile 0 (pipelined: + tile 1; tiles 2, 3 stay in flight)
+  if (PIPE) asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(3)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   if (grp) asm volatile("s_barrier" ::: "memory");
   // per step: 1 weight DMA XWD tiles ahead (+ XHI halo DMAs at tap HTAP, after it); the tile of the next
   // step is retired by vmcnt(XWD - 1), or vmcnt(XWD - 1 + XHI) at taps HTAP .. HTAP + XWD - 1 while the
@@ -976,7 +983,76 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
     }                                                                                                         \
     if (!(DBG & 16)) asm volatile("s_barrier" ::: "memory");                                                  \
   }
-  if (live) {
+  // pipelined form: a step's 32 MFMAs run as four quarters (the 4 weight fragments x the 2 halo fragments
+  // of one tile row); before quarter q's MFMAs the wave reads quarter q + 1's 2 halo fragments, before
+  // quarter 3's the next step's 4 weight fragments and its quarter-0 halo fragments, so every LDS read
+  // lies under the same wave's MFMAs (fragment registers: two 4-fragment weight buffers + a 2 x 2 halo
+  // ring = the former loop's 48). The next step's tile must then be published one step earlier: step s
+  // retires tile s + 2 (vmcnt(2), or vmcnt(8) while a halo chunk issued at step s - 2 .. s is younger),
+  // so a halo chunk issued at tap HTAP is retired at tap HTAP + 2 <= 7, before tap 8 reads its first
+  // fragments; its buffer was last read during step (kc - 1, 8). Tile s + 4 goes to ring slot
+  // (s + 4) & 7, last read during step s - 4. At the last step the reads for "step NS" hit valid LDS
+  // (clamped tile / halo) and are never used.
+#define C3X_PREAD_B(FB, tn, kn, qq)                                                                         \
+  {                                                                                                         \
+    const unsigned char* hb_ = hbuf + ((kn) & 1) * XHBUF;                                                   \
+    const int dy_ = (tn) / 3, dx_ = (tn) % 3;                                                               \
+    FB[0] = *(const bf16x8*)(hb_ + hoff[dx_] + ((qq) + dy_) * XHP * XROW);                                  \
+    FB[1] = *(const bf16x8*)(hb_ + hoff[dx_] + ((qq) + dy_) * XHP * XROW + 16 * XROW);                      \
+  }
+#define C3X_PREAD_A(FA, sn)                                                                                 \
+  {                                                                                                         \
+    const unsigned char* wt_ = wring + ((sn) & (XWR - 1)) * XWTILE;                                         \
+    _Pragma("unroll") for (int i = 0; i < 4; ++i) FA[i] = *(const bf16x8*)(wt_ + woff + i * 16 * XROW);     \
+  }
+#define C3X_PMMA(FA, FB, qq)                                                                                \
+  __builtin_amdgcn_s_setprio(1);                                                                            \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i)                                                             \
+    _Pragma("unroll") for (int j = 0; j < 2; ++j)                                                           \
+      acc[i][2 * (qq) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA[i], FB[j], acc[i][2 * (qq) + j], 0, 0, 0); \
+  __builtin_amdgcn_s_setprio(0);
+#define C3X_PSTEP(t, FA, NA, LIVE)                                                                          \
+  {                                                                                                         \
+    const int s_ = kc * 9 + (t);                                                                            \
+    issue_w(s_ + XWD);                                                                                      \
+    if ((t) == HTAP) issue_halo(min(kc + 1, NKC - 1), (kc + 1) & 1);                                        \
+    if (LIVE) {                                                                                             \
+      C3X_PREAD_B(by, (t), kc, 1)                                                                           \
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
+      C3X_PMMA(FA, bx, 0)                                                                                   \
+      C3X_PREAD_B(bx, (t), kc, 2)                                                                           \
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
+      C3X_PMMA(FA, by, 1)                                                                                   \
+      C3X_PREAD_B(by, (t), kc, 3)                                                                           \
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
+      C3X_PMMA(FA, bx, 2)                                                                                   \
+      C3X_PREAD_A(NA, s_ + 1)                                                                               \
+      C3X_PREAD_B(bx, ((t) + 1) % 9, kc + ((t) == 8), 0)                                                    \
+      asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");                                                    \
+      C3X_PMMA(FA, by, 3)                                                                                   \
+    }                                                                                                       \
+    if ((t) >= HTAP && (t) <= HTAP + 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                    \
+    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                   \
+    asm volatile("s_barrier" ::: "memory");                                                                 \
+  }
+#define C3X_PKC(LIVE)                                                                                       \
+  C3X_PSTEP(0, a0, a1, LIVE) C3X_PSTEP(1, a1, a0, LIVE) C3X_PSTEP(2, a0, a1, LIVE)                          \
+  C3X_PSTEP(3, a1, a0, LIVE) C3X_PSTEP(4, a0, a1, LIVE) C3X_PSTEP(5, a1, a0, LIVE)                          \
+  C3X_PSTEP(6, a0, a1, LIVE) C3X_PSTEP(7, a1, a0, LIVE) C3X_PSTEP(8, a0, a1, LIVE)
+  if constexpr (PIPE) {
+    bf16x8 a0[4], a1[4], bx[2], by[2];
+    if (live) {
+      C3X_PREAD_A(a0, 0)
+      C3X_PREAD_B(bx, 0, 0, 0)
+      for (int kc = 0; kc < NKC; ++kc) {   // 9 steps (odd): the next chunk's weight fragments move back to a0
+        C3X_PKC(true)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) a0[i] = a1[i];
+      }
+    } else {
+      for (int kc = 0; kc < NKC; ++kc) { C3X_PKC(false) }
+    }
+  } else if (live) {
     for (int kc = 0; kc < NKC; ++kc) {
       C3X_STEP(0, true)
       C3X_STEP(1, true)
@@ -1002,7 +1078,12 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
     }
   }
 #undef C3X_STEP
-  if (!grp) asm volatile("s_barrier" ::: "memory");
+#undef C3X_PKC
+#undef C3X_PSTEP
+#undef C3X_PMMA
+#undef C3X_PREAD_A
+#undef C3X_PREAD_B
+  if (!PIPE && !grp) asm volatile("s_barrier" ::: "memory");
   asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // ---- epilogue: lane holds co = n0 + wc*64 + i*16 + 4q + r of pixel (wp*4 + (j >> 1), (j & 1)*16 + a15)
@@ -2321,6 +2402,7 @@ static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t 
       case 30: hipLaunchKernelGGL(k_conv3x3x<30>, grid, dim3(WB), 0, st, c); break;
       case 31: hipLaunchKernelGGL(k_conv3x3x<31>, grid, dim3(WB), 0, st, c); break;
       case 32: hipLaunchKernelGGL(k_conv3x3x<32>, grid, dim3(WB), 0, st, c); break;
+      case 128: hipLaunchKernelGGL(k_conv3x3x<128>, grid, dim3(WB), 0, st, c); break;
       default: hipLaunchKernelGGL(k_conv3x3x<0>, grid, dim3(WB), 0, st, c);
     }
   } else if (bnz != nullptr) {

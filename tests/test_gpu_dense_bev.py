@@ -379,7 +379,7 @@ def test_s1_lds_dma_kernel_bitexact_vs_register_staged(ci, co, B, H, W):
                                          (128, 128, 1, 16, 32), (256, 128, 2, 37, 45), (128, 256, 2, 33, 17),
                                          (128, 128, 3, 24, 40), (128, 256, 1, 9, 130), (384, 128, 1, 21, 70),
                                          (192, 128, 1, 19, 33)])
-@pytest.mark.parametrize("variant", [3, 4, 41])
+@pytest.mark.parametrize("variant", [3, 4, 31, 41])
 def test_s1_wide_tile_kernel(ci, co, B, H, W, variant):
     """k_conv3x3x (16x32-pixel tiles, 32-channel K-steps, rpc_dense_tune knob 0 = 3) and k_conv3x3y (two
     4-wave 16x16 blocks per CU, knob 0 = 4) against float64 torch on
@@ -388,12 +388,13 @@ def test_s1_wide_tile_kernel(ci, co, B, H, W, variant):
     rpc_dense_conv_part_rows rows (later rows untouched), and the output within 1 bf16 ulp of k_conv3x3's
     (same 32-channel MFMA sums, added in another order). Shapes: SECOND's (200x176 with an 8-row last
     tile row and a 16-column last tile column; 100x88), one tile, partial rows / columns, an odd number of
-    32-channel K-steps (192 channels). Variant 41: k_conv3x3y's former loop (knob 4 = 128: a step's
-    fragments read, then all its MFMAs) against the default one, whose fragments are read a quarter step
-    ahead: the same MFMAs in the same order per accumulator, so bit-identical."""
+    32-channel K-steps (192 channels). Variants 31 / 41: knob 4 = 128 against the default loop of
+    k_conv3x3x / k_conv3x3y (x: the quarter-step-ahead fragment reads against the staggered partner
+    groups; y: the former read-then-MFMA loop against the quarter-step-ahead one): the same MFMAs in the
+    same order per accumulator, so bit-identical."""
     lib = _ffi.load()
-    pipe = variant == 41
-    variant = 4 if pipe else variant
+    pipe = variant in (31, 41)
+    variant = variant // 10 if pipe else variant
     x = _rand(B, ci, H, W, seed=31)
     Wt = _rand(co, ci, 3, 3, seed=32, scale=0.05)
     wf, _ = _wprep(Wt, 0, 9, 1)

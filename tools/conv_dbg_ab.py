@@ -16,7 +16,10 @@ def main(rounds=5, iters=10):
     lib = _ffi.load()
     dev = torch.device("cuda")
     st = torch.cuda.current_stream()
-    for (B, H, W, ci, co) in SHAPES:
+    shapes = [tuple(int(v) for v in t.split(",")) for t in os.environ["SHAPES"].split(";")] if os.environ.get("SHAPES") else SHAPES
+    if os.environ.get("VARIANT"):
+        lib.rpc_dense_tune(0, int(os.environ["VARIANT"]))
+    for (B, H, W, ci, co) in shapes:
         x = (torch.rand(B * H * W, ci, device=dev) * 2 - 1).to(torch.bfloat16)
         wt = ((torch.rand(9, co, ci, device=dev) * 2 - 1) * 0.05).to(torch.bfloat16)
         z = torch.empty(B * H * W, co, dtype=torch.bfloat16, device=dev)
@@ -39,7 +42,7 @@ def main(rounds=5, iters=10):
                 e1.synchronize()
                 times[d].append(e0.elapsed_time(e1) * 1e3 / iters)
         lib.rpc_dense_tune(4, 0)
-        names = {0: "y_real", 1: "y_no_mfma", 17: "y_no_kloop", 64: "y_no_stores", 65: "y_no_mfma_no_stores", 81: "y_skeleton", 128: "y_former_loop"}
+        names = {0: "y_real", 1: "y_no_mfma", 17: "y_no_kloop", 64: "y_no_stores", 65: "y_no_mfma_no_stores", 81: "y_skeleton", 128: "former_loop"}
         print(f"B{B} {H}x{W} {ci}->{co}", json.dumps({names[d]: round(sorted(v)[len(v) // 2], 2) for d, v in times.items()}),
               flush=True)
 

@@ -328,8 +328,11 @@ int rpc_dense_conv_s1_kernel(int map, int cout, const int* row_img);
 /* kernel-selection knob for A/B measurement (returns the previous value; value < 0 only reads it):
  * knob 0 = the S1 kernel for output channels that are a multiple of 128 (0: chosen by shape, default;
  * 1: the 64-channel register-staged kernel; 2: the 128-channel LDS-DMA kernel; 3: the 16x32-pixel
- * tile kernel); knob 1 = the S1 weight
- * gradient for 128-multiple channels (0: tap-sharing row-segment kernel, default; 1: per-tap kernel) */
+ * tile kernel; 4: the 16x16-pixel two-blocks-per-CU kernel); knob 1 = the S1 weight gradient for
+ * 128-multiple channels (0: tap-sharing row-segment kernel with the next sub-step's operand reads issued
+ * before this one's MFMAs, default; 1: per-tap kernel; 2: the row-segment kernel's former read-then-MFMA
+ * loop); knob 4 = k_conv3x3x / k_conv3x3y loop variants and timing arms (128: x with operand reads a
+ * quarter step ahead / y's former read-then-MFMA loop; bit-identical to the defaults) */
 int rpc_dense_tune(int knob, int value);
 /* dW (torch layout; kind 0 = Conv2d [co][ci][kh][kw], 1 = ConvTranspose2d [ci][co][kh][kw]) of the
  * forward map (S1/S2/P1/U2): sum over rows of x[src_row(row,t)][ci] * dz[row][co]; ci, co % 128 == 0 */

@@ -1827,7 +1827,7 @@ __device__ __forceinline__ s16x4 tr_read_asm(unsigned addr) {
   return r;
 }
 constexpr int WSB = 512;    // threads
-template <int SEG>
+template <int SEG, int PIPE = 0>
 __global__ __launch_bounds__(WSB, 1) void k_wgrad_s1(WG g, int nseg_x, int seg_per) {
   constexpr int TC = 128, RB = 256;                              // 256-byte rows (128 bf16 channels)
   constexpr int NWI = 2, NWJ = 4;                                // 16x16 tiles per wave (ci, co)
@@ -1956,45 +1956,114 @@ __global__ __launch_bounds__(WSB, 1) void k_wgrad_s1(WG g, int nseg_x, int seg_p
     for (int st = 0; st < WS_ST - 1; ++st) issue(st);
     int st = 0;
     const unsigned lds0 = (unsigned)(size_t)((__attribute__((address_space(3))) unsigned char*)lds);
-    for (int k = 0; k < nvalid; ++k) {
-      // retire this segment's DMAs (the WS_ST - 2 younger segments stay in flight), then publish
-      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((WS_ST - 2) * PW) : "memory");
-      // refill the stage computed last iteration (every wave has passed this barrier after reading it)
-      issue(st == 0 ? WS_ST - 1 : st - 1);
-      const unsigned base = lds0 + st * STB;
-#pragma unroll
-      for (int ks = 0; ks < SEG / 32; ++ks) {
-        // operand reads as inline asm: the compiler cannot tell the transposed-read intrinsic apart
-        // from the DMA-written stages in flight and put a vmcnt(0) (every DMA, the look-ahead too)
-        // before it. The asm wait below ties the fragments, so no MFMA is scheduled above it.
-        bf16x8 bv[NWJ], av[3][NWI];
-#pragma unroll
-        for (int j = 0; j < NWJ; ++j) {
-          const unsigned pb = base + boff[j] + 32 * ks * RB;
-          s16x4 v[2] = {tr_read_asm(pb), tr_read_asm(pb + 16 * RB)};
-          bv[j] = *(bf16x8*)v;
-        }
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-          for (int i = 0; i < NWI; ++i) {
-            const unsigned pa = base + aoff[dx][i] + 32 * ks * RB;
-            s16x4 v[2] = {tr_read_asm(pa), tr_read_asm(pa + 16 * RB)};
-            av[dx][i] = *(bf16x8*)v;
-          }
-        static_assert(NWI == 2 && NWJ == 4, "operand tie list");
-        asm volatile("s_waitcnt lgkmcnt(0)"
-                     : "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(av[0][0]), "+v"(av[0][1]),
-                       "+v"(av[1][0]), "+v"(av[1][1]), "+v"(av[2][0]), "+v"(av[2][1]));
-#pragma unroll
-        for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-          for (int i = 0; i < NWI; ++i)
-#pragma unroll
-            for (int j = 0; j < NWJ; ++j)
-              acc[dx][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[dx][i], bv[j], acc[dx][i][j], 0, 0, 0);
+    if constexpr (PIPE) {
+      // pipelined form: the 20 transposed reads of the next K sub-step (this segment's second, or the next
+      // segment's first) are issued before the 24 MFMAs of this one, whose fragments were read before
+      // the previous sub-step's MFMAs. The next segment's stage must then be published one segment
+      // earlier: each segment retires its own AND the next stage (vmcnt(PW): only the stage issued last
+      // segment stays in flight). The refill after the barrier overwrites the stage of segment k - 1,
+      // last read during segment k - 1. At the last segment the reads of "segment nvalid" hit LDS that
+      // is never used.
+#define WS1_READ(AV, BV, sbase, ks)                                                                         \
+      {                                                                                                     \
+        _Pragma("unroll") for (int j = 0; j < NWJ; ++j) {                                                   \
+          const unsigned pb = (sbase) + boff[j] + 32 * (ks) * RB;                                           \
+          s16x4 v[2] = {tr_read_asm(pb), tr_read_asm(pb + 16 * RB)};                                        \
+          BV[j] = *(bf16x8*)v;                                                                              \
+        }                                                                                                   \
+        _Pragma("unroll") for (int dx = 0; dx < 3; ++dx)                                                    \
+          _Pragma("unroll") for (int i = 0; i < NWI; ++i) {                                                 \
+            const unsigned pa = (sbase) + aoff[dx][i] + 32 * (ks) * RB;                                     \
+            s16x4 v[2] = {tr_read_asm(pa), tr_read_asm(pa + 16 * RB)};                                      \
+            AV[dx][i] = *(bf16x8*)v;                                                                        \
+          }                                                                                                 \
       }
-      st = st == WS_ST - 1 ? 0 : st + 1;
+#define WS1_MMA(AV, BV, WAIT)                                                                               \
+      {                                                                                                     \
+        asm volatile(WAIT : "+v"(BV[0]), "+v"(BV[1]), "+v"(BV[2]), "+v"(BV[3]), "+v"(AV[0][0]),              \
+                     "+v"(AV[0][1]), "+v"(AV[1][0]), "+v"(AV[1][1]), "+v"(AV[2][0]), "+v"(AV[2][1]));        \
+        _Pragma("unroll") for (int dx = 0; dx < 3; ++dx)                                                    \
+          _Pragma("unroll") for (int i = 0; i < NWI; ++i)                                                   \
+            _Pragma("unroll") for (int j = 0; j < NWJ; ++j)                                                 \
+              acc[dx][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AV[dx][i], BV[j], acc[dx][i][j], 0, 0, 0); \
+      }
+      // one segment: publish, refill, then its SEG / 32 sub-steps (FC: this sub-step's fragments)
+#define WS1_SEG(FCA, FCB, FNA, FNB)                                                                         \
+      {                                                                                                     \
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PW) : "memory");                             \
+        issue(st == 0 ? WS_ST - 1 : st - 1);                                                                \
+        const unsigned base = lds0 + st * STB;                                                              \
+        const unsigned nbase = lds0 + (st == WS_ST - 1 ? 0 : st + 1) * STB;                                 \
+        if constexpr (SEG == 64) {                                                                          \
+          WS1_READ(FNA, FNB, base, 1)                                                                       \
+          WS1_MMA(FCA, FCB, "s_waitcnt lgkmcnt(15)")                                                        \
+          WS1_READ(FCA, FCB, nbase, 0)                                                                      \
+          WS1_MMA(FNA, FNB, "s_waitcnt lgkmcnt(15)")                                                        \
+        } else {                                                                                            \
+          WS1_READ(FNA, FNB, nbase, 0)                                                                      \
+          WS1_MMA(FCA, FCB, "s_waitcnt lgkmcnt(15)")                                                        \
+        }                                                                                                   \
+        st = st == WS_ST - 1 ? 0 : st + 1;                                                                  \
+      }
+      static_assert(NWI == 2 && NWJ == 4 && (SEG == 64 || SEG == 32), "operand tie list");
+      bf16x8 a0[3][NWI], b0[NWJ], a1[3][NWI], b1[NWJ];
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(PW) : "memory");   // stages 0 and 1
+      WS1_READ(a0, b0, lds0, 0)
+      int k = 0;
+      if constexpr (SEG == 64) {
+        for (; k < nvalid; ++k) WS1_SEG(a0, b0, a1, b1)
+      } else {
+        for (; k + 1 < nvalid; k += 2) {
+          WS1_SEG(a0, b0, a1, b1)
+          WS1_SEG(a1, b1, a0, b0)
+        }
+        if (k < nvalid) WS1_SEG(a0, b0, a1, b1)
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#undef WS1_SEG
+#undef WS1_MMA
+#undef WS1_READ
+    } else {
+    for (int k = 0; k < nvalid; ++k) {
+        // retire this segment's DMAs (the WS_ST - 2 younger segments stay in flight), then publish
+        asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((WS_ST - 2) * PW) : "memory");
+        // refill the stage computed last iteration (every wave has passed this barrier after reading it)
+        issue(st == 0 ? WS_ST - 1 : st - 1);
+        const unsigned base = lds0 + st * STB;
+  #pragma unroll
+        for (int ks = 0; ks < SEG / 32; ++ks) {
+          // operand reads as inline asm: the compiler cannot tell the transposed-read intrinsic apart
+          // from the DMA-written stages in flight and put a vmcnt(0) (every DMA, the look-ahead too)
+          // before it. The asm wait below ties the fragments, so no MFMA is scheduled above it.
+          bf16x8 bv[NWJ], av[3][NWI];
+  #pragma unroll
+          for (int j = 0; j < NWJ; ++j) {
+            const unsigned pb = base + boff[j] + 32 * ks * RB;
+            s16x4 v[2] = {tr_read_asm(pb), tr_read_asm(pb + 16 * RB)};
+            bv[j] = *(bf16x8*)v;
+          }
+  #pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+  #pragma unroll
+            for (int i = 0; i < NWI; ++i) {
+              const unsigned pa = base + aoff[dx][i] + 32 * ks * RB;
+              s16x4 v[2] = {tr_read_asm(pa), tr_read_asm(pa + 16 * RB)};
+              av[dx][i] = *(bf16x8*)v;
+            }
+          static_assert(NWI == 2 && NWJ == 4, "operand tie list");
+          asm volatile("s_waitcnt lgkmcnt(0)"
+                       : "+v"(bv[0]), "+v"(bv[1]), "+v"(bv[2]), "+v"(bv[3]), "+v"(av[0][0]), "+v"(av[0][1]),
+                         "+v"(av[1][0]), "+v"(av[1][1]), "+v"(av[2][0]), "+v"(av[2][1]));
+  #pragma unroll
+          for (int dx = 0; dx < 3; ++dx)
+  #pragma unroll
+            for (int i = 0; i < NWI; ++i)
+  #pragma unroll
+              for (int j = 0; j < NWJ; ++j)
+                acc[dx][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[dx][i], bv[j], acc[dx][i][j], 0, 0, 0);
+        }
+        st = st == WS_ST - 1 ? 0 : st + 1;
+      }
     }
     // drain the look-ahead DMAs before the block exits
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2508,14 +2577,20 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
   }
   const int rows_per = ((M + chunks - 1) / chunks + 63) / 64 * 64;
   WG g{(const u16*)x, xp, (const u16*)dz, dp, ci, co, R, S, O, M, rows_per, part};
-  if (map == M_S1 && ci % 128 == 0 && co % 128 == 0 && g_wgrad_variant == 0) {
+  if (map == M_S1 && ci % 128 == 0 && co % 128 == 0 && (g_wgrad_variant == 0 || g_wgrad_variant == 2)) {
     // tap-sharing row-segment kernel: segment length with the least padding of the image row
     const int seg = (R.W + 63) / 64 * 64 <= (R.W + 31) / 32 * 32 ? 64 : 32;
     const int nsx = (R.W + seg - 1) / seg, nseg = R.B * R.H * nsx;
     const int seg_per = (nseg + chunks - 1) / chunks;
     const dim3 grid(chunks * 3 * (ci / 128) * (co / 128));
-    if (seg == 64) hipLaunchKernelGGL(k_wgrad_s1<64>, grid, dim3(WSB), 0, st, g, nsx, seg_per);
-    else hipLaunchKernelGGL(k_wgrad_s1<32>, grid, dim3(WSB), 0, st, g, nsx, seg_per);
+    // knob 1 = 2: the former loop (each sub-step's 20 transposed reads, then its 24 MFMAs); the default
+    // issues the next sub-step's reads first (bit-identical; 200x176 128->128 91.3 -> 90.7 us, 100x88
+    // 256->256 94.8 -> 90.9, 128->256 153.4 -> 150.2, profiles/r03_wgrad_pipe.log)
+    const bool pipe = g_wgrad_variant != 2;
+    if (seg == 64 && pipe) hipLaunchKernelGGL((k_wgrad_s1<64, 1>), grid, dim3(WSB), 0, st, g, nsx, seg_per);
+    else if (seg == 64) hipLaunchKernelGGL((k_wgrad_s1<64, 0>), grid, dim3(WSB), 0, st, g, nsx, seg_per);
+    else if (pipe) hipLaunchKernelGGL((k_wgrad_s1<32, 1>), grid, dim3(WSB), 0, st, g, nsx, seg_per);
+    else hipLaunchKernelGGL((k_wgrad_s1<32, 0>), grid, dim3(WSB), 0, st, g, nsx, seg_per);
   } else switch (map) {
     case M_S1: launch_wgrad<M_S1>(g, chunks, st); break;
     case M_S2: launch_wgrad<M_S2>(g, chunks, st); break;

@@ -494,7 +494,9 @@ def test_s1_dgrad_with_fused_bn_backward_sums(ci, co, B, H, W):
 def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):
     """k_wgrad_s1 (row segments, 3 taps per staged tile) against float64 torch at 1e-5 of the gradient
     scale, and against the per-tap kernel k_wgrad (rpc_dense_tune knob 1) — same bf16 products, fp32
-    sums in another order: within 2e-6 of the scale."""
+    sums in another order: within 2e-6 of the scale — and k_wgrad_s1's former loop (knob 1 = 2: each sub-step's
+    transposed reads, then its MFMAs) bit-identical to the default one, which issues the next sub-step's
+    reads before this one's MFMAs."""
     lib = _ffi.load()
     x = _rand(B, ci, H, W, seed=31)
     dz = _rand(B, co, H, W, seed=32)
@@ -506,7 +508,7 @@ def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):
     ws = _ffi.workspace(wsz, DEV)
     xn, dn = _nhwc(x), _nhwc(dz)
     outs = []
-    for variant in (0, 1):
+    for variant in (0, 1, 2):
         old = lib.rpc_dense_tune(1, variant)
         try:
             dW = torch.full(Wt.shape, float("nan"), dtype=torch.float32, device=DEV)
@@ -519,6 +521,7 @@ def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):
     scale = wr.grad.abs().max().item()
     assert (outs[0] - wr.grad).abs().max().item() <= 1e-5 * scale
     assert (outs[0] - outs[1]).abs().max().item() <= 2e-6 * scale
+    assert torch.equal(outs[0], outs[2])
 
 
 def test_wprep_batch_matches_per_layer_prep():

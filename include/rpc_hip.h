@@ -245,6 +245,12 @@ int rpc_spconv_prep_weight_bf16_batch(const RpcSpconvWprep* descs, int n, void* 
 int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out, const void* bt,
                          int ng, float* out, const float* prev_z, const float* prev_bn, float* part, int epi,
                          void* stream);
+/* the same with the gathered source table's row count n_src (rows of `a`), which bounds the kernel's 32-bit
+ * source offsets: RPC_ERR_UNSUPPORTED when n_src * round8(kg) * 2 >= 2^31. rpc_spconv_gemm_bf16 = n_src -1
+ * (bounded by n_out rows, exact for submanifold layers only). */
+int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
+                           const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
+                           float* part, int epi, void* stream);
 /* dW[k] = sum_r h[nbr[r,k]]^T dz[r] (bf16 rows, fp32 accumulate, fixed-order reduction) */
 size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co);
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,

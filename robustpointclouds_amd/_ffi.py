@@ -140,6 +140,7 @@ SIGNATURES = {
     "rpc_spconv_prep_weight_bf16": (i32, [vp, i32, i32, i32, i32, vp, vp]),
     "rpc_spconv_prep_weight_bf16_batch": (i32, [vp, i32, vp]),
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
+    "rpc_spconv_gemm_bf16_n": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_wgrad_bf16": (i32, [vp, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
     "rpc_sparse_backward_workspace_size": (sz, [vp, i32]),

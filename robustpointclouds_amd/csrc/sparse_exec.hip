@@ -113,7 +113,7 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
     if (li > 0 && L[li - 1].mat) {
       float* din = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
       if (l.bf16)
-        CHK(rpc_spconv_gemm_bf16(dzb, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, nullptr, nullptr, nullptr, 2, st));
+        CHK(rpc_spconv_gemm_bf16_n(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, nullptr, nullptr, nullptr, 2, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, din, nullptr, st));
       G[li - 1].push_back(din);
@@ -123,13 +123,13 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
       nblk = cdiv(n_in, BM) > 0 ? cdiv(n_in, BM) : 1;
       part = (float*)A.take(sizeof(float) * (size_t)nblk * 2 * l.ci);
       if (l.bf16)
-        CHK(rpc_spconv_gemm_bf16(dzb, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part, 1, st));
+        CHK(rpc_spconv_gemm_bf16_n(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part, 1, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, prev.z, prev.bn, din, part, st));
       dy = din;
     } else if (dfeat) {
       if (l.bf16)
-        CHK(rpc_spconv_gemm_bf16(dzb, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, dfeat, nullptr, nullptr, nullptr, 2,
+        CHK(rpc_spconv_gemm_bf16_n(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, dfeat, nullptr, nullptr, nullptr, 2,
                                  st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, dfeat, nullptr,

@@ -17,6 +17,7 @@
 // or the previous layer's ReLU mask + BatchNorm-backward partial sums). No atomics on data.
 #include <hip/hip_runtime.h>
 #include <string.h>
+#include <algorithm>
 
 #include "common.h"
 #include <stdlib.h>
@@ -722,10 +723,12 @@ extern "C" int rpc_spconv_prep_weight_bf16(const float* W, int kvol, int ci, int
 // out[r] = sum_k a[map[r, k']] . B_k  with a: bf16 rows of width round8(kg) (kg = GEMM K),
 // B^T from rpc_spconv_prep_weight_bf16; epi 0 = forward (z + BN partial sums), 1 = dgrad with the
 // previous layer's ReLU mask + BN-backward partial sums (prev_z, prev_bn), 2 = plain store.
-extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out,
-                                    const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
-                                    float* part, int epi, void* stream) {
+extern "C" int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
+                                      int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                                      const float* prev_bn, float* part, int epi, void* stream) {
   if (n_out < 0 || kvol > MAXK || kg < 1 || ng < 1) return RPC_ERR_ARG;
+  // 32-bit buffer offsets (src * CP + c) * 2 into the gathered source table of n_src rows
+  if (n_src >= 0 && (long long)n_src * r8(kg) * 2 >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
   if (n_out == 0) return RPC_OK;
   GB g;
   memset(&g, 0, sizeof(g));
@@ -741,14 +744,22 @@ extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int k
   g.ez = prev_z;
   g.ebn = prev_bn;
   g.part = part;
-  // 32-bit buffer offsets in k_gemm_bf16 (the source table's own size is not passed: n_out rows of it
-  // is the bound checked here, exact for submanifold layers)
-  if ((long long)n_out * g.CP * 2 >= (1LL << 31) || (long long)kvol * r16(ng) * r32(kg) * 2 >= (1LL << 31))
+  // 32-bit buffer offsets in k_gemm_bf16: the output rows (epilogue) and weight tiles; the source table's
+  // rows are checked above when the caller passes them (n_src < 0: the legacy entry point, which bounds
+  // the source by n_out rows — exact for submanifold layers only)
+  if ((long long)(n_src >= 0 ? std::max(n_src, n_out) : n_out) * g.CP * 2 >= (1LL << 31) ||
+      (long long)kvol * r16(ng) * r32(kg) * 2 >= (1LL << 31))
     return RPC_ERR_UNSUPPORTED;
   int rc = launch(r32(kg), r16(ng) / 16, epi, g, n_out, (hipStream_t)stream);
   if (rc) return rc;
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out,
+                                    const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
+                                    float* part, int epi, void* stream) {
+  return rpc_spconv_gemm_bf16_n(a, -1, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 
 template <int CI, int CO, int KG>

@@ -524,7 +524,7 @@ class SparseEncoderFn(torch.autograd.Function):
             if rec["bf16"]:
                 bt, rec["btd"] = wtiles[li]
                 e0 = enc.timer.start() if tm else None
-                _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(hsrc), sp.ci, _ffi.ptr(rec["nbr"]), sp.K, 0, n_out,
+                _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(hsrc), hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]), sp.K, 0, n_out,
                                                     _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None, _ffi.ptr(part), 0,
                                                     st), "rpc_spconv_gemm_bf16")
             else:
@@ -711,7 +711,7 @@ class SparseEncoderFn(torch.autograd.Function):
             if li > 0 and L[li - 1]["spec"].mat:
                 # the input is a materialised output: plain data gradient, masked by its own backward
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
                                "rpc_spconv_gemm_bf16(dgrad)")
                 else:
@@ -726,7 +726,7 @@ class SparseEncoderFn(torch.autograd.Function):
                 td = timer is not None and timer.wants("dgrad", sp)
                 if rec["bf16"]:
                     e0 = timer.start() if td else None
-                    _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), _ffi.ptr(prev["z"]),
                                                         _ffi.ptr(prev["bn"]), _ffi.ptr(part), 1, st),
                                "rpc_spconv_gemm_bf16(dgrad)")
@@ -743,7 +743,7 @@ class SparseEncoderFn(torch.autograd.Function):
                 dy = din
             elif ctx.needs_input_grad[0]:
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_bf16(_ffi.ptr(dzb), sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
                                "rpc_spconv_gemm_bf16(dgrad)")
                 else:

@@ -1094,6 +1094,16 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
     // row of 32 pixels is 8 KB contiguous. Direct 8-byte stores from the accumulator layout touched 16
     // rows per instruction (store-issue bound: 128 KB per block). BatchNorm sums from the same bf16
     // values: per thread 8 channels over its 16 pixels, then lane groups, then waves in fixed order.
+    // fused BatchNorm-backward sums: the 16 pre-activation loads of this thread's store column are issued
+    // before the accumulator tile is staged, so their latency lies under the staging and its barrier
+    uint4 zpre[CT];
+    if (g.bnz != nullptr) {
+      const int zc_ = tid & 15, zx_ = min(tx0 + (tid >> 4), g.W - 1);
+#pragma unroll
+      for (int k = 0; k < CT; ++k)
+        zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + zx_) * g.COUT + n0 +
+                                  zc_ * 8);
+    }
     unsigned char* tileb = lds;
     if (live) {
 #pragma unroll
@@ -1127,11 +1137,6 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
     if (g.bnz != nullptr) {
       // BatchNorm-backward sums of the layer this gradient enters: all 16 pre-activation loads issued
       // before the first is used (clamped addresses; a load per pixel waited out one round trip each)
-      uint4 zpre[CT];
-#pragma unroll
-      for (int k = 0; k < CT; ++k)
-        zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + min(x, g.W - 1)) * g.COUT +
-                                  n0 + c * 8);
 #pragma unroll
       for (int k = 0; k < CT; ++k) {
         const int y = ty0 + k, p = k * XTW + px;
@@ -1493,6 +1498,16 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
   if (!g.accum) {
     // bf16 tile [256 px][128 co] in LDS (granule g of pixel p at slot g ^ (p & 15)), written back as
     // whole 256-byte pixel rows; BatchNorm sums from the same bf16 values (as k_conv3x3x)
+    // fused BatchNorm-backward sums: the 16 pre-activation loads of this thread's store column are issued
+    // before the accumulator tile is staged, so their latency lies under the staging and its barrier
+    uint4 zpre[CT];
+    if (g.bnz != nullptr) {
+      const int zc_ = tid & 15, zx_ = min(tx0 + (tid >> 4), g.W - 1);
+#pragma unroll
+      for (int k = 0; k < CT; ++k)
+        zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + zx_) * g.COUT + n0 +
+                                  zc_ * 8);
+    }
     unsigned char* tileb = lds;
     if (live) {
 #pragma unroll
@@ -1526,11 +1541,6 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     if (g.bnz != nullptr) {
       // BatchNorm-backward sums of the layer this gradient enters: all 16 pre-activation loads issued
       // before the first is used (clamped addresses; a load per pixel waited out one round trip each)
-      uint4 zpre[CT];
-#pragma unroll
-      for (int k = 0; k < CT; ++k)
-        zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + min(x, g.W - 1)) * g.COUT +
-                                  n0 + c * 8);
 #pragma unroll
       for (int k = 0; k < CT; ++k) {
         const int y = ty0 + k, p = k * CT + px;

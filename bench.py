@@ -43,6 +43,9 @@ def _args():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-frames", type=int, default=2,
                     help="frames per CPU-baseline step (bounded sample: 3 warm-up + 5 timed steps)")
+    ap.add_argument("--no-parity-mode", action="store_true",
+                    help="skip the fp32 parity-mode timing that follows the headline (bf16) timing")
+    ap.add_argument("--parity-steps", type=int, default=8)
     ap.add_argument("--roofline-kernel", default="dense",
                     help="'dense' (the dominant kernel: 3x3 stride-1 bf16 conv, rpc::dn::k_conv3x3<0>) or "
                          "op,ci,co of the sparse conv launches timed with HIP events")
@@ -203,6 +206,84 @@ def _perturber_flops_per_point(adv):
     return 3 * 2.0 * sum(m.in_features * m.out_features for m in lin)
 
 
+def _perturber_stages(stages, n_valid, adv, peak):
+    """The perturber stages against the fp32 MFMA roof: its hidden layers are fp32 MFMA GEMMs over the
+    valid points (2·C_in·C_out FLOP per point per Linear forward, twice that backward: data + weight
+    gradient), so FLOP/s over the stage's HIP-event time is the figure that characterises it (its
+    compulsory HBM bytes — voxels in, perturbed voxels out — ignore the activation traffic that bounds it)."""
+    out = {}
+    fwd_pp = _perturber_flops_per_point(adv) / 3.0
+    for name, mult in (("perturber_fwd", 1.0), ("perturber_bwd", 2.0)):
+        st = (stages or {}).get(name)
+        if not st or n_valid <= 0:
+            continue
+        fl = mult * fwd_pp * n_valid
+        tf = fl / (st["avg_ms"] * 1e-3) / 1e12
+        out[name] = dict(bound="mfma", flops_per_launch=round(fl), avg_ms=st["avg_ms"], achieved=round(tf, 2),
+                         peak=peak, unit="TFLOP/s", frac=round(tf / peak, 4), valid_points=int(n_valid),
+                         work="2*C_in*C_out FLOP per valid point per Linear layer (x1 forward, x2 backward)")
+    return out
+
+
+def _parity_mode(a, data, ready, dev, nus, fpf):
+    """The reference's own precision on the same frames: the metric's config trains fp32
+    (configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:130-131, type
+    'OptimWrapper'). A fresh model (same seed) in the fp32 parity mode — fp32 perturber, fp32 sparse
+    encoder, SECOND / FPN / head on the fp32-MFMA engine — the mode the 1e-4 parity tests cover, timed
+    like the headline: warm-up, then K steps between barrier + synchronize, max over ranks."""
+    from robustpointclouds_amd import stage_timer
+    from robustpointclouds_amd.trainer import Trainer, make_kitti_model, make_nus_model
+    torch.manual_seed(0)
+    model = (make_nus_model(device=dev, epoch=3) if nus else
+             make_kitti_model(num_classes=a.classes, device=dev, epoch=3, variant=a.model))
+    tr = Trainer(model, ddp=dist.is_initialized(), bf16=False, device=dev)
+    NB, W, K = len(data), 3, a.parity_steps
+    for i in range(W):
+        tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0], next_ready=ready)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    t0 = time.perf_counter()
+    for i in range(K):
+        tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0], next_ready=ready)
+    torch.cuda.synchronize()
+    if dist.is_initialized():
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    # one more (eager) step with the stage timers on, for the perturber's fp32-MFMA figure
+    stage_timer.TIMER.reset()
+    stage_timer.TIMER.enabled = True
+    tr.train_step(*data[K % NB], next_points=data[(K + 1) % NB][0], next_ready=ready)
+    torch.cuda.synchronize()
+    stage_timer.TIMER.enabled = False
+    stages = stage_timer.TIMER.summary()
+    stage_timer.TIMER.reset()
+    flags = getattr(model, "_last_flags", None)
+    n_valid = float(flags[4].item()) if flags is not None else 0.0
+    if dist.is_initialized():
+        t = torch.tensor([dt], device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    world = dist.get_world_size() if dist.is_initialized() else 1
+    fps = world * a.batch * K / dt
+    res = dict(dtype="fp32", frames_per_s=round(fps, 3), ms_per_step=round(1000 * dt / K, 3), steps=K, warmup=W,
+               kernel_dtype="fp32 end to end: voxelize, perturber (fp32 MFMA), sparse encoder, SECOND/FPN and "
+                            "head GEMMs on v_mfma_f32_16x16x4_f32, fp32 losses")
+    if fpf:
+        ach = fps / world * fpf / 1e12
+        res["step_roofline"] = dict(bound="mfma", flop_per_frame=round(fpf), achieved=round(ach, 2),
+                                    peak=PEAK["fp32_mfma"], unit="TFLOP/s", frac=round(ach / PEAK["fp32_mfma"], 4),
+                                    work="the headline's algorithmic FLOPs per frame (dense + sparse + perturber, "
+                                         "forward + data gradient + weight gradient) per GPU")
+    if stages:
+        res["stage_roofline"] = dict(bound="hbm", unit="GB/s", stages=stages)
+    if model.__dict__.get("adversary") is not None or getattr(model, "adversary", None) is not None:
+        res["perturber_roofline"] = _perturber_stages(stages, n_valid, model.adversary, PEAK["fp32_mfma"])
+    del tr, model
+    torch.cuda.empty_cache()
+    return res
+
+
 def _launch_ranks(n: int) -> int:
     """Re-run this script under torch.distributed.run with n ranks (child process; no GPU touched
     here) and return its exit status."""
@@ -303,6 +384,15 @@ def main():
         t = torch.tensor([dt], device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
+    n_valid = 0.0
+    if step_flops is not None:
+        n_valid = step_flops["perturber"] / _perturber_flops_per_point(model.adversary) if model.adversary is not None \
+            else 0.0
+    # the reference's precision (fp32) on the same frames, after the headline timing (all ranks take part)
+    parity = None
+    if not a.fp32 and not a.no_parity_mode and a.roofline_kernel == "dense" and not nus:
+        fpf = step_flops["total"] / a.batch if step_flops is not None else None
+        parity = _parity_mode(a, data, ready, dev, nus, fpf)
     frames = world * a.batch * a.steps
     if rank == 0:
         metric = ("adversarial-train frames/sec/GPU, CenterPoint nuScenes 10-class (BASELINE config 4)" if nus else
@@ -373,6 +463,10 @@ def main():
                 k: round(v / a.batch) for k, v in step_flops.items() if k != "total"},
                 achieved=round(frames / dt * fpf / 1e12, 1), peak=PEAK["fp32_mfma" if a.fp32 else "bf16_mfma"], unit="TFLOP/s",
                 frac=round(frames / dt * fpf / 1e12 / PEAK["fp32_mfma" if a.fp32 else "bf16_mfma"], 4))
+        if stages and step_flops is not None and model.adversary is not None:
+            res["perturber_roofline"] = _perturber_stages(stages, n_valid, model.adversary, PEAK["fp32_mfma"])
+        if parity is not None:
+            res["parity_mode"] = parity
         if not a.no_cpu_baseline and a.model == "voxelnet":
             res["cpu_baseline"] = cpu_baseline(a.cpu_frames, a.classes)
         print(json.dumps(res), flush=True)

@@ -251,6 +251,37 @@ int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int re
 int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
                            const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
                            float* part, int epi, void* stream);
+/* the same GEMM with the BatchNorm finalize of its partial sums fused in (the last
+ * arriving blocks sum the partial rows in two fixed-order levels and apply rpc_bn_finalize's arithmetic),
+ * replacing the rpc_bn_finalize launch that followed it: epi 0 -> mode 0 (this layer's bn + running stats),
+ * epi 1 -> mode 1 (bnb, dgamma, dbeta of the layer whose ReLU mask the epilogue applies; fbn = its
+ * forward bn). `part` is still written (the fused sums read it). fin NULL = rpc_spconv_gemm_bf16_n.
+ * fin->ticket: rpc_bn_fin_tickets(n_out) counters, zero before first use (every launch leaves them zero);
+ * fin->gpart: rpc_bn_fin_groups(n_out) * 2 * ng doubles. ng <= 256. */
+typedef struct {
+  unsigned* ticket;
+  double* gpart;
+  int mode;
+  const float* gamma;
+  const float* beta;
+  float eps, momentum;
+  float* running_mean;
+  float* running_var;
+  const float* fbn;
+  float* bn;
+  float* dgamma;
+  float* dbeta;
+} RpcBnFin;
+int rpc_bn_fin_groups(int n_out);
+int rpc_bn_fin_tickets(int n_out);
+int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
+                             const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
+                             float* part, int epi, const RpcBnFin* fin, void* stream);
+/* kernel behind rpc_spconv_gemm_bf16[_n|_fin] (A/B measurement, tests; env RPC_SPGEMM): 0 (default) = one
+ * offset of look-ahead in registers, 1 = the S-stage LDS-DMA ring (k_gemm_pipe), 2 / 3 = its 4-wave / 3-stage
+ * forms. Same bits in every mode. 4..19: timing arms (garbage results). mode < 0 queries. Returns the
+ * previous mode. */
+int rpc_spconv_gemm_bf16_mode(int mode);
 /* dW[k] = sum_r h[nbr[r,k]]^T dz[r] (bf16 rows, fp32 accumulate, fixed-order reduction) */
 size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co);
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
@@ -285,6 +316,9 @@ typedef struct {
   float* dW;
   float* dgamma;
   float* dbeta;
+  unsigned* fin_ticket;  /* bf16 layers: rpc_bn_fin_tickets(n_in) zeroed counters — the data gradient into the
+                            layer below then finalizes that layer's BatchNorm backward in its own launch
+                            (rpc_spconv_gemm_bf16_fin); NULL: a separate rpc_bn_finalize */
 } RpcSparseLayer;
 /* Side-work stream (no reference counterpart: the reference runs one stream). which > 0: the device's
  * least stream priority, < 0: greatest, 0: default; hipStreamNonBlocking. */

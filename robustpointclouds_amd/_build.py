@@ -57,6 +57,13 @@ def build(force: bool = False, jobs: int | None = None) -> str:
     jobs = jobs or min(len(srcs), max(1, (os.cpu_count() or 4) // 2), 16)
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(lambda s: _compile(s, force), srcs))
+    # a kernel template whose host pass failed (hipcc defers device-code diagnostics in the host pass and can
+    # drop the kernel silently) leaves its launch stub undefined: fail the build, not the first dlopen
+    for o in objs:
+        r = subprocess.run(["nm", "-C", "--undefined-only", o], capture_output=True, text=True)
+        bad = [ln.strip() for ln in r.stdout.splitlines() if "__device_stub__" in ln]
+        if bad:
+            raise RuntimeError(f"{os.path.basename(o)}: kernels without a host launch stub:\n" + "\n".join(bad[:8]))
     vobj = os.path.join(OBJ, "version.o")
     subprocess.run(["g++", "-O2", "-fPIC", "-c", ver, "-o", vobj], check=True)
     tmp = LIB + ".tmp"

@@ -91,7 +91,15 @@ class RpcSparseLayer(C.Structure):
                 ("nbr", C.c_void_p), ("nbr_in", C.c_void_p), ("z", C.c_void_p), ("bn", C.c_void_p),
                 ("out", C.c_void_p), ("h_in", C.c_void_p), ("src", C.c_void_p), ("src_bn", C.c_void_p),
                 ("W", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("btd", C.c_void_p),
-                ("dW", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p)]
+                ("dW", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("fin_ticket", C.c_void_p)]
+
+
+class RpcBnFin(C.Structure):
+    """include/rpc_hip.h RpcBnFin (BatchNorm finalize fused into rpc_spconv_gemm_bf16_fin)."""
+    _fields_ = [("ticket", C.c_void_p), ("gpart", C.c_void_p), ("mode", C.c_int), ("gamma", C.c_void_p),
+                ("beta", C.c_void_p), ("eps", C.c_float), ("momentum", C.c_float), ("running_mean", C.c_void_p),
+                ("running_var", C.c_void_p), ("fbn", C.c_void_p), ("bn", C.c_void_p), ("dgamma", C.c_void_p),
+                ("dbeta", C.c_void_p)]
 
 
 class RpcCenterCfg(C.Structure):
@@ -141,6 +149,11 @@ SIGNATURES = {
     "rpc_spconv_prep_weight_bf16_batch": (i32, [vp, i32, vp]),
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_gemm_bf16_n": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
+    "rpc_spconv_gemm_bf16_mode": (i32, [i32]),
+    "rpc_bn_fin_groups": (i32, [i32]),
+    "rpc_bn_fin_tickets": (i32, [i32]),
+    "rpc_spconv_gemm_bf16_fin": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
+                                       C.POINTER(RpcBnFin), vp]),
     "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_wgrad_bf16": (i32, [vp, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
     "rpc_sparse_backward_workspace_size": (sz, [vp, i32]),

@@ -31,7 +31,7 @@ from torch import nn
 from .adversarial_loss import parse_losses
 
 
-def select_engines(model: nn.Module, bf16: bool) -> None:
+def select_engines(model: nn.Module, bf16: bool, pin: bool = False) -> None:
     """Route the dense part through the HIP engines: bf16 perf mode (sparse convs on bf16 MFMA,
     dense BEV handed over as a bf16 NHWC image to SECOND / SECONDFPN on the bf16 dense engine and
     the bf16 head GEMM) or fp32 parity mode (fp32 sparse convs, an fp32 NHWC image through the
@@ -51,6 +51,8 @@ def select_engines(model: nn.Module, bf16: bool) -> None:
         elif bf16:
             mod.to(memory_format=torch.channels_last)
     model.__dict__["_engine_mode"] = bool(bf16)
+    if pin:
+        model.__dict__["_engine_pinned"] = True
 
 
 def _autocast_on() -> bool:
@@ -65,7 +67,13 @@ class DetectorBase(nn.Module):
 
     # ------------------------------------------------------------------ engines
     def _sync_engines(self, device: torch.device) -> None:
-        if device.type != "cuda":
+        """Follow the autocast state with the engines: bf16 (perf mode) under autocast, fp32 (parity mode)
+        outside it — unless an engine mode was selected explicitly (Trainer / select_engines(pin=True)):
+        then that mode stays, so val_step / test_step run on the engines the model trains on. A switch
+        allocates the other engine's HIP graphs and dense BEV buffers on first use (the sparse encoder keeps
+        only the current shapes' buffers); switching back to fp32 keeps the channels_last layout of the
+        non-HIP modules (results are layout-independent)."""
+        if device.type != "cuda" or self.__dict__.get("_engine_pinned"):
             return
         want = _autocast_on()
         if self.__dict__.get("_engine_mode") != want:

@@ -15,6 +15,8 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 
+#include <map>
+#include <mutex>
 #include <vector>
 
 #include "common.h"
@@ -41,19 +43,35 @@ struct Arena {
 };
 
 // events of the main -> weight-gradient stream hand-offs, reused across calls (re-recording an event
-// after a stream has been told to wait on it is safe: the wait captured the earlier record)
-std::vector<hipEvent_t> g_events;
-hipEvent_t event_at(size_t i) {
-  while (g_events.size() <= i) {
+// after a stream has been told to wait on it is safe: the wait captured the earlier record). One set per
+// device (an event belongs to the device current at its creation), used under that device's lock: the
+// whole issue of one rpc_sparse_backward holds it, so two host threads never interleave records and waits
+// on the same events.
+struct DevEvents {
+  std::mutex mu;
+  std::vector<hipEvent_t> ev;
+};
+std::mutex g_dev_mu;
+std::map<int, DevEvents*> g_dev_events;   // never freed: the process's devices
+
+DevEvents* device_events(int dev) {
+  std::lock_guard<std::mutex> lk(g_dev_mu);
+  DevEvents*& d = g_dev_events[dev];
+  if (!d) d = new DevEvents();
+  return d;
+}
+
+hipEvent_t event_at(DevEvents* d, size_t i) {
+  while (d->ev.size() <= i) {
     hipEvent_t e;
     if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) return nullptr;
-    g_events.push_back(e);
+    d->ev.push_back(e);
   }
-  return g_events[i];
+  return d->ev[i];
 }
 
 int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coors_last, const int* shape, int flags,
-        float* dfeat, Arena& A, hipStream_t st, hipStream_t wg) {
+        float* dfeat, Arena& A, hipStream_t st, hipStream_t wg, DevEvents* evs) {
 #define CHK(x)                 \
   do {                         \
     if (!A.dry) {              \
@@ -70,6 +88,7 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
   // gradient contributions to materialised outputs (block outputs and their identities)
   std::vector<std::vector<const float*>> G(nl);
   const bool split = wg != nullptr && wg != st;
+  float* bnb_fused = nullptr;   // bnb of layer li, already finalized by layer li+1's data-gradient launch
   for (int li = nl - 1; li >= 0; --li) {
     const RpcSparseLayer& l = L[li];
     const int n_out = l.n_out;
@@ -82,10 +101,15 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
                                   part, st));
       if (l.res >= 0) G[l.res].push_back(dy);
     }
-    // BatchNorm backward statistics -> bnb, dgamma, dbeta
-    float* bnb = (float*)A.take(sizeof(float) * 5 * (size_t)l.co);
-    CHK(rpc_bn_finalize(part, nblk, l.co, n_out, 1, l.gamma, l.beta, 0.0f, 0.0f, nullptr, nullptr, l.bn, bnb, l.dgamma,
-                        l.dbeta, nullptr, st));
+    // BatchNorm backward statistics -> bnb, dgamma, dbeta (unless the data gradient that produced the partial
+    // sums already finalized them)
+    float* bnb = bnb_fused;
+    bnb_fused = nullptr;
+    if (!bnb) {
+      bnb = (float*)A.take(sizeof(float) * 5 * (size_t)l.co);
+      CHK(rpc_bn_finalize(part, nblk, l.co, n_out, 1, l.gamma, l.beta, 0.0f, 0.0f, nullptr, nullptr, l.bn, bnb,
+                          l.dgamma, l.dbeta, nullptr, st));
+    }
     // weight gradient, on the second stream (it reads only this layer's dz / input rows)
     void* dzb = nullptr;
     if (l.bf16) {
@@ -94,7 +118,7 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
     }
     hipStream_t sw = split ? wg : st;
     if (split && !A.dry) {
-      hipEvent_t e = event_at((size_t)li);
+      hipEvent_t e = event_at(evs, (size_t)li);
       if (!e) return RPC_ERR_HIP;
       RPC_CHECK(hipEventRecord(e, st));
       RPC_CHECK(hipStreamWaitEvent(wg, e, 0));
@@ -122,7 +146,22 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
       float* din = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
       nblk = cdiv(n_in, BM) > 0 ? cdiv(n_in, BM) : 1;
       part = (float*)A.take(sizeof(float) * (size_t)nblk * 2 * l.ci);
-      if (l.bf16)
+      if (l.bf16 && l.fin_ticket && n_in > 0) {
+        // + the layer below's BatchNorm-backward finalize (its bnb, dgamma, dbeta) in the same launch
+        RpcBnFin fin;
+        memset(&fin, 0, sizeof(fin));
+        fin.ticket = l.fin_ticket;
+        fin.gpart = (double*)A.take(sizeof(double) * 2 * (size_t)rpc_bn_fin_groups(n_in) * l.ci);
+        fin.mode = 1;
+        fin.gamma = prev.gamma;
+        fin.beta = prev.beta;
+        fin.fbn = prev.bn;
+        fin.bn = bnb_fused = (float*)A.take(sizeof(float) * 5 * (size_t)l.ci);
+        fin.dgamma = prev.dgamma;
+        fin.dbeta = prev.dbeta;
+        CHK(rpc_spconv_gemm_bf16_fin(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part,
+                                     1, &fin, st));
+      } else if (l.bf16)
         CHK(rpc_spconv_gemm_bf16_n(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part, 1, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, prev.z, prev.bn, din, part, st));
@@ -137,7 +176,7 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
     }
   }
   if (split && !A.dry) {   // the weight gradients are complete before the main stream goes on
-    hipEvent_t e = event_at((size_t)nl);
+    hipEvent_t e = event_at(evs, (size_t)nl);
     if (!e) return RPC_ERR_HIP;
     RPC_CHECK(hipEventRecord(e, wg));
     RPC_CHECK(hipStreamWaitEvent(st, e, 0));
@@ -165,7 +204,7 @@ extern "C" size_t rpc_sparse_backward_workspace_size(const RpcSparseLayer* layer
   if (check_layers(layers, nlayers)) return 0;
   Arena A{nullptr, 0, 0, true};
   int shape[4] = {1, 1, 1, 1};
-  if (run(layers, nlayers, nullptr, nullptr, shape, 0, nullptr, A, nullptr, nullptr)) return 0;
+  if (run(layers, nlayers, nullptr, nullptr, shape, 0, nullptr, A, nullptr, nullptr, nullptr)) return 0;
   return A.off + 256;
 }
 
@@ -179,11 +218,16 @@ extern "C" int rpc_sparse_backward(const RpcSparseLayer* layers, int nlayers, co
   // dry pass first: a workspace that is too small fails before anything is launched
   {
     Arena D{nullptr, 0, 0, true};
-    if (run(layers, nlayers, grad_dense, coors_last, shape, flags, dfeat, D, nullptr, nullptr)) return RPC_ERR_ARG;
+    if (run(layers, nlayers, grad_dense, coors_last, shape, flags, dfeat, D, nullptr, nullptr, nullptr))
+      return RPC_ERR_ARG;
     if (D.off > workspace_bytes) return RPC_ERR_WORKSPACE;
   }
+  int dev = 0;
+  RPC_CHECK(hipGetDevice(&dev));
+  DevEvents* evs = device_events(dev);
+  std::lock_guard<std::mutex> lk(evs->mu);
   return run(layers, nlayers, grad_dense, coors_last, shape, flags, dfeat, A, (hipStream_t)stream,
-             (hipStream_t)wgrad_stream);
+             (hipStream_t)wgrad_stream, evs);
 }
 
 // Side-work streams at the device's least priority (the trainer's batch prefetch, the sparse rulebooks

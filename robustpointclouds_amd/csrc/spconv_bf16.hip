@@ -68,11 +68,90 @@ struct GB {
   const float* ez;    // E_DGRAD: z of the layer whose grad this is [Nout][CO_real]
   const float* ebn;   // E_DGRAD: scale, beta, mean, invstd [4*CO_real]
   float* part;        // [blocks][2*NGP] or null
+  RpcBnFin fin;       // k_gemm_pipe: BatchNorm finalize by the last-arriving blocks (fin.ticket null: off)
 };
+
+// ---- BatchNorm finalize fused into the GEMM (k_gemm_pipe, RpcBnFin): the partial rows every block writes
+// are summed in two fixed-order levels by last-arriving blocks — each group of FGS consecutive blocks
+// (logical index lb) by its last arriver, in row order, into a double row gpart[q]; the groups by the
+// last group finisher, in group order — which then applies rpc_bn_finalize's arithmetic (mode 0 / 1) to
+// the totals. Replaces the standalone k_bn_finalize launch after each GEMM (run-to-run deterministic; the
+// totals are summed in another order than k_bn_finalize's, so they may differ from it in the last bits).
+constexpr int FGS = 32;
+__host__ __device__ inline int fin_groups(int nblk) { return (nblk + FGS - 1) / FGS; }
+
+template <int NTHR>
+__device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int* flag) {
+  const RpcBnFin& f = g.fin;
+  const int C = g.CO_real, C2 = 2 * C;
+  const int nblk = (int)gridDim.x, ng = fin_groups(nblk), q = lb / FGS;
+  const int nrow = (g.Nout + BM - 1) / BM;
+  const int gb0 = q * FGS, gbn = min(FGS, nblk - gb0);
+  if (!last_block_arrive_2d(f.ticket + 1 + q, flag, gbn)) return;
+  {
+    const int pr0 = gb0 * PRB, pr1 = min(nrow, (gb0 + gbn) * PRB);
+    for (int j = threadIdx.x; j < C2; j += NTHR) {
+      double t = 0.0;
+      int r = pr0;
+      for (; r + 8 <= pr1; r += 8) {
+        float v[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] = g.part[(long long)(r + i) * C2 + j];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) t += (double)v[i];
+      }
+      for (; r < pr1; ++r) t += (double)g.part[(long long)r * C2 + j];
+      f.gpart[(long long)q * C2 + j] = t;
+    }
+  }
+  if (!last_block_arrive_2d(f.ticket, flag, ng)) return;
+  for (int j = threadIdx.x; j < C2; j += NTHR) {
+    double t = 0.0;
+    int r = 0;
+    for (; r + 8 <= ng; r += 8) {
+      double v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = f.gpart[(long long)(r + i) * C2 + j];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) t += v[i];
+    }
+    for (; r < ng; ++r) t += f.gpart[(long long)r * C2 + j];
+    sh[j] = t;
+  }
+  __syncthreads();
+  const int N = g.Nout;
+  for (int c = threadIdx.x; c < C; c += NTHR) {
+    const double s1 = sh[c], s2 = sh[C + c];
+    if (f.mode == 0) {   // k_bn_finalize mode 0
+      const double mean = s1 / N;
+      double var = s2 / N - mean * mean;
+      if (var < 0) var = 0;
+      const float invstd = 1.0f / sqrtf((float)var + f.eps);
+      f.bn[c] = f.gamma[c] * invstd;
+      f.bn[C + c] = f.beta[c];
+      f.bn[2 * C + c] = (float)mean;
+      f.bn[3 * C + c] = invstd;
+      const double uvar = N > 1 ? var * N / (N - 1) : var;
+      f.running_mean[c] = (1.0f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
+      f.running_var[c] = (1.0f - f.momentum) * f.running_var[c] + f.momentum * (float)uvar;
+    } else {             // k_bn_finalize mode 1
+      f.bn[c] = f.gamma[c] * f.fbn[3 * C + c];
+      f.bn[C + c] = (float)(s1 / N);
+      f.bn[2 * C + c] = (float)(s2 / N);
+      f.bn[3 * C + c] = f.fbn[2 * C + c];
+      f.bn[4 * C + c] = f.fbn[3 * C + c];
+      if (f.dgamma) f.dgamma[c] = (float)s2;
+      if (f.dbeta) f.dbeta[c] = (float)s1;
+    }
+  }
+}
 
 // Occupancy: the <= 64 x 64 tiles are held to 64 VGPRs (8 waves per SIMD, 4 blocks per CU) — at 72 the
 // 106k-row 64-channel layers needed 1.08 rounds of 3 blocks per CU (k_gemm_bf16<64,4,1> 60.6 -> 51.5 us)
-template <int KGP, int NT, int EPI>
+// DBG (timing attribution only, rpc_spconv_gemm_bf16_mode 4 + DBG for the 64 x 64 tiles; results are
+// garbage): bit 0 = no MFMAs, bit 1 = every gather offset out of range (no memory traffic, same
+// instructions), bit 2 = the same for the weight tiles, bit 3 = no gather instructions at all
+template <int KGP, int NT, int EPI, int DBG = 0>
 __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) void k_gemm_bf16(GB g) {
   constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, RT = rt_of(KGP, NT), WR = 16 * RT, GBM = WR * GW;
   constexpr int KS = KGP / 32;
@@ -160,7 +239,11 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const int c0 = ks * 32 + ag * 8;
-        unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
+        if (DBG & 8) {
+          dst[rt][ks] = make_uint4(0u, 0u, 0u, 0u);
+          continue;
+        }
+        unsigned off = (src >= 0 && c0 < g.CP && !(DBG & 2)) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
         asm volatile("" : "+v"(off));   // keeps the select a select (else: one load per branch of a diamond)
         dst[rt][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
       }
@@ -171,7 +254,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       const int v = tid + j * GBLK;
-      unsigned off = (BV % GBLK == 0 || v < BV) ? base + (unsigned)v * 16u : OOB;
+      unsigned off = ((BV % GBLK == 0 || v < BV) && !(DBG & 4)) ? base + (unsigned)v * 16u : OOB;
       asm volatile("" : "+v"(off));
       dst[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, off, 0, 0));
     }
@@ -204,7 +287,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
       const int k = klist[t];
       load_b(klist[t + 2 < NK ? t + 2 : NK - 1], bn);
       load_a(klist[t + 1 < NK ? t + 1 : t], an);
-      if ((my >> k) & 1u) {
+      if (((my >> k) & 1u) && !(DBG & 1)) {
         const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -264,10 +347,10 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
             v = h > 0.0f ? v : 0.0f;
             float xh = (zz - pb[2]) * pb[3];
             s1[n] += v;
-            s2[n] += v * xh;
+            s2[n] = fmaf(v, xh, s2[n]);   // explicit: contraction left to -ffp-contract differed between kernels
           } else {
             s1[n] += v;
-            s2[n] += v * v;
+            s2[n] = fmaf(v, v, s2[n]);
           }
           g.out[(long long)row * g.CO_real + col] = v;
         }
@@ -299,6 +382,277 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     float s = 0.0f;
     for (int ww = 0; ww < WPR; ++ww) s += sP[WPR * h + ww][which * NGP + c];
     g.part[(long long)prow * 2 * C + jj] = s;
+  }
+  if (g.fin.ticket) {
+    // the neighbour table is free: the totals (double [2C], C <= 256 -> 4 KB) and the arrival flag go there
+    static_assert(GBM * MAXK * 4 >= 4096 + 4, "LDS for the fused finalize");
+    fused_bn_finalize<GBLK>(g, lb, PRB, (double*)sN, sN + 1024);
+  }
+}
+
+// ------------------------------------------------------------------ r04: deep LDS-DMA ring
+// k_gemm_bf16 waits out one memory round trip per kernel offset: the A fragments of offset t+1 are the
+// only loads in flight while offset t computes, and one offset of MFMAs (8 per wave at 64 x 64) is far
+// shorter than a gather under load (~1.7 us per offset step at the 106k-row layers: 23 steps, 39 us).
+// k_gemm_pipe issues S-1 offsets ahead instead, straight into LDS (`buffer_load ... lds`, no VGPR round
+// trip): per offset and wave the wave's own 16 gathered rows (16 x KGP bf16, NA instructions) and its
+// share of the weight tile (NGP x KGP bf16, WI instructions per block), into ring slot t % S. Per step:
+// wait for this wave's loads of stage t (vmcnt of the stages issued after it), one barrier (every wave's
+// stage-t loads have landed and every wave is done with stage t-1, whose slot the next issue reuses),
+// issue stage t+S-1, then the MFMAs of stage t from LDS. LDS rows are KGP bf16 (G = KGP/8 granules of
+// 16 B) with granule j of row r stored at j ^ pswz(r): every ds_read_b128 lane group of an A or B
+// fragment read then hits 16 distinct bank slots (exhaustive check, tools/swz_check.py). Gathers of
+// absent neighbours (and the padding granules of a 16-channel row) get an offset past the buffer range:
+// the DMA writes zeros and touches no memory. Same MFMAs in the same order per accumulator as
+// k_gemm_bf16 (offsets ascending, K-steps, output tiles), so the same bits; same epilogue.
+__host__ __device__ constexpr int pswz(int G, int row) { return G == 16 ? (row & 15) : ((row >> 1) & (G - 1)); }
+
+template <int NPS, int R>
+__device__ __forceinline__ void vm_wait(int rem) {
+  if constexpr (R > 0) {
+    if (rem >= R) {
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * NPS) : "memory");
+      return;
+    }
+    vm_wait<NPS, R - 1>(rem);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+template <int KGP, int NT, int GW, int S>
+struct PipeCfg {
+  // RT: 16-row MFMA tiles per wave, as k_gemm_bf16 (rt_of): the same rows per wave and per partial row,
+  // so the BatchNorm partial sums are added in the same order (same bits)
+  static constexpr int RT = rt_of(KGP, NT);
+  static constexpr int G = KGP / 8, KS = KGP / 32, NGP = NT * 16, WR = 16 * RT, GBM = WR * GW, GBLK = 64 * GW;
+  static constexpr int ABYTES = WR * KGP * 2;            // one wave's gathered rows
+  static constexpr int NA = WR * G / 64;                 // their DMA instructions (1 KB each)
+  static constexpr int WBYTES = NGP * KGP * 2;           // one offset's weight tile
+  static constexpr int WI = WBYTES / 1024;               // its DMA instructions (per block)
+  static constexpr int NWH = (WI + GW - 1) / GW, NWL = WI / GW, WREM = WI % GW;
+  static constexpr int STAGE = GW * ABYTES + WBYTES;
+  static constexpr int SN = GBM * MAXK * 4;
+  static constexpr int MISC = 256;                       // wmask[GW], klist[MAXK], nk
+  static constexpr int LDS = S * STAGE + SN + MISC;
+  static_assert(KGP % 32 == 0 && WBYTES % 1024 == 0 && ABYTES % 1024 == 0, "DMA tiles are whole KBs");
+  static_assert(GW * 2 * NGP * 4 <= S * STAGE && GW <= 8, "epilogue partials alias the ring");
+  static_assert(LDS <= 160 * 1024, "LDS");
+};
+
+template <int KGP, int NT, int EPI, int GW, int S>
+__global__ __launch_bounds__(64 * GW, 1) void k_gemm_pipe(GB g) {
+  using P = PipeCfg<KGP, NT, GW, S>;
+  constexpr int G = P::G, KS = P::KS, NGP = P::NGP, GBM = P::GBM, GBLK = P::GBLK, NA = P::NA, RT = P::RT;
+  constexpr int WR = P::WR;
+  // ONE LDS object: separate __shared__ arrays get alias scopes, and the compiler then drains every
+  // DMA in flight (vmcnt(0)) before the operand reads of each step (dense_conv.hip k_conv3x3x)
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[P::LDS];
+  int* const sN = (int*)(lds + S * P::STAGE);
+  unsigned* const wmask = (unsigned*)(lds + S * P::STAGE + P::SN);
+  int* const klist = (int*)(wmask + 8);
+  int* const nkp = klist + 32;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int lb = dn::xcd_remap(blockIdx.x, gridDim.x);
+  const int r0 = lb * GBM;
+  const int K = g.K;
+  {
+    // neighbour indices of the wave's rows into LDS, the wave's offset mask by ballots (k_gemm_bf16)
+    const int rr = lane & 15, k4 = lane >> 4;
+    unsigned m = 0;
+    constexpr int NP = (MAXK + 3) / 4;
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      const int lr = w * WR + rt * 16 + rr, row = r0 + lr;
+      int nv[NP];
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int k = 4 * i + k4;
+        nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
+      }
+#pragma unroll
+      for (int i = 0; i < NP; ++i) {
+        const int kb = 4 * i, k = kb + k4, v = nv[i];
+        if (kb >= K) break;
+        if (k < K) sN[lr * MAXK + k] = v;
+        const unsigned long long b = __ballot(v >= 0);
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          if ((b >> (16 * q)) & 0xffffull) m |= 1u << (kb + q);
+      }
+    }
+    if (lane == 0) wmask[w] = m;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    unsigned m = 0;
+    for (int q = 0; q < GW; ++q) m |= wmask[q];
+    int n = 0;
+    for (int k = 0; k < K; ++k)
+      if ((m >> k) & 1u) klist[n++] = k;
+    *nkp = n;
+  }
+  __syncthreads();
+  const int NK = *nkp;
+  const unsigned my = wmask[w];
+
+  // ---- fixed per-lane DMA geometry. A instruction i writes LDS granule P = i*64 + lane of this wave's
+  // slot: local row P / G, stored granule P % G, which holds source granule (P % G) ^ pswz(row)
+  constexpr unsigned OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.bt, (short)0, 0x7fffffff, 0x00020000);
+  int ar[NA], ac[NA];
+#pragma unroll
+  for (int i = 0; i < NA; ++i) {
+    const int Pg = i * 64 + lane, r = Pg / G, j = (Pg % G) ^ pswz(G, r);
+    ar[i] = (w * WR + r) * MAXK;
+    ac[i] = j * 8 < g.CP ? j * 8 : -1;
+  }
+  constexpr int NWH = P::NWH;
+  int wo[NWH > 0 ? NWH : 1];
+#pragma unroll
+  for (int m = 0; m < NWH; ++m) {
+    const int q = w + m * GW, Pg = q * 64 + lane, n = Pg / G, j = (Pg % G) ^ pswz(G, n);
+    wo[m] = q < P::WI ? (n * KGP + j * 8) * 2 : (int)OOB;
+  }
+  // (the DMA builtin's offsets as explicit int casts: passed as plain lvalues — or unsigned — hipcc dropped
+  // the kernel from the host pass without a diagnostic: no launch stub, an undefined symbol at load time)
+  auto issue = [&](int t) {
+    unsigned char* st = lds + (t % S) * P::STAGE;
+    const int k = __builtin_amdgcn_readfirstlane(klist[t]);   // the weight offset goes in an SGPR (soffset)
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int src = sN[ar[i] + k];
+      const int off = (src >= 0 && ac[i] >= 0) ? (int)(((unsigned)src * (unsigned)g.CP + (unsigned)ac[i]) * 2u)
+                                               : (int)OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(st + w * P::ABYTES + i * 1024),
+                                               16, (int)off, 0, 0, 0);
+    }
+    const int kb = k * P::WBYTES;
+#pragma unroll
+    for (int m = 0; m < NWH; ++m) {
+      const int q = w + m * GW;
+      if (m < P::NWL || w < P::WREM)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(
+            rsb, (__attribute__((address_space(3))) void*)(st + GW * P::ABYTES + q * 1024), 16, (int)wo[m], (int)kb, 0, 0);
+    }
+  };
+
+  f32x4 acc[RT][NT];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  // operand byte offsets inside a slot: A rows rt*16 + lane&15 of this wave, B rows n*16 + lane&15;
+  // granule ks*4 + (lane >> 4), swizzled by the row (pswz(n*16 + r) = pswz(r))
+  const int a15 = lane & 15, q4 = lane >> 4;
+  int aoff[RT][KS], boff[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+      aoff[rt][ks] = w * P::ABYTES + ((rt * 16 + a15) * G + ((ks * 4 + q4) ^ pswz(G, a15))) * 16;
+    boff[ks] = GW * P::ABYTES + (a15 * G + ((ks * 4 + q4) ^ pswz(G, a15))) * 16;
+  }
+
+#pragma unroll
+  for (int t = 0; t < S - 1; ++t)
+    if (t < NK) issue(t);
+  constexpr int NPS_H = NA + P::NWH, NPS_L = NA + P::NWL;
+  for (int t = 0; t < NK; ++t) {
+    const int rem = min(S - 2, NK - 1 - t);   // stages issued after stage t
+    if (P::WREM == 0 || w < P::WREM) vm_wait<NPS_H, S - 2>(rem);
+    else vm_wait<NPS_L, S - 2>(rem);
+    // a bare barrier: __syncthreads() is a workgroup fence and waits for every DMA in flight (vmcnt(0))
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    if (t + S - 1 < NK) issue(t + S - 1);
+    const int k = __builtin_amdgcn_readfirstlane(klist[t]);
+    if ((my >> k) & 1u) {
+      const unsigned char* st = lds + (t % S) * P::STAGE;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        bf16x8 av[RT];
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt) av[rt] = *(const bf16x8*)(st + aoff[rt][ks]);
+#pragma unroll
+        for (int n = 0; n < NT; ++n) {
+          const bf16x8 bv = *(const bf16x8*)(st + boff[ks] + n * 16 * G * 16);
+#pragma unroll
+          for (int rt = 0; rt < RT; ++rt)
+            acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[rt], bv, acc[rt][n], 0, 0, 0);
+        }
+      }
+    }
+  }
+
+  // epilogue: k_gemm_bf16's, line for line
+  float s1[NT], s2[NT];
+#pragma unroll
+  for (int n = 0; n < NT; ++n) s1[n] = s2[n] = 0.0f;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int rb = r0 + w * WR + rt * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      int col = n * 16 + (lane & 15);
+      float zr[4], pb[4];
+      if (EPI == E_DGRAD) {
+        const int C = g.CO_real, cc = min(col, C - 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)min(rb + j, g.Nout - 1) * C + cc];
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        int row = rb + j;
+        float v = acc[rt][n][j];
+        if (row < g.Nout && col < g.CO_real) {
+          if (EPI == E_DGRAD) {
+            const float zz = zr[j];
+            float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
+            v = h > 0.0f ? v : 0.0f;
+            float xh = (zz - pb[2]) * pb[3];
+            s1[n] += v;
+            s2[n] = fmaf(v, xh, s2[n]);   // explicit: contraction left to -ffp-contract differed between kernels
+          } else {
+            s1[n] += v;
+            s2[n] = fmaf(v, v, s2[n]);
+          }
+          g.out[(long long)row * g.CO_real + col] = v;
+        }
+      }
+    }
+  }
+  if (EPI == E_PLAIN || g.part == nullptr) return;
+  float* const sP = (float*)lds;   // aliases the ring: every wave is past its last step's reads
+  __syncthreads();
+#pragma unroll
+  for (int n = 0; n < NT; ++n) {
+    s1[n] += __shfl_xor(s1[n], 16, 64);
+    s1[n] += __shfl_xor(s1[n], 32, 64);
+    s2[n] += __shfl_xor(s2[n], 16, 64);
+    s2[n] += __shfl_xor(s2[n], 32, 64);
+    if (lane < 16) {
+      sP[w * 2 * NGP + n * 16 + lane] = s1[n];
+      sP[w * 2 * NGP + NGP + n * 16 + lane] = s2[n];
+    }
+  }
+  __syncthreads();
+  const int C = g.CO_real;
+  constexpr int WPR = 64 / WR, PRB = GBM / 64;
+  const int nrow = (g.Nout + BM - 1) / BM;
+  for (int j = tid; j < PRB * 2 * C; j += GBLK) {
+    const int h = j / (2 * C), jj = j - h * 2 * C, prow = lb * PRB + h;
+    if (prow >= nrow) continue;
+    int which = jj / C, c = jj - which * C;
+    float s = 0.0f;
+    for (int ww = 0; ww < WPR; ++ww) s += sP[(WPR * h + ww) * 2 * NGP + which * NGP + c];
+    g.part[(long long)prow * 2 * C + jj] = s;
+  }
+  if (g.fin.ticket) {
+    // the ring is free: the totals (double [2C], C <= 256 -> 4 KB) and the arrival flag go there
+    fused_bn_finalize<GBLK>(g, lb, PRB, (double*)(lds + 1024), (int*)(lds + 8192));
   }
 }
 
@@ -640,10 +994,75 @@ static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
   else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(64 * GW), 0, st, a);
 }
 
+template <int KGP, int NT, int GW, int S>
+static void launch_pipe_t(int epi, const GB& a, int n_rows, hipStream_t st) {
+  const int nblk = (n_rows + 16 * GW - 1) / (16 * GW);
+  if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_FWD, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_DGRAD, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_PLAIN, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
+}
+
+// RPC_SPGEMM (A/B): 0 (default) = k_gemm_bf16 (one offset of look-ahead in registers, 4 blocks per CU);
+// 1 = k_gemm_pipe, 8-wave blocks with a 4-stage ring; 2 = 4-wave blocks, 4 stages; 3 = 8-wave blocks,
+// 3 stages (the 128-wide GEMM K always takes 4-wave blocks: 4 stages, 3 at 128 x 128). Measured on the
+// metric's rulebooks (profiles/r04_spgemm_pipe_ab.txt): the ring is 2-2.6x SLOWER (<64,4,0> 87 vs 41 us,
+// <64,4,1> 138 vs 53 us) — one block per CU keeps fewer bytes in flight than four blocks with one offset of
+// register look-ahead each; kept for A/B. 4 + DBG: timing arms of k_gemm_bf16<64, 4, ·>.
+static int g_gemm_mode = -1;
+static int gemm_mode() {
+  if (g_gemm_mode < 0) {
+    const char* e = getenv("RPC_SPGEMM");
+    int m = e ? atoi(e) : 0;
+    g_gemm_mode = (m < 0 || m > 19) ? 0 : m;
+  }
+  return g_gemm_mode;
+}
+
 static int launch(int KGP, int NT, int epi, const GB& a, int n_rows, hipStream_t st) {
-#define C2(kg, nt) if (KGP == kg && NT == nt) { launch_t<kg, nt>(epi, a, n_rows, st); return RPC_OK; }
-  C2(32, 1) C2(32, 2) C2(32, 4) C2(64, 2) C2(64, 4) C2(64, 8) C2(128, 4) C2(32, 8) C2(64, 1) C2(128, 2) C2(128, 8)
+  int mode = gemm_mode();
+#define C2(kg, nt)                                                  \
+  if (KGP == kg && NT == nt) {                                      \
+    if (mode == 0) launch_t<kg, nt>(epi, a, n_rows, st);            \
+    else if (mode == 2) launch_pipe_t<kg, nt, 4, 4>(epi, a, n_rows, st); \
+    else if (mode == 3) launch_pipe_t<kg, nt, 8, 3>(epi, a, n_rows, st); \
+    else launch_pipe_t<kg, nt, 8, 4>(epi, a, n_rows, st);           \
+    return RPC_OK;                                                  \
+  }
+#define C2W(kg, nt, s)                                              \
+  if (KGP == kg && NT == nt) {                                      \
+    if (mode == 0) launch_t<kg, nt>(epi, a, n_rows, st);            \
+    else launch_pipe_t<kg, nt, 4, s>(epi, a, n_rows, st);           \
+    return RPC_OK;                                                  \
+  }
+  // 128-wide GEMM K: 4-wave blocks (a 32 KB weight tile per stage at 128 x 128)
+#define C2H(kg, nt)                                                 \
+  if (KGP == kg && NT == nt) {                                      \
+    if (mode == 0) launch_t<kg, nt>(epi, a, n_rows, st);            \
+    else if (mode == 3) launch_pipe_t<kg, nt, 8, 3>(epi, a, n_rows, st); \
+    else launch_pipe_t<kg, nt, 4, 4>(epi, a, n_rows, st);           \
+    return RPC_OK;                                                  \
+  }
+  // 64-wide GEMM K with two row tiles per wave (rt_of): 4-wave blocks by default (8 x 4 KB of gathered rows
+  // per stage would not fit 4 stages); 128-wide: 4-wave blocks (a 32 KB weight tile per stage at 128 x 128)
+  if (mode >= 4 && KGP == 64 && NT == 4) {   // timing arms of k_gemm_bf16 (DBG = mode - 4)
+    const int nblk = (n_rows + 127) / 128;
+#define DB(d)                                                                                              \
+  if (mode - 4 == d) {                                                                                     \
+    if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<64, 4, E_FWD, d>), dim3(nblk), dim3(512), 0, st, a);   \
+    else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<64, 4, E_DGRAD, d>), dim3(nblk), dim3(512), 0, st, a); \
+    else hipLaunchKernelGGL((k_gemm_bf16<64, 4, E_PLAIN, d>), dim3(nblk), dim3(512), 0, st, a);              \
+    return RPC_OK;                                                                                         \
+  }
+    DB(0) DB(1) DB(2) DB(3) DB(4) DB(5) DB(6) DB(7) DB(8) DB(9) DB(12) DB(13)
+#undef DB
+    return RPC_ERR_ARG;
+  }
+  if (mode >= 4) mode = 0;
+  C2(32, 1) C2(32, 2) C2(32, 4) C2H(64, 2) C2(64, 4) C2(64, 8) C2W(128, 4, 4) C2(32, 8) C2H(64, 1) C2W(128, 2, 4)
+  C2W(128, 8, 3)
+#undef C2H
 #undef C2
+#undef C2W
   return RPC_ERR_UNSUPPORTED;
 }
 
@@ -657,6 +1076,13 @@ static inline int r32(int c) { return (c + 31) / 32 * 32; }
 
 using namespace rpc;
 using namespace rpc::spb;
+
+// A/B and tests: select the sparse bf16 GEMM kernel (see gemm_mode); returns the previous mode
+extern "C" int rpc_spconv_gemm_bf16_mode(int mode) {
+  const int prev = gemm_mode();
+  if (mode >= 0 && mode <= 19) g_gemm_mode = mode;
+  return prev;
+}
 
 extern "C" int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, int relu, void* h, void* stream) {
   if (n < 0 || c < 1) return RPC_ERR_ARG;
@@ -723,15 +1149,13 @@ extern "C" int rpc_spconv_prep_weight_bf16(const float* W, int kvol, int ci, int
 // out[r] = sum_k a[map[r, k']] . B_k  with a: bf16 rows of width round8(kg) (kg = GEMM K),
 // B^T from rpc_spconv_prep_weight_bf16; epi 0 = forward (z + BN partial sums), 1 = dgrad with the
 // previous layer's ReLU mask + BN-backward partial sums (prev_z, prev_bn), 2 = plain store.
-extern "C" int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
-                                      int n_out, const void* bt, int ng, float* out, const float* prev_z,
-                                      const float* prev_bn, float* part, int epi, void* stream) {
+static int gemm_bf16_launch(GB& g, const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
+                            const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn, float* part,
+                            int epi, void* stream) {
   if (n_out < 0 || kvol > MAXK || kg < 1 || ng < 1) return RPC_ERR_ARG;
   // 32-bit buffer offsets (src * CP + c) * 2 into the gathered source table of n_src rows
   if (n_src >= 0 && (long long)n_src * r8(kg) * 2 >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
   if (n_out == 0) return RPC_OK;
-  GB g;
-  memset(&g, 0, sizeof(g));
   g.a = (const u16*)a;
   g.CP = r8(kg);
   g.nbr = map;
@@ -754,6 +1178,43 @@ extern "C" int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const in
   if (rc) return rc;
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+extern "C" int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
+                                      int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                                      const float* prev_bn, float* part, int epi, void* stream) {
+  GB g;
+  memset(&g, 0, sizeof(g));
+  return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
+}
+
+// largest block of the k_gemm_pipe launches (rows): fin_groups of n_out at the smallest block (64 rows)
+extern "C" int rpc_bn_fin_groups(int n_out) { return fin_groups(cdiv(n_out > 0 ? n_out : 1, 64)); }
+extern "C" int rpc_bn_fin_tickets(int n_out) { return 1 + rpc_bn_fin_groups(n_out); }
+
+extern "C" int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
+                                        int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                                        const float* prev_bn, float* part, int epi, const RpcBnFin* fin,
+                                        void* stream) {
+  if (!fin) return rpc_spconv_gemm_bf16_n(a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part,
+                                          epi, stream);
+  if ((epi != 0 && epi != 1) || !part || !fin->ticket || !fin->gpart || !fin->gamma || !fin->bn ||
+      (epi == 0 && (!fin->beta || !fin->running_mean || !fin->running_var)) || (epi == 1 && !fin->fbn) ||
+      fin->mode != epi || ng > 256)
+    return RPC_ERR_ARG;
+  if (n_out <= 0) return RPC_ERR_ARG;   // the finalize divides by the row count
+  if (gemm_mode() >= 4) {   // the timing arms of k_gemm_bf16: no fused finalize
+    int rc = rpc_spconv_gemm_bf16_n(a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi,
+                                    stream);
+    if (rc) return rc;
+    return rpc_bn_finalize(part, cdiv(n_out, BM), ng, n_out, epi, fin->gamma, fin->beta, fin->eps, fin->momentum,
+                           fin->running_mean, fin->running_var, fin->fbn, fin->bn, fin->dgamma, fin->dbeta, nullptr,
+                           stream);
+  }
+  GB g;
+  memset(&g, 0, sizeof(g));
+  g.fin = *fin;
+  return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 
 extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out,

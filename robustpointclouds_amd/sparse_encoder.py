@@ -51,6 +51,12 @@ class _Spec:
 SIDE_STREAMS = os.environ.get("RPC_SPARSE_STREAMS", "1") != "0"
 # the backward as one native call (csrc/sparse_exec.hip rpc_sparse_backward); 0: the per-layer Python loop
 NATIVE_BACKWARD = os.environ.get("RPC_SPARSE_NATIVE", "1") != "0"
+# RPC_SPARSE_FUSED_FIN=1: BatchNorm finalizes fused into the bf16 GEMMs that produce their partial sums
+# (rpc_spconv_gemm_bf16_fin, two-level last-arriving blocks). Off by default: measured SLOWER — every block's
+# agent-scope release before its ticket writes back its XCD L2's dirty lines (the GEMM's freshly stored output
+# rows), k_gemm_bf16<64,4,0> 41 -> 63 us and <64,4,1> 53 -> 92 us against a 6.2 us rpc_bn_finalize launch
+# (profiles/r04_spgemm_fused_fin.txt)
+FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "0") != "0"
 
 
 def _t3(v):
@@ -243,6 +249,28 @@ class SparseEncoder(nn.Module):
             ev = torch.cuda.Event()
             ev.record(torch.cuda.current_stream(coors.device))
             self._coors_ready = (coors.data_ptr(), ev)
+
+    FIN_SLOT = 1024   # ticket counters per fused BatchNorm finalize (rows up to 1023 * 32 * 64)
+
+    def fin_tickets(self, device):
+        """Zeroed ticket counters of the BatchNorm finalizes fused into the bf16 GEMMs (rpc_spconv_gemm_bf16_fin):
+        one slot of FIN_SLOT counters per layer and direction (forward: slot li, backward: len(specs) + li);
+        every launch leaves its counters zero again."""
+        key = str(device)
+        t = self.__dict__.setdefault("_fin_tickets", {}).get(key)
+        if t is None:
+            t = self._fin_tickets[key] = torch.zeros(2 * len(self.specs) * self.FIN_SLOT, dtype=torch.int32,
+                                                     device=device)
+        return t
+
+    def fin_ticket_ptr(self, device, slot, n_rows):
+        """Address of the ticket slot for a fused finalize over n_rows rows, or None (a separate finalize)
+        when the rows need more counters than a slot holds."""
+        lib = _ffi.load()
+        if lib.rpc_bn_fin_tickets(max(int(n_rows), 1)) > self.FIN_SLOT:
+            return None
+        t = self.fin_tickets(device)
+        return t.data_ptr() + 4 * slot * self.FIN_SLOT
 
     def grid(self, lvl, B, device):
         """Dense int32 index grid [B, D, H, W] kept all -1 between uses."""
@@ -521,12 +549,27 @@ class SparseEncoderFn(torch.autograd.Function):
             tm = enc.timer is not None and enc.timer.wants("fwd", sp)
             rec["bf16"] = bf16 and li > 0
             rec["h_in"] = hsrc if rec["bf16"] else None
+            bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
+            fused = False
             if rec["bf16"]:
                 bt, rec["btd"] = wtiles[li]
                 e0 = enc.timer.start() if tm else None
-                _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(hsrc), hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]), sp.K, 0, n_out,
-                                                    _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None, _ffi.ptr(part), 0,
-                                                    st), "rpc_spconv_gemm_bf16")
+                tk = enc.fin_ticket_ptr(dev, li, n_out) if FUSED_FINALIZE and n_out > 0 else None
+                if tk is not None:
+                    # GEMM + this layer's BatchNorm finalize in one launch (last-arriving blocks)
+                    gpart = torch.empty(lib.rpc_bn_fin_groups(n_out) * 2 * sp.co, dtype=torch.float64, device=dev)
+                    fin = _ffi.RpcBnFin(tk, gpart.data_ptr(), 0, gamma.data_ptr(), beta.data_ptr(), float(bnm.eps),
+                                        float(bnm.momentum), bnm.running_mean.data_ptr(), bnm.running_var.data_ptr(),
+                                        None, bn.data_ptr(), None, None)
+                    _ffi.check(lib.rpc_spconv_gemm_bf16_fin(_ffi.ptr(hsrc), hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
+                                                            sp.K, 0, n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None,
+                                                            _ffi.ptr(part), 0, _ffi.C.byref(fin), st),
+                               "rpc_spconv_gemm_bf16_fin")
+                    fused = True
+                else:
+                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(hsrc), hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
+                                                          0, n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None,
+                                                          _ffi.ptr(part), 0, st), "rpc_spconv_gemm_bf16")
             else:
                 e0 = enc.timer.start() if tm else None
                 _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
@@ -536,11 +579,11 @@ class SparseEncoderFn(torch.autograd.Function):
                 kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.ci)}, {_r16(sp.co) // 16}, 0>" if rec["bf16"] else
                       f"rpc::sp::k_gemm<{sp.ci}, {sp.co}, {1 if li else 0}, 0>")
                 enc.timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
-            bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
-            _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
-                                           float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
-                                           _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
-                                           None, st), "rpc_bn_finalize")
+            if not fused:
+                _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
+                                               float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
+                                               _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
+                                               None, st), "rpc_bn_finalize")
             rec.update(z=z, bn=bn, W=W, gamma=gamma, beta=beta)
             L.append(rec)
             if sp.mat:
@@ -570,13 +613,18 @@ class SparseEncoderFn(torch.autograd.Function):
         # forward graph (dense_bev._graph_run) then reads it in place instead of from a copy
         # one buffer per shape: a returning shape (full batches after a partial last one) reuses the
         # storage its graph captured, and a dropped encoder frees them all
+        # (at most the two most recent shapes are kept — e.g. full batches and a partial last one, or the
+        # two engines' dtypes; a captured graph that still holds an evicted buffer keeps it alive itself and
+        # copies from the new one when its shape returns)
         bkey = (B, H, Wd, C * D, dt, enc.dense_nhwc, dev)
         bufs = enc.__dict__.setdefault("_dense_bufs", {})
-        base = bufs.get(bkey)
+        base = bufs.pop(bkey, None)
         if base is None:
-            base = bufs[bkey] = torch.empty((B, H, Wd, C * D) if enc.dense_nhwc else (B, C * D, H, Wd), dtype=dt,
-                                            device=dev)
+            while len(bufs) >= 2:
+                bufs.pop(next(iter(bufs)))
+            base = torch.empty((B, H, Wd, C * D) if enc.dense_nhwc else (B, C * D, H, Wd), dtype=dt, device=dev)
             dense_bev.mark_stable(base)
+        bufs[bkey] = base      # most recently used last
         base.zero_()
         if enc.dense_nhwc:   # channels_last image, logically [B, C*D, H, W]
             dense = base.permute(0, 3, 1, 2)
@@ -800,7 +848,8 @@ def _native_backward(ctx, gdense):
             sp.res, vp(rec["nbr"]), vp(rec.get("nbr_in")), vp(rec["z"]), vp(rec["bn"]), vp(rec.get("out")),
             vp(rec["h_in"]) if bf else None, None if bf else vp(rec["src"]), None if bf else vp(rec["src_bn"]),
             vp(rec["W"]), vp(rec["gamma"]), vp(rec["beta"]), vp(rec.get("btd")) if bf else None,
-            dW.data_ptr(), dg.data_ptr(), db.data_ptr())
+            dW.data_ptr(), dg.data_ptr(), db.data_ptr(),
+            ctx.enc.fin_ticket_ptr(dev, nl + li, rec["n_in"]) if bf and FUSED_FINALIZE else None)
     dfeat = (torch.empty((L[0]["n_in"], L[0]["spec"].ci), dtype=torch.float32, device=dev)
              if ctx.needs_input_grad[0] else None)
     wsb = lib.rpc_sparse_backward_workspace_size(table, nl)

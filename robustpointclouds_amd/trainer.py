@@ -14,6 +14,7 @@ from __future__ import annotations
 import contextlib
 import math
 import os
+import warnings
 
 import torch
 import torch.distributed as dist
@@ -55,7 +56,9 @@ def build_optim_wrapper(model, cfg: dict):
     """mmengine `build_optim_wrapper` for the reference configs' `optim_wrapper` dict
     (…3class.py:130-139): type OptimWrapper | AmpOptimWrapper (dtype 'bfloat16' / 'float16'),
     optimizer AdamW(lr, betas, eps, weight_decay), clip_grad(max_norm, norm_type 2), paramwise_cfg
-    custom_keys lr_mult. On a ROCm device the optimizer is ClipAdamW (clip + AdamW, two launches)."""
+    custom_keys lr_mult. On a ROCm device the optimizer is ClipAdamW (clip + AdamW, two launches).
+    AmpOptimWrapper with dtype 'float16' or None (fp16 + GradScaler in mmengine) is run as bf16 autocast
+    without a scaler, with a warning: the HIP engines have no fp16 path."""
     cfg = dict(cfg)
     kind = cfg.get("type", "OptimWrapper")
     oc = dict(cfg["optimizer"])
@@ -75,7 +78,16 @@ def build_optim_wrapper(model, cfg: dict):
         opt = torch.optim.AdamW(groups, lr=lr, betas=betas, eps=eps, weight_decay=wd)
     amp = None
     if kind == "AmpOptimWrapper":
-        amp = {"bfloat16": torch.bfloat16, "float16": torch.bfloat16, None: torch.bfloat16}[cfg.get("dtype")]
+        dt = cfg.get("dtype")
+        if dt not in ("bfloat16", "float16", None):
+            raise ValueError(f"AmpOptimWrapper dtype {dt!r}: 'bfloat16', 'float16' or None")
+        if dt != "bfloat16":
+            # mmengine: None / 'float16' = fp16 autocast with a GradScaler (the reference's --amp,
+            # trainUpdated.bat:9). The HIP engines have no fp16 path: bf16 autocast (fp32 exponent range,
+            # so no loss scaler) is substituted
+            warnings.warn(f"AmpOptimWrapper dtype {dt!r} (fp16 + GradScaler in mmengine) runs as bfloat16 "
+                          "autocast without a loss scaler on the HIP engines", stacklevel=2)
+        amp = torch.bfloat16
     elif kind != "OptimWrapper":
         raise ValueError(f"optim_wrapper type {kind}")
     return OptimWrapper(opt, clip_grad=clip, amp_dtype=amp)
@@ -173,7 +185,8 @@ class Trainer:
 
     @staticmethod
     def _select_engines(model, bf16):
-        select_engines(model, bf16)
+        # pinned: evaluation (val_step outside autocast) keeps the training precision's engines
+        select_engines(model, bf16, pin=True)
 
     # mmengine-runner-like attributes used by custom_hook.py
     @property

@@ -1,0 +1,195 @@
+"""The LDS-DMA ring sparse GEMM (csrc/spconv_bf16.hip k_gemm_pipe, rpc_spconv_gemm_bf16_mode 1-3) against the
+one-offset-look-ahead kernel it replaces (mode 0): the same MFMAs in the same order per accumulator, so
+outputs and BatchNorm partial rows must be BIT-identical — for every (GEMM K, output width) instantiation,
+the three epilogues, ragged row counts (1, 15, 17, 129 rows: partial waves and blocks), offsets nobody
+uses, blocks whose rows have no neighbour at all, and the real SECOND rulebooks of a synthetic KITTI batch
+(whole bf16 SparseEncoder forward + backward, every layer)."""
+import pytest
+import torch
+
+from robustpointclouds_amd import _ffi
+
+pytestmark = pytest.mark.gpu
+
+# (gemm K = gathered row width, gemm N = output width): every launch shape of rpc_spconv_gemm_bf16
+SHAPES = [(16, 16), (32, 16), (32, 32), (16, 32), (32, 64), (64, 32), (64, 64), (64, 128), (128, 64),
+          (128, 128), (32, 128), (64, 16), (128, 32), (24, 32), (40, 64)]
+
+
+def _r8(c):
+    return (c + 7) // 8 * 8
+
+
+def _run(lib, mode, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev):
+    prev = lib.rpc_spconv_gemm_bf16_mode(mode)
+    try:
+        out = torch.full((n_out, ng), float("nan"), device=dev)
+        nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
+        part = torch.full((nblk, 2 * ng), float("nan"), device=dev) if epi != 2 else None
+        _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, rev, n_out, _ffi.ptr(bt), ng,
+                                              _ffi.ptr(out), _ffi.ptr(ez), _ffi.ptr(ebn), _ffi.ptr(part), epi,
+                                              _ffi.stream_of(out)), "rpc_spconv_gemm_bf16_n")
+        torch.cuda.synchronize()
+        return out, part
+    finally:
+        lib.rpc_spconv_gemm_bf16_mode(prev)
+
+
+@pytest.mark.parametrize("kg,ng", SHAPES)
+@pytest.mark.parametrize("n_out,K,rev", [(5000, 27, 0), (129, 27, 1), (17, 3, 0), (15, 27, 0), (1, 27, 1)])
+def test_pipe_gemm_bit_identical(kg, ng, n_out, K, rev):
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(kg * 131 + ng * 7 + n_out + K)
+    n_src = 3000
+    nbr = torch.randint(0, n_src, (n_out, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n_out, K), generator=g) > 0.35] = -1
+    if K > 2:
+        nbr[:, 1] = -1                      # an offset nobody uses
+    if n_out > 300:
+        nbr[128:256] = -1                   # a whole block of rows with no neighbour
+    a = torch.zeros((n_src, _r8(kg)), dtype=torch.bfloat16)
+    a[:, :kg] = torch.randn((n_src, kg), generator=g).to(torch.bfloat16)
+    W = torch.randn((K, kg, ng), generator=g) * 0.1
+    a, nbr, W = a.to(dev), nbr.to(dev), W.to(dev)
+    bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(K, kg, ng, 0), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), K, kg, ng, 0, _ffi.ptr(bt), _ffi.stream_of(bt)), "prep")
+    ez = torch.randn((n_out, ng), generator=g).to(dev)
+    ebn = torch.cat([torch.rand(ng, generator=g) + 0.5, torch.randn(ng, generator=g) * 0.1,
+                     torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
+    for epi in (0, 1, 2):
+        ref_out, ref_part = _run(lib, 0, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
+        assert torch.isfinite(ref_out).all()
+        for mode in (1, 2, 3):
+            out, part = _run(lib, mode, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
+            assert torch.equal(out, ref_out), (mode, epi)
+            if epi != 2:
+                assert torch.equal(part, ref_part), (mode, epi)
+
+
+def _encoder_case():
+    from robustpointclouds_amd import voxelize
+    from robustpointclouds_amd.sparse_encoder import SparseEncoder
+    from robustpointclouds_amd.synthetic import KITTI_PC_RANGE, KITTI_VOXEL_SIZE, kitti_batch
+    dev = torch.device("cuda")
+    pts, _, _ = kitti_batch(6, seed0=0, num_classes=3)
+    pts = [torch.from_numpy(p).to(dev) for p in pts]
+    d = voxelize.Voxelization(KITTI_VOXEL_SIZE, KITTI_PC_RANGE, 5, 16000).to(dev).voxelize_frames(pts)
+    feats = (d["voxels"][:, :, :4].sum(1) / d["num_points"].clamp(min=1).view(-1, 1).float()).contiguous()
+    torch.manual_seed(0)
+    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    enc.bf16 = enc.dense_nhwc = enc.dense_bf16 = True
+    return enc, feats, d["coors"]
+
+
+def _encoder_step(enc, feats, coors, mode, fused):
+    from robustpointclouds_amd import sparse_encoder as se
+    lib = _ffi.load()
+    prev, prev_f = lib.rpc_spconv_gemm_bf16_mode(mode), se.FUSED_FINALIZE
+    se.FUSED_FINALIZE = fused
+    try:
+        for p in enc.parameters():
+            p.grad = None
+        bns = [m[1] for m in enc.layers()]
+        saved = [(b.running_mean.clone(), b.running_var.clone()) for b in bns]
+        f = feats.clone().requires_grad_(True)
+        out = enc(f, coors, 6)
+        g = torch.Generator(device="cpu").manual_seed(1)
+        out.backward(torch.randn(out.shape, generator=g).to(out.device).to(out.dtype))
+        torch.cuda.synchronize()
+        stats = [torch.cat([b.running_mean, b.running_var]).clone() for b in bns]
+        for b, (m, v) in zip(bns, saved):   # every run starts from the same running statistics
+            b.running_mean.copy_(m)
+            b.running_var.copy_(v)
+        return out.detach().float().clone(), f.grad.clone(), [p.grad.clone() for p in enc.parameters()], stats
+    finally:
+        lib.rpc_spconv_gemm_bf16_mode(prev)
+        se.FUSED_FINALIZE = prev_f
+
+
+def test_pipe_encoder_step_bit_identical():
+    """The bf16 SparseEncoder forward + backward on a synthetic KITTI batch (the metric's shapes) with the
+    ring kernel equals the one with the former kernel, bit for bit (dense BEV, every gradient, running stats),
+    both with the separate BatchNorm finalize launches."""
+    enc, feats, coors = _encoder_case()
+    r0 = _encoder_step(enc, feats, coors, 0, False)
+    r1 = _encoder_step(enc, feats, coors, 1, False)
+    assert torch.equal(r0[0], r1[0])
+    assert torch.equal(r0[1], r1[1])
+    for a, b in zip(r0[2] + r0[3], r1[2] + r1[3]):
+        assert torch.equal(a, b)
+
+
+def test_fused_finalize_matches_separate_and_is_deterministic():
+    """BatchNorm finalizes fused into the GEMMs (two-level last-block sums) against the separate rpc_bn_finalize
+    launches: the same statistics up to summation order (rel 1e-5 on the BEV, gradients and running stats),
+    bit-identical from run to run, and the ticket counters back at zero after every launch."""
+    enc, feats, coors = _encoder_case()
+    ref = _encoder_step(enc, feats, coors, 1, False)
+    a = _encoder_step(enc, feats, coors, 1, True)
+    b = _encoder_step(enc, feats, coors, 1, True)
+    for x, y in zip([a[0], a[1]] + a[2] + a[3], [b[0], b[1]] + b[2] + b[3]):
+        assert torch.equal(x, y)
+    for x, y in zip([ref[0], ref[1]] + ref[2] + ref[3], [a[0], a[1]] + a[2] + a[3]):
+        d = (x.double() - y.double()).norm() / max(y.double().norm().item(), 1e-30)
+        assert d.item() < 1e-5
+    assert int(enc.fin_tickets(feats.device).abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("kg,ng,n_out,epi", [(64, 64, 106000, 0), (32, 64, 5000, 1), (64, 128, 130, 0),
+                                             (128, 128, 64, 1), (16, 32, 1, 0)])
+def test_gemm_fin_entry_point(kg, ng, n_out, epi):
+    """rpc_spconv_gemm_bf16_fin alone: the same output rows as the unfused GEMM, the finalize outputs of
+    rpc_bn_finalize on the same partial rows (mode 0: bn + running stats; mode 1: bnb, dgamma, dbeta) to
+    double-summation-order accuracy, repeated launches reuse the re-armed tickets."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(n_out + kg)
+    K, n_src = 27, max(n_out, 1000)
+    nbr = torch.randint(0, n_src, (n_out, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n_out, K), generator=g) > 0.3] = -1
+    a = torch.zeros((n_src, _r8(kg)), dtype=torch.bfloat16)
+    a[:, :kg] = torch.randn((n_src, kg), generator=g).to(torch.bfloat16)
+    W = torch.randn((K, kg, ng), generator=g) * 0.1
+    a, nbr, W = a.to(dev), nbr.to(dev), W.to(dev)
+    bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(K, kg, ng, 0), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), K, kg, ng, 0, _ffi.ptr(bt), _ffi.stream_of(bt)), "prep")
+    ez = torch.randn((n_out, ng), generator=g).to(dev)
+    ebn = torch.cat([torch.rand(ng, generator=g) + 0.5, torch.randn(ng, generator=g) * 0.1,
+                     torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
+    gamma, beta = (torch.rand(ng, generator=g) + 0.5).to(dev), torch.randn(ng, generator=g).to(dev)
+    ticket = torch.zeros(lib.rpc_bn_fin_tickets(n_out), dtype=torch.int32, device=dev)
+    gpart = torch.empty(lib.rpc_bn_fin_groups(n_out) * 2 * ng, dtype=torch.float64, device=dev)
+    nblk = lib.rpc_spconv_gemm_blocks(n_out)
+    st = _ffi.stream_of(ez)
+    nb = 4 if epi == 0 else 5
+    for rep in range(3):
+        out = torch.full((n_out, ng), float("nan"), device=dev)
+        part = torch.full((nblk, 2 * ng), float("nan"), device=dev)
+        rm0, rv0 = torch.zeros(ng, device=dev), torch.ones(ng, device=dev)
+        rm, rv = rm0.clone(), rv0.clone()
+        bn = torch.full((nb * ng,), float("nan"), device=dev)
+        dg, db = torch.full((ng,), float("nan"), device=dev), torch.full((ng,), float("nan"), device=dev)
+        fin = _ffi.RpcBnFin(ticket.data_ptr(), gpart.data_ptr(), epi, gamma.data_ptr(), beta.data_ptr(), 1e-3, 0.01,
+                            rm.data_ptr(), rv.data_ptr(), ebn.data_ptr() if epi else None, bn.data_ptr(),
+                            dg.data_ptr() if epi else None, db.data_ptr() if epi else None)
+        _ffi.check(lib.rpc_spconv_gemm_bf16_fin(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, n_out, _ffi.ptr(bt), ng,
+                                                _ffi.ptr(out), _ffi.ptr(ez) if epi else None,
+                                                _ffi.ptr(ebn) if epi else None, _ffi.ptr(part), epi,
+                                                _ffi.C.byref(fin), st), "rpc_spconv_gemm_bf16_fin")
+        ref_out, ref_part = _run(lib, 1, a, n_src, kg, nbr, K, 0, n_out, bt, ng, epi, ez, ebn, dev)
+        assert torch.equal(out, ref_out)
+        assert torch.equal(part, ref_part)
+        rrm, rrv = rm0.clone(), rv0.clone()
+        rbn = torch.full((nb * ng,), float("nan"), device=dev)
+        rdg, rdb = torch.full((ng,), float("nan"), device=dev), torch.full((ng,), float("nan"), device=dev)
+        _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, ng, n_out, epi, _ffi.ptr(gamma), _ffi.ptr(beta), 1e-3,
+                                       0.01, _ffi.ptr(rrm), _ffi.ptr(rrv), _ffi.ptr(ebn) if epi else None,
+                                       _ffi.ptr(rbn), _ffi.ptr(rdg) if epi else None, _ffi.ptr(rdb) if epi else None,
+                                       None, st), "rpc_bn_finalize")
+        torch.cuda.synchronize()
+        pairs = [(bn, rbn)] + ([(rm, rrm), (rv, rrv)] if epi == 0 else [(dg, rdg), (db, rdb)])
+        for x, y in pairs:
+            assert torch.isfinite(x).all()
+            assert torch.allclose(x, y, rtol=1e-6, atol=1e-6 * max(y.abs().max().item(), 1.0))
+        assert int(ticket.abs().sum().item()) == 0

@@ -210,6 +210,10 @@ int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const f
  * for rpc_bn_finalize mode 1. c <= 256. */
 int rpc_sparse_res_forward(const float* z, const float* bn, const float* res, int n, int c, float* out,
                            void* out_bf16, void* stream);
+/* the same with the 16-bit rows in format fmt (RPC_H16_BF16 / RPC_H16_F16), and with fmt RPC_H16_F16 optionally a
+ * bf16 copy (out_bf16) */
+int rpc_sparse_res_forward_h16(const float* z, const float* bn, const float* res, int n, int c, float* out,
+                               void* out_h16, int fmt, void* out_bf16, void* stream);
 int rpc_sparse_res_backward(const float* g1, const float* g2, const float* out, const float* z, const float* bn,
                             int n, int c, float* m, float* part, void* stream);
 /* SparseConvTensor.dense() of relu(bn(z)) viewed as [B, C*D, H, W] (channel c*D + z); backward
@@ -223,9 +227,18 @@ int rpc_sparse_to_dense(const float* z, const float* bn, const int* coors, int n
 int rpc_dense_to_sparse_grad(const void* grad_dense, const float* z, const float* bn, const int* coors,
                              int n, int c, const int* shape, int flags, float* dy, float* part, void* stream);
 
-/* ---- a6 perf mode (bf16 MFMA, fp32 accumulate and BatchNorm statistics) */
+/* ---- a6 perf mode (16-bit MFMA operands, fp32 accumulate and BatchNorm statistics). Forward GEMM operands
+ * (the gathered rows relu(bn(z)) and the forward weight tiles) may be fp16 (RPC_H16_F16: 3 more mantissa bits
+ * than bf16 at the same MFMA rate; the perf mode's default — see SparseEncoder.h16_fwd); the backward's dz rows
+ * and data-gradient tiles are bf16. */
+#define RPC_H16_BF16 0
+#define RPC_H16_F16 1
 /* h[r, c] = bf16(relu?(z*scale+shift)) (bn NULL: identity), rows padded to round8(c) */
 int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, int relu, void* h, void* stream);
+/* the same rows in format fmt; with fmt RPC_H16_F16, h_bf16 (optional) receives the same rows in bf16 too (the
+ * weight gradient's operand) */
+int rpc_to_h16_rows(const float* z, const float* bn, int n, int c, int relu, int fmt, void* h, void* h_bf16,
+                    void* stream);
 /* dz[r, c] = bf16(gi*(dy - m1 - xhat*m2)) with bnb = gi, m1, m2, mean, invstd (rpc_bn_finalize mode 1) */
 int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const float* bnb, int n, int c, void* dz, void* stream);
 /* W [K][ci][co] fp32 -> per-offset B^T tiles bf16 (forward: [K][co][ci]; dgrad: [K][ci][co]), zero padded */
@@ -236,6 +249,7 @@ typedef struct {
   const float* W;
   void* bt;
   int kvol, ci, co, dgrad;
+  int fmt;               /* tile format: RPC_H16_BF16, or RPC_H16_F16 (forward tiles, dgrad 0) */
 } RpcSpconvWprep;
 int rpc_spconv_prep_weight_bf16_batch(const RpcSpconvWprep* descs, int n, void* stream);
 /* out[r] = sum_k a[map[r, k']] . B_k ; epi 0 forward (+BN partial sums), 1 dgrad (prev ReLU mask +
@@ -251,6 +265,11 @@ int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int re
 int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
                            const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
                            float* part, int epi, void* stream);
+/* the same with the operand format of a and bt: RPC_H16_BF16, or RPC_H16_F16 for the forward (epi 0) only
+ * (RPC_ERR_UNSUPPORTED otherwise) */
+int rpc_spconv_gemm_h16(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
+                        const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn, float* part,
+                        int epi, void* stream);
 /* the same GEMM with the BatchNorm finalize of its partial sums fused in (the last
  * arriving blocks sum the partial rows in two fixed-order levels and apply rpc_bn_finalize's arithmetic),
  * replacing the rpc_bn_finalize launch that followed it: epi 0 -> mode 0 (this layer's bn + running stats),
@@ -286,6 +305,9 @@ int rpc_spconv_gemm_bf16_mode(int mode);
 size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co);
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
                           float* dW, void* workspace, size_t workspace_bytes, void* stream);
+/* the same with h in format hfmt (fp16 forward rows are rounded to bf16 as they are staged) */
+int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out, const void* dz,
+                         int co, float* dW, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- a6 runtime: the whole SparseEncoder backward in one call (csrc/sparse_exec.hip).
  * Replaces the per-layer backward of upstream mmdet3d SparseEncoder (adversarial_voxelnet.py:141;
@@ -316,6 +338,7 @@ typedef struct {
   float* dW;
   float* dgamma;
   float* dbeta;
+  int h_fmt;             /* bf16 layers: format of h_in (RPC_H16_BF16 / RPC_H16_F16) */
   unsigned* fin_ticket;  /* bf16 layers: rpc_bn_fin_tickets(n_in) zeroed counters — the data gradient into the
                             layer below then finalizes that layer's BatchNorm backward in its own launch
                             (rpc_spconv_gemm_bf16_fin); NULL: a separate rpc_bn_finalize */

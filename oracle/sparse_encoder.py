@@ -75,13 +75,54 @@ def spconv_pairs(coors, out_shape, ksize, stride, pad):
     return out_coors.astype(np.int64), pairs
 
 
-class OracleSparseEncoder:
-    """SECOND SparseEncoder with explicit float64 weights copied from a GPU module."""
+def _bf16(t):
+    return t.to(torch.bfloat16).to(t.dtype)
 
-    def __init__(self, enc, dtype=torch.float64):
+
+def _fp16(t):
+    return t.to(torch.float16).to(t.dtype)
+
+
+class _RoundFwd(torch.autograd.Function):
+    """bf16 (or fp16) rounding of a GEMM operand in the forward; the gradient passes through unrounded."""
+
+    @staticmethod
+    def forward(ctx, x, fp16=False):
+        return _fp16(x) if fp16 else _bf16(x)
+
+    @staticmethod
+    def backward(ctx, g):
+        return g, None
+
+
+class _RoundBwd(torch.autograd.Function):
+    """Identity in the forward; the gradient arriving at a conv output (the BatchNorm-backward dz that the
+    perf mode stores as bf16 rows before its data- and weight-gradient GEMMs) rounded to bf16."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return _bf16(g)
+
+
+class OracleSparseEncoder:
+    """SECOND SparseEncoder with explicit float64 weights copied from a GPU module.
+
+    bf16_from (optional layer index): emulate the perf mode's 16-bit GEMM operands from that layer on — the
+    gathered input rows relu(bn(z)) and the weights rounded to bf16 (fwd_fp16: to fp16) in the forward, the
+    BatchNorm-backward dz rounded to bf16 before the data / weight gradients — with every other operation in
+    `dtype`: the error an implementation with those operands cannot avoid (the bar of
+    tests/test_gpu_sparse_layers.py)."""
+
+    def __init__(self, enc, dtype=torch.float64, bf16_from=None, fwd_fp16=False):
         self.specs = enc.specs
         self.shapes = enc.shapes
         self.dtype = dtype
+        self.bf16_from = bf16_from
+        self.fwd_fp16 = fwd_fp16
         self.params = []
         for m in enc.layers():
             W = m[0].weight.detach().cpu().to(dtype).clone().requires_grad_(True)
@@ -97,7 +138,7 @@ class OracleSparseEncoder:
         cache = {}
         self.trace = []   # keep=True: per layer (coors, z pre-BN, pre-activation) for debugging
         outs = []         # per layer output features (SparseBasicBlock identities)
-        for sp, p in zip(self.specs, self.params):
+        for li, (sp, p) in enumerate(zip(self.specs, self.params)):
             if sp.kind == "subm":
                 if sp.key not in cache:
                     cache[sp.key] = subm_pairs(c, (B,) + self.shapes[sp.lvl_in], sp.ksize)
@@ -105,10 +146,14 @@ class OracleSparseEncoder:
             else:
                 c_out, pairs = spconv_pairs(c, (B,) + self.shapes[sp.lvl_out], sp.ksize, sp.stride, sp.pad)
                 n_out = c_out.shape[0]
+            q = self.bf16_from is not None and li >= self.bf16_from
+            xg, Wg = (_RoundFwd.apply(x, self.fwd_fp16), _RoundFwd.apply(p["W"], self.fwd_fp16)) if q else (x, p["W"])
             z = torch.zeros((n_out, sp.co), dtype=self.dtype)
             for k, (ri, ro) in enumerate(pairs):
                 if len(ri):
-                    z = z.index_add(0, torch.from_numpy(ro), x[torch.from_numpy(ri)] @ p["W"][k])
+                    z = z.index_add(0, torch.from_numpy(ro), xg[torch.from_numpy(ri)] @ Wg[k])
+            if q:
+                z = _RoundBwd.apply(z)
             mean = z.mean(0)
             var = z.var(0, unbiased=False)
             with torch.no_grad():

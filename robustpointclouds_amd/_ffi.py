@@ -81,7 +81,7 @@ class RpcDenseWprep(C.Structure):
 class RpcSpconvWprep(C.Structure):
     """include/rpc_hip.h RpcSpconvWprep."""
     _fields_ = [("W", C.c_void_p), ("bt", C.c_void_p), ("kvol", C.c_int), ("ci", C.c_int), ("co", C.c_int),
-                ("dgrad", C.c_int)]
+                ("dgrad", C.c_int), ("fmt", C.c_int)]
 
 
 class RpcSparseLayer(C.Structure):
@@ -91,7 +91,8 @@ class RpcSparseLayer(C.Structure):
                 ("nbr", C.c_void_p), ("nbr_in", C.c_void_p), ("z", C.c_void_p), ("bn", C.c_void_p),
                 ("out", C.c_void_p), ("h_in", C.c_void_p), ("src", C.c_void_p), ("src_bn", C.c_void_p),
                 ("W", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("btd", C.c_void_p),
-                ("dW", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("fin_ticket", C.c_void_p)]
+                ("dW", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("h_fmt", C.c_int),
+                ("fin_ticket", C.c_void_p)]
 
 
 class RpcBnFin(C.Structure):
@@ -150,6 +151,10 @@ SIGNATURES = {
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_gemm_bf16_n": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_gemm_bf16_mode": (i32, [i32]),
+    "rpc_spconv_gemm_h16": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
+    "rpc_to_h16_rows": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp]),
+    "rpc_spconv_wgrad_h16": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
+    "rpc_sparse_res_forward_h16": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
     "rpc_bn_fin_groups": (i32, [i32]),
     "rpc_bn_fin_tickets": (i32, [i32]),
     "rpc_spconv_gemm_bf16_fin": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,

@@ -127,7 +127,7 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
                               : rpc_spconv_wgrad_workspace_size(n_out, l.kvol, l.ci, l.co);
     void* wsw = A.take(wsz);
     if (l.bf16)
-      CHK(rpc_spconv_wgrad_bf16(l.h_in, l.ci, l.nbr, l.kvol, n_out, dzb, l.co, l.dW, wsw, wsz, sw));
+      CHK(rpc_spconv_wgrad_h16(l.h_in, l.h_fmt, l.ci, l.nbr, l.kvol, n_out, dzb, l.co, l.dW, wsw, wsz, sw));
     else
       CHK(rpc_spconv_wgrad(l.src, l.src_bn, l.ci, l.nbr, l.kvol, n_out, dy, l.z, bnb, l.co, l.dW, wsw, wsz, sw));
     // data gradient into the layer below (its ReLU mask + BatchNorm-backward partial sums)

@@ -717,9 +717,11 @@ __global__ __launch_bounds__(FBLK) void k_from_dense(const T* __restrict__ gd, c
 // forward: out = relu(bn(z) + res) (res optional), fp32 rows and optionally bf16 rows [n][round8(C)]
 // (upstream mmdet3d SparseBasicBlock.forward: norm2, + identity, relu; also materialises a plain
 // relu(bn(z)) output that a block reads as its identity)
+template <int FMT>   // hb: bf16 (0) or fp16 (1) rows
 __global__ __launch_bounds__(BLK) void k_res_fwd(const float* __restrict__ z, const float* __restrict__ bn,
                                                  const float* __restrict__ res, int N, int C, int CP,
-                                                 float* __restrict__ out, unsigned short* __restrict__ hb) {
+                                                 float* __restrict__ out, unsigned short* __restrict__ hb,
+                                                 unsigned short* __restrict__ hb2) {
   const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
   if (t >= (long long)N * CP) return;
   const int r = (int)(t / CP), c = (int)(t - (long long)r * CP);
@@ -732,8 +734,17 @@ __global__ __launch_bounds__(BLK) void k_res_fwd(const float* __restrict__ z, co
     out[i] = v;
   }
   if (hb) {
-    __bf16 b = (__bf16)v;
-    hb[t] = __builtin_bit_cast(unsigned short, b);
+    if (FMT) {
+      _Float16 h = (_Float16)v;
+      hb[t] = __builtin_bit_cast(unsigned short, h);
+      if (hb2) {
+        __bf16 b = (__bf16)v;
+        hb2[t] = __builtin_bit_cast(unsigned short, b);
+      }
+    } else {
+      __bf16 b = (__bf16)v;
+      hb[t] = __builtin_bit_cast(unsigned short, b);
+    }
   }
 }
 
@@ -1216,15 +1227,24 @@ extern "C" int rpc_dense_to_sparse_grad(const void* grad_dense, const float* z, 
   return RPC_OK;
 }
 
-extern "C" int rpc_sparse_res_forward(const float* z, const float* bn, const float* res, int n, int c, float* out,
-                                      void* out_bf16, void* stream) {
-  if (n < 0 || c < 1 || !z || !bn || !out) return RPC_ERR_ARG;
+extern "C" int rpc_sparse_res_forward_h16(const float* z, const float* bn, const float* res, int n, int c, float* out,
+                                          void* out_h16, int fmt, void* out_bf16, void* stream) {
+  if (n < 0 || c < 1 || !z || !bn || !out || (fmt != 0 && fmt != 1) || (out_bf16 && !fmt)) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   const int cp = (c + 7) / 8 * 8;
-  hipLaunchKernelGGL(k_res_fwd, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, res, n,
-                     c, cp, out, (unsigned short*)out_bf16);
+  if (fmt)
+    hipLaunchKernelGGL(k_res_fwd<1>, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, res,
+                       n, c, cp, out, (unsigned short*)out_h16, (unsigned short*)out_bf16);
+  else
+    hipLaunchKernelGGL(k_res_fwd<0>, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, res,
+                       n, c, cp, out, (unsigned short*)out_h16, (unsigned short*)nullptr);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+extern "C" int rpc_sparse_res_forward(const float* z, const float* bn, const float* res, int n, int c, float* out,
+                                      void* out_bf16, void* stream) {
+  return rpc_sparse_res_forward_h16(z, bn, res, n, c, out, out_bf16, 0, nullptr, stream);
 }
 
 extern "C" int rpc_sparse_res_backward(const float* g1, const float* g2, const float* out, const float* z,

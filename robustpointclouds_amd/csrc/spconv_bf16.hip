@@ -53,6 +53,27 @@ __device__ __forceinline__ u16 to_bf16(float f) {
   __bf16 b = (__bf16)f;   // round-to-nearest-even, NaN kept (v_cvt_pk_bf16_f32)
   return __builtin_bit_cast(u16, b);
 }
+__device__ __forceinline__ u16 to_f16(float f) {
+  _Float16 h = (_Float16)f;   // round-to-nearest-even (v_cvt_f16_f32)
+  return __builtin_bit_cast(u16, h);
+}
+// 16-bit GEMM operand format: 0 = bf16, 1 = fp16 (RPC_H16_*). fp16 (3 more mantissa bits, same MFMA rate) is
+// used for the FORWARD operands of the perf mode — the normalised activations relu(bn(z)) and the weights,
+// both far inside its range — where the operand rounding decides the ReLU masks every later gradient goes
+// through (oracle/sparse_encoder.py bf16_from emulation: perturber-gradient error 0.237 with bf16 forward
+// operands, 0.077 with fp16, the backward's bf16 dz rows alike); the backward's dz rows stay bf16 (no range
+// to manage: no loss scaling).
+template <int FMT>
+__device__ __forceinline__ u16 to_h16(float f) { return FMT ? to_f16(f) : to_bf16(f); }
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+template <bool F16>
+__device__ __forceinline__ f32x4 mfma16(uint4 a, uint4 b, f32x4 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                   0);
+}
 
 enum { E_FWD = 0, E_DGRAD = 1, E_PLAIN = 2 };
 
@@ -68,7 +89,8 @@ struct GB {
   const float* ez;    // E_DGRAD: z of the layer whose grad this is [Nout][CO_real]
   const float* ebn;   // E_DGRAD: scale, beta, mean, invstd [4*CO_real]
   float* part;        // [blocks][2*NGP] or null
-  RpcBnFin fin;       // k_gemm_pipe: BatchNorm finalize by the last-arriving blocks (fin.ticket null: off)
+  RpcBnFin fin;       // BatchNorm finalize by the last-arriving blocks (fin.ticket null: off)
+  int fmt;            // operand format of a and bt: 0 bf16, 1 fp16 (E_FWD only)
 };
 
 // ---- BatchNorm finalize fused into the GEMM (k_gemm_pipe, RpcBnFin): the partial rows every block writes
@@ -151,7 +173,7 @@ __device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int*
 // DBG (timing attribution only, rpc_spconv_gemm_bf16_mode 4 + DBG for the 64 x 64 tiles; results are
 // garbage): bit 0 = no MFMAs, bit 1 = every gather offset out of range (no memory traffic, same
 // instructions), bit 2 = the same for the weight tiles, bit 3 = no gather instructions at all
-template <int KGP, int NT, int EPI, int DBG = 0>
+template <int KGP, int NT, int EPI, int DBG = 0, bool F16 = false>
 __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) void k_gemm_bf16(GB g) {
   constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, RT = rt_of(KGP, NT), WR = 16 * RT, GBM = WR * GW;
   constexpr int KS = KGP / 32;
@@ -293,11 +315,9 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
         for (int ks = 0; ks < KS; ++ks) {
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
-            bf16x8 bv = *(const bf16x8*)(bb + n * 16 * LS + ks * 32);
+            const uint4 bv = *(const uint4*)(bb + n * 16 * LS + ks * 32);
 #pragma unroll
-            for (int rt = 0; rt < RT; ++rt)
-              acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ac[rt][ks]), bv,
-                                                                   acc[rt][n], 0, 0, 0);
+            for (int rt = 0; rt < RT; ++rt) acc[rt][n] = mfma16<F16>(ac[rt][ks], bv, acc[rt][n]);
           }
         }
       }
@@ -657,8 +677,9 @@ __global__ __launch_bounds__(64 * GW, 1) void k_gemm_pipe(GB g) {
 }
 
 // ------------------------------------------------------------------ elementwise producers
+template <int FMT>
 __global__ __launch_bounds__(BLK) void k_to_bf16(const float* __restrict__ z, const float* __restrict__ bn, int N,
-                                                 int C, int CP, int relu, u16* __restrict__ h) {
+                                                 int C, int CP, int relu, u16* __restrict__ h, u16* __restrict__ h2) {
   long long t = (long long)blockIdx.x * BLK + threadIdx.x;
   if (t >= (long long)N * CP) return;
   int r = (int)(t / CP), c = (int)(t - (long long)r * CP);
@@ -668,7 +689,8 @@ __global__ __launch_bounds__(BLK) void k_to_bf16(const float* __restrict__ z, co
     if (bn) v = fmaf(v - bn[2 * C + c], bn[c], bn[C + c]);   // (z - mean) * scale + beta
     if (relu) v = fmaxf(v, 0.0f);
   }
-  h[t] = to_bf16(v);
+  h[t] = to_h16<FMT>(v);
+  if (FMT && h2) h2[t] = to_bf16(v);
 }
 
 __global__ __launch_bounds__(BLK) void k_dz_bf16(const float* __restrict__ dy, const float* __restrict__ z,
@@ -694,10 +716,11 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
   const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
   v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
 }
+template <int FMT = 0>
 __device__ __forceinline__ void st8h(u16* p, const float (&v)[8]) {
   u16 o[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) o[j] = to_bf16(v[j]);
+  for (int j = 0; j < 8; ++j) o[j] = to_h16<FMT>(v[j]);
   *(uint4*)p = *(const uint4*)o;
 }
 
@@ -712,8 +735,9 @@ __host__ __device__ inline int rowpass_blocks(long long n, int c) {
   return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
 }
 
+template <int FMT>
 __global__ __launch_bounds__(BLK) void k_to_bf16_v8(const float* __restrict__ z, const float* __restrict__ bn, int N,
-                                                    int C, int relu, u16* __restrict__ h) {
+                                                    int C, int relu, u16* __restrict__ h, u16* __restrict__ h2) {
   const int C8 = C >> 3, RL = BLK / C8;
   const int cg = threadIdx.x % C8, rl = threadIdx.x / C8, c = cg * 8;
   if (rl >= RL) return;
@@ -740,7 +764,8 @@ __global__ __launch_bounds__(BLK) void k_to_bf16_v8(const float* __restrict__ z,
 #pragma unroll
         for (int j = 0; j < 8; ++j) v[u][j] = fmaxf(v[u][j], 0.0f);
       }
-      st8h(h + (size_t)r * C + c, v[u]);
+      st8h<FMT>(h + (size_t)r * C + c, v[u]);
+      if (FMT && h2) st8h<0>(h2 + (size_t)r * C + c, v[u]);   // + the bf16 rows the weight gradient gathers
     }
   }
 }
@@ -783,14 +808,14 @@ __global__ __launch_bounds__(BLK) void k_dz_bf16_v8(const float* __restrict__ dy
 
 // W fp32 [K][CI][CO] -> B^T bf16 [K][NGP][KGP]; fwd: n = co, kk = ci ; dgrad: n = ci, kk = co
 __device__ __forceinline__ void wprep_elem(long long t, const float* __restrict__ W, int CI, int CO, int dgrad,
-                                           int NGP, int KGP, u16* __restrict__ bt) {
+                                           int NGP, int KGP, u16* __restrict__ bt, int fmt = 0) {
   int kk = (int)(t % KGP);
   long long q = t / KGP;
   int n = (int)(q % NGP), k = (int)(q / NGP);
   float v = 0.0f;
   if (!dgrad) { if (n < CO && kk < CI) v = W[((long long)k * CI + kk) * CO + n]; }
   else { if (n < CI && kk < CO) v = W[((long long)k * CI + n) * CO + kk]; }
-  bt[t] = to_bf16(v);
+  bt[t] = fmt ? to_f16(v) : to_bf16(v);
 }
 
 __global__ __launch_bounds__(BLK) void k_wprep(const float* __restrict__ W, int K, int CI, int CO, int dgrad,
@@ -809,7 +834,7 @@ __global__ __launch_bounds__(BLK) void k_wprep_batch(SWprepBatch b) {
   const int ng = d.dgrad ? d.ci : d.co, kg = d.dgrad ? d.co : d.ci;
   const int NGP = (ng + 15) / 16 * 16, KGP = (kg + 31) / 32 * 32;
   const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (t < (long long)d.kvol * NGP * KGP) wprep_elem(t, d.W, d.ci, d.co, d.dgrad, NGP, KGP, (u16*)d.bt);
+  if (t < (long long)d.kvol * NGP * KGP) wprep_elem(t, d.W, d.ci, d.co, d.dgrad, NGP, KGP, (u16*)d.bt, d.fmt);
 }
 
 // ------------------------------------------------------------------ weight gradient
@@ -828,7 +853,16 @@ __device__ __forceinline__ s16x4 tr_read(const u16* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(p));
 }
 
-template <int CI, int CO, int KG>
+// 8 fp16 -> 8 bf16 (the fp16 forward rows of the perf mode, gathered by the bf16 weight gradient)
+__device__ __forceinline__ uint4 f16x8_to_bf16x8(uint4 v) {
+  const f16x8 h = __builtin_bit_cast(f16x8, v);
+  u16 o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = to_bf16((float)h[j]);
+  return *(const uint4*)o;
+}
+
+template <int CI, int CO, int KG, bool HF16 = false>
 __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
                                                     int K, int N, int rows_per, const u16* __restrict__ dz, int DP,
                                                     float* __restrict__ part) {
@@ -929,7 +963,7 @@ __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf1
           int q = tid + j * BLK;
           if (q < RT * CA) {
             int r = q / CA, c8 = q - r * CA;
-            *(uint4*)&sA[g][r * PA + c8 * 8] = ra[g][j];
+            *(uint4*)&sA[g][r * PA + c8 * 8] = HF16 ? f16x8_to_bf16x8(ra[g][j]) : ra[g][j];
           }
         }
       // which offsets have any neighbour in this sub-tile (wave-uniform, from the LDS indices)
@@ -989,7 +1023,9 @@ template <int KGP, int NT>
 static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
   constexpr int GW = gw_of(KGP, NT), GBM = 16 * rt_of(KGP, NT) * GW;
   const int nblk = (n_rows + GBM - 1) / GBM;
-  if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  if (a.fmt == 1)   // fp16 operands: forward GEMMs only (checked by gemm_bf16_launch)
+    hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, 0, true>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(64 * GW), 0, st, a);
 }
@@ -1057,7 +1093,7 @@ static int launch(int KGP, int NT, int epi, const GB& a, int n_rows, hipStream_t
 #undef DB
     return RPC_ERR_ARG;
   }
-  if (mode >= 4) mode = 0;
+  if (mode >= 4 || a.fmt) mode = 0;   // (the ring variants are bf16 only)
   C2(32, 1) C2(32, 2) C2(32, 4) C2H(64, 2) C2(64, 4) C2(64, 8) C2W(128, 4, 4) C2(32, 8) C2H(64, 1) C2W(128, 2, 4)
   C2W(128, 8, 3)
 #undef C2H
@@ -1084,18 +1120,28 @@ extern "C" int rpc_spconv_gemm_bf16_mode(int mode) {
   return prev;
 }
 
-extern "C" int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, int relu, void* h, void* stream) {
-  if (n < 0 || c < 1) return RPC_ERR_ARG;
+extern "C" int rpc_to_h16_rows(const float* z, const float* bn, int n, int c, int relu, int fmt, void* h,
+                               void* h_bf16, void* stream) {
+  if (n < 0 || c < 1 || (fmt != 0 && fmt != 1) || (h_bf16 && !fmt)) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   int cp = r8(c);
-  if (c % 8 == 0 && BLK % (c / 8) == 0 && (long long)n * c < (1LL << 31))
-    hipLaunchKernelGGL(k_to_bf16_v8, dim3(rowpass_blocks(n, c)), dim3(BLK), 0, (hipStream_t)stream, z, bn, n, c, relu,
-                       (u16*)h);
-  else
-    hipLaunchKernelGGL(k_to_bf16, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, n, c,
-                       cp, relu, (u16*)h);
+  hipStream_t st = (hipStream_t)stream;
+  u16 *o = (u16*)h, *o2 = (u16*)h_bf16;
+  if (c % 8 == 0 && BLK % (c / 8) == 0 && (long long)n * c < (1LL << 31)) {
+    if (fmt) hipLaunchKernelGGL(k_to_bf16_v8<1>, dim3(rowpass_blocks(n, c)), dim3(BLK), 0, st, z, bn, n, c, relu, o, o2);
+    else hipLaunchKernelGGL(k_to_bf16_v8<0>, dim3(rowpass_blocks(n, c)), dim3(BLK), 0, st, z, bn, n, c, relu, o, o2);
+  } else {
+    if (fmt)
+      hipLaunchKernelGGL(k_to_bf16<1>, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, st, z, bn, n, c, cp, relu, o, o2);
+    else
+      hipLaunchKernelGGL(k_to_bf16<0>, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, st, z, bn, n, c, cp, relu, o, o2);
+  }
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+extern "C" int rpc_to_bf16_rows(const float* z, const float* bn, int n, int c, int relu, void* h, void* stream) {
+  return rpc_to_h16_rows(z, bn, n, c, relu, 0, h, nullptr, stream);
 }
 
 extern "C" int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const float* bnb, int n, int c, void* dz,
@@ -1156,6 +1202,7 @@ static int gemm_bf16_launch(GB& g, const void* a, int n_src, int kg, const int* 
   // 32-bit buffer offsets (src * CP + c) * 2 into the gathered source table of n_src rows
   if (n_src >= 0 && (long long)n_src * r8(kg) * 2 >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
   if (n_out == 0) return RPC_OK;
+  if (g.fmt != 0 && (g.fmt != 1 || epi != E_FWD)) return RPC_ERR_UNSUPPORTED;
   g.a = (const u16*)a;
   g.CP = r8(kg);
   g.nbr = map;
@@ -1185,6 +1232,16 @@ extern "C" int rpc_spconv_gemm_bf16_n(const void* a, int n_src, int kg, const in
                                       const float* prev_bn, float* part, int epi, void* stream) {
   GB g;
   memset(&g, 0, sizeof(g));
+  return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
+}
+
+// the forward GEMM on 16-bit operands of either format (fmt RPC_H16_BF16 / RPC_H16_F16); other epilogues bf16
+extern "C" int rpc_spconv_gemm_h16(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
+                                   int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                                   const float* prev_bn, float* part, int epi, void* stream) {
+  GB g;
+  memset(&g, 0, sizeof(g));
+  g.fmt = fmt;
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 
@@ -1291,9 +1348,18 @@ extern "C" size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int 
   return (size_t)wgrad_chunks(n_out, kvol, ci, co) * kvol * ci * co * sizeof(float);
 }
 
-// dW[k] = sum_r h[nbr[r,k]]^T dz[r] with bf16 rows h [.][round8(ci)] and dz [n_out][round8(co)]
+// dW[k] = sum_r h[nbr[r,k]]^T dz[r] with 16-bit rows h [.][round8(ci)] (hfmt: bf16, or fp16 forward rows,
+// rounded to bf16 as they are staged) and bf16 dz [n_out][round8(co)]
+extern "C" int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out,
+                                    const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream);
 extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz,
                                      int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
+  return rpc_spconv_wgrad_h16(h, 0, ci, nbr, kvol, n_out, dz, co, dW, ws, ws_bytes, stream);
+}
+
+extern "C" int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out,
+                                    const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
+  if (hfmt != 0 && hfmt != 1) return RPC_ERR_ARG;
   if (n_out < 0 || kvol < 1 || kvol > MAXK) return RPC_ERR_ARG;
   bool ok = (ci == 16 && (co == 16 || co == 32)) || (ci == 32 && (co == 32 || co == 64)) ||
             (ci == 64 && (co == 64 || co == 128)) || (ci == 128 && co == 128);
@@ -1315,16 +1381,17 @@ extern "C" int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int 
   const u16* hp = (const u16*)h;
   const u16* dp = (const u16*)dz;
   int HP = r8(ci), DP = r8(co);
-#define W2(a, b)                                                                                       \
+#define W2(a, b, kg)                                                                                   \
   if (ci == a && co == b) {                                                                           \
-    hipLaunchKernelGGL((k_wgrad_bf16<a, b, 3>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp, \
-                       DP, part);                                                                     \
+    if (hfmt)                                                                                         \
+      hipLaunchKernelGGL((k_wgrad_bf16<a, b, kg, true>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, \
+                         dp, DP, part);                                                               \
+    else                                                                                              \
+      hipLaunchKernelGGL((k_wgrad_bf16<a, b, kg>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp, \
+                         DP, part);                                                                   \
   } else
-  W2(16, 16) W2(16, 32) W2(32, 32) W2(32, 64) W2(64, 64) W2(64, 128)
-  if (ci == 128 && co == 128) {
-    hipLaunchKernelGGL((k_wgrad_bf16<128, 128, 1>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp,
-                       DP, part);
-  } else { return RPC_ERR_UNSUPPORTED; }
+  W2(16, 16, 3) W2(16, 32, 3) W2(32, 32, 3) W2(32, 64, 3) W2(64, 64, 3) W2(64, 128, 3) W2(128, 128, 1)
+  { return RPC_ERR_UNSUPPORTED; }
 #undef W2
   RPC_LAUNCH_CHECK();
   long long total = (long long)kvol * ci * co;

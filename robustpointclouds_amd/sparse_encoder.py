@@ -57,6 +57,13 @@ NATIVE_BACKWARD = os.environ.get("RPC_SPARSE_NATIVE", "1") != "0"
 # rows), k_gemm_bf16<64,4,0> 41 -> 63 us and <64,4,1> 53 -> 92 us against a 6.2 us rpc_bn_finalize launch
 # (profiles/r04_spgemm_fused_fin.txt)
 FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "0") != "0"
+# perf mode forward GEMM operands (gathered rows relu(bn(z)) and forward weight tiles): fp16 (default) or bf16
+# (RPC_SPARSE_FWD_BF16=1, A/B). The operand rounding of the forward decides the ReLU masks that every gradient
+# passes: with bf16 forward operands the perturber's input gradient is 0.237 rel-L2 from float64, with fp16 0.077
+# (cosine 0.972 -> 0.997), the backward's bf16 dz rows alike (oracle/sparse_encoder.py bf16_from emulation,
+# tests/test_gpu_sparse_layers.py). fp16 MFMA runs at the bf16 rate; the normalised activations and the
+# weights sit far inside its range (the dz rows, which would need loss scaling in fp16, stay bf16)
+FWD_FMT = 0 if os.environ.get("RPC_SPARSE_FWD_BF16", "0") != "0" else 1
 
 
 def _t3(v):
@@ -305,9 +312,10 @@ def _r32(c):
     return (c + 31) // 32 * 32
 
 
-def _prep_bf16_weights(lib, specs, Ws, dev, st):
-    """Forward and data-gradient bf16 B^T tiles of every bf16 layer (entries of `specs` / `Ws`),
-    from the fp32 master weights in rpc_spconv_prep_weight_bf16_batch launches of up to 32 tiles."""
+def _prep_bf16_weights(lib, specs, Ws, dev, st, fwd_fmt=0):
+    """Forward (format fwd_fmt: 0 bf16, 1 fp16) and data-gradient (bf16) B^T tiles of every 16-bit layer
+    (entries of `specs` / `Ws`), from the fp32 master weights in rpc_spconv_prep_weight_bf16_batch launches of
+    up to 32 tiles."""
     jobs = []
     for sp, W in zip(specs, Ws):
         for dg in (0, 1):
@@ -318,7 +326,8 @@ def _prep_bf16_weights(lib, specs, Ws, dev, st):
         group = jobs[g0:g0 + 32]
         descs = (_ffi.RpcSpconvWprep * len(group))()
         for i, (sp, W, dg, bt) in enumerate(group):
-            descs[i] = _ffi.RpcSpconvWprep(W.data_ptr(), bt.data_ptr(), sp.K, sp.ci, sp.co, dg)
+            descs[i] = _ffi.RpcSpconvWprep(W.data_ptr(), bt.data_ptr(), sp.K, sp.ci, sp.co, dg,
+                                           0 if dg else int(fwd_fmt))
         _ffi.check(lib.rpc_spconv_prep_weight_bf16_batch(descs, len(group), st), "rpc_spconv_prep_weight_bf16_batch")
     return [(jobs[2 * i][3], jobs[2 * i + 1][3]) for i in range(len(specs))]
 
@@ -516,14 +525,15 @@ class SparseEncoderFn(torch.autograd.Function):
         # perf mode: layers >= 1 gather bf16 rows of relu(bn(z)) (O(1) values); layer 0 stays fp32 —
         # its input is the raw VFE mean (coordinates up to 70 m, where a bf16 step is 0.5 m)
         bf16 = enc.bf16
-        hsrc = None
+        fmt = FWD_FMT if bf16 else 0     # forward operand format of the 16-bit layers
+        hsrc = hwg = None
         L = []
-        # bf16 layers (1..): forward + data-gradient weight tiles of all of them in one launch
+        # 16-bit layers (1..): forward + data-gradient weight tiles of all of them in one launch
         wtiles = {}
         if bf16 and len(enc.specs) > 1:
             bl = list(range(1, len(enc.specs)))
             Ws = [params[3 * li].detach().float().contiguous() for li in bl]
-            for li, tiles in zip(bl, _prep_bf16_weights(lib, [enc.specs[li] for li in bl], Ws, dev, st)):
+            for li, tiles in zip(bl, _prep_bf16_weights(lib, [enc.specs[li] for li in bl], Ws, dev, st, fmt)):
                 wtiles[li] = tiles
         # rulebooks (and the strided layers' output counts, host reads) on a side stream, ahead of the GEMMs
         plan = enc.__dict__.get("_prepared", {}).pop((coors.data_ptr(), feats.shape[0], B), None)
@@ -548,13 +558,14 @@ class SparseEncoderFn(torch.autograd.Function):
             part = torch.empty((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
             tm = enc.timer is not None and enc.timer.wants("fwd", sp)
             rec["bf16"] = bf16 and li > 0
-            rec["h_in"] = hsrc if rec["bf16"] else None
+            rec["h_in"] = hwg if rec["bf16"] else None   # the weight gradient's bf16 rows
+            rec["h_fmt"] = 0
             bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
             fused = False
             if rec["bf16"]:
                 bt, rec["btd"] = wtiles[li]
                 e0 = enc.timer.start() if tm else None
-                tk = enc.fin_ticket_ptr(dev, li, n_out) if FUSED_FINALIZE and n_out > 0 else None
+                tk = enc.fin_ticket_ptr(dev, li, n_out) if FUSED_FINALIZE and n_out > 0 and fmt == 0 else None
                 if tk is not None:
                     # GEMM + this layer's BatchNorm finalize in one launch (last-arriving blocks)
                     gpart = torch.empty(lib.rpc_bn_fin_groups(n_out) * 2 * sp.co, dtype=torch.float64, device=dev)
@@ -567,9 +578,9 @@ class SparseEncoderFn(torch.autograd.Function):
                                "rpc_spconv_gemm_bf16_fin")
                     fused = True
                 else:
-                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(hsrc), hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
-                                                          0, n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None,
-                                                          _ffi.ptr(part), 0, st), "rpc_spconv_gemm_bf16")
+                    _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
+                                                       sp.K, 0, n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None,
+                                                       _ffi.ptr(part), 0, st), "rpc_spconv_gemm_h16")
             else:
                 e0 = enc.timer.start() if tm else None
                 _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
@@ -592,17 +603,23 @@ class SparseEncoderFn(torch.autograd.Function):
                 out = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
                 ob = (torch.empty((n_out, _r8(sp.co)), dtype=torch.bfloat16, device=dev)
                       if bf16 and li + 1 < len(enc.specs) else None)
+                ob2 = torch.empty_like(ob) if ob is not None and fmt else None
                 res = L[sp.res]["out"] if sp.res >= 0 else None
-                _ffi.check(lib.rpc_sparse_res_forward(_ffi.ptr(z), _ffi.ptr(bn), _ffi.ptr(res), n_out, sp.co,
-                                                      _ffi.ptr(out), _ffi.ptr(ob), st), "rpc_sparse_res_forward")
+                _ffi.check(lib.rpc_sparse_res_forward_h16(_ffi.ptr(z), _ffi.ptr(bn), _ffi.ptr(res), n_out, sp.co,
+                                                          _ffi.ptr(out), _ffi.ptr(ob), fmt, _ffi.ptr(ob2), st),
+                           "rpc_sparse_res_forward_h16")
                 rec["out"] = out
-                src, src_bn, hsrc = out, None, ob
+                src, src_bn, hsrc, hwg = out, None, ob, (ob2 if ob2 is not None else ob)
             else:
                 src, src_bn = z, bn
                 if bf16 and li + 1 < len(enc.specs):
+                    # the next layer's gathered rows in the forward format, and (fp16 forward) a bf16 copy for its
+                    # weight gradient, whose MFMAs pair them with the bf16 dz rows (one pass writes both: converting
+                    # while the weight gradient stages them cost it 10 %)
                     hsrc = torch.empty((n_out, _r8(sp.co)), dtype=torch.bfloat16, device=dev)
-                    _ffi.check(lib.rpc_to_bf16_rows(_ffi.ptr(z), _ffi.ptr(bn), n_out, sp.co, 1, _ffi.ptr(hsrc), st),
-                               "rpc_to_bf16_rows")
+                    hwg = torch.empty_like(hsrc) if fmt else hsrc
+                    _ffi.check(lib.rpc_to_h16_rows(_ffi.ptr(z), _ffi.ptr(bn), n_out, sp.co, 1, fmt, _ffi.ptr(hsrc),
+                                                   _ffi.ptr(hwg) if fmt else None, st), "rpc_to_h16_rows")
         _ffi.bump_batches([m[1] for m in mods])
         last = L[-1]
         D, H, Wd = enc.shapes[-1]
@@ -730,9 +747,9 @@ class SparseEncoderFn(torch.autograd.Function):
                     wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, sp.K, sp.ci, sp.co)
                     ws = _ffi.workspace(wsz, dev)
                     e0 = timer.start() if tw else None
-                    _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(rec["h_in"]), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
-                                                         n_out, _ffi.ptr(dzb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws), wsz,
-                                                         sw), "rpc_spconv_wgrad_bf16")
+                    _ffi.check(lib.rpc_spconv_wgrad_h16(_ffi.ptr(rec["h_in"]), rec["h_fmt"], sp.ci, _ffi.ptr(rec["nbr"]),
+                                                        sp.K, n_out, _ffi.ptr(dzb), sp.co, _ffi.ptr(dW), _ffi.ptr(ws),
+                                                        wsz, sw), "rpc_spconv_wgrad_h16")
                     kn = f"rpc::spb::k_wgrad_bf16<{sp.ci}, {sp.co}, 3>"
                 else:
                     wsz = lib.rpc_spconv_wgrad_workspace_size(n_out, sp.K, sp.ci, sp.co)
@@ -848,7 +865,7 @@ def _native_backward(ctx, gdense):
             sp.res, vp(rec["nbr"]), vp(rec.get("nbr_in")), vp(rec["z"]), vp(rec["bn"]), vp(rec.get("out")),
             vp(rec["h_in"]) if bf else None, None if bf else vp(rec["src"]), None if bf else vp(rec["src_bn"]),
             vp(rec["W"]), vp(rec["gamma"]), vp(rec["beta"]), vp(rec.get("btd")) if bf else None,
-            dW.data_ptr(), dg.data_ptr(), db.data_ptr(),
+            dW.data_ptr(), dg.data_ptr(), db.data_ptr(), int(rec.get("h_fmt", 0)),
             ctx.enc.fin_ticket_ptr(dev, nl + li, rec["n_in"]) if bf and FUSED_FINALIZE else None)
     dfeat = (torch.empty((L[0]["n_in"], L[0]["spec"].ci), dtype=torch.float32, device=dev)
              if ctx.needs_input_grad[0] else None)

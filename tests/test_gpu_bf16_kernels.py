@@ -123,3 +123,91 @@ def test_bf16_row_producers(n, c):
     _bf16_ulp_close(dz[:, :c], want_dz, atol=1e-5)
     if cp > c:
         assert (h[:, c:] == 0).all() and (dz[:, c:] == 0).all()
+
+
+@pytest.mark.parametrize("n,c", [(4097, 64), (515, 60), (70001, 128)])
+def test_f16_row_producer(n, c):
+    """rpc_to_h16_rows fmt 1 (the perf mode's fp16 forward rows): relu(bn(z)) within one fp16 ulp of float64, and
+    its bf16 copy within one bf16 ulp."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(n + 7 * c)
+    cp = _r8(c)
+    z = torch.randn(n, c, generator=g) * 2
+    bn = torch.cat([torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.3,
+                    torch.randn(c, generator=g) * 0.2, torch.rand(c, generator=g) + 0.5])
+    h = torch.full((n, cp), 7.0, dtype=torch.float16, device=dev)
+    hb = torch.full((n, cp), 7.0, dtype=torch.bfloat16, device=dev)
+    zd, bnd = z.to(dev), bn.to(dev)     # held: the kernel reads them after the call returns
+    _ffi.check(lib.rpc_to_h16_rows(_ffi.ptr(zd), _ffi.ptr(bnd), n, c, 1, 1, _ffi.ptr(h), _ffi.ptr(hb),
+                                   _ffi.stream_of(h)), "rpc_to_h16_rows")
+    torch.cuda.synchronize()
+    sc, be, mu = bn.double().view(4, c)[:3]
+    want = torch.clamp((z.double() - mu) * sc + be, min=0.0)
+    got = h[:, :c].double().cpu()
+    assert ((got - want).abs() <= want.abs() * 2.0 ** -10 + 1e-6).all()
+    _bf16_ulp_close(hb[:, :c], want, atol=1e-6)      # the bf16 copy of the same rows (weight gradient operand)
+    if cp > c:
+        assert (h[:, c:] == 0).all() and (hb[:, c:] == 0).all()
+
+
+@pytest.mark.parametrize("ci,co", [(16, 32), (32, 32), (64, 64), (64, 128), (128, 128)])
+def test_gemm_f16_forward_matches_fp64(ci, co):
+    """rpc_spconv_gemm_h16 fmt 1 (fp16 rows and fp16 forward weight tiles on v_mfma_f32_16x16x32_f16): against a
+    float64 gather-matmul of the same fp16 values, to fp32-accumulation accuracy; the BatchNorm partial rows
+    are the column sums of the stored rows; other epilogues refuse fp16."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    n_out, n_in, K = 3001, 2500, 27
+    g = torch.Generator().manual_seed(ci * 3 + co)
+    nbr = torch.randint(0, n_in, (n_out, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n_out, K), generator=g) > 0.3] = -1
+    h = torch.zeros((n_in, _r8(ci)), dtype=torch.float16)
+    h[:, :ci] = (torch.randn((n_in, ci), generator=g) * 3).to(torch.float16)
+    W = torch.randn((K, ci, co), generator=g) * 0.05
+    hd, nd, Wd = h.to(dev), nbr.to(dev), W.to(dev)
+    bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(K, ci, co, 0), dtype=torch.float16, device=dev)
+    desc = (_ffi.RpcSpconvWprep * 1)(_ffi.RpcSpconvWprep(Wd.data_ptr(), bt.data_ptr(), K, ci, co, 0, 1))
+    st = _ffi.stream_of(Wd)
+    _ffi.check(lib.rpc_spconv_prep_weight_bf16_batch(desc, 1, st), "prep fp16")
+    out = torch.full((n_out, co), float("nan"), device=dev)
+    part = torch.full((lib.rpc_spconv_gemm_blocks(n_out), 2 * co), float("nan"), device=dev)
+    _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(hd), 1, n_in, ci, _ffi.ptr(nd), K, 0, n_out, _ffi.ptr(bt), co,
+                                       _ffi.ptr(out), None, None, _ffi.ptr(part), 0, st), "gemm_h16")
+    assert lib.rpc_spconv_gemm_h16(_ffi.ptr(hd), 1, n_in, ci, _ffi.ptr(nd), K, 0, n_out, _ffi.ptr(bt), co,
+                                   _ffi.ptr(out), None, None, None, 2, st) == 3      # fp16: forward only
+    torch.cuda.synchronize()
+    Wq = W.to(torch.float16).double()
+    ref = torch.zeros((n_out, co), dtype=torch.float64)
+    hq = h[:, :ci].double()
+    for k in range(K):
+        ok = nbr[:, k] >= 0
+        ref[ok] += hq[nbr[ok, k].long()] @ Wq[k]
+    got = out.double().cpu()
+    assert (got - ref).abs().max().item() <= 2e-5 * max(ref.abs().max().item(), 1.0)
+    s = part.double().cpu().sum(0)
+    assert torch.allclose(s[:co], got.sum(0), rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("ci,co", [(16, 32), (64, 64), (128, 128)])
+def test_wgrad_h16_fp16_rows(ci, co):
+    """rpc_spconv_wgrad_h16 hfmt 1: the fp16 forward rows are rounded to bf16 as they are staged — the same
+    dW as rpc_spconv_wgrad_bf16 on those rows pre-rounded to bf16 (bit for bit)."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    n_out, K = 4000, 27
+    nbr, hb, dz = _case(n_out, 3500, K, ci, co, 0.3, seed=ci + co)
+    h16 = (hb.float() * 1.37).to(torch.float16)          # values off the bf16 grid
+    hq = h16.float().to(torch.bfloat16)                  # what the kernel stages
+    wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, K, ci, co)
+    ws = _ffi.workspace(wsz, dev)
+    nd, dd = nbr.to(dev), dz.to(dev)
+    dW16, dWb = torch.empty((K, ci, co), device=dev), torch.empty((K, ci, co), device=dev)
+    st = _ffi.stream_of(dd)
+    h16d, hqd = h16.to(dev), hq.to(dev)
+    _ffi.check(lib.rpc_spconv_wgrad_h16(_ffi.ptr(h16d), 1, ci, _ffi.ptr(nd), K, n_out, _ffi.ptr(dd), co,
+                                        _ffi.ptr(dW16), _ffi.ptr(ws), wsz, st), "wgrad_h16")
+    _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hqd), ci, _ffi.ptr(nd), K, n_out, _ffi.ptr(dd), co,
+                                         _ffi.ptr(dWb), _ffi.ptr(ws), wsz, st), "wgrad_bf16")
+    torch.cuda.synchronize()
+    assert torch.equal(dW16, dWb)

@@ -1,7 +1,7 @@
 """bf16 perf mode against the fp32 parity mode over a short training trajectory:
-the same 3-class model, initial weights and frames, trained 6 steps with Trainer(bf16=True) (bf16
-MFMA sparse layers 1-11, bf16 SECOND/FPN/head GEMMs) and Trainer(bf16=False) (fp32 HIP kernels end
-to end). Per step the detection losses and the total agree within the pinned bounds below, and the
+the same 3-class model, initial weights and frames, trained 6 steps with Trainer(bf16=True) (16-bit
+MFMA sparse layers 1-11 — fp16 forward operands, bf16 backward — bf16 SECOND/FPN/head GEMMs) and
+Trainer(bf16=False) (fp32 HIP kernels end to end). Per step the detection losses and the total agree within the pinned bounds below, and the
 adversary's parameter updates (what the perturber learns) point the same way. Bench numbers are
 bf16 perf-mode numbers; this test bounds how far that mode drifts from the parity mode."""
 import pytest
@@ -14,8 +14,10 @@ from robustpointclouds_amd.trainer import Trainer, make_kitti_model
 pytestmark = pytest.mark.gpu
 DEV = torch.device("cuda")
 STEPS = 6
-LOSS_REL = 2e-2      # (measured r02: 1.05e-2) per-step |bf16 - fp32| / |fp32| of loss_cls, loss_bbox, loss_dir and the total
-ADV_COS = 0.98       # (measured r02: 0.9915) cosine of the adversary's parameter change (bf16 vs fp32) after STEPS steps
+# r04: with the sparse encoder's forward GEMM operands in fp16 (SparseEncoder FWD_FMT; r02/r03 bf16: loss rel
+# 1.05e-2, adversary cosine 0.9915) measured 6.6e-3 and 0.99550
+LOSS_REL = 1e-2      # per-step |perf - fp32| / |fp32| of loss_cls, loss_bbox, loss_dir and the total
+ADV_COS = 0.995      # cosine of the adversary's parameter change (perf vs fp32) after STEPS steps
 
 
 def _run(bf16, batches):

@@ -1,6 +1,12 @@
-"""Per-layer diagnostic of the fp32 sparse encoder: every layer's pre-BN activation z and
-its backward gradient dy (= dL/d pre-activation, after the ReLU mask) against the float64
-oracle, rows matched by coordinates. Prints the table; asserts loose bounds."""
+"""Per-layer diagnostic of the sparse encoder: every layer's pre-BN activation z and its backward gradient
+dy (= dL/d pre-activation, after the ReLU mask) against the float64 oracle, rows matched by coordinates.
+Prints the table.
+
+Bars: the fp32 parity mode within 1e-4 of float64. The perf mode (16-bit MFMA operands from layer 1 on) is
+held to the error its operand formats cannot avoid: the same float64 oracle with the operands rounded where
+the kernels round them (oracle/sparse_encoder.py bf16_from / fwd_fp16 — forward rows and weights in fp16 by
+default, or bf16 under RPC_SPARSE_FWD_BF16; backward dz rows bf16) — per layer within max(0.05, 1.1x)
+of that emulation's own distance from float64, z within 2e-2 of the channel spread."""
 import numpy as np
 import pytest
 import torch
@@ -18,28 +24,38 @@ def _key(c):
     return ((c[:, 0] * 64 + c[:, 1]) * 2048 + c[:, 2]) * 2048 + c[:, 3]
 
 
-@pytest.mark.parametrize("bf16", [False, True])
-def test_per_layer_errors(capsys, bf16):
+def _oracle_run(enc, feats, coors, G, **kw):
+    orc = OracleSparseEncoder(enc, **kw)
+    f = torch.from_numpy(feats).double().requires_grad_(True)
+    ref = orc.forward(f, coors, 1, keep=True)
+    (ref * G.double()).sum().backward()
+    return orc, f.grad
+
+
+@pytest.mark.parametrize("mode", ["fp32", "perf", "perf_bf16fwd"])
+def test_per_layer_errors(capsys, mode, monkeypatch):
     torch.manual_seed(0)
     feats, coors = _inputs(1, 1)
     dev = torch.device("cuda")
     enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
-    enc.bf16 = bf16
+    enc.bf16 = mode != "fp32"
+    monkeypatch.setattr(SE, "FWD_FMT", 0 if mode == "perf_bf16fwd" else 1)
     with torch.no_grad():
         for m in enc.layers():
             m[1].weight.uniform_(0.5, 1.5)
             m[1].bias.uniform_(-0.2, 0.2)
-    orc = OracleSparseEncoder(enc)
+    G = torch.randn((1, 256, 200, 176), generator=torch.Generator().manual_seed(1))
+    orc, ref_fg = _oracle_run(enc, feats, coors, G)
+    emu, emu_fg = (_oracle_run(enc, feats, coors, G, bf16_from=1, fwd_fp16=mode == "perf")
+                   if mode != "fp32" else (None, None))
     enc.debug = []
     f = torch.from_numpy(feats).to(dev).requires_grad_(True)
     out = enc(f, torch.from_numpy(coors).to(dev), 1)
-    ref = orc.forward(torch.from_numpy(feats).double(), coors, 1, keep=True)
-    G = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
-    (out * G.to(dev)).sum().backward()
-    (ref * G.double()).sum().backward()
+    (out.float() * G.to(dev)).sum().backward()
     dbg = {li: (c, z, dy) for li, c, z, dy in enc.debug}
     enc.debug = None
-    worst_z = worst_d = 0.0
+    worst_z = 0.0
+    rows = []
     with capsys.disabled():
         for i, (rc, rz, pre) in enumerate(orc.trace):
             c, z, dy = dbg[i]
@@ -51,11 +67,21 @@ def test_per_layer_errors(capsys, bf16):
             es = ((z[pos] - rz.detach()).norm() / (rz - rz.mean(0)).norm()).item()
             ed = ((dy[pos] - pre.grad).norm() / pre.grad.norm()).item()
             flips = int(((dy[pos] == 0) != (pre.grad == 0)).sum())
-            print(f"{'bf16' if bf16 else 'fp32'} layer {i:2d} rows {len(kr):7d}  z rel {ez:.2e} (vs spread {es:.2e})  dy rel {ed:.2e}  mask flips {flips}")
-            worst_z, worst_d = max(worst_z, es), max(worst_d, ed)
-    if bf16:
-        # bf16 gathers: forward error grows ~1e-3 per layer; backward differences are dominated
-        # by ReLU masks that flip where the pre-activation is within bf16 noise of 0
-        assert worst_z < 2e-2 and worst_d < 0.35
+            ee = ((emu.trace[i][2].grad - pre.grad).norm() / pre.grad.norm()).item() if emu else 0.0
+            print(f"{mode:12s} layer {i:2d} rows {len(kr):7d}  z rel {ez:.2e} (vs spread {es:.2e})  dy rel {ed:.2e} "
+                  f"(operand-emulation oracle {ee:.2e})  mask flips {flips}")
+            worst_z = max(worst_z, es)
+            rows.append((ed, ee))
+        # the perturber-facing gradient: d loss / d encoder input
+        eg = ((f.grad.double().cpu() - ref_fg).norm() / ref_fg.norm()).item()
+        eeg = ((emu_fg - ref_fg).norm() / ref_fg.norm()).item() if emu else 0.0
+        print(f"{mode:12s} input gradient rel {eg:.3e} (operand-emulation oracle {eeg:.3e})")
+    if mode == "fp32":
+        assert worst_z < 1e-4 and max(ed for ed, _ in rows) < 1e-4 and eg < 1e-4
     else:
-        assert worst_z < 1e-4 and worst_d < 1e-4
+        assert worst_z < 2e-2
+        for ed, ee in rows:
+            assert ed <= max(0.05, 1.1 * ee)
+        assert eg <= max(0.05, 1.1 * eeg)
+        if mode == "perf":   # the fp16 forward operands: the perturber's gradient within 0.1 of float64
+            assert eg < 0.1

@@ -85,8 +85,9 @@ def _encoder_case():
 def _encoder_step(enc, feats, coors, mode, fused):
     from robustpointclouds_amd import sparse_encoder as se
     lib = _ffi.load()
-    prev, prev_f = lib.rpc_spconv_gemm_bf16_mode(mode), se.FUSED_FINALIZE
+    prev, prev_f, prev_fmt = lib.rpc_spconv_gemm_bf16_mode(mode), se.FUSED_FINALIZE, se.FWD_FMT
     se.FUSED_FINALIZE = fused
+    se.FWD_FMT = 0   # the ring kernel and the fused finalize are bf16 paths
     try:
         for p in enc.parameters():
             p.grad = None
@@ -105,6 +106,7 @@ def _encoder_step(enc, feats, coors, mode, fused):
     finally:
         lib.rpc_spconv_gemm_bf16_mode(prev)
         se.FUSED_FINALIZE = prev_f
+        se.FWD_FMT = prev_fmt
 
 
 def test_pipe_encoder_step_bit_identical():

@@ -390,7 +390,7 @@ def main():
             else 0.0
     # the reference's precision (fp32) on the same frames, after the headline timing (all ranks take part)
     parity = None
-    if not a.fp32 and not a.no_parity_mode and a.roofline_kernel == "dense" and not nus:
+    if not a.fp32 and not a.no_parity_mode and a.roofline_kernel == "dense":
         fpf = step_flops["total"] / a.batch if step_flops is not None else None
         parity = _parity_mode(a, data, ready, dev, nus, fpf)
     frames = world * a.batch * a.steps

@@ -296,6 +296,16 @@ int rpc_bn_fin_tickets(int n_out);
 int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
                              const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
                              float* part, int epi, const RpcBnFin* fin, void* stream);
+/* the general form: operand format fmt and the rows visited in the order perm ([n_out] row indices, a
+ * permutation: rpc_rulebook_mask_perm of `map`; NULL = natural order). Every row is written in place and its
+ * own sums are those of the natural order; only the BatchNorm partial rows (sums over 64 visited rows) differ. */
+int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
+                         const int* perm, int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                         const float* prev_bn, float* part, int epi, void* stream);
+/* the rows of a rulebook map [n][kvol] ordered by their neighbour masks within windows of 2048 rows
+ * (perm[i] = the row visited i-th): the 16-row MFMA tiles of rpc_spconv_gemm_perm then share offsets.
+ * No reference counterpart (spconv's implicit GEMM visits rows in index order). */
+int rpc_rulebook_mask_perm(const int* nbr, int n, int kvol, int* perm, void* stream);
 /* kernel behind rpc_spconv_gemm_bf16[_n|_fin] (A/B measurement, tests; env RPC_SPGEMM): 0 (default) = one
  * offset of look-ahead in registers, 1 = the S-stage LDS-DMA ring (k_gemm_pipe), 2 / 3 = its 4-wave / 3-stage
  * forms. Same bits in every mode. 4..19: timing arms (garbage results). mode < 0 queries. Returns the
@@ -339,6 +349,8 @@ typedef struct {
   float* dgamma;
   float* dbeta;
   int h_fmt;             /* bf16 layers: format of h_in (RPC_H16_BF16 / RPC_H16_F16) */
+  const int* perm_out;   /* bf16 layers (optional): visiting order of the forward map's rows (n_out) */
+  const int* perm_in;    /* bf16 layers (optional): visiting order of the data-gradient map's rows (n_in) */
   unsigned* fin_ticket;  /* bf16 layers: rpc_bn_fin_tickets(n_in) zeroed counters — the data gradient into the
                             layer below then finalizes that layer's BatchNorm backward in its own launch
                             (rpc_spconv_gemm_bf16_fin); NULL: a separate rpc_bn_finalize */
@@ -624,6 +636,11 @@ int rpc_head_pack(const void* z, int zp, int n, const float* bias, float* out, i
 size_t rpc_head_unpack_workspace_size(void);
 int rpc_head_unpack_grad(const float* dout, int dp, int doff, int n, void* dz, int zp, long long cells, float* dbias,
                          void* workspace, size_t ws_bytes, void* stream);
+/* parity mode: the same with fp32 z / dz images */
+int rpc_head_pack_f32(const float* z, int zp, int n, const float* bias, float* out, int op, int ooff, long long cells,
+                      void* stream);
+int rpc_head_unpack_grad_f32(const float* dout, int dp, int doff, int n, float* dz, int zp, long long cells,
+                             float* dbias, void* workspace, size_t ws_bytes, void* stream);
 int rpc_center_head_targets(const RpcCenterCfg* cfg, int max_gts, const void* workspace, const float** heatmap,
                             const int** ind, const int** mask, const float** anno);
 
@@ -643,6 +660,14 @@ size_t rpc_dcn_backward_workspace_size(int B, int H, int W);
 int rpc_dcn_backward(const void* x, int xp, const void* off, int offp, const float* off_bias, const void* w_bwd,
                      const void* dout, int dop, float* dx, void* doff, int doffp, float* doff_bias, float* dW,
                      int B, int H, int W, void* workspace, size_t ws_bytes, void* stream);
+/* parity mode: the same deformable convolution on fp32 images (x, off, out, dout, doff; pitches
+ * multiples of 4) in fp32 arithmetic, W [64][16][3][3] fp32 read directly (no prep); the backward
+ * workspace is rpc_dcn_backward_workspace_size's. */
+int rpc_dcn_forward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias, const float* W,
+                        float* out, int op, int B, int H, int W_, void* stream);
+int rpc_dcn_backward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias, const float* W,
+                         const float* dout, int dop, float* dx, float* doff, int doffp, float* doff_bias, float* dW,
+                         int B, int H, int W_, void* workspace, size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -92,7 +92,7 @@ class RpcSparseLayer(C.Structure):
                 ("out", C.c_void_p), ("h_in", C.c_void_p), ("src", C.c_void_p), ("src_bn", C.c_void_p),
                 ("W", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("btd", C.c_void_p),
                 ("dW", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("h_fmt", C.c_int),
-                ("fin_ticket", C.c_void_p)]
+                ("perm_out", C.c_void_p), ("perm_in", C.c_void_p), ("fin_ticket", C.c_void_p)]
 
 
 class RpcBnFin(C.Structure):
@@ -152,6 +152,8 @@ SIGNATURES = {
     "rpc_spconv_gemm_bf16_n": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_gemm_bf16_mode": (i32, [i32]),
     "rpc_spconv_gemm_h16": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
+    "rpc_spconv_gemm_perm": (i32, [vp, i32, i32, i32, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
+    "rpc_rulebook_mask_perm": (i32, [vp, i32, i32, vp, vp]),
     "rpc_to_h16_rows": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     "rpc_spconv_wgrad_h16": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
     "rpc_sparse_res_forward_h16": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
@@ -204,6 +206,11 @@ SIGNATURES = {
     "rpc_dcn_forward": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),
     "rpc_dcn_backward_workspace_size": (sz, [i32, i32, i32]),
     "rpc_dcn_backward": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, sz, vp]),
+    "rpc_dcn_forward_f32": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),
+    "rpc_dcn_backward_f32": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, sz,
+                                   vp]),
+    "rpc_head_pack_f32": (i32, [vp, i32, i32, vp, vp, i32, i32, C.c_longlong, vp]),
+    "rpc_head_unpack_grad_f32": (i32, [vp, i32, i32, i32, vp, i32, C.c_longlong, vp, vp, sz, vp]),
     "rpc_sparse_res_forward": (i32, [vp, vp, vp, i32, i32, vp, vp, vp]),
     "rpc_sparse_res_backward": (i32, [vp, vp, vp, vp, vp, i32, i32, vp, vp, vp]),
     "rpc_center_head_workspace_size": (sz, [C.POINTER(RpcCenterCfg), i32]),

@@ -206,33 +206,35 @@ def _imgs(B, H, W):
     return (B, H, W), (B, H, W), (B, H, W)
 
 
-def _conv_nobn_fwd(lib, weight, ci, h, pitch, B, H, W, dev, st):
-    """3x3 conv (no BN) on the dense engine with the outputs padded to 64 -> (z image, record)."""
+def _conv_nobn_fwd(eng, weight, ci, h, pitch, B, H, W, dev, st):
+    """3x3 conv (no BN) on the dense engine (bf16 or fp32) with the outputs padded to 64 ->
+    (z image, record)."""
     n = weight.shape[0]
     W32 = torch.zeros((_PAD, ci, 3, 3), dtype=torch.float32, device=dev)
     W32[:n] = weight.detach().float()
-    wf = torch.empty((9, _PAD, ci), dtype=torch.bfloat16, device=dev)
-    wd = torch.empty((9, ci, _PAD), dtype=torch.bfloat16, device=dev)
-    _ffi.check(lib.rpc_dense_wprep(_ffi.ptr(W32), 0, ci, _PAD, 9, 1, _ffi.ptr(wf), _ffi.ptr(wd), st), "rpc_dense_wprep")
-    z = db._image(B, _PAD, H, W, dev)
+    wf = torch.empty((9, _PAD, ci), dtype=eng.dt, device=dev)
+    wd = torch.empty((9, ci, _PAD), dtype=eng.dt, device=dev)
+    desc = (_ffi.RpcDenseWprep * 1)(_ffi.RpcDenseWprep(W32.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, _PAD, 9, 1))
+    _ffi.check(eng.wprep_batch(desc, 1, st), "rpc_dense_wprep_batch")
+    z = db._image(B, _PAD, H, W, dev, eng.dt)
     R = _ffi.int_arr((B, H, W))
-    _ffi.check(db._conv(lib, db.S1, _ffi.ptr(h), pitch, ci, _ffi.ptr(wf), _PAD, _ffi.ptr(z), _PAD, 0, 0, None, R, R, R,
+    _ffi.check(eng.conv(db.S1, _ffi.ptr(h), pitch, ci, _ffi.ptr(wf), _PAD, _ffi.ptr(z), _PAD, 0, 0, None, R, R, R,
                         st), "rpc_dense_conv")
-    return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, B=B, H=H, W=W)
+    return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, B=B, H=H, W=W, W32=W32)
 
 
-def _conv_nobn_bwd(lib, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=False):
+def _conv_nobn_bwd(eng, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=False):
     ci, B, H, W = rec["ci"], rec["B"], rec["H"], rec["W"]
     R = _ffi.int_arr((B, H, W))
     dW = torch.empty((_PAD, ci, 3, 3), dtype=torch.float32, device=dev)
-    wsz = lib.rpc_dense_wgrad_workspace_size(db.S1, R, ci, _PAD)
+    wsz = eng.wgrad_ws(db.S1, R, ci, _PAD)
     ws = _ffi.workspace(wsz, dev)
-    _ffi.check(lib.rpc_dense_wgrad(db.S1, 0, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), _PAD, _PAD, R, R, R,
-                                   _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
+    _ffi.check(eng.wgrad(db.S1, 0, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), _PAD, _PAD, R, R, R,
+                         _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
     dx = None
     if need_dx:
-        dx = dx_out if dx_out is not None else db._image(B, ci, H, W, dev)
-        _ffi.check(db._conv(lib, db.S1, _ffi.ptr(dz), _PAD, _PAD, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
+        dx = dx_out if dx_out is not None else db._image(B, ci, H, W, dev, eng.dt)
+        _ffi.check(eng.conv(db.S1, _ffi.ptr(dz), _PAD, _PAD, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
                             1 if accumulate else 0, None, R, R, R, st), "rpc_dense_conv(dgrad)")
     return dx, dW[:rec["n"]]
 
@@ -244,14 +246,18 @@ def _conv_module_layer(cm):
 class CenterHeadFn(torch.autograd.Function):
     """The whole CenterHead (shared conv + every DCNSeparateHead) as one node: neck image ->
     (hm [cells, hm_pitch], box [cells, box_pitch]) fp32; the shared feature gradient is accumulated in
-    fp32 (DCN input gradients) plus bf16 (offset-conv data gradients)."""
+    fp32 (DCN input gradients) plus the engine's dtype (offset-conv data gradients). The engine follows
+    the neck image: bf16 (perf mode: bf16 dense engine + bf16-MFMA DCN) or fp32 (parity mode: fp32
+    dense engine, fp32 DCN, fp32 head images)."""
 
     @staticmethod
     def forward(ctx, x, head, *params):
         lib = _ffi.load()
         dev = x.device
         st = _ffi.stream_of(x)
-        xi = db._nhwc(x)
+        eng = db._engine(lib, x)
+        f32 = eng.f32
+        xi = db._nhwc(x, eng.dt)
         B, Cin, H, W = xi.shape
         if H % 8 or W % 8:
             raise RuntimeError("HIP CenterHead needs a feature map with H, W multiples of 8")
@@ -259,31 +265,38 @@ class CenterHeadFn(torch.autograd.Function):
         cells = B * H * W
         hm = torch.empty((cells, head.hm_pitch), dtype=torch.float32, device=dev)
         box = torch.empty((cells, head.box_pitch), dtype=torch.float32, device=dev)
+        pack = lib.rpc_head_pack_f32 if f32 else lib.rpc_head_pack
         Lsh = _conv_module_layer(head.shared_conv)
-        y0, rsh, _, _ = db._forward_layer(db._Eng(lib, False), Lsh, xi, Cin, B, H, W, training, dev, st)
+        y0, rsh, _, _ = db._forward_layer(eng, Lsh, xi, Cin, B, H, W, training, dev, st)
         bns = [head.shared_conv.bn]
         trecs = []
         c0 = 0
         for t, th in enumerate(head.task_heads):
             tr = {}
             for br, dcn in (("cls", th.feature_adapt_cls), ("reg", th.feature_adapt_reg)):
-                oz, orec = _conv_nobn_fwd(lib, dcn.conv_offset.weight, 64, y0, 64, B, H, W, dev, st)
-                wf = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=dev)
-                wdd = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=dev)
-                _ffi.check(lib.rpc_dcn_prep_weight(_ffi.ptr(dcn.weight.detach().float().contiguous()), _ffi.ptr(wf),
-                                                   _ffi.ptr(wdd), st), "rpc_dcn_prep_weight")
+                oz, orec = _conv_nobn_fwd(eng, dcn.conv_offset.weight, 64, y0, 64, B, H, W, dev, st)
                 ob = dcn.conv_offset.bias.detach().float().contiguous()
-                feat = db._image(B, 64, H, W, dev)
-                _ffi.check(lib.rpc_dcn_forward(_ffi.ptr(y0), 64, _ffi.ptr(oz), _PAD, _ffi.ptr(ob), _ffi.ptr(wf),
-                                               _ffi.ptr(feat), 64, B, H, W, st), "rpc_dcn_forward")
+                feat = db._image(B, 64, H, W, dev, eng.dt)
+                if f32:
+                    wdd = dcn.weight.detach().float().contiguous()
+                    _ffi.check(lib.rpc_dcn_forward_f32(_ffi.ptr(y0), 64, _ffi.ptr(oz), _PAD, _ffi.ptr(ob),
+                                                       _ffi.ptr(wdd), _ffi.ptr(feat), 64, B, H, W, st),
+                               "rpc_dcn_forward_f32")
+                else:
+                    wf = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=dev)
+                    wdd = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=dev)
+                    _ffi.check(lib.rpc_dcn_prep_weight(_ffi.ptr(dcn.weight.detach().float().contiguous()),
+                                                       _ffi.ptr(wf), _ffi.ptr(wdd), st), "rpc_dcn_prep_weight")
+                    _ffi.check(lib.rpc_dcn_forward(_ffi.ptr(y0), 64, _ffi.ptr(oz), _PAD, _ffi.ptr(ob), _ffi.ptr(wf),
+                                                   _ffi.ptr(feat), 64, B, H, W, st), "rpc_dcn_forward")
                 tr[br] = dict(dcn=dcn, oz=oz, orec=orec, wd=wdd, ob=ob, feat=feat)
             # cls branch -> heatmap logits
             L = _conv_module_layer(th.cls_head[0])
-            hcls, rc, _, _ = db._forward_layer(db._Eng(lib, False), L, tr["cls"]["feat"], 64, B, H, W, training, dev, st)
+            hcls, rc, _, _ = db._forward_layer(eng, L, tr["cls"]["feat"], 64, B, H, W, training, dev, st)
             bns.append(th.cls_head[0].bn)
             fc = th.cls_head[1]
-            z, frec = _conv_nobn_fwd(lib, fc.weight, 64, hcls, 64, B, H, W, dev, st)
-            _ffi.check(lib.rpc_head_pack(_ffi.ptr(z), _PAD, th.num_cls, _ffi.ptr(fc.bias.detach().float().contiguous()),
+            z, frec = _conv_nobn_fwd(eng, fc.weight, 64, hcls, 64, B, H, W, dev, st)
+            _ffi.check(pack(_ffi.ptr(z), _PAD, th.num_cls, _ffi.ptr(fc.bias.detach().float().contiguous()),
                                          _ffi.ptr(hm), head.hm_pitch, c0, cells, st), "rpc_head_pack")
             tr["cls_layers"] = (rc, frec, fc, c0, th.num_cls, hm, head.hm_pitch)
             c0 += th.num_cls
@@ -292,12 +305,12 @@ class CenterHeadFn(torch.autograd.Function):
             for name in _BOX_ORDER:
                 seq = getattr(th.task_head, name)
                 L = _conv_module_layer(seq[0])
-                hr, rr, _, _ = db._forward_layer(db._Eng(lib, False), L, tr["reg"]["feat"], 64, B, H, W, training, dev, st)
+                hr, rr, _, _ = db._forward_layer(eng, L, tr["reg"]["feat"], 64, B, H, W, training, dev, st)
                 bns.append(seq[0].bn)
                 fcv = seq[1]
                 n = fcv.weight.shape[0]
-                z, frec = _conv_nobn_fwd(lib, fcv.weight, 64, hr, 64, B, H, W, dev, st)
-                _ffi.check(lib.rpc_head_pack(_ffi.ptr(z), _PAD, n, _ffi.ptr(fcv.bias.detach().float().contiguous()),
+                z, frec = _conv_nobn_fwd(eng, fcv.weight, 64, hr, 64, B, H, W, dev, st)
+                _ffi.check(pack(_ffi.ptr(z), _PAD, n, _ffi.ptr(fcv.bias.detach().float().contiguous()),
                                              _ffi.ptr(box), head.box_pitch, bo, cells, st), "rpc_head_pack")
                 regs.append((rr, frec, fcv, bo, n))
                 bo += n
@@ -307,6 +320,7 @@ class CenterHeadFn(torch.autograd.Function):
             _ffi.bump_batches(bns)
         ctx.head, ctx.rsh, ctx.trecs = head, rsh, trecs
         ctx.shape = (B, H, W, Cin)
+        ctx.f32 = f32
         ctx.param_list = params
         ctx.need_x = ctx.needs_input_grad[0]
         return hm, box
@@ -320,6 +334,8 @@ class CenterHeadFn(torch.autograd.Function):
         st = _ffi.stream_of(g_any)
         cells = B * H * W
         head = ctx.head
+        eng = db._Eng(lib, ctx.f32)
+        f32 = eng.f32
         ghm = ghm.contiguous() if ghm is not None else torch.zeros((cells, head.hm_pitch), device=dev)
         gbox = gbox.contiguous() if gbox is not None else torch.zeros((cells, head.box_pitch), device=dev)
         grads = {}
@@ -331,13 +347,14 @@ class CenterHeadFn(torch.autograd.Function):
         dws = _ffi.workspace(dwsz, dev)
 
         def head_branch(rec_cm, frec, conv, g, gp, off, n, dfeat, acc):
-            dz = db._image(B, _PAD, H, W, dev)
+            dz = db._image(B, _PAD, H, W, dev, eng.dt)
             db_ = torch.empty(n, dtype=torch.float32, device=dev)
-            _ffi.check(lib.rpc_head_unpack_grad(_ffi.ptr(g), gp, off, n, _ffi.ptr(dz), _PAD, cells, _ffi.ptr(db_),
+            unpack = lib.rpc_head_unpack_grad_f32 if f32 else lib.rpc_head_unpack_grad
+            _ffi.check(unpack(_ffi.ptr(g), gp, off, n, _ffi.ptr(dz), _PAD, cells, _ffi.ptr(db_),
                                                 _ffi.ptr(uws), uwsz, st), "rpc_head_unpack_grad")
-            dh, dW = _conv_nobn_bwd(lib, frec, dz, dev, st)
+            dh, dW = _conv_nobn_bwd(eng, frec, dz, dev, st)
             grads[id(conv.weight)], grads[id(conv.bias)] = dW, db_
-            dfeat, dWc, dg, dbt, _ = db._backward_layer(db._Eng(lib, False), rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
+            dfeat, dWc, dg, dbt, _ = db._backward_layer(eng, rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
             L = rec_cm["L"]
             grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWc, dg, dbt
             return dfeat
@@ -350,10 +367,11 @@ class CenterHeadFn(torch.autograd.Function):
                 dfr = head_branch(rr, frec2, fcv, gbox, head.box_pitch, bo, n, dfr, i > 0)
             for br, dfeat in (("cls", dfc), ("reg", dfr)):
                 d = tr[br]
-                doff = db._image(B, _PAD, H, W, dev)
+                doff = db._image(B, _PAD, H, W, dev, eng.dt)
                 dob = torch.empty(18, dtype=torch.float32, device=dev)
                 dWd = torch.empty((64, 16, 3, 3), dtype=torch.float32, device=dev)
-                _ffi.check(lib.rpc_dcn_backward(_ffi.ptr(d["orec"]["h"]), 64, _ffi.ptr(d["oz"]),
+                dcn_bwd = lib.rpc_dcn_backward_f32 if f32 else lib.rpc_dcn_backward
+                _ffi.check(dcn_bwd(_ffi.ptr(d["orec"]["h"]), 64, _ffi.ptr(d["oz"]),
                                                 _PAD, _ffi.ptr(d["ob"]), _ffi.ptr(d["wd"]), _ffi.ptr(dfeat), 64,
                                                 _ffi.ptr(dY0f), _ffi.ptr(doff), _PAD, _ffi.ptr(dob), _ffi.ptr(dWd), B, H,
                                                 W, _ffi.ptr(dws), dwsz, st), "rpc_dcn_backward")
@@ -361,11 +379,11 @@ class CenterHeadFn(torch.autograd.Function):
                 grads[id(dcn.weight)] = dWd
                 grads[id(dcn.conv_offset.bias)] = dob
                 first = dY0b is None
-                dY0b, dWo = _conv_nobn_bwd(lib, d["orec"], doff, dev, st, True, dY0b, not first)
+                dY0b, dWo = _conv_nobn_bwd(eng, d["orec"], doff, dev, st, True, dY0b, not first)
                 grads[id(dcn.conv_offset.weight)] = dWo
-        dY0 = (dY0f + dY0b.permute(0, 2, 3, 1).reshape(cells, 64).float()).to(torch.bfloat16)
+        dY0 = (dY0f + dY0b.permute(0, 2, 3, 1).reshape(cells, 64).float()).to(eng.dt)
         dY0 = dY0.view(B, H, W, 64).permute(0, 3, 1, 2)
-        dx, dWs, dgs, dbs, _ = db._backward_layer(db._Eng(lib, False), ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
+        dx, dWs, dgs, dbs, _ = db._backward_layer(eng, ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
         L = ctx.rsh["L"]
         grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWs, dgs, dbs
         ctx.trecs = ctx.rsh = None

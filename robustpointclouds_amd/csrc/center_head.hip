@@ -412,18 +412,23 @@ namespace rpc {
 namespace ctr {
 constexpr int PACK_NB = 256;
 
-__global__ __launch_bounds__(BLK) void k_pack(const unsigned short* __restrict__ z, int zp, int n,
+// F32: fp32 z / dz images (parity mode), else bf16
+template <bool F32>
+__global__ __launch_bounds__(BLK) void k_pack(const void* __restrict__ zv, int zp, int n,
                                               const float* __restrict__ bias, float* __restrict__ out, int op,
                                               int ooff, long long cells) {
   const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
   if (e >= cells * n) return;
   const long long p = e / n;
   const int c = (int)(e - p * n);
-  out[p * op + ooff + c] = __uint_as_float((unsigned)z[p * zp + c] << 16) + bias[c];
+  const float v = F32 ? ((const float*)zv)[p * zp + c]
+                      : __uint_as_float((unsigned)((const unsigned short*)zv)[p * zp + c] << 16);
+  out[p * op + ooff + c] = v + bias[c];
 }
 
+template <bool F32>
 __global__ __launch_bounds__(BLK) void k_unpack(const float* __restrict__ d, int dp, int doff, int n,
-                                                unsigned short* __restrict__ dz, int zp, long long cells,
+                                                void* __restrict__ dzv, int zp, long long cells,
                                                 float* __restrict__ part) {
   __shared__ float sh[BLK / 64][16];
   const long long per = (cells + gridDim.x - 1) / gridDim.x;
@@ -433,6 +438,15 @@ __global__ __launch_bounds__(BLK) void k_unpack(const float* __restrict__ d, int
   for (int c = 0; c < 16; ++c) acc[c] = 0.0f;
   for (long long p = p0 + threadIdx.x; p < p1; p += BLK) {
     for (int c = 0; c < zp; c += 8) {
+      if (F32) {
+        float v[8];
+#pragma unroll
+        for (int h = 0; h < 8; ++h) v[h] = c + h < n ? d[p * dp + doff + c + h] : 0.0f;
+        float4* o = (float4*)((float*)dzv + p * zp + c);
+        o[0] = make_float4(v[0], v[1], v[2], v[3]);
+        o[1] = make_float4(v[4], v[5], v[6], v[7]);
+        continue;
+      }
       unsigned w[4];
 #pragma unroll
       for (int h = 0; h < 4; ++h) {
@@ -442,7 +456,7 @@ __global__ __launch_bounds__(BLK) void k_unpack(const float* __restrict__ d, int
         w[h] = (unsigned)__builtin_bit_cast(unsigned short, (__bf16)a) |
                ((unsigned)__builtin_bit_cast(unsigned short, (__bf16)b) << 16);
       }
-      *(uint4*)(dz + p * zp + c) = make_uint4(w[0], w[1], w[2], w[3]);
+      *(uint4*)((unsigned short*)dzv + p * zp + c) = make_uint4(w[0], w[1], w[2], w[3]);
     }
 #pragma unroll
     for (int c = 0; c < 16; ++c)
@@ -461,32 +475,58 @@ __global__ __launch_bounds__(BLK) void k_unpack(const float* __restrict__ d, int
     part[(size_t)blockIdx.x * n + threadIdx.x] = s;
   }
 }
+static int head_pack(bool f32, const void* z, int zp, int n, const float* bias, float* out, int op, int ooff,
+                     long long cells, void* stream) {
+  if (!z || !bias || !out || n < 1 || n > 16 || zp < n || op < ooff + n || cells < 0) return RPC_ERR_ARG;
+  if (cells == 0) return RPC_OK;
+  const dim3 grid((unsigned)((cells * n + BLK - 1) / BLK));
+  if (f32)
+    hipLaunchKernelGGL(k_pack<true>, grid, dim3(BLK), 0, (hipStream_t)stream, z, zp, n, bias, out, op, ooff, cells);
+  else
+    hipLaunchKernelGGL(k_pack<false>, grid, dim3(BLK), 0, (hipStream_t)stream, z, zp, n, bias, out, op, ooff, cells);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+static int head_unpack(bool f32, const float* dout, int dp, int doff, int n, void* dz, int zp, long long cells,
+                       float* dbias, void* workspace, size_t ws_bytes, void* stream) {
+  if (!dout || !dz || !dbias || !workspace || n < 1 || n > 16 || zp < n || (zp & 7) || dp < doff + n || cells < 1)
+    return RPC_ERR_ARG;
+  if (ws_bytes < (size_t)PACK_NB * 16 * sizeof(float)) return RPC_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int nb = (int)(cells < PACK_NB * 64 ? (cells + 63) / 64 : PACK_NB);
+  if (f32)
+    hipLaunchKernelGGL(k_unpack<true>, dim3(nb), dim3(BLK), 0, st, dout, dp, doff, n, dz, zp, cells, (float*)workspace);
+  else
+    hipLaunchKernelGGL(k_unpack<false>, dim3(nb), dim3(BLK), 0, st, dout, dp, doff, n, dz, zp, cells,
+                       (float*)workspace);
+  RPC_LAUNCH_CHECK();
+  slab_reduce((const float*)workspace, nb, n, dbias, st);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
 }  // namespace ctr
 }  // namespace rpc
 
 extern "C" int rpc_head_pack(const void* z, int zp, int n, const float* bias, float* out, int op, int ooff,
                              long long cells, void* stream) {
-  if (!z || !bias || !out || n < 1 || n > 16 || zp < n || op < ooff + n || cells < 0) return RPC_ERR_ARG;
-  if (cells == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_pack, dim3((unsigned)((cells * n + BLK - 1) / BLK)), dim3(BLK), 0, (hipStream_t)stream,
-                     (const unsigned short*)z, zp, n, bias, out, op, ooff, cells);
-  RPC_LAUNCH_CHECK();
-  return RPC_OK;
+  return head_pack(false, z, zp, n, bias, out, op, ooff, cells, stream);
+}
+
+extern "C" int rpc_head_pack_f32(const float* z, int zp, int n, const float* bias, float* out, int op, int ooff,
+                                 long long cells, void* stream) {
+  return head_pack(true, z, zp, n, bias, out, op, ooff, cells, stream);
 }
 
 extern "C" size_t rpc_head_unpack_workspace_size(void) { return (size_t)PACK_NB * 16 * sizeof(float); }
 
 extern "C" int rpc_head_unpack_grad(const float* dout, int dp, int doff, int n, void* dz, int zp, long long cells,
                                     float* dbias, void* workspace, size_t ws_bytes, void* stream) {
-  if (!dout || !dz || !dbias || !workspace || n < 1 || n > 16 || zp < n || (zp & 7) || dp < doff + n || cells < 1)
-    return RPC_ERR_ARG;
-  if (ws_bytes < rpc_head_unpack_workspace_size()) return RPC_ERR_WORKSPACE;
-  hipStream_t st = (hipStream_t)stream;
-  const int nb = (int)(cells < PACK_NB * 64 ? (cells + 63) / 64 : PACK_NB);
-  hipLaunchKernelGGL(k_unpack, dim3(nb), dim3(BLK), 0, st, dout, dp, doff, n, (unsigned short*)dz, zp, cells,
-                     (float*)workspace);
-  RPC_LAUNCH_CHECK();
-  slab_reduce((const float*)workspace, nb, n, dbias, st);
-  RPC_LAUNCH_CHECK();
-  return RPC_OK;
+  return head_unpack(false, dout, dp, doff, n, dz, zp, cells, dbias, workspace, ws_bytes, stream);
+}
+
+extern "C" int rpc_head_unpack_grad_f32(const float* dout, int dp, int doff, int n, float* dz, int zp,
+                                        long long cells, float* dbias, void* workspace, size_t ws_bytes,
+                                        void* stream) {
+  return head_unpack(true, dout, dp, doff, n, dz, zp, cells, dbias, workspace, ws_bytes, stream);
 }

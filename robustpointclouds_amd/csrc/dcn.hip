@@ -480,6 +480,215 @@ __global__ __launch_bounds__(BLK) void k_wstore(const float* __restrict__ d, flo
   dW[((gq * CG + m) * CG + n) * KT + k] = d[e];
 }
 
+// ------------------------------------------------------------------ fp32 (parity mode)
+// The same semantics on fp32 images with fp32 VALU arithmetic (the 1e-4 loss parity of north_star):
+//   forward:  thread = (pixel, group) of an 8 x 8 tile; per tap the 16 sampled channels of its group
+//             (corners from global memory: the 12 x 12 window of a tile stays in L1/L2) times the
+//             group's 16 x 16 block of W_k (LDS) -> 16 fp32 outputs.
+//   backward: per tap, thread-local dcol = W_k^T dOut (its group), the offset gradient (four groups
+//             combined by xor shuffles, as in k_bwd), the input gradient added with LDS float atomics
+//             into the tile's window (-> the same per-tile slab + k_gather_dx; corners outside the
+//             window: global atomics), and dW_k's diagonal blocks from the staged col / dOut tiles.
+constexpr int PF = C + 4;        // fp32 tile pitch (floats)
+
+__device__ __forceinline__ void fetch16f(const Geo& g, int b, const float* __restrict__ x, int xp, int cy, int cx,
+                                         int q, float* v) {
+  const float4* p = (const float4*)(x + ((size_t)(b * g.H + cy) * g.W + cx) * xp + q * CG);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float4 t = p[i];
+    v[4 * i] = t.x;
+    v[4 * i + 1] = t.y;
+    v[4 * i + 2] = t.z;
+    v[4 * i + 3] = t.w;
+  }
+}
+
+__device__ __forceinline__ void sample16f(const Geo& g, int b, const float* __restrict__ x, int xp, const Samp& s,
+                                          int q, float* col) {
+#pragma unroll
+  for (int c = 0; c < CG; ++c) col[c] = 0.0f;
+  if (!s.valid) return;
+  const int cok[4] = {s.c1, s.c2, s.c3, s.c4};
+  const float wq[4] = {s.hh * s.hw, s.hh * s.lw, s.lh * s.hw, s.lh * s.lw};
+  float v[CG];
+#pragma unroll
+  for (int cn = 0; cn < 4; ++cn) {
+    if (!cok[cn]) continue;
+    fetch16f(g, b, x, xp, s.hl + (cn >> 1), s.wl + (cn & 1), q, v);
+#pragma unroll
+    for (int c = 0; c < CG; ++c) col[c] = fmaf(wq[cn], v[c], col[c]);
+  }
+}
+
+// W [64 co][16 ci][3][3] -> sW[k][group][a][b]: forward (a = ci, b = co) or backward (a = co, b = ci)
+template <bool FWD>
+__device__ __forceinline__ void stage_w(const float* __restrict__ W, float* sW) {
+  for (int e = threadIdx.x; e < C * CG * KT; e += BLK) {
+    const int co = e / (CG * KT), r = e - co * CG * KT, ci = r / KT, k = r - ci * KT;
+    const int gq = co / CG, col = co % CG;
+    sW[((k * 4 + gq) * CG + (FWD ? ci : col)) * CG + (FWD ? col : ci)] = W[e];
+  }
+}
+
+__global__ __launch_bounds__(BLK) void k_fwd_f32(Geo g, const float* __restrict__ x, int xp,
+                                                 const float* __restrict__ off, int offp,
+                                                 const float* __restrict__ ob, const float* __restrict__ W,
+                                                 float* __restrict__ out, int op) {
+  __shared__ __attribute__((aligned(16))) float sW[KT * C * CG];
+  stage_w<true>(W, sW);
+  __syncthreads();
+  const Tile tl = tile_of(g, blockIdx.x);
+  const int p = threadIdx.x >> 2, q = threadIdx.x & 3;
+  const int y = tl.y0 + (p >> 3), xx = tl.x0 + (p & 7);
+  const size_t pix = (size_t)(tl.b * g.H + y) * g.W + xx;
+  float acc[CG];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) acc[c] = 0.0f;
+#pragma unroll 1
+  for (int k = 0; k < KT; ++k) {
+    const Samp s = samp(g, y, xx, k, off[pix * offp + 2 * k] + ob[2 * k], off[pix * offp + 2 * k + 1] + ob[2 * k + 1]);
+    if (!s.valid) continue;
+    float col[CG];
+    sample16f(g, tl.b, x, xp, s, q, col);
+    const float4* wk = (const float4*)&sW[(k * 4 + q) * CG * CG];
+#pragma unroll
+    for (int ci = 0; ci < CG; ++ci)
+#pragma unroll
+      for (int c4 = 0; c4 < CG / 4; ++c4) {
+        const float4 w = wk[ci * (CG / 4) + c4];
+        acc[4 * c4] = fmaf(w.x, col[ci], acc[4 * c4]);
+        acc[4 * c4 + 1] = fmaf(w.y, col[ci], acc[4 * c4 + 1]);
+        acc[4 * c4 + 2] = fmaf(w.z, col[ci], acc[4 * c4 + 2]);
+        acc[4 * c4 + 3] = fmaf(w.w, col[ci], acc[4 * c4 + 3]);
+      }
+  }
+  float4* o = (float4*)(out + pix * op + q * CG);
+#pragma unroll
+  for (int c4 = 0; c4 < CG / 4; ++c4) o[c4] = make_float4(acc[4 * c4], acc[4 * c4 + 1], acc[4 * c4 + 2], acc[4 * c4 + 3]);
+}
+
+__global__ __launch_bounds__(BLK) void k_bwd_f32(Geo g, const float* __restrict__ x, int xp,
+                                                 const float* __restrict__ off, int offp,
+                                                 const float* __restrict__ ob, const float* __restrict__ W,
+                                                 const float* __restrict__ dout, int dop, float* __restrict__ dx,
+                                                 float* __restrict__ doff, int doffp, float* __restrict__ pw_part,
+                                                 float* __restrict__ pb_part, float* __restrict__ win_part) {
+  __shared__ __attribute__((aligned(16))) float sW[KT * C * CG];     // [k][group][co][ci]
+  __shared__ __attribute__((aligned(16))) float sWin[WR * C];        // window input gradient
+  __shared__ __attribute__((aligned(16))) float sC[64 * PF];         // col of the current tap
+  __shared__ __attribute__((aligned(16))) float sDo[64 * PF];        // dOut of the tile
+  __shared__ float sOff[64 * 2 * KT];
+  const int tid = threadIdx.x;
+  const Tile tl = tile_of(g, blockIdx.x);
+  stage_w<false>(W, sW);
+  for (int i = tid; i < WR * C / 4; i += BLK) ((float4*)sWin)[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int qd = tid; qd < 64 * 16; qd += BLK) {
+    const int pp = qd >> 4, seg = qd & 15;
+    const size_t pix = (size_t)(tl.b * g.H + tl.y0 + (pp >> 3)) * g.W + tl.x0 + (pp & 7);
+    *(float4*)&sDo[pp * PF + seg * 4] = *(const float4*)(dout + pix * dop + seg * 4);
+  }
+  __syncthreads();
+  const int p = tid >> 2, q = tid & 3;
+  const int y = tl.y0 + (p >> 3), xx = tl.x0 + (p & 7);
+  const size_t pix = (size_t)(tl.b * g.H + y) * g.W + xx;
+  float go[CG];
+#pragma unroll
+  for (int c = 0; c < CG; ++c) go[c] = sDo[p * PF + q * CG + c];
+  // dW phase: 64 threads per group, thread = (co, 4 consecutive ci)
+  const int wq_ = tid >> 6, wr = tid & 63, wco = wr >> 2, wci = (wr & 3) * 4;
+#pragma unroll 1
+  for (int k = 0; k < KT; ++k) {
+    const Samp s = samp(g, y, xx, k, off[pix * offp + 2 * k] + ob[2 * k], off[pix * offp + 2 * k + 1] + ob[2 * k + 1]);
+    float col[CG], dc[CG];
+    sample16f(g, tl.b, x, xp, s, q, col);
+#pragma unroll
+    for (int c4 = 0; c4 < CG / 4; ++c4)
+      *(float4*)&sC[p * PF + q * CG + 4 * c4] = make_float4(col[4 * c4], col[4 * c4 + 1], col[4 * c4 + 2], col[4 * c4 + 3]);
+#pragma unroll
+    for (int c = 0; c < CG; ++c) dc[c] = 0.0f;
+    const float4* wk = (const float4*)&sW[(k * 4 + q) * CG * CG];
+#pragma unroll
+    for (int co = 0; co < CG; ++co)
+#pragma unroll
+      for (int c4 = 0; c4 < CG / 4; ++c4) {
+        const float4 w = wk[co * (CG / 4) + c4];
+        dc[4 * c4] = fmaf(w.x, go[co], dc[4 * c4]);
+        dc[4 * c4 + 1] = fmaf(w.y, go[co], dc[4 * c4 + 1]);
+        dc[4 * c4 + 2] = fmaf(w.z, go[co], dc[4 * c4 + 2]);
+        dc[4 * c4 + 3] = fmaf(w.w, go[co], dc[4 * c4 + 3]);
+      }
+    // offset gradient (mmcv get_coordinate_weight) and the input-gradient scatter
+    float gh = 0.0f, gw = 0.0f;
+    if (s.valid) {
+      const int cok[4] = {s.c1, s.c2, s.c3, s.c4};
+      const float ch[4] = {-s.hw, -s.lw, s.hw, s.lw}, cwd[4] = {-s.hh, s.hh, -s.lh, s.lh};
+      const float wq[4] = {s.hh * s.hw, s.hh * s.lw, s.lh * s.hw, s.lh * s.lw};
+#pragma unroll
+      for (int cn = 0; cn < 4; ++cn) {
+        if (!cok[cn]) continue;
+        const int cy = s.hl + (cn >> 1), cx = s.wl + (cn & 1);
+        float v[CG];
+        fetch16f(g, tl.b, x, xp, cy, cx, q, v);
+        float sv = 0.0f;
+#pragma unroll
+        for (int c = 0; c < CG; ++c) sv = fmaf(dc[c], v[c], sv);
+        gh = fmaf(ch[cn], sv, gh);
+        gw = fmaf(cwd[cn], sv, gw);
+        const int wy = cy - (tl.y0 - 2), wx = cx - (tl.x0 - 2);
+        if (wy >= 0 && wy < WE && wx >= 0 && wx < WE) {
+          float* dst = &sWin[(wy * WE + wx) * C + q * CG];
+#pragma unroll
+          for (int c = 0; c < CG; ++c) atomicAdd(&dst[c], wq[cn] * dc[c]);
+        } else {
+          float* dst = dx + ((size_t)(tl.b * g.H + cy) * g.W + cx) * C + q * CG;
+#pragma unroll
+          for (int c = 0; c < CG; ++c) atomicAdd(&dst[c], wq[cn] * dc[c]);
+        }
+      }
+    }
+    gh += __shfl_xor(gh, 1, 64);
+    gw += __shfl_xor(gw, 1, 64);
+    gh += __shfl_xor(gh, 2, 64);
+    gw += __shfl_xor(gw, 2, 64);
+    if (q == 0) {
+      sOff[p * 2 * KT + 2 * k] = gh;
+      sOff[p * 2 * KT + 2 * k + 1] = gw;
+    }
+    __syncthreads();
+    // dW_k[co][ci] of group wq_ = sum over the tile's pixels of dOut[co] * col[ci]
+    {
+      float a4[4] = {0.f, 0.f, 0.f, 0.f};
+      for (int pp = 0; pp < 64; ++pp) {
+        const float d = sDo[pp * PF + wq_ * CG + wco];
+        const float4 cv = *(const float4*)&sC[pp * PF + wq_ * CG + wci];
+        a4[0] = fmaf(d, cv.x, a4[0]);
+        a4[1] = fmaf(d, cv.y, a4[1]);
+        a4[2] = fmaf(d, cv.z, a4[2]);
+        a4[3] = fmaf(d, cv.w, a4[3]);
+      }
+      float* dst = pw_part + (((size_t)blockIdx.x * KT + k) * 4 + wq_) * 256 + wco * 16 + wci;
+      *(float4*)dst = make_float4(a4[0], a4[1], a4[2], a4[3]);
+    }
+    __syncthreads();
+  }
+  for (int qd = tid; qd < 64 * (doffp / 4); qd += BLK) {
+    const int pp = qd / (doffp / 4), seg = qd - pp * (doffp / 4);
+    const size_t px = (size_t)(tl.b * g.H + tl.y0 + (pp >> 3)) * g.W + tl.x0 + (pp & 7);
+    float v[4];
+#pragma unroll
+    for (int h = 0; h < 4; ++h) v[h] = seg * 4 + h < 2 * KT ? sOff[pp * 2 * KT + seg * 4 + h] : 0.0f;
+    *(float4*)(doff + px * doffp + seg * 4) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  if (tid < 2 * KT) {
+    float sacc = 0.0f;
+    for (int pp = 0; pp < 64; ++pp) sacc += sOff[pp * 2 * KT + tid];
+    pb_part[(size_t)blockIdx.x * 2 * KT + tid] = sacc;
+  }
+  float* wdst = win_part + (size_t)blockIdx.x * WR * C;
+  for (int i = tid; i < WR * C / 4; i += BLK) ((float4*)wdst)[i] = ((const float4*)sWin)[i];
+}
+
 static int check_geo(int B, int H, int W, Geo* g) {
   if (B < 1 || H < 1 || W < 1 || H % TE || W % TE) return 0;
   *g = Geo{B, H, W, H / TE, W / TE};
@@ -540,6 +749,46 @@ extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp
                      (const u16*)w_bwd, (const u16*)dout, dop, dx, (u16*)doff, doffp, pw, pb, win);
   RPC_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_gather_dx, dim3((unsigned)(((long long)B * H * W * C + BLK - 1) / BLK)), dim3(BLK), 0, st, g,
+                     (const float*)win, dx);
+  slab_reduce(pw, tiles, (long long)KT * 1024, dwd, st);
+  slab_reduce(pb, tiles, 2 * KT, doff_bias, st);
+  hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dcn_forward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias,
+                                   const float* W, float* out, int op, int B, int H, int Wd, void* stream) {
+  Geo g;
+  if (!check_geo(B, H, Wd, &g)) return RPC_ERR_UNSUPPORTED;
+  if (!x || !off || !off_bias || !W || !out || xp < C || (xp & 3) || offp < 2 * KT || op < C || (op & 3))
+    return RPC_ERR_ARG;
+  hipLaunchKernelGGL(k_fwd_f32, dim3(B * g.TY * g.TX), dim3(BLK), 0, (hipStream_t)stream, g, x, xp, off, offp,
+                     off_bias, W, out, op);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_dcn_backward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias,
+                                    const float* W, const float* dout, int dop, float* dx, float* doff, int doffp,
+                                    float* doff_bias, float* dW, int B, int H, int Wd, void* workspace,
+                                    size_t ws_bytes, void* stream) {
+  Geo g;
+  if (!check_geo(B, H, Wd, &g)) return RPC_ERR_UNSUPPORTED;
+  if (!x || !off || !off_bias || !W || !dout || !dx || !doff || !doff_bias || !dW || !workspace) return RPC_ERR_ARG;
+  if (xp < C || (xp & 3) || offp < 2 * KT || dop < C || (dop & 3) || doffp < 2 * KT || (doffp & 3))
+    return RPC_ERR_ARG;
+  if (ws_bytes < rpc_dcn_backward_workspace_size(B, H, Wd)) return RPC_ERR_WORKSPACE;
+  hipStream_t st = (hipStream_t)stream;
+  const int tiles = B * g.TY * g.TX;
+  float* pw = (float*)workspace;
+  float* pb = pw + (size_t)tiles * KT * 1024;
+  float* dwd = pb + (size_t)tiles * 2 * KT;
+  float* win = dwd + KT * 1024;
+  hipLaunchKernelGGL(k_bwd_f32, dim3(tiles), dim3(BLK), 0, st, g, x, xp, off, offp, off_bias, W, dout, dop, dx, doff,
+                     doffp, pw, pb, win);
+  RPC_LAUNCH_CHECK();
+  hipLaunchKernelGGL(k_gather_dx, dim3((unsigned)(((long long)B * H * Wd * C + BLK - 1) / BLK)), dim3(BLK), 0, st, g,
                      (const float*)win, dx);
   slab_reduce(pw, tiles, (long long)KT * 1024, dwd, st);
   slab_reduce(pb, tiles, 2 * KT, doff_bias, st);

@@ -133,11 +133,13 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
     // data gradient into the layer below (its ReLU mask + BatchNorm-backward partial sums)
     const int* mp = l.kind == 0 ? l.nbr : l.nbr_in;
     const int rev = l.kind == 0 ? 1 : 0;
+    const int* pin = l.perm_in;   // visiting order of the data-gradient rows (n_in)
     const int n_in = l.n_in;
     if (li > 0 && L[li - 1].mat) {
       float* din = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
       if (l.bf16)
-        CHK(rpc_spconv_gemm_bf16_n(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, nullptr, nullptr, nullptr, 2, st));
+        CHK(rpc_spconv_gemm_perm(dzb, 0, n_out, l.co, mp, l.kvol, rev, pin, n_in, l.btd, l.ci, din, nullptr, nullptr,
+                                 nullptr, 2, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, din, nullptr, st));
       G[li - 1].push_back(din);
@@ -162,14 +164,15 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
         CHK(rpc_spconv_gemm_bf16_fin(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part,
                                      1, &fin, st));
       } else if (l.bf16)
-        CHK(rpc_spconv_gemm_bf16_n(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part, 1, st));
+        CHK(rpc_spconv_gemm_perm(dzb, 0, n_out, l.co, mp, l.kvol, rev, pin, n_in, l.btd, l.ci, din, prev.z, prev.bn,
+                                 part, 1, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, prev.z, prev.bn, din, part, st));
       dy = din;
     } else if (dfeat) {
       if (l.bf16)
-        CHK(rpc_spconv_gemm_bf16_n(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, dfeat, nullptr, nullptr, nullptr, 2,
-                                 st));
+        CHK(rpc_spconv_gemm_perm(dzb, 0, n_out, l.co, mp, l.kvol, rev, pin, n_in, l.btd, l.ci, dfeat, nullptr, nullptr,
+                                 nullptr, 2, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, dfeat, nullptr,
                              st));

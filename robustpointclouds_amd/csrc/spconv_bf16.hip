@@ -91,6 +91,7 @@ struct GB {
   float* part;        // [blocks][2*NGP] or null
   RpcBnFin fin;       // BatchNorm finalize by the last-arriving blocks (fin.ticket null: off)
   int fmt;            // operand format of a and bt: 0 bf16, 1 fp16 (E_FWD only)
+  const int* perm;    // row visiting order [Nout] (rpc_rulebook_mask_perm) or null; rows are written in place
 };
 
 // ---- BatchNorm finalize fused into the GEMM (k_gemm_pipe, RpcBnFin): the partial rows every block writes
@@ -189,6 +190,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
   __shared__ int klist[MAXK];
   __shared__ int nk;
   __shared__ float sP[GW][2 * NGP];
+  __shared__ int sRow[GBM];   // physical row of each logical row (the visiting order; -1 past Nout)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // XCD-aware row blocks: each XCD takes one contiguous eighth of the (spatially sorted) rows, so the
   // neighbour rows its blocks gather — mostly within a few thousand rows — stay in that XCD's L2
@@ -206,7 +208,9 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     constexpr int NP = (MAXK + 3) / 4;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      const int lr = w * WR + rt * 16 + rr, row = r0 + lr;
+      const int lr = w * WR + rt * 16 + rr, lrow = r0 + lr;
+      const int row = lrow < g.Nout ? (g.perm ? g.perm[lrow] : lrow) : g.Nout;
+      if (k4 == 0) sRow[lr] = row < g.Nout ? row : -1;
       int nv[NP];
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
@@ -342,9 +346,14 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
   float s1[NT], s2[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) s1[n] = s2[n] = 0.0f;
+  // (rows in visiting order: lane rows lr .. lr + 3 of the block, physical rows from sRow)
+  int prow[RT][4];
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) prow[rt][j] = sRow[w * WR + rt * 16 + (lane >> 4) * 4 + j];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
-    const int rb = r0 + w * WR + rt * 16 + (lane >> 4) * 4;
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       int col = n * 16 + (lane & 15);
@@ -354,13 +363,13 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
 #pragma unroll
         for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];   // scale, beta, mean, invstd
 #pragma unroll
-        for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)min(rb + j, g.Nout - 1) * C + cc];
+        for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)max(prow[rt][j], 0) * C + cc];
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        int row = rb + j;
+        int row = prow[rt][j];
         float v = acc[rt][n][j];
-        if (row < g.Nout && col < g.CO_real) {
+        if (row >= 0 && col < g.CO_real) {
           if (EPI == E_DGRAD) {
             const float zz = zr[j];
             float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
@@ -1093,7 +1102,7 @@ static int launch(int KGP, int NT, int epi, const GB& a, int n_rows, hipStream_t
 #undef DB
     return RPC_ERR_ARG;
   }
-  if (mode >= 4 || a.fmt) mode = 0;   // (the ring variants are bf16 only)
+  if (mode >= 4 || a.fmt || a.perm) mode = 0;   // (the ring variants: bf16, natural row order only)
   C2(32, 1) C2(32, 2) C2(32, 4) C2H(64, 2) C2(64, 4) C2(64, 8) C2W(128, 4, 4) C2(32, 8) C2H(64, 1) C2W(128, 2, 4)
   C2W(128, 8, 3)
 #undef C2H
@@ -1242,6 +1251,17 @@ extern "C" int rpc_spconv_gemm_h16(const void* a, int fmt, int n_src, int kg, co
   GB g;
   memset(&g, 0, sizeof(g));
   g.fmt = fmt;
+  return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
+}
+
+// the general form: operand format fmt (fp16: forward only) and rows visited in the order perm (may be NULL)
+extern "C" int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
+                                    const int* perm, int n_out, const void* bt, int ng, float* out,
+                                    const float* prev_z, const float* prev_bn, float* part, int epi, void* stream) {
+  GB g;
+  memset(&g, 0, sizeof(g));
+  g.fmt = fmt;
+  g.perm = perm;
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 

@@ -64,6 +64,9 @@ FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "0") != "0"
 # tests/test_gpu_sparse_layers.py). fp16 MFMA runs at the bf16 rate; the normalised activations and the
 # weights sit far inside its range (the dz rows, which would need loss scaling in fp16, stay bf16)
 FWD_FMT = 0 if os.environ.get("RPC_SPARSE_FWD_BF16", "0") != "0" else 1
+# 16-bit GEMMs visit each map's rows in neighbour-mask order (rpc_rulebook_mask_perm, built with the rulebooks
+# on their side stream); 0: index order (A/B)
+MASK_PERM = os.environ.get("RPC_SPARSE_PERM", "1") != "0"
 
 
 def _t3(v):
@@ -475,11 +478,24 @@ class _RulebookPlan:
                     _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, _ffi.int_arr(sp.ksize),
                                                      _ffi.ptr(enc.grid(sp.lvl_in, B, dev)), _ffi.ptr(nbr), st),
                                "rpc_subm_rulebook")
-                    self.rb[sp.key] = nbr
-                    made.append(nbr)
-                self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=self.rb[sp.key], n_out=cur_n,
-                                    coors_out=cur_coors), made)
+                    perm = self._perm(nbr, st)
+                    self.rb[sp.key] = (nbr, perm)
+                    made += [t for t in (nbr, perm) if t is not None]
+                nbr, perm = self.rb[sp.key]
+                # (a submanifold map's transpose has the reversed masks: one order serves both directions)
+                self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr, n_out=cur_n, coors_out=cur_coors,
+                                    perm=perm, perm_in=perm), made)
                 self.next += 1
+
+    def _perm(self, nbr, st):
+        """Visiting order of a map's rows by neighbour mask (on the side stream), or None (perf-mode GEMMs
+        only; RPC_SPARSE_PERM=0)."""
+        if not (MASK_PERM and self.enc.bf16) or nbr.shape[0] == 0:
+            return None
+        perm = torch.empty(nbr.shape[0], dtype=torch.int32, device=self.dev)
+        _ffi.check(self.lib.rpc_rulebook_mask_perm(_ffi.ptr(nbr), nbr.shape[0], nbr.shape[1], _ffi.ptr(perm), st),
+                   "rpc_rulebook_mask_perm")
+        return perm
 
     def get(self, li):
         if self.plan[li] is None:
@@ -501,8 +517,10 @@ class _RulebookPlan:
                                                          _ffi.int_arr(sp.pad), _ffi.ptr(gout), n_out,
                                                          _ffi.ptr(coors_out), _ffi.ptr(nbr_out), _ffi.ptr(nbr_in),
                                                          _ffi.ptr(ws), st), "rpc_spconv_rulebook_build")
+                perm_out, perm_in = self._perm(nbr_out, st), self._perm(nbr_in, st)
             self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr_out, nbr_in=nbr_in, n_out=n_out,
-                                coors_out=coors_out), [coors_out, nbr_out, nbr_in])
+                                coors_out=coors_out, perm=perm_out, perm_in=perm_in),
+                       [t for t in (coors_out, nbr_out, nbr_in, perm_out, perm_in) if t is not None])
             self.pending = None
             self.cur = (coors_out, n_out)
             self.next = li + 1
@@ -548,7 +566,7 @@ class SparseEncoderFn(torch.autograd.Function):
             bnm = m[1]
             p = plan.get(li)
             rec = dict(spec=sp, n_in=p["n_in"], src=src, src_bn=src_bn, coors_in=p["coors_in"], nbr=p["nbr"],
-                       n_out=p["n_out"], coors_out=p["coors_out"])
+                       n_out=p["n_out"], coors_out=p["coors_out"], perm=p.get("perm"), perm_in=p.get("perm_in"))
             if "nbr_in" in p:
                 rec["nbr_in"] = p["nbr_in"]
             main.wait_event(p["ev"])
@@ -578,9 +596,10 @@ class SparseEncoderFn(torch.autograd.Function):
                                "rpc_spconv_gemm_bf16_fin")
                     fused = True
                 else:
-                    _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
-                                                       sp.K, 0, n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None,
-                                                       _ffi.ptr(part), 0, st), "rpc_spconv_gemm_h16")
+                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
+                                                        sp.K, 0, _ffi.ptr(rec["perm"]), n_out, _ffi.ptr(bt), sp.co,
+                                                        _ffi.ptr(z), None, None, _ffi.ptr(part), 0, st),
+                               "rpc_spconv_gemm_perm")
             else:
                 e0 = enc.timer.start() if tm else None
                 _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
@@ -776,7 +795,7 @@ class SparseEncoderFn(torch.autograd.Function):
             if li > 0 and L[li - 1]["spec"].mat:
                 # the input is a materialised output: plain data gradient, masked by its own backward
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _ffi.ptr(rec["perm_in"]), n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
                                "rpc_spconv_gemm_bf16(dgrad)")
                 else:
@@ -791,7 +810,7 @@ class SparseEncoderFn(torch.autograd.Function):
                 td = timer is not None and timer.wants("dgrad", sp)
                 if rec["bf16"]:
                     e0 = timer.start() if td else None
-                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _ffi.ptr(rec["perm_in"]), n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), _ffi.ptr(prev["z"]),
                                                         _ffi.ptr(prev["bn"]), _ffi.ptr(part), 1, st),
                                "rpc_spconv_gemm_bf16(dgrad)")
@@ -808,7 +827,7 @@ class SparseEncoderFn(torch.autograd.Function):
                 dy = din
             elif ctx.needs_input_grad[0]:
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _ffi.ptr(rec["perm_in"]), n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
                                "rpc_spconv_gemm_bf16(dgrad)")
                 else:
@@ -866,6 +885,7 @@ def _native_backward(ctx, gdense):
             vp(rec["h_in"]) if bf else None, None if bf else vp(rec["src"]), None if bf else vp(rec["src_bn"]),
             vp(rec["W"]), vp(rec["gamma"]), vp(rec["beta"]), vp(rec.get("btd")) if bf else None,
             dW.data_ptr(), dg.data_ptr(), db.data_ptr(), int(rec.get("h_fmt", 0)),
+            vp(rec.get("perm")) if bf else None, vp(rec.get("perm_in")) if bf else None,
             ctx.enc.fin_ticket_ptr(dev, nl + li, rec["n_in"]) if bf and FUSED_FINALIZE else None)
     dfeat = (torch.empty((L[0]["n_in"], L[0]["spec"].ci), dtype=torch.float32, device=dev)
              if ctx.needs_input_grad[0] else None)

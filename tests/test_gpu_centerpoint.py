@@ -24,10 +24,13 @@ def _batch(B, seed, sweeps=3):
     return pts, dict(gt_boxes=gb, gt_labels=gl)
 
 
-def test_adversarial_centerpoint_steps():
+@pytest.mark.parametrize("bf16", [True, False])
+def test_adversarial_centerpoint_steps(bf16):
+    """bf16 perf mode and the fp32 parity mode (fp32 perturber, 128-wide fp32 sparse convs, fp32 dense
+    engine, fp32 DCN and head images)."""
     torch.manual_seed(0)
     model = make_nus_model(device=DEV, epoch=3)
-    tr = Trainer(model, bf16=True, device=DEV)
+    tr = Trainer(model, bf16=bf16, device=DEV)
     before = {k: v.detach().clone() for k, v in model.named_parameters()}
     pts, gt = _batch(2, 0)
     logs = [tr.train_step(pts, gt) for _ in range(3)]

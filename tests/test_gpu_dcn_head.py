@@ -6,7 +6,11 @@ input, offsets and weights; the kernel samples in fp32 and multiplies bf16 colum
 so agreement is bf16-level: forward relative L2 <= 1e-2, gradients (input, offsets, offset bias,
 weights) relative L2 <= 2e-2. Head: the same layer stack in float64 torch (conv / BatchNorm (batch
 statistics) / ReLU / oracle DCN), outputs relative L2 <= 3e-2 and gradient directions (cosine)
->= 0.98 — the head runs in bf16 activations. Parity w.r.t. mmcv / mmdet3d is unpinned (not vendored)."""
+>= 0.98 — the head runs in bf16 activations. Parity mode (fp32 neck image -> fp32 dense engine, fp32
+DCN rpc_dcn_*_f32, fp32 head images): DCN forward relative L2 <= 1e-5 and gradients <= 1e-4 against the
+float64 oracle on the same fp32 values; the whole head's outputs <= 1e-4, input gradient <= 1e-3 and every
+parameter gradient <= 5e-3 (BatchNorm-backward cancellation). Parity w.r.t. mmcv / mmdet3d is unpinned
+(not vendored)."""
 import pytest
 import torch
 import torch.nn.functional as Fn
@@ -26,6 +30,49 @@ def _bf(t):
 
 def _rel(a, b):
     return ((a - b).norm() / b.norm().clamp_min(1e-30)).item()
+
+
+@pytest.mark.parametrize("B,H,W,amp", [(2, 16, 24, 0.8), (1, 8, 8, 2.5), (1, 16, 16, 6.0)])
+def test_dcn_forward_backward_f32(B, H, W, amp):
+    """fp32 parity-mode DCN (large offsets in the last case: most corners leave the tile window)."""
+    g = torch.Generator().manual_seed(int(amp * 10) + H + 1)
+    x = torch.randn(B, 64, H, W, generator=g).double()
+    offz = torch.randn(B, 64, H, W, generator=g).double() * amp
+    offz[:, 18:] = 0
+    ob = torch.randn(18, generator=g).double() * 0.3
+    Wt = torch.randn(64, 16, 3, 3, generator=g).double() * 0.1
+    gout = torch.randn(B, 64, H, W, generator=g).double()
+    x, offz, ob, Wt, gout = (t.float().double() for t in (x, offz, ob, Wt, gout))
+    lib = _ffi.load()
+    st = _ffi.stream_of(torch.empty(1, device=DEV))
+    xi = db._nhwc(x.to(DEV), torch.float32)
+    oi = db._nhwc(offz.to(DEV), torch.float32)
+    obd = ob.float().to(DEV)
+    W32 = Wt.float().to(DEV).contiguous()
+    out = db._image(B, 64, H, W, DEV, torch.float32)
+    _ffi.check(lib.rpc_dcn_forward_f32(_ffi.ptr(xi), 64, _ffi.ptr(oi), 64, _ffi.ptr(obd), _ffi.ptr(W32),
+                                       _ffi.ptr(out), 64, B, H, W, st), "fwd")
+    gi = db._nhwc(gout.to(DEV), torch.float32)
+    dx = torch.zeros((B * H * W, 64), dtype=torch.float32, device=DEV)
+    doff = db._image(B, 64, H, W, DEV, torch.float32)
+    dob = torch.empty(18, device=DEV)
+    dW = torch.empty((64, 16, 3, 3), device=DEV)
+    wsz = lib.rpc_dcn_backward_workspace_size(B, H, W)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    _ffi.check(lib.rpc_dcn_backward_f32(_ffi.ptr(xi), 64, _ffi.ptr(oi), 64, _ffi.ptr(obd), _ffi.ptr(W32),
+                                        _ffi.ptr(gi), 64, _ffi.ptr(dx), _ffi.ptr(doff), 64, _ffi.ptr(dob),
+                                        _ffi.ptr(dW), B, H, W, _ffi.ptr(ws), wsz, st), "bwd")
+    xr = x.clone().requires_grad_(True)
+    offr = (offz[:, :18] + ob.view(1, 18, 1, 1)).clone().requires_grad_(True)
+    Wr = Wt.clone().requires_grad_(True)
+    ref = deform_conv2d(xr, offr, Wr, groups=4)
+    (ref * gout).sum().backward()
+    assert _rel(out.cpu().double(), ref.detach()) <= 1e-5
+    assert _rel(dx.view(B, H, W, 64).permute(0, 3, 1, 2).cpu().double(), xr.grad) <= 1e-4
+    assert _rel(doff.cpu().double()[:, :18], offr.grad) <= 1e-4
+    assert float(doff[:, 18:].abs().max()) == 0.0
+    assert _rel(dob.cpu().double(), offr.grad.sum((0, 2, 3))) <= 1e-4
+    assert _rel(dW.cpu().double(), Wr.grad) <= 1e-4
 
 
 @pytest.mark.parametrize("B,H,W,amp", [(2, 16, 24, 0.8), (1, 8, 8, 2.5)])
@@ -103,7 +150,10 @@ def _ref_head(head, x, B, H, W):
     return torch.cat(hms, 1), torch.cat(boxes, 1), P
 
 
-def test_center_head_forward_backward():
+@pytest.mark.parametrize("mode", ["bf16", "fp32"])
+def test_center_head_forward_backward(mode):
+    f32 = mode == "fp32"
+    tol_out, tol_x, cos_min = (1e-4, 1e-3, 0.99999) if f32 else (3e-2, None, 0.98)
     torch.manual_seed(0)
     B, Cin, H, W = 2, 128, 32, 32
     head = CenterHead(in_channels=Cin).to(DEV)
@@ -113,21 +163,23 @@ def test_center_head_forward_backward():
                 dcn.conv_offset.weight.normal_(0, 0.05)
                 dcn.conv_offset.bias.uniform_(-0.5, 0.5)
     x = _bf(torch.randn(B, Cin, H, W)).float()
-    xd = x.to(DEV).requires_grad_(True)
+    xd = x.to(DEV).to(torch.float32 if f32 else torch.bfloat16).requires_grad_(True)
     preds = head([xd])
     hm = torch.cat([p[0]["heatmap"] for p in preds], 1)
     box = torch.cat([torch.cat([p[0][n] for n in _BOX_ORDER], 1) for p in preds], 1)
     xr = x.double().requires_grad_(True)
     # the reference reads the module's parameters after the step's running-stat update is irrelevant
     rhm, rbox, _ = _ref_head(head, xr, B, H, W)
-    assert _rel(hm.detach().cpu().double(), rhm.detach()) <= 3e-2
-    assert _rel(box.detach().cpu().double(), rbox.detach()) <= 3e-2
+    assert _rel(hm.detach().cpu().double(), rhm.detach()) <= tol_out
+    assert _rel(box.detach().cpu().double(), rbox.detach()) <= tol_out
     g = torch.Generator().manual_seed(5)
     ghm, gbox = torch.randn(rhm.shape, generator=g).double(), torch.randn(rbox.shape, generator=g).double()
     ((hm * ghm.float().to(DEV)).sum() + (box * gbox.float().to(DEV)).sum()).backward()
     ((rhm * ghm).sum() + (rbox * gbox).sum()).backward()
     cos = lambda a, b: (a.flatten() @ b.flatten() / (a.norm() * b.norm())).item()
-    assert cos(xd.grad.cpu().double(), xr.grad) >= 0.98
+    assert cos(xd.grad.cpu().double(), xr.grad) >= cos_min
+    if f32:
+        assert _rel(xd.grad.cpu().double(), xr.grad) <= tol_x
     Pref = {}
     P = {k: v.detach().cpu().double().requires_grad_(True) for k, v in head.named_parameters()}
     # parameter gradients: recompute the reference with parameters as leaves
@@ -158,6 +210,6 @@ def test_center_head_forward_backward():
     bad = []
     for k, p in head.named_parameters():
         c = cos(p.grad.cpu().double(), P[k].grad)
-        if not c >= 0.98:
-            bad.append((k, c))
+        if not c >= cos_min or (f32 and not _rel(p.grad.cpu().double(), P[k].grad) <= 5e-3):
+            bad.append((k, c, _rel(p.grad.cpu().double(), P[k].grad)))
     assert not bad, bad

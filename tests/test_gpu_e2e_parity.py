@@ -53,6 +53,10 @@ LOSS_TOL = 1e-4
 GRAD_REL = 2e-2
 GRAD_F64_MAX = 1e-2
 GRAD_F64_MEAN = 2e-3
+# middle.11.gamma (the sparse encoder's conv_out BatchNorm scale: the last BatchNorm before the dense BEV, whose
+# gradient sums dy*xhat over all 61k output rows — the tensor the fp32 oracle itself is farthest from float64 on)
+# measured 1.005e-2 next to the fp32 oracle's 0.98e-2 in round 3; bounded by the oracle's own distance + 1e-3
+GRAD_F64_EXCEPT = {"middle.11.gamma": lambda e_ora: e_ora + 1e-3}
 
 
 class _VFE(nn.Module):            # upstream HardSimpleVFE formula (…3class.py:17)
@@ -257,8 +261,9 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
           f"fp32 oracle mean {mean_ora:.2e} max {ora_level:.2e}")
     for rel, name, cos, e_hip, e_ora in worst:
         assert rel <= GRAD_REL and cos >= 0.9998, (name, rel, cos)
-        # no farther from float64 than 1e-2, or than 1.5x the fp32 oracle's own distance where that exceeds
-        # it (the fp32 oracle reaches 1.2e-2 on the most BatchNorm-amplified tensors; a summation-order
-        # change upstream moved middle.11.gamma to 1.005e-2 next to the oracle's 0.98e-2)
-        assert e_hip <= max(GRAD_F64_MAX, 1.5 * e_ora), (name, e_hip, e_ora)
+        print(f"  {name:40s} hip vs f64 {e_hip:.3e}  fp32 oracle vs f64 {e_ora:.3e}") if e_hip > 5e-3 else None
+        # no farther from float64 than GRAD_F64_MAX — one named exception, bounded by the fp32 oracle's own
+        # distance + 1e-3 (GRAD_F64_EXCEPT)
+        bound = GRAD_F64_EXCEPT[name](e_ora) if name in GRAD_F64_EXCEPT else GRAD_F64_MAX
+        assert e_hip <= bound, (name, e_hip, e_ora, bound)
     assert mean_hip <= GRAD_F64_MEAN, (mean_hip, mean_ora)

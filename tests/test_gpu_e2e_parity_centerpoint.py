@@ -1,0 +1,279 @@
+"""BASELINE config 4's parity: one AdversarialCenterPoint training step (every loss and every parameter
+gradient) on synthetic nuScenes-like frames with fixed weights, HIP path in fp32 parity mode against the
+CPU oracle composition of the same step (the SECOND counterpart is tests/test_gpu_e2e_parity.py).
+
+HIP (one GPU):   rpc_hard_voxelize (F = 5) -> fused perturber + compaction + HardSimpleVFE -> fp32
+                 basicblock SparseEncoder (128-wide fp32 convs) -> fp32-MFMA SECOND / SECONDFPN -> fp32
+                 CenterHead (dense engine, rpc_dcn_*_f32, fp32 head images) -> rpc_center_head_loss ->
+                 AdversarialCenterPoint.loss_by_feat_single combination -> parse_losses -> backward
+Oracle (host):   oracle/voxelize_ref.c -> the SAME plugin AdversarialCenterPoint (whose combination the
+                 golden centerpoint_* fixtures pin to models/detectors/adversarial_centerpoint.py:203-257)
+                 on CPU modules: oracle perturber (float64, the explicit compaction path :77-81), the
+                 HardSimpleVFE formula, oracle SparseEncoder, torch-CPU SECOND / SECONDFPN, the CenterHead
+                 layer stack in torch with oracle/dcn.py, oracle/center_head.py targets + losses.
+
+Tolerances as in the SECOND test: voxels bit-exact; every loss key within 1e-4 * max(1, |ref|) of the
+fp32 oracle; each gradient tensor within relative L2 2e-2 (cosine >= 0.9998) of the fp32 oracle and no
+farther from the float64 oracle than GRAD_F64_MAX (or the fp32 oracle's own distance + 1e-3 where that
+is larger: BatchNorm-amplified fp32 rounding that no fp32 evaluation avoids), mean over all tensors
+<= GRAD_F64_MEAN. B = 2 one-sweep frames (~25k points, ~14k voxels each) on the config's full grid
+(41 x 1024 x 1024 -> 128 x 128 BEV): the two oracle steps (float64 ~50 s, fp32 ~15 s, dominated by the
+128 x 128 SECOND / FPN / head convolutions) fit the per-test limit on the host.
+"""
+import copy
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as Fn
+from torch import nn
+
+import robustpointclouds_amd.plugin.models  # noqa: F401
+from oracle import center_head as och
+from oracle import voxelize as ov
+from oracle.dcn import deform_conv2d
+from oracle.perturber import OraclePerturber
+from oracle.sparse_encoder import OracleSparseEncoder
+from robustpointclouds_amd.adversarial_loss import parse_losses
+from robustpointclouds_amd.center_head import _BOX_ORDER, pack_gt
+from robustpointclouds_amd.centerpoint import NUS_PC_RANGE, NUS_VOXEL_SIZE
+from robustpointclouds_amd.plugin.models.detectors.adversarial_centerpoint import AdversarialCenterPoint
+from robustpointclouds_amd.synthetic import nus_frame, nus_gt_boxes
+
+B, SWEEPS = 2, 1
+LOSS_TOL = 1e-4
+GRAD_REL = 2e-2
+GRAD_F64_MAX = 1e-2
+GRAD_F64_MEAN = 2e-3
+
+
+class _VFE(nn.Module):            # upstream HardSimpleVFE(num_features=5) formula
+    def forward(self, features, num_points, coors):
+        return features[:, :, :5].sum(dim=1) / num_points.type_as(features).view(-1, 1)
+
+
+class _Middle(nn.Module):
+    def __init__(self, enc, dtype):
+        super().__init__()
+        self.enc, self.dtype = enc, dtype
+
+    def forward(self, feats, coors, batch_size):
+        return self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size).to(self.dtype)
+
+
+class _Adversary(nn.Module):
+    def __init__(self, op):
+        super().__init__()
+        self.op = op
+
+    def forward(self, x):
+        out, ld = self.op.forward(x)
+        return out.to(x.dtype), ld
+
+
+class _CenterHead(nn.Module):
+    """The CenterHead layer stack (shared ConvModule, per task two DCNSeparateHead DeformConv2dPacks with
+    their offset convs, cls / reg ConvModule + final conv) in torch ops on a CPU copy of the module's
+    parameters, train-mode BatchNorm, oracle/dcn.py; loss_by_feat = oracle/center_head.py losses."""
+
+    def __init__(self, head, dtype):
+        super().__init__()
+        self.m = copy.deepcopy(head).cpu().to(dtype)
+        self.cfg = och.CenterCfg()
+
+    @staticmethod
+    def _cm(cm, h):
+        z = Fn.conv2d(h, cm.conv.weight, padding=1)
+        m = z.mean((0, 2, 3), keepdim=True)
+        v = z.var((0, 2, 3), unbiased=False, keepdim=True)
+        return torch.relu((z - m) / torch.sqrt(v + cm.bn.eps) * cm.bn.weight.view(1, -1, 1, 1)
+                          + cm.bn.bias.view(1, -1, 1, 1))
+
+    def forward(self, feats):
+        x = feats[0] if isinstance(feats, (list, tuple)) else feats
+        y0 = self._cm(self.m.shared_conv, x)
+        hms, boxes = [], []
+        for th in self.m.task_heads:
+            f = {}
+            for br, dcn in (("cls", th.feature_adapt_cls), ("reg", th.feature_adapt_reg)):
+                off = Fn.conv2d(y0, dcn.conv_offset.weight, dcn.conv_offset.bias, padding=1)
+                f[br] = deform_conv2d(y0, off, dcn.weight, groups=4)
+            fc = th.cls_head[1]
+            hms.append(Fn.conv2d(self._cm(th.cls_head[0], f["cls"]), fc.weight, fc.bias, padding=1))
+            parts = []
+            for name in _BOX_ORDER:
+                seq = getattr(th.task_head, name)
+                parts.append(Fn.conv2d(self._cm(seq[0], f["reg"]), seq[1].weight, seq[1].bias, padding=1))
+            boxes.append(torch.cat(parts, 1))
+        return hms, boxes
+
+    def loss_by_feat(self, outs, gts):
+        hms, boxes = outs
+        return dict(och.losses(self.cfg, hms, boxes, gts["boxes"], gts["labels"]))
+
+
+def _perturber_weights(adv):
+    lin = [m for m in adv.model if isinstance(m, nn.Linear)]
+    bns = [m for m in adv.model if isinstance(m, nn.BatchNorm1d)]
+    att = [m for m in adv.attention if isinstance(m, nn.Linear)]
+    w = {}
+    for l, m in enumerate(lin):
+        w[f"W{l}"], w[f"b{l}"] = m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()
+    for l, m in enumerate(bns):
+        w[f"g{l}"], w[f"be{l}"] = m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()
+    for l, m in enumerate(att):
+        w[f"Wa{l}"], w[f"ba{l}"] = m.weight.detach().cpu().numpy(), m.bias.detach().cpu().numpy()
+    return w, lin, bns, att
+
+
+def _rel(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a - b).norm() / b.norm().clamp_min(1e-30))
+
+
+def _cos(a, b):
+    a, b = a.double().flatten(), b.double().flatten()
+    return float((a @ b) / (a.norm() * b.norm()).clamp_min(1e-30))
+
+
+class OracleStep:
+    """The oracle composition of the step; the sparse encoder / SECOND / FPN / head stack in `dtype`, the
+    perturber restatement in float64."""
+
+    def __init__(self, model, dtype):
+        adv = model.adversary
+        self.hidden = list(adv.hidden_channels)
+        w, self.lin, self.bns, self.att = _perturber_weights(adv)
+        self.enc = OracleSparseEncoder(model.pts_middle_encoder, dtype=dtype)
+        backbone = copy.deepcopy(model.pts_backbone).cpu().to(dtype)
+        neck = copy.deepcopy(model.pts_neck).cpu().to(dtype)
+        backbone.hip = neck.hip = False
+        self.ref = AdversarialCenterPoint(
+            adversary_cfg=dict(type="VoxelPerturber", hidden_channels=self.hidden, sensor_error_bound=0.2,
+                               voxel_size=NUS_VOXEL_SIZE, use_spatial_attention=True),
+            adversarial_loss_weight=model.adversarial_loss_weight,
+            regularization_weight=model.regularization_weight, pts_voxel_encoder=_VFE(),
+            pts_middle_encoder=_Middle(self.enc, dtype), pts_backbone=backbone, pts_neck=neck,
+            pts_bbox_head=_CenterHead(model.pts_bbox_head, dtype))
+        self.op = OraclePerturber(w, 5, self.hidden, dtype=torch.float64)
+        self.ref.adversary = _Adversary(self.op)
+        self.ref.train()
+        self.ref._epoch = model._epoch
+
+    def step(self, rv, rn, rc, gts):
+        batch = dict(voxels=dict(voxels=torch.from_numpy(rv).to(self.enc.dtype), num_points=torch.from_numpy(rn),
+                                 coors=torch.from_numpy(rc)), batch_size=B)
+        self.losses = self.ref.loss(batch, gts)
+        self.total, _ = parse_losses(self.losses)
+        self.total.backward()
+
+    def grads(self):
+        g = self.op.grads()
+        out = [(f"adversary.W{l}", g[f"dW{l}"]) for l in range(len(self.lin))]
+        out += [(f"adversary.Wa{l}", g[f"dWa{l}"]) for l in range(len(self.att))]
+        out += [(f"adversary.g{l}", g[f"dg{l}"]) for l in range(len(self.bns))]
+        for i, p in enumerate(self.enc.params):
+            out += [(f"middle.{i}.W", p["W"].grad), (f"middle.{i}.gamma", p["g"].grad),
+                    (f"middle.{i}.beta", p["b"].grad)]
+        r = self.ref
+        out += [(f"backbone.{n}", p.grad) for n, p in r.pts_backbone.named_parameters()]
+        out += [(f"neck.{n}", p.grad) for n, p in r.pts_neck.named_parameters()]
+        out += [(f"head.{n}", p.grad) for n, p in r.pts_bbox_head.m.named_parameters()]
+        return out
+
+
+def hip_grads(model):
+    """(name, grad) in the order of OracleStep.grads()."""
+    adv = model.adversary
+    lin = [m for m in adv.model if isinstance(m, nn.Linear)]
+    bns = [m for m in adv.model if isinstance(m, nn.BatchNorm1d)]
+    att = [m for m in adv.attention if isinstance(m, nn.Linear)]
+    out = [(f"adversary.W{l}", m.weight.grad) for l, m in enumerate(lin)]
+    out += [(f"adversary.Wa{l}", m.weight.grad) for l, m in enumerate(att)]
+    out += [(f"adversary.g{l}", m.weight.grad) for l, m in enumerate(bns)]
+    for i, m in enumerate(model.pts_middle_encoder.layers()):
+        out += [(f"middle.{i}.W", m[0].weight.grad), (f"middle.{i}.gamma", m[1].weight.grad),
+                (f"middle.{i}.beta", m[1].bias.grad)]
+    out += [(f"backbone.{n}", p.grad) for n, p in model.pts_backbone.named_parameters()]
+    out += [(f"neck.{n}", p.grad) for n, p in model.pts_neck.named_parameters()]
+    out += [(f"head.{n}", p.grad) for n, p in model.pts_bbox_head.named_parameters()]
+    return out
+
+
+def frames(seed0=900):
+    pts = [nus_frame(seed0 + i, sweeps=SWEEPS) for i in range(B)]
+    gts = [nus_gt_boxes(seed0 + i) for i in range(B)]
+    return pts, gts
+
+
+def oracle_voxels(pts):
+    return ov.voxelize_frames(pts, NUS_VOXEL_SIZE, NUS_PC_RANGE, 10, 90000)
+
+
+@pytest.mark.gpu
+def test_adversarial_centerpoint_step_fp32_hip_matches_oracle():
+    from robustpointclouds_amd.trainer import Trainer, make_nus_model
+    dev = torch.device("cuda")
+    torch.manual_seed(21)
+    model = make_nus_model(device=dev, epoch=3)
+    with torch.no_grad():   # non-zero DCN offsets (the offset convs are zero-initialised upstream)
+        for th in model.pts_bbox_head.task_heads:
+            for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
+                dcn.conv_offset.weight.normal_(0, 0.02)
+                dcn.conv_offset.bias.uniform_(-0.5, 0.5)
+    Trainer._select_engines(model, bf16=False)
+    model.train()
+    pts, gts = frames()
+    o32 = OracleStep(model, torch.float32)
+    o64 = OracleStep(model, torch.float64)
+
+    # ---- HIP step
+    gpts = [torch.from_numpy(p).to(dev) for p in pts]
+    batch = model.data_preprocessor(dict(inputs=dict(points=gpts)), training=True)["inputs"]
+    batch["batch_size"] = B
+    gb, gl = pack_gt([torch.from_numpy(b) for b, _ in gts], [torch.from_numpy(l) for _, l in gts], dev)
+    losses = model.loss(batch, dict(gt_boxes=gb, gt_labels=gl))
+    total, _ = parse_losses(losses)
+    total.backward()
+    torch.cuda.synchronize()
+
+    # ---- voxelisation: bit-exact
+    rv, rc, rn = oracle_voxels(pts)
+    vd = batch["voxels"]
+    assert np.array_equal(vd["coors"].cpu().numpy(), rc)
+    assert np.array_equal(vd["num_points"].cpu().numpy(), rn)
+    assert np.array_equal(vd["voxels"].cpu().numpy().view(np.uint32), rv.view(np.uint32))
+
+    # ---- oracle steps
+    ogts = dict(boxes=[torch.from_numpy(b) for b, _ in gts], labels=[torch.from_numpy(l) for _, l in gts])
+    o32.step(rv, rn, rc, ogts)
+    o64.step(rv, rn, rc, ogts)
+
+    # ---- losses
+    assert set(losses) == set(o32.losses), (sorted(losses), sorted(o32.losses))
+    report = {}
+    for k, r in o32.losses.items():
+        a, r = float(losses[k].detach()), float(r.detach())
+        report[k] = (a, r)
+        assert abs(a - r) <= LOSS_TOL * max(1.0, abs(r)), (k, a, r)
+    assert abs(float(total) - float(o32.total)) <= LOSS_TOL * max(1.0, abs(float(o32.total)))
+    print("losses (hip, oracle):", report)
+
+    # ---- gradients
+    hg, g32, g64 = hip_grads(model), o32.grads(), o64.grads()
+    assert [n for n, _ in hg] == [n for n, _ in g32] == [n for n, _ in g64]
+    worst = []
+    for (name, a), (_, r), (_, r64) in zip(hg, g32, g64):
+        assert a is not None and r is not None and r64 is not None, name
+        a, r = a.cpu(), r.cpu()
+        worst.append((_rel(a, r), name, _cos(a, r), _rel(a, r64), _rel(r, r64)))
+    worst.sort(reverse=True)
+    print("worst gradient rel-L2 (vs fp32 oracle, cos, hip vs f64, fp32 oracle vs f64):", worst[:6])
+    mean_hip = sum(w[3] for w in worst) / len(worst)
+    mean_ora = sum(w[4] for w in worst) / len(worst)
+    print(f"vs float64: hip mean {mean_hip:.2e} max {max(w[3] for w in worst):.2e}; "
+          f"fp32 oracle mean {mean_ora:.2e} max {max(w[4] for w in worst):.2e}")
+    for rel, name, cos, e_hip, e_ora in worst:
+        assert rel <= GRAD_REL and cos >= 0.9998, (name, rel, cos)
+        assert e_hip <= max(GRAD_F64_MAX, e_ora + 1e-3), (name, e_hip, e_ora)
+    assert mean_hip <= GRAD_F64_MEAN, (mean_hip, mean_ora)

@@ -19,12 +19,17 @@ def _inputs(B, stride=3, seed=0):
     return feats.astype(np.float32), coors.astype(np.int32)
 
 
-@pytest.mark.parametrize("B,stride", [(2, 4), (1, 1)])
-def test_sparse_encoder_forward_backward_matches_oracle(B, stride):
+BASIC = dict(output_channels=128, encoder_channels=((16, 16, 32), (32, 32, 64), (64, 64, 128), (128, 128)),
+             encoder_paddings=((0, 0, 1), (0, 0, 1), (0, 0, [0, 1, 1]), (1, 1)), block_type="basicblock")
+
+
+@pytest.mark.parametrize("B,stride,basic", [(2, 4, False), (1, 1, False), (1, 4, True)])
+def test_sparse_encoder_forward_backward_matches_oracle(B, stride, basic):
+    """basic: the CenterPoint basicblock encoder (residual SparseBasicBlocks, 128-wide fp32 convs)."""
     torch.manual_seed(0)
     feats, coors = _inputs(B, stride)
     dev = torch.device("cuda")
-    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    enc = SparseEncoder(4, [41, 1600, 1408], **(BASIC if basic else {})).to(dev)
     with torch.no_grad():   # non-trivial BN affine params
         for m in enc.layers():
             m[1].weight.uniform_(0.5, 1.5)
@@ -166,7 +171,7 @@ def test_bf16_perf_mode_config_size():
     assert cf >= 0.95 and min(cw) >= 0.95, (cf, cw)
 
 
-@pytest.mark.parametrize("bf16,basic", [(True, False), (False, False), (True, True)])  # fp32 basicblock: 128-wide fp32 convs not built
+@pytest.mark.parametrize("bf16,basic", [(True, False), (False, False), (True, True), (False, True)])
 def test_native_backward_bit_identical_to_layer_loop(bf16, basic):
     """rpc_sparse_backward (one C++ loop, weight gradients on the side stream) issues the same kernels
     with the same arguments in the same order as the per-layer Python loop: identical bits for the

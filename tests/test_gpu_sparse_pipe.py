@@ -82,12 +82,13 @@ def _encoder_case():
     return enc, feats, d["coors"]
 
 
-def _encoder_step(enc, feats, coors, mode, fused):
+def _encoder_step(enc, feats, coors, mode, fused, perm=False):
     from robustpointclouds_amd import sparse_encoder as se
     lib = _ffi.load()
-    prev, prev_f, prev_fmt = lib.rpc_spconv_gemm_bf16_mode(mode), se.FUSED_FINALIZE, se.FWD_FMT
+    prev, prev_f, prev_fmt, prev_p = lib.rpc_spconv_gemm_bf16_mode(mode), se.FUSED_FINALIZE, se.FWD_FMT, se.MASK_PERM
     se.FUSED_FINALIZE = fused
     se.FWD_FMT = 0   # the ring kernel and the fused finalize are bf16 paths
+    se.MASK_PERM = perm
     try:
         for p in enc.parameters():
             p.grad = None
@@ -107,6 +108,7 @@ def _encoder_step(enc, feats, coors, mode, fused):
         lib.rpc_spconv_gemm_bf16_mode(prev)
         se.FUSED_FINALIZE = prev_f
         se.FWD_FMT = prev_fmt
+        se.MASK_PERM = prev_p
 
 
 def test_pipe_encoder_step_bit_identical():
@@ -195,3 +197,78 @@ def test_gemm_fin_entry_point(kg, ng, n_out, epi):
             assert torch.isfinite(x).all()
             assert torch.allclose(x, y, rtol=1e-6, atol=1e-6 * max(y.abs().max().item(), 1.0))
         assert int(ticket.abs().sum().item()) == 0
+
+
+@pytest.mark.parametrize("n,K", [(5000, 27), (2048, 27), (1, 27), (70001, 3), (4099, 27)])
+def test_mask_perm_orders_rows_by_mask(n, K):
+    """rpc_rulebook_mask_perm: a permutation of the rows that, within every window of 2048 rows, lists them by
+    neighbour mask (bit k = a neighbour at offset k), ties in row order — numpy's stable sort of the same keys."""
+    import numpy as np
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(n + K)
+    nbr = torch.randint(0, 100, (n, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n, K), generator=g) > 0.3] = -1
+    nd = nbr.to(dev)
+    perm = torch.full((n,), -7, dtype=torch.int32, device=dev)
+    _ffi.check(lib.rpc_rulebook_mask_perm(_ffi.ptr(nd), n, K, _ffi.ptr(perm), _ffi.stream_of(perm)), "mask_perm")
+    torch.cuda.synchronize()
+    got = perm.cpu().numpy()
+    mask = ((nbr.numpy() >= 0).astype(np.int64) << np.arange(K)).sum(1)
+    want = np.concatenate([s + np.argsort(mask[s:s + 2048], kind="stable") for s in range(0, n, 2048)])
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("kg,ng", [(32, 32), (64, 64), (32, 64), (64, 32), (128, 128)])
+def test_gemm_perm_writes_rows_in_place(kg, ng):
+    """rpc_spconv_gemm_perm with the mask order: every output row equal to the natural order's (each row's own
+    sums are unchanged; -0 == +0), forward / data gradient / plain; the BatchNorm partial rows sum to the same
+    column totals (another grouping of the same values)."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(kg * 5 + ng)
+    n_out, n_src, K = 9000, 6000, 27
+    nbr = torch.randint(0, n_src, (n_out, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n_out, K), generator=g) > 0.3] = -1
+    a = torch.zeros((n_src, _r8(kg)), dtype=torch.bfloat16)
+    a[:, :kg] = torch.randn((n_src, kg), generator=g).to(torch.bfloat16)
+    W = torch.randn((K, kg, ng), generator=g) * 0.1
+    a, nbr, W = a.to(dev), nbr.to(dev), W.to(dev)
+    bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(K, kg, ng, 0), dtype=torch.bfloat16, device=dev)
+    st = _ffi.stream_of(W)
+    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), K, kg, ng, 0, _ffi.ptr(bt), st), "prep")
+    perm = torch.empty(n_out, dtype=torch.int32, device=dev)
+    _ffi.check(lib.rpc_rulebook_mask_perm(_ffi.ptr(nbr), n_out, K, _ffi.ptr(perm), st), "mask_perm")
+    ez = torch.randn((n_out, ng), generator=g).to(dev)
+    ebn = torch.cat([torch.rand(ng, generator=g) + 0.5, torch.randn(ng, generator=g) * 0.1,
+                     torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
+    nblk = lib.rpc_spconv_gemm_blocks(n_out)
+    for epi in (0, 1, 2):
+        res = []
+        for pm in (None, perm):
+            out = torch.full((n_out, ng), float("nan"), device=dev)
+            part = torch.full((nblk, 2 * ng), float("nan"), device=dev) if epi != 2 else None
+            _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(a), 0, n_src, kg, _ffi.ptr(nbr), K, 0, _ffi.ptr(pm), n_out,
+                                                _ffi.ptr(bt), ng, _ffi.ptr(out), _ffi.ptr(ez), _ffi.ptr(ebn),
+                                                _ffi.ptr(part), epi, st), "gemm_perm")
+            torch.cuda.synchronize()
+            res.append((out, part))
+        assert torch.equal(res[0][0], res[1][0]), epi
+        if epi != 2:
+            t0, t1 = res[0][1].double().sum(0), res[1][1].double().sum(0)
+            assert torch.allclose(t0, t1, rtol=1e-5, atol=1e-4 * float(t0.abs().max())), epi
+
+
+def test_mask_order_encoder_step_close_and_deterministic():
+    """The bf16 encoder step with the rows of every 16-bit GEMM in mask order against index order: the same
+    step up to the BatchNorm sums' grouping (rel 1e-5 on the BEV, every gradient and the running stats), and
+    bit-identical from run to run."""
+    enc, feats, coors = _encoder_case()
+    ref = _encoder_step(enc, feats, coors, 0, False, perm=False)
+    a = _encoder_step(enc, feats, coors, 0, False, perm=True)
+    b = _encoder_step(enc, feats, coors, 0, False, perm=True)
+    for x, y in zip([a[0], a[1]] + a[2] + a[3], [b[0], b[1]] + b[2] + b[3]):
+        assert torch.equal(x, y)
+    for x, y in zip([ref[0], ref[1]] + ref[2] + ref[3], [a[0], a[1]] + a[2] + a[3]):
+        d = (x.double() - y.double()).norm() / max(y.double().norm().item(), 1e-30)
+        assert d.item() < 1e-5

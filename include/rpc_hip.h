@@ -141,6 +141,8 @@ typedef struct {
   float bn_eps;           /* 1e-3 (voxel_perturber.py:462) */
   float bn_momentum;      /* 0.1  (voxel_perturber.py:461) */
   int vfe_features;       /* fused mode: HardSimpleVFE num_features (4 KITTI) */
+  int wgrad_split_bf16;   /* perf mode: hidden-layer weight gradients on bf16 MFMA with hi/lo-split fp32
+                             operands (~2^-16 relative per product); 0 = fp32 MFMA (parity mode) */
 } rpc_perturber_cfg;
 
 size_t rpc_perturber_workspace_size(const rpc_perturber_cfg* cfg, int rows, int slots);

@@ -25,6 +25,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import torch
 from torch import nn
 
@@ -50,6 +52,11 @@ def select_engines(model: nn.Module, bf16: bool, pin: bool = False) -> None:
             mod.hip = True
         elif bf16:
             mod.to(memory_format=torch.channels_last)
+    adv = getattr(model, "adversary", None)
+    if adv is not None and hasattr(adv, "sensor_error_bound"):
+        # perf mode: the perturber's hidden-layer weight gradients on split-bf16 MFMA (perturb.make_cfg);
+        # RPC_PERT_SPLIT=0 keeps them on fp32 MFMA
+        adv.wgrad_split_bf16 = bool(bf16) and os.environ.get("RPC_PERT_SPLIT", "1") != "0"
     model.__dict__["_engine_mode"] = bool(bf16)
     if pin:
         model.__dict__["_engine_pinned"] = True

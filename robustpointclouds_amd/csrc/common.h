@@ -74,6 +74,34 @@ __device__ __forceinline__ bool last_block_arrive_2d(unsigned* ticket, int* lds_
   return *lds_flag != 0;
 }
 
+// The same hand-off without the agent-scope release / acquire fences, for producers whose hand-off data is
+// written with agent-scope atomic stores (st_agent: `global_store ... sc1`, coherent across the XCDs' L2s)
+// and read back with agent-scope atomic loads (ld_agent: `... sc1`). The release fence of
+// last_block_arrive_2d is a `buffer_wbl2`, which writes back every dirty line of the XCD's L2 — under a
+// GEMM epilogue that is the block's whole output tile, once per block; here each block only waits for its
+// own sc1 stores to complete (vmcnt(0)) before taking a ticket. Data not written with st_agent is not
+// handed off.
+__device__ __forceinline__ bool last_block_arrive_lite(unsigned* ticket, int* lds_flag, int nblocks) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int last = (t == (unsigned)nblocks - 1);
+    if (last) __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = last;
+  }
+  __syncthreads();
+  return *lds_flag != 0;
+}
+template <typename T>
+__device__ __forceinline__ void st_agent(T* p, T v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename T>
+__device__ __forceinline__ T ld_agent(const T* p) {
+  return __hip_atomic_load(const_cast<T*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Fixed-order reduction of split-K slabs: dW[e] = sum_c part[c * total + e] (c ascending within
 // each of 8 interleaved lanes, lanes combined as a fixed pairwise tree), in double. Block = 64
 // outputs x 8 lanes, each lane with 8 loads in flight -> deterministic and latency-tolerant (the

@@ -1572,6 +1572,137 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad_mf(Dev d, MfJobs J) {
   }
 }
 
+// Perf mode (cfg->wgrad_split_bf16): the same weight gradient on bf16 MFMA with each fp32 operand split
+// into hi = bf16(v) and lo = bf16(v - hi) and dW += lo_a hi_b + hi_a lo_b + hi_a hi_b (fp32 accumulate):
+// ~16 significant bits per product (relative error ~2^-16, the lo*lo term dropped) at 3 x 16-cycle
+// v_mfma_f32_16x16x32_bf16 per 32 points where the fp32 path issues 8 x 32-cycle 16x16x4 MFMAs (5.3x
+// fewer MFMA cycles). Lane (a, g) holds 8 consecutive points n0 + 8g .. of channel row 16i + a (A = dz_l
+// rows, B = h_{l-1} rows), so one k-step covers 32 points; the tile / wave / bias bookkeeping is
+// k_wgrad_mf's (same slab row, reduced by k_wgrad_reduce).
+typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split_bf16x8(const float* v, bf16x8_t& hi, bf16x8_t& lo) {
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const __bf16 h = (__bf16)v[k];
+    hi[k] = h;
+    lo[k] = (__bf16)(v[k] - (float)h);
+  }
+}
+
+template <int CO, int CI>
+__global__ __launch_bounds__(BLK, 2) void k_wgrad_bx3(Dev d, MfJobs J) {
+  // above 8 accumulator tiles the output tiles are split in two halves (along the wider of CO / CI): waves
+  // (2p + h) take half h of the tiles over the point stream p (32-point blocks, the 2 streams interleaved),
+  // so a wave holds at most 16 tiles plus its hi / lo operand splits without spilling; the operand rows of
+  // the other dimension are loaded by both halves (the second read hits L2)
+  constexpr int TO = CO / 16, TC = CI / 16;
+  static_assert(TO * TC <= 32, "accumulator tiles");
+  constexpr bool SPLIT = TO * TC > 8, SPLIT_C = SPLIT && TC >= TO, SPLIT_O = SPLIT && !SPLIT_C;
+  constexpr int TOW = SPLIT_O ? TO / 2 : TO, TCW = SPLIT_C ? TC / 2 : TC;
+  constexpr int NSTREAM = SPLIT ? NWAVE / 2 : NWAVE;
+  __shared__ float red[CO * CI];
+  __shared__ float bred[NWAVE][CO];
+  const MfJob& job = J.j[blockIdx.y];
+  const int N = d.meta[0];
+  const int rows_per = ((N + J.KS - 1) / J.KS + 31) & ~31;
+  const int r0 = blockIdx.x * rows_per, r1 = min(N, r0 + rows_per);
+  const int lane = threadIdx.x & 63, a = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
+  const int half = SPLIT ? (wv & 1) : 0, stream = SPLIT ? (wv >> 1) : wv;
+  const int o0 = SPLIT_O ? half * TOW : 0, c0 = SPLIT_C ? half * TCW : 0;   // first tile row / column
+  float sc[TCW], sh[TCW], mu[TCW];
+#pragma unroll
+  for (int jc = 0; jc < TCW; ++jc) {
+    const int c = 16 * (c0 + jc) + a;
+    sc[jc] = job.bn[c];
+    sh[jc] = job.bn[CI + c];
+    mu[jc] = job.bn[2 * CI + c];
+  }
+  f32x4 acc[TOW][TCW];
+  float bsum[TOW];
+#pragma unroll
+  for (int i = 0; i < TOW; ++i) {
+    bsum[i] = 0.0f;
+#pragma unroll
+    for (int jc = 0; jc < TCW; ++jc) acc[i][jc] = (f32x4){0.0f, 0.0f, 0.0f, 0.0f};
+  }
+  for (int n0 = r0 + 32 * stream; n0 < r1; n0 += 32 * NSTREAM) {
+    const int nb = n0 + 8 * g;
+    f32x4 dv[TOW][2], zv[TCW][2];
+#pragma unroll
+    for (int i = 0; i < TOW; ++i) {
+      const float* row = job.dz + (size_t)(16 * (o0 + i) + a) * d.S;
+      dv[i][0] = ld4(row, nb, r1);
+      dv[i][1] = ld4(row, nb + 4, r1);
+    }
+#pragma unroll
+    for (int jc = 0; jc < TCW; ++jc) {
+      const float* row = job.z + (size_t)(16 * (c0 + jc) + a) * d.S;
+      zv[jc][0] = ld4(row, nb, r1);
+      zv[jc][1] = ld4(row, nb + 4, r1);
+    }
+    bf16x8_t ah[TOW], al[TOW];
+#pragma unroll
+    for (int i = 0; i < TOW; ++i) {
+      float t[8];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        t[k] = dv[i][0][k];
+        t[4 + k] = dv[i][1][k];
+      }
+      bsum[i] += ((t[0] + t[1]) + (t[2] + t[3])) + ((t[4] + t[5]) + (t[6] + t[7]));
+      split_bf16x8(t, ah[i], al[i]);
+    }
+#pragma unroll
+    for (int jc = 0; jc < TCW; ++jc) {
+      float t[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float z = k < 4 ? zv[jc][0][k] : zv[jc][1][k - 4];
+        t[k] = nb + k < r1 ? fmaxf(fmaf(z - mu[jc], sc[jc], sh[jc]), 0.0f) : 0.0f;
+      }
+      bf16x8_t bh, bl;
+      split_bf16x8(t, bh, bl);
+#pragma unroll
+      for (int i = 0; i < TOW; ++i) {
+        acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][jc], 0, 0, 0);
+        acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][jc], 0, 0, 0);
+        acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][jc], 0, 0, 0);
+      }
+    }
+  }
+  // streams summed in order per tile (the two halves own disjoint tiles)
+  for (int s = 0; s < NSTREAM; ++s) {
+    if (stream == s) {
+#pragma unroll
+      for (int i = 0; i < TOW; ++i)
+#pragma unroll
+        for (int jc = 0; jc < TCW; ++jc)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            float* e = &red[(16 * (o0 + i) + 4 * g + r) * CI + 16 * (c0 + jc) + a];
+            *e = s == 0 ? acc[i][jc][r] : *e + acc[i][jc][r];
+          }
+    }
+    __syncthreads();
+  }
+  // bias sums: every stream's own rows (with the CI split both halves summed the same rows: half 0 only)
+#pragma unroll
+  for (int i = 0; i < TOW; ++i) {
+    const float bt = grp_sum(bsum[i]);
+    if (g == 0 && !(SPLIT_C && half == 1)) bred[stream][16 * (o0 + i) + a] = bt;
+  }
+  __syncthreads();
+  float* out = d.wpart + (size_t)blockIdx.x * J.total + job.eoff;
+  for (int e = threadIdx.x; e < CO * (CI + 1); e += BLK) {
+    const int o = e / (CI + 1), c = e - o * (CI + 1);
+    float b = 0.0f;
+    if (c == CI)
+      for (int s2 = 0; s2 < NSTREAM; ++s2) b += bred[s2][o];
+    out[e] = c < CI ? red[o * CI + c] : b;
+  }
+}
+
 // ------------------------------------------------------------------ host side
 static inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 // channel stride of the SoA activation buffers: whole 64-point MFMA groups, 16-byte aligned rows
@@ -1827,21 +1958,25 @@ static int launch_mid(int CI, int CO, Dev& d, int l, hipStream_t st, bool bwd, i
 }
 static bool wgrad_mf_ok(int CO, int CI) { return CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192; }
 template <int CO, int CI>
-static void launch_wgrad_mf_t(Dev& d, const MfJobs& M, int njob, hipStream_t st) {
-  if constexpr (CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192)
-    hipLaunchKernelGGL((k_wgrad_mf<CO, CI>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M);
+static void launch_wgrad_mf_t(Dev& d, const MfJobs& M, int njob, bool split, hipStream_t st) {
+  if constexpr (CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192) {
+    if (split)
+      hipLaunchKernelGGL((k_wgrad_bx3<CO, CI>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M);
+    else
+      hipLaunchKernelGGL((k_wgrad_mf<CO, CI>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M);
+  }
 }
 template <int CO>
-static void launch_wgrad_mf_ci(int CI, Dev& d, const MfJobs& M, int njob, hipStream_t st) {
+static void launch_wgrad_mf_ci(int CI, Dev& d, const MfJobs& M, int njob, bool split, hipStream_t st) {
   switch (CI) {
-#define CASE(c) case c: launch_wgrad_mf_t<CO, c>(d, M, njob, st); break;
+#define CASE(c) case c: launch_wgrad_mf_t<CO, c>(d, M, njob, split, st); break;
     RPC_HID(CASE)
 #undef CASE
   }
 }
-static void launch_wgrad_mf(int CO, int CI, Dev& d, const MfJobs& M, int njob, hipStream_t st) {
+static void launch_wgrad_mf(int CO, int CI, Dev& d, const MfJobs& M, int njob, bool split, hipStream_t st) {
   switch (CO) {
-#define CASE(c) case c: launch_wgrad_mf_ci<c>(CI, d, M, njob, st); break;
+#define CASE(c) case c: launch_wgrad_mf_ci<c>(CI, d, M, njob, split, st); break;
     RPC_HID(CASE)
 #undef CASE
   }
@@ -2031,7 +2166,7 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
         M.j[nm++] = MfJob{d.dz[k], d.z[k - 1], d.bn[k - 1], J.j[k].eoff};
     M.total = J.total;
     M.KS = ks;
-    launch_wgrad_mf(d.C[l + 1], d.C[l], d, M, nm, st);
+    launch_wgrad_mf(d.C[l + 1], d.C[l], d, M, nm, cfg->wgrad_split_bf16 != 0, st);
     RPC_LAUNCH_CHECK();
   }
   for (int l = 0; l < 5; ++l) {

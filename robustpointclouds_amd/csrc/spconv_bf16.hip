@@ -103,6 +103,8 @@ struct GB {
 constexpr int FGS = 32;
 __host__ __device__ inline int fin_groups(int nblk) { return (nblk + FGS - 1) / FGS; }
 
+// hand-off data (partial rows, group totals) written with agent-scope atomic stores and read with agent-scope
+// atomic loads: the blocks' arrivals need no L2 writeback (last_block_arrive_lite)
 template <int NTHR>
 __device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int* flag) {
   const RpcBnFin& f = g.fin;
@@ -110,7 +112,7 @@ __device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int*
   const int nblk = (int)gridDim.x, ng = fin_groups(nblk), q = lb / FGS;
   const int nrow = (g.Nout + BM - 1) / BM;
   const int gb0 = q * FGS, gbn = min(FGS, nblk - gb0);
-  if (!last_block_arrive_2d(f.ticket + 1 + q, flag, gbn)) return;
+  if (!last_block_arrive_lite(f.ticket + 1 + q, flag, gbn)) return;
   {
     const int pr0 = gb0 * PRB, pr1 = min(nrow, (gb0 + gbn) * PRB);
     for (int j = threadIdx.x; j < C2; j += NTHR) {
@@ -119,26 +121,26 @@ __device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int*
       for (; r + 8 <= pr1; r += 8) {
         float v[8];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = g.part[(long long)(r + i) * C2 + j];
+        for (int i = 0; i < 8; ++i) v[i] = ld_agent(&g.part[(long long)(r + i) * C2 + j]);
 #pragma unroll
         for (int i = 0; i < 8; ++i) t += (double)v[i];
       }
-      for (; r < pr1; ++r) t += (double)g.part[(long long)r * C2 + j];
-      f.gpart[(long long)q * C2 + j] = t;
+      for (; r < pr1; ++r) t += (double)ld_agent(&g.part[(long long)r * C2 + j]);
+      st_agent(&f.gpart[(long long)q * C2 + j], t);
     }
   }
-  if (!last_block_arrive_2d(f.ticket, flag, ng)) return;
+  if (!last_block_arrive_lite(f.ticket, flag, ng)) return;
   for (int j = threadIdx.x; j < C2; j += NTHR) {
     double t = 0.0;
     int r = 0;
     for (; r + 8 <= ng; r += 8) {
       double v[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = f.gpart[(long long)(r + i) * C2 + j];
+      for (int i = 0; i < 8; ++i) v[i] = ld_agent(&f.gpart[(long long)(r + i) * C2 + j]);
 #pragma unroll
       for (int i = 0; i < 8; ++i) t += v[i];
     }
-    for (; r < ng; ++r) t += f.gpart[(long long)r * C2 + j];
+    for (; r < ng; ++r) t += ld_agent(&f.gpart[(long long)r * C2 + j]);
     sh[j] = t;
   }
   __syncthreads();
@@ -410,7 +412,10 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     int which = jj / C, c = jj - which * C;
     float s = 0.0f;
     for (int ww = 0; ww < WPR; ++ww) s += sP[WPR * h + ww][which * NGP + c];
-    g.part[(long long)prow * 2 * C + jj] = s;
+    if (g.fin.ticket)
+      st_agent(&g.part[(long long)prow * 2 * C + jj], s);
+    else
+      g.part[(long long)prow * 2 * C + jj] = s;
   }
   if (g.fin.ticket) {
     // the neighbour table is free: the totals (double [2C], C <= 256 -> 4 KB) and the arrival flag go there
@@ -677,7 +682,10 @@ __global__ __launch_bounds__(64 * GW, 1) void k_gemm_pipe(GB g) {
     int which = jj / C, c = jj - which * C;
     float s = 0.0f;
     for (int ww = 0; ww < WPR; ++ww) s += sP[(WPR * h + ww) * 2 * NGP + which * NGP + c];
-    g.part[(long long)prow * 2 * C + jj] = s;
+    if (g.fin.ticket)
+      st_agent(&g.part[(long long)prow * 2 * C + jj], s);
+    else
+      g.part[(long long)prow * 2 * C + jj] = s;
   }
   if (g.fin.ticket) {
     // the ring is free: the totals (double [2C], C <= 256 -> 4 KB) and the arrival flag go there

@@ -242,7 +242,8 @@ class VoxelPerturber(nn.Module):
     def _cfg(self, F, vfe_features=4):
         bn = [m for m in self.model if isinstance(m, nn.BatchNorm1d)][0]
         return _P.make_cfg(F, self._kernel_hidden, self.use_spatial_attention, self.training,
-                           self.sensor_error_bound, bn.eps, bn.momentum, vfe_features)
+                           self.sensor_error_bound, bn.eps, bn.momentum, vfe_features,
+                           getattr(self, "wgrad_split_bf16", False))
 
     def _ensure_width(self, F):
         if F != self.in_features:

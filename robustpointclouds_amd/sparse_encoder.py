@@ -64,9 +64,12 @@ FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "0") != "0"
 # tests/test_gpu_sparse_layers.py). fp16 MFMA runs at the bf16 rate; the normalised activations and the
 # weights sit far inside its range (the dz rows, which would need loss scaling in fp16, stay bf16)
 FWD_FMT = 0 if os.environ.get("RPC_SPARSE_FWD_BF16", "0") != "0" else 1
-# 16-bit GEMMs visit each map's rows in neighbour-mask order (rpc_rulebook_mask_perm, built with the rulebooks
-# on their side stream); 0: index order (A/B)
-MASK_PERM = os.environ.get("RPC_SPARSE_PERM", "1") != "0"
+# RPC_SPARSE_PERM=1: the 16-bit GEMMs visit each map's rows in neighbour-mask order (rpc_rulebook_mask_perm,
+# built with the rulebooks on their side stream). Off by default: measured on the metric's step
+# (profiles/r04_perm_ab.txt) the sorts cost 12 x 24.9 us and the GEMMs did not get faster
+# (k_gemm_bf16<64,4,1> 53.4 -> 52.9 us, <64,4,0,f16> 40.5 -> 42.4 us): they wait on the per-offset gather
+# round trip, not on the MFMA rows a mask-sorted block skips; 7.26 vs 7.39 ms/step without / with
+MASK_PERM = os.environ.get("RPC_SPARSE_PERM", "0") != "0"
 
 
 def _t3(v):

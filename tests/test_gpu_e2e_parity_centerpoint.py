@@ -268,7 +268,9 @@ def test_adversarial_centerpoint_step_fp32_hip_matches_oracle():
         a, r = a.cpu(), r.cpu()
         worst.append((_rel(a, r), name, _cos(a, r), _rel(a, r64), _rel(r, r64)))
     worst.sort(reverse=True)
-    print("worst gradient rel-L2 (vs fp32 oracle, cos, hip vs f64, fp32 oracle vs f64):", worst[:6])
+    print("gradient rel-L2 (vs fp32 oracle, cos, hip vs f64, fp32 oracle vs f64), worst first:")
+    for w in worst:
+        print(f"  {w[1]:48s} {w[0]:.3e} {w[2]:.6f} {w[3]:.3e} {w[4]:.3e}")
     mean_hip = sum(w[3] for w in worst) / len(worst)
     mean_ora = sum(w[4] for w in worst) / len(worst)
     print(f"vs float64: hip mean {mean_hip:.2e} max {max(w[3] for w in worst):.2e}; "

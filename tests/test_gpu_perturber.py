@@ -87,40 +87,43 @@ def test_standalone_matches_reference_golden(tag):
 
 def _voxels(seed, V, x_pool):
     rng = np.random.default_rng(seed)
-    vox = np.zeros((V, 5, 4), np.float32)
+    F = x_pool.shape[1]
+    vox = np.zeros((V, 5, F), np.float32)
     npts = rng.choice([1, 1, 1, 1, 2, 2, 3, 4, 5], V).astype(np.int32)
     for v in range(V):
         vox[v, :npts[v]] = x_pool[rng.integers(0, len(x_pool), npts[v])]
-    vox[5, 0] = [1.0, -1.0, 0.0, 0.0]     # real point with zero feature sum (reference: padding)
+    vox[5, 0] = [1.0, -1.0] + [0.0] * (F - 2)     # real point with zero feature sum (reference: padding)
     return vox, npts
 
 
-@pytest.mark.parametrize("tag,V", [("car_small", 3000), ("3class", 1500), ("car_small", 70000)])
+@pytest.mark.parametrize("tag,V", [("car_small", 3000), ("3class", 1500), ("car_small", 70000), ("nus", 3000)])
 def test_fused_voxels_vfe_matches_oracle(tag, V):
+    """nus: F = 5 (x, y, z, intensity, time lag) with HardSimpleVFE(num_features=5), CenterPoint's path."""
     d = _load(tag)
     hidden = [int(h) for h in d["hidden"]]
+    F = d["x"].shape[1]
     dev = torch.device("cuda")
     vox, npts = _voxels(1, V, d["x"])
-    ps = _params(d, 4, hidden, dev)
+    ps = _params(d, F, hidden, dev)
     for p in ps:
         if p is not None:
             p.requires_grad_(True)
     for l in range(5):
         ps[6 * l + 4].requires_grad_(False)
         ps[6 * l + 5].requires_grad_(False)
-    cfg = P.make_cfg(4, hidden, True, True, 0.2, vfe_features=4)
+    cfg = P.make_cfg(F, hidden, True, True, 0.2, vfe_features=F)
     vt, nt = torch.from_numpy(vox).to(dev), torch.from_numpy(npts).to(dev)
     vfe, lvec, pert, flags = P.PerturbVoxelsFn.apply(vt, nt, cfg, *ps)
-    op = OraclePerturber(d, 4, hidden, dtype=torch.float64)
-    rvfe, rpert, rld = perturb_voxels(op, vox, npts)
+    op = OraclePerturber(d, F, hidden, dtype=torch.float64)
+    rvfe, rpert, rld = perturb_voxels(op, vox, npts, vfe_features=F)
     np.testing.assert_allclose(pert.cpu().numpy(), rpert.detach().numpy(), rtol=0, atol=TOL)
     np.testing.assert_allclose(vfe.detach().cpu().numpy(), rvfe.detach().numpy(), rtol=0, atol=TOL)
     ref = torch.stack([rld[k] for k in ["l2_norm", "intensity_loss", "bias_loss", "imbalance_loss"]])
     np.testing.assert_allclose(lvec.detach().cpu().numpy(), ref.detach().numpy(), rtol=TOL, atol=1e-6)
-    assert int(flags[4].item()) == int((vox.reshape(-1, 4).sum(1) != 0).sum())
+    assert int(flags[4].item()) == int((vox.reshape(-1, F).sum(1) != 0).sum())
     # backward through the fused VFE
     rng = np.random.default_rng(2)
-    Gv = rng.standard_normal((V, 4)).astype(np.float32) * 1e-3
+    Gv = rng.standard_normal((V, F)).astype(np.float32) * 1e-3
     cl = np.array([1e-3, -2e-3, 3e-3, 1e-3], np.float32)
     ((vfe * torch.from_numpy(Gv).to(dev)).sum() + (lvec * torch.from_numpy(cl).to(dev)).sum()).backward()
     rloss = (rvfe * torch.from_numpy(Gv.astype(np.float64))).sum() + (ref * torch.from_numpy(cl.astype(np.float64))).sum()
@@ -230,3 +233,39 @@ def test_plugin_arbitrary_widths_match_oracle(hidden):
     for l, m in enumerate(bns):
         np.testing.assert_allclose(m.running_mean.cpu().numpy(), op.rm[l].numpy(), rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(m.running_var.cpu().numpy(), op.rv[l].numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_wgrad_split_bf16_close_to_fp32():
+    """Perf mode's hidden-layer weight gradients on split-bf16 MFMA (hi/lo operands, k_wgrad_bx3) against
+    the fp32-MFMA path on the same step (metric widths [64, 128, 64], 60k points): every gradient within
+    relative L2 1e-4 (the dropped lo*lo term and bf16 hi/lo rounding: ~2^-16 per product); the other
+    gradients, the forward and the loss terms unchanged bit for bit."""
+    from robustpointclouds_amd.plugin.models.adversarial.voxel_perturber import VoxelPerturber
+    dev = torch.device("cuda")
+    torch.manual_seed(7)
+    vp = VoxelPerturber(hidden_channels=[64, 128, 64]).to(dev).train()
+    g = torch.Generator().manual_seed(8)
+    x = (torch.randn(60000, 4, generator=g) * torch.tensor([20.0, 20.0, 1.0, 0.3])).to(dev)
+    G = (torch.randn(60000, 4, generator=g) * 1e-4).to(dev)
+    res = {}
+    for split in (False, True):
+        vp.wgrad_split_bf16 = split
+        vp.zero_grad(set_to_none=True)
+        out, ld = vp(x)
+        ((out * G).sum() + 1e-3 * ld["l2_norm"]).backward()
+        torch.cuda.synchronize()
+        res[split] = (out.detach().clone(), {n: p.grad.detach().clone() for n, p in vp.named_parameters()})
+    assert torch.equal(res[False][0], res[True][0])
+    lin = [n for n, m in vp.model.named_children() if isinstance(m, torch.nn.Linear)]
+    mf = {f"model.{lin[l]}.weight" for l in range(1, 5)}
+    # their biases feed train-mode BatchNorm: exact gradient 0, both paths give summation noise
+    noise = {f"model.{lin[l]}.bias" for l in range(1, 5)}
+    for n, a in res[False][1].items():
+        b = res[True][1][n]
+        if n in noise:
+            continue
+        if n in mf:
+            rel = float((b - a).norm() / a.norm().clamp_min(1e-30))
+            assert rel <= 1e-4, (n, rel)
+        else:
+            assert torch.equal(a, b), n

@@ -23,13 +23,16 @@ BASIC = dict(output_channels=128, encoder_channels=((16, 16, 32), (32, 32, 64), 
              encoder_paddings=((0, 0, 1), (0, 0, 1), (0, 0, [0, 1, 1]), (1, 1)), block_type="basicblock")
 
 
-@pytest.mark.parametrize("B,stride,basic", [(2, 4, False), (1, 1, False), (1, 4, True)])
+@pytest.mark.parametrize("B,stride,basic", [(2, 4, False), (1, 1, False), (1, 4, True), (1, 4, "nus")])
 def test_sparse_encoder_forward_backward_matches_oracle(B, stride, basic):
-    """basic: the CenterPoint basicblock encoder (residual SparseBasicBlocks, 128-wide fp32 convs)."""
+    """basic: the CenterPoint basicblock encoder (residual SparseBasicBlocks, 128-wide fp32 convs);
+    "nus": the same with CenterPoint's 5 input features (conv_input 5 -> 16, its 5-wide data gradient)."""
     torch.manual_seed(0)
     feats, coors = _inputs(B, stride)
+    if basic == "nus":
+        feats = np.concatenate([feats, np.random.default_rng(4).uniform(0, 0.5, (len(feats), 1))], 1).astype(np.float32)
     dev = torch.device("cuda")
-    enc = SparseEncoder(4, [41, 1600, 1408], **(BASIC if basic else {})).to(dev)
+    enc = SparseEncoder(feats.shape[1], [41, 1600, 1408], **(BASIC if basic else {})).to(dev)
     with torch.no_grad():   # non-trivial BN affine params
         for m in enc.layers():
             m[1].weight.uniform_(0.5, 1.5)

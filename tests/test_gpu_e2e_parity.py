@@ -24,8 +24,7 @@ so two correct fp32 evaluations (HIP, and the fp32 oracle whose dense part is to
 up to ~1e-2 depending on how their rounding happens to correlate. The oracle composition is
 therefore also run with float64 sparse encoder / SECOND / FPN, and each parameter gradient must be
 (a) within relative L2 2e-2, cosine >= 0.9998 of the fp32 oracle and (b) within relative L2 1e-2 of
-the float64 oracle (or 1.5x the fp32 oracle's own distance, where that is larger), with the mean over all
-gradient tensors <= 2e-3 — as close to the exact step as
+the float64 oracle, with the mean over all gradient tensors <= 2e-3 — as close to the exact step as
 an fp32 evaluation of it gets (the fp32 oracle itself: mean 4.8e-3 / max 1.2e-2 for 3 classes,
 2.3e-4 / 1.1e-3 for Car; HIP: 1.7e-3 / 5.7e-3 and 4.6e-4 / 2.6e-3, profiles/r02_e2e_parity_fp32.log).
 """
@@ -53,10 +52,12 @@ LOSS_TOL = 1e-4
 GRAD_REL = 2e-2
 GRAD_F64_MAX = 1e-2
 GRAD_F64_MEAN = 2e-3
-# middle.11.gamma (the sparse encoder's conv_out BatchNorm scale: the last BatchNorm before the dense BEV, whose
-# gradient sums dy*xhat over all 61k output rows — the tensor the fp32 oracle itself is farthest from float64 on)
-# measured 1.005e-2 next to the fp32 oracle's 0.98e-2 in round 3; bounded by the oracle's own distance + 1e-3
-GRAD_F64_EXCEPT = {"middle.11.gamma": lambda e_ora: e_ora + 1e-3}
+# Round 3 measured middle.11.gamma at 1.005e-2 from float64 and loosened this bound; round 4 re-ran the test with
+# each backward variant switched off (tools/gpu_e2e_ab.sh: default, RPC_SPARSE_NATIVE=0, RPC_DENSE_BNFUSE=0, both;
+# profiles/r04_e2e_backward_ab.log): all four give the same gradients — the one-call sparse backward is bit-identical
+# to the layer loop and the fused BatchNorm-backward sums are a bf16-only path — with HIP 1.66e-3 mean / 4.84e-3
+# max from float64 (middle.11.gamma well below 1e-2; the fp32 oracle itself 4.84e-3 / 1.21e-2). The fixed bound
+# holds for every tensor again, with no exception.
 
 
 class _VFE(nn.Module):            # upstream HardSimpleVFE formula (…3class.py:17)
@@ -261,9 +262,6 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
           f"fp32 oracle mean {mean_ora:.2e} max {ora_level:.2e}")
     for rel, name, cos, e_hip, e_ora in worst:
         assert rel <= GRAD_REL and cos >= 0.9998, (name, rel, cos)
-        print(f"  {name:40s} hip vs f64 {e_hip:.3e}  fp32 oracle vs f64 {e_ora:.3e}") if e_hip > 5e-3 else None
-        # no farther from float64 than GRAD_F64_MAX — one named exception, bounded by the fp32 oracle's own
-        # distance + 1e-3 (GRAD_F64_EXCEPT)
-        bound = GRAD_F64_EXCEPT[name](e_ora) if name in GRAD_F64_EXCEPT else GRAD_F64_MAX
-        assert e_hip <= bound, (name, e_hip, e_ora, bound)
+        # no farther from float64 than GRAD_F64_MAX, every tensor
+        assert e_hip <= GRAD_F64_MAX, (name, e_hip, e_ora)
     assert mean_hip <= GRAD_F64_MEAN, (mean_hip, mean_ora)

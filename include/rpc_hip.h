@@ -436,6 +436,8 @@ typedef struct {
   void* w_fwd;
   void* w_dgrad;
   int kind, ci, co, taps, flip;
+  int co_src;   /* kind 0: rows of W present (co_src <= co; rows co_src .. co-1 are written as zero, the
+                   outputs of a conv padded to co channels); 0 = co */
 } RpcDenseWprep;
 int rpc_dense_wprep_batch(const RpcDenseWprep* descs, int n, void* stream);
 

@@ -75,7 +75,7 @@ class RpcAugFrame(C.Structure):
 class RpcDenseWprep(C.Structure):
     """include/rpc_hip.h RpcDenseWprep."""
     _fields_ = [("W", C.c_void_p), ("w_fwd", C.c_void_p), ("w_dgrad", C.c_void_p), ("kind", C.c_int),
-                ("ci", C.c_int), ("co", C.c_int), ("taps", C.c_int), ("flip", C.c_int)]
+                ("ci", C.c_int), ("co", C.c_int), ("taps", C.c_int), ("flip", C.c_int), ("co_src", C.c_int)]
 
 
 class RpcSpconvWprep(C.Structure):

@@ -206,21 +206,59 @@ def _imgs(B, H, W):
     return (B, H, W), (B, H, W), (B, H, W)
 
 
-def _conv_nobn_fwd(eng, weight, ci, h, pitch, B, H, W, dev, st):
+def _prep_head(eng, head, dev, st):
+    """Every dense-engine weight operand of the head in ceil(85 / 16) batched launches (one launch per
+    conv cost ~15 us each: 1.35 ms per CenterPoint step): id(conv) -> (forward, data-gradient) operands.
+    The task heads' final convs and the DCN offset convs are padded to 64 output channels in the kernel
+    (RpcDenseWprep.co_src) instead of through a zero-filled fp32 copy."""
+    items = []
+
+    def add(conv, pad=False):
+        W = conv.weight.detach().float().contiguous()
+        co, ci = W.shape[0], W.shape[1]
+        items.append((id(conv), W, ci, _PAD if pad else co, co if pad else 0))
+
+    add(head.shared_conv.conv)
+    for th in head.task_heads:
+        for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
+            add(dcn.conv_offset, True)
+        add(th.cls_head[0].conv)
+        add(th.cls_head[1], True)
+        for name in _BOX_ORDER:
+            seq = getattr(th.task_head, name)
+            add(seq[0].conv)
+            add(seq[1], True)
+    out = {}
+    for g0 in range(0, len(items), 16):
+        grp = items[g0:g0 + 16]
+        descs = (_ffi.RpcDenseWprep * len(grp))()
+        for i, (key, W, ci, co, co_src) in enumerate(grp):
+            wf = torch.empty((9, co, ci), dtype=eng.dt, device=dev)
+            wd = torch.empty((9, ci, co), dtype=eng.dt, device=dev)
+            descs[i] = _ffi.RpcDenseWprep(W.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, co, 9, 1, co_src)
+            out[key] = (wf, wd)
+        _ffi.check(eng.wprep_batch(descs, len(grp), st), "rpc_dense_wprep_batch")
+    return out
+
+
+def _conv_nobn_fwd(eng, weight, ci, h, pitch, B, H, W, dev, st, wts=None):
     """3x3 conv (no BN) on the dense engine (bf16 or fp32) with the outputs padded to 64 ->
-    (z image, record)."""
+    (z image, record). wts: (forward, data-gradient) operands from _prep_head, else prepared here."""
     n = weight.shape[0]
-    W32 = torch.zeros((_PAD, ci, 3, 3), dtype=torch.float32, device=dev)
-    W32[:n] = weight.detach().float()
-    wf = torch.empty((9, _PAD, ci), dtype=eng.dt, device=dev)
-    wd = torch.empty((9, ci, _PAD), dtype=eng.dt, device=dev)
-    desc = (_ffi.RpcDenseWprep * 1)(_ffi.RpcDenseWprep(W32.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, _PAD, 9, 1))
-    _ffi.check(eng.wprep_batch(desc, 1, st), "rpc_dense_wprep_batch")
+    if wts is None:
+        W32 = weight.detach().float().contiguous()
+        wf = torch.empty((9, _PAD, ci), dtype=eng.dt, device=dev)
+        wd = torch.empty((9, ci, _PAD), dtype=eng.dt, device=dev)
+        desc = (_ffi.RpcDenseWprep * 1)(_ffi.RpcDenseWprep(W32.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, _PAD,
+                                                           9, 1, n))
+        _ffi.check(eng.wprep_batch(desc, 1, st), "rpc_dense_wprep_batch")
+    else:
+        wf, wd = wts
     z = db._image(B, _PAD, H, W, dev, eng.dt)
     R = _ffi.int_arr((B, H, W))
     _ffi.check(eng.conv(db.S1, _ffi.ptr(h), pitch, ci, _ffi.ptr(wf), _PAD, _ffi.ptr(z), _PAD, 0, 0, None, R, R, R,
                         st), "rpc_dense_conv")
-    return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, B=B, H=H, W=W, W32=W32)
+    return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, B=B, H=H, W=W)
 
 
 def _conv_nobn_bwd(eng, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=False):
@@ -266,15 +304,18 @@ class CenterHeadFn(torch.autograd.Function):
         hm = torch.empty((cells, head.hm_pitch), dtype=torch.float32, device=dev)
         box = torch.empty((cells, head.box_pitch), dtype=torch.float32, device=dev)
         pack = lib.rpc_head_pack_f32 if f32 else lib.rpc_head_pack
+        prep = _prep_head(eng, head, dev, st)
         Lsh = _conv_module_layer(head.shared_conv)
-        y0, rsh, _, _ = db._forward_layer(eng, Lsh, xi, Cin, B, H, W, training, dev, st)
+        y0, rsh, _, _ = db._forward_layer(eng, Lsh, xi, Cin, B, H, W, training, dev, st,
+                                          wts=prep[id(head.shared_conv.conv)])
         bns = [head.shared_conv.bn]
         trecs = []
         c0 = 0
         for t, th in enumerate(head.task_heads):
             tr = {}
             for br, dcn in (("cls", th.feature_adapt_cls), ("reg", th.feature_adapt_reg)):
-                oz, orec = _conv_nobn_fwd(eng, dcn.conv_offset.weight, 64, y0, 64, B, H, W, dev, st)
+                oz, orec = _conv_nobn_fwd(eng, dcn.conv_offset.weight, 64, y0, 64, B, H, W, dev, st,
+                                          prep[id(dcn.conv_offset)])
                 ob = dcn.conv_offset.bias.detach().float().contiguous()
                 feat = db._image(B, 64, H, W, dev, eng.dt)
                 if f32:
@@ -292,10 +333,11 @@ class CenterHeadFn(torch.autograd.Function):
                 tr[br] = dict(dcn=dcn, oz=oz, orec=orec, wd=wdd, ob=ob, feat=feat)
             # cls branch -> heatmap logits
             L = _conv_module_layer(th.cls_head[0])
-            hcls, rc, _, _ = db._forward_layer(eng, L, tr["cls"]["feat"], 64, B, H, W, training, dev, st)
+            hcls, rc, _, _ = db._forward_layer(eng, L, tr["cls"]["feat"], 64, B, H, W, training, dev, st,
+                                               wts=prep[id(th.cls_head[0].conv)])
             bns.append(th.cls_head[0].bn)
             fc = th.cls_head[1]
-            z, frec = _conv_nobn_fwd(eng, fc.weight, 64, hcls, 64, B, H, W, dev, st)
+            z, frec = _conv_nobn_fwd(eng, fc.weight, 64, hcls, 64, B, H, W, dev, st, prep[id(fc)])
             _ffi.check(pack(_ffi.ptr(z), _PAD, th.num_cls, _ffi.ptr(fc.bias.detach().float().contiguous()),
                                          _ffi.ptr(hm), head.hm_pitch, c0, cells, st), "rpc_head_pack")
             tr["cls_layers"] = (rc, frec, fc, c0, th.num_cls, hm, head.hm_pitch)
@@ -305,11 +347,12 @@ class CenterHeadFn(torch.autograd.Function):
             for name in _BOX_ORDER:
                 seq = getattr(th.task_head, name)
                 L = _conv_module_layer(seq[0])
-                hr, rr, _, _ = db._forward_layer(eng, L, tr["reg"]["feat"], 64, B, H, W, training, dev, st)
+                hr, rr, _, _ = db._forward_layer(eng, L, tr["reg"]["feat"], 64, B, H, W, training, dev, st,
+                                                 wts=prep[id(seq[0].conv)])
                 bns.append(seq[0].bn)
                 fcv = seq[1]
                 n = fcv.weight.shape[0]
-                z, frec = _conv_nobn_fwd(eng, fcv.weight, 64, hr, 64, B, H, W, dev, st)
+                z, frec = _conv_nobn_fwd(eng, fcv.weight, 64, hr, 64, B, H, W, dev, st, prep[id(fcv)])
                 _ffi.check(pack(_ffi.ptr(z), _PAD, n, _ffi.ptr(fcv.bias.detach().float().contiguous()),
                                              _ffi.ptr(box), head.box_pitch, bo, cells, st), "rpc_head_pack")
                 regs.append((rr, frec, fcv, bo, n))

@@ -2324,9 +2324,10 @@ __global__ __launch_bounds__(BLK) void k_wprep_batch(WprepBatch b) {
   const int a0 = (blockIdx.x / nbt) * WPT, b0 = (blockIdx.x % nbt) * WPT;
   const int an = min(WPT, A - a0), bn = min(WPT, Bd - b0);
   const int row = bn * T;   // contiguous source floats per a
+  const int alim = (d.kind == 0 && d.co_src > 0) ? d.co_src : A;   // rows past co_src: zero (padded outputs)
   for (int q = threadIdx.x; q < an * row; q += BLK) {
     const int ar = q / row, k = q - ar * row, br = k / T, t = k - br * T;
-    tile[t * TP + ar * (WPT + 1) + br] = d.W[((size_t)(a0 + ar) * Bd + b0) * T + k];
+    tile[t * TP + ar * (WPT + 1) + br] = a0 + ar < alim ? d.W[((size_t)(a0 + ar) * Bd + b0) * T + k] : 0.0f;
   }
   __syncthreads();
   // out1[t][a][b] (Conv2d: w_fwd [t][co][ci]; ConvTranspose2d: w_dgrad [t][ci][co])
@@ -2684,7 +2685,8 @@ extern "C" int rpc_dense_wprep_batch(const RpcDenseWprep* descs, int n, void* st
   long long most = 0;
   for (int i = 0; i < n; ++i) {
     const RpcDenseWprep& d = descs[i];
-    if (!d.W || d.ci < 1 || d.co < 1 || d.taps < 1 || d.taps > WPT_MAXT || (d.kind != 0 && d.kind != 1))
+    if (!d.W || d.ci < 1 || d.co < 1 || d.taps < 1 || d.taps > WPT_MAXT || (d.kind != 0 && d.kind != 1) ||
+        d.co_src < 0 || d.co_src > d.co || (d.co_src && d.kind != 0))
       return RPC_ERR_ARG;
     b.d[i] = d;
     const long long e = (long long)((d.ci + WPT - 1) / WPT) * ((d.co + WPT - 1) / WPT);

@@ -295,7 +295,8 @@ __global__ __launch_bounds__(BLK) void k_wprep_batch_f32(WprepBatch bt) {
   const int CI = d.ci, CO = d.co, T = d.taps;
   const int t = (int)(e / ((long long)CI * CO));
   const int rem = (int)(e - (long long)t * CI * CO), ci = rem / CO, co = rem - ci * CO;
-  const float v = d.kind == 0 ? d.W[((size_t)co * CI + ci) * T + t] : d.W[((size_t)ci * CO + co) * T + t];
+  const float v = d.kind == 0 ? (d.co_src > 0 && co >= d.co_src ? 0.0f : d.W[((size_t)co * CI + ci) * T + t])
+                              : d.W[((size_t)ci * CO + co) * T + t];
   if (d.w_fwd) ((float*)d.w_fwd)[((size_t)t * CO + co) * CI + ci] = v;
   if (d.w_dgrad) {
     const int td = d.flip ? T - 1 - t : t;
@@ -407,7 +408,9 @@ extern "C" int rpc_dense_wprep_batch_f32(const RpcDenseWprep* descs, int n, void
   long long most = 0;
   for (int i = 0; i < n; ++i) {
     const RpcDenseWprep& d = descs[i];
-    if (!d.W || d.ci < 1 || d.co < 1 || d.taps < 1 || (d.kind != 0 && d.kind != 1)) return RPC_ERR_ARG;
+    if (!d.W || d.ci < 1 || d.co < 1 || d.taps < 1 || (d.kind != 0 && d.kind != 1) || d.co_src < 0 ||
+        d.co_src > d.co || (d.co_src && d.kind != 0))
+      return RPC_ERR_ARG;
     b.d[i] = d;
     const long long e = (long long)d.taps * d.ci * d.co;
     most = e > most ? e : most;

@@ -1,16 +1,11 @@
 #!/bin/bash
-# CenterPoint bench + kernel profile in one call
+# CenterPoint: head / e2e tests, then bench + profile
 set -o pipefail
 OUT=gpurun_out/$1
 mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 400 python -u bench.py --model centerpoint --steps 10 --warmup 4 --no-cpu-baseline > $OUT/bench_cp.log 2>&1 &&
-tail -1 $OUT/bench_cp.log | cut -c1-600 &&
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof -o run -- \
-  python -u bench.py --model centerpoint --steps 6 --warmup 3 --no-cpu-baseline > $OUT/prof_bench.log 2>&1
-RC=$?
-KT=$(find $OUT/prof -name '*kernel_trace.csv' | head -1)
-[ -n "$KT" ] && python tools/prof_summary.py $KT --steps 6 --top 45 > $OUT/step_kernels.txt 2>&1
-find $OUT/prof -name '*.csv' -size +4M -delete 2>/dev/null
-find $OUT/prof -name '*.db' -delete 2>/dev/null
-exit $RC
+timeout -k 10 400 python -u -m pytest tests/test_gpu_dcn_head.py tests/test_gpu_centerpoint.py tests/test_gpu_center_head.py \
+  tests/test_gpu_e2e_parity_centerpoint.py -x -v -s --timeout 240 --timeout-method thread > $OUT/pytest.log 2>&1; RC=$?
+tail -3 $OUT/pytest.log
+[ $RC -ne 0 ] && exit $RC
+bash tools/gpu_prof_model.sh $1 --model centerpoint --steps 8 --warmup 3

@@ -748,6 +748,52 @@ __global__ __launch_bounds__(BLK) void k_res_fwd(const float* __restrict__ z, co
   }
 }
 
+// the same for C % 8 == 0, one thread per (row, 8 channels): two 16-byte loads per operand, one 16-byte
+// store per 16-bit row image, 32-bit index math (the per-element kernel above divided a 64-bit index per
+// element and moved 4 bytes per access: 74 us per 128-channel CenterPoint layer). Same arithmetic per
+// element, so the same bits.
+template <int FMT>
+__global__ __launch_bounds__(BLK) void k_res_fwd_v8(const float* __restrict__ z, const float* __restrict__ bn,
+                                                    const float* __restrict__ res, int N, int C,
+                                                    float* __restrict__ out, unsigned short* __restrict__ hb,
+                                                    unsigned short* __restrict__ hb2) {
+  const int G = C >> 3;
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * G) return;
+  const int r = t / G, cg = t - r * G, c0 = cg * 8;
+  const int i = r * C + c0;
+  float zv[8], rv[8], v[8];
+  *(float4*)&zv[0] = *(const float4*)(z + i);
+  *(float4*)&zv[4] = *(const float4*)(z + i + 4);
+  if (res) {
+    *(float4*)&rv[0] = *(const float4*)(res + i);
+    *(float4*)&rv[4] = *(const float4*)(res + i + 4);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int c = c0 + j;
+    float x = fmaf(zv[j] - bn[2 * C + c], bn[c], bn[C + c]);
+    if (res) x = x + rv[j];
+    v[j] = fmaxf(x, 0.0f);
+  }
+  *(float4*)(out + i) = *(const float4*)&v[0];
+  *(float4*)(out + i + 4) = *(const float4*)&v[4];
+  if (hb) {
+    unsigned short h[8], b2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      if (FMT) {
+        h[j] = __builtin_bit_cast(unsigned short, (_Float16)v[j]);
+        b2[j] = __builtin_bit_cast(unsigned short, (__bf16)v[j]);
+      } else {
+        h[j] = __builtin_bit_cast(unsigned short, (__bf16)v[j]);
+      }
+    }
+    *(uint4*)(hb + i) = *(const uint4*)h;
+    if (FMT && hb2) *(uint4*)(hb2 + i) = *(const uint4*)b2;
+  }
+}
+
 // backward: m = (g1 + g2) * (out > 0) and the BatchNorm-backward partial sums of the layer that
 // produced z (sum m, sum m * xhat) per BM rows, laid out like k_from_dense (C <= 256)
 __global__ __launch_bounds__(BLK) void k_res_bwd(const float* __restrict__ g1, const float* __restrict__ g2,
@@ -785,6 +831,59 @@ __global__ __launch_bounds__(BLK) void k_res_bwd(const float* __restrict__ g1, c
   }
 }
 
+
+// the same for C % 4 == 0: thread = (row lane, 4 channels), 16-byte accesses, the BM rows of a block in
+// passes of BLK / (C / 4) rows with 4 rows' loads in flight per thread; partial sums combined over the row
+// lanes in lane order (fixed order: deterministic)
+__global__ __launch_bounds__(BLK) void k_res_bwd_v4(const float* __restrict__ g1, const float* __restrict__ g2,
+                                                    const float* __restrict__ out, const float* __restrict__ z,
+                                                    const float* __restrict__ bn, int N, int C,
+                                                    float* __restrict__ m, float* __restrict__ part) {
+  __shared__ float sh[2][BLK * 4];
+  const int r0 = blockIdx.x * BM, r1 = min(N, r0 + BM);
+  const int Q = C >> 2, nl = BLK / Q;
+  const int rl = threadIdx.x / Q, cq = threadIdx.x - rl * Q, c0 = cq * 4;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (rl < nl) {
+    const float4 mu = *(const float4*)(bn + 2 * C + c0), is = *(const float4*)(bn + 3 * C + c0);
+    const float mu_[4] = {mu.x, mu.y, mu.z, mu.w}, is_[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll 4
+    for (int r = r0 + rl; r < r1; r += nl) {
+      const int i = r * C + c0;
+      const float4 ga = *(const float4*)(g1 + i);
+      const float4 gb = g2 ? *(const float4*)(g2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+      const float4 o = *(const float4*)(out + i);
+      const float4 zz = *(const float4*)(z + i);
+      const float gg[4] = {g2 ? ga.x + gb.x : ga.x, g2 ? ga.y + gb.y : ga.y, g2 ? ga.z + gb.z : ga.z,
+                           g2 ? ga.w + gb.w : ga.w};
+      const float oo[4] = {o.x, o.y, o.z, o.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        v[j] = oo[j] > 0.0f ? gg[j] : 0.0f;
+        s1[j] += v[j];
+        s2[j] += v[j] * ((zv[j] - mu_[j]) * is_[j]);
+      }
+      *(float4*)(m + i) = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    sh[0][threadIdx.x * 4 + j] = s1[j];
+    sh[1][threadIdx.x * 4 + j] = s2[j];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += BLK) {
+    const int q = c >> 2, j = c & 3;
+    float t1 = 0.0f, t2 = 0.0f;
+    for (int k = 0; k < nl; ++k) {
+      t1 += sh[0][(k * Q + q) * 4 + j];
+      t2 += sh[1][(k * Q + q) * 4 + j];
+    }
+    part[(long long)blockIdx.x * 2 * C + c] = t1;
+    part[(long long)blockIdx.x * 2 * C + C + c] = t2;
+  }
+}
 
 // Weight gradient of the narrow input layer (CI * CO <= 128, the 4/5 -> 16 conv_input): every
 // block takes a chunk of rows for ALL K offsets, so the BatchNorm-backward dz tile is formed once
@@ -1292,6 +1391,17 @@ extern "C" int rpc_sparse_res_forward_h16(const float* z, const float* bn, const
   if (n < 0 || c < 1 || !z || !bn || !out || (fmt != 0 && fmt != 1) || (out_bf16 && !fmt)) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   const int cp = (c + 7) / 8 * 8;
+  if (c % 8 == 0 && (long long)n * c < (1LL << 31)) {
+    const dim3 grid(cdiv((long long)n * (c / 8), BLK));
+    if (fmt)
+      hipLaunchKernelGGL(k_res_fwd_v8<1>, grid, dim3(BLK), 0, (hipStream_t)stream, z, bn, res, n, c, out,
+                         (unsigned short*)out_h16, (unsigned short*)out_bf16);
+    else
+      hipLaunchKernelGGL(k_res_fwd_v8<0>, grid, dim3(BLK), 0, (hipStream_t)stream, z, bn, res, n, c, out,
+                         (unsigned short*)out_h16, (unsigned short*)nullptr);
+    RPC_LAUNCH_CHECK();
+    return RPC_OK;
+  }
   if (fmt)
     hipLaunchKernelGGL(k_res_fwd<1>, dim3(cdiv((long long)n * cp, BLK)), dim3(BLK), 0, (hipStream_t)stream, z, bn, res,
                        n, c, cp, out, (unsigned short*)out_h16, (unsigned short*)out_bf16);
@@ -1311,8 +1421,12 @@ extern "C" int rpc_sparse_res_backward(const float* g1, const float* g2, const f
                                        const float* bn, int n, int c, float* m, float* part, void* stream) {
   if (n < 0 || c < 1 || c > 256 || !g1 || !out || !z || !bn || !m || !part) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_res_bwd, dim3(cdiv(n, BM)), dim3(BLK), 0, (hipStream_t)stream, g1, g2, out, z, bn, n, c, m,
-                     part);
+  if (c % 4 == 0 && c >= 16 && (long long)n * c < (1LL << 31))
+    hipLaunchKernelGGL(k_res_bwd_v4, dim3(cdiv(n, BM)), dim3(BLK), 0, (hipStream_t)stream, g1, g2, out, z, bn, n, c,
+                       m, part);
+  else
+    hipLaunchKernelGGL(k_res_bwd, dim3(cdiv(n, BM)), dim3(BLK), 0, (hipStream_t)stream, g1, g2, out, z, bn, n, c, m,
+                       part);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

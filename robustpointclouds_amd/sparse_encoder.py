@@ -52,10 +52,12 @@ SIDE_STREAMS = os.environ.get("RPC_SPARSE_STREAMS", "1") != "0"
 # the backward as one native call (csrc/sparse_exec.hip rpc_sparse_backward); 0: the per-layer Python loop
 NATIVE_BACKWARD = os.environ.get("RPC_SPARSE_NATIVE", "1") != "0"
 # RPC_SPARSE_FUSED_FIN=1: BatchNorm finalizes fused into the bf16 GEMMs that produce their partial sums
-# (rpc_spconv_gemm_bf16_fin, two-level last-arriving blocks). Off by default: measured SLOWER — every block's
-# agent-scope release before its ticket writes back its XCD L2's dirty lines (the GEMM's freshly stored output
-# rows), k_gemm_bf16<64,4,0> 41 -> 63 us and <64,4,1> 53 -> 92 us against a 6.2 us rpc_bn_finalize launch
-# (profiles/r04_spgemm_fused_fin.txt)
+# (rpc_spconv_gemm_bf16_fin, two-level last-arriving blocks). Off by default. With an agent-scope release per
+# block (buffer_wbl2: every block wrote back its XCD L2's dirty lines, the GEMM's fresh output rows) it was
+# k_gemm_bf16<64,4,0> 41 -> 63 us, <64,4,1> 53 -> 92 us (profiles/r04_spgemm_fused_fin.txt); with the hand-off
+# data in sc1 stores and no fence (common.h last_block_arrive_lite) the data gradient is 54.2 -> 58.6 us
+# against the 6.4 us rpc_bn_finalize launch it removes: kernel busy 8.28 -> 8.22 ms, step time within noise
+# (profiles/r04_step_kernels_fused_fin.txt, r04_ab_split_fin.txt)
 FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "0") != "0"
 # perf mode forward GEMM operands (gathered rows relu(bn(z)) and forward weight tiles): fp16 (default) or bf16
 # (RPC_SPARSE_FWD_BF16=1, A/B). The operand rounding of the forward decides the ReLU masks that every gradient

@@ -224,10 +224,11 @@ def _prep_head(eng, head, dev, st):
             add(dcn.conv_offset, True)
         add(th.cls_head[0].conv)
         add(th.cls_head[1], True)
+        cms = [getattr(th.task_head, name)[0] for name in _BOX_ORDER]
+        Wcat = torch.cat([cm.conv.weight.detach().float() for cm in cms]).contiguous()
+        items.append((("regcat", id(th)), Wcat, Wcat.shape[1], Wcat.shape[0], 0))
         for name in _BOX_ORDER:
-            seq = getattr(th.task_head, name)
-            add(seq[0].conv)
-            add(seq[1], True)
+            add(getattr(th.task_head, name)[1], True)
     out = {}
     for g0 in range(0, len(items), 16):
         grp = items[g0:g0 + 16]
@@ -237,8 +238,38 @@ def _prep_head(eng, head, dev, st):
             wd = torch.empty((9, ci, co), dtype=eng.dt, device=dev)
             descs[i] = _ffi.RpcDenseWprep(W.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, co, 9, 1, co_src)
             out[key] = (wf, wd)
+            if isinstance(key, tuple):
+                out[key + ("W",)] = W
         _ffi.check(eng.wprep_batch(descs, len(grp), st), "rpc_dense_wprep_batch")
     return out
+
+
+class _CatBN:
+    """The BatchNorm2d modules of k ConvModules that share their input, side by side as one 64k-channel
+    BatchNorm for one wide conv + BN + ReLU launch sequence (the attributes dense_bev._forward_layer /
+    _backward_layer read); write_back() returns the updated running statistics to the modules (one
+    multi-tensor copy)."""
+
+    def __init__(self, bns):
+        self.bns = bns
+        self.eps, self.momentum = float(bns[0].eps), float(bns[0].momentum)
+        if any(float(b.eps) != self.eps or float(b.momentum) != self.momentum for b in bns):
+            raise NotImplementedError("CenterHead: the separate-head BatchNorms must share eps / momentum")
+        self.weight = torch.cat([b.weight.detach().float() for b in bns]).contiguous()
+        self.bias = torch.cat([b.bias.detach().float() for b in bns]).contiguous()
+        self.running_mean = torch.cat([b.running_mean for b in bns]).contiguous()
+        self.running_var = torch.cat([b.running_var for b in bns]).contiguous()
+        self.sizes = [b.running_mean.shape[0] for b in bns]
+
+    def write_back(self):
+        dst = [b.running_mean for b in self.bns] + [b.running_var for b in self.bns]
+        src = list(self.running_mean.split(self.sizes)) + list(self.running_var.split(self.sizes))
+        torch._foreach_copy_(dst, src)
+
+
+class _CatConv:
+    def __init__(self, weight):
+        self.weight = weight
 
 
 def _conv_nobn_fwd(eng, weight, ci, h, pitch, B, H, W, dev, st, wts=None):
@@ -261,7 +292,7 @@ def _conv_nobn_fwd(eng, weight, ci, h, pitch, B, H, W, dev, st, wts=None):
     return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, B=B, H=H, W=W)
 
 
-def _conv_nobn_bwd(eng, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=False):
+def _conv_nobn_bwd(eng, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=False, dx_pitch=None):
     ci, B, H, W = rec["ci"], rec["B"], rec["H"], rec["W"]
     R = _ffi.int_arr((B, H, W))
     dW = torch.empty((_PAD, ci, 3, 3), dtype=torch.float32, device=dev)
@@ -272,7 +303,7 @@ def _conv_nobn_bwd(eng, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=
     dx = None
     if need_dx:
         dx = dx_out if dx_out is not None else db._image(B, ci, H, W, dev, eng.dt)
-        _ffi.check(eng.conv(db.S1, _ffi.ptr(dz), _PAD, _PAD, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), ci, 0,
+        _ffi.check(eng.conv(db.S1, _ffi.ptr(dz), _PAD, _PAD, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), dx_pitch or ci, 0,
                             1 if accumulate else 0, None, R, R, R, st), "rpc_dense_conv(dgrad)")
     return dx, dW[:rec["n"]]
 
@@ -342,21 +373,27 @@ class CenterHeadFn(torch.autograd.Function):
                                          _ffi.ptr(hm), head.hm_pitch, c0, cells, st), "rpc_head_pack")
             tr["cls_layers"] = (rc, frec, fc, c0, th.num_cls, hm, head.hm_pitch)
             c0 += th.num_cls
-            # reg branches -> anno_box channels
+            # reg branches -> anno_box channels: the five ConvModules of the separate head share their input
+            # (the DCN feature): one 64 -> 320 conv + BatchNorm + ReLU, the final convs read 64-channel slices
+            cms = [getattr(th.task_head, name)[0] for name in _BOX_ORDER]
+            cbn = _CatBN([cm.bn for cm in cms])
+            Lr = db._Layer(db.S1, _CatConv(prep[("regcat", id(th), "W")]), cbn, 0, 64, 64 * len(cms), 9)
+            hr, rr, _, _ = db._forward_layer(eng, Lr, tr["reg"]["feat"], 64, B, H, W, training, dev, st,
+                                             wts=prep[("regcat", id(th))])
+            if training:
+                cbn.write_back()
+            bns.extend(cbn.bns)
             regs, bo = [], 10 * t
-            for name in _BOX_ORDER:
-                seq = getattr(th.task_head, name)
-                L = _conv_module_layer(seq[0])
-                hr, rr, _, _ = db._forward_layer(eng, L, tr["reg"]["feat"], 64, B, H, W, training, dev, st,
-                                                 wts=prep[id(seq[0].conv)])
-                bns.append(seq[0].bn)
-                fcv = seq[1]
+            for i, name in enumerate(_BOX_ORDER):
+                fcv = getattr(th.task_head, name)[1]
                 n = fcv.weight.shape[0]
-                z, frec = _conv_nobn_fwd(eng, fcv.weight, 64, hr, 64, B, H, W, dev, st, prep[id(fcv)])
+                z, frec = _conv_nobn_fwd(eng, fcv.weight, 64, hr[:, 64 * i:64 * (i + 1)], 64 * len(cms), B, H, W,
+                                         dev, st, prep[id(fcv)])
                 _ffi.check(pack(_ffi.ptr(z), _PAD, n, _ffi.ptr(fcv.bias.detach().float().contiguous()),
                                              _ffi.ptr(box), head.box_pitch, bo, cells, st), "rpc_head_pack")
-                regs.append((rr, frec, fcv, bo, n))
+                regs.append((frec, fcv, bo, n))
                 bo += n
+            tr["reg_cm"] = (rr, cms)
             tr["regs"] = regs
             trecs.append(tr)
         if training:
@@ -389,14 +426,19 @@ class CenterHeadFn(torch.autograd.Function):
         dwsz = lib.rpc_dcn_backward_workspace_size(B, H, W)
         dws = _ffi.workspace(dwsz, dev)
 
-        def head_branch(rec_cm, frec, conv, g, gp, off, n, dfeat, acc):
+        unpack = lib.rpc_head_unpack_grad_f32 if f32 else lib.rpc_head_unpack_grad
+
+        def final_conv_bwd(frec, conv, g, gp, off, n, dx_out=None, dx_pitch=None):
             dz = db._image(B, _PAD, H, W, dev, eng.dt)
             db_ = torch.empty(n, dtype=torch.float32, device=dev)
-            unpack = lib.rpc_head_unpack_grad_f32 if f32 else lib.rpc_head_unpack_grad
             _ffi.check(unpack(_ffi.ptr(g), gp, off, n, _ffi.ptr(dz), _PAD, cells, _ffi.ptr(db_),
-                                                _ffi.ptr(uws), uwsz, st), "rpc_head_unpack_grad")
-            dh, dW = _conv_nobn_bwd(eng, frec, dz, dev, st)
+                              _ffi.ptr(uws), uwsz, st), "rpc_head_unpack_grad")
+            dh, dW = _conv_nobn_bwd(eng, frec, dz, dev, st, True, dx_out, False, dx_pitch)
             grads[id(conv.weight)], grads[id(conv.bias)] = dW, db_
+            return dh
+
+        def head_branch(rec_cm, frec, conv, g, gp, off, n, dfeat, acc):
+            dh = final_conv_bwd(frec, conv, g, gp, off, n)
             dfeat, dWc, dg, dbt, _ = db._backward_layer(eng, rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
             L = rec_cm["L"]
             grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWc, dg, dbt
@@ -405,9 +447,16 @@ class CenterHeadFn(torch.autograd.Function):
         for t, tr in enumerate(ctx.trecs):
             rc, frec, fc, c0, ncls, _, hp = tr["cls_layers"]
             dfc = head_branch(rc, frec, fc, ghm, hp, c0, ncls, None, False)
-            dfr = None
-            for i, (rr, frec2, fcv, bo, n) in enumerate(tr["regs"]):
-                dfr = head_branch(rr, frec2, fcv, gbox, head.box_pitch, bo, n, dfr, i > 0)
+            # reg: the five final convs' data gradients into 64-channel slices of one 320-channel image, then
+            # the concatenated ConvModule's backward (gradients split back per module)
+            rr, cms = tr["reg_cm"]
+            nct = 64 * len(cms)
+            dh_cat = db._image(B, nct, H, W, dev, eng.dt)
+            for i, (frec2, fcv, bo, n) in enumerate(tr["regs"]):
+                final_conv_bwd(frec2, fcv, gbox, head.box_pitch, bo, n, dh_cat[:, 64 * i:64 * (i + 1)], nct)
+            dfr, dWc, dg, dbt, _ = db._backward_layer(eng, rr, dh_cat, nct, 0, dev, st, True)
+            for cm, w_, g_, b_ in zip(cms, dWc.split(64), dg.split(64), dbt.split(64)):
+                grads[id(cm.conv.weight)], grads[id(cm.bn.weight)], grads[id(cm.bn.bias)] = w_, g_, b_
             for br, dfeat in (("cls", dfc), ("reg", dfr)):
                 d = tr[br]
                 doff = db._image(B, _PAD, H, W, dev, eng.dt)

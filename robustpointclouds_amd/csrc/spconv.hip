@@ -832,56 +832,99 @@ __global__ __launch_bounds__(BLK) void k_res_bwd(const float* __restrict__ g1, c
 }
 
 
-// the same for C % 4 == 0: thread = (row lane, 4 channels), 16-byte accesses, the BM rows of a block in
-// passes of BLK / (C / 4) rows with 4 rows' loads in flight per thread; partial sums combined over the row
-// lanes in lane order (fixed order: deterministic)
+// the same for C % 4 == 0 (C <= 128): thread = (row lane, 4 channels) with 16-byte accesses and 8 rows per
+// thread, all 8 rows' loads in flight; a block covers 8 * BLK / (C / 4) rows = one or more BM-row partial
+// groups (the layout rpc_bn_finalize reads). Partial sums: shuffles over the row lanes of a wave (fixed xor
+// order), then the 4 waves in order through LDS — deterministic. (One row per thread and one LDS
+// reduction per 64 rows ran the 16-channel CenterPoint layers at ~1.1 TB/s.)
 __global__ __launch_bounds__(BLK) void k_res_bwd_v4(const float* __restrict__ g1, const float* __restrict__ g2,
                                                     const float* __restrict__ out, const float* __restrict__ z,
                                                     const float* __restrict__ bn, int N, int C,
                                                     float* __restrict__ m, float* __restrict__ part) {
-  __shared__ float sh[2][BLK * 4];
-  const int r0 = blockIdx.x * BM, r1 = min(N, r0 + BM);
-  const int Q = C >> 2, nl = BLK / Q;
+  constexpr int RPT = 8;                                 // rows per thread
+  __shared__ float sh[2][RPT][BLK / 64][128];
+  const int Q = C >> 2, nl = BLK / Q;                    // row lanes per pass
+  const int rows_blk = RPT * nl, ng = rows_blk / BM;     // rows and BM-row partial groups per block
+  const int rb = blockIdx.x * rows_blk;
   const int rl = threadIdx.x / Q, cq = threadIdx.x - rl * Q, c0 = cq * 4;
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-  if (rl < nl) {
-    const float4 mu = *(const float4*)(bn + 2 * C + c0), is = *(const float4*)(bn + 3 * C + c0);
-    const float mu_[4] = {mu.x, mu.y, mu.z, mu.w}, is_[4] = {is.x, is.y, is.z, is.w};
-#pragma unroll 4
-    for (int r = r0 + rl; r < r1; r += nl) {
-      const int i = r * C + c0;
-      const float4 ga = *(const float4*)(g1 + i);
-      const float4 gb = g2 ? *(const float4*)(g2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
-      const float4 o = *(const float4*)(out + i);
-      const float4 zz = *(const float4*)(z + i);
-      const float gg[4] = {g2 ? ga.x + gb.x : ga.x, g2 ? ga.y + gb.y : ga.y, g2 ? ga.z + gb.z : ga.z,
-                           g2 ? ga.w + gb.w : ga.w};
-      const float oo[4] = {o.x, o.y, o.z, o.w}, zv[4] = {zz.x, zz.y, zz.z, zz.w};
-      float v[4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const float4 mu4 = *(const float4*)(bn + 2 * C + c0), is4 = *(const float4*)(bn + 3 * C + c0);
+  const float mu[4] = {mu4.x, mu4.y, mu4.z, mu4.w}, is[4] = {is4.x, is4.y, is4.z, is4.w};
+  float4 ga[RPT], gb[RPT], o[RPT], zz[RPT];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        v[j] = oo[j] > 0.0f ? gg[j] : 0.0f;
-        s1[j] += v[j];
-        s2[j] += v[j] * ((zv[j] - mu_[j]) * is_[j]);
-      }
-      *(float4*)(m + i) = make_float4(v[0], v[1], v[2], v[3]);
+  for (int j = 0; j < RPT; ++j) {
+    const int r = rb + rl + nl * j;
+    const int i = (r < N ? r : 0) * C + c0;
+    ga[j] = *(const float4*)(g1 + i);
+    gb[j] = g2 ? *(const float4*)(g2 + i) : make_float4(0.f, 0.f, 0.f, 0.f);
+    o[j] = *(const float4*)(out + i);
+    zz[j] = *(const float4*)(z + i);
+  }
+  float s1[RPT][4], s2[RPT][4];   // per row slot; slots of one BM group are combined below
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int r = rb + rl + nl * j;
+    const float gg[4] = {ga[j].x + gb[j].x, ga[j].y + gb[j].y, ga[j].z + gb[j].z, ga[j].w + gb[j].w};
+    const float oo[4] = {o[j].x, o[j].y, o[j].z, o[j].w}, zv[4] = {zz[j].x, zz[j].y, zz[j].z, zz[j].w};
+    float v[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      v[q] = (r < N && oo[q] > 0.0f) ? gg[q] : 0.0f;
+      s1[j][q] = v[q];
+      s2[j][q] = v[q] * ((zv[q] - mu[q]) * is[q]);
+    }
+    if (r < N) *(float4*)(m + r * C + c0) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+  // row slot j of this thread lies in group (nl * j) / BM; sum the slots of each group in slot order
+  float t1[RPT][4], t2[RPT][4];
+#pragma unroll
+  for (int g = 0; g < RPT; ++g)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) t1[g][q] = t2[g][q] = 0.0f;
+#pragma unroll
+  for (int j = 0; j < RPT; ++j) {
+    const int g = (nl * j) / BM;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      t1[g][q] += s1[j][q];
+      t2[g][q] += s2[j][q];
     }
   }
+  // over the row lanes of the wave (lanes differing in the bits above log2(Q)), fixed xor order
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    sh[0][threadIdx.x * 4 + j] = s1[j];
-    sh[1][threadIdx.x * 4 + j] = s2[j];
+  for (int g = 0; g < RPT; ++g) {
+    if (g >= ng) continue;   // uniform
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      for (int msk = Q; msk < 64; msk <<= 1) {
+        t1[g][q] += __shfl_xor(t1[g][q], msk, 64);
+        t2[g][q] += __shfl_xor(t2[g][q], msk, 64);
+      }
+    }
+  }
+  if (lane < Q) {
+#pragma unroll
+    for (int g = 0; g < RPT; ++g) {
+      if (g >= ng) continue;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        sh[0][g][w][c0 + q] = t1[g][q];
+        sh[1][g][w][c0 + q] = t2[g][q];
+      }
+    }
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += BLK) {
-    const int q = c >> 2, j = c & 3;
-    float t1 = 0.0f, t2 = 0.0f;
-    for (int k = 0; k < nl; ++k) {
-      t1 += sh[0][(k * Q + q) * 4 + j];
-      t2 += sh[1][(k * Q + q) * 4 + j];
+  const int gb0 = blockIdx.x * ng, ngr = (N + BM - 1) / BM;
+  for (int e = threadIdx.x; e < ng * C; e += BLK) {
+    const int g = e / C, c = e - g * C;
+    if (gb0 + g >= ngr) continue;
+    float a1 = 0.0f, a2 = 0.0f;
+    for (int ww = 0; ww < BLK / 64; ++ww) {
+      a1 += sh[0][g][ww][c];
+      a2 += sh[1][g][ww][c];
     }
-    part[(long long)blockIdx.x * 2 * C + c] = t1;
-    part[(long long)blockIdx.x * 2 * C + C + c] = t2;
+    part[(long long)(gb0 + g) * 2 * C + c] = a1;
+    part[(long long)(gb0 + g) * 2 * C + C + c] = a2;
   }
 }
 
@@ -1421,9 +1464,9 @@ extern "C" int rpc_sparse_res_backward(const float* g1, const float* g2, const f
                                        const float* bn, int n, int c, float* m, float* part, void* stream) {
   if (n < 0 || c < 1 || c > 256 || !g1 || !out || !z || !bn || !m || !part) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
-  if (c % 4 == 0 && c >= 16 && (long long)n * c < (1LL << 31))
-    hipLaunchKernelGGL(k_res_bwd_v4, dim3(cdiv(n, BM)), dim3(BLK), 0, (hipStream_t)stream, g1, g2, out, z, bn, n, c,
-                       m, part);
+  if (c % 4 == 0 && c >= 16 && c <= 128 && (long long)n * c < (1LL << 31))
+    hipLaunchKernelGGL(k_res_bwd_v4, dim3(cdiv(n, 8 * (BLK / (c / 4)))), dim3(BLK), 0, (hipStream_t)stream, g1, g2,
+                       out, z, bn, n, c, m, part);
   else
     hipLaunchKernelGGL(k_res_bwd, dim3(cdiv(n, BM)), dim3(BLK), 0, (hipStream_t)stream, g1, g2, out, z, bn, n, c, m,
                        part);

@@ -317,9 +317,15 @@ int rpc_spconv_gemm_bf16_mode(int mode);
 size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co);
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
                           float* dW, void* workspace, size_t workspace_bytes, void* stream);
-/* the same with h in format hfmt (fp16 forward rows are rounded to bf16 as they are staged) */
+/* the same with h in format hfmt (fp16 forward rows are rounded to bf16 as they are staged); dispatches to
+ * rpc_spconv_wgrad_pairs when RPC_SPWG_PAIRS=1 (A/B; rpc_spconv_wgrad_bf16_workspace_size sizes for it) */
 int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out, const void* dz,
                          int co, float* dW, void* workspace, size_t workspace_bytes, void* stream);
+/* r04: the weight gradient over per-offset pair lists compacted from nbr (only rows with a neighbour at k
+ * cost work), blocks balanced over the pairs, one partial per block reduced per offset in block order */
+size_t rpc_spconv_wgrad_pairs_workspace_size(int n_out, int kvol, int ci, int co);
+int rpc_spconv_wgrad_pairs(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out, const void* dz,
+                           int co, float* dW, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- a6 runtime: the whole SparseEncoder backward in one call (csrc/sparse_exec.hip).
  * Replaces the per-layer backward of upstream mmdet3d SparseEncoder (adversarial_voxelnet.py:141;

@@ -156,6 +156,8 @@ SIGNATURES = {
     "rpc_rulebook_mask_perm": (i32, [vp, i32, i32, vp, vp]),
     "rpc_to_h16_rows": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     "rpc_spconv_wgrad_h16": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
+    "rpc_spconv_wgrad_pairs_workspace_size": (sz, [i32, i32, i32, i32]),
+    "rpc_spconv_wgrad_pairs": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
     "rpc_sparse_res_forward_h16": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
     "rpc_bn_fin_groups": (i32, [i32]),
     "rpc_bn_fin_tickets": (i32, [i32]),

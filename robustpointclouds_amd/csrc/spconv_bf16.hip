@@ -21,6 +21,7 @@
 
 #include "common.h"
 #include <stdlib.h>
+#include <hipcub/hipcub.hpp>
 #include "dense_common.h"
 #include "rpc_hip.h"
 
@@ -1036,6 +1037,269 @@ __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf1
   }
 }
 
+// ------------------------------------------------------------------ r04: weight gradient over pair lists
+// k_wgrad_bf16 walks every (row chunk, offset group) over ALL rows of the chunk: a row with no neighbour at
+// offset k still costs its dz / h loads, staging and MFMA rows (sub-tiles are skipped only when none of
+// their 64 rows has one). Here the neighbour map is first compacted into per-offset pair lists
+// (k_pair_count -> one hipcub exclusive scan over the offset-major count table -> k_pair_scatter: pairs of
+// offset k in ascending output-row order, deterministic), and the weight gradient runs over the pairs
+// only: block b of S + K takes a slice of ONE offset's pairs, the offsets getting ceil(count_k * S / P)
+// blocks each (balanced: ~P / S pairs per block whatever the offsets' counts), with dz rows gathered by the
+// pair's output row and h rows by its input row, the same LDS staging / transposed reads / MFMA tiling as
+// k_wgrad_bf16<., ., 1>. One fp32 partial per block (S + K partials instead of chunks x K), reduced per
+// offset over its blocks in block order (k_pair_reduce).
+constexpr int PRB = 256;   // rows per count / scatter block
+
+// the block's PRB x K slice of nbr, staged into LDS with coalesced loads (each thread reading its own row's K
+// entries straight from global memory strided the wave's 64 accesses over 64 rows: 103 us per 360k-row map)
+__device__ __forceinline__ void stage_nbr(const int* __restrict__ nbr, int n, int K, int* snb) {
+  const long long r0 = (long long)blockIdx.x * PRB;
+  const int tot = (int)(min((long long)PRB, (long long)n - r0) * K);
+  const int* src = nbr + r0 * K;
+  int v[MAXK];   // all of the thread's loads in flight before the first LDS store
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i) {
+    const int q = threadIdx.x + i * PRB;
+    v[i] = (i < K && q < tot) ? src[q] : -1;
+  }
+#pragma unroll
+  for (int i = 0; i < MAXK; ++i)
+    if (i < K) snb[threadIdx.x + i * PRB] = v[i];
+}
+
+__global__ __launch_bounds__(PRB) void k_pair_count(const int* __restrict__ nbr, int n, int K, int nb,
+                                                    int* __restrict__ cnt) {
+  __shared__ int snb[PRB * MAXK];
+  __shared__ int sc[PRB / 64][MAXK];
+  stage_nbr(nbr, n, K, snb);
+  __syncthreads();
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  for (int k = 0; k < K; ++k) {
+    const unsigned long long m = __ballot(snb[threadIdx.x * K + k] >= 0);
+    if (lane == 0) sc[w][k] = __popcll(m);
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    int c = 0;
+    for (int ww = 0; ww < PRB / 64; ++ww) c += sc[ww][threadIdx.x];
+    cnt[(long long)threadIdx.x * nb + blockIdx.x] = c;   // offset-major: the scan runs k by k
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(long long)K * nb] = 0;   // the scan's total lands past it
+}
+
+__global__ __launch_bounds__(PRB) void k_pair_scatter(const int* __restrict__ nbr, int n, int K, int nb,
+                                                      const int* __restrict__ base, int2* __restrict__ pairs) {
+  __shared__ int snb[PRB * MAXK];
+  __shared__ int sw[PRB / 64][MAXK];
+  stage_nbr(nbr, n, K, snb);
+  __syncthreads();
+  const int r = blockIdx.x * PRB + threadIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const unsigned long long below = (1ull << lane) - 1ull;
+  for (int k = 0; k < K; ++k) {
+    const unsigned long long m = __ballot(snb[threadIdx.x * K + k] >= 0);
+    if (lane == 0) sw[w][k] = __popcll(m);
+  }
+  __syncthreads();
+  for (int k = 0; k < K; ++k) {
+    const int src = snb[threadIdx.x * K + k];
+    const unsigned long long m = __ballot(src >= 0);
+    if (src < 0) continue;
+    int pos = base[(long long)k * nb + blockIdx.x];
+    for (int ww = 0; ww < w; ++ww) pos += sw[ww][k];
+    pos += __popcll(m & below);
+    pairs[pos] = make_int2(r, src);
+  }
+}
+
+// the block -> (offset, slice) assignment every block and the reduce recompute from the K + 1 offsets
+__device__ __forceinline__ void pair_blocks(const int* koff, int K, int S, int* kb) {
+  const long long P = koff[K];
+  kb[0] = 0;
+  for (int k = 0; k < K; ++k) {
+    const long long c = koff[k + 1] - koff[k];
+    kb[k + 1] = kb[k] + (c > 0 ? (int)((c * S + P - 1) / P) : 0);
+  }
+}
+
+template <int CI, int CO, bool HF16 = false>
+__global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_pairs(
+    const u16* __restrict__ h, int HP, const int2* __restrict__ pairs, const int* __restrict__ base, int nb, int K,
+    int S, const u16* __restrict__ dz, int DP, float* __restrict__ part) {
+  constexpr int RT = 64, SEG = 512;
+  constexpr int CIR = (CI + 15) / 16 * 16;
+  constexpr int PA = CIR + 16, PD = CO + 16;
+  constexpr int MT = CIR / 16, NT = CO / 16;
+  constexpr int WM = MT < 4 ? MT : 4, WN = 4 / WM;
+  constexpr int WMT = MT / WM, WNT = (NT + WN - 1) / WN, TPW = WMT * WNT;
+  constexpr int CA = (CI + 7) / 8, CD = CO / 8;
+  constexpr int NA = (RT * CA + BLK - 1) / BLK, ND = (RT * CD + BLK - 1) / BLK;
+  __shared__ __attribute__((aligned(16))) u16 sA[RT * PA];
+  __shared__ __attribute__((aligned(16))) u16 sD[RT * PD];
+  __shared__ int2 sP[SEG];
+  __shared__ int skoff[MAXK + 1], skb[MAXK + 1];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int wm = w % WM, wn = w / WM;
+  if (tid <= K) skoff[tid] = base[(long long)tid * nb];
+  __syncthreads();
+  if (tid == 0) pair_blocks(skoff, K, S, skb);
+  __syncthreads();
+  const int b = blockIdx.x;
+  if (b >= skb[K]) return;   // uniform: a spare block of the S + K grid
+  int k = 0;
+  while (skb[k + 1] <= b) ++k;
+  const long long cnt = skoff[k + 1] - skoff[k];
+  const int nbk = skb[k + 1] - skb[k], i = b - skb[k];
+  const int p0 = skoff[k] + (int)(cnt * i / nbk), p1 = skoff[k] + (int)(cnt * (i + 1) / nbk);
+  f32x4 acc[TPW];
+#pragma unroll
+  for (int t = 0; t < TPW; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
+  if (CIR != CI)
+    for (int q = tid; q < RT * PA; q += BLK) sA[q] = 0;
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
+  const int rowoff = 4 * g4 + qq;
+  // register prefetch PF sub-tiles ahead: one. Two measured slower (64 x 64: 50.9 -> 57.6 us in the step,
+  // CenterPoint 358 -> 409 us, profiles/r04_wgrad_pairs_ab.txt); kept as a compile-time choice
+  constexpr int PF = 1;
+  uint4 ra0[NA], rd0[ND], ra1[NA], rd1[ND];
+  for (int seg = p0; seg < p1; seg += SEG) {
+    const int se = min(p1, seg + SEG), len = se - seg;
+    __syncthreads();
+    for (int q = tid; q < SEG; q += BLK) sP[q] = q < len ? pairs[seg + q] : make_int2(-1, -1);
+    __syncthreads();
+    auto load = [&](int rs, uint4 (&ra)[NA], uint4 (&rd)[ND]) {
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const int q = tid + j * BLK;
+        rd[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (q < RT * CD) {
+          const int r = q / CD, c8 = q - r * CD;
+          const int row = rs + r < SEG ? sP[rs + r].x : -1;
+          if (row >= 0) rd[j] = *(const uint4*)(dz + (long long)row * DP + c8 * 8);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int q = tid + j * BLK;
+        ra[j] = make_uint4(0u, 0u, 0u, 0u);
+        if (q < RT * CA) {
+          const int r = q / CA, c8 = q - r * CA;
+          const int src = rs + r < SEG ? sP[rs + r].y : -1;
+          if (src >= 0) ra[j] = *(const uint4*)(h + (long long)src * HP + c8 * 8);
+        }
+      }
+    };
+    auto stage = [&](const uint4 (&ra)[NA], const uint4 (&rd)[ND]) {
+      __syncthreads();   // the previous sub-tile's MFMAs are done with the LDS tiles
+#pragma unroll
+      for (int j = 0; j < ND; ++j) {
+        const int q = tid + j * BLK;
+        if (q < RT * CD) {
+          const int r = q / CD, c8 = q - r * CD;
+          *(uint4*)&sD[r * PD + c8 * 8] = rd[j];
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int q = tid + j * BLK;
+        if (q < RT * CA) {
+          const int r = q / CA, c8 = q - r * CA;
+          *(uint4*)&sA[r * PA + c8 * 8] = HF16 ? f16x8_to_bf16x8(ra[j]) : ra[j];
+        }
+      }
+      __syncthreads();
+    };
+    auto mma = [&]() {
+#pragma unroll
+      for (int ks = 0; ks < RT / 32; ++ks) {
+        const int r0 = 32 * ks + rowoff;
+        bf16x8 bv[WNT];
+#pragma unroll
+        for (int bb = 0; bb < WNT; ++bb) {
+          const int n = wn + WN * bb;
+          s16x4 x[2] = {tr_read(&sD[r0 * PD + n * 16 + 4 * pp]), tr_read(&sD[(r0 + 16) * PD + n * 16 + 4 * pp])};
+          bv[bb] = *(bf16x8*)x;
+        }
+#pragma unroll
+        for (int a = 0; a < WMT; ++a) {
+          const int m = wm + WM * a;
+          s16x4 x[2] = {tr_read(&sA[r0 * PA + m * 16 + 4 * pp]), tr_read(&sA[(r0 + 16) * PA + m * 16 + 4 * pp])};
+          const bf16x8 av = *(bf16x8*)x;
+#pragma unroll
+          for (int bb = 0; bb < WNT; ++bb)
+            acc[a * WNT + bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bb], acc[a * WNT + bb], 0, 0, 0);
+        }
+      }
+    };
+    load(0, ra0, rd0);
+    if (PF == 2 && RT < len) load(RT, ra1, rd1);
+    for (int rs = 0; rs < len; rs += RT * PF) {
+      stage(ra0, rd0);
+      if (rs + PF * RT < len) load(rs + PF * RT, ra0, rd0);   // in flight during the MFMAs below
+      mma();
+      if constexpr (PF == 2) {
+        if (rs + RT >= len) break;
+        stage(ra1, rd1);
+        if (rs + 3 * RT < len) load(rs + 3 * RT, ra1, rd1);
+        mma();
+      }
+    }
+  }
+  float* out = part + (long long)b * CI * CO;
+#pragma unroll
+  for (int a = 0; a < WMT; ++a)
+#pragma unroll
+    for (int bb = 0; bb < WNT; ++bb) {
+      const int m = wm + WM * a, n = wn + WN * bb;
+      if (n >= NT) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ci = m * 16 + (lane >> 4) * 4 + j, co = n * 16 + (lane & 15);
+        if (ci < CI) out[ci * CO + co] = acc[a * WNT + bb][j];
+      }
+    }
+}
+
+// dW[k][e] = sum of the partials of offset k's blocks, in block order (8 interleaved sums, fixed combine)
+__global__ __launch_bounds__(BLK) void k_pair_reduce(const float* __restrict__ part, const int* __restrict__ base,
+                                                     int nb, int K, int S, long long per, float* __restrict__ dW) {
+  __shared__ int skoff[MAXK + 1], skb[MAXK + 1];
+  if (threadIdx.x <= K) skoff[threadIdx.x] = base[(long long)threadIdx.x * nb];
+  __syncthreads();
+  if (threadIdx.x == 0) pair_blocks(skoff, K, S, skb);
+  __syncthreads();
+  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (e >= per * K) return;
+  const int k = (int)(e / per);
+  const long long j = e - (long long)k * per;
+  const int b0 = skb[k], b1 = skb[k + 1];
+  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  int bb = b0;
+  for (; bb + 8 <= b1; bb += 8) {   // 8 loads in flight
+    float v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = part[(long long)(bb + u) * per + j];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s[u] += v[u];
+  }
+  for (int u = 0; bb < b1; ++bb, ++u) s[u] += part[(long long)bb * per + j];
+  dW[e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+template <int CI, int CO>
+static int pairs_slots() {   // resident k_wgrad_pairs blocks on the device
+  static int r = 0;
+  if (r == 0) {
+    int per = 0, dev = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wgrad_pairs<CI, CO>, BLK, 0) != hipSuccess || per <= 0)
+      per = 1;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+    r = per * cus;
+  }
+  return r;
+}
+
 template <int KGP, int NT>
 static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
   constexpr int GW = gw_of(KGP, NT), GBM = 16 * rt_of(KGP, NT) * GW;
@@ -1372,7 +1636,122 @@ static int wgrad_chunks(int n, int kvol, int ci, int co) {
   return c;
 }
 
+static int pairs_slots_dyn(int ci, int co) {
+#define PS(a, b) if (ci == a && co == b) return pairs_slots<a, b>();
+  PS(16, 16) PS(16, 32) PS(32, 32) PS(32, 64) PS(64, 64) PS(64, 128) PS(128, 128)
+#undef PS
+  return 0;
+}
+
+struct PairWs {
+  int* cnt;
+  int* base;
+  void* scan_tmp;
+  size_t scan_bytes;
+  int2* pairs;
+  float* part;
+  size_t total;
+};
+
+static int pair_ws(int n_out, int kvol, int ci, int co, char* w, PairWs* o) {
+  const int S = pairs_slots_dyn(ci, co);
+  if (S <= 0) return RPC_ERR_UNSUPPORTED;
+  const int nb = cdiv(n_out > 0 ? n_out : 1, PRB);
+  const long long nc = (long long)kvol * nb + 1;
+  size_t scan_b = 0;
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (const int*)nullptr, (int*)nullptr, (int)nc, (hipStream_t)0) !=
+      hipSuccess)
+    return RPC_ERR_HIP;
+  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
+  size_t off = 0;
+  o->cnt = (int*)(w + off);
+  off += al(sizeof(int) * nc);
+  o->base = (int*)(w + off);
+  off += al(sizeof(int) * nc);
+  o->scan_tmp = w + off;
+  o->scan_bytes = scan_b;
+  off += al(scan_b);
+  o->pairs = (int2*)(w + off);
+  off += al(sizeof(int2) * (size_t)(n_out > 0 ? n_out : 1) * kvol);
+  o->part = (float*)(w + off);
+  off += al(sizeof(float) * (size_t)(S + kvol) * ci * co);
+  o->total = off;
+  return RPC_OK;
+}
+
+extern "C" size_t rpc_spconv_wgrad_pairs_workspace_size(int n_out, int kvol, int ci, int co) {
+  PairWs o;
+  if (n_out < 0 || kvol < 1 || kvol > MAXK || pair_ws(n_out, kvol, ci, co, nullptr, &o)) return 0;
+  return o.total;
+}
+
+// the same weight gradient as rpc_spconv_wgrad_h16 over per-offset pair lists built from nbr here
+extern "C" int rpc_spconv_wgrad_pairs(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out,
+                                      const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
+  if (hfmt != 0 && hfmt != 1) return RPC_ERR_ARG;
+  if (n_out < 0 || kvol < 1 || kvol > MAXK || !h || !nbr || !dz || !dW || !ws) return RPC_ERR_ARG;
+  hipStream_t st = (hipStream_t)stream;
+  if (n_out == 0) {
+    RPC_CHECK(hipMemsetAsync(dW, 0, sizeof(float) * (size_t)kvol * ci * co, st));
+    return RPC_OK;
+  }
+  if ((long long)n_out * kvol >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
+  PairWs o;
+  int rc = pair_ws(n_out, kvol, ci, co, (char*)ws, &o);
+  if (rc) return rc;
+  if (ws_bytes < o.total) return RPC_ERR_WORKSPACE;
+  const int S = pairs_slots_dyn(ci, co), nb = cdiv(n_out, PRB);
+  const int nc = kvol * nb + 1;
+  hipLaunchKernelGGL(k_pair_count, dim3(nb), dim3(PRB), 0, st, nbr, n_out, kvol, nb, o.cnt);
+  RPC_LAUNCH_CHECK();
+  size_t sb = o.scan_bytes;
+  if (hipcub::DeviceScan::ExclusiveSum(o.scan_tmp, sb, o.cnt, o.base, nc, st) != hipSuccess) return RPC_ERR_HIP;
+  hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(PRB), 0, st, nbr, n_out, kvol, nb, (const int*)o.base, o.pairs);
+  RPC_LAUNCH_CHECK();
+  const u16* hp = (const u16*)h;
+  const u16* dp = (const u16*)dz;
+  const int HP = r8(ci), DP = r8(co);
+  const dim3 grid(S + kvol);
+#define W2(a, b)                                                                                              \
+  if (ci == a && co == b) {                                                                                  \
+    if (hfmt)                                                                                                \
+      hipLaunchKernelGGL((k_wgrad_pairs<a, b, true>), grid, dim3(BLK), 0, st, hp, HP, (const int2*)o.pairs,    \
+                         (const int*)o.base, nb, kvol, S, dp, DP, o.part);                                    \
+    else                                                                                                     \
+      hipLaunchKernelGGL((k_wgrad_pairs<a, b>), grid, dim3(BLK), 0, st, hp, HP, (const int2*)o.pairs,          \
+                         (const int*)o.base, nb, kvol, S, dp, DP, o.part);                                    \
+  } else
+  W2(16, 16) W2(16, 32) W2(32, 32) W2(32, 64) W2(64, 64) W2(64, 128) W2(128, 128)
+  { return RPC_ERR_UNSUPPORTED; }
+#undef W2
+  RPC_LAUNCH_CHECK();
+  const long long per = (long long)ci * co;
+  hipLaunchKernelGGL(k_pair_reduce, dim3((unsigned)((per * kvol + BLK - 1) / BLK)), dim3(BLK), 0, st,
+                     (const float*)o.part, (const int*)o.base, nb, kvol, S, per, dW);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_spconv_wgrad_pairs(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out,
+                                      const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream);
+// RPC_SPWG_PAIRS=1 (A/B): the pair-list weight gradient behind rpc_spconv_wgrad_h16. Off by default: measured
+// on the step (profiles/r04_wgrad_pairs_ab.txt) the weight-gradient kernel gets only 10-25 % faster
+// (k_wgrad_bf16<64,64,3> 69.6 -> 50.9 us; CenterPoint <128,128> 449 -> 354 us) — rows without a neighbour
+// at an offset were cheap already (contiguous dz rows, no h gather, zero MFMA rows) and the time is the
+// per-sub-tile gather round trip, which the pairs keep — while the compaction (count + scan + scatter per
+// layer: 10-50 us) and the per-offset reduce eat the gain: SECOND 7.16 -> 7.65 ms/step, CenterPoint
+// 150.0 -> 147.1 frames/s
+static bool wgrad_pairs_mode() {
+  static int m = -1;
+  if (m < 0) {
+    const char* e = getenv("RPC_SPWG_PAIRS");
+    m = (e && atoi(e) != 0) ? 1 : 0;
+  }
+  return m == 1;
+}
+
 extern "C" size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co) {
+  if (wgrad_pairs_mode() && pairs_slots_dyn(ci, co) > 0) return rpc_spconv_wgrad_pairs_workspace_size(n_out, kvol, ci, co);
   return (size_t)wgrad_chunks(n_out, kvol, ci, co) * kvol * ci * co * sizeof(float);
 }
 
@@ -1389,6 +1768,8 @@ extern "C" int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* 
                                     const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
   if (hfmt != 0 && hfmt != 1) return RPC_ERR_ARG;
   if (n_out < 0 || kvol < 1 || kvol > MAXK) return RPC_ERR_ARG;
+  if (wgrad_pairs_mode() && pairs_slots_dyn(ci, co) > 0)
+    return rpc_spconv_wgrad_pairs(h, hfmt, ci, nbr, kvol, n_out, dz, co, dW, ws, ws_bytes, stream);
   bool ok = (ci == 16 && (co == 16 || co == 32)) || (ci == 32 && (co == 32 || co == 64)) ||
             (ci == 64 && (co == 64 || co == 128)) || (ci == 128 && co == 128);
   if (!ok) return RPC_ERR_UNSUPPORTED;

@@ -678,6 +678,19 @@ int rpc_dcn_forward_f32(const float* x, int xp, const float* off, int offp, cons
 int rpc_dcn_backward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias, const float* W,
                          const float* dout, int dop, float* dx, float* doff, int doffp, float* doff_bias, float* dW,
                          int B, int H, int W_, void* workspace, size_t ws_bytes, void* stream);
+/* rpc_dcn_backward / _f32 with the offset-gradient channel count: doff_channels = 64 is the calls above
+ * (a padded image of its own), 18 writes exactly the 18 offset channels at doff (4-byte aligned bf16 /
+ * 8-byte aligned fp32, doffp >= 18 and even), so several DCNs can write their slices of ONE image: the
+ * output gradient of the head's concatenated offset conv (12 offset convs of a CenterPoint head as one
+ * 64 -> 216 (+40 zero) conv, DCN j at channel 18 j, pitch 256; center_head.py). */
+int rpc_dcn_backward_ex(const void* x, int xp, const void* off, int offp, const float* off_bias, const void* w_bwd,
+                        const void* dout, int dop, float* dx, void* doff, int doffp, int doff_channels,
+                        float* doff_bias, float* dW, int B, int H, int W, void* workspace, size_t ws_bytes,
+                        void* stream);
+int rpc_dcn_backward_f32_ex(const float* x, int xp, const float* off, int offp, const float* off_bias,
+                            const float* W, const float* dout, int dop, float* dx, float* doff, int doffp,
+                            int doff_channels, float* doff_bias, float* dW, int B, int H, int W_, void* workspace,
+                            size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

@@ -211,6 +211,10 @@ SIGNATURES = {
     "rpc_dcn_forward_f32": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, i32, i32, i32, vp]),
     "rpc_dcn_backward_f32": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, vp, vp, i32, i32, i32, vp, sz,
                                    vp]),
+    "rpc_dcn_backward_ex": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, i32, vp, vp, i32, i32, i32, vp, sz,
+                                  vp]),
+    "rpc_dcn_backward_f32_ex": (i32, [vp, i32, vp, i32, vp, vp, vp, i32, vp, vp, i32, i32, vp, vp, i32, i32, i32, vp,
+                                      sz, vp]),
     "rpc_head_pack_f32": (i32, [vp, i32, i32, vp, vp, i32, i32, C.c_longlong, vp]),
     "rpc_head_unpack_grad_f32": (i32, [vp, i32, i32, i32, vp, i32, C.c_longlong, vp, vp, sz, vp]),
     "rpc_sparse_res_forward": (i32, [vp, vp, vp, i32, i32, vp, vp, vp]),

@@ -206,12 +206,45 @@ def _imgs(B, H, W):
     return (B, H, W), (B, H, W), (B, H, W)
 
 
+def _reg_blockdiag(head):
+    """Every task's five separate-head final convs (64 -> n_i, i over _BOX_ORDER, each reading its own
+    64-channel slice of the 320-channel reg image) as ONE 320 -> sum(n_i) conv per task: the weight is
+    block-diagonal (output rows of head i read only input channels 64 i .. 64 i + 63), so it does the
+    same MACs as the five convs in one launch and its data gradient lands in the 320-channel image
+    directly. Built for all tasks at once (one cat + one scatter): [tasks * nr, 5 * 64, 3, 3] fp32, and
+    the (row, block) index of every real weight row for splitting the gradient back."""
+    ws, blk = [], []
+    for th in head.task_heads:
+        for i, name in enumerate(_BOX_ORDER):
+            w = getattr(th.task_head, name)[1].weight
+            ws.append(w.detach().float().reshape(w.shape[0], -1))
+            blk.extend([i] * w.shape[0])
+    nb = len(_BOX_ORDER)
+    Wall = torch.cat(ws)
+    rows = Wall.shape[0]
+    key = (rows, tuple(blk), Wall.device)
+    idx = _BD_IDX.get(key)
+    if idx is None:
+        idx = (torch.arange(rows, device=Wall.device), torch.tensor(blk, device=Wall.device))
+        _BD_IDX.clear()
+        _BD_IDX[key] = idx
+    Wbd = torch.zeros((rows, nb, Wall.shape[1]), dtype=torch.float32, device=Wall.device)
+    Wbd[idx] = Wall
+    return Wbd.view(rows, nb * 64, 3, 3), idx
+
+
+_BD_IDX = {}
+
+
 def _prep_head(eng, head, dev, st):
-    """Every dense-engine weight operand of the head in ceil(85 / 16) batched launches (one launch per
-    conv cost ~15 us each: 1.35 ms per CenterPoint step): id(conv) -> (forward, data-gradient) operands.
-    The task heads' final convs and the DCN offset convs are padded to 64 output channels in the kernel
-    (RpcDenseWprep.co_src) instead of through a zero-filled fp32 copy."""
+    """Every dense-engine weight operand of the head in batched launches (one launch per conv cost ~15 us
+    each: 1.35 ms per CenterPoint step): key -> (forward, data-gradient) operands. Small convs are padded
+    to 64 output channels in the kernel (RpcDenseWprep.co_src) instead of through a zero-filled fp32 copy.
+    The 2 * tasks DCN offset convs (all reading the shared-conv image) are ONE 64 -> 18 * 2 * tasks conv
+    ("offcat", padded to a multiple of 64 outputs), each task's five reg final convs one block-diagonal
+    320 -> sum(n_i) conv ("regbd")."""
     items = []
+    out = {}
 
     def add(conv, pad=False):
         W = conv.weight.detach().float().contiguous()
@@ -219,17 +252,25 @@ def _prep_head(eng, head, dev, st):
         items.append((id(conv), W, ci, _PAD if pad else co, co if pad else 0))
 
     add(head.shared_conv.conv)
-    for th in head.task_heads:
-        for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
-            add(dcn.conv_offset, True)
+    offs = [dcn.conv_offset.weight.detach().float() for th in head.task_heads
+            for dcn in (th.feature_adapt_cls, th.feature_adapt_reg)]
+    Woff = torch.cat(offs).contiguous()
+    nof = Woff.shape[0]
+    items.append((("offcat",), Woff, Woff.shape[1], -(-nof // 64) * 64, nof))
+    out[("offcat", "n")] = nof
+    Wbd, bd_idx = _reg_blockdiag(head)
+    out[("regbd", "idx")] = bd_idx
+    nr = Wbd.shape[0] // len(head.task_heads)
+    for t, th in enumerate(head.task_heads):
         add(th.cls_head[0].conv)
         add(th.cls_head[1], True)
         cms = [getattr(th.task_head, name)[0] for name in _BOX_ORDER]
         Wcat = torch.cat([cm.conv.weight.detach().float() for cm in cms]).contiguous()
         items.append((("regcat", id(th)), Wcat, Wcat.shape[1], Wcat.shape[0], 0))
-        for name in _BOX_ORDER:
-            add(getattr(th.task_head, name)[1], True)
-    out = {}
+        out[("regcat", id(th), "W")] = Wcat
+        if nr > _PAD:
+            raise NotImplementedError("CenterHead: more than 64 box channels per task")
+        items.append((("regbd", id(th)), Wbd[nr * t:nr * (t + 1)], Wbd.shape[1], _PAD, nr))
     for g0 in range(0, len(items), 16):
         grp = items[g0:g0 + 16]
         descs = (_ffi.RpcDenseWprep * len(grp))()
@@ -238,8 +279,6 @@ def _prep_head(eng, head, dev, st):
             wd = torch.empty((9, ci, co), dtype=eng.dt, device=dev)
             descs[i] = _ffi.RpcDenseWprep(W.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, co, 9, 1, co_src)
             out[key] = (wf, wd)
-            if isinstance(key, tuple):
-                out[key + ("W",)] = W
         _ffi.check(eng.wprep_batch(descs, len(grp), st), "rpc_dense_wprep_batch")
     return out
 
@@ -272,38 +311,39 @@ class _CatConv:
         self.weight = weight
 
 
-def _conv_nobn_fwd(eng, weight, ci, h, pitch, B, H, W, dev, st, wts=None):
-    """3x3 conv (no BN) on the dense engine (bf16 or fp32) with the outputs padded to 64 ->
+def _conv_nobn_fwd(eng, weight, ci, h, pitch, B, H, W, dev, st, wts=None, n=None, co=_PAD):
+    """3x3 conv (no BN) on the dense engine (bf16 or fp32) with the n real outputs padded to co ->
     (z image, record). wts: (forward, data-gradient) operands from _prep_head, else prepared here."""
-    n = weight.shape[0]
+    n = weight.shape[0] if n is None else n
     if wts is None:
         W32 = weight.detach().float().contiguous()
-        wf = torch.empty((9, _PAD, ci), dtype=eng.dt, device=dev)
-        wd = torch.empty((9, ci, _PAD), dtype=eng.dt, device=dev)
-        desc = (_ffi.RpcDenseWprep * 1)(_ffi.RpcDenseWprep(W32.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, _PAD,
+        wf = torch.empty((9, co, ci), dtype=eng.dt, device=dev)
+        wd = torch.empty((9, ci, co), dtype=eng.dt, device=dev)
+        desc = (_ffi.RpcDenseWprep * 1)(_ffi.RpcDenseWprep(W32.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, ci, co,
                                                            9, 1, n))
         _ffi.check(eng.wprep_batch(desc, 1, st), "rpc_dense_wprep_batch")
     else:
         wf, wd = wts
-    z = db._image(B, _PAD, H, W, dev, eng.dt)
+    z = db._image(B, co, H, W, dev, eng.dt)
     R = _ffi.int_arr((B, H, W))
-    _ffi.check(eng.conv(db.S1, _ffi.ptr(h), pitch, ci, _ffi.ptr(wf), _PAD, _ffi.ptr(z), _PAD, 0, 0, None, R, R, R,
+    _ffi.check(eng.conv(db.S1, _ffi.ptr(h), pitch, ci, _ffi.ptr(wf), co, _ffi.ptr(z), co, 0, 0, None, R, R, R,
                         st), "rpc_dense_conv")
-    return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, B=B, H=H, W=W)
+    return z, dict(h=h, pitch=pitch, wd=wd, ci=ci, n=n, co=co, B=B, H=H, W=W)
 
 
 def _conv_nobn_bwd(eng, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=False, dx_pitch=None):
-    ci, B, H, W = rec["ci"], rec["B"], rec["H"], rec["W"]
+    """dz: the padded output gradient image (rec["co"] channels, the padding zero) -> (dx, dW[:n])."""
+    ci, co, B, H, W = rec["ci"], rec["co"], rec["B"], rec["H"], rec["W"]
     R = _ffi.int_arr((B, H, W))
-    dW = torch.empty((_PAD, ci, 3, 3), dtype=torch.float32, device=dev)
-    wsz = eng.wgrad_ws(db.S1, R, ci, _PAD)
+    dW = torch.empty((co, ci, 3, 3), dtype=torch.float32, device=dev)
+    wsz = eng.wgrad_ws(db.S1, R, ci, co)
     ws = _ffi.workspace(wsz, dev)
-    _ffi.check(eng.wgrad(db.S1, 0, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), _PAD, _PAD, R, R, R,
+    _ffi.check(eng.wgrad(db.S1, 0, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), co, co, R, R, R,
                          _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
     dx = None
     if need_dx:
         dx = dx_out if dx_out is not None else db._image(B, ci, H, W, dev, eng.dt)
-        _ffi.check(eng.conv(db.S1, _ffi.ptr(dz), _PAD, _PAD, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), dx_pitch or ci, 0,
+        _ffi.check(eng.conv(db.S1, _ffi.ptr(dz), co, co, _ffi.ptr(rec["wd"]), ci, _ffi.ptr(dx), dx_pitch or ci, 0,
                             1 if accumulate else 0, None, R, R, R, st), "rpc_dense_conv(dgrad)")
     return dx, dW[:rec["n"]]
 
@@ -342,16 +382,20 @@ class CenterHeadFn(torch.autograd.Function):
         bns = [head.shared_conv.bn]
         trecs = []
         c0 = 0
+        # the DCN offsets of every task and branch: one 64 -> 18 * 2 * tasks conv of the shared image
+        nof = prep[("offcat", "n")]
+        cof = -(-nof // 64) * 64
+        ozc, orec = _conv_nobn_fwd(eng, None, 64, y0, 64, B, H, W, dev, st, prep[("offcat",)], n=nof, co=cof)
         for t, th in enumerate(head.task_heads):
             tr = {}
             for br, dcn in (("cls", th.feature_adapt_cls), ("reg", th.feature_adapt_reg)):
-                oz, orec = _conv_nobn_fwd(eng, dcn.conv_offset.weight, 64, y0, 64, B, H, W, dev, st,
-                                          prep[id(dcn.conv_offset)])
+                j = 2 * t + (br == "reg")
+                oz = ozc[:, 18 * j:18 * (j + 1)]
                 ob = dcn.conv_offset.bias.detach().float().contiguous()
                 feat = db._image(B, 64, H, W, dev, eng.dt)
                 if f32:
                     wdd = dcn.weight.detach().float().contiguous()
-                    _ffi.check(lib.rpc_dcn_forward_f32(_ffi.ptr(y0), 64, _ffi.ptr(oz), _PAD, _ffi.ptr(ob),
+                    _ffi.check(lib.rpc_dcn_forward_f32(_ffi.ptr(y0), 64, _ffi.ptr(oz), cof, _ffi.ptr(ob),
                                                        _ffi.ptr(wdd), _ffi.ptr(feat), 64, B, H, W, st),
                                "rpc_dcn_forward_f32")
                 else:
@@ -359,9 +403,9 @@ class CenterHeadFn(torch.autograd.Function):
                     wdd = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=dev)
                     _ffi.check(lib.rpc_dcn_prep_weight(_ffi.ptr(dcn.weight.detach().float().contiguous()),
                                                        _ffi.ptr(wf), _ffi.ptr(wdd), st), "rpc_dcn_prep_weight")
-                    _ffi.check(lib.rpc_dcn_forward(_ffi.ptr(y0), 64, _ffi.ptr(oz), _PAD, _ffi.ptr(ob), _ffi.ptr(wf),
+                    _ffi.check(lib.rpc_dcn_forward(_ffi.ptr(y0), 64, _ffi.ptr(oz), cof, _ffi.ptr(ob), _ffi.ptr(wf),
                                                    _ffi.ptr(feat), 64, B, H, W, st), "rpc_dcn_forward")
-                tr[br] = dict(dcn=dcn, oz=oz, orec=orec, wd=wdd, ob=ob, feat=feat)
+                tr[br] = dict(dcn=dcn, oz=oz, j=j, wd=wdd, ob=ob, feat=feat)
             # cls branch -> heatmap logits
             L = _conv_module_layer(th.cls_head[0])
             hcls, rc, _, _ = db._forward_layer(eng, L, tr["cls"]["feat"], 64, B, H, W, training, dev, st,
@@ -374,7 +418,8 @@ class CenterHeadFn(torch.autograd.Function):
             tr["cls_layers"] = (rc, frec, fc, c0, th.num_cls, hm, head.hm_pitch)
             c0 += th.num_cls
             # reg branches -> anno_box channels: the five ConvModules of the separate head share their input
-            # (the DCN feature): one 64 -> 320 conv + BatchNorm + ReLU, the final convs read 64-channel slices
+            # (the DCN feature): one 64 -> 320 conv + BatchNorm + ReLU; the five final convs as one
+            # block-diagonal 320 -> sum(n_i) conv whose outputs are the task's contiguous anno_box channels
             cms = [getattr(th.task_head, name)[0] for name in _BOX_ORDER]
             cbn = _CatBN([cm.bn for cm in cms])
             Lr = db._Layer(db.S1, _CatConv(prep[("regcat", id(th), "W")]), cbn, 0, 64, 64 * len(cms), 9)
@@ -383,22 +428,20 @@ class CenterHeadFn(torch.autograd.Function):
             if training:
                 cbn.write_back()
             bns.extend(cbn.bns)
-            regs, bo = [], 10 * t
-            for i, name in enumerate(_BOX_ORDER):
-                fcv = getattr(th.task_head, name)[1]
-                n = fcv.weight.shape[0]
-                z, frec = _conv_nobn_fwd(eng, fcv.weight, 64, hr[:, 64 * i:64 * (i + 1)], 64 * len(cms), B, H, W,
-                                         dev, st, prep[id(fcv)])
-                _ffi.check(pack(_ffi.ptr(z), _PAD, n, _ffi.ptr(fcv.bias.detach().float().contiguous()),
-                                             _ffi.ptr(box), head.box_pitch, bo, cells, st), "rpc_head_pack")
-                regs.append((frec, fcv, bo, n))
-                bo += n
+            fcs = [getattr(th.task_head, name)[1] for name in _BOX_ORDER]
+            nb = sum(f.weight.shape[0] for f in fcs)
+            z, frec = _conv_nobn_fwd(eng, None, 64 * len(cms), hr, 64 * len(cms), B, H, W, dev, st,
+                                     prep[("regbd", id(th))], n=nb)
+            bcat = torch.cat([f.bias.detach().float() for f in fcs])
+            _ffi.check(pack(_ffi.ptr(z), _PAD, nb, _ffi.ptr(bcat), _ffi.ptr(box), head.box_pitch, 10 * t, cells, st),
+                       "rpc_head_pack")
             tr["reg_cm"] = (rr, cms)
-            tr["regs"] = regs
+            tr["regs"] = (frec, fcs, 10 * t, nb)
             trecs.append(tr)
         if training:
             _ffi.bump_batches(bns)
-        ctx.head, ctx.rsh, ctx.trecs = head, rsh, trecs
+        ctx.head, ctx.rsh, ctx.trecs, ctx.orec = head, rsh, trecs, orec
+        ctx.bd_idx = prep[("regbd", "idx")]
         ctx.shape = (B, H, W, Cin)
         ctx.f32 = f32
         ctx.param_list = params
@@ -422,63 +465,68 @@ class CenterHeadFn(torch.autograd.Function):
         uwsz = lib.rpc_head_unpack_workspace_size()
         uws = _ffi.workspace(uwsz, dev)
         dY0f = torch.zeros((cells, 64), dtype=torch.float32, device=dev)     # DCN input gradients
-        dY0b = None                                                           # offset-conv data gradients
         dwsz = lib.rpc_dcn_backward_workspace_size(B, H, W)
         dws = _ffi.workspace(dwsz, dev)
+        orec = ctx.orec
+        cof = orec["co"]
+        # the concatenated offset conv's output gradient: every DCN writes its 18 channels (channel 18 j),
+        # the padding channels stay zero
+        doffc = torch.zeros((B, H, W, cof), dtype=eng.dt, device=dev).permute(0, 3, 1, 2)
 
         unpack = lib.rpc_head_unpack_grad_f32 if f32 else lib.rpc_head_unpack_grad
 
-        def final_conv_bwd(frec, conv, g, gp, off, n, dx_out=None, dx_pitch=None):
+        def final_conv_bwd(frec, g, gp, off, n, dx_out=None, dx_pitch=None):
             dz = db._image(B, _PAD, H, W, dev, eng.dt)
             db_ = torch.empty(n, dtype=torch.float32, device=dev)
             _ffi.check(unpack(_ffi.ptr(g), gp, off, n, _ffi.ptr(dz), _PAD, cells, _ffi.ptr(db_),
                               _ffi.ptr(uws), uwsz, st), "rpc_head_unpack_grad")
             dh, dW = _conv_nobn_bwd(eng, frec, dz, dev, st, True, dx_out, False, dx_pitch)
-            grads[id(conv.weight)], grads[id(conv.bias)] = dW, db_
-            return dh
+            return dh, dW, db_
 
-        def head_branch(rec_cm, frec, conv, g, gp, off, n, dfeat, acc):
-            dh = final_conv_bwd(frec, conv, g, gp, off, n)
-            dfeat, dWc, dg, dbt, _ = db._backward_layer(eng, rec_cm, dh, 64, 0, dev, st, True, dfeat, acc)
-            L = rec_cm["L"]
-            grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWc, dg, dbt
-            return dfeat
-
+        rows, blk = ctx.bd_idx
+        rb = 0
         for t, tr in enumerate(ctx.trecs):
             rc, frec, fc, c0, ncls, _, hp = tr["cls_layers"]
-            dfc = head_branch(rc, frec, fc, ghm, hp, c0, ncls, None, False)
-            # reg: the five final convs' data gradients into 64-channel slices of one 320-channel image, then
-            # the concatenated ConvModule's backward (gradients split back per module)
+            dh, grads[id(fc.weight)], grads[id(fc.bias)] = final_conv_bwd(frec, ghm, hp, c0, ncls)
+            dfc, dWc, dg, dbt, _ = db._backward_layer(eng, rc, dh, 64, 0, dev, st, True)
+            L = rc["L"]
+            grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWc, dg, dbt
+            # reg: the block-diagonal final conv's data gradient is the 320-channel image of the concatenated
+            # ConvModule; its weight gradient's diagonal blocks are the five final convs' (gathered in one op)
             rr, cms = tr["reg_cm"]
             nct = 64 * len(cms)
-            dh_cat = db._image(B, nct, H, W, dev, eng.dt)
-            for i, (frec2, fcv, bo, n) in enumerate(tr["regs"]):
-                final_conv_bwd(frec2, fcv, gbox, head.box_pitch, bo, n, dh_cat[:, 64 * i:64 * (i + 1)], nct)
+            frec2, fcs, bo, nb = tr["regs"]
+            dh_cat, dWbd, dbb = final_conv_bwd(frec2, gbox, head.box_pitch, bo, nb)
+            dWr = dWbd.reshape(nb, len(cms), -1)[rows[:nb], blk[rb:rb + nb]]
+            rb += nb
+            for f, w_, b_ in zip(fcs, dWr.split([f.weight.shape[0] for f in fcs]),
+                                 dbb.split([f.weight.shape[0] for f in fcs])):
+                grads[id(f.weight)], grads[id(f.bias)] = w_.view_as(f.weight), b_
             dfr, dWc, dg, dbt, _ = db._backward_layer(eng, rr, dh_cat, nct, 0, dev, st, True)
             for cm, w_, g_, b_ in zip(cms, dWc.split(64), dg.split(64), dbt.split(64)):
                 grads[id(cm.conv.weight)], grads[id(cm.bn.weight)], grads[id(cm.bn.bias)] = w_, g_, b_
             for br, dfeat in (("cls", dfc), ("reg", dfr)):
                 d = tr[br]
-                doff = db._image(B, _PAD, H, W, dev, eng.dt)
                 dob = torch.empty(18, dtype=torch.float32, device=dev)
                 dWd = torch.empty((64, 16, 3, 3), dtype=torch.float32, device=dev)
-                dcn_bwd = lib.rpc_dcn_backward_f32 if f32 else lib.rpc_dcn_backward
-                _ffi.check(dcn_bwd(_ffi.ptr(d["orec"]["h"]), 64, _ffi.ptr(d["oz"]),
-                                                _PAD, _ffi.ptr(d["ob"]), _ffi.ptr(d["wd"]), _ffi.ptr(dfeat), 64,
-                                                _ffi.ptr(dY0f), _ffi.ptr(doff), _PAD, _ffi.ptr(dob), _ffi.ptr(dWd), B, H,
-                                                W, _ffi.ptr(dws), dwsz, st), "rpc_dcn_backward")
+                dcn_bwd = lib.rpc_dcn_backward_f32_ex if f32 else lib.rpc_dcn_backward_ex
+                _ffi.check(dcn_bwd(_ffi.ptr(orec["h"]), 64, _ffi.ptr(d["oz"]), cof, _ffi.ptr(d["ob"]), _ffi.ptr(d["wd"]),
+                                   _ffi.ptr(dfeat), 64, _ffi.ptr(dY0f), _ffi.ptr(doffc[:, 18 * d["j"]:]), cof, 18,
+                                   _ffi.ptr(dob), _ffi.ptr(dWd), B, H, W, _ffi.ptr(dws), dwsz, st), "rpc_dcn_backward")
                 dcn = d["dcn"]
                 grads[id(dcn.weight)] = dWd
                 grads[id(dcn.conv_offset.bias)] = dob
-                first = dY0b is None
-                dY0b, dWo = _conv_nobn_bwd(eng, d["orec"], doff, dev, st, True, dY0b, not first)
-                grads[id(dcn.conv_offset.weight)] = dWo
+        dY0b, dWo = _conv_nobn_bwd(eng, orec, doffc, dev, st, True)
+        for t, tr in enumerate(ctx.trecs):
+            for br in ("cls", "reg"):
+                d = tr[br]
+                grads[id(d["dcn"].conv_offset.weight)] = dWo[18 * d["j"]:18 * (d["j"] + 1)]
         dY0 = (dY0f + dY0b.permute(0, 2, 3, 1).reshape(cells, 64).float()).to(eng.dt)
         dY0 = dY0.view(B, H, W, 64).permute(0, 3, 1, 2)
         dx, dWs, dgs, dbs, _ = db._backward_layer(eng, ctx.rsh, dY0, 64, 0, dev, st, ctx.need_x)
         L = ctx.rsh["L"]
         grads[id(L.conv.weight)], grads[id(L.bnm.weight)], grads[id(L.bnm.bias)] = dWs, dgs, dbs
-        ctx.trecs = ctx.rsh = None
+        ctx.trecs = ctx.rsh = ctx.orec = None
         return (dx, None) + tuple(grads.get(id(p)) for p in ctx.param_list)
 
 

@@ -248,7 +248,7 @@ constexpr int PS = 64 + 8;     // S row pitch (elements)
 __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, int xp, const u16* __restrict__ off,
                                              int offp, const float* __restrict__ ob, const u16* __restrict__ wd,
                                              const u16* __restrict__ dout, int dop, float* __restrict__ dx,
-                                             u16* __restrict__ doff, int doffp, float* __restrict__ pw_part,
+                                             u16* __restrict__ doff, int doffp, int dch, float* __restrict__ pw_part,
                                              float* __restrict__ pb_part, float* __restrict__ win_part) {
   __shared__ __attribute__((aligned(16))) u16 sXw[WR * PW];
   __shared__ __attribute__((aligned(16))) u16 sDo[64 * P];
@@ -415,19 +415,29 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
     }
     __syncthreads();
   }
-  // offset-conv output gradient (bf16 image, channels >= 18 zero) and its bias partials
-  for (int qd = tid; qd < 64 * 8; qd += BLK) {
-    const int pp = qd >> 3, seg = qd & 7;
-    const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
-    unsigned wv[4];
+  // offset-conv output gradient (bf16 image) and its bias partials: dch = 64 writes channels 18..63 as zero
+  // (a 64-wide image of its own), dch = 18 exactly the 18 offset channels (a slice of a shared image)
+  if (dch == C) {
+    for (int qd = tid; qd < 64 * 8; qd += BLK) {
+      const int pp = qd >> 3, seg = qd & 7;
+      const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
+      unsigned wv[4];
 #pragma unroll
-    for (int h = 0; h < 4; ++h) {
-      const int c0 = seg * 8 + 2 * h;
-      const float a = c0 < 2 * KT ? sOff[pp * 2 * KT + c0] : 0.0f;
-      const float bq = c0 + 1 < 2 * KT ? sOff[pp * 2 * KT + c0 + 1] : 0.0f;
-      wv[h] = f2bf(a) | ((unsigned)f2bf(bq) << 16);
+      for (int h = 0; h < 4; ++h) {
+        const int c0 = seg * 8 + 2 * h;
+        const float a = c0 < 2 * KT ? sOff[pp * 2 * KT + c0] : 0.0f;
+        const float bq = c0 + 1 < 2 * KT ? sOff[pp * 2 * KT + c0 + 1] : 0.0f;
+        wv[h] = f2bf(a) | ((unsigned)f2bf(bq) << 16);
+      }
+      *(uint4*)(doff + ((size_t)(tl.b * g.H + yy) * g.W + xw) * doffp + seg * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
     }
-    *(uint4*)(doff + ((size_t)(tl.b * g.H + yy) * g.W + xw) * doffp + seg * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
+  } else {
+    for (int qd = tid; qd < 64 * KT; qd += BLK) {
+      const int pp = qd / KT, h = qd - pp * KT;
+      const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
+      const unsigned v = f2bf(sOff[pp * 2 * KT + 2 * h]) | ((unsigned)f2bf(sOff[pp * 2 * KT + 2 * h + 1]) << 16);
+      *(unsigned*)(doff + ((size_t)(tl.b * g.H + yy) * g.W + xw) * doffp + 2 * h) = v;
+    }
   }
   if (tid < 2 * KT) {
     float sacc = 0.0f;
@@ -572,7 +582,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_f32(Geo g, const float* __restrict_
                                                  const float* __restrict__ off, int offp,
                                                  const float* __restrict__ ob, const float* __restrict__ W,
                                                  const float* __restrict__ dout, int dop, float* __restrict__ dx,
-                                                 float* __restrict__ doff, int doffp, float* __restrict__ pw_part,
+                                                 float* __restrict__ doff, int doffp, int dch, float* __restrict__ pw_part,
                                                  float* __restrict__ pb_part, float* __restrict__ win_part) {
   __shared__ __attribute__((aligned(16))) float sW[KT * C * CG];     // [k][group][co][ci]
   __shared__ __attribute__((aligned(16))) float sWin[WR * C];        // window input gradient
@@ -672,8 +682,14 @@ __global__ __launch_bounds__(BLK) void k_bwd_f32(Geo g, const float* __restrict_
     }
     __syncthreads();
   }
-  for (int qd = tid; qd < 64 * (doffp / 4); qd += BLK) {
-    const int pp = qd / (doffp / 4), seg = qd - pp * (doffp / 4);
+  const int nseg = dch == C ? doffp / 4 : 0;   // dch = 18: exactly the offset channels (float2 stores below)
+  for (int qd = tid; dch != C && qd < 64 * KT; qd += BLK) {
+    const int pp = qd / KT, h = qd - pp * KT;
+    const size_t px = (size_t)(tl.b * g.H + tl.y0 + (pp >> 3)) * g.W + tl.x0 + (pp & 7);
+    *(float2*)(doff + px * doffp + 2 * h) = make_float2(sOff[pp * 2 * KT + 2 * h], sOff[pp * 2 * KT + 2 * h + 1]);
+  }
+  for (int qd = tid; qd < 64 * nseg; qd += BLK) {
+    const int pp = qd / nseg, seg = qd - pp * nseg;
     const size_t px = (size_t)(tl.b * g.H + tl.y0 + (pp >> 3)) * g.W + tl.x0 + (pp & 7);
     float v[4];
 #pragma unroll
@@ -729,14 +745,19 @@ extern "C" size_t rpc_dcn_backward_workspace_size(int B, int H, int W) {
   return (tiles * KT * 1024 + tiles * 2 * KT + KT * 1024 + tiles * WR * C) * sizeof(float);
 }
 
-extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp, const float* off_bias,
-                                const void* w_bwd, const void* dout, int dop, float* dx, void* doff, int doffp,
-                                float* doff_bias, float* dW, int B, int H, int W, void* workspace, size_t ws_bytes,
-                                void* stream) {
+// dch: offset-gradient channels written per pixel. C (64): a padded image of its own (channels 18..doffp-1
+// zero, 16-byte stores); 2 * KT (18): exactly the offset channels, e.g. one DCN's slice of a shared image
+// written by several DCNs (the concatenated offset conv of a CenterPoint head: doff at channel 18 j, pitch 256)
+static int dcn_backward_bf16(const void* x, int xp, const void* off, int offp, const float* off_bias,
+                             const void* w_bwd, const void* dout, int dop, float* dx, void* doff, int doffp, int dch,
+                             float* doff_bias, float* dW, int B, int H, int W, void* workspace, size_t ws_bytes,
+                             void* stream) {
   Geo g;
   if (!check_geo(B, H, W, &g)) return RPC_ERR_UNSUPPORTED;
   if (!x || !off || !off_bias || !w_bwd || !dout || !dx || !doff || !doff_bias || !dW || !workspace) return RPC_ERR_ARG;
-  if (xp < C || (xp & 7) || offp < 2 * KT || (offp & 7) || dop < C || (dop & 7) || doffp < C || (doffp & 7))
+  if (xp < C || (xp & 7) || offp < 2 * KT || (offp & 7) || dop < C || (dop & 7)) return RPC_ERR_ARG;
+  if (dch == C ? (doffp < C || (doffp & 7) || ((uintptr_t)doff & 15))
+               : (dch != 2 * KT || doffp < 2 * KT || (doffp & 1) || ((uintptr_t)doff & 3)))
     return RPC_ERR_ARG;
   if (ws_bytes < rpc_dcn_backward_workspace_size(B, H, W)) return RPC_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
@@ -746,7 +767,7 @@ extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp
   float* dwd = pb + (size_t)tiles * 2 * KT;
   float* win = dwd + KT * 1024;
   hipLaunchKernelGGL(k_bwd, dim3(tiles), dim3(BLK), 0, st, g, (const u16*)x, xp, (const u16*)off, offp, off_bias,
-                     (const u16*)w_bwd, (const u16*)dout, dop, dx, (u16*)doff, doffp, pw, pb, win);
+                     (const u16*)w_bwd, (const u16*)dout, dop, dx, (u16*)doff, doffp, dch, pw, pb, win);
   RPC_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_gather_dx, dim3((unsigned)(((long long)B * H * W * C + BLK - 1) / BLK)), dim3(BLK), 0, st, g,
                      (const float*)win, dx);
@@ -755,6 +776,22 @@ extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp
   hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+extern "C" int rpc_dcn_backward(const void* x, int xp, const void* off, int offp, const float* off_bias,
+                                const void* w_bwd, const void* dout, int dop, float* dx, void* doff, int doffp,
+                                float* doff_bias, float* dW, int B, int H, int W, void* workspace, size_t ws_bytes,
+                                void* stream) {
+  return dcn_backward_bf16(x, xp, off, offp, off_bias, w_bwd, dout, dop, dx, doff, doffp, C, doff_bias, dW, B, H, W,
+                           workspace, ws_bytes, stream);
+}
+
+extern "C" int rpc_dcn_backward_ex(const void* x, int xp, const void* off, int offp, const float* off_bias,
+                                   const void* w_bwd, const void* dout, int dop, float* dx, void* doff, int doffp,
+                                   int doff_channels, float* doff_bias, float* dW, int B, int H, int W,
+                                   void* workspace, size_t ws_bytes, void* stream) {
+  return dcn_backward_bf16(x, xp, off, offp, off_bias, w_bwd, dout, dop, dx, doff, doffp, doff_channels, doff_bias,
+                           dW, B, H, W, workspace, ws_bytes, stream);
 }
 
 extern "C" int rpc_dcn_forward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias,
@@ -769,14 +806,16 @@ extern "C" int rpc_dcn_forward_f32(const float* x, int xp, const float* off, int
   return RPC_OK;
 }
 
-extern "C" int rpc_dcn_backward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias,
-                                    const float* W, const float* dout, int dop, float* dx, float* doff, int doffp,
-                                    float* doff_bias, float* dW, int B, int H, int Wd, void* workspace,
-                                    size_t ws_bytes, void* stream) {
+static int dcn_backward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias,
+                            const float* W, const float* dout, int dop, float* dx, float* doff, int doffp, int dch,
+                            float* doff_bias, float* dW, int B, int H, int Wd, void* workspace, size_t ws_bytes,
+                            void* stream) {
   Geo g;
   if (!check_geo(B, H, Wd, &g)) return RPC_ERR_UNSUPPORTED;
   if (!x || !off || !off_bias || !W || !dout || !dx || !doff || !doff_bias || !dW || !workspace) return RPC_ERR_ARG;
-  if (xp < C || (xp & 3) || offp < 2 * KT || dop < C || (dop & 3) || doffp < 2 * KT || (doffp & 3))
+  if (xp < C || (xp & 3) || offp < 2 * KT || dop < C || (dop & 3)) return RPC_ERR_ARG;
+  if (dch == C ? (doffp < 2 * KT || (doffp & 3) || ((uintptr_t)doff & 15))
+               : (dch != 2 * KT || doffp < 2 * KT || (doffp & 1) || ((uintptr_t)doff & 7)))
     return RPC_ERR_ARG;
   if (ws_bytes < rpc_dcn_backward_workspace_size(B, H, Wd)) return RPC_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
@@ -786,7 +825,7 @@ extern "C" int rpc_dcn_backward_f32(const float* x, int xp, const float* off, in
   float* dwd = pb + (size_t)tiles * 2 * KT;
   float* win = dwd + KT * 1024;
   hipLaunchKernelGGL(k_bwd_f32, dim3(tiles), dim3(BLK), 0, st, g, x, xp, off, offp, off_bias, W, dout, dop, dx, doff,
-                     doffp, pw, pb, win);
+                     doffp, dch, pw, pb, win);
   RPC_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_gather_dx, dim3((unsigned)(((long long)B * H * Wd * C + BLK - 1) / BLK)), dim3(BLK), 0, st, g,
                      (const float*)win, dx);
@@ -795,4 +834,20 @@ extern "C" int rpc_dcn_backward_f32(const float* x, int xp, const float* off, in
   hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
+}
+
+extern "C" int rpc_dcn_backward_f32(const float* x, int xp, const float* off, int offp, const float* off_bias,
+                                    const float* W, const float* dout, int dop, float* dx, float* doff, int doffp,
+                                    float* doff_bias, float* dW, int B, int H, int Wd, void* workspace,
+                                    size_t ws_bytes, void* stream) {
+  return dcn_backward_f32(x, xp, off, offp, off_bias, W, dout, dop, dx, doff, doffp, C, doff_bias, dW, B, H, Wd,
+                          workspace, ws_bytes, stream);
+}
+
+extern "C" int rpc_dcn_backward_f32_ex(const float* x, int xp, const float* off, int offp, const float* off_bias,
+                                       const float* W, const float* dout, int dop, float* dx, float* doff, int doffp,
+                                       int doff_channels, float* doff_bias, float* dW, int B, int H, int Wd,
+                                       void* workspace, size_t ws_bytes, void* stream) {
+  return dcn_backward_f32(x, xp, off, offp, off_bias, W, dout, dop, dx, doff, doffp, doff_channels, doff_bias, dW, B,
+                          H, Wd, workspace, ws_bytes, stream);
 }

@@ -121,6 +121,67 @@ def test_dcn_forward_backward(B, H, W, amp):
     assert _rel(dW.cpu().double(), Wr.grad) <= 2e-2
 
 
+@pytest.mark.parametrize("f32", [False, True])
+def test_dcn_backward_offset_slice(f32):
+    """rpc_dcn_backward(_f32)_ex with 18 offset-gradient channels: the DCN reads its offsets from channel 18 j
+    of a shared 256-wide image and writes exactly its 18 gradient channels there (the head's concatenated
+    offset conv), bit-identical to the 64-wide padded form; the neighbours' channels are untouched."""
+    B, H, W, j, P = 2, 16, 24, 5, 256
+    dt = torch.float32 if f32 else torch.bfloat16
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(B, 64, H, W, generator=g)
+    offw = torch.randn(B, P, H, W, generator=g) * 1.5
+    ob = (torch.randn(18, generator=g) * 0.3).to(DEV)
+    Wt = (torch.randn(64, 16, 3, 3, generator=g) * 0.1).to(DEV).contiguous()
+    gout = torch.randn(B, 64, H, W, generator=g)
+    lib = _ffi.load()
+    st = _ffi.stream_of(torch.empty(1, device=DEV))
+    xi, gi = db._nhwc(x.to(DEV), dt), db._nhwc(gout.to(DEV), dt)
+    wide = db._nhwc(offw.to(DEV), dt)
+    narrow = db._nhwc(torch.cat([offw[:, 18 * j:18 * (j + 1)], torch.zeros(B, 46, H, W)], 1).to(DEV), dt)
+    if f32:
+        wb = Wt
+    else:
+        wf = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=DEV)
+        wb = torch.empty((9, 64, 64), dtype=torch.bfloat16, device=DEV)
+        _ffi.check(lib.rpc_dcn_prep_weight(_ffi.ptr(Wt), _ffi.ptr(wf), _ffi.ptr(wb), st), "prep")
+    wsz = lib.rpc_dcn_backward_workspace_size(B, H, W)
+    ws = torch.empty(wsz, dtype=torch.uint8, device=DEV)
+    res = []
+    for mode in ("pad", "slice"):
+        dx = torch.zeros((B * H * W, 64), dtype=torch.float32, device=DEV)
+        dob = torch.empty(18, device=DEV)
+        dW = torch.empty((64, 16, 3, 3), device=DEV)
+        if mode == "pad":
+            doff = db._image(B, 64, H, W, DEV, dt)
+            fn = lib.rpc_dcn_backward_f32_ex if f32 else lib.rpc_dcn_backward_ex
+            _ffi.check(fn(_ffi.ptr(xi), 64, _ffi.ptr(narrow), 64, _ffi.ptr(ob), _ffi.ptr(wb), _ffi.ptr(gi), 64,
+                          _ffi.ptr(dx), _ffi.ptr(doff), 64, 64, _ffi.ptr(dob), _ffi.ptr(dW), B, H, W, _ffi.ptr(ws), wsz,
+                          st), "bwd pad")
+            got = doff[:, :18]
+        else:
+            doff = torch.full((B, H, W, P), 7.0, dtype=dt, device=DEV).permute(0, 3, 1, 2)
+            fn = lib.rpc_dcn_backward_f32_ex if f32 else lib.rpc_dcn_backward_ex
+            _ffi.check(fn(_ffi.ptr(xi), 64, _ffi.ptr(wide[:, 18 * j:]), P, _ffi.ptr(ob), _ffi.ptr(wb), _ffi.ptr(gi),
+                          64, _ffi.ptr(dx), _ffi.ptr(doff[:, 18 * j:]), P, 18, _ffi.ptr(dob), _ffi.ptr(dW), B, H, W,
+                          _ffi.ptr(ws), wsz, st), "bwd slice")
+            got = doff[:, 18 * j:18 * (j + 1)]
+            rest = torch.cat([doff[:, :18 * j], doff[:, 18 * (j + 1):]], 1)
+            assert bool((rest == 7.0).all())
+        res.append((dx.clone(), got.clone(), dob.clone(), dW.clone()))
+    (dx0, *r0), (dx1, *r1) = res
+    assert _rel(dx1.double(), dx0.double()) <= 1e-6   # input gradient: float atomics (summation order)
+    for a, b in zip(r0, r1):
+        assert torch.equal(a, b)
+    # argument checks: misaligned slice, unsupported channel count
+    bad = db._image(B, P, H, W, DEV, dt)
+    fn = lib.rpc_dcn_backward_f32_ex if f32 else lib.rpc_dcn_backward_ex
+    assert fn(_ffi.ptr(xi), 64, _ffi.ptr(wide), P, _ffi.ptr(ob), _ffi.ptr(wb), _ffi.ptr(gi), 64, _ffi.ptr(dx),
+              _ffi.ptr(bad[:, 1:]), P, 18, _ffi.ptr(dob), _ffi.ptr(dW), B, H, W, _ffi.ptr(ws), wsz, st) != 0
+    assert fn(_ffi.ptr(xi), 64, _ffi.ptr(wide), P, _ffi.ptr(ob), _ffi.ptr(wb), _ffi.ptr(gi), 64, _ffi.ptr(dx),
+              _ffi.ptr(bad), P, 20, _ffi.ptr(dob), _ffi.ptr(dW), B, H, W, _ffi.ptr(ws), wsz, st) != 0
+
+
 def _ref_head(head, x, B, H, W):
     """float64 torch forward of the same stack (BN in training mode: batch statistics)."""
     P = {k: v.detach().cpu().double() for k, v in head.named_parameters()}

@@ -39,10 +39,10 @@ __host__ __device__ constexpr int gw_of(int kgp, int nt) { return kgp * nt * 16 
 // <64,2,1> 49 -> 42. Measured and kept at RT=1: the 64x64 tiles (88 VGPRs, 5 waves/SIMD: <64,4,1>
 // 47 -> 54 us) and the 32x16 tiles (<32,1,0> 21.3 -> 23.4 us)
 __host__ __device__ constexpr int rt_of(int kgp, int nt) {
-  return (kgp * nt >= 64 && kgp * nt <= 128 && nt <= 4) ? 2 : 1;
+  return ((kgp * nt >= 64 && kgp * nt <= 128 && nt <= 4) || (kgp == 128 && nt == 8)) ? 2 : 1;
 }
 __host__ __device__ constexpr int gemm_waves_per_simd(int kgp, int nt) {
-  return rt_of(kgp, nt) == 2 ? 5 : ((kgp * nt <= 256 && nt <= 4 && kgp <= 64) ? 8 : 1);
+  return kgp * nt >= 1024 ? 1 : rt_of(kgp, nt) == 2 ? 5 : ((kgp * nt <= 256 && nt <= 4 && kgp <= 64) ? 8 : 1);
 }
 constexpr int MAXK = 27;
 
@@ -458,8 +458,9 @@ __device__ __forceinline__ void vm_wait(int rem) {
 template <int KGP, int NT, int GW, int S>
 struct PipeCfg {
   // RT: 16-row MFMA tiles per wave, as k_gemm_bf16 (rt_of): the same rows per wave and per partial row,
-  // so the BatchNorm partial sums are added in the same order (same bits)
-  static constexpr int RT = rt_of(KGP, NT);
+  // so the BatchNorm partial sums are added in the same order (same bits) — except 128 x 128, whose two-tile
+  // waves would not fit the ring's LDS (one tile here)
+  static constexpr int RT = (KGP == 128 && NT == 8) ? 1 : rt_of(KGP, NT);
   static constexpr int G = KGP / 8, KS = KGP / 32, NGP = NT * 16, WR = 16 * RT, GBM = WR * GW, GBLK = 64 * GW;
   static constexpr int ABYTES = WR * KGP * 2;            // one wave's gathered rows
   static constexpr int NA = WR * G / 64;                 // their DMA instructions (1 KB each)
@@ -1313,7 +1314,8 @@ static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
 
 template <int KGP, int NT, int GW, int S>
 static void launch_pipe_t(int epi, const GB& a, int n_rows, hipStream_t st) {
-  const int nblk = (n_rows + 16 * GW - 1) / (16 * GW);
+  constexpr int GBM = PipeCfg<KGP, NT, GW, S>::GBM;
+  const int nblk = (n_rows + GBM - 1) / GBM;
   if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_FWD, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_DGRAD, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_PLAIN, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);

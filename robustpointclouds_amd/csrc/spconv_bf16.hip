@@ -37,7 +37,11 @@ __host__ __device__ constexpr int gw_of(int kgp, int nt) { return kgp * nt * 16 
 // mid-size tiles (K x 16*NT of 32x32 .. 64x32), whose time went to LDS weight reads (every wave re-read
 // the whole tile per offset for its 16 rows): r02v30 <32,2,0> 35.0 -> 30.0 us, <32,2,1> 38.5 -> 36.5,
 // <64,2,1> 49 -> 42. Measured and kept at RT=1: the 64x64 tiles (88 VGPRs, 5 waves/SIMD: <64,4,1>
-// 47 -> 54 us) and the 32x16 tiles (<32,1,0> 21.3 -> 23.4 us)
+// 47 -> 54 us) and the 32x16 tiles (<32,1,0> 21.3 -> 23.4 us). The 128 x 128 tiles (CenterPoint) take two
+// (128-row blocks, one per CU: 88 KB of LDS, 262 registers): forward 259 -> 262, data gradient 624 -> 606,
+// plain 407 -> 370 us per launch (profiles/r04_step_kernels_centerpoint_rt2.txt) — the weight tile
+// staging and its LDS reads were not the limit either; the data-gradient launches run beside the
+// 128 x 128 weight gradient on the side stream
 __host__ __device__ constexpr int rt_of(int kgp, int nt) {
   return ((kgp * nt >= 64 && kgp * nt <= 128 && nt <= 4) || (kgp == 128 && nt == 8)) ? 2 : 1;
 }

@@ -63,7 +63,11 @@ def test_pipe_gemm_bit_identical(kg, ng, n_out, K, rev):
         for mode in (1, 2, 3):
             out, part = _run(lib, mode, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
             assert torch.equal(out, ref_out), (mode, epi)
-            if epi != 2:
+            if epi != 2 and (kg, ng) == (128, 128):
+                # k_gemm_bf16 runs the 128 x 128 tiles as two 16-row tiles per wave, the ring one (LDS):
+                # the same rows per partial row, summed over 2 vs 4 waves
+                assert torch.allclose(part, ref_part, rtol=1e-5, atol=1e-5), (mode, epi)
+            elif epi != 2:
                 assert torch.equal(part, ref_part), (mode, epi)
 
 
@@ -184,7 +188,7 @@ def test_gemm_fin_entry_point(kg, ng, n_out, epi):
                                                 _ffi.ptr(out), _ffi.ptr(ez) if epi else None,
                                                 _ffi.ptr(ebn) if epi else None, _ffi.ptr(part), epi,
                                                 _ffi.C.byref(fin), st), "rpc_spconv_gemm_bf16_fin")
-        ref_out, ref_part = _run(lib, 1, a, n_src, kg, nbr, K, 0, n_out, bt, ng, epi, ez, ebn, dev)
+        ref_out, ref_part = _run(lib, 0, a, n_src, kg, nbr, K, 0, n_out, bt, ng, epi, ez, ebn, dev)
         assert torch.equal(out, ref_out)
         assert torch.equal(part, ref_part)
         rrm, rrv = rm0.clone(), rv0.clone()

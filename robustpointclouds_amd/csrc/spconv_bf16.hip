@@ -885,20 +885,26 @@ __device__ __forceinline__ uint4 f16x8_to_bf16x8(uint4 v) {
   return *(const uint4*)o;
 }
 
+// weight-gradient block: 4 waves; 8 for the 128 x 128 tiles, whose 3 offsets per block (KG = 3) then fit
+// 24 accumulator tiles per wave (192 VGPRs, no spill): each staged dz sub-tile serves 3 offsets instead
+// of 1 — CenterPoint k_wgrad_bf16<128,128> 458 -> 403 us per launch (r04_step_kernels_centerpoint_wg3.txt;
+// the step unchanged: these run on the side stream beside the data-gradient chain)
+__host__ __device__ constexpr int wg_threads(int ci, int co) { return ci * co >= 128 * 128 ? 512 : 256; }
 template <int CI, int CO, int KG, bool HF16 = false>
-__global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
+__global__ __launch_bounds__(wg_threads(CI, CO), (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
                                                     int K, int N, int rows_per, const u16* __restrict__ dz, int DP,
                                                     float* __restrict__ part) {
+  constexpr int TB = wg_threads(CI, CO), NWV = TB / 64;   // threads, waves
   constexpr int RT = 64;                                   // rows per sub-tile (2 MFMA k-steps)
   constexpr int SEG = 512;                                 // rows per neighbour preload
   constexpr int CIR = (CI + 15) / 16 * 16;
   constexpr int PA = CIR + 16, PD = CO + 16;               // LDS row pitch (elements)
   constexpr int MT = CIR / 16, NT = CO / 16;
-  // 4 waves as WM x WN over the (ci, co) tiles: wave (wm, wn) owns m = wm + WM*a, n = wn + WN*b
-  constexpr int WM = MT < 4 ? MT : 4, WN = 4 / WM;
+  // NWV waves as WM x WN over the (ci, co) tiles: wave (wm, wn) owns m = wm + WM*a, n = wn + WN*b
+  constexpr int WM = MT < 4 ? MT : 4, WN = NWV / WM;
   constexpr int WMT = MT / WM, WNT = (NT + WN - 1) / WN, TPW = WMT * WNT;
   constexpr int CA = (CI + 7) / 8, CD = CO / 8;            // 16-B chunks per row
-  constexpr int NA = (RT * CA + BLK - 1) / BLK, ND = (RT * CD + BLK - 1) / BLK;
+  constexpr int NA = (RT * CA + TB - 1) / TB, ND = (RT * CD + TB - 1) / TB;
   __shared__ __attribute__((aligned(16))) u16 sA[KG][RT * PA];
   __shared__ __attribute__((aligned(16))) u16 sD[RT * PD];
   __shared__ int sN[SEG * KG];
@@ -918,7 +924,7 @@ __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf1
     for (int i = 0; i < TPW; ++i) acc[g][i] = (f32x4){0.f, 0.f, 0.f, 0.f};
   // zero the padded channels of the A tiles once (CI = 16 * MT always here, kept for safety)
   if (CIR != CI)
-    for (int q = tid; q < KG * RT * PA; q += BLK) (&sA[0][0])[q] = 0;
+    for (int q = tid; q < KG * RT * PA; q += TB) (&sA[0][0])[q] = 0;
   // transposed-read lane geometry: group g4, lane i = 4q + p of the group
   const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
   const int rowoff = 4 * g4 + qq;                          // + 16*half + 32*kstep
@@ -930,25 +936,25 @@ __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf1
       // all of a thread's index loads in flight at once, from clamped addresses (a guarded load per
       // pass compiled to a branch that waited for its load before the next pass: 2-6 round trips)
       // (32-bit buffer offsets; an index outside the map reads as -1 via the OOB-zero + select)
-      constexpr int NQ = (SEG * KG + BLK - 1) / BLK;
+      constexpr int NQ = (SEG * KG + TB - 1) / TB;
       const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc((void*)nbr, (short)0, 0x7fffffff, 0x00020000);
       int v[NQ];
 #pragma unroll
       for (int i = 0; i < NQ; ++i) {
-        const int q = tid + i * BLK, r = q / KG, g = q - r * KG, row = seg + r, k = k0 + g;
+        const int q = tid + i * TB, r = q / KG, g = q - r * KG, row = seg + r, k = k0 + g;
         unsigned off = (q < SEG * KG && row < se && k < K) ? (unsigned)(row * K + k) * 4u : 0x80000000u;
         asm volatile("" : "+v"(off));
         v[i] = off == 0x80000000u ? -1 : __builtin_amdgcn_raw_buffer_load_b32(rn, off, 0, 0);
       }
 #pragma unroll
       for (int i = 0; i < NQ; ++i)
-        if (tid + i * BLK < SEG * KG) sN[tid + i * BLK] = v[i];
+        if (tid + i * TB < SEG * KG) sN[tid + i * TB] = v[i];
     }
     __syncthreads();
     auto load = [&](int rs) {   // global -> registers for the sub-tile starting at segment row rs
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
-        int q = tid + j * BLK;
+        int q = tid + j * TB;
         rd[j] = make_uint4(0u, 0u, 0u, 0u);
         if (q < RT * CD) {
           int r = q / CD, c8 = q - r * CD, row = seg + rs + r;
@@ -959,7 +965,7 @@ __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf1
       for (int g = 0; g < KG; ++g)
 #pragma unroll
         for (int j = 0; j < NA; ++j) {
-          int q = tid + j * BLK;
+          int q = tid + j * TB;
           ra[g][j] = make_uint4(0u, 0u, 0u, 0u);
           if (q < RT * CA) {
             int r = q / CA, c8 = q - r * CA;
@@ -973,7 +979,7 @@ __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf1
       __syncthreads();   // previous sub-tile's MFMAs are done with the LDS tiles
 #pragma unroll
       for (int j = 0; j < ND; ++j) {
-        int q = tid + j * BLK;
+        int q = tid + j * TB;
         if (q < RT * CD) {
           int r = q / CD, c8 = q - r * CD;
           *(uint4*)&sD[r * PD + c8 * 8] = rd[j];
@@ -983,7 +989,7 @@ __global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf1
       for (int g = 0; g < KG; ++g)
 #pragma unroll
         for (int j = 0; j < NA; ++j) {
-          int q = tid + j * BLK;
+          int q = tid + j * TB;
           if (q < RT * CA) {
             int r = q / CA, c8 = q - r * CA;
             *(uint4*)&sA[g][r * PA + c8 * 8] = HF16 ? f16x8_to_bf16x8(ra[g][j]) : ra[g][j];
@@ -1581,7 +1587,7 @@ extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int k
 template <int CI, int CO, int KG>
 static int wgrad_resident() {   // resident blocks per CU of one k_wgrad_bf16 instantiation
   static int r = 0;
-  if (r == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&r, k_wgrad_bf16<CI, CO, KG>, BLK, 0) != hipSuccess ||
+  if (r == 0 && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&r, k_wgrad_bf16<CI, CO, KG>, wg_threads(CI, CO), 0) != hipSuccess ||
                  r <= 0))
     r = 1;
   return r;
@@ -1597,12 +1603,12 @@ static int wgrad_slots(int ci, int co) {   // resident blocks on the whole devic
   }
   int per = 1;
 #define WR(a, b, kg) if (ci == a && co == b) per = wgrad_resident<a, b, kg>(); else
-  WR(16, 16, 3) WR(16, 32, 3) WR(32, 32, 3) WR(32, 64, 3) WR(64, 64, 3) WR(64, 128, 3) WR(128, 128, 1) {}
+  WR(16, 16, 3) WR(16, 32, 3) WR(32, 32, 3) WR(32, 64, 3) WR(64, 64, 3) WR(64, 128, 3) WR(128, 128, 3) {}
 #undef WR
   return per * cus;
 }
 
-static int wgrad_kg(int ci, int co) { return (ci == 128 && co == 128) ? 1 : 3; }
+static int wgrad_kg(int ci, int co) { (void)ci; (void)co; return 3; }
 
 static int wgrad_fill() {   // RPC_SPWG_FILL (A/B): percent of one round of resident blocks, 0 = 512-row chunks
   static int r = -1;
@@ -1789,7 +1795,8 @@ extern "C" int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* 
   int chunks = wgrad_chunks(n_out, kvol, ci, co);
   if (ws_bytes < (size_t)chunks * kvol * ci * co * sizeof(float)) return RPC_ERR_WORKSPACE;
   int rows_per = ((n_out + chunks - 1) / chunks + 31) / 32 * 32;
-  // 128 x 128 tiles keep one kernel offset per block (KG = 1: 64 accumulator registers / lane)
+  // 3 kernel offsets per block share each staged dz sub-tile (the 128 x 128 tiles with 8 waves: 24
+  // accumulator tiles per wave)
   const int KG = wgrad_kg(ci, co);
   dim3 grid(chunks * ((kvol + KG - 1) / KG));
   float* part = (float*)ws;
@@ -1799,13 +1806,13 @@ extern "C" int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* 
 #define W2(a, b, kg)                                                                                   \
   if (ci == a && co == b) {                                                                           \
     if (hfmt)                                                                                         \
-      hipLaunchKernelGGL((k_wgrad_bf16<a, b, kg, true>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, \
-                         dp, DP, part);                                                               \
+      hipLaunchKernelGGL((k_wgrad_bf16<a, b, kg, true>), grid, dim3(wg_threads(a, b)), 0, st, hp, HP, nbr, kvol, n_out, \
+                         rows_per, dp, DP, part);                                                     \
     else                                                                                              \
-      hipLaunchKernelGGL((k_wgrad_bf16<a, b, kg>), grid, dim3(BLK), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp, \
+      hipLaunchKernelGGL((k_wgrad_bf16<a, b, kg>), grid, dim3(wg_threads(a, b)), 0, st, hp, HP, nbr, kvol, n_out, rows_per, dp, \
                          DP, part);                                                                   \
   } else
-  W2(16, 16, 3) W2(16, 32, 3) W2(32, 32, 3) W2(32, 64, 3) W2(64, 64, 3) W2(64, 128, 3) W2(128, 128, 1)
+  W2(16, 16, 3) W2(16, 32, 3) W2(32, 32, 3) W2(32, 64, 3) W2(64, 64, 3) W2(64, 128, 3) W2(128, 128, 3)
   { return RPC_ERR_UNSUPPORTED; }
 #undef W2
   RPC_LAUNCH_CHECK();

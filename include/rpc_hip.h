@@ -298,6 +298,10 @@ int rpc_bn_fin_tickets(int n_out);
 int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
                              const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
                              float* part, int epi, const RpcBnFin* fin, void* stream);
+/* the same with the operand format of rpc_spconv_gemm_h16 (fmt 1 = fp16: the forward, epi 0, only) */
+int rpc_spconv_gemm_h16_fin(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
+                            const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
+                            float* part, int epi, const RpcBnFin* fin, void* stream);
 /* the general form: operand format fmt and the rows visited in the order perm ([n_out] row indices, a
  * permutation: rpc_rulebook_mask_perm of `map`; NULL = natural order). Every row is written in place and its
  * own sums are those of the natural order; only the BatchNorm partial rows (sums over 64 visited rows) differ. */

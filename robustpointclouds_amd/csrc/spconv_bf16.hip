@@ -1553,20 +1553,21 @@ extern "C" int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, c
 extern "C" int rpc_bn_fin_groups(int n_out) { return fin_groups(cdiv(n_out > 0 ? n_out : 1, 64)); }
 extern "C" int rpc_bn_fin_tickets(int n_out) { return 1 + rpc_bn_fin_groups(n_out); }
 
-extern "C" int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
-                                        int n_out, const void* bt, int ng, float* out, const float* prev_z,
-                                        const float* prev_bn, float* part, int epi, const RpcBnFin* fin,
-                                        void* stream) {
-  if (!fin) return rpc_spconv_gemm_bf16_n(a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part,
-                                          epi, stream);
+// the fused-finalize GEMM on 16-bit operands of either format (fp16: the forward, epi 0, only)
+extern "C" int rpc_spconv_gemm_h16_fin(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
+                                       int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                                       const float* prev_bn, float* part, int epi, const RpcBnFin* fin, void* stream) {
+  if (fmt != 0 && (fmt != 1 || epi != 0)) return RPC_ERR_ARG;
+  if (!fin) return rpc_spconv_gemm_h16(a, fmt, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part,
+                                       epi, stream);
   if ((epi != 0 && epi != 1) || !part || !fin->ticket || !fin->gpart || !fin->gamma || !fin->bn ||
       (epi == 0 && (!fin->beta || !fin->running_mean || !fin->running_var)) || (epi == 1 && !fin->fbn) ||
       fin->mode != epi || ng > 256)
     return RPC_ERR_ARG;
   if (n_out <= 0) return RPC_ERR_ARG;   // the finalize divides by the row count
   if (gemm_mode() >= 4) {   // the timing arms of k_gemm_bf16: no fused finalize
-    int rc = rpc_spconv_gemm_bf16_n(a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi,
-                                    stream);
+    int rc = rpc_spconv_gemm_h16(a, fmt, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi,
+                                 stream);
     if (rc) return rc;
     return rpc_bn_finalize(part, cdiv(n_out, BM), ng, n_out, epi, fin->gamma, fin->beta, fin->eps, fin->momentum,
                            fin->running_mean, fin->running_var, fin->fbn, fin->bn, fin->dgamma, fin->dbeta, nullptr,
@@ -1574,8 +1575,17 @@ extern "C" int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const 
   }
   GB g;
   memset(&g, 0, sizeof(g));
+  g.fmt = fmt;
   g.fin = *fin;
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
+}
+
+extern "C" int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
+                                        int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                                        const float* prev_bn, float* part, int epi, const RpcBnFin* fin,
+                                        void* stream) {
+  return rpc_spconv_gemm_h16_fin(a, 0, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, fin,
+                                 stream);
 }
 
 extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out,

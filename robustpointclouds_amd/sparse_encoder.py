@@ -51,14 +51,21 @@ class _Spec:
 SIDE_STREAMS = os.environ.get("RPC_SPARSE_STREAMS", "1") != "0"
 # the backward as one native call (csrc/sparse_exec.hip rpc_sparse_backward); 0: the per-layer Python loop
 NATIVE_BACKWARD = os.environ.get("RPC_SPARSE_NATIVE", "1") != "0"
-# RPC_SPARSE_FUSED_FIN=1: BatchNorm finalizes fused into the bf16 GEMMs that produce their partial sums
-# (rpc_spconv_gemm_bf16_fin, two-level last-arriving blocks). Off by default. With an agent-scope release per
-# block (buffer_wbl2: every block wrote back its XCD L2's dirty lines, the GEMM's fresh output rows) it was
-# k_gemm_bf16<64,4,0> 41 -> 63 us, <64,4,1> 53 -> 92 us (profiles/r04_spgemm_fused_fin.txt); with the hand-off
-# data in sc1 stores and no fence (common.h last_block_arrive_lite) the data gradient is 54.2 -> 58.6 us
-# against the 6.4 us rpc_bn_finalize launch it removes: kernel busy 8.28 -> 8.22 ms, step time within noise
-# (profiles/r04_step_kernels_fused_fin.txt, r04_ab_split_fin.txt)
-FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "0") != "0"
+# BatchNorm finalizes fused into the 16-bit GEMMs that produce their partial sums (rpc_spconv_gemm_bf16_fin:
+# data gradient, the default; rpc_spconv_gemm_h16_fin: forward, fp16 or bf16 operands, off; two-level
+# last-arriving blocks): no standalone rpc_bn_finalize launch in the backward of sparse layers 1-11.
+# RPC_SPARSE_FUSED_FIN=0: separate finalizes (A/B).
+# With an agent-scope release per block (buffer_wbl2: every block wrote back its XCD L2's dirty lines, the
+# GEMM's fresh output rows) it was k_gemm_bf16<64,4,0> 41 -> 63 us, <64,4,1> 53 -> 92 us
+# (profiles/r04_spgemm_fused_fin.txt); with the hand-off data in sc1 stores and no fence (common.h
+# last_block_arrive_lite) the data gradient is 54.2 -> 58.6 us against the 6.4 us rpc_bn_finalize launch it
+# removes: SECOND 3-class step within noise (7.155 / 7.157 vs 7.160 / 7.153 ms), CenterPoint 159.7 / 160.0 ->
+# 161.0 / 161.1 frames/s with the backward finalizes fused (profiles/r04_ab_fused_fin.txt). The forward's
+# (RPC_SPARSE_FUSED_FIN_FWD=1, fp16 operands) measured slower on the metric's step: sparse forward 0.70 -> 0.74
+# ms, 834.8 / 837.3 -> 831.1 / 832.2 frames/s (CenterPoint +0.2 %), so it stays off. Fused and separate
+# finalizes give bit-identical results on the metric's encoder (tests/test_gpu_sparse_pipe.py)
+FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "1") != "0"
+FUSED_FINALIZE_FWD = os.environ.get("RPC_SPARSE_FUSED_FIN_FWD", "0") != "0"
 # perf mode forward GEMM operands (gathered rows relu(bn(z)) and forward weight tiles): fp16 (default) or bf16
 # (RPC_SPARSE_FWD_BF16=1, A/B). The operand rounding of the forward decides the ReLU masks that every gradient
 # passes: with bf16 forward operands the perturber's input gradient is 0.237 rel-L2 from float64, with fp16 0.077
@@ -588,17 +595,18 @@ class SparseEncoderFn(torch.autograd.Function):
             if rec["bf16"]:
                 bt, rec["btd"] = wtiles[li]
                 e0 = enc.timer.start() if tm else None
-                tk = enc.fin_ticket_ptr(dev, li, n_out) if FUSED_FINALIZE and n_out > 0 and fmt == 0 else None
+                tk = (enc.fin_ticket_ptr(dev, li, n_out)
+                      if FUSED_FINALIZE_FWD and n_out > 0 and rec["perm"] is None else None)
                 if tk is not None:
                     # GEMM + this layer's BatchNorm finalize in one launch (last-arriving blocks)
                     gpart = torch.empty(lib.rpc_bn_fin_groups(n_out) * 2 * sp.co, dtype=torch.float64, device=dev)
                     fin = _ffi.RpcBnFin(tk, gpart.data_ptr(), 0, gamma.data_ptr(), beta.data_ptr(), float(bnm.eps),
                                         float(bnm.momentum), bnm.running_mean.data_ptr(), bnm.running_var.data_ptr(),
                                         None, bn.data_ptr(), None, None)
-                    _ffi.check(lib.rpc_spconv_gemm_bf16_fin(_ffi.ptr(hsrc), hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
-                                                            sp.K, 0, n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None,
-                                                            _ffi.ptr(part), 0, _ffi.C.byref(fin), st),
-                               "rpc_spconv_gemm_bf16_fin")
+                    _ffi.check(lib.rpc_spconv_gemm_h16_fin(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci,
+                                                           _ffi.ptr(rec["nbr"]), sp.K, 0, n_out, _ffi.ptr(bt), sp.co,
+                                                           _ffi.ptr(z), None, None, _ffi.ptr(part), 0,
+                                                           _ffi.C.byref(fin), st), "rpc_spconv_gemm_h16_fin")
                     fused = True
                 else:
                     _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),

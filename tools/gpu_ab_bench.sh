@@ -8,7 +8,7 @@ mkdir -p $OUT
 export TMPDIR=/tmp
 for v in "$@"; do
   if [ "$v" = default ]; then E=""; else E="$v"; fi
-  env $E timeout -k 10 200 python -u bench.py --steps 30 --warmup 8 --no-cpu-baseline --no-parity-mode \
+  env $E timeout -k 10 200 python -u bench.py $BENCH_ARGS --steps 30 --warmup 8 --no-cpu-baseline --no-parity-mode \
     > "$OUT/ab_${v// /_}.log" 2>&1 || exit $?
   python - "$OUT/ab_${v// /_}.log" "$v" <<'PY' | tee -a $OUT/ab.txt
 import json, sys

@@ -243,6 +243,11 @@ __global__ __launch_bounds__(BLK) void k_fwd(Geo g, const u16* __restrict__ x, i
 // Input-gradient scatter as a GEMM: per tap, S_k [144 window pixels][64 tile pixels] holds the
 // bilinear weight of every in-window corner (4 per sampled pixel), and dx_window += S_k x dcol_k
 // (bf16 MFMA, fp32 accumulators held in registers across the taps: 9 16x16 tiles per wave).
+// LDS 76 KB, two blocks per CU (r04; was 118 KB, one 4-wave block per CU: 157 -> 101 us per CenterPoint
+// launch, profiles/r04_step_kernels_centerpoint_v4.txt): one S buffer (a thread clears its tap k-1 entry
+// in phase A and sets its tap k entry after the A/B barrier), the offset gradients stored to the image per
+// tap (no [64][18] staging) with the bias partials reduced per wave by shuffles, and the offset gradient's
+// dcol read from the bf16 dcol^T tile of phase D (the fp32 copy is gone)
 constexpr int PS = 64 + 8;     // S row pitch (elements)
 
 __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, int xp, const u16* __restrict__ off,
@@ -254,10 +259,9 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
   __shared__ __attribute__((aligned(16))) u16 sDo[64 * P];
   __shared__ __attribute__((aligned(16))) u16 sC[64 * P];
   __shared__ __attribute__((aligned(16))) u16 sDcT[64 * PS];    // dcol^T [channel][pixel], bf16
-  __shared__ __attribute__((aligned(16))) u16 sS[2][WR * PS];    // S_k, double-buffered
-  __shared__ __attribute__((aligned(16))) float sDc[64 * (C + 4)];
+  __shared__ __attribute__((aligned(16))) u16 sS[WR * PS];       // S_k (one buffer: cleared in A, set in B)
   __shared__ float sOin[64 * 2 * KT];     // offsets (+ bias) of the tile, all taps
-  __shared__ float sOff[64 * 2 * KT];     // offset gradients
+  __shared__ float sPb[4 * 2 * KT];       // offset-bias gradient partials per wave
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const Tile tl = tile_of(g, blockIdx.x);
   stage_window(g, tl, x, xp, sXw);
@@ -272,7 +276,8 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
     const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
     sOin[i] = bf2f(off[((size_t)(tl.b * g.H + yy) * g.W + xw) * offp + c]) + ob[c];
   }
-  for (int i = tid; i < 2 * WR * PS / 8; i += BLK) ((uint4*)&sS[0][0])[i] = make_uint4(0u, 0u, 0u, 0u);
+  for (int i = tid; i < WR * PS / 8; i += BLK) ((uint4*)sS)[i] = make_uint4(0u, 0u, 0u, 0u);
+  const size_t mypix = (size_t)(tl.b * g.H + tl.y0 + ((tid >> 2) >> 3)) * g.W + tl.x0 + ((tid >> 2) & 7);
   const int p = tid >> 2, q = tid & 3;
   const int y = tl.y0 + (p >> 3), xx = tl.x0 + (p & 7);
   const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp4 = lane & 3, rowoff = 4 * g4 + qq;
@@ -293,20 +298,22 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
   for (int i = 0; i < 3; ++i)
 #pragma unroll
     for (int n = 0; n < 4; ++n) acc[i][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  int prev_u = -1;                        // this thread's S entry of the previous use of the buffer
+  int prev_u = -1;                        // this thread's S entry of the previous tap
   __syncthreads();
 #pragma unroll 1
   for (int k = 0; k < KT; ++k) {
-    u16* S = sS[k & 1];
+    u16* S = sS;
     // A: sample the column block of tap k (thread = pixel x group); thread q also owns corner q of
-    // its pixel: it clears its entry of tap k-1 in the other buffer (read by tap k-1's phase D before
-    // the last barrier, next written at tap k+1 after two more) and writes the new bilinear weight
+    // its pixel: it clears its S entry of tap k-1 here (read by tap k-1's phase D before the last
+    // barrier) and writes the new bilinear weight in phase B (after every thread's clear)
     const Samp s = samp(g, y, xx, k, sOin[p * 2 * KT + 2 * k], sOin[p * 2 * KT + 2 * k + 1]);
+    int new_u = -1;
+    u16 new_w = 0;
     {
       float col[CG];
       sample16(g, tl, x, xp, sXw, s, q, col);
       store_col(sC, p, q, col);
-      if (prev_u >= 0) sS[(k + 1) & 1][prev_u * PS + p] = 0;
+      if (prev_u >= 0) S[prev_u * PS + p] = 0;
       prev_u = -1;
       const int cok = q == 0 ? s.c1 : (q == 1 ? s.c2 : (q == 2 ? s.c3 : s.c4));
       if (s.valid && cok) {
@@ -314,14 +321,18 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
         const int cy = s.hl + (q >> 1), cx = s.wl + (q & 1);
         const int wy = cy - (tl.y0 - 2), wx = cx - (tl.x0 - 2);
         if (wy >= 0 && wy < WE && wx >= 0 && wx < WE) {
-          prev_u = wy * WE + wx;
-          S[prev_u * PS + p] = f2bf(wq);
+          new_u = wy * WE + wx;
+          new_w = f2bf(wq);
         } else {
           prev_u = -2 - (cy * 65536 + cx);   // out-of-window corner: global atomics after dcol
         }
       }
     }
     __syncthreads();
+    if (new_u >= 0) {
+      S[new_u * PS + p] = new_w;
+      prev_u = new_u;
+    }
     // B: dW_k diagonal block of group w (dOut^T col over the tile) and dcol (wave w: pixels 16w..)
     {
       f32x4 aw = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -350,7 +361,6 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int pr = 16 * w + 4 * g4 + r, cc = 16 * n + (lane & 15);
-          sDc[pr * (C + 4) + cc] = d[n][r];
           sDcT[cc * PS + pr] = f2bf(d[n][r]);
         }
     }
@@ -362,13 +372,7 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
       if (s.valid) {
         float dc[CG], v[CG];
 #pragma unroll
-        for (int c4 = 0; c4 < CG / 4; ++c4) {
-          const float4 t4 = *(const float4*)&sDc[p * (C + 4) + q * CG + 4 * c4];
-          dc[4 * c4] = t4.x;
-          dc[4 * c4 + 1] = t4.y;
-          dc[4 * c4 + 2] = t4.z;
-          dc[4 * c4 + 3] = t4.w;
-        }
+        for (int c = 0; c < CG; ++c) dc[c] = bf2f(sDcT[(q * CG + c) * PS + p]);   // the bf16 dcol of phase D
         const int cok[4] = {s.c1, s.c2, s.c3, s.c4};
         const float ch[4] = {-s.hw, -s.lw, s.hw, s.lw}, cwd[4] = {-s.hh, s.hh, -s.lh, s.lh};
 #pragma unroll
@@ -386,15 +390,25 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
       gw += __shfl_xor(gw, 1, 64);
       gh += __shfl_xor(gh, 2, 64);
       gw += __shfl_xor(gw, 2, 64);
-      if (q == 0) {
-        sOff[p * 2 * KT + 2 * k] = gh;
-        sOff[p * 2 * KT + 2 * k + 1] = gw;
+      // the offset-conv output gradient of (pixel, tap k) straight to the image (bf16 pair), and the bias
+      // gradient partials: the wave's 16 pixels summed by xor shuffles (fixed order), one row per wave
+      if (q == 0)
+        *(unsigned*)(doff + mypix * doffp + 2 * k) = (unsigned)f2bf(gh) | ((unsigned)f2bf(gw) << 16);
+      float sh = gh, sw = gw;
+#pragma unroll
+      for (int m = 4; m < 64; m <<= 1) {
+        sh += __shfl_xor(sh, m, 64);
+        sw += __shfl_xor(sw, m, 64);
+      }
+      if (lane == 0) {
+        sPb[w * 2 * KT + 2 * k] = sh;
+        sPb[w * 2 * KT + 2 * k + 1] = sw;
       }
       if (prev_u <= -2) {                  // rare: this thread's corner lies outside the window
         const int code = -2 - prev_u, cy = code >> 16, cx = code & 0xffff;
         const float wq = q == 0 ? s.hh * s.hw : (q == 1 ? s.hh * s.lw : (q == 2 ? s.lh * s.hw : s.lh * s.lw));
         float* dst = dx + ((size_t)(tl.b * g.H + cy) * g.W + cx) * C;
-        for (int c = 0; c < C; ++c) atomicAdd(&dst[c], wq * sDc[p * (C + 4) + c]);
+        for (int c = 0; c < C; ++c) atomicAdd(&dst[c], wq * bf2f(sDcT[c * PS + p]));
         prev_u = -1;
       }
     }
@@ -415,35 +429,19 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
     }
     __syncthreads();
   }
-  // offset-conv output gradient (bf16 image) and its bias partials: dch = 64 writes channels 18..63 as zero
-  // (a 64-wide image of its own), dch = 18 exactly the 18 offset channels (a slice of a shared image)
+  // the padded offset-gradient image (dch = 64): channels 18..63 zero (channels 0..17 were written per tap;
+  // dch = 18 writes exactly those, a slice of a shared image)
   if (dch == C) {
     for (int qd = tid; qd < 64 * 8; qd += BLK) {
-      const int pp = qd >> 3, seg = qd & 7;
-      const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
-      unsigned wv[4];
-#pragma unroll
-      for (int h = 0; h < 4; ++h) {
-        const int c0 = seg * 8 + 2 * h;
-        const float a = c0 < 2 * KT ? sOff[pp * 2 * KT + c0] : 0.0f;
-        const float bq = c0 + 1 < 2 * KT ? sOff[pp * 2 * KT + c0 + 1] : 0.0f;
-        wv[h] = f2bf(a) | ((unsigned)f2bf(bq) << 16);
-      }
-      *(uint4*)(doff + ((size_t)(tl.b * g.H + yy) * g.W + xw) * doffp + seg * 8) = make_uint4(wv[0], wv[1], wv[2], wv[3]);
-    }
-  } else {
-    for (int qd = tid; qd < 64 * KT; qd += BLK) {
-      const int pp = qd / KT, h = qd - pp * KT;
-      const int yy = tl.y0 + (pp >> 3), xw = tl.x0 + (pp & 7);
-      const unsigned v = f2bf(sOff[pp * 2 * KT + 2 * h]) | ((unsigned)f2bf(sOff[pp * 2 * KT + 2 * h + 1]) << 16);
-      *(unsigned*)(doff + ((size_t)(tl.b * g.H + yy) * g.W + xw) * doffp + 2 * h) = v;
+      const int pp = qd >> 3, j = qd & 7;
+      u16* row = doff + ((size_t)(tl.b * g.H + tl.y0 + (pp >> 3)) * g.W + tl.x0 + (pp & 7)) * doffp;
+      if (j < 3) *(unsigned*)(row + 2 * KT + 2 * j) = 0u;          // channels 18..23
+      else *(uint4*)(row + 24 + 8 * (j - 3)) = make_uint4(0u, 0u, 0u, 0u);   // 24..63
     }
   }
-  if (tid < 2 * KT) {
-    float sacc = 0.0f;
-    for (int pp = 0; pp < 64; ++pp) sacc += sOff[pp * 2 * KT + tid];
-    pb_part[(size_t)blockIdx.x * 2 * KT + tid] = sacc;
-  }
+  __syncthreads();
+  if (tid < 2 * KT)
+    pb_part[(size_t)blockIdx.x * 2 * KT + tid] = ((sPb[tid] + sPb[2 * KT + tid]) + sPb[4 * KT + tid]) + sPb[6 * KT + tid];
   // the window's input gradient -> this tile's slab [144][64] (k_gather_dx sums the <= 4 covering
   // slabs per pixel in a fixed order: no atomics, deterministic)
   float* wdst = win_part + (size_t)blockIdx.x * WR * C;

@@ -382,7 +382,10 @@ def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
 
 
 # RPC_DENSE_WG_SIDE=1 (A/B): the SECOND backbone's weight gradients on a side stream (forked after each
-# layer's BN-backward apply, joined at the end of the backbone backward), beside the data-gradient chain
+# layer's BN-backward apply, joined at the end of the backbone backward), beside the data-gradient chain.
+# Off: measured slower (SECOND 835.8 / 827.8 -> 766.0 / 627.2 frames/s, CenterPoint 164.8 -> 158.1,
+# profiles/r04_ab_dense_wg_side.txt): the one-block-per-CU S1 kernels and the weight gradient contend for
+# the CUs and the chain behind them waits longer (as round 1 measured with the former kernels)
 WG_SIDE = os.environ.get("RPC_DENSE_WG_SIDE", "0") != "0"
 _WG_STREAMS = {}
 

@@ -90,8 +90,13 @@ def _traffic(kernel_tag):
     (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, KB -> bytes) and that summary's file name,
     else (None, None). `kernel_tag` is matched against the kernel's name without its argument list."""
     import glob
+    import re
+
+    def order(f):   # rNN_pmc_traffic_vMM.json: newest round, then newest version (mtimes do not survive copies)
+        m = re.search(r"r(\d+)_pmc_traffic_v(\d+)", os.path.basename(f))
+        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic*.json")),
-                   key=os.path.getmtime)
+                   key=order)
     for f in reversed(files):
         d = json.load(open(f))
         for name, v in d.get("kernels", {}).items():

@@ -2417,7 +2417,17 @@ static bool s1_ybig(const int* r_img, int cout) {
 static bool s1_ytwo(const int* r_img, int cout) {
   return cout % 128 == 0 && (g_s1_variant == 4 || (g_s1_variant == 0 && s1_ybig(r_img, cout)));
 }
-static bool s1_xwide(int cout) { return cout % 128 == 0 && (g_s1_variant == 0 || g_s1_variant == 3); }
+// grids of at most half a round of the x kernel's one-block-per-CU slots (CenterPoint's 128x128 / 64x64 images at
+// batch 4: 128 / 64 blocks) leave most CUs idle; there the 64-channel k_conv3x3 (two 4-wave blocks per CU, 4x
+// the blocks) is used (CenterPoint 164.8 / 164.9 -> 166.5 / 166.4 frames/s with every S1 launch on it,
+// profiles/r04_ab_centerpoint_s1.txt; the metric's SECOND shapes keep x / y: their smallest grid is 252 blocks)
+static bool s1_small(const int* r_img, int cout) {
+  const long long bx = (long long)r_img[0] * ((r_img[1] + CT - 1) / CT) * ((r_img[2] + XTW - 1) / XTW) * (cout / 128);
+  return 2 * bx <= cu_count();
+}
+static bool s1_xwide(const int* r_img, int cout) {
+  return cout % 128 == 0 && (g_s1_variant == 3 || (g_s1_variant == 0 && !s1_small(r_img, cout)));
+}
 
 static bool s1_wide(int tiles, int cout) {
   if (cout % 128 || g_s1_variant == 1) return false;
@@ -2470,7 +2480,7 @@ static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t 
       case 128: hipLaunchKernelGGL(k_conv3x3y<128>, grid, dim3(YB), 0, st, c); break;
       default: hipLaunchKernelGGL(k_conv3x3y<0>, grid, dim3(YB), 0, st, c);
     }
-  } else if (s1_xwide(g.COUT)) {
+  } else if (s1_xwide(rimg, g.COUT)) {
     if (!fits32) return RPC_ERR_UNSUPPORTED;   // 32-bit buffer offsets (part rows are those of 16x32 tiles)
     c.TX = (g.R.W + XTW - 1) / XTW;
     const dim3 grid(g.R.B * TY * c.TX * (g.COUT / 128));
@@ -2534,7 +2544,7 @@ extern "C" int rpc_dense_conv_bnbwd(const void* src, int sp, int cin, const void
                                     const void* bnz, const float* bnp, float* part, const int* r_img, void* stream) {
   if (!src || !wt || !out || !r_img || !bnz || !bnp || !part) return RPC_ERR_ARG;
   if (cin % BK || cout % 128 || sp < cin || op < cout || (sp & 7) || (op & 7)) return RPC_ERR_ARG;
-  if (!s1_ytwo(r_img, cout) && !s1_xwide(cout)) return RPC_ERR_UNSUPPORTED;
+  if (!s1_ytwo(r_img, cout) && !s1_xwide(r_img, cout)) return RPC_ERR_UNSUPPORTED;
   IG g{(const u16*)src, sp, cin, (const u16*)wt, cout, (u16*)out, op, 0, 0, part, img3(r_img), img3(r_img),
        img3(r_img), 0};
   g.M = g.R.B * g.R.H * g.R.W;
@@ -2547,13 +2557,13 @@ extern "C" int rpc_dense_conv_s1_kernel(int map, int cout, const int* r_img) {
   if (map != M_S1 || !r_img || cout % 64) return -1;
   const int TY = (r_img[1] + CT - 1) / CT, TX = (r_img[2] + CT - 1) / CT;
   if (s1_ytwo(r_img, cout)) return 3;
-  if (s1_xwide(cout)) return 2;
+  if (s1_xwide(r_img, cout)) return 2;
   return s1_wide(r_img[0] * TY * TX, cout) ? 1 : 0;
 }
 
 extern "C" int rpc_dense_conv_part_rows(int map, int cout, const int* r_img) {
   if (!r_img || map < M_S1 || map > M_G2) return -1;
-  if (map == M_S1 && !s1_ytwo(r_img, cout) && s1_xwide(cout))   // one row per 16x32 tile
+  if (map == M_S1 && !s1_ytwo(r_img, cout) && s1_xwide(r_img, cout))   // one row per 16x32 tile
     return r_img[0] * ((r_img[1] + CT - 1) / CT) * ((r_img[2] + XTW - 1) / XTW);
   return rpc_dense_conv_blocks(map, r_img);
 }

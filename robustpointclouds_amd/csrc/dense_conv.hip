@@ -2402,7 +2402,7 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 static int g_s1_variant = env_int("RPC_DENSE_S1", 0);   // A/B: RPC_DENSE_S1=<knob 0 value> for a whole run
-static int g_wgrad_variant = 0;
+static int g_wgrad_variant = env_int("RPC_DENSE_WGRAD", 0);   // A/B: RPC_DENSE_WGRAD=<knob 1 value>
 static int g_s1x_dbg = 0;          // knob 4: k_conv3x3x timing experiments (0 = the real kernel)
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 

@@ -385,7 +385,10 @@ def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
 # layer's BN-backward apply, joined at the end of the backbone backward), beside the data-gradient chain.
 # Off: measured slower (SECOND 835.8 / 827.8 -> 766.0 / 627.2 frames/s, CenterPoint 164.8 -> 158.1,
 # profiles/r04_ab_dense_wg_side.txt): the one-block-per-CU S1 kernels and the weight gradient contend for
-# the CUs and the chain behind them waits longer (as round 1 measured with the former kernels)
+# the CUs and the chain behind them waits longer (as round 1 measured with the former kernels). Only the
+# slab reductions on the side stream (the row-chunk kernels on the training stream) measured slower still:
+# 842.7 / 841.5 -> 755.9 / 739.7 frames/s (profiles/r04_ab_dense_wgred_side.txt) — the fork / join per layer
+# inside the captured backward costs more than the 11 us reductions it moves
 WG_SIDE = os.environ.get("RPC_DENSE_WG_SIDE", "0") != "0"
 _WG_STREAMS = {}
 

@@ -17,6 +17,7 @@
 
 #include <map>
 #include <mutex>
+#include <cstdlib>
 #include <vector>
 
 #include "common.h"
@@ -70,6 +71,17 @@ hipEvent_t event_at(DevEvents* d, size_t i) {
   return d->ev[i];
 }
 
+// RPC_SPARSE_RES_FUSE=0 (A/B): the basicblock residual backward as its own pass (rpc_sparse_res_backward) instead
+// of in the epilogue of the bf16 data-gradient GEMM that produces the block output's gradient (rpc_spconv_gemm_res)
+int g_res_fuse = -1;
+bool res_fuse() {
+  if (g_res_fuse < 0) {
+    const char* e = getenv("RPC_SPARSE_RES_FUSE");
+    g_res_fuse = (e && atoi(e) == 0) ? 0 : 1;
+  }
+  return g_res_fuse == 1;
+}
+
 int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coors_last, const int* shape, int flags,
         float* dfeat, Arena& A, hipStream_t st, hipStream_t wg, DevEvents* evs) {
 #define CHK(x)                 \
@@ -89,16 +101,24 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
   std::vector<std::vector<const float*>> G(nl);
   const bool split = wg != nullptr && wg != st;
   float* bnb_fused = nullptr;   // bnb of layer li, already finalized by layer li+1's data-gradient launch
+  // block outputs whose residual backward (m rows + partial sums) the layer above's data gradient produced
+  std::vector<char> res_done(nl, 0);
+  std::vector<float*> res_m(nl, nullptr), res_part(nl, nullptr);
   for (int li = nl - 1; li >= 0; --li) {
     const RpcSparseLayer& l = L[li];
     const int n_out = l.n_out;
     if (l.mat) {
-      if (G[li].empty()) return RPC_ERR_ARG;
-      dy = (float*)A.take(sizeof(float) * (size_t)n_out * l.co);
       nblk = cdiv(n_out, BM) > 0 ? cdiv(n_out, BM) : 1;
-      part = (float*)A.take(sizeof(float) * (size_t)nblk * 2 * l.co);
-      CHK(rpc_sparse_res_backward(G[li][0], G[li].size() > 1 ? G[li][1] : nullptr, l.out, l.z, l.bn, n_out, l.co, dy,
-                                  part, st));
+      if (res_done[li]) {
+        dy = res_m[li];
+        part = res_part[li];
+      } else {
+        if (G[li].empty()) return RPC_ERR_ARG;
+        dy = (float*)A.take(sizeof(float) * (size_t)n_out * l.co);
+        part = (float*)A.take(sizeof(float) * (size_t)nblk * 2 * l.co);
+        CHK(rpc_sparse_res_backward(G[li][0], G[li].size() > 1 ? G[li][1] : nullptr, l.out, l.z, l.bn, n_out, l.co,
+                                    dy, part, st));
+      }
       if (l.res >= 0) G[l.res].push_back(dy);
     }
     // BatchNorm backward statistics -> bnb, dgamma, dbeta (unless the data gradient that produced the partial
@@ -135,7 +155,18 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
     const int rev = l.kind == 0 ? 1 : 0;
     const int* pin = l.perm_in;   // visiting order of the data-gradient rows (n_in)
     const int n_in = l.n_in;
-    if (li > 0 && L[li - 1].mat) {
+    if (li > 0 && L[li - 1].mat && l.bf16 && res_fuse() && G[li - 1].size() <= 1) {
+      // the layer below is a block output: its residual backward in this GEMM's epilogue
+      const RpcSparseLayer& prev = L[li - 1];
+      const int nb = cdiv(n_in, BM) > 0 ? cdiv(n_in, BM) : 1;
+      float* m = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
+      float* pp = (float*)A.take(sizeof(float) * (size_t)nb * 2 * l.ci);
+      CHK(rpc_spconv_gemm_res(dzb, n_out, l.co, mp, l.kvol, rev, pin, n_in, l.btd, l.ci, m,
+                              G[li - 1].empty() ? nullptr : G[li - 1][0], prev.out, prev.z, prev.bn, pp, st));
+      res_done[li - 1] = 1;
+      res_m[li - 1] = m;
+      res_part[li - 1] = pp;
+    } else if (li > 0 && L[li - 1].mat) {
       float* din = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
       if (l.bf16)
         CHK(rpc_spconv_gemm_perm(dzb, 0, n_out, l.co, mp, l.kvol, rev, pin, n_in, l.btd, l.ci, din, nullptr, nullptr,
@@ -251,4 +282,13 @@ extern "C" int rpc_stream_priority_range(int* least, int* greatest) {
   if (!least || !greatest) return RPC_ERR_ARG;
   RPC_CHECK(hipDeviceGetStreamPriorityRange(least, greatest));
   return RPC_OK;
+}
+
+// knob 0: the fused residual backward (1 on, 0 off; the default follows RPC_SPARSE_RES_FUSE). Returns the
+// previous value; value < 0 only reads it.
+extern "C" int rpc_sparse_tune(int knob, int value) {
+  if (knob != 0) return RPC_ERR_ARG;
+  const int old = res_fuse() ? 1 : 0;
+  if (value >= 0) g_res_fuse = value ? 1 : 0;
+  return old;
 }

@@ -80,7 +80,9 @@ __device__ __forceinline__ f32x4 mfma16(uint4 a, uint4 b, f32x4 c) {
                                                    0);
 }
 
-enum { E_FWD = 0, E_DGRAD = 1, E_PLAIN = 2 };
+// E_RES: the data gradient into a basicblock's output rows: m = (acc + g2) * [out > 0] with the BatchNorm-
+// backward partial sums (sum m, sum m * xhat(z)) of that layer — rpc_sparse_res_backward fused into the GEMM
+enum { E_FWD = 0, E_DGRAD = 1, E_PLAIN = 2, E_RES = 3 };
 
 struct GB {
   const u16* a;       // gathered source rows [Nsrc][CP] bf16
@@ -97,6 +99,8 @@ struct GB {
   RpcBnFin fin;       // BatchNorm finalize by the last-arriving blocks (fin.ticket null: off)
   int fmt;            // operand format of a and bt: 0 bf16, 1 fp16 (E_FWD only)
   const int* perm;    // row visiting order [Nout] (rpc_rulebook_mask_perm) or null; rows are written in place
+  const float* eg2;   // E_RES: the other gradient contribution [Nout][CO_real] (identity path) or null
+  const float* eout;  // E_RES: the block output rows [Nout][CO_real] (ReLU mask)
 };
 
 // ---- BatchNorm finalize fused into the GEMM (k_gemm_pipe, RpcBnFin): the partial rows every block writes
@@ -364,20 +368,34 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
 #pragma unroll
     for (int n = 0; n < NT; ++n) {
       int col = n * 16 + (lane & 15);
-      float zr[4], pb[4];
-      if (EPI == E_DGRAD) {
+      float zr[4], pb[4], orr[4], g2r[4];
+      if (EPI == E_DGRAD || EPI == E_RES) {
         const int C = g.CO_real, cc = min(col, C - 1);
 #pragma unroll
         for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];   // scale, beta, mean, invstd
 #pragma unroll
         for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)max(prow[rt][j], 0) * C + cc];
       }
+      if (EPI == E_RES) {
+        const int C = g.CO_real, cc = min(col, C - 1);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long long e = (long long)max(prow[rt][j], 0) * C + cc;
+          orr[j] = g.eout[e];
+          g2r[j] = g.eg2 ? g.eg2[e] : 0.0f;
+        }
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         int row = prow[rt][j];
         float v = acc[rt][n][j];
         if (row >= 0 && col < g.CO_real) {
-          if (EPI == E_DGRAD) {
+          if (EPI == E_RES) {
+            const float gg = v + g2r[j];
+            v = orr[j] > 0.0f ? gg : 0.0f;
+            s1[n] += v;
+            s2[n] += v * ((zr[j] - pb[2]) * pb[3]);
+          } else if (EPI == E_DGRAD) {
             const float zz = zr[j];
             float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
             v = h > 0.0f ? v : 0.0f;
@@ -1319,6 +1337,7 @@ static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
     hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, 0, true>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_RES) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_RES>), dim3(nblk), dim3(64 * GW), 0, st, a);
   else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(64 * GW), 0, st, a);
 }
 
@@ -1373,6 +1392,7 @@ static int launch(int KGP, int NT, int epi, const GB& a, int n_rows, hipStream_t
   }
   // 64-wide GEMM K with two row tiles per wave (rt_of): 4-wave blocks by default (8 x 4 KB of gathered rows
   // per stage would not fit 4 stages); 128-wide: 4-wave blocks (a 32 KB weight tile per stage at 128 x 128)
+  if (epi == E_RES) mode = 0;   // the regular kernel only
   if (mode >= 4 && KGP == 64 && NT == 4) {   // timing arms of k_gemm_bf16 (DBG = mode - 4)
     const int nblk = (n_rows + 127) / 128;
 #define DB(d)                                                                                              \
@@ -1547,6 +1567,21 @@ extern "C" int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, c
   g.fmt = fmt;
   g.perm = perm;
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
+}
+
+// the data gradient into a basicblock's output rows with rpc_sparse_res_backward fused into its epilogue:
+// m = (dgrad + g2) * [out > 0] -> m [n_out][ng] fp32, and the BatchNorm-backward partial rows (sum m,
+// sum m * (z - mean) * invstd) of that layer (bn: scale, beta, mean, invstd) -> part [gemm blocks][2 * ng]
+extern "C" int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
+                                   const int* perm, int n_out, const void* bt, int ng, float* m, const float* g2,
+                                   const float* out, const float* z, const float* bn, float* part, void* stream) {
+  if (!m || !out || !z || !bn || !part) return RPC_ERR_ARG;
+  GB g;
+  memset(&g, 0, sizeof(g));
+  g.perm = perm;
+  g.eg2 = g2;
+  g.eout = out;
+  return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, m, z, bn, part, E_RES, stream);
 }
 
 // largest block of the k_gemm_pipe launches (rows): fin_groups of n_out at the smallest block (64 rows)

@@ -110,3 +110,58 @@ def test_basicblock_nuscenes_bf16_close_to_oracle():
     for i, (m, p) in enumerate(zip(enc.layers(), orc.params)):
         c = cos(m[0].weight.grad.cpu().double(), p["W"].grad)
         assert c > 0.95, (i, c)
+
+
+def test_fused_residual_backward_matches_separate():
+    """The bf16 basicblock encoder's backward with the residual backward fused into the data-gradient GEMMs
+    (rpc_sparse_tune knob 0 = 1, the default) against the separate rpc_sparse_res_backward passes: the m rows
+    are the same, the BatchNorm-backward partial sums are added in another order, and a last-bit difference there
+    moves bf16 roundings and ReLU decisions downstream — every gradient within relative L2 5e-2 of the separate
+    path (the bound of the row-order test, tests/test_gpu_sparse_pipe.py; measured 6.4e-3 on the input gradient),
+    the input gradient as close to the float64 oracle as the separate path's, bit-identical from run to run."""
+    from robustpointclouds_amd import _ffi
+    lib = _ffi.load()
+    torch.manual_seed(0)
+    B = 1
+    feats, coors = _inputs(B, stride=4)
+    enc = SparseEncoder(5, NUS_SHAPE, output_channels=128,
+                        encoder_channels=((16, 16, 32), (32, 32, 64), (64, 64, 128), (128, 128)),
+                        encoder_paddings=((0, 0, 1), (0, 0, 1), (0, 0, [0, 1, 1]), (1, 1)),
+                        block_type="basicblock").to(DEV)
+    enc.bf16 = True
+    G = torch.randn((B, 256, 128, 128), generator=torch.Generator().manual_seed(1)).to(DEV)
+    bns = [m[1] for m in enc.layers()]
+    saved = [(b.running_mean.clone(), b.running_var.clone()) for b in bns]
+
+    def step(fuse):
+        old = lib.rpc_sparse_tune(0, fuse)
+        try:
+            for q in enc.parameters():
+                q.grad = None
+            for b, (mm, vv) in zip(bns, saved):
+                b.running_mean.copy_(mm)
+                b.running_var.copy_(vv)
+            f = torch.from_numpy(feats).to(DEV).requires_grad_(True)
+            out = enc(f, torch.from_numpy(coors).to(DEV), B)
+            (out * G).sum().backward()
+            torch.cuda.synchronize()
+            return [f.grad.clone()] + [q.grad.clone() for q in enc.parameters()]
+        finally:
+            lib.rpc_sparse_tune(0, old)
+
+    sep, fa, fb = step(0), step(1), step(1)
+    for x, y in zip(fa, fb):
+        assert torch.equal(x, y)
+    worst = 0.0
+    for i, (x, y) in enumerate(zip(fa, sep)):
+        d = ((x.double() - y.double()).norm() / y.double().norm().clamp_min(1e-30)).item()
+        worst = max(worst, d)
+        assert d <= 5e-2, (i, d)
+    print(f"fused vs separate residual backward: worst relative L2 {worst:.2e}")
+    orc = OracleSparseEncoder(enc)
+    ref_f = torch.from_numpy(feats).double().requires_grad_(True)
+    (orc.forward(ref_f, coors, B) * G.cpu().double()).sum().backward()
+    rel = lambda x: ((x.cpu().double() - ref_f.grad).norm() / ref_f.grad.norm()).item()
+    ef, es = rel(fa[0]), rel(sep[0])
+    print(f"input gradient vs float64: fused {ef:.3e}, separate {es:.3e}")
+    assert ef <= 1.1 * es + 1e-3, (ef, es)

@@ -293,3 +293,47 @@ def test_mask_order_encoder_step_close_and_deterministic():
         worst = max(worst, d)
         assert d < 5e-2, (i, d)
     print(f"mask order vs index order: worst relative L2 {worst:.2e}")
+
+
+@pytest.mark.parametrize("kg,ng,n_out,K,g2", [(32, 32, 3000, 27, True), (128, 128, 700, 27, False),
+                                               (64, 64, 129, 3, True), (16, 16, 1, 27, True)])
+def test_gemm_res_matches_separate_residual_backward(kg, ng, n_out, K, g2):
+    """rpc_spconv_gemm_res (the basicblock residual backward in the data-gradient epilogue) against the plain
+    GEMM followed by rpc_sparse_res_backward: m = (dgrad + g2) * [out > 0] bit-identical, the BatchNorm-backward
+    partial rows equal up to the summation order (the same 64-row groups)."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(n_out + kg + K)
+    n_src = max(n_out, 500)
+    nbr = torch.randint(0, n_src, (n_out, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n_out, K), generator=g) > 0.3] = -1
+    a = torch.zeros((n_src, _r8(kg)), dtype=torch.bfloat16)
+    a[:, :kg] = torch.randn((n_src, kg), generator=g).to(torch.bfloat16)
+    W = torch.randn((K, kg, ng), generator=g) * 0.1
+    a, nbr, W = a.to(dev), nbr.to(dev), W.to(dev)
+    st = _ffi.stream_of(W)
+    bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(K, kg, ng, 0), dtype=torch.bfloat16, device=dev)
+    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), K, kg, ng, 0, _ffi.ptr(bt), st), "prep")
+    out = torch.randn((n_out, ng), generator=g).to(dev)
+    z = torch.randn((n_out, ng), generator=g).to(dev)
+    gid = torch.randn((n_out, ng), generator=g).to(dev) if g2 else None
+    bn = torch.cat([torch.rand(ng, generator=g) + 0.5, torch.randn(ng, generator=g) * 0.1,
+                    torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
+    nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
+    # separate: plain GEMM, then the residual pass
+    din, _ = _run(lib, 0, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 2, None, None, dev)
+    m_ref = torch.full((n_out, ng), float("nan"), device=dev)
+    p_ref = torch.full((nblk, 2 * ng), float("nan"), device=dev)
+    _ffi.check(lib.rpc_sparse_res_backward(_ffi.ptr(gid) if g2 else _ffi.ptr(din), _ffi.ptr(din) if g2 else None,
+                                           _ffi.ptr(out), _ffi.ptr(z), _ffi.ptr(bn), n_out, ng, _ffi.ptr(m_ref),
+                                           _ffi.ptr(p_ref), st), "rpc_sparse_res_backward")
+    # fused
+    m = torch.full((n_out, ng), float("nan"), device=dev)
+    p = torch.full((nblk, 2 * ng), float("nan"), device=dev)
+    _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, None, n_out, _ffi.ptr(bt), ng,
+                                       _ffi.ptr(m), _ffi.ptr(gid) if g2 else None, _ffi.ptr(out), _ffi.ptr(z),
+                                       _ffi.ptr(bn), _ffi.ptr(p), st), "rpc_spconv_gemm_res")
+    torch.cuda.synchronize()
+    assert torch.equal(m, m_ref)
+    scale = torch.cat([m.abs().sum(0), (m * ((z - bn[2 * ng:3 * ng]) * bn[3 * ng:])).abs().sum(0)])
+    assert torch.all((p.sum(0) - p_ref.sum(0)).abs() <= 1e-5 * scale + 1e-6)

@@ -301,12 +301,13 @@ int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, i
 /* the data gradient into a basicblock's output rows with rpc_sparse_res_backward in its epilogue (r04):
  * m = (dgrad + g2) * [out > 0] -> m [n_out][ng] fp32 (g2: the identity path's contribution or NULL; out: the
  * block output rows), and that layer's BatchNorm-backward partial rows (sum m, sum m * (z - mean) * invstd;
- * bn = scale, beta, mean, invstd) -> part [rpc_spconv_gemm_blocks(n_out)][2 * ng]. perm as rpc_spconv_gemm_perm. */
+ * bn = scale, beta, mean, invstd) -> part [rpc_spconv_gemm_blocks(n_out)][2 * ng]. perm as rpc_spconv_gemm_perm;
+ * fin (mode 1, or NULL): that layer's BatchNorm-backward finalize in the last-arriving blocks. */
 /* knob 0: rpc_sparse_backward's fused residual backward (1 on, 0 off); returns the previous value */
 int rpc_sparse_tune(int knob, int value);
 int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev, const int* perm,
                         int n_out, const void* bt, int ng, float* m, const float* g2, const float* out, const float* z,
-                        const float* bn, float* part, void* stream);
+                        const float* bn, float* part, const RpcBnFin* fin, void* stream);
 /* the same with the operand format of rpc_spconv_gemm_h16 (fmt 1 = fp16: the forward, epi 0, only) */
 int rpc_spconv_gemm_h16_fin(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
                             const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,

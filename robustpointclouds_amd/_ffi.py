@@ -164,7 +164,8 @@ SIGNATURES = {
     "rpc_spconv_gemm_bf16_fin": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
                                        C.POINTER(RpcBnFin), vp]),
     "rpc_sparse_tune": (i32, [i32, i32]),
-    "rpc_spconv_gemm_res": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp, vp]),
+    "rpc_spconv_gemm_res": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, vp, i32, vp, vp, vp, vp, vp, vp,
+                                  C.POINTER(RpcBnFin), vp]),
     "rpc_spconv_gemm_h16_fin": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
                                        C.POINTER(RpcBnFin), vp]),
     "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),

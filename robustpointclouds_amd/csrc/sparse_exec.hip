@@ -161,8 +161,23 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
       const int nb = cdiv(n_in, BM) > 0 ? cdiv(n_in, BM) : 1;
       float* m = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
       float* pp = (float*)A.take(sizeof(float) * (size_t)nb * 2 * l.ci);
+      RpcBnFin fin;
+      const RpcBnFin* fp = nullptr;
+      if (l.fin_ticket && n_in > 0) {   // + that layer's BatchNorm-backward finalize (bnb, dgamma, dbeta)
+        memset(&fin, 0, sizeof(fin));
+        fin.ticket = l.fin_ticket;
+        fin.gpart = (double*)A.take(sizeof(double) * 2 * (size_t)rpc_bn_fin_groups(n_in) * l.ci);
+        fin.mode = 1;
+        fin.gamma = prev.gamma;
+        fin.beta = prev.beta;
+        fin.fbn = prev.bn;
+        fin.bn = bnb_fused = (float*)A.take(sizeof(float) * 5 * (size_t)l.ci);
+        fin.dgamma = prev.dgamma;
+        fin.dbeta = prev.dbeta;
+        fp = &fin;
+      }
       CHK(rpc_spconv_gemm_res(dzb, n_out, l.co, mp, l.kvol, rev, pin, n_in, l.btd, l.ci, m,
-                              G[li - 1].empty() ? nullptr : G[li - 1][0], prev.out, prev.z, prev.bn, pp, st));
+                              G[li - 1].empty() ? nullptr : G[li - 1][0], prev.out, prev.z, prev.bn, pp, fp, st));
       res_done[li - 1] = 1;
       res_m[li - 1] = m;
       res_part[li - 1] = pp;

@@ -1574,10 +1574,15 @@ extern "C" int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, c
 // sum m * (z - mean) * invstd) of that layer (bn: scale, beta, mean, invstd) -> part [gemm blocks][2 * ng]
 extern "C" int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
                                    const int* perm, int n_out, const void* bt, int ng, float* m, const float* g2,
-                                   const float* out, const float* z, const float* bn, float* part, void* stream) {
+                                   const float* out, const float* z, const float* bn, float* part,
+                                   const RpcBnFin* fin, void* stream) {
   if (!m || !out || !z || !bn || !part) return RPC_ERR_ARG;
+  if (fin && (fin->mode != 1 || !fin->ticket || !fin->gpart || !fin->gamma || !fin->fbn || !fin->bn || ng > 256 ||
+              n_out <= 0))
+    return RPC_ERR_ARG;
   GB g;
   memset(&g, 0, sizeof(g));
+  if (fin) g.fin = *fin;   // + that layer's BatchNorm-backward finalize (mode 1) in the last-arriving blocks
   g.perm = perm;
   g.eg2 = g2;
   g.eout = out;

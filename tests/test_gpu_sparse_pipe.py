@@ -332,7 +332,7 @@ def test_gemm_res_matches_separate_residual_backward(kg, ng, n_out, K, g2):
     p = torch.full((nblk, 2 * ng), float("nan"), device=dev)
     _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, None, n_out, _ffi.ptr(bt), ng,
                                        _ffi.ptr(m), _ffi.ptr(gid) if g2 else None, _ffi.ptr(out), _ffi.ptr(z),
-                                       _ffi.ptr(bn), _ffi.ptr(p), st), "rpc_spconv_gemm_res")
+                                       _ffi.ptr(bn), _ffi.ptr(p), None, st), "rpc_spconv_gemm_res")
     torch.cuda.synchronize()
     assert torch.equal(m, m_ref)
     scale = torch.cat([m.abs().sum(0), (m * ((z - bn[2 * ng:3 * ng]) * bn[3 * ng:])).abs().sum(0)])

@@ -737,13 +737,16 @@ class SparseEncoderFn(torch.autograd.Function):
             if sp.mat:
                 # d out -> ReLU mask -> d(bn output); the block identity receives the same gradient
                 g = G[li]
-                dy = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
                 nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
-                part = torch.empty((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
-                _ffi.check(lib.rpc_sparse_res_backward(_ffi.ptr(g[0]), _ffi.ptr(g[1] if len(g) > 1 else None),
-                                                       _ffi.ptr(rec["out"]), _ffi.ptr(rec["z"]), _ffi.ptr(rec["bn"]),
-                                                       n_out, sp.co, _ffi.ptr(dy), _ffi.ptr(part), st),
-                           "rpc_sparse_res_backward")
+                if rec.get("res_m") is not None:   # done by the layer above's data-gradient epilogue
+                    dy, part = rec.pop("res_m"), rec.pop("res_part")
+                else:
+                    dy = torch.empty((n_out, sp.co), dtype=torch.float32, device=dev)
+                    part = torch.empty((nblk, 2 * sp.co), dtype=torch.float32, device=dev)
+                    _ffi.check(lib.rpc_sparse_res_backward(_ffi.ptr(g[0]), _ffi.ptr(g[1] if len(g) > 1 else None),
+                                                           _ffi.ptr(rec["out"]), _ffi.ptr(rec["z"]),
+                                                           _ffi.ptr(rec["bn"]), n_out, sp.co, _ffi.ptr(dy),
+                                                           _ffi.ptr(part), st), "rpc_sparse_res_backward")
                 G[li] = None
                 if sp.res >= 0:
                     G[sp.res].append(dy)
@@ -805,7 +808,19 @@ class SparseEncoderFn(torch.autograd.Function):
             else:
                 mp, rev = rec["nbr_in"], 0
             din = torch.empty((n_in, sp.ci), dtype=torch.float32, device=dev)
-            if li > 0 and L[li - 1]["spec"].mat:
+            if li > 0 and L[li - 1]["spec"].mat and rec["bf16"] and lib.rpc_sparse_tune(0, -1) and len(G[li - 1]) <= 1:
+                # the input is a block output: its residual backward in this data gradient's epilogue
+                # (rpc_spconv_gemm_res), as rpc_sparse_backward does
+                prev = L[li - 1]
+                nb = max(lib.rpc_spconv_gemm_blocks(n_in), 1)
+                pp = torch.empty((nb, 2 * sp.ci), dtype=torch.float32, device=dev)
+                gid = G[li - 1][0] if G[li - 1] else None
+                _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev,
+                                                   _ffi.ptr(rec["perm_in"]), n_in, _ffi.ptr(btd), sp.ci, _ffi.ptr(din),
+                                                   _ffi.ptr(gid), _ffi.ptr(prev["out"]), _ffi.ptr(prev["z"]),
+                                                   _ffi.ptr(prev["bn"]), _ffi.ptr(pp), None, st), "rpc_spconv_gemm_res")
+                prev["res_m"], prev["res_part"] = din, pp
+            elif li > 0 and L[li - 1]["spec"].mat:
                 # the input is a materialised output: plain data gradient, masked by its own backward
                 if rec["bf16"]:
                     _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _ffi.ptr(rec["perm_in"]), n_in,

@@ -97,10 +97,12 @@ def _traffic(kernel_tag):
         return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
     files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic*.json")),
                    key=order)
+    loose = kernel_tag[:-1] + "," if kernel_tag.endswith(">") else None   # trailing template arguments omitted
     for f in reversed(files):
         d = json.load(open(f))
         for name, v in d.get("kernels", {}).items():
-            if name.split("(")[0].strip() == kernel_tag or name.startswith(kernel_tag + "("):
+            base = name.split("(")[0].strip()
+            if base == kernel_tag or name.startswith(kernel_tag + "(") or (loose and base.startswith(loose)):
                 return v.get("hbm_bytes_per_launch"), os.path.basename(f)
     return None, None
 
@@ -328,10 +330,16 @@ def main():
     tr = Trainer(model, ddp=dist.is_initialized(), bf16=not a.fp32, device=dev)
     from robustpointclouds_amd import dense_bev
     from robustpointclouds_amd.sparse_encoder import KernelTimer
+    sparse_timer = None
     if a.roofline_kernel == "dense":
         timer = dense_bev.ConvTimer()
         dense_bev.TIMER = timer
         op = ci = co = None
+        # every sparse conv launch too (forward, data and weight gradients): the roofline entry is the MFMA
+        # kernel with the most time per step across dense and sparse (config 4's is sparse)
+        if getattr(model, "middle_encoder", None) is not None:
+            sparse_timer = KernelTimer()
+            model.middle_encoder.timer = sparse_timer
     else:
         op, ci, co = a.roofline_kernel.split(",")
         timer = KernelTimer(op, int(ci), int(co))
@@ -364,6 +372,8 @@ def main():
     graphs = dense_bev.GRAPHS
     dense_bev.GRAPHS = False
     timer.enabled = True
+    if sparse_timer is not None:
+        sparse_timer.enabled = True
     stage_timer.TIMER.enabled = True
     me = getattr(model, "middle_encoder", None)
     for i in range(a.steps, a.steps + 2):
@@ -372,9 +382,12 @@ def main():
         tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0], next_ready=ready)
     torch.cuda.synchronize()
     timer.enabled = False
+    if sparse_timer is not None:
+        sparse_timer.enabled = False
     stage_timer.TIMER.enabled = False
     dense_bev.GRAPHS = graphs
     ks = timer.summary()
+    sks = sparse_timer.per_kernel() if sparse_timer is not None else {}
     stages = stage_timer.TIMER.summary()
     step_flops = None
     if me is not None and me.flop_probe and not nus:
@@ -472,6 +485,16 @@ def main():
                                  ms_per_step=round(c["ms"] / 2, 4),
                                  work="2*B*H*W*C_in*C_out*9 FLOP per launch over every launch of the kernel "
                                       "(forward, data gradient, fused-epilogue data gradient)"))
+            # the sparse conv kernels (HIP events per launch; FLOPs from the valid rulebook pairs)
+            for name, k in sks.items():
+                pk = PEAK["bf16_mfma"] if k["dtype"] == "bf16" else PEAK["fp32_mfma"]
+                tr_bytes, tr_src = _traffic(name)
+                alls.append(dict(bound="mfma", kernel=name, achieved=round(k["tflops"], 3), peak=pk, unit="TFLOP/s",
+                                 frac=round(k["tflops"] / pk, 4), traffic=tr_bytes, traffic_source=tr_src,
+                                 avg_launch_ms=round(k["avg_ms"], 4), launches=k["launches"],
+                                 flops_per_launch=k["flops_per_launch"], ms_per_step=round(k["total_ms"] / 2, 4),
+                                 work="2*C_in*C_out FLOP per valid rulebook pair (sparse conv, " + k["dtype"] +
+                                      " MFMA; timed in the per-layer backward loop)"))
             alls.sort(key=lambda e: -e["ms_per_step"])
             res["roofline"] = dict(alls[0])
             res["roofline_kernels"] = alls + ents

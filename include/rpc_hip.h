@@ -295,51 +295,48 @@ typedef struct {
 } RpcBnFin;
 int rpc_bn_fin_groups(int n_out);
 int rpc_bn_fin_tickets(int n_out);
-int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
-                             const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
-                             float* part, int epi, const RpcBnFin* fin, void* stream);
+/* Per-block source-row unions of a rulebook map [n][kvol] (r05; no reference counterpart — spconv's implicit
+ * GEMM gathers per offset): for each block of RPC_UNION_ROWS consecutive rows, the distinct source rows its
+ * valid entries name (ulist[block][0..ucnt)) and each entry rewritten as the slot of its source in that list
+ * (lnbr, 0xFFFF = no neighbour). The 16-bit GEMMs below gather a block's list into LDS once instead of one
+ * gather round trip per offset; blocks with ucnt above the kernel's LDS capacity gather from the map as before.
+ * lnbr: [n][kvol] u16; ulist: [rpc_rulebook_union_blocks(n)][RPC_UNION_CAP] int; ucnt: [blocks] int. The union
+ * serves every GEMM whose OUTPUT rows are the map's rows (forward, and with rev the submanifold data gradient). */
+#define RPC_UNION_ROWS 128
+#define RPC_UNION_CAP 512
+typedef struct {
+  const unsigned short* lnbr;
+  const int* ulist;
+  const int* ucnt;
+} RpcRowUnion;
+int rpc_rulebook_union_blocks(int n);
+int rpc_rulebook_union(const int* nbr, int n, int kvol, unsigned short* lnbr, int* ulist, int* ucnt, void* stream);
+/* data gradient (epi 1) only; un: unions of `map` or NULL */
+int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
+                             const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                             const float* prev_bn, float* part, int epi, const RpcBnFin* fin, void* stream);
 /* the data gradient into a basicblock's output rows with rpc_sparse_res_backward in its epilogue (r04):
  * m = (dgrad + g2) * [out > 0] -> m [n_out][ng] fp32 (g2: the identity path's contribution or NULL; out: the
  * block output rows), and that layer's BatchNorm-backward partial rows (sum m, sum m * (z - mean) * invstd;
- * bn = scale, beta, mean, invstd) -> part [rpc_spconv_gemm_blocks(n_out)][2 * ng]. perm as rpc_spconv_gemm_perm;
+ * bn = scale, beta, mean, invstd) -> part [rpc_spconv_gemm_blocks(n_out)][2 * ng]. un as rpc_spconv_gemm_ex;
  * fin (mode 1, or NULL): that layer's BatchNorm-backward finalize in the last-arriving blocks. */
 /* knob 0: rpc_sparse_backward's fused residual backward (1 on, 0 off); returns the previous value */
 int rpc_sparse_tune(int knob, int value);
-int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev, const int* perm,
+int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev, const RpcRowUnion* un,
                         int n_out, const void* bt, int ng, float* m, const float* g2, const float* out, const float* z,
                         const float* bn, float* part, const RpcBnFin* fin, void* stream);
-/* the same with the operand format of rpc_spconv_gemm_h16 (fmt 1 = fp16: the forward, epi 0, only) */
-int rpc_spconv_gemm_h16_fin(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
-                            const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
-                            float* part, int epi, const RpcBnFin* fin, void* stream);
-/* the general form: operand format fmt and the rows visited in the order perm ([n_out] row indices, a
- * permutation: rpc_rulebook_mask_perm of `map`; NULL = natural order). Every row is written in place and its
- * own sums are those of the natural order; only the BatchNorm partial rows (sums over 64 visited rows) differ. */
-int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
-                         const int* perm, int n_out, const void* bt, int ng, float* out, const float* prev_z,
-                         const float* prev_bn, float* part, int epi, void* stream);
-/* the rows of a rulebook map [n][kvol] ordered by their neighbour masks within windows of 2048 rows
- * (perm[i] = the row visited i-th): the 16-row MFMA tiles of rpc_spconv_gemm_perm then share offsets.
- * No reference counterpart (spconv's implicit GEMM visits rows in index order). */
-int rpc_rulebook_mask_perm(const int* nbr, int n, int kvol, int* perm, void* stream);
-/* kernel behind rpc_spconv_gemm_bf16[_n|_fin] (A/B measurement, tests; env RPC_SPGEMM): 0 (default) = one
- * offset of look-ahead in registers, 1 = the S-stage LDS-DMA ring (k_gemm_pipe), 2 / 3 = its 4-wave / 3-stage
- * forms. Same bits in every mode. 4..19: timing arms (garbage results). mode < 0 queries. Returns the
- * previous mode. */
-int rpc_spconv_gemm_bf16_mode(int mode);
+/* the general form: operand format fmt (RPC_H16_F16: the forward, epi 0, only) and the per-block source-row
+ * unions of `map` (rpc_rulebook_union; NULL = every gather from global memory). Same results either way. */
+int rpc_spconv_gemm_ex(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
+                       const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                       const float* prev_bn, float* part, int epi, void* stream);
 /* dW[k] = sum_r h[nbr[r,k]]^T dz[r] (bf16 rows, fp32 accumulate, fixed-order reduction) */
 size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co);
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
                           float* dW, void* workspace, size_t workspace_bytes, void* stream);
-/* the same with h in format hfmt (fp16 forward rows are rounded to bf16 as they are staged); dispatches to
- * rpc_spconv_wgrad_pairs when RPC_SPWG_PAIRS=1 (A/B; rpc_spconv_wgrad_bf16_workspace_size sizes for it) */
+/* the same with h in format hfmt (fp16 forward rows are rounded to bf16 as they are staged) */
 int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out, const void* dz,
                          int co, float* dW, void* workspace, size_t workspace_bytes, void* stream);
-/* r04: the weight gradient over per-offset pair lists compacted from nbr (only rows with a neighbour at k
- * cost work), blocks balanced over the pairs, one partial per block reduced per offset in block order */
-size_t rpc_spconv_wgrad_pairs_workspace_size(int n_out, int kvol, int ci, int co);
-int rpc_spconv_wgrad_pairs(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out, const void* dz,
-                           int co, float* dW, void* workspace, size_t workspace_bytes, void* stream);
 
 /* ---- a6 runtime: the whole SparseEncoder backward in one call (csrc/sparse_exec.hip).
  * Replaces the per-layer backward of upstream mmdet3d SparseEncoder (adversarial_voxelnet.py:141;
@@ -371,8 +368,8 @@ typedef struct {
   float* dgamma;
   float* dbeta;
   int h_fmt;             /* bf16 layers: format of h_in (RPC_H16_BF16 / RPC_H16_F16) */
-  const int* perm_out;   /* bf16 layers (optional): visiting order of the forward map's rows (n_out) */
-  const int* perm_in;    /* bf16 layers (optional): visiting order of the data-gradient map's rows (n_in) */
+  const RpcRowUnion* un_out; /* bf16 layers (optional): unions of nbr (the submanifold data gradient's map) */
+  const RpcRowUnion* un_in;  /* bf16 strided layers (optional): unions of nbr_in (their data gradient's map) */
   unsigned* fin_ticket;  /* bf16 layers: rpc_bn_fin_tickets(n_in) zeroed counters — the data gradient into the
                             layer below then finalizes that layer's BatchNorm backward in its own launch
                             (rpc_spconv_gemm_bf16_fin); NULL: a separate rpc_bn_finalize */

@@ -713,6 +713,11 @@ __global__ __launch_bounds__(FBLK) void k_from_dense(const T* __restrict__ gd, c
   }
 }
 
+// fp16 rows: finite values beyond the fp16 range saturate to +-65504 (inf / NaN pass through)
+__device__ __forceinline__ float sat_f16(float f) {
+  return (fabsf(f) > 65504.0f && fabsf(f) < __builtin_inff()) ? copysignf(65504.0f, f) : f;
+}
+
 // ------------------------------------------------------------------ SparseBasicBlock residual
 // forward: out = relu(bn(z) + res) (res optional), fp32 rows and optionally bf16 rows [n][round8(C)]
 // (upstream mmdet3d SparseBasicBlock.forward: norm2, + identity, relu; also materialises a plain
@@ -735,7 +740,7 @@ __global__ __launch_bounds__(BLK) void k_res_fwd(const float* __restrict__ z, co
   }
   if (hb) {
     if (FMT) {
-      _Float16 h = (_Float16)v;
+      _Float16 h = (_Float16)sat_f16(v);
       hb[t] = __builtin_bit_cast(unsigned short, h);
       if (hb2) {
         __bf16 b = (__bf16)v;
@@ -783,7 +788,7 @@ __global__ __launch_bounds__(BLK) void k_res_fwd_v8(const float* __restrict__ z,
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       if (FMT) {
-        h[j] = __builtin_bit_cast(unsigned short, (_Float16)v[j]);
+        h[j] = __builtin_bit_cast(unsigned short, (_Float16)sat_f16(v[j]));
         b2[j] = __builtin_bit_cast(unsigned short, (__bf16)v[j]);
       } else {
         h[j] = __builtin_bit_cast(unsigned short, (__bf16)v[j]);
@@ -1114,60 +1119,75 @@ static KGeom geom(const int* ks, const int* st, const int* pd) {
   return g;
 }
 
-// ------------------------------------------------------------------ neighbour-mask row order
-// Rows of a rulebook visited in order of their neighbour masks (bit k = a neighbour at offset k) within
-// windows of PW rows: the 16-row MFMA tiles of the implicit GEMM then hold rows that share most offsets, so
-// fewer tiles multiply a row with no neighbour (the useful fraction of MFMA rows of SECOND's submanifold
-// layers 0.45 -> 0.78, strided 0.21 -> 0.5-0.6 by a CPU simulation), fewer gathers run out of range and fewer
-// weight fragments are read per useful row. The GEMM writes every row in place (the order only changes which
-// rows share a tile; each row's own sums are unchanged). One block per window: keys (mask << 11 | row) sorted
-// by a bitonic network in LDS — unique keys, so a fixed result. The submanifold map's transpose (rev) has the
-// reversed masks: the same order groups it alike.
-constexpr int PW = 2048, PBLK = 1024;
-__global__ __launch_bounds__(PBLK) void k_mask_perm(const int* __restrict__ nbr, int N, int K, int* __restrict__ perm) {
-  __shared__ unsigned long long key[PW];
-  const int w0 = blockIdx.x * PW;
+// ------------------------------------------------------------------ per-block source-row unions
+// The bf16 implicit GEMM (spconv_bf16.hip) visits a map's rows in blocks of RPC_UNION_ROWS; for each block this
+// pass lists the distinct source rows its valid (row, offset) entries reference — on SECOND's rulebooks ~200
+// per 128-row block against ~1000 valid entries (tools/sim_union.py) — and rewrites each entry as the slot of
+// its source in that list. The GEMM then gathers a block's U source rows into LDS once, all loads in flight
+// together, and runs every offset's MFMAs out of LDS instead of waiting one gather round trip per offset.
+// Dedup by an open-addressing table in LDS (linear probing, CAS insert); a new key takes the next slot by an
+// LDS atomic, so slot NUMBERS depend on arrival order — what the GEMM computes does not (each entry still
+// names its own source row). Blocks with more than RPC_UNION_CAP sources keep ucnt > cap: the GEMM gathers
+// those from the map as before.
+constexpr int UHT = 8192, UBLK = 256;
+__global__ __launch_bounds__(UBLK) void k_union_build(const int* __restrict__ nbr, int N, int K,
+                                                      unsigned short* __restrict__ lnbr, int* __restrict__ ulist,
+                                                      int* __restrict__ ucnt) {
+  constexpr int R = RPC_UNION_ROWS, EPT = (R * MAXK + UBLK - 1) / UBLK;
+  __shared__ int tab[UHT];
+  __shared__ unsigned short slot_of[UHT];
+  __shared__ int cnt;
+  for (int i = threadIdx.x; i < UHT; i += UBLK) tab[i] = -1;
+  if (threadIdx.x == 0) cnt = 0;
+  __syncthreads();
+  const int r0 = blockIdx.x * R, ne = R * K;
+  const long long e0 = (long long)r0 * K;
+  const long long eN = (long long)N * K;
+  int pos[EPT];
+  int src[EPT];
 #pragma unroll
-  for (int h = 0; h < PW / PBLK; ++h) {
-    const int i = threadIdx.x + h * PBLK, r = w0 + i;
-    unsigned long long kk = ~0ull;
-    if (r < N) {
-      unsigned m = 0;
-      const int* row = nbr + (long long)r * K;
-      for (int k = 0; k < K; ++k) m |= (row[k] >= 0 ? 1u : 0u) << k;
-      kk = ((unsigned long long)m << 11) | (unsigned)i;
+  for (int j = 0; j < EPT; ++j) {
+    const int e = threadIdx.x + j * UBLK;
+    src[j] = (e < ne && e0 + e < eN) ? nbr[e0 + e] : -1;
+  }
+#pragma unroll
+  for (int j = 0; j < EPT; ++j) {
+    pos[j] = -1;
+    const int v = src[j];
+    if (v < 0) continue;
+    unsigned h = ((unsigned)v * 2654435761u) >> (32 - 13);   // UHT = 2^13
+    while (true) {
+      const int old = atomicCAS(&tab[h], -1, v);
+      if (old == -1) {
+        const int sl = atomicAdd(&cnt, 1);
+        slot_of[h] = (unsigned short)(sl < RPC_UNION_CAP ? sl : 0xFFFE);
+        if (sl < RPC_UNION_CAP) ulist[(long long)blockIdx.x * RPC_UNION_CAP + sl] = v;
+        break;
+      }
+      if (old == v) break;
+      h = (h + 1) & (UHT - 1);
     }
-    key[i] = kk;
+    pos[j] = (int)h;
   }
   __syncthreads();
-  for (int size = 2; size <= PW; size <<= 1) {
-    for (int stride = size >> 1; stride > 0; stride >>= 1) {
 #pragma unroll
-      for (int h = 0; h < PW / 2 / PBLK; ++h) {
-        const int t = threadIdx.x + h * PBLK;                       // compare-exchange pair t
-        const int i = 2 * t - (t & (stride - 1)), j = i + stride;   // i has bit `stride` clear
-        const bool up = (i & size) == 0;
-        const unsigned long long a = key[i], b = key[j];
-        if ((a > b) == up) {
-          key[i] = b;
-          key[j] = a;
-        }
-      }
-      __syncthreads();
-    }
+  for (int j = 0; j < EPT; ++j) {
+    const int e = threadIdx.x + j * UBLK;
+    if (e < ne && e0 + e < eN) lnbr[e0 + e] = pos[j] >= 0 ? slot_of[pos[j]] : (unsigned short)0xFFFF;
   }
-#pragma unroll
-  for (int h = 0; h < PW / PBLK; ++h) {
-    const int i = threadIdx.x + h * PBLK;
-    if (w0 + i < N) perm[w0 + i] = w0 + (int)(key[i] & 2047ull);
-  }
+  if (threadIdx.x == 0) ucnt[blockIdx.x] = cnt;
 }
 
-extern "C" int rpc_rulebook_mask_perm(const int* nbr, int n, int kvol, int* perm, void* stream) {
+extern "C" int rpc_rulebook_union_blocks(int n) { return cdiv(n, RPC_UNION_ROWS); }
+
+extern "C" int rpc_rulebook_union(const int* nbr, int n, int kvol, unsigned short* lnbr, int* ulist, int* ucnt,
+                                  void* stream) {
   if (n < 0 || kvol < 1 || kvol > MAXK) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
-  if (!nbr || !perm) return RPC_ERR_ARG;
-  hipLaunchKernelGGL(k_mask_perm, dim3(cdiv(n, PW)), dim3(PBLK), 0, (hipStream_t)stream, nbr, n, kvol, perm);
+  if (!nbr || !lnbr || !ulist || !ucnt) return RPC_ERR_ARG;
+  if ((long long)n * kvol >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(k_union_build, dim3(cdiv(n, RPC_UNION_ROWS)), dim3(UBLK), 0, (hipStream_t)stream, nbr, n, kvol,
+                     lnbr, ulist, ucnt);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
@@ -1464,7 +1484,10 @@ extern "C" int rpc_sparse_res_backward(const float* g1, const float* g2, const f
                                        const float* bn, int n, int c, float* m, float* part, void* stream) {
   if (n < 0 || c < 1 || c > 256 || !g1 || !out || !z || !bn || !m || !part) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
-  if (c % 4 == 0 && c >= 16 && c <= 128 && (long long)n * c < (1LL << 31))
+  // k_res_bwd_v4 needs Q = c / 4 to be a power of two: its row lanes tile a wave (64 % Q == 0), its xor
+  // shuffles run over the lane bits above log2(Q), and its blocks cover whole BM-row partial groups
+  const int q4 = c / 4;
+  if (c % 4 == 0 && c >= 16 && c <= 128 && (q4 & (q4 - 1)) == 0 && (long long)n * c < (1LL << 31))
     hipLaunchKernelGGL(k_res_bwd_v4, dim3(cdiv(n, 8 * (BLK / (c / 4)))), dim3(BLK), 0, (hipStream_t)stream, g1, g2,
                        out, z, bn, n, c, m, part);
   else

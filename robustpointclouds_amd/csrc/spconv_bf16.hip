@@ -58,8 +58,13 @@ __device__ __forceinline__ u16 to_bf16(float f) {
   __bf16 b = (__bf16)f;   // round-to-nearest-even, NaN kept (v_cvt_pk_bf16_f32)
   return __builtin_bit_cast(u16, b);
 }
+// finite values beyond the fp16 range saturate to +-65504 instead of becoming inf (which the MFMA and the
+// BatchNorm sums would turn into NaN); inf / NaN pass through as they would in bf16
+__device__ __forceinline__ float sat_f16(float f) {
+  return (fabsf(f) > 65504.0f && fabsf(f) < __builtin_inff()) ? copysignf(65504.0f, f) : f;
+}
 __device__ __forceinline__ u16 to_f16(float f) {
-  _Float16 h = (_Float16)f;   // round-to-nearest-even (v_cvt_f16_f32)
+  _Float16 h = (_Float16)sat_f16(f);   // round-to-nearest-even (v_cvt_f16_f32)
   return __builtin_bit_cast(u16, h);
 }
 // 16-bit GEMM operand format: 0 = bf16, 1 = fp16 (RPC_H16_*). fp16 (3 more mantissa bits, same MFMA rate) is
@@ -98,12 +103,15 @@ struct GB {
   float* part;        // [blocks][2*NGP] or null
   RpcBnFin fin;       // BatchNorm finalize by the last-arriving blocks (fin.ticket null: off)
   int fmt;            // operand format of a and bt: 0 bf16, 1 fp16 (E_FWD only)
-  const int* perm;    // row visiting order [Nout] (rpc_rulebook_mask_perm) or null; rows are written in place
   const float* eg2;   // E_RES: the other gradient contribution [Nout][CO_real] (identity path) or null
   const float* eout;  // E_RES: the block output rows [Nout][CO_real] (ReLU mask)
+  // source-row unions of the map's RPC_UNION_ROWS-row blocks (rpc_rulebook_union), or lnbr null
+  const unsigned short* lnbr;   // [Nout][K] slot of each entry's source in its block's list, 0xFFFF none
+  const int* ulist;             // [blocks][RPC_UNION_CAP] source rows
+  const int* ucnt;              // [blocks] list lengths (> the kernel's capacity: the block gathers from nbr)
 };
 
-// ---- BatchNorm finalize fused into the GEMM (k_gemm_pipe, RpcBnFin): the partial rows every block writes
+// ---- BatchNorm finalize fused into the GEMM (RpcBnFin, data gradients): the partial rows every block writes
 // are summed in two fixed-order levels by last-arriving blocks — each group of FGS consecutive blocks
 // (logical index lb) by its last arriver, in row order, into a double row gpart[q]; the groups by the
 // last group finisher, in group order — which then applies rpc_bn_finalize's arithmetic (mode 0 / 1) to
@@ -154,40 +162,36 @@ __device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int*
   }
   __syncthreads();
   const int N = g.Nout;
-  for (int c = threadIdx.x; c < C; c += NTHR) {
+  for (int c = threadIdx.x; c < C; c += NTHR) {   // rpc_bn_finalize mode 1
     const double s1 = sh[c], s2 = sh[C + c];
-    if (f.mode == 0) {   // k_bn_finalize mode 0
-      const double mean = s1 / N;
-      double var = s2 / N - mean * mean;
-      if (var < 0) var = 0;
-      const float invstd = 1.0f / sqrtf((float)var + f.eps);
-      f.bn[c] = f.gamma[c] * invstd;
-      f.bn[C + c] = f.beta[c];
-      f.bn[2 * C + c] = (float)mean;
-      f.bn[3 * C + c] = invstd;
-      const double uvar = N > 1 ? var * N / (N - 1) : var;
-      f.running_mean[c] = (1.0f - f.momentum) * f.running_mean[c] + f.momentum * (float)mean;
-      f.running_var[c] = (1.0f - f.momentum) * f.running_var[c] + f.momentum * (float)uvar;
-    } else {             // k_bn_finalize mode 1
-      f.bn[c] = f.gamma[c] * f.fbn[3 * C + c];
-      f.bn[C + c] = (float)(s1 / N);
-      f.bn[2 * C + c] = (float)(s2 / N);
-      f.bn[3 * C + c] = f.fbn[2 * C + c];
-      f.bn[4 * C + c] = f.fbn[3 * C + c];
-      if (f.dgamma) f.dgamma[c] = (float)s2;
-      if (f.dbeta) f.dbeta[c] = (float)s1;
-    }
+    f.bn[c] = f.gamma[c] * f.fbn[3 * C + c];
+    f.bn[C + c] = (float)(s1 / N);
+    f.bn[2 * C + c] = (float)(s2 / N);
+    f.bn[3 * C + c] = f.fbn[2 * C + c];
+    f.bn[4 * C + c] = f.fbn[3 * C + c];
+    if (f.dgamma) f.dgamma[c] = (float)s2;
+    if (f.dbeta) f.dbeta[c] = (float)s1;
   }
 }
 
+// Union path (UNI, r05): the block's RPC_UNION_ROWS rows take their source rows from the per-block union lists
+// of rpc_rulebook_union. Before the offset loop the block gathers its U distinct source rows (~200 for ~1000
+// valid entries on SECOND's maps) into LDS with every load in flight at once, then every offset's A fragments
+// are LDS reads: the loop no longer waits one gather round trip per offset (the regular path's limit: PMC
+// MFMA busy 12 %, waves waiting 57 %). Blocks whose list exceeds the kernel's LDS capacity (ucap_of) gather
+// from the map as before (same kernel, a block-uniform branch). Same products, summed in the same order per
+// accumulator: the two paths give the same bits.
+__host__ __device__ constexpr int ucap_of(int kgp) { return kgp >= 128 ? 224 : 512; }
+__host__ __device__ constexpr int gw_u(int kgp, int nt) { return RPC_UNION_ROWS / (16 * rt_of(kgp, nt)); }
+
 // Occupancy: the <= 64 x 64 tiles are held to 64 VGPRs (8 waves per SIMD, 4 blocks per CU) — at 72 the
 // 106k-row 64-channel layers needed 1.08 rounds of 3 blocks per CU (k_gemm_bf16<64,4,1> 60.6 -> 51.5 us)
-// DBG (timing attribution only, rpc_spconv_gemm_bf16_mode 4 + DBG for the 64 x 64 tiles; results are
-// garbage): bit 0 = no MFMAs, bit 1 = every gather offset out of range (no memory traffic, same
-// instructions), bit 2 = the same for the weight tiles, bit 3 = no gather instructions at all
-template <int KGP, int NT, int EPI, int DBG = 0, bool F16 = false>
-__global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) void k_gemm_bf16(GB g) {
-  constexpr int GW = gw_of(KGP, NT), GBLK = 64 * GW, RT = rt_of(KGP, NT), WR = 16 * RT, GBM = WR * GW;
+template <int KGP, int NT, int EPI, bool F16 = false, bool UNI = false>
+__global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
+                             UNI ? 1 : gemm_waves_per_simd(KGP, NT)) void k_gemm_bf16(GB g) {
+  constexpr int RT = rt_of(KGP, NT), GW = UNI ? gw_u(KGP, NT) : gw_of(KGP, NT), GBLK = 64 * GW, WR = 16 * RT,
+                GBM = WR * GW;
+  static_assert(!UNI || GBM == RPC_UNION_ROWS, "union blocks");
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;
   // LDS row stride: 8 mod 16 dwords (conflict-free b128 reads), except the 128 x 128 tiles, whose
@@ -195,20 +199,25 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
   constexpr int LS = (KGP >= 128 && NT >= 8) ? KGP + 8 : KGP + 16;
   constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
   constexpr int BPT = (BV + GBLK - 1) / GBLK;
+  // union rows in LDS: UC rows of KGP elements (pitch LA) + one zero row for entries without a neighbour
+  constexpr int UC = UNI ? ucap_of(KGP) : 0, LA = KGP + 8, CH = KGP / 8;
   __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];
+  __shared__ __attribute__((aligned(16))) u16 sA[UNI ? (UC + 1) * LA : 8];
   __shared__ int sN[GBM * MAXK];
   __shared__ unsigned wmask[GW];
   __shared__ int klist[MAXK];
   __shared__ int nk;
   __shared__ float sP[GW][2 * NGP];
-  __shared__ int sRow[GBM];   // physical row of each logical row (the visiting order; -1 past Nout)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // XCD-aware row blocks: each XCD takes one contiguous eighth of the (spatially sorted) rows, so the
   // neighbour rows its blocks gather — mostly within a few thousand rows — stay in that XCD's L2
-  // (round-robin placement made every XCD gather from the whole source table: L2 misses)
-  const int lb = dn::xcd_remap(blockIdx.x, gridDim.x);
+  // (round-robin placement made every XCD gather from the whole source table: L2 misses). The union path
+  // keeps the natural order: block b of the grid is union block b.
+  const int lb = UNI ? (int)blockIdx.x : dn::xcd_remap(blockIdx.x, gridDim.x);
   const int r0 = lb * GBM;
   const int K = g.K;
+  const int ucnt = UNI ? g.ucnt[lb] : 0;
+  const bool uni = UNI && ucnt <= UC;          // block-uniform
   {
     // each wave stages its own 16 rows: lane = (offset group k4, row lane&15), 4 offsets per pass;
     // the wave's offset mask comes from ballots (no LDS atomics)
@@ -219,14 +228,22 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     constexpr int NP = (MAXK + 3) / 4;
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt) {
-      const int lr = w * WR + rt * 16 + rr, lrow = r0 + lr;
-      const int row = lrow < g.Nout ? (g.perm ? g.perm[lrow] : lrow) : g.Nout;
-      if (k4 == 0) sRow[lr] = row < g.Nout ? row : -1;
+      const int lr = w * WR + rt * 16 + rr, row = r0 + lr;
       int nv[NP];
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
         const int k = 4 * i + k4;
-        nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
+        const long long e = (long long)row * K + (g.rev ? K - 1 - k : k);
+        if (k < K && row < g.Nout) {
+          if (uni) {
+            const unsigned short sl = g.lnbr[e];
+            nv[i] = sl == 0xFFFF ? -1 : (int)sl;
+          } else {
+            nv[i] = g.nbr[e];
+          }
+        } else {
+          nv[i] = -1;
+        }
       }
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
@@ -240,6 +257,30 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
       }
     }
     if (lane == 0) wmask[w] = m;
+  }
+  constexpr unsigned OOB = 0x80000000u;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.bt, (short)0, 0x7fffffff, 0x00020000);
+  if (UNI && uni) {
+    // the block's source rows -> LDS, 8 chunks of 16 B in flight per thread; channels past CP (and the zero
+    // row) read as zeros through out-of-range offsets
+    const int nq = (ucnt + 1) * CH;
+    for (int q0 = 0; q0 < nq; q0 += 8 * GBLK) {
+      uint4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = q0 + tid + j * GBLK, sl = q / CH, c0 = (q - sl * CH) * 8;
+        const int src = (q < nq && sl < ucnt) ? g.ulist[(long long)lb * RPC_UNION_CAP + sl] : -1;
+        unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
+        asm volatile("" : "+v"(off));
+        v[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int q = q0 + tid + j * GBLK, sl = q / CH, c0 = (q - sl * CH) * 8;
+        if (q < nq) *(uint4*)&sA[(sl < ucnt ? sl : UC) * LA + c0] = v[j];
+      }
+    }
   }
   __syncthreads();
   if (tid == 0) {
@@ -261,37 +302,12 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
 
   const int arow = w * WR + (lane & 15);
   const int ag = lane >> 4;
-  // Every load of the main loop is issued unconditionally as a buffer load: a missing neighbour, a
-  // padding column or an idle thread gets an offset past the descriptor's range, which the hardware
-  // returns as zeros. With conditional loads the compiler could not count the loads in flight: the
-  // weight-tile LDS store waited on vmcnt(0), i.e. for the next offset's gathers too, every offset.
-  // Offsets are 32-bit: the host checks that the source table and the weight tiles fit below 2 GB.
-  constexpr unsigned OOB = 0x80000000u;
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.bt, (short)0, 0x7fffffff, 0x00020000);
-  auto load_a = [&](int k, uint4 (&dst)[RT][KS]) {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int src = sN[(arow + rt * 16) * MAXK + k];
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int c0 = ks * 32 + ag * 8;
-        if (DBG & 8) {
-          dst[rt][ks] = make_uint4(0u, 0u, 0u, 0u);
-          continue;
-        }
-        unsigned off = (src >= 0 && c0 < g.CP && !(DBG & 2)) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
-        asm volatile("" : "+v"(off));   // keeps the select a select (else: one load per branch of a diamond)
-        dst[rt][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
-      }
-    }
-  };
   auto load_b = [&](int k, uint4 (&dst)[BPT]) {
     const unsigned base = (unsigned)k * (unsigned)(NGP * KGP * 2);
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
       const int v = tid + j * GBLK;
-      unsigned off = ((BV % GBLK == 0 || v < BV) && !(DBG & 4)) ? base + (unsigned)v * 16u : OOB;
+      unsigned off = (BV % GBLK == 0 || v < BV) ? base + (unsigned)v * 16u : OOB;
       asm volatile("" : "+v"(off));
       dst[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, off, 0, 0));
     }
@@ -306,8 +322,31 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
       }
     }
   };
-
-  if (NK > 0) {
+  // The offset loop, for A fragments from global memory (LU false) or from the LDS union rows (LU true).
+  auto mainloop = [&](auto lu_tag) {
+    constexpr bool LU = decltype(lu_tag)::value;
+    // Every global load of the loop is issued unconditionally as a buffer load: a missing neighbour, a
+    // padding column or an idle thread gets an offset past the descriptor's range, which the hardware
+    // returns as zeros. With conditional loads the compiler could not count the loads in flight: the
+    // weight-tile LDS store waited on vmcnt(0), i.e. for the next offset's gathers too, every offset.
+    // Offsets are 32-bit: the host checks that the source table and the weight tiles fit below 2 GB.
+    auto load_a = [&](int k, uint4 (&dst)[RT][KS]) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int src = sN[(arow + rt * 16) * MAXK + k];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int c0 = ks * 32 + ag * 8;
+          if constexpr (LU) {
+            dst[rt][ks] = *(const uint4*)&sA[(src >= 0 ? src : UC) * LA + c0];
+          } else {
+            unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
+            asm volatile("" : "+v"(off));   // keeps the select a select (else: one load per branch of a diamond)
+            dst[rt][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
+          }
+        }
+      }
+    };
     uint4 a0[RT][KS], a1[RT][KS], bw0[BPT], bw1[BPT];
     load_b(klist[0], bw0);
     store_b(0, bw0);
@@ -324,7 +363,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
       const int k = klist[t];
       load_b(klist[t + 2 < NK ? t + 2 : NK - 1], bn);
       load_a(klist[t + 1 < NK ? t + 1 : t], an);
-      if (((my >> k) & 1u) && !(DBG & 1)) {
+      if ((my >> k) & 1u) {
         const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
@@ -348,6 +387,60 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
       step(t + 1, a1, a0, bw1, bw0);
     }
     if (t < NK) step(t, a0, a1, bw0, bw1);
+  };
+  // The union loop: A fragments are LDS reads, so a step is only its MFMAs + LDS reads (~0.2 us at 64 x 64), far
+  // shorter than an L2 round trip for the weight tile — the tiles are fetched D-1 offsets ahead into a ring of D
+  // register sets (compile-time set indices: the loop runs D steps per iteration, padded with steps that only
+  // fetch and store, so every step issues the same loads and the compiler's waits stay exact). With the regular
+  // loop's one offset of look-ahead the union path ran at ~1.8 us per step (k_gemm_bf16<64,4,1> 117 vs 60 us).
+  auto unionloop = [&]() {
+    constexpr int D = BPT <= 2 ? 6 : (BPT <= 4 ? 4 : 2);
+    uint4 bw[D][BPT], aa[2][RT][KS];
+    auto kl = [&](int t) { return klist[t < NK ? t : NK - 1]; };
+    auto lda = [&](int k, uint4 (&dst)[RT][KS]) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt) {
+        const int src = sN[(arow + rt * 16) * MAXK + k];
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) dst[rt][ks] = *(const uint4*)&sA[(src >= 0 ? src : UC) * LA + ks * 32 + ag * 8];
+      }
+    };
+#pragma unroll
+    for (int j = 0; j < D - 1; ++j) load_b(kl(j), bw[j]);
+    store_b(0, bw[0]);
+    lda(kl(0), aa[0]);
+    __syncthreads();
+    const int NKP = (NK + D - 1) / D * D;
+    for (int t = 0; t < NKP; t += D) {
+#define USTEP(J)                                                                                  \
+  if constexpr (J < D) {                                                                         \
+    const int tt = t + (J);                                                                      \
+    load_b(kl(tt + D - 1), bw[((J) + D - 1) % D]);                                               \
+    if (tt + 1 < NK) lda(kl(tt + 1), aa[((J) + 1) & 1]);                                         \
+    if (tt < NK && ((my >> kl(tt)) & 1u)) {                                                      \
+      const u16* bb = sB[tt & 1] + (lane & 15) * LS + ag * 8;                                    \
+      _Pragma("unroll") for (int ks = 0; ks < KS; ++ks) {                                        \
+        _Pragma("unroll") for (int n = 0; n < NT; ++n) {                                         \
+          const uint4 bv = *(const uint4*)(bb + n * 16 * LS + ks * 32);                          \
+          _Pragma("unroll") for (int rt = 0; rt < RT; ++rt)                                      \
+            acc[rt][n] = mfma16<F16>(aa[(J) & 1][rt][ks], bv, acc[rt][n]);                       \
+        }                                                                                        \
+      }                                                                                          \
+    }                                                                                            \
+    store_b((tt + 1) & 1, bw[((J) + 1) % D]);                                                    \
+    __syncthreads();                                                                             \
+  }
+      USTEP(0) USTEP(1) USTEP(2) USTEP(3) USTEP(4) USTEP(5)
+#undef USTEP
+    }
+  };
+  if (NK > 0) {
+    if constexpr (UNI) {
+      if (uni) unionloop();
+      else mainloop(std::false_type{});
+    } else {
+      mainloop(std::false_type{});
+    }
   }
 
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg (16x16 shapes, gfx950)
@@ -357,12 +450,14 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
   float s1[NT], s2[NT];
 #pragma unroll
   for (int n = 0; n < NT; ++n) s1[n] = s2[n] = 0.0f;
-  // (rows in visiting order: lane rows lr .. lr + 3 of the block, physical rows from sRow)
   int prow[RT][4];
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) prow[rt][j] = sRow[w * WR + rt * 16 + (lane >> 4) * 4 + j];
+    for (int j = 0; j < 4; ++j) {
+      const int r = r0 + w * WR + rt * 16 + (lane >> 4) * 4 + j;
+      prow[rt][j] = r < g.Nout ? r : -1;
+    }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
@@ -394,7 +489,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
             const float gg = v + g2r[j];
             v = orr[j] > 0.0f ? gg : 0.0f;
             s1[n] += v;
-            s2[n] += v * ((zr[j] - pb[2]) * pb[3]);
+            s2[n] = fmaf(v, (zr[j] - pb[2]) * pb[3], s2[n]);   // explicit (see E_DGRAD)
           } else if (EPI == E_DGRAD) {
             const float zz = zr[j];
             float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
@@ -444,276 +539,6 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     // the neighbour table is free: the totals (double [2C], C <= 256 -> 4 KB) and the arrival flag go there
     static_assert(GBM * MAXK * 4 >= 4096 + 4, "LDS for the fused finalize");
     fused_bn_finalize<GBLK>(g, lb, PRB, (double*)sN, sN + 1024);
-  }
-}
-
-// ------------------------------------------------------------------ r04: deep LDS-DMA ring
-// k_gemm_bf16 waits out one memory round trip per kernel offset: the A fragments of offset t+1 are the
-// only loads in flight while offset t computes, and one offset of MFMAs (8 per wave at 64 x 64) is far
-// shorter than a gather under load (~1.7 us per offset step at the 106k-row layers: 23 steps, 39 us).
-// k_gemm_pipe issues S-1 offsets ahead instead, straight into LDS (`buffer_load ... lds`, no VGPR round
-// trip): per offset and wave the wave's own 16 gathered rows (16 x KGP bf16, NA instructions) and its
-// share of the weight tile (NGP x KGP bf16, WI instructions per block), into ring slot t % S. Per step:
-// wait for this wave's loads of stage t (vmcnt of the stages issued after it), one barrier (every wave's
-// stage-t loads have landed and every wave is done with stage t-1, whose slot the next issue reuses),
-// issue stage t+S-1, then the MFMAs of stage t from LDS. LDS rows are KGP bf16 (G = KGP/8 granules of
-// 16 B) with granule j of row r stored at j ^ pswz(r): every ds_read_b128 lane group of an A or B
-// fragment read then hits 16 distinct bank slots (exhaustive check, tools/swz_check.py). Gathers of
-// absent neighbours (and the padding granules of a 16-channel row) get an offset past the buffer range:
-// the DMA writes zeros and touches no memory. Same MFMAs in the same order per accumulator as
-// k_gemm_bf16 (offsets ascending, K-steps, output tiles), so the same bits; same epilogue.
-__host__ __device__ constexpr int pswz(int G, int row) { return G == 16 ? (row & 15) : ((row >> 1) & (G - 1)); }
-
-template <int NPS, int R>
-__device__ __forceinline__ void vm_wait(int rem) {
-  if constexpr (R > 0) {
-    if (rem >= R) {
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R * NPS) : "memory");
-      return;
-    }
-    vm_wait<NPS, R - 1>(rem);
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
-
-template <int KGP, int NT, int GW, int S>
-struct PipeCfg {
-  // RT: 16-row MFMA tiles per wave, as k_gemm_bf16 (rt_of): the same rows per wave and per partial row,
-  // so the BatchNorm partial sums are added in the same order (same bits) — except 128 x 128, whose two-tile
-  // waves would not fit the ring's LDS (one tile here)
-  static constexpr int RT = (KGP == 128 && NT == 8) ? 1 : rt_of(KGP, NT);
-  static constexpr int G = KGP / 8, KS = KGP / 32, NGP = NT * 16, WR = 16 * RT, GBM = WR * GW, GBLK = 64 * GW;
-  static constexpr int ABYTES = WR * KGP * 2;            // one wave's gathered rows
-  static constexpr int NA = WR * G / 64;                 // their DMA instructions (1 KB each)
-  static constexpr int WBYTES = NGP * KGP * 2;           // one offset's weight tile
-  static constexpr int WI = WBYTES / 1024;               // its DMA instructions (per block)
-  static constexpr int NWH = (WI + GW - 1) / GW, NWL = WI / GW, WREM = WI % GW;
-  static constexpr int STAGE = GW * ABYTES + WBYTES;
-  static constexpr int SN = GBM * MAXK * 4;
-  static constexpr int MISC = 256;                       // wmask[GW], klist[MAXK], nk
-  static constexpr int LDS = S * STAGE + SN + MISC;
-  static_assert(KGP % 32 == 0 && WBYTES % 1024 == 0 && ABYTES % 1024 == 0, "DMA tiles are whole KBs");
-  static_assert(GW * 2 * NGP * 4 <= S * STAGE && GW <= 8, "epilogue partials alias the ring");
-  static_assert(LDS <= 160 * 1024, "LDS");
-};
-
-template <int KGP, int NT, int EPI, int GW, int S>
-__global__ __launch_bounds__(64 * GW, 1) void k_gemm_pipe(GB g) {
-  using P = PipeCfg<KGP, NT, GW, S>;
-  constexpr int G = P::G, KS = P::KS, NGP = P::NGP, GBM = P::GBM, GBLK = P::GBLK, NA = P::NA, RT = P::RT;
-  constexpr int WR = P::WR;
-  // ONE LDS object: separate __shared__ arrays get alias scopes, and the compiler then drains every
-  // DMA in flight (vmcnt(0)) before the operand reads of each step (dense_conv.hip k_conv3x3x)
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[P::LDS];
-  int* const sN = (int*)(lds + S * P::STAGE);
-  unsigned* const wmask = (unsigned*)(lds + S * P::STAGE + P::SN);
-  int* const klist = (int*)(wmask + 8);
-  int* const nkp = klist + 32;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int lb = dn::xcd_remap(blockIdx.x, gridDim.x);
-  const int r0 = lb * GBM;
-  const int K = g.K;
-  {
-    // neighbour indices of the wave's rows into LDS, the wave's offset mask by ballots (k_gemm_bf16)
-    const int rr = lane & 15, k4 = lane >> 4;
-    unsigned m = 0;
-    constexpr int NP = (MAXK + 3) / 4;
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      const int lr = w * WR + rt * 16 + rr, row = r0 + lr;
-      int nv[NP];
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int k = 4 * i + k4;
-        nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
-      }
-#pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int kb = 4 * i, k = kb + k4, v = nv[i];
-        if (kb >= K) break;
-        if (k < K) sN[lr * MAXK + k] = v;
-        const unsigned long long b = __ballot(v >= 0);
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-          if ((b >> (16 * q)) & 0xffffull) m |= 1u << (kb + q);
-      }
-    }
-    if (lane == 0) wmask[w] = m;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    unsigned m = 0;
-    for (int q = 0; q < GW; ++q) m |= wmask[q];
-    int n = 0;
-    for (int k = 0; k < K; ++k)
-      if ((m >> k) & 1u) klist[n++] = k;
-    *nkp = n;
-  }
-  __syncthreads();
-  const int NK = *nkp;
-  const unsigned my = wmask[w];
-
-  // ---- fixed per-lane DMA geometry. A instruction i writes LDS granule P = i*64 + lane of this wave's
-  // slot: local row P / G, stored granule P % G, which holds source granule (P % G) ^ pswz(row)
-  constexpr unsigned OOB = 0x80000000u;
-  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.bt, (short)0, 0x7fffffff, 0x00020000);
-  int ar[NA], ac[NA];
-#pragma unroll
-  for (int i = 0; i < NA; ++i) {
-    const int Pg = i * 64 + lane, r = Pg / G, j = (Pg % G) ^ pswz(G, r);
-    ar[i] = (w * WR + r) * MAXK;
-    ac[i] = j * 8 < g.CP ? j * 8 : -1;
-  }
-  constexpr int NWH = P::NWH;
-  int wo[NWH > 0 ? NWH : 1];
-#pragma unroll
-  for (int m = 0; m < NWH; ++m) {
-    const int q = w + m * GW, Pg = q * 64 + lane, n = Pg / G, j = (Pg % G) ^ pswz(G, n);
-    wo[m] = q < P::WI ? (n * KGP + j * 8) * 2 : (int)OOB;
-  }
-  // (the DMA builtin's offsets as explicit int casts: passed as plain lvalues — or unsigned — hipcc dropped
-  // the kernel from the host pass without a diagnostic: no launch stub, an undefined symbol at load time)
-  auto issue = [&](int t) {
-    unsigned char* st = lds + (t % S) * P::STAGE;
-    const int k = __builtin_amdgcn_readfirstlane(klist[t]);   // the weight offset goes in an SGPR (soffset)
-#pragma unroll
-    for (int i = 0; i < NA; ++i) {
-      const int src = sN[ar[i] + k];
-      const int off = (src >= 0 && ac[i] >= 0) ? (int)(((unsigned)src * (unsigned)g.CP + (unsigned)ac[i]) * 2u)
-                                               : (int)OOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (__attribute__((address_space(3))) void*)(st + w * P::ABYTES + i * 1024),
-                                               16, (int)off, 0, 0, 0);
-    }
-    const int kb = k * P::WBYTES;
-#pragma unroll
-    for (int m = 0; m < NWH; ++m) {
-      const int q = w + m * GW;
-      if (m < P::NWL || w < P::WREM)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rsb, (__attribute__((address_space(3))) void*)(st + GW * P::ABYTES + q * 1024), 16, (int)wo[m], (int)kb, 0, 0);
-    }
-  };
-
-  f32x4 acc[RT][NT];
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-    for (int n = 0; n < NT; ++n) acc[rt][n] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  // operand byte offsets inside a slot: A rows rt*16 + lane&15 of this wave, B rows n*16 + lane&15;
-  // granule ks*4 + (lane >> 4), swizzled by the row (pswz(n*16 + r) = pswz(r))
-  const int a15 = lane & 15, q4 = lane >> 4;
-  int aoff[RT][KS], boff[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt)
-      aoff[rt][ks] = w * P::ABYTES + ((rt * 16 + a15) * G + ((ks * 4 + q4) ^ pswz(G, a15))) * 16;
-    boff[ks] = GW * P::ABYTES + (a15 * G + ((ks * 4 + q4) ^ pswz(G, a15))) * 16;
-  }
-
-#pragma unroll
-  for (int t = 0; t < S - 1; ++t)
-    if (t < NK) issue(t);
-  constexpr int NPS_H = NA + P::NWH, NPS_L = NA + P::NWL;
-  for (int t = 0; t < NK; ++t) {
-    const int rem = min(S - 2, NK - 1 - t);   // stages issued after stage t
-    if (P::WREM == 0 || w < P::WREM) vm_wait<NPS_H, S - 2>(rem);
-    else vm_wait<NPS_L, S - 2>(rem);
-    // a bare barrier: __syncthreads() is a workgroup fence and waits for every DMA in flight (vmcnt(0))
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    if (t + S - 1 < NK) issue(t + S - 1);
-    const int k = __builtin_amdgcn_readfirstlane(klist[t]);
-    if ((my >> k) & 1u) {
-      const unsigned char* st = lds + (t % S) * P::STAGE;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        bf16x8 av[RT];
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt) av[rt] = *(const bf16x8*)(st + aoff[rt][ks]);
-#pragma unroll
-        for (int n = 0; n < NT; ++n) {
-          const bf16x8 bv = *(const bf16x8*)(st + boff[ks] + n * 16 * G * 16);
-#pragma unroll
-          for (int rt = 0; rt < RT; ++rt)
-            acc[rt][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[rt], bv, acc[rt][n], 0, 0, 0);
-        }
-      }
-    }
-  }
-
-  // epilogue: k_gemm_bf16's, line for line
-  float s1[NT], s2[NT];
-#pragma unroll
-  for (int n = 0; n < NT; ++n) s1[n] = s2[n] = 0.0f;
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    const int rb = r0 + w * WR + rt * 16 + (lane >> 4) * 4;
-#pragma unroll
-    for (int n = 0; n < NT; ++n) {
-      int col = n * 16 + (lane & 15);
-      float zr[4], pb[4];
-      if (EPI == E_DGRAD) {
-        const int C = g.CO_real, cc = min(col, C - 1);
-#pragma unroll
-        for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)min(rb + j, g.Nout - 1) * C + cc];
-      }
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        int row = rb + j;
-        float v = acc[rt][n][j];
-        if (row < g.Nout && col < g.CO_real) {
-          if (EPI == E_DGRAD) {
-            const float zz = zr[j];
-            float h = fmaxf(fmaf(zz - pb[2], pb[0], pb[1]), 0.0f);
-            v = h > 0.0f ? v : 0.0f;
-            float xh = (zz - pb[2]) * pb[3];
-            s1[n] += v;
-            s2[n] = fmaf(v, xh, s2[n]);   // explicit: contraction left to -ffp-contract differed between kernels
-          } else {
-            s1[n] += v;
-            s2[n] = fmaf(v, v, s2[n]);
-          }
-          g.out[(long long)row * g.CO_real + col] = v;
-        }
-      }
-    }
-  }
-  if (EPI == E_PLAIN || g.part == nullptr) return;
-  float* const sP = (float*)lds;   // aliases the ring: every wave is past its last step's reads
-  __syncthreads();
-#pragma unroll
-  for (int n = 0; n < NT; ++n) {
-    s1[n] += __shfl_xor(s1[n], 16, 64);
-    s1[n] += __shfl_xor(s1[n], 32, 64);
-    s2[n] += __shfl_xor(s2[n], 16, 64);
-    s2[n] += __shfl_xor(s2[n], 32, 64);
-    if (lane < 16) {
-      sP[w * 2 * NGP + n * 16 + lane] = s1[n];
-      sP[w * 2 * NGP + NGP + n * 16 + lane] = s2[n];
-    }
-  }
-  __syncthreads();
-  const int C = g.CO_real;
-  constexpr int WPR = 64 / WR, PRB = GBM / 64;
-  const int nrow = (g.Nout + BM - 1) / BM;
-  for (int j = tid; j < PRB * 2 * C; j += GBLK) {
-    const int h = j / (2 * C), jj = j - h * 2 * C, prow = lb * PRB + h;
-    if (prow >= nrow) continue;
-    int which = jj / C, c = jj - which * C;
-    float s = 0.0f;
-    for (int ww = 0; ww < WPR; ++ww) s += sP[(WPR * h + ww) * 2 * NGP + which * NGP + c];
-    if (g.fin.ticket)
-      st_agent(&g.part[(long long)prow * 2 * C + jj], s);
-    else
-      g.part[(long long)prow * 2 * C + jj] = s;
-  }
-  if (g.fin.ticket) {
-    // the ring is free: the totals (double [2C], C <= 256 -> 4 KB) and the arrival flag go there
-    fused_bn_finalize<GBLK>(g, lb, PRB, (double*)(lds + 1024), (int*)(lds + 8192));
   }
 }
 
@@ -1066,352 +891,28 @@ __global__ __launch_bounds__(wg_threads(CI, CO), (CI * CO <= 32 * 32) ? 4 : 1) v
   }
 }
 
-// ------------------------------------------------------------------ r04: weight gradient over pair lists
-// k_wgrad_bf16 walks every (row chunk, offset group) over ALL rows of the chunk: a row with no neighbour at
-// offset k still costs its dz / h loads, staging and MFMA rows (sub-tiles are skipped only when none of
-// their 64 rows has one). Here the neighbour map is first compacted into per-offset pair lists
-// (k_pair_count -> one hipcub exclusive scan over the offset-major count table -> k_pair_scatter: pairs of
-// offset k in ascending output-row order, deterministic), and the weight gradient runs over the pairs
-// only: block b of S + K takes a slice of ONE offset's pairs, the offsets getting ceil(count_k * S / P)
-// blocks each (balanced: ~P / S pairs per block whatever the offsets' counts), with dz rows gathered by the
-// pair's output row and h rows by its input row, the same LDS staging / transposed reads / MFMA tiling as
-// k_wgrad_bf16<., ., 1>. One fp32 partial per block (S + K partials instead of chunks x K), reduced per
-// offset over its blocks in block order (k_pair_reduce).
-constexpr int PRB = 256;   // rows per count / scatter block
-
-// the block's PRB x K slice of nbr, staged into LDS with coalesced loads (each thread reading its own row's K
-// entries straight from global memory strided the wave's 64 accesses over 64 rows: 103 us per 360k-row map)
-__device__ __forceinline__ void stage_nbr(const int* __restrict__ nbr, int n, int K, int* snb) {
-  const long long r0 = (long long)blockIdx.x * PRB;
-  const int tot = (int)(min((long long)PRB, (long long)n - r0) * K);
-  const int* src = nbr + r0 * K;
-  int v[MAXK];   // all of the thread's loads in flight before the first LDS store
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i) {
-    const int q = threadIdx.x + i * PRB;
-    v[i] = (i < K && q < tot) ? src[q] : -1;
-  }
-#pragma unroll
-  for (int i = 0; i < MAXK; ++i)
-    if (i < K) snb[threadIdx.x + i * PRB] = v[i];
-}
-
-__global__ __launch_bounds__(PRB) void k_pair_count(const int* __restrict__ nbr, int n, int K, int nb,
-                                                    int* __restrict__ cnt) {
-  __shared__ int snb[PRB * MAXK];
-  __shared__ int sc[PRB / 64][MAXK];
-  stage_nbr(nbr, n, K, snb);
-  __syncthreads();
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  for (int k = 0; k < K; ++k) {
-    const unsigned long long m = __ballot(snb[threadIdx.x * K + k] >= 0);
-    if (lane == 0) sc[w][k] = __popcll(m);
-  }
-  __syncthreads();
-  if (threadIdx.x < K) {
-    int c = 0;
-    for (int ww = 0; ww < PRB / 64; ++ww) c += sc[ww][threadIdx.x];
-    cnt[(long long)threadIdx.x * nb + blockIdx.x] = c;   // offset-major: the scan runs k by k
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) cnt[(long long)K * nb] = 0;   // the scan's total lands past it
-}
-
-__global__ __launch_bounds__(PRB) void k_pair_scatter(const int* __restrict__ nbr, int n, int K, int nb,
-                                                      const int* __restrict__ base, int2* __restrict__ pairs) {
-  __shared__ int snb[PRB * MAXK];
-  __shared__ int sw[PRB / 64][MAXK];
-  stage_nbr(nbr, n, K, snb);
-  __syncthreads();
-  const int r = blockIdx.x * PRB + threadIdx.x, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const unsigned long long below = (1ull << lane) - 1ull;
-  for (int k = 0; k < K; ++k) {
-    const unsigned long long m = __ballot(snb[threadIdx.x * K + k] >= 0);
-    if (lane == 0) sw[w][k] = __popcll(m);
-  }
-  __syncthreads();
-  for (int k = 0; k < K; ++k) {
-    const int src = snb[threadIdx.x * K + k];
-    const unsigned long long m = __ballot(src >= 0);
-    if (src < 0) continue;
-    int pos = base[(long long)k * nb + blockIdx.x];
-    for (int ww = 0; ww < w; ++ww) pos += sw[ww][k];
-    pos += __popcll(m & below);
-    pairs[pos] = make_int2(r, src);
-  }
-}
-
-// the block -> (offset, slice) assignment every block and the reduce recompute from the K + 1 offsets
-__device__ __forceinline__ void pair_blocks(const int* koff, int K, int S, int* kb) {
-  const long long P = koff[K];
-  kb[0] = 0;
-  for (int k = 0; k < K; ++k) {
-    const long long c = koff[k + 1] - koff[k];
-    kb[k + 1] = kb[k] + (c > 0 ? (int)((c * S + P - 1) / P) : 0);
-  }
-}
-
-template <int CI, int CO, bool HF16 = false>
-__global__ __launch_bounds__(BLK, (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_pairs(
-    const u16* __restrict__ h, int HP, const int2* __restrict__ pairs, const int* __restrict__ base, int nb, int K,
-    int S, const u16* __restrict__ dz, int DP, float* __restrict__ part) {
-  constexpr int RT = 64, SEG = 512;
-  constexpr int CIR = (CI + 15) / 16 * 16;
-  constexpr int PA = CIR + 16, PD = CO + 16;
-  constexpr int MT = CIR / 16, NT = CO / 16;
-  constexpr int WM = MT < 4 ? MT : 4, WN = 4 / WM;
-  constexpr int WMT = MT / WM, WNT = (NT + WN - 1) / WN, TPW = WMT * WNT;
-  constexpr int CA = (CI + 7) / 8, CD = CO / 8;
-  constexpr int NA = (RT * CA + BLK - 1) / BLK, ND = (RT * CD + BLK - 1) / BLK;
-  __shared__ __attribute__((aligned(16))) u16 sA[RT * PA];
-  __shared__ __attribute__((aligned(16))) u16 sD[RT * PD];
-  __shared__ int2 sP[SEG];
-  __shared__ int skoff[MAXK + 1], skb[MAXK + 1];
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int wm = w % WM, wn = w / WM;
-  if (tid <= K) skoff[tid] = base[(long long)tid * nb];
-  __syncthreads();
-  if (tid == 0) pair_blocks(skoff, K, S, skb);
-  __syncthreads();
-  const int b = blockIdx.x;
-  if (b >= skb[K]) return;   // uniform: a spare block of the S + K grid
-  int k = 0;
-  while (skb[k + 1] <= b) ++k;
-  const long long cnt = skoff[k + 1] - skoff[k];
-  const int nbk = skb[k + 1] - skb[k], i = b - skb[k];
-  const int p0 = skoff[k] + (int)(cnt * i / nbk), p1 = skoff[k] + (int)(cnt * (i + 1) / nbk);
-  f32x4 acc[TPW];
-#pragma unroll
-  for (int t = 0; t < TPW; ++t) acc[t] = (f32x4){0.f, 0.f, 0.f, 0.f};
-  if (CIR != CI)
-    for (int q = tid; q < RT * PA; q += BLK) sA[q] = 0;
-  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
-  const int rowoff = 4 * g4 + qq;
-  // register prefetch PF sub-tiles ahead: one. Two measured slower (64 x 64: 50.9 -> 57.6 us in the step,
-  // CenterPoint 358 -> 409 us, profiles/r04_wgrad_pairs_ab.txt); kept as a compile-time choice
-  constexpr int PF = 1;
-  uint4 ra0[NA], rd0[ND], ra1[NA], rd1[ND];
-  for (int seg = p0; seg < p1; seg += SEG) {
-    const int se = min(p1, seg + SEG), len = se - seg;
-    __syncthreads();
-    for (int q = tid; q < SEG; q += BLK) sP[q] = q < len ? pairs[seg + q] : make_int2(-1, -1);
-    __syncthreads();
-    auto load = [&](int rs, uint4 (&ra)[NA], uint4 (&rd)[ND]) {
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        const int q = tid + j * BLK;
-        rd[j] = make_uint4(0u, 0u, 0u, 0u);
-        if (q < RT * CD) {
-          const int r = q / CD, c8 = q - r * CD;
-          const int row = rs + r < SEG ? sP[rs + r].x : -1;
-          if (row >= 0) rd[j] = *(const uint4*)(dz + (long long)row * DP + c8 * 8);
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const int q = tid + j * BLK;
-        ra[j] = make_uint4(0u, 0u, 0u, 0u);
-        if (q < RT * CA) {
-          const int r = q / CA, c8 = q - r * CA;
-          const int src = rs + r < SEG ? sP[rs + r].y : -1;
-          if (src >= 0) ra[j] = *(const uint4*)(h + (long long)src * HP + c8 * 8);
-        }
-      }
-    };
-    auto stage = [&](const uint4 (&ra)[NA], const uint4 (&rd)[ND]) {
-      __syncthreads();   // the previous sub-tile's MFMAs are done with the LDS tiles
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        const int q = tid + j * BLK;
-        if (q < RT * CD) {
-          const int r = q / CD, c8 = q - r * CD;
-          *(uint4*)&sD[r * PD + c8 * 8] = rd[j];
-        }
-      }
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        const int q = tid + j * BLK;
-        if (q < RT * CA) {
-          const int r = q / CA, c8 = q - r * CA;
-          *(uint4*)&sA[r * PA + c8 * 8] = HF16 ? f16x8_to_bf16x8(ra[j]) : ra[j];
-        }
-      }
-      __syncthreads();
-    };
-    auto mma = [&]() {
-#pragma unroll
-      for (int ks = 0; ks < RT / 32; ++ks) {
-        const int r0 = 32 * ks + rowoff;
-        bf16x8 bv[WNT];
-#pragma unroll
-        for (int bb = 0; bb < WNT; ++bb) {
-          const int n = wn + WN * bb;
-          s16x4 x[2] = {tr_read(&sD[r0 * PD + n * 16 + 4 * pp]), tr_read(&sD[(r0 + 16) * PD + n * 16 + 4 * pp])};
-          bv[bb] = *(bf16x8*)x;
-        }
-#pragma unroll
-        for (int a = 0; a < WMT; ++a) {
-          const int m = wm + WM * a;
-          s16x4 x[2] = {tr_read(&sA[r0 * PA + m * 16 + 4 * pp]), tr_read(&sA[(r0 + 16) * PA + m * 16 + 4 * pp])};
-          const bf16x8 av = *(bf16x8*)x;
-#pragma unroll
-          for (int bb = 0; bb < WNT; ++bb)
-            acc[a * WNT + bb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[bb], acc[a * WNT + bb], 0, 0, 0);
-        }
-      }
-    };
-    load(0, ra0, rd0);
-    if (PF == 2 && RT < len) load(RT, ra1, rd1);
-    for (int rs = 0; rs < len; rs += RT * PF) {
-      stage(ra0, rd0);
-      if (rs + PF * RT < len) load(rs + PF * RT, ra0, rd0);   // in flight during the MFMAs below
-      mma();
-      if constexpr (PF == 2) {
-        if (rs + RT >= len) break;
-        stage(ra1, rd1);
-        if (rs + 3 * RT < len) load(rs + 3 * RT, ra1, rd1);
-        mma();
-      }
-    }
-  }
-  float* out = part + (long long)b * CI * CO;
-#pragma unroll
-  for (int a = 0; a < WMT; ++a)
-#pragma unroll
-    for (int bb = 0; bb < WNT; ++bb) {
-      const int m = wm + WM * a, n = wn + WN * bb;
-      if (n >= NT) continue;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int ci = m * 16 + (lane >> 4) * 4 + j, co = n * 16 + (lane & 15);
-        if (ci < CI) out[ci * CO + co] = acc[a * WNT + bb][j];
-      }
-    }
-}
-
-// dW[k][e] = sum of the partials of offset k's blocks, in block order (8 interleaved sums, fixed combine)
-__global__ __launch_bounds__(BLK) void k_pair_reduce(const float* __restrict__ part, const int* __restrict__ base,
-                                                     int nb, int K, int S, long long per, float* __restrict__ dW) {
-  __shared__ int skoff[MAXK + 1], skb[MAXK + 1];
-  if (threadIdx.x <= K) skoff[threadIdx.x] = base[(long long)threadIdx.x * nb];
-  __syncthreads();
-  if (threadIdx.x == 0) pair_blocks(skoff, K, S, skb);
-  __syncthreads();
-  const long long e = (long long)blockIdx.x * BLK + threadIdx.x;
-  if (e >= per * K) return;
-  const int k = (int)(e / per);
-  const long long j = e - (long long)k * per;
-  const int b0 = skb[k], b1 = skb[k + 1];
-  float s[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  int bb = b0;
-  for (; bb + 8 <= b1; bb += 8) {   // 8 loads in flight
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = part[(long long)(bb + u) * per + j];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s[u] += v[u];
-  }
-  for (int u = 0; bb < b1; ++bb, ++u) s[u] += part[(long long)bb * per + j];
-  dW[e] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
-}
-
-template <int CI, int CO>
-static int pairs_slots() {   // resident k_wgrad_pairs blocks on the device
-  static int r = 0;
-  if (r == 0) {
-    int per = 0, dev = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, k_wgrad_pairs<CI, CO>, BLK, 0) != hipSuccess || per <= 0)
-      per = 1;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
-      cus = 256;
-    r = per * cus;
-  }
-  return r;
-}
-
-template <int KGP, int NT>
-static void launch_t(int epi, const GB& a, int n_rows, hipStream_t st) {
-  constexpr int GW = gw_of(KGP, NT), GBM = 16 * rt_of(KGP, NT) * GW;
+template <int KGP, int NT, bool UNI>
+static void launch_k(int epi, const GB& a, int n_rows, hipStream_t st) {
+  constexpr int RT = rt_of(KGP, NT), GW = UNI ? gw_u(KGP, NT) : gw_of(KGP, NT), GBM = 16 * RT * GW;
   const int nblk = (n_rows + GBM - 1) / GBM;
   if (a.fmt == 1)   // fp16 operands: forward GEMMs only (checked by gemm_bf16_launch)
-    hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, 0, true>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else if (epi == E_RES) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_RES>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(64 * GW), 0, st, a);
-}
-
-template <int KGP, int NT, int GW, int S>
-static void launch_pipe_t(int epi, const GB& a, int n_rows, hipStream_t st) {
-  constexpr int GBM = PipeCfg<KGP, NT, GW, S>::GBM;
-  const int nblk = (n_rows + GBM - 1) / GBM;
-  if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_FWD, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_DGRAD, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else hipLaunchKernelGGL((k_gemm_pipe<KGP, NT, E_PLAIN, GW, S>), dim3(nblk), dim3(64 * GW), 0, st, a);
-}
-
-// RPC_SPGEMM (A/B): 0 (default) = k_gemm_bf16 (one offset of look-ahead in registers, 4 blocks per CU);
-// 1 = k_gemm_pipe, 8-wave blocks with a 4-stage ring; 2 = 4-wave blocks, 4 stages; 3 = 8-wave blocks,
-// 3 stages (the 128-wide GEMM K always takes 4-wave blocks: 4 stages, 3 at 128 x 128). Measured on the
-// metric's rulebooks (profiles/r04_spgemm_pipe_ab.txt): the ring is 2-2.6x SLOWER (<64,4,0> 87 vs 41 us,
-// <64,4,1> 138 vs 53 us) — one block per CU keeps fewer bytes in flight than four blocks with one offset of
-// register look-ahead each; kept for A/B. 4 + DBG: timing arms of k_gemm_bf16<64, 4, ·>.
-static int g_gemm_mode = -1;
-static int gemm_mode() {
-  if (g_gemm_mode < 0) {
-    const char* e = getenv("RPC_SPGEMM");
-    int m = e ? atoi(e) : 0;
-    g_gemm_mode = (m < 0 || m > 19) ? 0 : m;
-  }
-  return g_gemm_mode;
+    hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, true, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_RES) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_RES, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
 }
 
 static int launch(int KGP, int NT, int epi, const GB& a, int n_rows, hipStream_t st) {
-  int mode = gemm_mode();
-#define C2(kg, nt)                                                  \
-  if (KGP == kg && NT == nt) {                                      \
-    if (mode == 0) launch_t<kg, nt>(epi, a, n_rows, st);            \
-    else if (mode == 2) launch_pipe_t<kg, nt, 4, 4>(epi, a, n_rows, st); \
-    else if (mode == 3) launch_pipe_t<kg, nt, 8, 3>(epi, a, n_rows, st); \
-    else launch_pipe_t<kg, nt, 8, 4>(epi, a, n_rows, st);           \
-    return RPC_OK;                                                  \
+  const bool uni = a.lnbr != nullptr;
+#define C2(kg, nt)                                          \
+  if (KGP == kg && NT == nt) {                              \
+    if (uni) launch_k<kg, nt, true>(epi, a, n_rows, st);    \
+    else launch_k<kg, nt, false>(epi, a, n_rows, st);       \
+    return RPC_OK;                                          \
   }
-#define C2W(kg, nt, s)                                              \
-  if (KGP == kg && NT == nt) {                                      \
-    if (mode == 0) launch_t<kg, nt>(epi, a, n_rows, st);            \
-    else launch_pipe_t<kg, nt, 4, s>(epi, a, n_rows, st);           \
-    return RPC_OK;                                                  \
-  }
-  // 128-wide GEMM K: 4-wave blocks (a 32 KB weight tile per stage at 128 x 128)
-#define C2H(kg, nt)                                                 \
-  if (KGP == kg && NT == nt) {                                      \
-    if (mode == 0) launch_t<kg, nt>(epi, a, n_rows, st);            \
-    else if (mode == 3) launch_pipe_t<kg, nt, 8, 3>(epi, a, n_rows, st); \
-    else launch_pipe_t<kg, nt, 4, 4>(epi, a, n_rows, st);           \
-    return RPC_OK;                                                  \
-  }
-  // 64-wide GEMM K with two row tiles per wave (rt_of): 4-wave blocks by default (8 x 4 KB of gathered rows
-  // per stage would not fit 4 stages); 128-wide: 4-wave blocks (a 32 KB weight tile per stage at 128 x 128)
-  if (epi == E_RES) mode = 0;   // the regular kernel only
-  if (mode >= 4 && KGP == 64 && NT == 4) {   // timing arms of k_gemm_bf16 (DBG = mode - 4)
-    const int nblk = (n_rows + 127) / 128;
-#define DB(d)                                                                                              \
-  if (mode - 4 == d) {                                                                                     \
-    if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<64, 4, E_FWD, d>), dim3(nblk), dim3(512), 0, st, a);   \
-    else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<64, 4, E_DGRAD, d>), dim3(nblk), dim3(512), 0, st, a); \
-    else hipLaunchKernelGGL((k_gemm_bf16<64, 4, E_PLAIN, d>), dim3(nblk), dim3(512), 0, st, a);              \
-    return RPC_OK;                                                                                         \
-  }
-    DB(0) DB(1) DB(2) DB(3) DB(4) DB(5) DB(6) DB(7) DB(8) DB(9) DB(12) DB(13)
-#undef DB
-    return RPC_ERR_ARG;
-  }
-  if (mode >= 4 || a.fmt || a.perm) mode = 0;   // (the ring variants: bf16, natural row order only)
-  C2(32, 1) C2(32, 2) C2(32, 4) C2H(64, 2) C2(64, 4) C2(64, 8) C2W(128, 4, 4) C2(32, 8) C2H(64, 1) C2W(128, 2, 4)
-  C2W(128, 8, 3)
-#undef C2H
+  C2(32, 1) C2(32, 2) C2(32, 4) C2(64, 2) C2(64, 4) C2(64, 8) C2(128, 4) C2(32, 8) C2(64, 1) C2(128, 2) C2(128, 8)
 #undef C2
-#undef C2W
   return RPC_ERR_UNSUPPORTED;
 }
 
@@ -1425,13 +926,6 @@ static inline int r32(int c) { return (c + 31) / 32 * 32; }
 
 using namespace rpc;
 using namespace rpc::spb;
-
-// A/B and tests: select the sparse bf16 GEMM kernel (see gemm_mode); returns the previous mode
-extern "C" int rpc_spconv_gemm_bf16_mode(int mode) {
-  const int prev = gemm_mode();
-  if (mode >= 0 && mode <= 19) g_gemm_mode = mode;
-  return prev;
-}
 
 extern "C" int rpc_to_h16_rows(const float* z, const float* bn, int n, int c, int relu, int fmt, void* h,
                                void* h_bf16, void* stream) {
@@ -1558,14 +1052,24 @@ extern "C" int rpc_spconv_gemm_h16(const void* a, int fmt, int n_src, int kg, co
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 
-// the general form: operand format fmt (fp16: forward only) and rows visited in the order perm (may be NULL)
-extern "C" int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
-                                    const int* perm, int n_out, const void* bt, int ng, float* out,
-                                    const float* prev_z, const float* prev_bn, float* part, int epi, void* stream) {
+static void set_union(GB& g, const RpcRowUnion* un) {
+  if (un && un->lnbr) {
+    g.lnbr = un->lnbr;
+    g.ulist = un->ulist;
+    g.ucnt = un->ucnt;
+  }
+}
+
+// the general form: operand format fmt (fp16: forward only) and the map's per-block source-row unions (un, from
+// rpc_rulebook_union of the same map; NULL = every gather from global memory)
+extern "C" int rpc_spconv_gemm_ex(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
+                                  const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out,
+                                  const float* prev_z, const float* prev_bn, float* part, int epi, void* stream) {
+  if (un && un->lnbr && (!un->ulist || !un->ucnt)) return RPC_ERR_ARG;
   GB g;
   memset(&g, 0, sizeof(g));
   g.fmt = fmt;
-  g.perm = perm;
+  set_union(g, un);
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 
@@ -1573,59 +1077,43 @@ extern "C" int rpc_spconv_gemm_perm(const void* a, int fmt, int n_src, int kg, c
 // m = (dgrad + g2) * [out > 0] -> m [n_out][ng] fp32, and the BatchNorm-backward partial rows (sum m,
 // sum m * (z - mean) * invstd) of that layer (bn: scale, beta, mean, invstd) -> part [gemm blocks][2 * ng]
 extern "C" int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
-                                   const int* perm, int n_out, const void* bt, int ng, float* m, const float* g2,
+                                   const RpcRowUnion* un, int n_out, const void* bt, int ng, float* m, const float* g2,
                                    const float* out, const float* z, const float* bn, float* part,
                                    const RpcBnFin* fin, void* stream) {
   if (!m || !out || !z || !bn || !part) return RPC_ERR_ARG;
+  if (un && un->lnbr && (!un->ulist || !un->ucnt)) return RPC_ERR_ARG;
   if (fin && (fin->mode != 1 || !fin->ticket || !fin->gpart || !fin->gamma || !fin->fbn || !fin->bn || ng > 256 ||
               n_out <= 0))
     return RPC_ERR_ARG;
   GB g;
   memset(&g, 0, sizeof(g));
   if (fin) g.fin = *fin;   // + that layer's BatchNorm-backward finalize (mode 1) in the last-arriving blocks
-  g.perm = perm;
+  set_union(g, un);
   g.eg2 = g2;
   g.eout = out;
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, m, z, bn, part, E_RES, stream);
 }
 
-// largest block of the k_gemm_pipe launches (rows): fin_groups of n_out at the smallest block (64 rows)
+// largest block of the GEMM launches (rows): fin_groups of n_out at the smallest block (64 rows)
 extern "C" int rpc_bn_fin_groups(int n_out) { return fin_groups(cdiv(n_out > 0 ? n_out : 1, 64)); }
 extern "C" int rpc_bn_fin_tickets(int n_out) { return 1 + rpc_bn_fin_groups(n_out); }
 
-// the fused-finalize GEMM on 16-bit operands of either format (fp16: the forward, epi 0, only)
-extern "C" int rpc_spconv_gemm_h16_fin(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
-                                       int n_out, const void* bt, int ng, float* out, const float* prev_z,
-                                       const float* prev_bn, float* part, int epi, const RpcBnFin* fin, void* stream) {
-  if (fmt != 0 && (fmt != 1 || epi != 0)) return RPC_ERR_ARG;
-  if (!fin) return rpc_spconv_gemm_h16(a, fmt, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part,
-                                       epi, stream);
-  if ((epi != 0 && epi != 1) || !part || !fin->ticket || !fin->gpart || !fin->gamma || !fin->bn ||
-      (epi == 0 && (!fin->beta || !fin->running_mean || !fin->running_var)) || (epi == 1 && !fin->fbn) ||
-      fin->mode != epi || ng > 256)
-    return RPC_ERR_ARG;
-  if (n_out <= 0) return RPC_ERR_ARG;   // the finalize divides by the row count
-  if (gemm_mode() >= 4) {   // the timing arms of k_gemm_bf16: no fused finalize
-    int rc = rpc_spconv_gemm_h16(a, fmt, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi,
-                                 stream);
-    if (rc) return rc;
-    return rpc_bn_finalize(part, cdiv(n_out, BM), ng, n_out, epi, fin->gamma, fin->beta, fin->eps, fin->momentum,
-                           fin->running_mean, fin->running_var, fin->fbn, fin->bn, fin->dgamma, fin->dbeta, nullptr,
-                           stream);
-  }
+// the data gradient (epi 1) with the BatchNorm-backward finalize of the layer whose ReLU mask it applies fused in
+extern "C" int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
+                                        const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out,
+                                        const float* prev_z, const float* prev_bn, float* part, int epi,
+                                        const RpcBnFin* fin, void* stream) {
+  if (un && un->lnbr && (!un->ulist || !un->ucnt)) return RPC_ERR_ARG;
   GB g;
   memset(&g, 0, sizeof(g));
-  g.fmt = fmt;
-  g.fin = *fin;
+  set_union(g, un);
+  if (fin) {
+    if (epi != 1 || !part || !fin->ticket || !fin->gpart || !fin->gamma || !fin->bn || !fin->fbn || fin->mode != 1 ||
+        ng > 256 || n_out <= 0)
+      return RPC_ERR_ARG;
+    g.fin = *fin;
+  }
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
-}
-
-extern "C" int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
-                                        int n_out, const void* bt, int ng, float* out, const float* prev_z,
-                                        const float* prev_bn, float* part, int epi, const RpcBnFin* fin,
-                                        void* stream) {
-  return rpc_spconv_gemm_h16_fin(a, 0, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, fin,
-                                 stream);
 }
 
 extern "C" int rpc_spconv_gemm_bf16(const void* a, int kg, const int* map, int kvol, int rev, int n_out,
@@ -1698,122 +1186,7 @@ static int wgrad_chunks(int n, int kvol, int ci, int co) {
   return c;
 }
 
-static int pairs_slots_dyn(int ci, int co) {
-#define PS(a, b) if (ci == a && co == b) return pairs_slots<a, b>();
-  PS(16, 16) PS(16, 32) PS(32, 32) PS(32, 64) PS(64, 64) PS(64, 128) PS(128, 128)
-#undef PS
-  return 0;
-}
-
-struct PairWs {
-  int* cnt;
-  int* base;
-  void* scan_tmp;
-  size_t scan_bytes;
-  int2* pairs;
-  float* part;
-  size_t total;
-};
-
-static int pair_ws(int n_out, int kvol, int ci, int co, char* w, PairWs* o) {
-  const int S = pairs_slots_dyn(ci, co);
-  if (S <= 0) return RPC_ERR_UNSUPPORTED;
-  const int nb = cdiv(n_out > 0 ? n_out : 1, PRB);
-  const long long nc = (long long)kvol * nb + 1;
-  size_t scan_b = 0;
-  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan_b, (const int*)nullptr, (int*)nullptr, (int)nc, (hipStream_t)0) !=
-      hipSuccess)
-    return RPC_ERR_HIP;
-  auto al = [](size_t x) { return (x + 255) & ~(size_t)255; };
-  size_t off = 0;
-  o->cnt = (int*)(w + off);
-  off += al(sizeof(int) * nc);
-  o->base = (int*)(w + off);
-  off += al(sizeof(int) * nc);
-  o->scan_tmp = w + off;
-  o->scan_bytes = scan_b;
-  off += al(scan_b);
-  o->pairs = (int2*)(w + off);
-  off += al(sizeof(int2) * (size_t)(n_out > 0 ? n_out : 1) * kvol);
-  o->part = (float*)(w + off);
-  off += al(sizeof(float) * (size_t)(S + kvol) * ci * co);
-  o->total = off;
-  return RPC_OK;
-}
-
-extern "C" size_t rpc_spconv_wgrad_pairs_workspace_size(int n_out, int kvol, int ci, int co) {
-  PairWs o;
-  if (n_out < 0 || kvol < 1 || kvol > MAXK || pair_ws(n_out, kvol, ci, co, nullptr, &o)) return 0;
-  return o.total;
-}
-
-// the same weight gradient as rpc_spconv_wgrad_h16 over per-offset pair lists built from nbr here
-extern "C" int rpc_spconv_wgrad_pairs(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out,
-                                      const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
-  if (hfmt != 0 && hfmt != 1) return RPC_ERR_ARG;
-  if (n_out < 0 || kvol < 1 || kvol > MAXK || !h || !nbr || !dz || !dW || !ws) return RPC_ERR_ARG;
-  hipStream_t st = (hipStream_t)stream;
-  if (n_out == 0) {
-    RPC_CHECK(hipMemsetAsync(dW, 0, sizeof(float) * (size_t)kvol * ci * co, st));
-    return RPC_OK;
-  }
-  if ((long long)n_out * kvol >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
-  PairWs o;
-  int rc = pair_ws(n_out, kvol, ci, co, (char*)ws, &o);
-  if (rc) return rc;
-  if (ws_bytes < o.total) return RPC_ERR_WORKSPACE;
-  const int S = pairs_slots_dyn(ci, co), nb = cdiv(n_out, PRB);
-  const int nc = kvol * nb + 1;
-  hipLaunchKernelGGL(k_pair_count, dim3(nb), dim3(PRB), 0, st, nbr, n_out, kvol, nb, o.cnt);
-  RPC_LAUNCH_CHECK();
-  size_t sb = o.scan_bytes;
-  if (hipcub::DeviceScan::ExclusiveSum(o.scan_tmp, sb, o.cnt, o.base, nc, st) != hipSuccess) return RPC_ERR_HIP;
-  hipLaunchKernelGGL(k_pair_scatter, dim3(nb), dim3(PRB), 0, st, nbr, n_out, kvol, nb, (const int*)o.base, o.pairs);
-  RPC_LAUNCH_CHECK();
-  const u16* hp = (const u16*)h;
-  const u16* dp = (const u16*)dz;
-  const int HP = r8(ci), DP = r8(co);
-  const dim3 grid(S + kvol);
-#define W2(a, b)                                                                                              \
-  if (ci == a && co == b) {                                                                                  \
-    if (hfmt)                                                                                                \
-      hipLaunchKernelGGL((k_wgrad_pairs<a, b, true>), grid, dim3(BLK), 0, st, hp, HP, (const int2*)o.pairs,    \
-                         (const int*)o.base, nb, kvol, S, dp, DP, o.part);                                    \
-    else                                                                                                     \
-      hipLaunchKernelGGL((k_wgrad_pairs<a, b>), grid, dim3(BLK), 0, st, hp, HP, (const int2*)o.pairs,          \
-                         (const int*)o.base, nb, kvol, S, dp, DP, o.part);                                    \
-  } else
-  W2(16, 16) W2(16, 32) W2(32, 32) W2(32, 64) W2(64, 64) W2(64, 128) W2(128, 128)
-  { return RPC_ERR_UNSUPPORTED; }
-#undef W2
-  RPC_LAUNCH_CHECK();
-  const long long per = (long long)ci * co;
-  hipLaunchKernelGGL(k_pair_reduce, dim3((unsigned)((per * kvol + BLK - 1) / BLK)), dim3(BLK), 0, st,
-                     (const float*)o.part, (const int*)o.base, nb, kvol, S, per, dW);
-  RPC_LAUNCH_CHECK();
-  return RPC_OK;
-}
-
-extern "C" int rpc_spconv_wgrad_pairs(const void* h, int hfmt, int ci, const int* nbr, int kvol, int n_out,
-                                      const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream);
-// RPC_SPWG_PAIRS=1 (A/B): the pair-list weight gradient behind rpc_spconv_wgrad_h16. Off by default: measured
-// on the step (profiles/r04_wgrad_pairs_ab.txt) the weight-gradient kernel gets only 10-25 % faster
-// (k_wgrad_bf16<64,64,3> 69.6 -> 50.9 us; CenterPoint <128,128> 449 -> 354 us) — rows without a neighbour
-// at an offset were cheap already (contiguous dz rows, no h gather, zero MFMA rows) and the time is the
-// per-sub-tile gather round trip, which the pairs keep — while the compaction (count + scan + scatter per
-// layer: 10-50 us) and the per-offset reduce eat the gain: SECOND 7.16 -> 7.65 ms/step, CenterPoint
-// 150.0 -> 147.1 frames/s
-static bool wgrad_pairs_mode() {
-  static int m = -1;
-  if (m < 0) {
-    const char* e = getenv("RPC_SPWG_PAIRS");
-    m = (e && atoi(e) != 0) ? 1 : 0;
-  }
-  return m == 1;
-}
-
 extern "C" size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co) {
-  if (wgrad_pairs_mode() && pairs_slots_dyn(ci, co) > 0) return rpc_spconv_wgrad_pairs_workspace_size(n_out, kvol, ci, co);
   return (size_t)wgrad_chunks(n_out, kvol, ci, co) * kvol * ci * co * sizeof(float);
 }
 
@@ -1830,8 +1203,6 @@ extern "C" int rpc_spconv_wgrad_h16(const void* h, int hfmt, int ci, const int* 
                                     const void* dz, int co, float* dW, void* ws, size_t ws_bytes, void* stream) {
   if (hfmt != 0 && hfmt != 1) return RPC_ERR_ARG;
   if (n_out < 0 || kvol < 1 || kvol > MAXK) return RPC_ERR_ARG;
-  if (wgrad_pairs_mode() && pairs_slots_dyn(ci, co) > 0)
-    return rpc_spconv_wgrad_pairs(h, hfmt, ci, nbr, kvol, n_out, dz, co, dW, ws, ws_bytes, stream);
   bool ok = (ci == 16 && (co == 16 || co == 32)) || (ci == 32 && (co == 32 || co == 64)) ||
             (ci == 64 && (co == 64 || co == 128)) || (ci == 128 && co == 128);
   if (!ok) return RPC_ERR_UNSUPPORTED;

@@ -381,27 +381,13 @@ def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
     return y, rec, Ho, Wo
 
 
-# RPC_DENSE_WG_SIDE=1 (A/B): the SECOND backbone's weight gradients on a side stream (forked after each
-# layer's BN-backward apply, joined at the end of the backbone backward), beside the data-gradient chain.
-# Off: measured slower (SECOND 835.8 / 827.8 -> 766.0 / 627.2 frames/s, CenterPoint 164.8 -> 158.1,
-# profiles/r04_ab_dense_wg_side.txt): the one-block-per-CU S1 kernels and the weight gradient contend for
-# the CUs and the chain behind them waits longer (as round 1 measured with the former kernels). Only the
-# slab reductions on the side stream (the row-chunk kernels on the training stream) measured slower still:
-# 842.7 / 841.5 -> 755.9 / 739.7 frames/s (profiles/r04_ab_dense_wgred_side.txt) — the fork / join per layer
-# inside the captured backward costs more than the 11 us reductions it moves
-WG_SIDE = os.environ.get("RPC_DENSE_WG_SIDE", "0") != "0"
-_WG_STREAMS = {}
-
-
-def _wg_stream(dev):
-    s = _WG_STREAMS.get(str(dev))
-    if s is None:
-        s = _WG_STREAMS[str(dev)] = _ffi.side_stream(dev)
-    return s
+# (r04 measured the SECOND backbone's weight gradients on a side stream beside the data-gradient chain:
+# slower — SECOND 835.8 / 827.8 -> 766.0 / 627.2 frames/s, profiles/r04_ab_dense_wg_side.txt — and r05
+# removed it: they run on the training stream.)
 
 
 def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=None, accumulate=False,
-                    bn_part=None, next_rec=None, wg_side=None):
+                    bn_part=None, next_rec=None):
     """BN+ReLU backward, weight gradient and (optionally) data gradient of one layer.
     bn_part: this layer's BatchNorm-backward partial sums, already written by the data-gradient conv that
     produced dh (rpc_dense_conv_bnbwd) — else rpc_dense_bnbwd_stats computes them. next_rec: the layer the
@@ -435,16 +421,8 @@ def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
     wsz = eng.wgrad_ws(L.map, ri, ci, co)
     ws = _ffi.workspace(wsz, dev)
     # the U2 weight-gradient GEMM reads dz at the output rows; the others read it at the GEMM rows
-    wst = st
-    if wg_side is not None:   # fork: the side stream runs this weight gradient after dz exists
-        ev = torch.cuda.Event()
-        ev.record(torch.cuda.current_stream(dev))
-        wg_side.wait_event(ev)
-        wst = wg_side.cuda_stream
-        for t in (dz, ws, rec["h"], dW):   # no reuse of their memory before the side stream is done
-            t.record_stream(wg_side)
     _ffi.check(eng.wgrad(L.map, L.kind, _ffi.ptr(rec["h"]), rec["pitch"], ci, _ffi.ptr(dz), co, co,
-                                   ri, si, oi, _ffi.ptr(dW), _ffi.ptr(ws), wsz, wst), "rpc_dense_wgrad")
+                                   ri, si, oi, _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "rpc_dense_wgrad")
     dx = None
     next_part = None
     if need_dx:
@@ -536,7 +514,6 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
     # block bi+1's first data-gradient GEMM accumulated into a copy of it)
     dh = _nhwc(gouts[-1], dt) if gouts[-1] is not None else None
     dx = None
-    side = _wg_stream(dev) if WG_SIDE else None
     for bi in range(nb - 1, -1, -1):
         brecs = recs[bi]
         if dh is None:   # nothing flows through this block
@@ -560,17 +537,12 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
                 need_dx = need_x
             dh, dW, dgam, dbet, bn_part = _backward_layer(eng, rec, dh, rec["L"].co, 0, dev, st, need_dx, dx_out,
                                                           accumulate, bn_part=bn_part,
-                                                          next_rec=brecs[li - 1] if li > 0 else None,
-                                                          wg_side=side)
+                                                          next_rec=brecs[li - 1] if li > 0 else None)
             grads[id(rec["L"].conv.weight)] = dW
             grads[id(rec["L"].bnm.weight)] = dgam
             grads[id(rec["L"].bnm.bias)] = dbet
         if bi == 0:
             dx = dh
-    if side is not None:   # join: the weight gradients are done before anything reads them
-        ev = torch.cuda.Event()
-        ev.record(side)
-        torch.cuda.current_stream(dev).wait_event(ev)
     return (dx,) + tuple(grads.get(id(p)) for p in params), None
 
 

@@ -52,8 +52,8 @@ SIDE_STREAMS = os.environ.get("RPC_SPARSE_STREAMS", "1") != "0"
 # the backward as one native call (csrc/sparse_exec.hip rpc_sparse_backward); 0: the per-layer Python loop
 NATIVE_BACKWARD = os.environ.get("RPC_SPARSE_NATIVE", "1") != "0"
 # BatchNorm finalizes fused into the 16-bit GEMMs that produce their partial sums (rpc_spconv_gemm_bf16_fin:
-# data gradient, the default; rpc_spconv_gemm_h16_fin: forward, fp16 or bf16 operands, off; two-level
-# last-arriving blocks): no standalone rpc_bn_finalize launch in the backward of sparse layers 1-11.
+# data gradients; two-level last-arriving blocks): no standalone rpc_bn_finalize launch in the backward of
+# sparse layers 1-11.
 # RPC_SPARSE_FUSED_FIN=0: separate finalizes (A/B).
 # With an agent-scope release per block (buffer_wbl2: every block wrote back its XCD L2's dirty lines, the
 # GEMM's fresh output rows) it was k_gemm_bf16<64,4,0> 41 -> 63 us, <64,4,1> 53 -> 92 us
@@ -61,11 +61,9 @@ NATIVE_BACKWARD = os.environ.get("RPC_SPARSE_NATIVE", "1") != "0"
 # last_block_arrive_lite) the data gradient is 54.2 -> 58.6 us against the 6.4 us rpc_bn_finalize launch it
 # removes: SECOND 3-class step within noise (7.155 / 7.157 vs 7.160 / 7.153 ms), CenterPoint 159.7 / 160.0 ->
 # 161.0 / 161.1 frames/s with the backward finalizes fused (profiles/r04_ab_fused_fin.txt). The forward's
-# (RPC_SPARSE_FUSED_FIN_FWD=1, fp16 operands) measured slower on the metric's step: sparse forward 0.70 -> 0.74
-# ms, 834.8 / 837.3 -> 831.1 / 832.2 frames/s (CenterPoint +0.2 %), so it stays off. Fused and separate
-# finalizes give bit-identical results on the metric's encoder (tests/test_gpu_sparse_pipe.py)
+# measured slower on the metric's step (sparse forward 0.70 -> 0.74 ms) and was removed in r05. Fused and
+# separate finalizes give bit-identical results on the metric's encoder (tests/test_gpu_sparse_pipe.py)
 FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "1") != "0"
-FUSED_FINALIZE_FWD = os.environ.get("RPC_SPARSE_FUSED_FIN_FWD", "0") != "0"
 # perf mode forward GEMM operands (gathered rows relu(bn(z)) and forward weight tiles): fp16 (default) or bf16
 # (RPC_SPARSE_FWD_BF16=1, A/B). The operand rounding of the forward decides the ReLU masks that every gradient
 # passes: with bf16 forward operands the perturber's input gradient is 0.237 rel-L2 from float64, with fp16 0.077
@@ -73,12 +71,37 @@ FUSED_FINALIZE_FWD = os.environ.get("RPC_SPARSE_FUSED_FIN_FWD", "0") != "0"
 # tests/test_gpu_sparse_layers.py). fp16 MFMA runs at the bf16 rate; the normalised activations and the
 # weights sit far inside its range (the dz rows, which would need loss scaling in fp16, stay bf16)
 FWD_FMT = 0 if os.environ.get("RPC_SPARSE_FWD_BF16", "0") != "0" else 1
-# RPC_SPARSE_PERM=1: the 16-bit GEMMs visit each map's rows in neighbour-mask order (rpc_rulebook_mask_perm,
-# built with the rulebooks on their side stream). Off by default: measured on the metric's step
-# (profiles/r04_perm_ab.txt) the sorts cost 12 x 24.9 us and the GEMMs did not get faster
-# (k_gemm_bf16<64,4,1> 53.4 -> 52.9 us, <64,4,0,f16> 40.5 -> 42.4 us): they wait on the per-offset gather
-# round trip, not on the MFMA rows a mask-sorted block skips; 7.26 vs 7.39 ms/step without / with
-MASK_PERM = os.environ.get("RPC_SPARSE_PERM", "0") != "0"
+# r05: the 16-bit GEMMs gather each 128-row block's distinct source rows into LDS once (rpc_rulebook_union,
+# built with the rulebooks on their side stream) instead of one gather round trip per kernel offset.
+# RPC_SPARSE_UNION=0: every gather from global memory (A/B; same results). (r04's neighbour-mask row order,
+# RPC_SPARSE_PERM, measured slower and was removed: profiles/r04_perm_ab.txt)
+UNION = os.environ.get("RPC_SPARSE_UNION", "1") != "0"
+
+
+class _Union:
+    """Per-block source-row unions of one rulebook map [n][K] (rpc_rulebook_union) and the RpcRowUnion
+    descriptor the GEMM entry points take."""
+
+    def __init__(self, lib, nbr, st, dev):
+        n, K = nbr.shape
+        nb = max(lib.rpc_rulebook_union_blocks(n), 1)
+        self.lnbr = torch.empty((n, K), dtype=torch.int16, device=dev)      # u16 slots
+        self.ulist = torch.empty((nb, RPC_UNION_CAP), dtype=torch.int32, device=dev)
+        self.ucnt = torch.empty(nb, dtype=torch.int32, device=dev)
+        _ffi.check(lib.rpc_rulebook_union(_ffi.ptr(nbr), n, K, _ffi.ptr(self.lnbr), _ffi.ptr(self.ulist),
+                                          _ffi.ptr(self.ucnt), st), "rpc_rulebook_union")
+        self.c = _ffi.RpcRowUnion(self.lnbr.data_ptr(), self.ulist.data_ptr(), self.ucnt.data_ptr())
+
+    def tensors(self):
+        return (self.lnbr, self.ulist, self.ucnt)
+
+
+RPC_UNION_CAP = 512   # include/rpc_hip.h
+
+
+def _uref(u):
+    """the ctypes argument for an optional _Union"""
+    return _ffi.C.byref(u.c) if u is not None else None
 
 
 def _t3(v):
@@ -379,19 +402,20 @@ def _sparse_bytes(L, bf16, dense_bytes, backward):
 
 
 class KernelTimer:
-    """HIP-event timing of selected conv launches on the stream they are launched on.
+    """HIP-event timing of sparse conv launches on the stream they are launched on.
 
-    select: (op, ci, co) with op in {'fwd', 'dgrad', 'wgrad'}; records per launch the event pair
-    and the algorithmic FLOPs 2 * pairs * ci * co (pairs = valid rulebook entries, counted on the
-    device, read once at the end)."""
+    select: (op, ci, co) with op in {'fwd', 'dgrad', 'wgrad'}, or op None for every launch of every layer
+    (bench.py's all-kernel roofline). Records per launch the event pair and the algorithmic FLOPs
+    2 * pairs * ci * co (pairs = valid rulebook entries, counted on the device, read once at the end)."""
 
-    def __init__(self, op, ci, co):
+    def __init__(self, op=None, ci=None, co=None):
         self.sel = (op, ci, co)
         self.recs = []
         self.enabled = False
+        self.kernel, self.dtype = None, None
 
     def wants(self, op, sp):
-        return self.enabled and self.sel == (op, sp.ci, sp.co)
+        return self.enabled and (self.sel[0] is None or self.sel == (op, sp.ci, sp.co))
 
     def reset(self):
         self.recs = []
@@ -404,18 +428,29 @@ class KernelTimer:
     def stop(self, e0, nbr, ci, co, kernel=None, dtype="fp32"):
         e1 = torch.cuda.Event(enable_timing=True)
         e1.record(torch.cuda.current_stream())
-        self.recs.append((e0, e1, nbr, ci, co))   # pairs counted after the timed region
+        self.recs.append((e0, e1, nbr, ci, co, kernel, dtype))   # pairs counted after the timed region
         self.kernel, self.dtype = kernel, dtype
 
+    @staticmethod
+    def _entry(recs):
+        ms = sum(a.elapsed_time(b) for a, b, *_ in recs)
+        flops = sum(2.0 * float((nbr >= 0).sum().item()) * ci * co for _, _, nbr, ci, co, _, _ in recs)
+        n = len(recs)
+        return dict(launches=n, avg_ms=ms / n, total_ms=ms, flops_per_launch=flops / n,
+                    tflops=flops / (ms * 1e-3) / 1e12, kernel=recs[-1][5], dtype=recs[-1][6])
+
     def summary(self):
+        """the selected launches as one entry (None if nothing was recorded)"""
         torch.cuda.synchronize()
-        if not self.recs:
-            return None
-        ms = sum(a.elapsed_time(b) for a, b, *_ in self.recs)
-        flops = sum(2.0 * float((nbr >= 0).sum().item()) * ci * co for _, _, nbr, ci, co in self.recs)
-        n = len(self.recs)
-        return dict(launches=n, avg_ms=ms / n, flops_per_launch=flops / n, tflops=flops / (ms * 1e-3) / 1e12,
-                    kernel=self.kernel, dtype=self.dtype)
+        return self._entry(self.recs) if self.recs else None
+
+    def per_kernel(self):
+        """{kernel name: entry} over every recorded launch, grouped by kernel instantiation"""
+        torch.cuda.synchronize()
+        by = {}
+        for r in self.recs:
+            by.setdefault(r[5], []).append(r)
+        return {k: self._entry(v) for k, v in by.items()}
 
 
 class _RulebookPlan:
@@ -490,24 +525,22 @@ class _RulebookPlan:
                     _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, _ffi.int_arr(sp.ksize),
                                                      _ffi.ptr(enc.grid(sp.lvl_in, B, dev)), _ffi.ptr(nbr), st),
                                "rpc_subm_rulebook")
-                    perm = self._perm(nbr, st)
-                    self.rb[sp.key] = (nbr, perm)
-                    made += [t for t in (nbr, perm) if t is not None]
-                nbr, perm = self.rb[sp.key]
-                # (a submanifold map's transpose has the reversed masks: one order serves both directions)
+                    un = self._union(nbr, st)
+                    self.rb[sp.key] = (nbr, un)
+                    made += [nbr] + (list(un.tensors()) if un is not None else [])
+                nbr, un = self.rb[sp.key]
+                # (a submanifold map's transpose (rev) names the same source rows per row: one union serves the
+                # forward and the data gradient)
                 self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr, n_out=cur_n, coors_out=cur_coors,
-                                    perm=perm, perm_in=perm), made)
+                                    un=un, un_in=un), made)
                 self.next += 1
 
-    def _perm(self, nbr, st):
-        """Visiting order of a map's rows by neighbour mask (on the side stream), or None (perf-mode GEMMs
-        only; RPC_SPARSE_PERM=0)."""
-        if not (MASK_PERM and self.enc.bf16) or nbr.shape[0] == 0:
+    def _union(self, nbr, st):
+        """The map's per-block source-row unions (on the side stream), or None (16-bit GEMMs only;
+        RPC_SPARSE_UNION=0)."""
+        if not (UNION and self.enc.bf16) or nbr.shape[0] == 0:
             return None
-        perm = torch.empty(nbr.shape[0], dtype=torch.int32, device=self.dev)
-        _ffi.check(self.lib.rpc_rulebook_mask_perm(_ffi.ptr(nbr), nbr.shape[0], nbr.shape[1], _ffi.ptr(perm), st),
-                   "rpc_rulebook_mask_perm")
-        return perm
+        return _Union(self.lib, nbr, st, self.dev)
 
     def get(self, li):
         if self.plan[li] is None:
@@ -529,10 +562,11 @@ class _RulebookPlan:
                                                          _ffi.int_arr(sp.pad), _ffi.ptr(gout), n_out,
                                                          _ffi.ptr(coors_out), _ffi.ptr(nbr_out), _ffi.ptr(nbr_in),
                                                          _ffi.ptr(ws), st), "rpc_spconv_rulebook_build")
-                perm_out, perm_in = self._perm(nbr_out, st), self._perm(nbr_in, st)
+                un_out, un_in = self._union(nbr_out, st), self._union(nbr_in, st)
             self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr_out, nbr_in=nbr_in, n_out=n_out,
-                                coors_out=coors_out, perm=perm_out, perm_in=perm_in),
-                       [t for t in (coors_out, nbr_out, nbr_in, perm_out, perm_in) if t is not None])
+                                coors_out=coors_out, un=un_out, un_in=un_in),
+                       [coors_out, nbr_out, nbr_in] + [t for u in (un_out, un_in) if u is not None
+                                                       for t in u.tensors()])
             self.pending = None
             self.cur = (coors_out, n_out)
             self.next = li + 1
@@ -578,7 +612,7 @@ class SparseEncoderFn(torch.autograd.Function):
             bnm = m[1]
             p = plan.get(li)
             rec = dict(spec=sp, n_in=p["n_in"], src=src, src_bn=src_bn, coors_in=p["coors_in"], nbr=p["nbr"],
-                       n_out=p["n_out"], coors_out=p["coors_out"], perm=p.get("perm"), perm_in=p.get("perm_in"))
+                       n_out=p["n_out"], coors_out=p["coors_out"], un=p.get("un"), un_in=p.get("un_in"))
             if "nbr_in" in p:
                 rec["nbr_in"] = p["nbr_in"]
             main.wait_event(p["ev"])
@@ -591,28 +625,12 @@ class SparseEncoderFn(torch.autograd.Function):
             rec["h_in"] = hwg if rec["bf16"] else None   # the weight gradient's bf16 rows
             rec["h_fmt"] = 0
             bn = torch.empty(4 * sp.co, dtype=torch.float32, device=dev)
-            fused = False
             if rec["bf16"]:
                 bt, rec["btd"] = wtiles[li]
                 e0 = enc.timer.start() if tm else None
-                tk = (enc.fin_ticket_ptr(dev, li, n_out)
-                      if FUSED_FINALIZE_FWD and n_out > 0 and rec["perm"] is None else None)
-                if tk is not None:
-                    # GEMM + this layer's BatchNorm finalize in one launch (last-arriving blocks)
-                    gpart = torch.empty(lib.rpc_bn_fin_groups(n_out) * 2 * sp.co, dtype=torch.float64, device=dev)
-                    fin = _ffi.RpcBnFin(tk, gpart.data_ptr(), 0, gamma.data_ptr(), beta.data_ptr(), float(bnm.eps),
-                                        float(bnm.momentum), bnm.running_mean.data_ptr(), bnm.running_var.data_ptr(),
-                                        None, bn.data_ptr(), None, None)
-                    _ffi.check(lib.rpc_spconv_gemm_h16_fin(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci,
-                                                           _ffi.ptr(rec["nbr"]), sp.K, 0, n_out, _ffi.ptr(bt), sp.co,
-                                                           _ffi.ptr(z), None, None, _ffi.ptr(part), 0,
-                                                           _ffi.C.byref(fin), st), "rpc_spconv_gemm_h16_fin")
-                    fused = True
-                else:
-                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
-                                                        sp.K, 0, _ffi.ptr(rec["perm"]), n_out, _ffi.ptr(bt), sp.co,
-                                                        _ffi.ptr(z), None, None, _ffi.ptr(part), 0, st),
-                               "rpc_spconv_gemm_perm")
+                _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
+                                                  sp.K, 0, _uref(rec["un"]), n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z),
+                                                  None, None, _ffi.ptr(part), 0, st), "rpc_spconv_gemm_ex")
             else:
                 e0 = enc.timer.start() if tm else None
                 _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
@@ -622,11 +640,10 @@ class SparseEncoderFn(torch.autograd.Function):
                 kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.ci)}, {_r16(sp.co) // 16}, 0>" if rec["bf16"] else
                       f"rpc::sp::k_gemm<{sp.ci}, {sp.co}, {1 if li else 0}, 0>")
                 enc.timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
-            if not fused:
-                _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
-                                               float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
-                                               _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
-                                               None, st), "rpc_bn_finalize")
+            _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, sp.co, n_out, 0, _ffi.ptr(gamma), _ffi.ptr(beta),
+                                           float(bnm.eps), float(bnm.momentum), _ffi.ptr(bnm.running_mean),
+                                           _ffi.ptr(bnm.running_var), None, _ffi.ptr(bn), None, None,
+                                           None, st), "rpc_bn_finalize")
             rec.update(z=z, bn=bn, W=W, gamma=gamma, beta=beta)
             L.append(rec)
             if sp.mat:
@@ -808,7 +825,11 @@ class SparseEncoderFn(torch.autograd.Function):
             else:
                 mp, rev = rec["nbr_in"], 0
             din = torch.empty((n_in, sp.ci), dtype=torch.float32, device=dev)
+            td = timer is not None and timer.wants("dgrad", sp) and (li > 0 or ctx.needs_input_grad[0])
+            e0 = timer.start() if td else None
+            epi = 2    # the data-gradient epilogue: 1 = BN-backward partial rows, 2 = plain, 3 = residual (E_RES)
             if li > 0 and L[li - 1]["spec"].mat and rec["bf16"] and lib.rpc_sparse_tune(0, -1) and len(G[li - 1]) <= 1:
+                epi = 3
                 # the input is a block output: its residual backward in this data gradient's epilogue
                 # (rpc_spconv_gemm_res), as rpc_sparse_backward does
                 prev = L[li - 1]
@@ -816,16 +837,16 @@ class SparseEncoderFn(torch.autograd.Function):
                 pp = torch.empty((nb, 2 * sp.ci), dtype=torch.float32, device=dev)
                 gid = G[li - 1][0] if G[li - 1] else None
                 _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev,
-                                                   _ffi.ptr(rec["perm_in"]), n_in, _ffi.ptr(btd), sp.ci, _ffi.ptr(din),
+                                                   _uref(rec["un_in"]), n_in, _ffi.ptr(btd), sp.ci, _ffi.ptr(din),
                                                    _ffi.ptr(gid), _ffi.ptr(prev["out"]), _ffi.ptr(prev["z"]),
                                                    _ffi.ptr(prev["bn"]), _ffi.ptr(pp), None, st), "rpc_spconv_gemm_res")
                 prev["res_m"], prev["res_part"] = din, pp
             elif li > 0 and L[li - 1]["spec"].mat:
                 # the input is a materialised output: plain data gradient, masked by its own backward
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _ffi.ptr(rec["perm_in"]), n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _uref(rec["un_in"]), n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
-                               "rpc_spconv_gemm_bf16(dgrad)")
+                               "rpc_spconv_gemm_ex(dgrad)")
                 else:
                     _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
@@ -835,34 +856,32 @@ class SparseEncoderFn(torch.autograd.Function):
                 prev = L[li - 1]
                 nblk = max(lib.rpc_spconv_gemm_blocks(n_in), 1)
                 part = torch.empty((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
-                td = timer is not None and timer.wants("dgrad", sp)
+                epi = 1
                 if rec["bf16"]:
-                    e0 = timer.start() if td else None
-                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _ffi.ptr(rec["perm_in"]), n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _uref(rec["un_in"]), n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), _ffi.ptr(prev["z"]),
                                                         _ffi.ptr(prev["bn"]), _ffi.ptr(part), 1, st),
-                               "rpc_spconv_gemm_bf16(dgrad)")
+                               "rpc_spconv_gemm_ex(dgrad)")
                 else:
-                    e0 = timer.start() if td else None
                     _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci,
                                                     _ffi.ptr(prev["z"]), _ffi.ptr(prev["bn"]), _ffi.ptr(din),
                                                     _ffi.ptr(part), st), "rpc_spconv_dgrad")
-                if td:
-                    kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.co)}, {_r16(sp.ci) // 16}, 1>" if rec["bf16"] else
-                          f"rpc::sp::k_gemm<{sp.co}, {sp.ci}, 2, 1>")
-                    timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
                 dy = din
             elif ctx.needs_input_grad[0]:
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _ffi.ptr(rec["perm_in"]), n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _uref(rec["un_in"]), n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
-                               "rpc_spconv_gemm_bf16(dgrad)")
+                               "rpc_spconv_gemm_ex(dgrad)")
                 else:
                     _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
                                                     None, _ffi.ptr(din), None, st), "rpc_spconv_dgrad")
                 dfeat = din
+            if td:
+                kn = (f"rpc::spb::k_gemm_bf16<{_r32(sp.co)}, {_r16(sp.ci) // 16}, {epi}>" if rec["bf16"] else
+                      f"rpc::sp::k_gemm<{sp.co}, {sp.ci}, 2, {1 if epi == 1 else 0}>")
+                timer.stop(e0, rec["nbr"], sp.ci, sp.co, kn, "bf16" if rec["bf16"] else "fp32")
         main.wait_stream(wg)    # the weight gradients are complete before autograd hands them on
         if tm_stage:
             stage_timer.TIMER.stop("sparse_bwd", e_stage, nbytes)
@@ -896,6 +915,7 @@ def _native_backward(ctx, gdense):
     grads = []
     table = (_ffi.RpcSparseLayer * nl)()
     vp = lambda t: None if t is None else t.data_ptr()
+    up = lambda u: _ffi.C.pointer(u.c) if u is not None else None
     for li, rec in enumerate(L):
         sp = rec["spec"]
         dW = parts[3 * li].view(rec["W"].shape)
@@ -913,7 +933,7 @@ def _native_backward(ctx, gdense):
             vp(rec["h_in"]) if bf else None, None if bf else vp(rec["src"]), None if bf else vp(rec["src_bn"]),
             vp(rec["W"]), vp(rec["gamma"]), vp(rec["beta"]), vp(rec.get("btd")) if bf else None,
             dW.data_ptr(), dg.data_ptr(), db.data_ptr(), int(rec.get("h_fmt", 0)),
-            vp(rec.get("perm")) if bf else None, vp(rec.get("perm_in")) if bf else None,
+            up(rec.get("un")) if bf else None, up(rec.get("un_in")) if bf else None,
             ctx.enc.fin_ticket_ptr(dev, nl + li, rec["n_in"]) if bf and FUSED_FINALIZE else None)
     dfeat = (torch.empty((L[0]["n_in"], L[0]["spec"].ci), dtype=torch.float32, device=dev)
              if ctx.needs_input_grad[0] else None)

@@ -216,22 +216,22 @@ def test_wgrad_h16_fp16_rows(ci, co):
 @pytest.mark.parametrize("ci,co,n_out,K,density", [(64, 64, 30001, 27, 0.1), (128, 128, 20000, 27, 0.25),
                                                    (16, 16, 70000, 27, 0.05), (32, 32, 1000, 27, 0.0),
                                                    (64, 128, 513, 3, 1.0)])
-def test_wgrad_pairs_matches_fp64(ci, co, n_out, K, density):
-    """r04 pair-list weight gradient (rpc_spconv_wgrad_pairs, the default behind rpc_spconv_wgrad_h16): sparse
-    and dense maps, a map with no neighbour at all (density 0: every offset's block count is 0), tails of
-    the 512-pair segments and 64-pair sub-tiles; fp64 reference on the same bf16 values; deterministic."""
+def test_wgrad_maps_matches_fp64(ci, co, n_out, K, density):
+    """rpc_spconv_wgrad_bf16 on sparse and dense maps, a map with no neighbour at all (density 0), tails of the
+    512-row segments and 64-row sub-tiles; fp64 reference on the same bf16 values; deterministic. (r04's pair-list
+    variant of this kernel measured slower on the step and was removed in r05.)"""
     lib = _ffi.load()
     dev = torch.device("cuda")
     nbr, h, dz = _case(n_out, 20000, K, ci, co, density, seed=7 + ci + n_out)
     ref = _wgrad_ref(nbr, h, dz, K, ci, co)
-    wsz = lib.rpc_spconv_wgrad_pairs_workspace_size(n_out, K, ci, co)
+    wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, K, ci, co)
     ws = _ffi.workspace(wsz, dev)
     hd, nd, dd = h.to(dev), nbr.to(dev), dz.to(dev)
     outs = []
     for _ in range(2):
         dW = torch.full((K, ci, co), float("nan"), device=dev)
-        _ffi.check(lib.rpc_spconv_wgrad_pairs(_ffi.ptr(hd), 0, ci, _ffi.ptr(nd), K, n_out, _ffi.ptr(dd), co,
-                                              _ffi.ptr(dW), _ffi.ptr(ws), wsz, _ffi.stream_of(dW)), "wgrad_pairs")
+        _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(hd), ci, _ffi.ptr(nd), K, n_out, _ffi.ptr(dd), co,
+                                             _ffi.ptr(dW), _ffi.ptr(ws), wsz, _ffi.stream_of(dW)), "wgrad_bf16")
         outs.append(dW)
     got = outs[0].cpu().double()
     assert torch.isfinite(got).all()

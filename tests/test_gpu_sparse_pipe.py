@@ -1,9 +1,13 @@
-"""The LDS-DMA ring sparse GEMM (csrc/spconv_bf16.hip k_gemm_pipe, rpc_spconv_gemm_bf16_mode 1-3) against the
-one-offset-look-ahead kernel it replaces (mode 0): the same MFMAs in the same order per accumulator, so
-outputs and BatchNorm partial rows must be BIT-identical — for every (GEMM K, output width) instantiation,
-the three epilogues, ragged row counts (1, 15, 17, 129 rows: partial waves and blocks), offsets nobody
-uses, blocks whose rows have no neighbour at all, and the real SECOND rulebooks of a synthetic KITTI batch
-(whole bf16 SparseEncoder forward + backward, every layer)."""
+"""The sparse 16-bit GEMM's union path (csrc/spconv_bf16.hip k_gemm_bf16<..., UNI>: each 128-row block gathers
+the distinct source rows of its map entries — rpc_rulebook_union — into LDS once) against the regular path
+(one gather round trip per kernel offset): the same MFMAs in the same order per accumulator, so outputs and
+BatchNorm partial rows must be BIT-identical — for every (GEMM K, output width) instantiation, the epilogues,
+ragged row counts (1, 15, 17, 129 rows: partial waves and blocks), offsets nobody uses, blocks whose rows have no
+neighbour at all, blocks whose union overflows the LDS capacity (they take the regular gathers inside the same
+kernel), and the real SECOND rulebooks of a synthetic KITTI batch (whole bf16 SparseEncoder forward + backward).
+Also: the union lists themselves, the fused BatchNorm finalizes of the data gradients, and the basicblock
+residual backward (alone and fused into the data-gradient epilogue)."""
+import numpy as np
 import pytest
 import torch
 
@@ -11,37 +15,82 @@ from robustpointclouds_amd import _ffi
 
 pytestmark = pytest.mark.gpu
 
-# (gemm K = gathered row width, gemm N = output width): every launch shape of rpc_spconv_gemm_bf16
+# (gemm K = gathered row width, gemm N = output width): every launch shape of the 16-bit GEMM
 SHAPES = [(16, 16), (32, 16), (32, 32), (16, 32), (32, 64), (64, 32), (64, 64), (64, 128), (128, 64),
           (128, 128), (32, 128), (64, 16), (128, 32), (24, 32), (40, 64)]
+UNION_CAP = 512   # include/rpc_hip.h RPC_UNION_CAP
 
 
 def _r8(c):
     return (c + 7) // 8 * 8
 
 
-def _run(lib, mode, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev):
-    prev = lib.rpc_spconv_gemm_bf16_mode(mode)
-    try:
-        out = torch.full((n_out, ng), float("nan"), device=dev)
-        nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
-        part = torch.full((nblk, 2 * ng), float("nan"), device=dev) if epi != 2 else None
-        _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, rev, n_out, _ffi.ptr(bt), ng,
-                                              _ffi.ptr(out), _ffi.ptr(ez), _ffi.ptr(ebn), _ffi.ptr(part), epi,
-                                              _ffi.stream_of(out)), "rpc_spconv_gemm_bf16_n")
-        torch.cuda.synchronize()
-        return out, part
-    finally:
-        lib.rpc_spconv_gemm_bf16_mode(prev)
+class _U:
+    def __init__(self, lib, nbr):
+        n, K = nbr.shape
+        nb = max(lib.rpc_rulebook_union_blocks(n), 1)
+        dev = nbr.device
+        self.lnbr = torch.full((n, K), -2, dtype=torch.int16, device=dev)
+        self.ulist = torch.full((nb, UNION_CAP), -7, dtype=torch.int32, device=dev)
+        self.ucnt = torch.full((nb,), -1, dtype=torch.int32, device=dev)
+        _ffi.check(lib.rpc_rulebook_union(_ffi.ptr(nbr), n, K, _ffi.ptr(self.lnbr), _ffi.ptr(self.ulist),
+                                          _ffi.ptr(self.ucnt), _ffi.stream_of(nbr)), "rpc_rulebook_union")
+        self.c = _ffi.RpcRowUnion(self.lnbr.data_ptr(), self.ulist.data_ptr(), self.ucnt.data_ptr())
+
+    def ref(self):
+        return _ffi.C.byref(self.c)
+
+
+def _run(lib, un, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev):
+    out = torch.full((n_out, ng), float("nan"), device=dev)
+    nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
+    part = torch.full((nblk, 2 * ng), float("nan"), device=dev) if epi != 2 else None
+    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(a), 0, n_src, kg, _ffi.ptr(nbr), K, rev,
+                                      un.ref() if un is not None else None, n_out, _ffi.ptr(bt), ng, _ffi.ptr(out),
+                                      _ffi.ptr(ez), _ffi.ptr(ebn), _ffi.ptr(part), epi, _ffi.stream_of(out)),
+               "rpc_spconv_gemm_ex")
+    torch.cuda.synchronize()
+    return out, part
+
+
+@pytest.mark.parametrize("n,K,n_src", [(5000, 27, 300), (5000, 27, 100000), (129, 27, 50), (1, 27, 5), (7000, 3, 9000),
+                                       (128, 27, 20000)])
+def test_union_lists(n, K, n_src):
+    """rpc_rulebook_union: per 128-row block, ulist[:ucnt] holds distinct rows, every valid entry's slot names its
+    own source (ulist[block][lnbr[r, k]] == nbr[r, k]), absent entries are 0xFFFF, ucnt is the exact distinct
+    count (blocks past the LDS capacity included: their slots are not used)."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(n + K + n_src)
+    nbr = torch.randint(0, n_src, (n, K), generator=g, dtype=torch.int32)
+    nbr[torch.rand((n, K), generator=g) > 0.35] = -1
+    u = _U(lib, nbr.to(dev))
+    torch.cuda.synchronize()
+    ln = u.lnbr.cpu().numpy().view(np.uint16).astype(np.int64)
+    ul, uc = u.ulist.cpu().numpy(), u.ucnt.cpu().numpy()
+    nb = nbr.numpy()
+    for b in range(ul.shape[0]):
+        rows = nb[b * 128:(b + 1) * 128]
+        want = np.unique(rows[rows >= 0])
+        assert uc[b] == len(want), b
+        lb = ln[b * 128:(b + 1) * 128]
+        assert np.all(lb[rows < 0] == 0xFFFF)
+        if uc[b] <= UNION_CAP:
+            lst = ul[b, :uc[b]]
+            assert np.array_equal(np.sort(lst), want)
+            assert np.array_equal(lst[lb[rows >= 0]], rows[rows >= 0])
 
 
 @pytest.mark.parametrize("kg,ng", SHAPES)
-@pytest.mark.parametrize("n_out,K,rev", [(5000, 27, 0), (129, 27, 1), (17, 3, 0), (15, 27, 0), (1, 27, 1)])
-def test_pipe_gemm_bit_identical(kg, ng, n_out, K, rev):
+@pytest.mark.parametrize("n_out,K,rev,n_src", [(5000, 27, 0, 300), (5000, 27, 1, 60000), (129, 27, 1, 200),
+                                               (17, 3, 0, 3000), (15, 27, 0, 40), (1, 27, 1, 3000)])
+def test_union_gemm_bit_identical(kg, ng, n_out, K, rev, n_src):
+    """The union path equals the regular gathers bit for bit (outputs and partial rows, all three epilogues);
+    n_src 60000 makes most blocks overflow the LDS capacity (regular gathers inside the union kernel), n_src
+    300 / 200 / 40 keeps every block in LDS."""
     lib = _ffi.load()
     dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(kg * 131 + ng * 7 + n_out + K)
-    n_src = 3000
+    g = torch.Generator().manual_seed(kg * 131 + ng * 7 + n_out + K + n_src)
     nbr = torch.randint(0, n_src, (n_out, K), generator=g, dtype=torch.int32)
     nbr[torch.rand((n_out, K), generator=g) > 0.35] = -1
     if K > 2:
@@ -57,18 +106,14 @@ def test_pipe_gemm_bit_identical(kg, ng, n_out, K, rev):
     ez = torch.randn((n_out, ng), generator=g).to(dev)
     ebn = torch.cat([torch.rand(ng, generator=g) + 0.5, torch.randn(ng, generator=g) * 0.1,
                      torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
+    un = _U(lib, nbr)
     for epi in (0, 1, 2):
-        ref_out, ref_part = _run(lib, 0, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
+        ref_out, ref_part = _run(lib, None, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
         assert torch.isfinite(ref_out).all()
-        for mode in (1, 2, 3):
-            out, part = _run(lib, mode, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
-            assert torch.equal(out, ref_out), (mode, epi)
-            if epi != 2 and (kg, ng) == (128, 128):
-                # k_gemm_bf16 runs the 128 x 128 tiles as two 16-row tiles per wave, the ring one (LDS):
-                # the same rows per partial row, summed over 2 vs 4 waves
-                assert torch.allclose(part, ref_part, rtol=1e-5, atol=1e-5), (mode, epi)
-            elif epi != 2:
-                assert torch.equal(part, ref_part), (mode, epi)
+        out, part = _run(lib, un, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
+        assert torch.equal(out, ref_out), epi
+        if epi != 2:
+            assert torch.equal(part, ref_part), epi
 
 
 def _encoder_case():
@@ -86,14 +131,10 @@ def _encoder_case():
     return enc, feats, d["coors"]
 
 
-def _encoder_step(enc, feats, coors, mode, fused, perm=False, fmt=0):
+def _encoder_step(enc, feats, coors, union, fused, fmt=1):
     from robustpointclouds_amd import sparse_encoder as se
-    lib = _ffi.load()
-    prev, prev_f, prev_fmt, prev_p = lib.rpc_spconv_gemm_bf16_mode(mode), se.FUSED_FINALIZE, se.FWD_FMT, se.MASK_PERM
-    prev_ff = se.FUSED_FINALIZE_FWD
-    se.FUSED_FINALIZE = se.FUSED_FINALIZE_FWD = fused
-    se.FWD_FMT = fmt   # 0: bf16 forward operands (the ring kernel is a bf16 path), 1: fp16 (the perf default)
-    se.MASK_PERM = perm
+    prev_u, prev_f, prev_fmt = se.UNION, se.FUSED_FINALIZE, se.FWD_FMT
+    se.UNION, se.FUSED_FINALIZE, se.FWD_FMT = union, fused, fmt
     try:
         for p in enc.parameters():
             p.grad = None
@@ -110,38 +151,33 @@ def _encoder_step(enc, feats, coors, mode, fused, perm=False, fmt=0):
             b.running_var.copy_(v)
         return out.detach().float().clone(), f.grad.clone(), [p.grad.clone() for p in enc.parameters()], stats
     finally:
-        lib.rpc_spconv_gemm_bf16_mode(prev)
-        se.FUSED_FINALIZE = prev_f
-        se.FUSED_FINALIZE_FWD = prev_ff
-        se.FWD_FMT = prev_fmt
-        se.MASK_PERM = prev_p
+        se.UNION, se.FUSED_FINALIZE, se.FWD_FMT = prev_u, prev_f, prev_fmt
 
 
-def test_pipe_encoder_step_bit_identical():
-    """The bf16 SparseEncoder forward + backward on a synthetic KITTI batch (the metric's shapes) with the
-    ring kernel equals the one with the former kernel, bit for bit (dense BEV, every gradient, running stats),
-    both with the separate BatchNorm finalize launches."""
+@pytest.mark.parametrize("fmt", [1, 0])
+def test_union_encoder_step_bit_identical(fmt):
+    """The perf-mode SparseEncoder forward + backward on a synthetic KITTI batch (the metric's rulebooks) with the
+    union path equals the one with per-offset gathers, bit for bit (dense BEV, every gradient, running stats) —
+    fp16 (default) and bf16 forward operands."""
     enc, feats, coors = _encoder_case()
-    r0 = _encoder_step(enc, feats, coors, 0, False)
-    r1 = _encoder_step(enc, feats, coors, 1, False)
+    r0 = _encoder_step(enc, feats, coors, False, True, fmt)
+    r1 = _encoder_step(enc, feats, coors, True, True, fmt)
     assert torch.equal(r0[0], r1[0])
     assert torch.equal(r0[1], r1[1])
     for a, b in zip(r0[2] + r0[3], r1[2] + r1[3]):
         assert torch.equal(a, b)
 
 
-@pytest.mark.parametrize("mode,fmt", [(1, 0), (0, 0), (0, 1)])
-def test_fused_finalize_matches_separate_and_is_deterministic(mode, fmt):
-    """BatchNorm finalizes fused into the GEMMs (two-level last-block sums; forward on bf16 or fp16 operands,
-    the ring or the regular kernel) against the separate rpc_bn_finalize launches: bit-identical from run to run,
-    the ticket counters back at zero after every launch, and the same results up to the double-sum order of the
-    statistics, whose last-bit differences could flip a bf16 rounding or a ReLU mask downstream (relative L2 <= 5e-2
-    on the BEV, every gradient and the running statistics, the bound of the row-order test below; measured 0:
-    bit-identical on this case, r04)."""
+def test_fused_finalize_matches_separate_and_is_deterministic():
+    """BatchNorm-backward finalizes fused into the data-gradient GEMMs (two-level last-block sums) against the
+    separate rpc_bn_finalize launches: bit-identical from run to run, the ticket counters back at zero after every
+    launch, and the same results up to the double-sum order of the statistics, whose last-bit differences could
+    flip a bf16 rounding or a ReLU mask downstream (relative L2 <= 5e-2 on the BEV, every gradient and the running
+    statistics; measured 0: bit-identical on this case, r04)."""
     enc, feats, coors = _encoder_case()
-    ref = _encoder_step(enc, feats, coors, mode, False, fmt=fmt)
-    a = _encoder_step(enc, feats, coors, mode, True, fmt=fmt)
-    b = _encoder_step(enc, feats, coors, mode, True, fmt=fmt)
+    ref = _encoder_step(enc, feats, coors, True, False)
+    a = _encoder_step(enc, feats, coors, True, True)
+    b = _encoder_step(enc, feats, coors, True, True)
     for x, y in zip([a[0], a[1]] + a[2] + a[3], [b[0], b[1]] + b[2] + b[3]):
         assert torch.equal(x, y)
     worst = 0.0
@@ -149,15 +185,15 @@ def test_fused_finalize_matches_separate_and_is_deterministic(mode, fmt):
         d = ((x.double() - y.double()).norm() / max(y.double().norm().item(), 1e-30)).item()
         worst = max(worst, d)
         assert d < 5e-2, (i, d)
-    print(f"fused vs separate finalize (mode {mode}, fmt {fmt}): worst relative L2 {worst:.2e}")
+    print(f"fused vs separate finalize: worst relative L2 {worst:.2e}")
     assert int(enc.fin_tickets(feats.device).abs().sum().item()) == 0
 
 
-@pytest.mark.parametrize("kg,ng,n_out,epi", [(64, 64, 106000, 0), (32, 64, 5000, 1), (64, 128, 130, 0),
-                                             (128, 128, 64, 1), (16, 32, 1, 0)])
-def test_gemm_fin_entry_point(kg, ng, n_out, epi):
-    """rpc_spconv_gemm_bf16_fin alone: the same output rows as the unfused GEMM, the finalize outputs of
-    rpc_bn_finalize on the same partial rows (mode 0: bn + running stats; mode 1: bnb, dgamma, dbeta) to
+@pytest.mark.parametrize("kg,ng,n_out,union", [(64, 64, 106000, True), (32, 64, 5000, False), (64, 128, 130, True),
+                                               (128, 128, 64, True), (16, 32, 1, False)])
+def test_gemm_fin_entry_point(kg, ng, n_out, union):
+    """rpc_spconv_gemm_bf16_fin alone (data gradient, epi 1): the same output rows as the unfused GEMM, the
+    finalize outputs of rpc_bn_finalize mode 1 on the same partial rows (bnb, dgamma, dbeta) to
     double-summation-order accuracy, repeated launches reuse the re-armed tickets."""
     lib = _ffi.load()
     dev = torch.device("cuda")
@@ -179,120 +215,31 @@ def test_gemm_fin_entry_point(kg, ng, n_out, epi):
     gpart = torch.empty(lib.rpc_bn_fin_groups(n_out) * 2 * ng, dtype=torch.float64, device=dev)
     nblk = lib.rpc_spconv_gemm_blocks(n_out)
     st = _ffi.stream_of(ez)
-    nb = 4 if epi == 0 else 5
+    un = _U(lib, nbr) if union else None
     for rep in range(3):
         out = torch.full((n_out, ng), float("nan"), device=dev)
         part = torch.full((nblk, 2 * ng), float("nan"), device=dev)
-        rm0, rv0 = torch.zeros(ng, device=dev), torch.ones(ng, device=dev)
-        rm, rv = rm0.clone(), rv0.clone()
-        bn = torch.full((nb * ng,), float("nan"), device=dev)
+        bn = torch.full((5 * ng,), float("nan"), device=dev)
         dg, db = torch.full((ng,), float("nan"), device=dev), torch.full((ng,), float("nan"), device=dev)
-        fin = _ffi.RpcBnFin(ticket.data_ptr(), gpart.data_ptr(), epi, gamma.data_ptr(), beta.data_ptr(), 1e-3, 0.01,
-                            rm.data_ptr(), rv.data_ptr(), ebn.data_ptr() if epi else None, bn.data_ptr(),
-                            dg.data_ptr() if epi else None, db.data_ptr() if epi else None)
-        _ffi.check(lib.rpc_spconv_gemm_bf16_fin(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, n_out, _ffi.ptr(bt), ng,
-                                                _ffi.ptr(out), _ffi.ptr(ez) if epi else None,
-                                                _ffi.ptr(ebn) if epi else None, _ffi.ptr(part), epi,
+        fin = _ffi.RpcBnFin(ticket.data_ptr(), gpart.data_ptr(), 1, gamma.data_ptr(), beta.data_ptr(), 1e-3, 0.01,
+                            None, None, ebn.data_ptr(), bn.data_ptr(), dg.data_ptr(), db.data_ptr())
+        _ffi.check(lib.rpc_spconv_gemm_bf16_fin(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0,
+                                                un.ref() if un is not None else None, n_out, _ffi.ptr(bt), ng,
+                                                _ffi.ptr(out), _ffi.ptr(ez), _ffi.ptr(ebn), _ffi.ptr(part), 1,
                                                 _ffi.C.byref(fin), st), "rpc_spconv_gemm_bf16_fin")
-        ref_out, ref_part = _run(lib, 0, a, n_src, kg, nbr, K, 0, n_out, bt, ng, epi, ez, ebn, dev)
+        ref_out, ref_part = _run(lib, None, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 1, ez, ebn, dev)
         assert torch.equal(out, ref_out)
         assert torch.equal(part, ref_part)
-        rrm, rrv = rm0.clone(), rv0.clone()
-        rbn = torch.full((nb * ng,), float("nan"), device=dev)
+        rbn = torch.full((5 * ng,), float("nan"), device=dev)
         rdg, rdb = torch.full((ng,), float("nan"), device=dev), torch.full((ng,), float("nan"), device=dev)
-        _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, ng, n_out, epi, _ffi.ptr(gamma), _ffi.ptr(beta), 1e-3,
-                                       0.01, _ffi.ptr(rrm), _ffi.ptr(rrv), _ffi.ptr(ebn) if epi else None,
-                                       _ffi.ptr(rbn), _ffi.ptr(rdg) if epi else None, _ffi.ptr(rdb) if epi else None,
+        _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nblk, ng, n_out, 1, _ffi.ptr(gamma), _ffi.ptr(beta), 1e-3,
+                                       0.01, None, None, _ffi.ptr(ebn), _ffi.ptr(rbn), _ffi.ptr(rdg), _ffi.ptr(rdb),
                                        None, st), "rpc_bn_finalize")
         torch.cuda.synchronize()
-        pairs = [(bn, rbn)] + ([(rm, rrm), (rv, rrv)] if epi == 0 else [(dg, rdg), (db, rdb)])
-        for x, y in pairs:
+        for x, y in [(bn, rbn), (dg, rdg), (db, rdb)]:
             assert torch.isfinite(x).all()
             assert torch.allclose(x, y, rtol=1e-6, atol=1e-6 * max(y.abs().max().item(), 1.0))
         assert int(ticket.abs().sum().item()) == 0
-
-
-@pytest.mark.parametrize("n,K", [(5000, 27), (2048, 27), (1, 27), (70001, 3), (4099, 27)])
-def test_mask_perm_orders_rows_by_mask(n, K):
-    """rpc_rulebook_mask_perm: a permutation of the rows that, within every window of 2048 rows, lists them by
-    neighbour mask (bit k = a neighbour at offset k), ties in row order — numpy's stable sort of the same keys."""
-    import numpy as np
-    lib = _ffi.load()
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(n + K)
-    nbr = torch.randint(0, 100, (n, K), generator=g, dtype=torch.int32)
-    nbr[torch.rand((n, K), generator=g) > 0.3] = -1
-    nd = nbr.to(dev)
-    perm = torch.full((n,), -7, dtype=torch.int32, device=dev)
-    _ffi.check(lib.rpc_rulebook_mask_perm(_ffi.ptr(nd), n, K, _ffi.ptr(perm), _ffi.stream_of(perm)), "mask_perm")
-    torch.cuda.synchronize()
-    got = perm.cpu().numpy()
-    mask = ((nbr.numpy() >= 0).astype(np.int64) << np.arange(K)).sum(1)
-    want = np.concatenate([s + np.argsort(mask[s:s + 2048], kind="stable") for s in range(0, n, 2048)])
-    assert np.array_equal(got, want)
-
-
-@pytest.mark.parametrize("kg,ng", [(32, 32), (64, 64), (32, 64), (64, 32), (128, 128)])
-def test_gemm_perm_writes_rows_in_place(kg, ng):
-    """rpc_spconv_gemm_perm with the mask order: every output row equal to the natural order's (each row's own
-    sums are unchanged; -0 == +0), forward / data gradient / plain; the BatchNorm partial rows sum to the same
-    column totals (another grouping of the same values)."""
-    lib = _ffi.load()
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(kg * 5 + ng)
-    n_out, n_src, K = 9000, 6000, 27
-    nbr = torch.randint(0, n_src, (n_out, K), generator=g, dtype=torch.int32)
-    nbr[torch.rand((n_out, K), generator=g) > 0.3] = -1
-    a = torch.zeros((n_src, _r8(kg)), dtype=torch.bfloat16)
-    a[:, :kg] = torch.randn((n_src, kg), generator=g).to(torch.bfloat16)
-    W = torch.randn((K, kg, ng), generator=g) * 0.1
-    a, nbr, W = a.to(dev), nbr.to(dev), W.to(dev)
-    bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(K, kg, ng, 0), dtype=torch.bfloat16, device=dev)
-    st = _ffi.stream_of(W)
-    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), K, kg, ng, 0, _ffi.ptr(bt), st), "prep")
-    perm = torch.empty(n_out, dtype=torch.int32, device=dev)
-    _ffi.check(lib.rpc_rulebook_mask_perm(_ffi.ptr(nbr), n_out, K, _ffi.ptr(perm), st), "mask_perm")
-    ez = torch.randn((n_out, ng), generator=g).to(dev)
-    ebn = torch.cat([torch.rand(ng, generator=g) + 0.5, torch.randn(ng, generator=g) * 0.1,
-                     torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
-    nblk = lib.rpc_spconv_gemm_blocks(n_out)
-    for epi in (0, 1, 2):
-        res = []
-        for pm in (None, perm):
-            out = torch.full((n_out, ng), float("nan"), device=dev)
-            part = torch.full((nblk, 2 * ng), float("nan"), device=dev) if epi != 2 else None
-            _ffi.check(lib.rpc_spconv_gemm_perm(_ffi.ptr(a), 0, n_src, kg, _ffi.ptr(nbr), K, 0, _ffi.ptr(pm), n_out,
-                                                _ffi.ptr(bt), ng, _ffi.ptr(out), _ffi.ptr(ez), _ffi.ptr(ebn),
-                                                _ffi.ptr(part), epi, st), "gemm_perm")
-            torch.cuda.synchronize()
-            res.append((out, part))
-        assert torch.equal(res[0][0], res[1][0]), epi
-        if epi != 2:
-            t0, t1 = res[0][1].double().sum(0), res[1][1].double().sum(0)
-            assert torch.allclose(t0, t1, rtol=1e-5, atol=1e-4 * float(t0.abs().max())), epi
-
-
-def test_mask_order_encoder_step_close_and_deterministic():
-    """The bf16 encoder step with the rows of every 16-bit GEMM in mask order against index order, and
-    bit-identical from run to run. Every row's GEMM sum is unchanged (absent neighbours add exact zeros);
-    the BatchNorm partial sums are grouped differently, so mean / var move in the last fp32 bits and some
-    bf16-stored activations and gradients round one ulp the other way. With the bf16 forward operands this
-    test runs (FWD_FMT = 0), each ordering is ~0.22 (relative L2) from float64 on the input gradient
-    (tests/test_gpu_sparse_layers.py, perf_bf16fwd) and the two differ by 2.5e-2 there, 1.5e-3 on the
-    BEV: bounded at 5e-2 — the mask order is as accurate as the index order (measured with the default
-    fp16 forward: input gradient 7.37e-2 from float64 against the operand-emulation oracle's 7.39e-2)."""
-    enc, feats, coors = _encoder_case()
-    ref = _encoder_step(enc, feats, coors, 0, False, perm=False)
-    a = _encoder_step(enc, feats, coors, 0, False, perm=True)
-    b = _encoder_step(enc, feats, coors, 0, False, perm=True)
-    for x, y in zip([a[0], a[1]] + a[2] + a[3], [b[0], b[1]] + b[2] + b[3]):
-        assert torch.equal(x, y)
-    worst = 0.0
-    for i, (x, y) in enumerate(zip([ref[0], ref[1]] + ref[2] + ref[3], [a[0], a[1]] + a[2] + a[3])):
-        d = ((x.double() - y.double()).norm() / max(y.double().norm().item(), 1e-30)).item()
-        worst = max(worst, d)
-        assert d < 5e-2, (i, d)
-    print(f"mask order vs index order: worst relative L2 {worst:.2e}")
 
 
 @pytest.mark.parametrize("kg,ng,n_out,K,g2", [(32, 32, 3000, 27, True), (128, 128, 700, 27, False),
@@ -321,19 +268,56 @@ def test_gemm_res_matches_separate_residual_backward(kg, ng, n_out, K, g2):
                     torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
     nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
     # separate: plain GEMM, then the residual pass
-    din, _ = _run(lib, 0, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 2, None, None, dev)
+    din, _ = _run(lib, None, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 2, None, None, dev)
     m_ref = torch.full((n_out, ng), float("nan"), device=dev)
     p_ref = torch.full((nblk, 2 * ng), float("nan"), device=dev)
     _ffi.check(lib.rpc_sparse_res_backward(_ffi.ptr(gid) if g2 else _ffi.ptr(din), _ffi.ptr(din) if g2 else None,
                                            _ffi.ptr(out), _ffi.ptr(z), _ffi.ptr(bn), n_out, ng, _ffi.ptr(m_ref),
                                            _ffi.ptr(p_ref), st), "rpc_sparse_res_backward")
-    # fused
-    m = torch.full((n_out, ng), float("nan"), device=dev)
-    p = torch.full((nblk, 2 * ng), float("nan"), device=dev)
-    _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, None, n_out, _ffi.ptr(bt), ng,
-                                       _ffi.ptr(m), _ffi.ptr(gid) if g2 else None, _ffi.ptr(out), _ffi.ptr(z),
-                                       _ffi.ptr(bn), _ffi.ptr(p), None, st), "rpc_spconv_gemm_res")
+    # fused, per-offset gathers and the union path (same bits)
+    un = _U(lib, nbr)
+    for u in (None, un):
+        m = torch.full((n_out, ng), float("nan"), device=dev)
+        p = torch.full((nblk, 2 * ng), float("nan"), device=dev)
+        _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, u.ref() if u else None, n_out,
+                                           _ffi.ptr(bt), ng, _ffi.ptr(m), _ffi.ptr(gid) if g2 else None, _ffi.ptr(out),
+                                           _ffi.ptr(z), _ffi.ptr(bn), _ffi.ptr(p), None, st), "rpc_spconv_gemm_res")
+        torch.cuda.synchronize()
+        assert torch.equal(m, m_ref)
+        if u is None:
+            p0 = p
+        else:
+            assert torch.equal(p, p0)
+        scale = torch.cat([m.abs().sum(0), (m * ((z - bn[2 * ng:3 * ng]) * bn[3 * ng:])).abs().sum(0)])
+        assert torch.all((p.sum(0) - p_ref.sum(0)).abs() <= 1e-5 * scale + 1e-6)
+
+
+@pytest.mark.parametrize("c", [16, 48, 64, 96, 128, 200])
+@pytest.mark.parametrize("n", [1, 333, 4100])
+def test_res_backward_any_width(c, n):
+    """rpc_sparse_res_backward at every width, including the ones whose c / 4 is not a power of two (those take
+    the per-element kernel; the vectorized one tiles a wave with c / 4 lanes): m = (g1 + g2) * [out > 0] exact,
+    the (sum m, sum m * xhat) rows of every 64-row group against torch in float64."""
+    lib = _ffi.load()
+    dev = torch.device("cuda")
+    g = torch.Generator().manual_seed(c * 7 + n)
+    g1, g2, out, z = (torch.randn((n, c), generator=g).to(dev) for _ in range(4))
+    bn = torch.cat([torch.rand(c, generator=g) + 0.5, torch.randn(c, generator=g) * 0.1,
+                    torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5]).to(dev)
+    ngr = lib.rpc_spconv_gemm_blocks(n)
+    m = torch.full((n, c), float("nan"), device=dev)
+    part = torch.full((ngr + 1, 2 * c), float("nan"), device=dev)   # one guard row past the groups
+    _ffi.check(lib.rpc_sparse_res_backward(_ffi.ptr(g1), _ffi.ptr(g2), _ffi.ptr(out), _ffi.ptr(z), _ffi.ptr(bn), n, c,
+                                           _ffi.ptr(m), _ffi.ptr(part), _ffi.stream_of(m)), "rpc_sparse_res_backward")
     torch.cuda.synchronize()
+    m_ref = (g1 + g2) * (out > 0)
     assert torch.equal(m, m_ref)
-    scale = torch.cat([m.abs().sum(0), (m * ((z - bn[2 * ng:3 * ng]) * bn[3 * ng:])).abs().sum(0)])
-    assert torch.all((p.sum(0) - p_ref.sum(0)).abs() <= 1e-5 * scale + 1e-6)
+    xh = (z.double() - bn[2 * c:3 * c].double()) * bn[3 * c:].double()
+    pad = ngr * 64 - n
+    md = torch.cat([m_ref.double(), torch.zeros((pad, c), dtype=torch.float64, device=dev)]).view(ngr, 64, c)
+    xd = torch.cat([xh, torch.zeros((pad, c), dtype=torch.float64, device=dev)]).view(ngr, 64, c)
+    s1, s2 = md.sum(1), (md * xd).sum(1)
+    scale1, scale2 = md.abs().sum(1), (md * xd).abs().sum(1)
+    assert torch.all((part[:ngr, :c].double() - s1).abs() <= 1e-5 * scale1 + 1e-6)
+    assert torch.all((part[:ngr, c:].double() - s2).abs() <= 1e-5 * scale2 + 1e-6)
+    assert torch.isnan(part[ngr]).all()     # nothing written past the last group

@@ -109,7 +109,9 @@ struct GB {
   const unsigned short* lnbr;   // [Nout][K] slot of each entry's source in its block's list, 0xFFFF none
   const int* ulist;             // [blocks][RPC_UNION_CAP] source rows
   const int* ucnt;              // [blocks] list lengths (> the kernel's capacity: the block gathers from nbr)
+  long long* dbg;               // (diagnostics) per block 8 words of phase timestamps, or null
 };
+static long long* g_gemm_dbg = nullptr;
 
 // ---- BatchNorm finalize fused into the GEMM (RpcBnFin, data gradients): the partial rows every block writes
 // are summed in two fixed-order levels by last-arriving blocks — each group of FGS consecutive blocks
@@ -181,14 +183,16 @@ __device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int*
 // MFMA busy 12 %, waves waiting 57 %). Blocks whose list exceeds the kernel's LDS capacity (ucap_of) gather
 // from the map as before (same kernel, a block-uniform branch). Same products, summed in the same order per
 // accumulator: the two paths give the same bits.
-__host__ __device__ constexpr int ucap_of(int kgp) { return kgp >= 128 ? 224 : 512; }
+// LDS capacity of the union rows: two blocks per CU up to 64 channels (<= 80 KB each), one for the 128-wide tiles
+__host__ __device__ constexpr int ucap_of(int kgp) { return kgp >= 128 ? 224 : (kgp >= 64 ? 320 : 512); }
 __host__ __device__ constexpr int gw_u(int kgp, int nt) { return RPC_UNION_ROWS / (16 * rt_of(kgp, nt)); }
 
 // Occupancy: the <= 64 x 64 tiles are held to 64 VGPRs (8 waves per SIMD, 4 blocks per CU) — at 72 the
 // 106k-row 64-channel layers needed 1.08 rounds of 3 blocks per CU (k_gemm_bf16<64,4,1> 60.6 -> 51.5 us)
 template <int KGP, int NT, int EPI, bool F16 = false, bool UNI = false>
 __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
-                             UNI ? 1 : gemm_waves_per_simd(KGP, NT)) void k_gemm_bf16(GB g) {
+                             UNI ? (KGP >= 128 ? 1 : gw_u(KGP, NT) / 2) : gemm_waves_per_simd(KGP, NT)) void
+k_gemm_bf16(GB g) {
   constexpr int RT = rt_of(KGP, NT), GW = UNI ? gw_u(KGP, NT) : gw_of(KGP, NT), GBLK = 64 * GW, WR = 16 * RT,
                 GBM = WR * GW;
   static_assert(!UNI || GBM == RPC_UNION_ROWS, "union blocks");
@@ -199,15 +203,20 @@ __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
   constexpr int LS = (KGP >= 128 && NT >= 8) ? KGP + 8 : KGP + 16;
   constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
   constexpr int BPT = (BV + GBLK - 1) / GBLK;
-  // union rows in LDS: UC rows of KGP elements (pitch LA) + one zero row for entries without a neighbour
-  constexpr int UC = UNI ? ucap_of(KGP) : 0, LA = KGP + 8, CH = KGP / 8;
+  // union rows in LDS: UC rows of KGP elements + one zero row for entries without a neighbour, unpadded, the 16-B
+  // chunks of row s XOR-swizzled by s % CH (the 16 rows of one ds_read_b128 lane group then spread over the banks)
+  constexpr int UC = UNI ? ucap_of(KGP) : 0, LA = KGP, CH = KGP / 8;
   __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];
   __shared__ __attribute__((aligned(16))) u16 sA[UNI ? (UC + 1) * LA : 8];
+  __shared__ int sU[UNI ? UC : 1];
   __shared__ int sN[GBM * MAXK];
   __shared__ unsigned wmask[GW];
   __shared__ int klist[MAXK];
   __shared__ int nk;
-  __shared__ float sP[GW][2 * NGP];
+  // the epilogue's partial sums: in the union rows' LDS once the offset loop is done (UNI)
+  static_assert(!UNI || (UC + 1) * LA * 2 >= GW * 2 * NGP * 4, "sP alias");
+  __shared__ float sP_own[UNI ? 1 : GW][UNI ? 1 : 2 * NGP];
+  float (*sP)[2 * NGP] = UNI ? (float (*)[2 * NGP])(void*)sA : (float (*)[2 * NGP])(void*)sP_own;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // XCD-aware row blocks: each XCD takes one contiguous eighth of the (spatially sorted) rows, so the
   // neighbour rows its blocks gather — mostly within a few thousand rows — stay in that XCD's L2
@@ -217,6 +226,7 @@ __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
   const int r0 = lb * GBM;
   const int K = g.K;
   const int ucnt = UNI ? g.ucnt[lb] : 0;
+  const long long tdbg0 = (UNI && g.dbg) ? (long long)__builtin_amdgcn_s_memtime() : 0;
   const bool uni = UNI && ucnt <= UC;          // block-uniform
   {
     // each wave stages its own 16 rows: lane = (offset group k4, row lane&15), 4 offsets per pass;
@@ -230,19 +240,19 @@ __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
     for (int rt = 0; rt < RT; ++rt) {
       const int lr = w * WR + rt * 16 + rr, row = r0 + lr;
       int nv[NP];
+      if (UNI && uni) {   // (one uniform branch around each loop: per-element branches serialised the loads)
 #pragma unroll
-      for (int i = 0; i < NP; ++i) {
-        const int k = 4 * i + k4;
-        const long long e = (long long)row * K + (g.rev ? K - 1 - k : k);
-        if (k < K && row < g.Nout) {
-          if (uni) {
-            const unsigned short sl = g.lnbr[e];
-            nv[i] = sl == 0xFFFF ? -1 : (int)sl;
-          } else {
-            nv[i] = g.nbr[e];
-          }
-        } else {
-          nv[i] = -1;
+        for (int i = 0; i < NP; ++i) {
+          const int k = 4 * i + k4;
+          const unsigned short sl = (k < K && row < g.Nout) ? g.lnbr[(long long)row * K + (g.rev ? K - 1 - k : k)]
+                                                            : (unsigned short)0xFFFF;
+          nv[i] = sl == 0xFFFF ? -1 : (int)sl;
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < NP; ++i) {
+          const int k = 4 * i + k4;
+          nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
         }
       }
 #pragma unroll
@@ -262,15 +272,19 @@ __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.bt, (short)0, 0x7fffffff, 0x00020000);
   if (UNI && uni) {
-    // the block's source rows -> LDS, 8 chunks of 16 B in flight per thread; channels past CP (and the zero
-    // row) read as zeros through out-of-range offsets
+    // the block's list -> LDS (coalesced), then its source rows -> LDS, 8 chunks of 16 B in flight per thread;
+    // channels past CP (and the zero row) read as zeros through out-of-range offsets. (Read from global memory
+    // inside the gather loop, each list entry's load sat between two gathers and the compiler waited out
+    // every gather before the next: 8 serial round trips per block.)
+    for (int i = tid; i < ucnt; i += GBLK) sU[i] = g.ulist[(long long)lb * RPC_UNION_CAP + i];
+    __syncthreads();
     const int nq = (ucnt + 1) * CH;
     for (int q0 = 0; q0 < nq; q0 += 8 * GBLK) {
       uint4 v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int q = q0 + tid + j * GBLK, sl = q / CH, c0 = (q - sl * CH) * 8;
-        const int src = (q < nq && sl < ucnt) ? g.ulist[(long long)lb * RPC_UNION_CAP + sl] : -1;
+        const int src = (q < nq && sl < ucnt) ? sU[sl] : -1;
         unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
         asm volatile("" : "+v"(off));
         v[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
@@ -278,11 +292,13 @@ __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const int q = q0 + tid + j * GBLK, sl = q / CH, c0 = (q - sl * CH) * 8;
-        if (q < nq) *(uint4*)&sA[(sl < ucnt ? sl : UC) * LA + c0] = v[j];
+        const int ss = sl < ucnt ? sl : UC;
+        if (q < nq) *(uint4*)&sA[ss * LA + (((c0 >> 3) ^ (ss & (CH - 1))) << 3)] = v[j];
       }
     }
   }
   __syncthreads();
+  const long long tdbg1 = (UNI && g.dbg) ? (long long)__builtin_amdgcn_s_memtime() : 0;
   if (tid == 0) {
     unsigned m = 0;
     for (int q = 0; q < GW; ++q) m |= wmask[q];
@@ -388,50 +404,59 @@ __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
     }
     if (t < NK) step(t, a0, a1, bw0, bw1);
   };
-  // The union loop: A fragments are LDS reads, so a step is only its MFMAs + LDS reads (~0.2 us at 64 x 64), far
-  // shorter than an L2 round trip for the weight tile — the tiles are fetched D-1 offsets ahead into a ring of D
-  // register sets (compile-time set indices: the loop runs D steps per iteration, padded with steps that only
-  // fetch and store, so every step issues the same loads and the compiler's waits stay exact). With the regular
-  // loop's one offset of look-ahead the union path ran at ~1.8 us per step (k_gemm_bf16<64,4,1> 117 vs 60 us).
+  // The union loop: A fragments are LDS reads, so a step is only its MFMAs + LDS reads, far shorter than an L2
+  // round trip for the weight tile — the tiles are fetched D-1 offsets ahead into a ring of D register sets.
+  // The loop is unrolled over all MAXK steps (guards on NK, uniform): every per-step value is then a register —
+  // the step's offset comes from a lane of kv by readlane, each lane's A address per step was formed in the
+  // prologue — so a step waits on no chain of dependent LDS reads (klist -> neighbour slot -> row: with them the
+  // union loop ran ~1200 clk per step, as slow per CU as the per-offset gathers it replaces).
   auto unionloop = [&]() {
     constexpr int D = BPT <= 2 ? 6 : (BPT <= 4 ? 4 : 2);
-    uint4 bw[D][BPT], aa[2][RT][KS];
-    auto kl = [&](int t) { return klist[t < NK ? t : NK - 1]; };
-    auto lda = [&](int k, uint4 (&dst)[RT][KS]) {
+    const int kv = klist[lane < NK ? lane : NK - 1];        // lane t: offset of step t (NK <= 27 < 64)
+    unsigned aoff[MAXK][RT];   // LDS byte offset of this lane's A row per step (a multiple of 64) | its chunk swizzle
+#pragma unroll
+    for (int t = 0; t < MAXK; ++t) {
+      const int k = __builtin_amdgcn_readlane(kv, t);
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
-        const int src = sN[(arow + rt * 16) * MAXK + k];
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks) dst[rt][ks] = *(const uint4*)&sA[(src >= 0 ? src : UC) * LA + ks * 32 + ag * 8];
+        const int src = sN[(arow + rt * 16) * MAXK + k], ss = src >= 0 ? src : UC;
+        aoff[t][rt] = (unsigned)(ss * LA) * 2u | (unsigned)(ss & (CH - 1));
       }
+    }
+    uint4 bw[D][BPT], aa[2][RT][KS];
+    auto lda = [&](const unsigned (&off)[RT], uint4 (&dst)[RT][KS]) {
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          dst[rt][ks] = *(const uint4*)((const char*)sA + (off[rt] & ~63u) + (((ks * 4 + ag) ^ (off[rt] & 15u)) << 4));
     };
 #pragma unroll
-    for (int j = 0; j < D - 1; ++j) load_b(kl(j), bw[j]);
+    for (int j = 0; j < D - 1; ++j) load_b(__builtin_amdgcn_readlane(kv, j), bw[j]);
     store_b(0, bw[0]);
-    lda(kl(0), aa[0]);
+    lda(aoff[0], aa[0]);
     __syncthreads();
-    const int NKP = (NK + D - 1) / D * D;
-    for (int t = 0; t < NKP; t += D) {
-#define USTEP(J)                                                                                  \
-  if constexpr (J < D) {                                                                         \
-    const int tt = t + (J);                                                                      \
-    load_b(kl(tt + D - 1), bw[((J) + D - 1) % D]);                                               \
-    if (tt + 1 < NK) lda(kl(tt + 1), aa[((J) + 1) & 1]);                                         \
-    if (tt < NK && ((my >> kl(tt)) & 1u)) {                                                      \
-      const u16* bb = sB[tt & 1] + (lane & 15) * LS + ag * 8;                                    \
-      _Pragma("unroll") for (int ks = 0; ks < KS; ++ks) {                                        \
-        _Pragma("unroll") for (int n = 0; n < NT; ++n) {                                         \
-          const uint4 bv = *(const uint4*)(bb + n * 16 * LS + ks * 32);                          \
-          _Pragma("unroll") for (int rt = 0; rt < RT; ++rt)                                      \
-            acc[rt][n] = mfma16<F16>(aa[(J) & 1][rt][ks], bv, acc[rt][n]);                       \
-        }                                                                                        \
-      }                                                                                          \
-    }                                                                                            \
-    store_b((tt + 1) & 1, bw[((J) + 1) % D]);                                                    \
-    __syncthreads();                                                                             \
-  }
-      USTEP(0) USTEP(1) USTEP(2) USTEP(3) USTEP(4) USTEP(5)
-#undef USTEP
+#pragma unroll
+    for (int t = 0; t < MAXK; ++t) {
+      if (t < NK) {
+        load_b(__builtin_amdgcn_readlane(kv, t + D - 1 < MAXK ? t + D - 1 : MAXK - 1), bw[(t + D - 1) % D]);
+        if (t + 1 < MAXK) lda(aoff[t + 1 < MAXK ? t + 1 : t], aa[(t + 1) & 1]);
+        const int k = __builtin_amdgcn_readlane(kv, t);
+        if ((my >> k) & 1u) {
+          const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks) {
+#pragma unroll
+            for (int n = 0; n < NT; ++n) {
+              const uint4 bv = *(const uint4*)(bb + n * 16 * LS + ks * 32);
+#pragma unroll
+              for (int rt = 0; rt < RT; ++rt) acc[rt][n] = mfma16<F16>(aa[t & 1][rt][ks], bv, acc[rt][n]);
+            }
+          }
+        }
+        store_b((t + 1) & 1, bw[(t + 1) % D]);
+        __syncthreads();
+      }
     }
   };
   if (NK > 0) {
@@ -441,6 +466,16 @@ __global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
     } else {
       mainloop(std::false_type{});
     }
+  }
+  if (UNI && g.dbg && tid == 0) {
+    const long long t3 = (long long)__builtin_amdgcn_s_memtime();
+    long long* d = g.dbg + (long long)lb * 8;
+    d[0] = tdbg0;
+    d[1] = tdbg1;
+    d[2] = t3;
+    d[3] = NK;
+    d[4] = ucnt;
+    d[5] = uni;
   }
 
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg (16x16 shapes, gfx950)
@@ -1052,7 +1087,13 @@ extern "C" int rpc_spconv_gemm_h16(const void* a, int fmt, int n_src, int kg, co
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 
+extern "C" int rpc_spconv_gemm_debug(long long* buf) {   // diagnostics (not in the header): phase timestamps
+  g_gemm_dbg = buf;
+  return 0;
+}
+
 static void set_union(GB& g, const RpcRowUnion* un) {
+  g.dbg = g_gemm_dbg;
   if (un && un->lnbr) {
     g.lnbr = un->lnbr;
     g.ulist = un->ulist;

@@ -12,22 +12,23 @@ Oracle (host):   oracle/voxelize_ref.c -> the SAME plugin AdversarialCenterPoint
                  HardSimpleVFE formula, oracle SparseEncoder, torch-CPU SECOND / SECONDFPN, the CenterHead
                  layer stack in torch with oracle/dcn.py, oracle/center_head.py targets + losses.
 
-Tolerances: voxels bit-exact; every loss key within 1e-4 * max(1, |ref|) of the fp32 oracle (north_star).
-Gradients are bounded by the step's own conditioning, measured in the test: the sparse-encoder output of
-this step feeds ~40 train-mode BatchNorm layers over a mostly empty 128 x 128 BEV, and a relative
-perturbation of 1e-6 on it moves the float64 step's gradients by up to 2.7e-3 (mean 3.3e-4; x2700, the
-backbone / neck / head BatchNorm biases and the DCN offset convolutions most). HIP's fp32 encoder output
-is 2.1e-6 (relative L2) from float64 — ordinary fp32 rounding through 21 sparse layers (the fp32 oracle's
-is 7.8e-7) — and the fp32 oracle re-run with its encoder output perturbed by that much (white noise) moves
-the gradients by 4.7e-3 on average, up to 2.7e-2 (the perturber's, through the encoder's input gradient).
-The DCN offset gradients add their own fp32 floor: a sample point whose y - 1 + i + dy lies within an ulp of
-an integer (ulp(128) = 1.5e-5; ~300k samples per DCN) moves to the neighbouring bilinear cell. So the
-gradients are bounded by the measured conditioning: mean relative L2 from float64 over all tensors <=
-GRAD_SENS_MEAN x the probe's mean, every tensor <= max(GRAD_F64_MAX, GRAD_SENS x max(its probe value,
-the probe's mean)) and cosine >= COS_MIN against float64 (measured r04: HIP mean 5.5e-3 vs probe mean
-4.7e-3; worst tensors adversary.Wa1 5.6e-2 (probe 7.6e-3), W5 4.2e-2 (probe 2.7e-2); worst cosine 0.99912). B = 2 one-sweep frames (~25k points, ~14k voxels each) on the config's full grid
-(41 x 1024 x 1024 -> 128 x 128 BEV): the two oracle steps (float64 ~50 s, fp32 ~15 s, dominated by the
-128 x 128 SECOND / FPN / head convolutions) fit the per-test limit on the host.
+Tolerances: voxels bit-exact; every loss key within 1e-4 * max(1, |ref|) of the fp32 oracle (north_star); every
+parameter gradient within GRAD_F64_MAX relative L2 of float64, their mean within GRAD_F64_MEAN, cosine >= COS_MIN
+(the fixed bounds of tests/test_gpu_e2e_parity.py).
+
+DCN offsets (r05). The DCN offset gradient is piecewise constant in the sampling position: it jumps where a
+sample crosses a bilinear cell edge. With the offsets of r04's test (conv_offset weights N(0, 0.02), biases
+U(-0.5, 0.5): positions spread over whole cells) ~12 of each DCN's 590k samples lie within 1e-5 of an edge, and
+a 1e-5 relative change of the neck output (fp32 rounding: HIP 1.1e-5, torch fp32 4e-6) moves 1-3 of them across
+(tools/dbg_cp_flip.py, gpurun_out r05b). One crossing near a GT peak moved that DCN's offset-conv gradient by
+2.3e-2 and, through the shared conv, every gradient upstream by ~1e-2 — for HIP and equally for the float64 oracle
+fed HIP's neck output (tools/dbg_cp_sub.py: f64 | N_hip mean 5.5e-3), while HIP fed the float64 neck output was
+1.4e-4 (mean) / 2.0e-3 (max) from float64. The test therefore draws offsets that keep every sampling position
+mid-cell — conv_offset biases U(0.35, 0.65) and weights N(0, 5e-4) (the shared-conv features reach ~10 near
+objects, so the offset conv adds up to ~0.1: positions n + 0.5 +- 0.25) — so the bilinear weights, their offset
+gradients and the offset convs all stay active while no fp32 rounding can cross an edge. (With weights N(0, 0.004)
+the offsets near objects still reached cell edges: the fp32 oracle itself was then 1.6e-3 mean / 2e-2 max from
+float64, gpurun_out r05c.)
 """
 import copy
 
@@ -49,12 +50,20 @@ from robustpointclouds_amd.centerpoint import NUS_PC_RANGE, NUS_VOXEL_SIZE
 from robustpointclouds_amd.plugin.models.detectors.adversarial_centerpoint import AdversarialCenterPoint
 from robustpointclouds_amd.synthetic import nus_frame, nus_gt_boxes
 
-B, SWEEPS = 2, 1
 LOSS_TOL = 1e-4
 GRAD_F64_MAX = 1e-2
-GRAD_SENS_MEAN = 2.0
-GRAD_SENS = 10.0
-COS_MIN = 0.998
+GRAD_F64_MEAN = 2e-3
+COS_MIN = 0.9995
+
+
+def init_mid_cell_offsets(model):
+    """DCN offsets that keep every sampling position mid-cell (module docstring); upstream zero-initialises
+    the offset convs, which would put every sample exactly ON a cell edge."""
+    with torch.no_grad():
+        for th in model.pts_bbox_head.task_heads:
+            for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
+                dcn.conv_offset.weight.normal_(0, 5e-4)
+                dcn.conv_offset.bias.uniform_(0.35, 0.65)
 
 
 class _VFE(nn.Module):            # upstream HardSimpleVFE(num_features=5) formula
@@ -63,19 +72,15 @@ class _VFE(nn.Module):            # upstream HardSimpleVFE(num_features=5) formu
 
 
 class _Middle(nn.Module):
-    """The oracle sparse encoder; `noise` > 0 multiplies its output by (1 + noise * N(0, 1)) (the
-    conditioning probe), `out` keeps the last output."""
+    """The oracle sparse encoder; `out` keeps the last output."""
 
-    def __init__(self, enc, dtype, noise=0.0):
+    def __init__(self, enc, dtype):
         super().__init__()
-        self.enc, self.dtype, self.noise = enc, dtype, noise
+        self.enc, self.dtype = enc, dtype
         self.out = None
 
     def forward(self, feats, coors, batch_size):
         out = self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size).to(self.dtype)
-        if self.noise:
-            g = torch.Generator().manual_seed(3)
-            out = out * (1 + self.noise * torch.randn(out.shape, generator=g, dtype=out.dtype))
         self.out = out.detach()
         return out
 
@@ -159,7 +164,7 @@ class OracleStep:
     """The oracle composition of the step; the sparse encoder / SECOND / FPN / head stack in `dtype`, the
     perturber restatement in float64."""
 
-    def __init__(self, model, dtype, noise=0.0):
+    def __init__(self, model, dtype):
         adv = model.adversary
         self.hidden = list(adv.hidden_channels)
         w, self.lin, self.bns, self.att = _perturber_weights(adv)
@@ -172,7 +177,7 @@ class OracleStep:
                                voxel_size=NUS_VOXEL_SIZE, use_spatial_attention=True),
             adversarial_loss_weight=model.adversarial_loss_weight,
             regularization_weight=model.regularization_weight, pts_voxel_encoder=_VFE(),
-            pts_middle_encoder=_Middle(self.enc, dtype, noise), pts_backbone=backbone, pts_neck=neck,
+            pts_middle_encoder=_Middle(self.enc, dtype), pts_backbone=backbone, pts_neck=neck,
             pts_bbox_head=_CenterHead(model.pts_bbox_head, dtype))
         self.op = OraclePerturber(w, 5, self.hidden, dtype=torch.float64)
         self.ref.adversary = _Adversary(self.op)
@@ -181,7 +186,7 @@ class OracleStep:
 
     def step(self, rv, rn, rc, gts):
         batch = dict(voxels=dict(voxels=torch.from_numpy(rv).to(self.enc.dtype), num_points=torch.from_numpy(rn),
-                                 coors=torch.from_numpy(rc)), batch_size=B)
+                                 coors=torch.from_numpy(rc)), batch_size=len(gts["boxes"]))
         self.losses = self.ref.loss(batch, gts)
         self.total, _ = parse_losses(self.losses)
         self.total.backward()
@@ -219,8 +224,8 @@ def hip_grads(model):
     return out
 
 
-def frames(seed0=900):
-    pts = [nus_frame(seed0 + i, sweeps=SWEEPS) for i in range(B)]
+def frames(seed0=900, B=2, sweeps=1):
+    pts = [nus_frame(seed0 + i, sweeps=sweeps) for i in range(B)]
     gts = [nus_gt_boxes(seed0 + i) for i in range(B)]
     return pts, gts
 
@@ -230,19 +235,20 @@ def oracle_voxels(pts):
 
 
 @pytest.mark.gpu
-def test_adversarial_centerpoint_step_fp32_hip_matches_oracle():
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("B,sweeps", [(2, 1), (4, 3)])
+def test_adversarial_centerpoint_step_fp32_hip_matches_oracle(B, sweeps):
+    """B = 2 one-sweep frames (~25k points each) and B = 4 three-sweep frames (config 4's batch; ~75k points
+    each — 10 sweeps would put the float64 oracle step past the test's time) on the config's full grid
+    (41 x 1024 x 1024 -> 128 x 128 BEV)."""
     from robustpointclouds_amd.trainer import Trainer, make_nus_model
     dev = torch.device("cuda")
     torch.manual_seed(21)
     model = make_nus_model(device=dev, epoch=3)
-    with torch.no_grad():   # non-zero DCN offsets (the offset convs are zero-initialised upstream)
-        for th in model.pts_bbox_head.task_heads:
-            for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
-                dcn.conv_offset.weight.normal_(0, 0.02)
-                dcn.conv_offset.bias.uniform_(-0.5, 0.5)
+    init_mid_cell_offsets(model)
     Trainer._select_engines(model, bf16=False)
     model.train()
-    pts, gts = frames()
+    pts, gts = frames(B=B, sweeps=sweeps)
     o32 = OracleStep(model, torch.float32)
     o64 = OracleStep(model, torch.float64)
     mid = {}
@@ -269,11 +275,9 @@ def test_adversarial_centerpoint_step_fp32_hip_matches_oracle():
     ogts = dict(boxes=[torch.from_numpy(b) for b, _ in gts], labels=[torch.from_numpy(l) for _, l in gts])
     o32.step(rv, rn, rc, ogts)
     o64.step(rv, rn, rc, ogts)
-    # conditioning probe: the fp32 oracle with its encoder output perturbed at HIP's distance from float64
     eps_mid = _rel(mid["hip"].float().cpu(), o64.ref.pts_middle_encoder.out)
-    o32p = OracleStep(model, torch.float32, noise=eps_mid)
-    o32p.step(rv, rn, rc, ogts)
-    print(f"encoder output: HIP vs float64 {eps_mid:.2e} (fp32 oracle {_rel(o32.ref.pts_middle_encoder.out, o64.ref.pts_middle_encoder.out):.2e})")
+    print(f"B={B} sweeps={sweeps} voxels {rv.shape[0]}; encoder output: HIP vs float64 {eps_mid:.2e} "
+          f"(fp32 oracle {_rel(o32.ref.pts_middle_encoder.out, o64.ref.pts_middle_encoder.out):.2e})")
 
     # ---- losses
     assert set(losses) == set(o32.losses), (sorted(losses), sorted(o32.losses))
@@ -285,22 +289,22 @@ def test_adversarial_centerpoint_step_fp32_hip_matches_oracle():
     assert abs(float(total) - float(o32.total)) <= LOSS_TOL * max(1.0, abs(float(o32.total)))
     print("losses (hip, oracle):", report)
 
-    # ---- gradients against float64, bounded by the measured sensitivity
-    hg, g32, g64, g32p = hip_grads(model), o32.grads(), o64.grads(), o32p.grads()
-    assert [n for n, _ in hg] == [n for n, _ in g32] == [n for n, _ in g64] == [n for n, _ in g32p]
+    # ---- gradients against float64, fixed bounds
+    hg, g32, g64 = hip_grads(model), o32.grads(), o64.grads()
+    assert [n for n, _ in hg] == [n for n, _ in g32] == [n for n, _ in g64]
     rows = []
-    for (name, a), (_, r), (_, r64), (_, rp) in zip(hg, g32, g64, g32p):
-        assert a is not None and r is not None and r64 is not None and rp is not None, name
+    for (name, a), (_, r), (_, r64) in zip(hg, g32, g64):
+        assert a is not None and r is not None and r64 is not None, name
         a = a.cpu()
-        rows.append((_rel(a, r64), name, _cos(a, r64), _rel(r, r64), _rel(rp, r)))
+        rows.append((_rel(a, r64), name, _cos(a, r64), _rel(r, r64)))
     rows.sort(reverse=True)
-    print("gradient rel-L2 vs float64 (hip, cos, fp32 oracle, sensitivity at HIP's encoder error), worst first:")
-    for e, name, cos, e_ora, sens in rows:
-        print(f"  {name:48s} {e:.3e} {cos:.6f} {e_ora:.3e} {sens:.3e}")
+    print("gradient rel-L2 vs float64 (hip, cos, fp32 oracle), worst first:")
+    for e, name, cos, e_ora in rows[:40]:
+        print(f"  {name:48s} {e:.3e} {cos:.6f} {e_ora:.3e}")
     mean_hip = sum(r[0] for r in rows) / len(rows)
-    mean_sens = sum(r[4] for r in rows) / len(rows)
-    print(f"mean: hip {mean_hip:.2e}  sensitivity {mean_sens:.2e}")
-    for e, name, cos, e_ora, sens in rows:
-        assert e <= max(GRAD_F64_MAX, GRAD_SENS * max(sens, mean_sens)), (name, e, sens, mean_sens)
+    mean_ora = sum(r[3] for r in rows) / len(rows)
+    print(f"mean: hip {mean_hip:.2e}  fp32 oracle {mean_ora:.2e}")
+    for e, name, cos, e_ora in rows:
+        assert e <= GRAD_F64_MAX, (name, e)
         assert cos >= COS_MIN, (name, cos)
-    assert mean_hip <= GRAD_SENS_MEAN * mean_sens, (mean_hip, mean_sens)
+    assert mean_hip <= GRAD_F64_MEAN, mean_hip

@@ -2,10 +2,12 @@
 float64 oracle composition (same setup as tests/test_gpu_e2e_parity_centerpoint.py)."""
 import sys
 
+B = 2   # the r04 case: frames() defaults (2 one-sweep frames)
+
 import torch
 
 sys.path.insert(0, ".")
-from tests.test_gpu_e2e_parity_centerpoint import B, OracleStep, frames, oracle_voxels  # noqa: E402
+from tests.test_gpu_e2e_parity_centerpoint import OracleStep, frames, oracle_voxels  # noqa: E402
 from robustpointclouds_amd.adversarial_loss import parse_losses  # noqa: E402
 from robustpointclouds_amd.center_head import pack_gt  # noqa: E402
 from robustpointclouds_amd.trainer import Trainer, make_nus_model  # noqa: E402

@@ -4,13 +4,15 @@ sample's bilinear cell (floor of the sampling position) and validity, per layer 
 entries that differ from the plain float64 run (tests/test_gpu_e2e_parity_centerpoint.py setup)."""
 import sys
 
+B = 2   # the r04 case: frames() defaults (2 one-sweep frames)
+
 import torch
 from torch import nn
 
 sys.path.insert(0, ".")
 import oracle.dcn as odcn  # noqa: E402
 import tests.test_gpu_e2e_parity_centerpoint as tp  # noqa: E402
-from tests.test_gpu_e2e_parity_centerpoint import B, OracleStep, frames, oracle_voxels  # noqa: E402
+from tests.test_gpu_e2e_parity_centerpoint import OracleStep, frames, oracle_voxels  # noqa: E402
 from robustpointclouds_amd.adversarial_loss import parse_losses  # noqa: E402
 from robustpointclouds_amd.center_head import pack_gt  # noqa: E402
 from robustpointclouds_amd.trainer import Trainer, make_nus_model  # noqa: E402

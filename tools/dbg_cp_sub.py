@@ -3,12 +3,14 @@ float64 / fp32 oracle compositions of tests/test_gpu_e2e_parity_centerpoint.py w
 (E) or the neck output (N) of one side fed into the other side's downstream (value substitution, the gradient
 still flows through the receiving side's own upstream), and report each run's gradients against plain float64."""
 import sys
+
+B = 2   # the r04 case: frames() defaults (2 one-sweep frames)
 import time
 
 import torch
 
 sys.path.insert(0, ".")
-from tests.test_gpu_e2e_parity_centerpoint import (B, OracleStep, frames, hip_grads,  # noqa: E402
+from tests.test_gpu_e2e_parity_centerpoint import (OracleStep, frames, hip_grads,  # noqa: E402
                                                    oracle_voxels)
 from robustpointclouds_amd.adversarial_loss import parse_losses  # noqa: E402
 from robustpointclouds_amd.center_head import pack_gt  # noqa: E402

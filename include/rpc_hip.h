@@ -295,41 +295,20 @@ typedef struct {
 } RpcBnFin;
 int rpc_bn_fin_groups(int n_out);
 int rpc_bn_fin_tickets(int n_out);
-/* Per-block source-row unions of a rulebook map [n][kvol] (r05; no reference counterpart — spconv's implicit
- * GEMM gathers per offset): for each block of RPC_UNION_ROWS consecutive rows, the distinct source rows its
- * valid entries name (ulist[block][0..ucnt)) and each entry rewritten as the slot of its source in that list
- * (lnbr, 0xFFFF = no neighbour). The 16-bit GEMMs below gather a block's list into LDS once instead of one
- * gather round trip per offset; blocks with ucnt above the kernel's LDS capacity gather from the map as before.
- * lnbr: [n][kvol] u16; ulist: [rpc_rulebook_union_blocks(n)][RPC_UNION_CAP] int; ucnt: [blocks] int. The union
- * serves every GEMM whose OUTPUT rows are the map's rows (forward, and with rev the submanifold data gradient). */
-#define RPC_UNION_ROWS 128
-#define RPC_UNION_CAP 512
-typedef struct {
-  const unsigned short* lnbr;
-  const int* ulist;
-  const int* ucnt;
-} RpcRowUnion;
-int rpc_rulebook_union_blocks(int n);
-int rpc_rulebook_union(const int* nbr, int n, int kvol, unsigned short* lnbr, int* ulist, int* ucnt, void* stream);
-/* data gradient (epi 1) only; un: unions of `map` or NULL */
-int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
-                             const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out, const float* prev_z,
-                             const float* prev_bn, float* part, int epi, const RpcBnFin* fin, void* stream);
+/* data gradient (epi 1) only (r05: the forward's fused finalize measured slower and was removed) */
+int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out,
+                             const void* bt, int ng, float* out, const float* prev_z, const float* prev_bn,
+                             float* part, int epi, const RpcBnFin* fin, void* stream);
 /* the data gradient into a basicblock's output rows with rpc_sparse_res_backward in its epilogue (r04):
  * m = (dgrad + g2) * [out > 0] -> m [n_out][ng] fp32 (g2: the identity path's contribution or NULL; out: the
  * block output rows), and that layer's BatchNorm-backward partial rows (sum m, sum m * (z - mean) * invstd;
- * bn = scale, beta, mean, invstd) -> part [rpc_spconv_gemm_blocks(n_out)][2 * ng]. un as rpc_spconv_gemm_ex;
+ * bn = scale, beta, mean, invstd) -> part [rpc_spconv_gemm_blocks(n_out)][2 * ng];
  * fin (mode 1, or NULL): that layer's BatchNorm-backward finalize in the last-arriving blocks. */
 /* knob 0: rpc_sparse_backward's fused residual backward (1 on, 0 off); returns the previous value */
 int rpc_sparse_tune(int knob, int value);
-int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev, const RpcRowUnion* un,
-                        int n_out, const void* bt, int ng, float* m, const float* g2, const float* out, const float* z,
-                        const float* bn, float* part, const RpcBnFin* fin, void* stream);
-/* the general form: operand format fmt (RPC_H16_F16: the forward, epi 0, only) and the per-block source-row
- * unions of `map` (rpc_rulebook_union; NULL = every gather from global memory). Same results either way. */
-int rpc_spconv_gemm_ex(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
-                       const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out, const float* prev_z,
-                       const float* prev_bn, float* part, int epi, void* stream);
+int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev, int n_out, const void* bt,
+                        int ng, float* m, const float* g2, const float* out, const float* z, const float* bn,
+                        float* part, const RpcBnFin* fin, void* stream);
 /* dW[k] = sum_r h[nbr[r,k]]^T dz[r] (bf16 rows, fp32 accumulate, fixed-order reduction) */
 size_t rpc_spconv_wgrad_bf16_workspace_size(int n_out, int kvol, int ci, int co);
 int rpc_spconv_wgrad_bf16(const void* h, int ci, const int* nbr, int kvol, int n_out, const void* dz, int co,
@@ -368,8 +347,6 @@ typedef struct {
   float* dgamma;
   float* dbeta;
   int h_fmt;             /* bf16 layers: format of h_in (RPC_H16_BF16 / RPC_H16_F16) */
-  const RpcRowUnion* un_out; /* bf16 layers (optional): unions of nbr (the submanifold data gradient's map) */
-  const RpcRowUnion* un_in;  /* bf16 strided layers (optional): unions of nbr_in (their data gradient's map) */
   unsigned* fin_ticket;  /* bf16 layers: rpc_bn_fin_tickets(n_in) zeroed counters — the data gradient into the
                             layer below then finalizes that layer's BatchNorm backward in its own launch
                             (rpc_spconv_gemm_bf16_fin); NULL: a separate rpc_bn_finalize */

@@ -84,11 +84,6 @@ class RpcSpconvWprep(C.Structure):
                 ("dgrad", C.c_int), ("fmt", C.c_int)]
 
 
-class RpcRowUnion(C.Structure):
-    """include/rpc_hip.h RpcRowUnion (per-block source-row unions of a rulebook map, rpc_rulebook_union)."""
-    _fields_ = [("lnbr", C.c_void_p), ("ulist", C.c_void_p), ("ucnt", C.c_void_p)]
-
-
 class RpcSparseLayer(C.Structure):
     """include/rpc_hip.h RpcSparseLayer (one sparse conv of the rpc_sparse_backward layer table)."""
     _fields_ = [("kind", C.c_int), ("ci", C.c_int), ("co", C.c_int), ("kvol", C.c_int), ("n_in", C.c_int),
@@ -97,7 +92,7 @@ class RpcSparseLayer(C.Structure):
                 ("out", C.c_void_p), ("h_in", C.c_void_p), ("src", C.c_void_p), ("src_bn", C.c_void_p),
                 ("W", C.c_void_p), ("gamma", C.c_void_p), ("beta", C.c_void_p), ("btd", C.c_void_p),
                 ("dW", C.c_void_p), ("dgamma", C.c_void_p), ("dbeta", C.c_void_p), ("h_fmt", C.c_int),
-                ("un_out", C.POINTER(RpcRowUnion)), ("un_in", C.POINTER(RpcRowUnion)), ("fin_ticket", C.c_void_p)]
+                ("fin_ticket", C.c_void_p)]
 
 
 class RpcBnFin(C.Structure):
@@ -156,20 +151,16 @@ SIGNATURES = {
     "rpc_spconv_gemm_bf16": (i32, [vp, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_gemm_bf16_n": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
     "rpc_spconv_gemm_h16": (i32, [vp, i32, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32, vp]),
-    "rpc_spconv_gemm_ex": (i32, [vp, i32, i32, i32, vp, i32, i32, C.POINTER(RpcRowUnion), i32, vp, i32, vp, vp,
-                                 vp, vp, i32, vp]),
-    "rpc_rulebook_union_blocks": (i32, [i32]),
-    "rpc_rulebook_union": (i32, [vp, i32, i32, vp, vp, vp, vp]),
     "rpc_to_h16_rows": (i32, [vp, vp, i32, i32, i32, i32, vp, vp, vp]),
     "rpc_spconv_wgrad_h16": (i32, [vp, i32, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
     "rpc_sparse_res_forward_h16": (i32, [vp, vp, vp, i32, i32, vp, vp, i32, vp, vp]),
     "rpc_bn_fin_groups": (i32, [i32]),
     "rpc_bn_fin_tickets": (i32, [i32]),
-    "rpc_spconv_gemm_bf16_fin": (i32, [vp, i32, i32, vp, i32, i32, C.POINTER(RpcRowUnion), i32, vp, i32, vp, vp,
-                                       vp, vp, i32, C.POINTER(RpcBnFin), vp]),
+    "rpc_spconv_gemm_bf16_fin": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
+                                       C.POINTER(RpcBnFin), vp]),
     "rpc_sparse_tune": (i32, [i32, i32]),
-    "rpc_spconv_gemm_res": (i32, [vp, i32, i32, vp, i32, i32, C.POINTER(RpcRowUnion), i32, vp, i32, vp, vp, vp,
-                                  vp, vp, vp, C.POINTER(RpcBnFin), vp]),
+    "rpc_spconv_gemm_res": (i32, [vp, i32, i32, vp, i32, i32, i32, vp, i32, vp, vp, vp, vp, vp, vp,
+                                  C.POINTER(RpcBnFin), vp]),
     "rpc_spconv_wgrad_bf16_workspace_size": (sz, [i32, i32, i32, i32]),
     "rpc_spconv_wgrad_bf16": (i32, [vp, i32, vp, i32, i32, vp, i32, vp, vp, sz, vp]),
     "rpc_sparse_backward_workspace_size": (sz, [vp, i32]),

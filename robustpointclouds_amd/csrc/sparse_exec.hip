@@ -153,7 +153,6 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
     // data gradient into the layer below (its ReLU mask + BatchNorm-backward partial sums)
     const int* mp = l.kind == 0 ? l.nbr : l.nbr_in;
     const int rev = l.kind == 0 ? 1 : 0;
-    const RpcRowUnion* un = l.kind == 0 ? l.un_out : l.un_in;   // source-row unions of the data-gradient map
     const int n_in = l.n_in;
     if (li > 0 && L[li - 1].mat && l.bf16 && res_fuse() && G[li - 1].size() <= 1) {
       // the layer below is a block output: its residual backward in this GEMM's epilogue
@@ -176,7 +175,7 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
         fin.dbeta = prev.dbeta;
         fp = &fin;
       }
-      CHK(rpc_spconv_gemm_res(dzb, n_out, l.co, mp, l.kvol, rev, un, n_in, l.btd, l.ci, m,
+      CHK(rpc_spconv_gemm_res(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, m,
                               G[li - 1].empty() ? nullptr : G[li - 1][0], prev.out, prev.z, prev.bn, pp, fp, st));
       res_done[li - 1] = 1;
       res_m[li - 1] = m;
@@ -184,7 +183,7 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
     } else if (li > 0 && L[li - 1].mat) {
       float* din = (float*)A.take(sizeof(float) * (size_t)n_in * l.ci);
       if (l.bf16)
-        CHK(rpc_spconv_gemm_ex(dzb, 0, n_out, l.co, mp, l.kvol, rev, un, n_in, l.btd, l.ci, din, nullptr, nullptr,
+        CHK(rpc_spconv_gemm_h16(dzb, 0, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, nullptr, nullptr,
                                  nullptr, 2, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, din, nullptr, st));
@@ -207,17 +206,17 @@ int run(const RpcSparseLayer* L, int nl, const void* grad_dense, const int* coor
         fin.bn = bnb_fused = (float*)A.take(sizeof(float) * 5 * (size_t)l.ci);
         fin.dgamma = prev.dgamma;
         fin.dbeta = prev.dbeta;
-        CHK(rpc_spconv_gemm_bf16_fin(dzb, n_out, l.co, mp, l.kvol, rev, un, n_in, l.btd, l.ci, din, prev.z, prev.bn, part,
+        CHK(rpc_spconv_gemm_bf16_fin(dzb, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn, part,
                                      1, &fin, st));
       } else if (l.bf16)
-        CHK(rpc_spconv_gemm_ex(dzb, 0, n_out, l.co, mp, l.kvol, rev, un, n_in, l.btd, l.ci, din, prev.z, prev.bn,
+        CHK(rpc_spconv_gemm_h16(dzb, 0, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, din, prev.z, prev.bn,
                                  part, 1, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, prev.z, prev.bn, din, part, st));
       dy = din;
     } else if (dfeat) {
       if (l.bf16)
-        CHK(rpc_spconv_gemm_ex(dzb, 0, n_out, l.co, mp, l.kvol, rev, un, n_in, l.btd, l.ci, dfeat, nullptr, nullptr,
+        CHK(rpc_spconv_gemm_h16(dzb, 0, n_out, l.co, mp, l.kvol, rev, n_in, l.btd, l.ci, dfeat, nullptr, nullptr,
                                  nullptr, 2, st));
       else
         CHK(rpc_spconv_dgrad(dy, l.z, bnb, l.co, mp, l.kvol, rev, n_in, l.W, l.ci, nullptr, nullptr, dfeat, nullptr,

@@ -1119,79 +1119,6 @@ static KGeom geom(const int* ks, const int* st, const int* pd) {
   return g;
 }
 
-// ------------------------------------------------------------------ per-block source-row unions
-// The bf16 implicit GEMM (spconv_bf16.hip) visits a map's rows in blocks of RPC_UNION_ROWS; for each block this
-// pass lists the distinct source rows its valid (row, offset) entries reference — on SECOND's rulebooks ~200
-// per 128-row block against ~1000 valid entries (tools/sim_union.py) — and rewrites each entry as the slot of
-// its source in that list. The GEMM then gathers a block's U source rows into LDS once, all loads in flight
-// together, and runs every offset's MFMAs out of LDS instead of waiting one gather round trip per offset.
-// Dedup by an open-addressing table in LDS (linear probing, CAS insert); a new key takes the next slot by an
-// LDS atomic, so slot NUMBERS depend on arrival order — what the GEMM computes does not (each entry still
-// names its own source row). Blocks with more than RPC_UNION_CAP sources keep ucnt > cap: the GEMM gathers
-// those from the map as before.
-constexpr int UHT = 8192, UBLK = 256;
-__global__ __launch_bounds__(UBLK) void k_union_build(const int* __restrict__ nbr, int N, int K,
-                                                      unsigned short* __restrict__ lnbr, int* __restrict__ ulist,
-                                                      int* __restrict__ ucnt) {
-  constexpr int R = RPC_UNION_ROWS, EPT = (R * MAXK + UBLK - 1) / UBLK;
-  __shared__ int tab[UHT];
-  __shared__ unsigned short slot_of[UHT];
-  __shared__ int cnt;
-  for (int i = threadIdx.x; i < UHT; i += UBLK) tab[i] = -1;
-  if (threadIdx.x == 0) cnt = 0;
-  __syncthreads();
-  const int r0 = blockIdx.x * R, ne = R * K;
-  const long long e0 = (long long)r0 * K;
-  const long long eN = (long long)N * K;
-  int pos[EPT];
-  int src[EPT];
-#pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = threadIdx.x + j * UBLK;
-    src[j] = (e < ne && e0 + e < eN) ? nbr[e0 + e] : -1;
-  }
-#pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    pos[j] = -1;
-    const int v = src[j];
-    if (v < 0) continue;
-    unsigned h = ((unsigned)v * 2654435761u) >> (32 - 13);   // UHT = 2^13
-    while (true) {
-      const int old = atomicCAS(&tab[h], -1, v);
-      if (old == -1) {
-        const int sl = atomicAdd(&cnt, 1);
-        slot_of[h] = (unsigned short)(sl < RPC_UNION_CAP ? sl : 0xFFFE);
-        if (sl < RPC_UNION_CAP) ulist[(long long)blockIdx.x * RPC_UNION_CAP + sl] = v;
-        break;
-      }
-      if (old == v) break;
-      h = (h + 1) & (UHT - 1);
-    }
-    pos[j] = (int)h;
-  }
-  __syncthreads();
-#pragma unroll
-  for (int j = 0; j < EPT; ++j) {
-    const int e = threadIdx.x + j * UBLK;
-    if (e < ne && e0 + e < eN) lnbr[e0 + e] = pos[j] >= 0 ? slot_of[pos[j]] : (unsigned short)0xFFFF;
-  }
-  if (threadIdx.x == 0) ucnt[blockIdx.x] = cnt;
-}
-
-extern "C" int rpc_rulebook_union_blocks(int n) { return cdiv(n, RPC_UNION_ROWS); }
-
-extern "C" int rpc_rulebook_union(const int* nbr, int n, int kvol, unsigned short* lnbr, int* ulist, int* ucnt,
-                                  void* stream) {
-  if (n < 0 || kvol < 1 || kvol > MAXK) return RPC_ERR_ARG;
-  if (n == 0) return RPC_OK;
-  if (!nbr || !lnbr || !ulist || !ucnt) return RPC_ERR_ARG;
-  if ((long long)n * kvol >= (1LL << 31)) return RPC_ERR_UNSUPPORTED;
-  hipLaunchKernelGGL(k_union_build, dim3(cdiv(n, RPC_UNION_ROWS)), dim3(UBLK), 0, (hipStream_t)stream, nbr, n, kvol,
-                     lnbr, ulist, ucnt);
-  RPC_LAUNCH_CHECK();
-  return RPC_OK;
-}
-
 extern "C" int rpc_subm_rulebook(const int* coors, int N, const int* shape /* host B,D,H,W */,
                                  const int* ksize /* host [3] */, int* grid, int* nbr, void* stream) {
   if (N < 0 || !shape || !ksize) return RPC_ERR_ARG;

@@ -105,13 +105,7 @@ struct GB {
   int fmt;            // operand format of a and bt: 0 bf16, 1 fp16 (E_FWD only)
   const float* eg2;   // E_RES: the other gradient contribution [Nout][CO_real] (identity path) or null
   const float* eout;  // E_RES: the block output rows [Nout][CO_real] (ReLU mask)
-  // source-row unions of the map's RPC_UNION_ROWS-row blocks (rpc_rulebook_union), or lnbr null
-  const unsigned short* lnbr;   // [Nout][K] slot of each entry's source in its block's list, 0xFFFF none
-  const int* ulist;             // [blocks][RPC_UNION_CAP] source rows
-  const int* ucnt;              // [blocks] list lengths (> the kernel's capacity: the block gathers from nbr)
-  long long* dbg;               // (diagnostics) per block 8 words of phase timestamps, or null
 };
-static long long* g_gemm_dbg = nullptr;
 
 // ---- BatchNorm finalize fused into the GEMM (RpcBnFin, data gradients): the partial rows every block writes
 // are summed in two fixed-order levels by last-arriving blocks — each group of FGS consecutive blocks
@@ -176,26 +170,11 @@ __device__ void fused_bn_finalize(const GB& g, int lb, int PRB, double* sh, int*
   }
 }
 
-// Union path (UNI, r05): the block's RPC_UNION_ROWS rows take their source rows from the per-block union lists
-// of rpc_rulebook_union. Before the offset loop the block gathers its U distinct source rows (~200 for ~1000
-// valid entries on SECOND's maps) into LDS with every load in flight at once, then every offset's A fragments
-// are LDS reads: the loop no longer waits one gather round trip per offset (the regular path's limit: PMC
-// MFMA busy 12 %, waves waiting 57 %). Blocks whose list exceeds the kernel's LDS capacity (ucap_of) gather
-// from the map as before (same kernel, a block-uniform branch). Same products, summed in the same order per
-// accumulator: the two paths give the same bits.
-// LDS capacity of the union rows: two blocks per CU up to 64 channels (<= 80 KB each), one for the 128-wide tiles
-__host__ __device__ constexpr int ucap_of(int kgp) { return kgp >= 128 ? 224 : (kgp >= 64 ? 320 : 512); }
-__host__ __device__ constexpr int gw_u(int kgp, int nt) { return RPC_UNION_ROWS / (16 * rt_of(kgp, nt)); }
-
 // Occupancy: the <= 64 x 64 tiles are held to 64 VGPRs (8 waves per SIMD, 4 blocks per CU) — at 72 the
 // 106k-row 64-channel layers needed 1.08 rounds of 3 blocks per CU (k_gemm_bf16<64,4,1> 60.6 -> 51.5 us)
-template <int KGP, int NT, int EPI, bool F16 = false, bool UNI = false>
-__global__ __launch_bounds__(64 * (UNI ? gw_u(KGP, NT) : gw_of(KGP, NT)),
-                             UNI ? (KGP >= 128 ? 1 : gw_u(KGP, NT) / 2) : gemm_waves_per_simd(KGP, NT)) void
-k_gemm_bf16(GB g) {
-  constexpr int RT = rt_of(KGP, NT), GW = UNI ? gw_u(KGP, NT) : gw_of(KGP, NT), GBLK = 64 * GW, WR = 16 * RT,
-                GBM = WR * GW;
-  static_assert(!UNI || GBM == RPC_UNION_ROWS, "union blocks");
+template <int KGP, int NT, int EPI, bool F16 = false>
+__global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) void k_gemm_bf16(GB g) {
+  constexpr int RT = rt_of(KGP, NT), GW = gw_of(KGP, NT), GBLK = 64 * GW, WR = 16 * RT, GBM = WR * GW;
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;
   // LDS row stride: 8 mod 16 dwords (conflict-free b128 reads), except the 128 x 128 tiles, whose
@@ -203,31 +182,19 @@ k_gemm_bf16(GB g) {
   constexpr int LS = (KGP >= 128 && NT >= 8) ? KGP + 8 : KGP + 16;
   constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
   constexpr int BPT = (BV + GBLK - 1) / GBLK;
-  // union rows in LDS: UC rows of KGP elements + one zero row for entries without a neighbour, unpadded, the 16-B
-  // chunks of row s XOR-swizzled by s % CH (the 16 rows of one ds_read_b128 lane group then spread over the banks)
-  constexpr int UC = UNI ? ucap_of(KGP) : 0, LA = KGP, CH = KGP / 8;
   __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];
-  __shared__ __attribute__((aligned(16))) u16 sA[UNI ? (UC + 1) * LA : 8];
-  __shared__ int sU[UNI ? UC : 1];
   __shared__ int sN[GBM * MAXK];
   __shared__ unsigned wmask[GW];
   __shared__ int klist[MAXK];
   __shared__ int nk;
-  // the epilogue's partial sums: in the union rows' LDS once the offset loop is done (UNI)
-  static_assert(!UNI || (UC + 1) * LA * 2 >= GW * 2 * NGP * 4, "sP alias");
-  __shared__ float sP_own[UNI ? 1 : GW][UNI ? 1 : 2 * NGP];
-  float (*sP)[2 * NGP] = UNI ? (float (*)[2 * NGP])(void*)sA : (float (*)[2 * NGP])(void*)sP_own;
+  __shared__ float sP[GW][2 * NGP];
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   // XCD-aware row blocks: each XCD takes one contiguous eighth of the (spatially sorted) rows, so the
   // neighbour rows its blocks gather — mostly within a few thousand rows — stay in that XCD's L2
-  // (round-robin placement made every XCD gather from the whole source table: L2 misses). The union path
-  // keeps the natural order: block b of the grid is union block b.
-  const int lb = UNI ? (int)blockIdx.x : dn::xcd_remap(blockIdx.x, gridDim.x);
+  // (round-robin placement made every XCD gather from the whole source table: L2 misses)
+  const int lb = dn::xcd_remap(blockIdx.x, gridDim.x);
   const int r0 = lb * GBM;
   const int K = g.K;
-  const int ucnt = UNI ? g.ucnt[lb] : 0;
-  const long long tdbg0 = (UNI && g.dbg) ? (long long)__builtin_amdgcn_s_memtime() : 0;
-  const bool uni = UNI && ucnt <= UC;          // block-uniform
   {
     // each wave stages its own 16 rows: lane = (offset group k4, row lane&15), 4 offsets per pass;
     // the wave's offset mask comes from ballots (no LDS atomics)
@@ -240,20 +207,10 @@ k_gemm_bf16(GB g) {
     for (int rt = 0; rt < RT; ++rt) {
       const int lr = w * WR + rt * 16 + rr, row = r0 + lr;
       int nv[NP];
-      if (UNI && uni) {   // (one uniform branch around each loop: per-element branches serialised the loads)
 #pragma unroll
-        for (int i = 0; i < NP; ++i) {
-          const int k = 4 * i + k4;
-          const unsigned short sl = (k < K && row < g.Nout) ? g.lnbr[(long long)row * K + (g.rev ? K - 1 - k : k)]
-                                                            : (unsigned short)0xFFFF;
-          nv[i] = sl == 0xFFFF ? -1 : (int)sl;
-        }
-      } else {
-#pragma unroll
-        for (int i = 0; i < NP; ++i) {
-          const int k = 4 * i + k4;
-          nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
-        }
+      for (int i = 0; i < NP; ++i) {
+        const int k = 4 * i + k4;
+        nv[i] = (k < K && row < g.Nout) ? g.nbr[(long long)row * K + (g.rev ? K - 1 - k : k)] : -1;
       }
 #pragma unroll
       for (int i = 0; i < NP; ++i) {
@@ -271,34 +228,7 @@ k_gemm_bf16(GB g) {
   constexpr unsigned OOB = 0x80000000u;
   const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.a, (short)0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.bt, (short)0, 0x7fffffff, 0x00020000);
-  if (UNI && uni) {
-    // the block's list -> LDS (coalesced), then its source rows -> LDS, 8 chunks of 16 B in flight per thread;
-    // channels past CP (and the zero row) read as zeros through out-of-range offsets. (Read from global memory
-    // inside the gather loop, each list entry's load sat between two gathers and the compiler waited out
-    // every gather before the next: 8 serial round trips per block.)
-    for (int i = tid; i < ucnt; i += GBLK) sU[i] = g.ulist[(long long)lb * RPC_UNION_CAP + i];
-    __syncthreads();
-    const int nq = (ucnt + 1) * CH;
-    for (int q0 = 0; q0 < nq; q0 += 8 * GBLK) {
-      uint4 v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int q = q0 + tid + j * GBLK, sl = q / CH, c0 = (q - sl * CH) * 8;
-        const int src = (q < nq && sl < ucnt) ? sU[sl] : -1;
-        unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
-        asm volatile("" : "+v"(off));
-        v[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const int q = q0 + tid + j * GBLK, sl = q / CH, c0 = (q - sl * CH) * 8;
-        const int ss = sl < ucnt ? sl : UC;
-        if (q < nq) *(uint4*)&sA[ss * LA + (((c0 >> 3) ^ (ss & (CH - 1))) << 3)] = v[j];
-      }
-    }
-  }
   __syncthreads();
-  const long long tdbg1 = (UNI && g.dbg) ? (long long)__builtin_amdgcn_s_memtime() : 0;
   if (tid == 0) {
     unsigned m = 0;
     for (int q = 0; q < GW; ++q) m |= wmask[q];
@@ -338,9 +268,8 @@ k_gemm_bf16(GB g) {
       }
     }
   };
-  // The offset loop, for A fragments from global memory (LU false) or from the LDS union rows (LU true).
-  auto mainloop = [&](auto lu_tag) {
-    constexpr bool LU = decltype(lu_tag)::value;
+  // The offset loop.
+  auto mainloop = [&]() {
     // Every global load of the loop is issued unconditionally as a buffer load: a missing neighbour, a
     // padding column or an idle thread gets an offset past the descriptor's range, which the hardware
     // returns as zeros. With conditional loads the compiler could not count the loads in flight: the
@@ -353,13 +282,9 @@ k_gemm_bf16(GB g) {
 #pragma unroll
         for (int ks = 0; ks < KS; ++ks) {
           const int c0 = ks * 32 + ag * 8;
-          if constexpr (LU) {
-            dst[rt][ks] = *(const uint4*)&sA[(src >= 0 ? src : UC) * LA + c0];
-          } else {
-            unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
-            asm volatile("" : "+v"(off));   // keeps the select a select (else: one load per branch of a diamond)
-            dst[rt][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
-          }
+          unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
+          asm volatile("" : "+v"(off));   // keeps the select a select (else: one load per branch of a diamond)
+          dst[rt][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
         }
       }
     };
@@ -404,79 +329,7 @@ k_gemm_bf16(GB g) {
     }
     if (t < NK) step(t, a0, a1, bw0, bw1);
   };
-  // The union loop: A fragments are LDS reads, so a step is only its MFMAs + LDS reads, far shorter than an L2
-  // round trip for the weight tile — the tiles are fetched D-1 offsets ahead into a ring of D register sets.
-  // The loop is unrolled over all MAXK steps (guards on NK, uniform): every per-step value is then a register —
-  // the step's offset comes from a lane of kv by readlane, each lane's A address per step was formed in the
-  // prologue — so a step waits on no chain of dependent LDS reads (klist -> neighbour slot -> row: with them the
-  // union loop ran ~1200 clk per step, as slow per CU as the per-offset gathers it replaces).
-  auto unionloop = [&]() {
-    constexpr int D = BPT <= 2 ? 6 : (BPT <= 4 ? 4 : 2);
-    const int kv = klist[lane < NK ? lane : NK - 1];        // lane t: offset of step t (NK <= 27 < 64)
-    unsigned aoff[MAXK][RT];   // LDS byte offset of this lane's A row per step (a multiple of 64) | its chunk swizzle
-#pragma unroll
-    for (int t = 0; t < MAXK; ++t) {
-      const int k = __builtin_amdgcn_readlane(kv, t);
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt) {
-        const int src = sN[(arow + rt * 16) * MAXK + k], ss = src >= 0 ? src : UC;
-        aoff[t][rt] = (unsigned)(ss * LA) * 2u | (unsigned)(ss & (CH - 1));
-      }
-    }
-    uint4 bw[D][BPT], aa[2][RT][KS];
-    auto lda = [&](const unsigned (&off)[RT], uint4 (&dst)[RT][KS]) {
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          dst[rt][ks] = *(const uint4*)((const char*)sA + (off[rt] & ~63u) + (((ks * 4 + ag) ^ (off[rt] & 15u)) << 4));
-    };
-#pragma unroll
-    for (int j = 0; j < D - 1; ++j) load_b(__builtin_amdgcn_readlane(kv, j), bw[j]);
-    store_b(0, bw[0]);
-    lda(aoff[0], aa[0]);
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < MAXK; ++t) {
-      if (t < NK) {
-        load_b(__builtin_amdgcn_readlane(kv, t + D - 1 < MAXK ? t + D - 1 : MAXK - 1), bw[(t + D - 1) % D]);
-        if (t + 1 < MAXK) lda(aoff[t + 1 < MAXK ? t + 1 : t], aa[(t + 1) & 1]);
-        const int k = __builtin_amdgcn_readlane(kv, t);
-        if ((my >> k) & 1u) {
-          const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
-#pragma unroll
-          for (int ks = 0; ks < KS; ++ks) {
-#pragma unroll
-            for (int n = 0; n < NT; ++n) {
-              const uint4 bv = *(const uint4*)(bb + n * 16 * LS + ks * 32);
-#pragma unroll
-              for (int rt = 0; rt < RT; ++rt) acc[rt][n] = mfma16<F16>(aa[t & 1][rt][ks], bv, acc[rt][n]);
-            }
-          }
-        }
-        store_b((t + 1) & 1, bw[(t + 1) % D]);
-        __syncthreads();
-      }
-    }
-  };
-  if (NK > 0) {
-    if constexpr (UNI) {
-      if (uni) unionloop();
-      else mainloop(std::false_type{});
-    } else {
-      mainloop(std::false_type{});
-    }
-  }
-  if (UNI && g.dbg && tid == 0) {
-    const long long t3 = (long long)__builtin_amdgcn_s_memtime();
-    long long* d = g.dbg + (long long)lb * 8;
-    d[0] = tdbg0;
-    d[1] = tdbg1;
-    d[2] = t3;
-    d[3] = NK;
-    d[4] = ucnt;
-    d[5] = uni;
-  }
+  if (NK > 0) mainloop();
 
   // epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + reg (16x16 shapes, gfx950)
   // E_DGRAD: per output tile n, the previous layer's z of the lane's 4 rows and the column's BatchNorm
@@ -926,24 +779,22 @@ __global__ __launch_bounds__(wg_threads(CI, CO), (CI * CO <= 32 * 32) ? 4 : 1) v
   }
 }
 
-template <int KGP, int NT, bool UNI>
+template <int KGP, int NT>
 static void launch_k(int epi, const GB& a, int n_rows, hipStream_t st) {
-  constexpr int RT = rt_of(KGP, NT), GW = UNI ? gw_u(KGP, NT) : gw_of(KGP, NT), GBM = 16 * RT * GW;
+  constexpr int RT = rt_of(KGP, NT), GW = gw_of(KGP, NT), GBM = 16 * RT * GW;
   const int nblk = (n_rows + GBM - 1) / GBM;
   if (a.fmt == 1)   // fp16 operands: forward GEMMs only (checked by gemm_bf16_launch)
-    hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, true, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else if (epi == E_RES) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_RES, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
-  else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN, false, UNI>), dim3(nblk), dim3(64 * GW), 0, st, a);
+    hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD, true>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_FWD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_FWD>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_DGRAD) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_DGRAD>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else if (epi == E_RES) hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_RES>), dim3(nblk), dim3(64 * GW), 0, st, a);
+  else hipLaunchKernelGGL((k_gemm_bf16<KGP, NT, E_PLAIN>), dim3(nblk), dim3(64 * GW), 0, st, a);
 }
 
 static int launch(int KGP, int NT, int epi, const GB& a, int n_rows, hipStream_t st) {
-  const bool uni = a.lnbr != nullptr;
 #define C2(kg, nt)                                          \
   if (KGP == kg && NT == nt) {                              \
-    if (uni) launch_k<kg, nt, true>(epi, a, n_rows, st);    \
-    else launch_k<kg, nt, false>(epi, a, n_rows, st);       \
+    launch_k<kg, nt>(epi, a, n_rows, st);                   \
     return RPC_OK;                                          \
   }
   C2(32, 1) C2(32, 2) C2(32, 4) C2(64, 2) C2(64, 4) C2(64, 8) C2(128, 4) C2(32, 8) C2(64, 1) C2(128, 2) C2(128, 8)
@@ -1087,49 +938,19 @@ extern "C" int rpc_spconv_gemm_h16(const void* a, int fmt, int n_src, int kg, co
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
 }
 
-extern "C" int rpc_spconv_gemm_debug(long long* buf) {   // diagnostics (not in the header): phase timestamps
-  g_gemm_dbg = buf;
-  return 0;
-}
-
-static void set_union(GB& g, const RpcRowUnion* un) {
-  g.dbg = g_gemm_dbg;
-  if (un && un->lnbr) {
-    g.lnbr = un->lnbr;
-    g.ulist = un->ulist;
-    g.ucnt = un->ucnt;
-  }
-}
-
-// the general form: operand format fmt (fp16: forward only) and the map's per-block source-row unions (un, from
-// rpc_rulebook_union of the same map; NULL = every gather from global memory)
-extern "C" int rpc_spconv_gemm_ex(const void* a, int fmt, int n_src, int kg, const int* map, int kvol, int rev,
-                                  const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out,
-                                  const float* prev_z, const float* prev_bn, float* part, int epi, void* stream) {
-  if (un && un->lnbr && (!un->ulist || !un->ucnt)) return RPC_ERR_ARG;
-  GB g;
-  memset(&g, 0, sizeof(g));
-  g.fmt = fmt;
-  set_union(g, un);
-  return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, out, prev_z, prev_bn, part, epi, stream);
-}
-
 // the data gradient into a basicblock's output rows with rpc_sparse_res_backward fused into its epilogue:
 // m = (dgrad + g2) * [out > 0] -> m [n_out][ng] fp32, and the BatchNorm-backward partial rows (sum m,
 // sum m * (z - mean) * invstd) of that layer (bn: scale, beta, mean, invstd) -> part [gemm blocks][2 * ng]
 extern "C" int rpc_spconv_gemm_res(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
-                                   const RpcRowUnion* un, int n_out, const void* bt, int ng, float* m, const float* g2,
-                                   const float* out, const float* z, const float* bn, float* part,
-                                   const RpcBnFin* fin, void* stream) {
+                                   int n_out, const void* bt, int ng, float* m, const float* g2, const float* out,
+                                   const float* z, const float* bn, float* part, const RpcBnFin* fin, void* stream) {
   if (!m || !out || !z || !bn || !part) return RPC_ERR_ARG;
-  if (un && un->lnbr && (!un->ulist || !un->ucnt)) return RPC_ERR_ARG;
   if (fin && (fin->mode != 1 || !fin->ticket || !fin->gpart || !fin->gamma || !fin->fbn || !fin->bn || ng > 256 ||
               n_out <= 0))
     return RPC_ERR_ARG;
   GB g;
   memset(&g, 0, sizeof(g));
   if (fin) g.fin = *fin;   // + that layer's BatchNorm-backward finalize (mode 1) in the last-arriving blocks
-  set_union(g, un);
   g.eg2 = g2;
   g.eout = out;
   return gemm_bf16_launch(g, a, n_src, kg, map, kvol, rev, n_out, bt, ng, m, z, bn, part, E_RES, stream);
@@ -1141,13 +962,11 @@ extern "C" int rpc_bn_fin_tickets(int n_out) { return 1 + rpc_bn_fin_groups(n_ou
 
 // the data gradient (epi 1) with the BatchNorm-backward finalize of the layer whose ReLU mask it applies fused in
 extern "C" int rpc_spconv_gemm_bf16_fin(const void* a, int n_src, int kg, const int* map, int kvol, int rev,
-                                        const RpcRowUnion* un, int n_out, const void* bt, int ng, float* out,
-                                        const float* prev_z, const float* prev_bn, float* part, int epi,
-                                        const RpcBnFin* fin, void* stream) {
-  if (un && un->lnbr && (!un->ulist || !un->ucnt)) return RPC_ERR_ARG;
+                                        int n_out, const void* bt, int ng, float* out, const float* prev_z,
+                                        const float* prev_bn, float* part, int epi, const RpcBnFin* fin,
+                                        void* stream) {
   GB g;
   memset(&g, 0, sizeof(g));
-  set_union(g, un);
   if (fin) {
     if (epi != 1 || !part || !fin->ticket || !fin->gpart || !fin->gamma || !fin->bn || !fin->fbn || fin->mode != 1 ||
         ng > 256 || n_out <= 0)

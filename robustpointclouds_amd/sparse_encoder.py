@@ -71,37 +71,8 @@ FUSED_FINALIZE = os.environ.get("RPC_SPARSE_FUSED_FIN", "1") != "0"
 # tests/test_gpu_sparse_layers.py). fp16 MFMA runs at the bf16 rate; the normalised activations and the
 # weights sit far inside its range (the dz rows, which would need loss scaling in fp16, stay bf16)
 FWD_FMT = 0 if os.environ.get("RPC_SPARSE_FWD_BF16", "0") != "0" else 1
-# r05: the 16-bit GEMMs gather each 128-row block's distinct source rows into LDS once (rpc_rulebook_union,
-# built with the rulebooks on their side stream) instead of one gather round trip per kernel offset.
-# RPC_SPARSE_UNION=0: every gather from global memory (A/B; same results). (r04's neighbour-mask row order,
-# RPC_SPARSE_PERM, measured slower and was removed: profiles/r04_perm_ab.txt)
-UNION = os.environ.get("RPC_SPARSE_UNION", "1") != "0"
-
-
-class _Union:
-    """Per-block source-row unions of one rulebook map [n][K] (rpc_rulebook_union) and the RpcRowUnion
-    descriptor the GEMM entry points take."""
-
-    def __init__(self, lib, nbr, st, dev):
-        n, K = nbr.shape
-        nb = max(lib.rpc_rulebook_union_blocks(n), 1)
-        self.lnbr = torch.empty((n, K), dtype=torch.int16, device=dev)      # u16 slots
-        self.ulist = torch.empty((nb, RPC_UNION_CAP), dtype=torch.int32, device=dev)
-        self.ucnt = torch.empty(nb, dtype=torch.int32, device=dev)
-        _ffi.check(lib.rpc_rulebook_union(_ffi.ptr(nbr), n, K, _ffi.ptr(self.lnbr), _ffi.ptr(self.ulist),
-                                          _ffi.ptr(self.ucnt), st), "rpc_rulebook_union")
-        self.c = _ffi.RpcRowUnion(self.lnbr.data_ptr(), self.ulist.data_ptr(), self.ucnt.data_ptr())
-
-    def tensors(self):
-        return (self.lnbr, self.ulist, self.ucnt)
-
-
-RPC_UNION_CAP = 512   # include/rpc_hip.h
-
-
-def _uref(u):
-    """the ctypes argument for an optional _Union"""
-    return _ffi.C.byref(u.c) if u is not None else None
+# (r04's neighbour-mask row order and r05's per-block source-row unions staged in LDS were measured slower on the
+# metric's step and removed: profiles/r04_perm_ab.txt, profiles/r05_union_ab.txt)
 
 
 def _t3(v):
@@ -525,22 +496,11 @@ class _RulebookPlan:
                     _ffi.check(lib.rpc_subm_rulebook(_ffi.ptr(cur_coors), cur_n, shp, _ffi.int_arr(sp.ksize),
                                                      _ffi.ptr(enc.grid(sp.lvl_in, B, dev)), _ffi.ptr(nbr), st),
                                "rpc_subm_rulebook")
-                    un = self._union(nbr, st)
-                    self.rb[sp.key] = (nbr, un)
-                    made += [nbr] + (list(un.tensors()) if un is not None else [])
-                nbr, un = self.rb[sp.key]
-                # (a submanifold map's transpose (rev) names the same source rows per row: one union serves the
-                # forward and the data gradient)
-                self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr, n_out=cur_n, coors_out=cur_coors,
-                                    un=un, un_in=un), made)
+                    self.rb[sp.key] = nbr
+                    made.append(nbr)
+                nbr = self.rb[sp.key]
+                self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr, n_out=cur_n, coors_out=cur_coors), made)
                 self.next += 1
-
-    def _union(self, nbr, st):
-        """The map's per-block source-row unions (on the side stream), or None (16-bit GEMMs only;
-        RPC_SPARSE_UNION=0)."""
-        if not (UNION and self.enc.bf16) or nbr.shape[0] == 0:
-            return None
-        return _Union(self.lib, nbr, st, self.dev)
 
     def get(self, li):
         if self.plan[li] is None:
@@ -562,11 +522,8 @@ class _RulebookPlan:
                                                          _ffi.int_arr(sp.pad), _ffi.ptr(gout), n_out,
                                                          _ffi.ptr(coors_out), _ffi.ptr(nbr_out), _ffi.ptr(nbr_in),
                                                          _ffi.ptr(ws), st), "rpc_spconv_rulebook_build")
-                un_out, un_in = self._union(nbr_out, st), self._union(nbr_in, st)
             self._done(li, dict(n_in=cur_n, coors_in=cur_coors, nbr=nbr_out, nbr_in=nbr_in, n_out=n_out,
-                                coors_out=coors_out, un=un_out, un_in=un_in),
-                       [coors_out, nbr_out, nbr_in] + [t for u in (un_out, un_in) if u is not None
-                                                       for t in u.tensors()])
+                                coors_out=coors_out), [coors_out, nbr_out, nbr_in])
             self.pending = None
             self.cur = (coors_out, n_out)
             self.next = li + 1
@@ -612,7 +569,7 @@ class SparseEncoderFn(torch.autograd.Function):
             bnm = m[1]
             p = plan.get(li)
             rec = dict(spec=sp, n_in=p["n_in"], src=src, src_bn=src_bn, coors_in=p["coors_in"], nbr=p["nbr"],
-                       n_out=p["n_out"], coors_out=p["coors_out"], un=p.get("un"), un_in=p.get("un_in"))
+                       n_out=p["n_out"], coors_out=p["coors_out"])
             if "nbr_in" in p:
                 rec["nbr_in"] = p["nbr_in"]
             main.wait_event(p["ev"])
@@ -628,9 +585,9 @@ class SparseEncoderFn(torch.autograd.Function):
             if rec["bf16"]:
                 bt, rec["btd"] = wtiles[li]
                 e0 = enc.timer.start() if tm else None
-                _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
-                                                  sp.K, 0, _uref(rec["un"]), n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z),
-                                                  None, None, _ffi.ptr(part), 0, st), "rpc_spconv_gemm_ex")
+                _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(hsrc), fmt, hsrc.shape[0], sp.ci, _ffi.ptr(rec["nbr"]),
+                                                   sp.K, 0, n_out, _ffi.ptr(bt), sp.co, _ffi.ptr(z), None, None,
+                                                   _ffi.ptr(part), 0, st), "rpc_spconv_gemm_h16")
             else:
                 e0 = enc.timer.start() if tm else None
                 _ffi.check(lib.rpc_spconv_forward(_ffi.ptr(src), _ffi.ptr(src_bn), sp.ci, _ffi.ptr(rec["nbr"]), sp.K,
@@ -837,16 +794,16 @@ class SparseEncoderFn(torch.autograd.Function):
                 pp = torch.empty((nb, 2 * sp.ci), dtype=torch.float32, device=dev)
                 gid = G[li - 1][0] if G[li - 1] else None
                 _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(dzb), dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev,
-                                                   _uref(rec["un_in"]), n_in, _ffi.ptr(btd), sp.ci, _ffi.ptr(din),
+                                                   n_in, _ffi.ptr(btd), sp.ci, _ffi.ptr(din),
                                                    _ffi.ptr(gid), _ffi.ptr(prev["out"]), _ffi.ptr(prev["z"]),
                                                    _ffi.ptr(prev["bn"]), _ffi.ptr(pp), None, st), "rpc_spconv_gemm_res")
                 prev["res_m"], prev["res_part"] = din, pp
             elif li > 0 and L[li - 1]["spec"].mat:
                 # the input is a materialised output: plain data gradient, masked by its own backward
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _uref(rec["un_in"]), n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
-                               "rpc_spconv_gemm_ex(dgrad)")
+                               "rpc_spconv_gemm_h16(dgrad)")
                 else:
                     _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
@@ -858,10 +815,10 @@ class SparseEncoderFn(torch.autograd.Function):
                 part = torch.empty((nblk, 2 * sp.ci), dtype=torch.float32, device=dev)
                 epi = 1
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _uref(rec["un_in"]), n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), _ffi.ptr(prev["z"]),
                                                         _ffi.ptr(prev["bn"]), _ffi.ptr(part), 1, st),
-                               "rpc_spconv_gemm_ex(dgrad)")
+                               "rpc_spconv_gemm_h16(dgrad)")
                 else:
                     _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci,
@@ -870,9 +827,9 @@ class SparseEncoderFn(torch.autograd.Function):
                 dy = din
             elif ctx.needs_input_grad[0]:
                 if rec["bf16"]:
-                    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, _uref(rec["un_in"]), n_in,
+                    _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(dzb), 0, dzb.shape[0], sp.co, _ffi.ptr(mp), sp.K, rev, n_in,
                                                         _ffi.ptr(btd), sp.ci, _ffi.ptr(din), None, None, None, 2, st),
-                               "rpc_spconv_gemm_ex(dgrad)")
+                               "rpc_spconv_gemm_h16(dgrad)")
                 else:
                     _ffi.check(lib.rpc_spconv_dgrad(_ffi.ptr(dy), _ffi.ptr(rec["z"]), _ffi.ptr(bnb), sp.co,
                                                     _ffi.ptr(mp), sp.K, rev, n_in, _ffi.ptr(rec["W"]), sp.ci, None,
@@ -915,7 +872,6 @@ def _native_backward(ctx, gdense):
     grads = []
     table = (_ffi.RpcSparseLayer * nl)()
     vp = lambda t: None if t is None else t.data_ptr()
-    up = lambda u: _ffi.C.pointer(u.c) if u is not None else None
     for li, rec in enumerate(L):
         sp = rec["spec"]
         dW = parts[3 * li].view(rec["W"].shape)
@@ -933,7 +889,6 @@ def _native_backward(ctx, gdense):
             vp(rec["h_in"]) if bf else None, None if bf else vp(rec["src"]), None if bf else vp(rec["src_bn"]),
             vp(rec["W"]), vp(rec["gamma"]), vp(rec["beta"]), vp(rec.get("btd")) if bf else None,
             dW.data_ptr(), dg.data_ptr(), db.data_ptr(), int(rec.get("h_fmt", 0)),
-            up(rec.get("un")) if bf else None, up(rec.get("un_in")) if bf else None,
             ctx.enc.fin_ticket_ptr(dev, nl + li, rec["n_in"]) if bf and FUSED_FINALIZE else None)
     dfeat = (torch.empty((L[0]["n_in"], L[0]["spec"].ci), dtype=torch.float32, device=dev)
              if ctx.needs_input_grad[0] else None)

@@ -1,13 +1,8 @@
-"""The sparse 16-bit GEMM's union path (csrc/spconv_bf16.hip k_gemm_bf16<..., UNI>: each 128-row block gathers
-the distinct source rows of its map entries — rpc_rulebook_union — into LDS once) against the regular path
-(one gather round trip per kernel offset): the same MFMAs in the same order per accumulator, so outputs and
-BatchNorm partial rows must be BIT-identical — for every (GEMM K, output width) instantiation, the epilogues,
-ragged row counts (1, 15, 17, 129 rows: partial waves and blocks), offsets nobody uses, blocks whose rows have no
-neighbour at all, blocks whose union overflows the LDS capacity (they take the regular gathers inside the same
-kernel), and the real SECOND rulebooks of a synthetic KITTI batch (whole bf16 SparseEncoder forward + backward).
-Also: the union lists themselves, the fused BatchNorm finalizes of the data gradients, and the basicblock
-residual backward (alone and fused into the data-gradient epilogue)."""
-import numpy as np
+"""The sparse 16-bit GEMM's BatchNorm finalize fused into the data-gradient launches (rpc_spconv_gemm_bf16_fin)
+against the separate finalize, on random maps and on the real SECOND rulebooks of a synthetic KITTI batch (whole
+bf16 SparseEncoder forward + backward), and the basicblock residual backward (alone, at every width, and fused
+into the data-gradient epilogue). (r05's per-block source-row union path, bit-identical but slower, was removed:
+profiles/r05_union_ab.txt.)"""
 import pytest
 import torch
 
@@ -15,105 +10,20 @@ from robustpointclouds_amd import _ffi
 
 pytestmark = pytest.mark.gpu
 
-# (gemm K = gathered row width, gemm N = output width): every launch shape of the 16-bit GEMM
-SHAPES = [(16, 16), (32, 16), (32, 32), (16, 32), (32, 64), (64, 32), (64, 64), (64, 128), (128, 64),
-          (128, 128), (32, 128), (64, 16), (128, 32), (24, 32), (40, 64)]
-UNION_CAP = 512   # include/rpc_hip.h RPC_UNION_CAP
-
 
 def _r8(c):
     return (c + 7) // 8 * 8
 
 
-class _U:
-    def __init__(self, lib, nbr):
-        n, K = nbr.shape
-        nb = max(lib.rpc_rulebook_union_blocks(n), 1)
-        dev = nbr.device
-        self.lnbr = torch.full((n, K), -2, dtype=torch.int16, device=dev)
-        self.ulist = torch.full((nb, UNION_CAP), -7, dtype=torch.int32, device=dev)
-        self.ucnt = torch.full((nb,), -1, dtype=torch.int32, device=dev)
-        _ffi.check(lib.rpc_rulebook_union(_ffi.ptr(nbr), n, K, _ffi.ptr(self.lnbr), _ffi.ptr(self.ulist),
-                                          _ffi.ptr(self.ucnt), _ffi.stream_of(nbr)), "rpc_rulebook_union")
-        self.c = _ffi.RpcRowUnion(self.lnbr.data_ptr(), self.ulist.data_ptr(), self.ucnt.data_ptr())
-
-    def ref(self):
-        return _ffi.C.byref(self.c)
-
-
-def _run(lib, un, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev):
+def _run(lib, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev):
     out = torch.full((n_out, ng), float("nan"), device=dev)
     nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
     part = torch.full((nblk, 2 * ng), float("nan"), device=dev) if epi != 2 else None
-    _ffi.check(lib.rpc_spconv_gemm_ex(_ffi.ptr(a), 0, n_src, kg, _ffi.ptr(nbr), K, rev,
-                                      un.ref() if un is not None else None, n_out, _ffi.ptr(bt), ng, _ffi.ptr(out),
-                                      _ffi.ptr(ez), _ffi.ptr(ebn), _ffi.ptr(part), epi, _ffi.stream_of(out)),
-               "rpc_spconv_gemm_ex")
+    _ffi.check(lib.rpc_spconv_gemm_h16(_ffi.ptr(a), 0, n_src, kg, _ffi.ptr(nbr), K, rev, n_out, _ffi.ptr(bt), ng,
+                                       _ffi.ptr(out), _ffi.ptr(ez), _ffi.ptr(ebn), _ffi.ptr(part), epi,
+                                       _ffi.stream_of(out)), "rpc_spconv_gemm_h16")
     torch.cuda.synchronize()
     return out, part
-
-
-@pytest.mark.parametrize("n,K,n_src", [(5000, 27, 300), (5000, 27, 100000), (129, 27, 50), (1, 27, 5), (7000, 3, 9000),
-                                       (128, 27, 20000)])
-def test_union_lists(n, K, n_src):
-    """rpc_rulebook_union: per 128-row block, ulist[:ucnt] holds distinct rows, every valid entry's slot names its
-    own source (ulist[block][lnbr[r, k]] == nbr[r, k]), absent entries are 0xFFFF, ucnt is the exact distinct
-    count (blocks past the LDS capacity included: their slots are not used)."""
-    lib = _ffi.load()
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(n + K + n_src)
-    nbr = torch.randint(0, n_src, (n, K), generator=g, dtype=torch.int32)
-    nbr[torch.rand((n, K), generator=g) > 0.35] = -1
-    u = _U(lib, nbr.to(dev))
-    torch.cuda.synchronize()
-    ln = u.lnbr.cpu().numpy().view(np.uint16).astype(np.int64)
-    ul, uc = u.ulist.cpu().numpy(), u.ucnt.cpu().numpy()
-    nb = nbr.numpy()
-    for b in range(ul.shape[0]):
-        rows = nb[b * 128:(b + 1) * 128]
-        want = np.unique(rows[rows >= 0])
-        assert uc[b] == len(want), b
-        lb = ln[b * 128:(b + 1) * 128]
-        assert np.all(lb[rows < 0] == 0xFFFF)
-        if uc[b] <= UNION_CAP:
-            lst = ul[b, :uc[b]]
-            assert np.array_equal(np.sort(lst), want)
-            assert np.array_equal(lst[lb[rows >= 0]], rows[rows >= 0])
-
-
-@pytest.mark.parametrize("kg,ng", SHAPES)
-@pytest.mark.parametrize("n_out,K,rev,n_src", [(5000, 27, 0, 300), (5000, 27, 1, 60000), (129, 27, 1, 200),
-                                               (17, 3, 0, 3000), (15, 27, 0, 40), (1, 27, 1, 3000)])
-def test_union_gemm_bit_identical(kg, ng, n_out, K, rev, n_src):
-    """The union path equals the regular gathers bit for bit (outputs and partial rows, all three epilogues);
-    n_src 60000 makes most blocks overflow the LDS capacity (regular gathers inside the union kernel), n_src
-    300 / 200 / 40 keeps every block in LDS."""
-    lib = _ffi.load()
-    dev = torch.device("cuda")
-    g = torch.Generator().manual_seed(kg * 131 + ng * 7 + n_out + K + n_src)
-    nbr = torch.randint(0, n_src, (n_out, K), generator=g, dtype=torch.int32)
-    nbr[torch.rand((n_out, K), generator=g) > 0.35] = -1
-    if K > 2:
-        nbr[:, 1] = -1                      # an offset nobody uses
-    if n_out > 300:
-        nbr[128:256] = -1                   # a whole block of rows with no neighbour
-    a = torch.zeros((n_src, _r8(kg)), dtype=torch.bfloat16)
-    a[:, :kg] = torch.randn((n_src, kg), generator=g).to(torch.bfloat16)
-    W = torch.randn((K, kg, ng), generator=g) * 0.1
-    a, nbr, W = a.to(dev), nbr.to(dev), W.to(dev)
-    bt = torch.empty(lib.rpc_spconv_bf16_weight_elems(K, kg, ng, 0), dtype=torch.bfloat16, device=dev)
-    _ffi.check(lib.rpc_spconv_prep_weight_bf16(_ffi.ptr(W), K, kg, ng, 0, _ffi.ptr(bt), _ffi.stream_of(bt)), "prep")
-    ez = torch.randn((n_out, ng), generator=g).to(dev)
-    ebn = torch.cat([torch.rand(ng, generator=g) + 0.5, torch.randn(ng, generator=g) * 0.1,
-                     torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
-    un = _U(lib, nbr)
-    for epi in (0, 1, 2):
-        ref_out, ref_part = _run(lib, None, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
-        assert torch.isfinite(ref_out).all()
-        out, part = _run(lib, un, a, n_src, kg, nbr, K, rev, n_out, bt, ng, epi, ez, ebn, dev)
-        assert torch.equal(out, ref_out), epi
-        if epi != 2:
-            assert torch.equal(part, ref_part), epi
 
 
 def _encoder_case():
@@ -131,10 +41,10 @@ def _encoder_case():
     return enc, feats, d["coors"]
 
 
-def _encoder_step(enc, feats, coors, union, fused, fmt=1):
+def _encoder_step(enc, feats, coors, fused, fmt=1):
     from robustpointclouds_amd import sparse_encoder as se
-    prev_u, prev_f, prev_fmt = se.UNION, se.FUSED_FINALIZE, se.FWD_FMT
-    se.UNION, se.FUSED_FINALIZE, se.FWD_FMT = union, fused, fmt
+    prev_f, prev_fmt = se.FUSED_FINALIZE, se.FWD_FMT
+    se.FUSED_FINALIZE, se.FWD_FMT = fused, fmt
     try:
         for p in enc.parameters():
             p.grad = None
@@ -151,21 +61,7 @@ def _encoder_step(enc, feats, coors, union, fused, fmt=1):
             b.running_var.copy_(v)
         return out.detach().float().clone(), f.grad.clone(), [p.grad.clone() for p in enc.parameters()], stats
     finally:
-        se.UNION, se.FUSED_FINALIZE, se.FWD_FMT = prev_u, prev_f, prev_fmt
-
-
-@pytest.mark.parametrize("fmt", [1, 0])
-def test_union_encoder_step_bit_identical(fmt):
-    """The perf-mode SparseEncoder forward + backward on a synthetic KITTI batch (the metric's rulebooks) with the
-    union path equals the one with per-offset gathers, bit for bit (dense BEV, every gradient, running stats) —
-    fp16 (default) and bf16 forward operands."""
-    enc, feats, coors = _encoder_case()
-    r0 = _encoder_step(enc, feats, coors, False, True, fmt)
-    r1 = _encoder_step(enc, feats, coors, True, True, fmt)
-    assert torch.equal(r0[0], r1[0])
-    assert torch.equal(r0[1], r1[1])
-    for a, b in zip(r0[2] + r0[3], r1[2] + r1[3]):
-        assert torch.equal(a, b)
+        se.FUSED_FINALIZE, se.FWD_FMT = prev_f, prev_fmt
 
 
 def test_fused_finalize_matches_separate_and_is_deterministic():
@@ -175,9 +71,9 @@ def test_fused_finalize_matches_separate_and_is_deterministic():
     flip a bf16 rounding or a ReLU mask downstream (relative L2 <= 5e-2 on the BEV, every gradient and the running
     statistics; measured 0: bit-identical on this case, r04)."""
     enc, feats, coors = _encoder_case()
-    ref = _encoder_step(enc, feats, coors, True, False)
-    a = _encoder_step(enc, feats, coors, True, True)
-    b = _encoder_step(enc, feats, coors, True, True)
+    ref = _encoder_step(enc, feats, coors, False)
+    a = _encoder_step(enc, feats, coors, True)
+    b = _encoder_step(enc, feats, coors, True)
     for x, y in zip([a[0], a[1]] + a[2] + a[3], [b[0], b[1]] + b[2] + b[3]):
         assert torch.equal(x, y)
     worst = 0.0
@@ -189,9 +85,9 @@ def test_fused_finalize_matches_separate_and_is_deterministic():
     assert int(enc.fin_tickets(feats.device).abs().sum().item()) == 0
 
 
-@pytest.mark.parametrize("kg,ng,n_out,union", [(64, 64, 106000, True), (32, 64, 5000, False), (64, 128, 130, True),
-                                               (128, 128, 64, True), (16, 32, 1, False)])
-def test_gemm_fin_entry_point(kg, ng, n_out, union):
+@pytest.mark.parametrize("kg,ng,n_out", [(64, 64, 106000), (32, 64, 5000), (64, 128, 130), (128, 128, 64),
+                                         (16, 32, 1)])
+def test_gemm_fin_entry_point(kg, ng, n_out):
     """rpc_spconv_gemm_bf16_fin alone (data gradient, epi 1): the same output rows as the unfused GEMM, the
     finalize outputs of rpc_bn_finalize mode 1 on the same partial rows (bnb, dgamma, dbeta) to
     double-summation-order accuracy, repeated launches reuse the re-armed tickets."""
@@ -215,7 +111,6 @@ def test_gemm_fin_entry_point(kg, ng, n_out, union):
     gpart = torch.empty(lib.rpc_bn_fin_groups(n_out) * 2 * ng, dtype=torch.float64, device=dev)
     nblk = lib.rpc_spconv_gemm_blocks(n_out)
     st = _ffi.stream_of(ez)
-    un = _U(lib, nbr) if union else None
     for rep in range(3):
         out = torch.full((n_out, ng), float("nan"), device=dev)
         part = torch.full((nblk, 2 * ng), float("nan"), device=dev)
@@ -223,11 +118,10 @@ def test_gemm_fin_entry_point(kg, ng, n_out, union):
         dg, db = torch.full((ng,), float("nan"), device=dev), torch.full((ng,), float("nan"), device=dev)
         fin = _ffi.RpcBnFin(ticket.data_ptr(), gpart.data_ptr(), 1, gamma.data_ptr(), beta.data_ptr(), 1e-3, 0.01,
                             None, None, ebn.data_ptr(), bn.data_ptr(), dg.data_ptr(), db.data_ptr())
-        _ffi.check(lib.rpc_spconv_gemm_bf16_fin(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0,
-                                                un.ref() if un is not None else None, n_out, _ffi.ptr(bt), ng,
+        _ffi.check(lib.rpc_spconv_gemm_bf16_fin(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, n_out, _ffi.ptr(bt), ng,
                                                 _ffi.ptr(out), _ffi.ptr(ez), _ffi.ptr(ebn), _ffi.ptr(part), 1,
                                                 _ffi.C.byref(fin), st), "rpc_spconv_gemm_bf16_fin")
-        ref_out, ref_part = _run(lib, None, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 1, ez, ebn, dev)
+        ref_out, ref_part = _run(lib, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 1, ez, ebn, dev)
         assert torch.equal(out, ref_out)
         assert torch.equal(part, ref_part)
         rbn = torch.full((5 * ng,), float("nan"), device=dev)
@@ -268,28 +162,22 @@ def test_gemm_res_matches_separate_residual_backward(kg, ng, n_out, K, g2):
                     torch.randn(ng, generator=g) * 0.1, torch.rand(ng, generator=g) + 0.5]).to(dev)
     nblk = max(lib.rpc_spconv_gemm_blocks(n_out), 1)
     # separate: plain GEMM, then the residual pass
-    din, _ = _run(lib, None, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 2, None, None, dev)
+    din, _ = _run(lib, a, n_src, kg, nbr, K, 0, n_out, bt, ng, 2, None, None, dev)
     m_ref = torch.full((n_out, ng), float("nan"), device=dev)
     p_ref = torch.full((nblk, 2 * ng), float("nan"), device=dev)
     _ffi.check(lib.rpc_sparse_res_backward(_ffi.ptr(gid) if g2 else _ffi.ptr(din), _ffi.ptr(din) if g2 else None,
                                            _ffi.ptr(out), _ffi.ptr(z), _ffi.ptr(bn), n_out, ng, _ffi.ptr(m_ref),
                                            _ffi.ptr(p_ref), st), "rpc_sparse_res_backward")
-    # fused, per-offset gathers and the union path (same bits)
-    un = _U(lib, nbr)
-    for u in (None, un):
-        m = torch.full((n_out, ng), float("nan"), device=dev)
-        p = torch.full((nblk, 2 * ng), float("nan"), device=dev)
-        _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, u.ref() if u else None, n_out,
-                                           _ffi.ptr(bt), ng, _ffi.ptr(m), _ffi.ptr(gid) if g2 else None, _ffi.ptr(out),
-                                           _ffi.ptr(z), _ffi.ptr(bn), _ffi.ptr(p), None, st), "rpc_spconv_gemm_res")
-        torch.cuda.synchronize()
-        assert torch.equal(m, m_ref)
-        if u is None:
-            p0 = p
-        else:
-            assert torch.equal(p, p0)
-        scale = torch.cat([m.abs().sum(0), (m * ((z - bn[2 * ng:3 * ng]) * bn[3 * ng:])).abs().sum(0)])
-        assert torch.all((p.sum(0) - p_ref.sum(0)).abs() <= 1e-5 * scale + 1e-6)
+    # fused
+    m = torch.full((n_out, ng), float("nan"), device=dev)
+    p = torch.full((nblk, 2 * ng), float("nan"), device=dev)
+    _ffi.check(lib.rpc_spconv_gemm_res(_ffi.ptr(a), n_src, kg, _ffi.ptr(nbr), K, 0, n_out, _ffi.ptr(bt), ng,
+                                       _ffi.ptr(m), _ffi.ptr(gid) if g2 else None, _ffi.ptr(out), _ffi.ptr(z),
+                                       _ffi.ptr(bn), _ffi.ptr(p), None, st), "rpc_spconv_gemm_res")
+    torch.cuda.synchronize()
+    assert torch.equal(m, m_ref)
+    scale = torch.cat([m.abs().sum(0), (m * ((z - bn[2 * ng:3 * ng]) * bn[3 * ng:])).abs().sum(0)])
+    assert torch.all((p.sum(0) - p_ref.sum(0)).abs() <= 1e-5 * scale + 1e-6)
 
 
 @pytest.mark.parametrize("c", [16, 48, 64, 96, 128, 200])

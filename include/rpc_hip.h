@@ -197,10 +197,12 @@ int rpc_spconv_wgrad(const float* in, const float* in_bn, int ci, const int* nbr
                      void* workspace, size_t workspace_bytes, void* stream);
 /* BatchNorm1d finalize from partial sums. mode 0: bn_out = scale, shift, mean, invstd and the
  * running stats update (train). mode 1: bn_out = gi, m1, m2, mean, invstd for the backward and
- * dgamma = sum dy*xhat, dbeta = sum dy. One block per channel, no cross-block step: the
- * workspace is unused (size 0; may be NULL) and kept for signature stability. */
+ * dgamma = sum dy*xhat, dbeta = sum dy. mode | RPC_BN_PART_F64: part holds double rows (the fp32
+ * parity engine's rpc_dense_bnbwd_stats_f32), else float rows. One block per channel, no cross-block
+ * step: the workspace is unused (size 0; may be NULL) and kept for signature stability. */
+#define RPC_BN_PART_F64 4
 size_t rpc_bn_finalize_workspace_size(int c);
-int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const float* gamma,
+int rpc_bn_finalize(const void* part, int nblk, int c, int n, int mode, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean, float* running_var,
                     const float* fwd_bn, float* bn_out, float* dgamma, float* dbeta, void* workspace,
                     void* stream);
@@ -452,7 +454,7 @@ int rpc_dense_wgrad_f32(int map, int kind, const float* x, int x_pitch, int ci, 
 int rpc_dense_bn_apply_f32(const float* z, int m, int c, const float* bn, float* out, int out_pitch, int out_offset,
                            void* stream);
 int rpc_dense_bnbwd_stats_f32(const float* dh, int dh_pitch, int dh_offset, const float* z, int m, int c,
-                              const float* bn, float* part, void* stream);
+                              const float* bn, double* part, void* stream);
 int rpc_dense_bnbwd_apply_f32(const float* dh, int dh_pitch, int dh_offset, const float* z, int m, int c,
                               const float* bn, const float* bnb, float* dz, void* stream);
 int rpc_dense_wprep_batch_f32(const RpcDenseWprep* descs, int n, void* stream);

@@ -79,6 +79,15 @@ def _bf16(t):
     return t.to(torch.bfloat16).to(t.dtype)
 
 
+def _match(c_to, c_from, rows):
+    """rows given in the order of coordinates c_from, reordered to the order of c_to (the same coordinate set)"""
+    kf, kt = _keys(c_from, (1 << 8, 1 << 8, 1 << 12, 1 << 12)), _keys(c_to, (1 << 8, 1 << 8, 1 << 12, 1 << 12))
+    order = np.argsort(kf)
+    pos = order[np.searchsorted(kf, kt, sorter=order)]
+    assert np.array_equal(kf[pos], kt)
+    return rows[pos]
+
+
 def _fp16(t):
     return t.to(torch.float16).to(t.dtype)
 
@@ -132,7 +141,12 @@ class OracleSparseEncoder:
                                     rm=m[1].running_mean.detach().cpu().to(dtype).clone(),
                                     rv=m[1].running_var.detach().cpu().to(dtype).clone()))
 
-    def forward(self, feats, coors, B, keep=False):
+    def forward(self, feats, coors, B, keep=False, masks=None):
+        """masks (optional): per layer (coors, bool [n, co]) — the ReLU decisions of the implementation under test,
+        rows matched here by coordinates; the layer's output is then (pre [+ identity]) * mask instead of relu(...):
+        float64 arithmetic on the implementation's own branch of the piecewise-linear encoder. A pre-activation
+        within an fp32 rounding of 0 lands on either side in fp32; evaluated on the other branch, one such element
+        moved every gradient below its layer by ~1e-3 (tests/test_gpu_sparse_layers.py)."""
         x = torch.as_tensor(feats).to(self.dtype)
         c = np.asarray(coors, np.int64)
         cache = {}
@@ -165,7 +179,12 @@ class OracleSparseEncoder:
                 pre.retain_grad()
                 self.trace.append((c_out, z, pre))
             res = getattr(sp, "res", -1)
-            x = torch.relu(pre + outs[res]) if res >= 0 else torch.relu(pre)   # SparseBasicBlock: + identity
+            act = pre + outs[res] if res >= 0 else pre                         # SparseBasicBlock: + identity
+            if masks is not None:
+                mc, mm = masks[li]
+                x = act * torch.from_numpy(_match(c_out, np.asarray(mc), np.asarray(mm))).to(self.dtype)
+            else:
+                x = torch.relu(act)
             outs.append(x)
             c = c_out
         D, H, W = self.shapes[-1]
@@ -175,3 +194,21 @@ class OracleSparseEncoder:
                torch.from_numpy(c[:, 3]))
         dense = dense.index_put(idx, x)
         return dense.permute(0, 4, 1, 2, 3).reshape(B, C * D, H, W)
+
+
+def implementation_masks(debug):
+    """The ReLU decisions of the HIP SparseEncoder from its debug trace (SparseEncoder.debug: per layer (layer,
+    coors, z, dy, bn, out)), for OracleSparseEncoder.forward(masks=...): out > 0 for materialised layers (the
+    kernel's own relu(bn(z) + identity)), else the kernels' fmaxf(fmaf(z - mean, scale, beta), 0) > 0 — z - mean
+    rounded in fp32 as the kernel does, the fused multiply-add's sign that of its exact value (exact in float64)."""
+    masks = []
+    for li, c, z, dy, bn, out in sorted(debug, key=lambda t: t[0]):
+        if out is not None:
+            m = (out > 0).numpy()
+        else:
+            C = z.shape[1]
+            a = (z.float() - bn[2 * C:3 * C].float()).double()
+            m = (a * bn[:C].float().double() + bn[C:2 * C].float().double() > 0).numpy()
+        masks.append((c, m))
+    return masks
+

@@ -2160,17 +2160,19 @@ __global__ __launch_bounds__(BLK) void k_bn_apply(const E* __restrict__ z, int M
   }
 }
 
-// BatchNorm-backward partial sums: dm = dh * [pre > 0]; part[blk] = (sum dm, sum dm * xhat)
-template <typename E>
+// BatchNorm-backward partial sums: dm = dh * [pre > 0]; part[blk] = (sum dm, sum dm * xhat).
+// A: the accumulator and partial-row type — float for the bf16 engine; double for the fp32 (parity)
+// engine, whose sums over sparse BEV images cancel (rpc_bn_finalize mode 1 | RPC_BN_PART_F64 reads them)
+template <typename E, typename A>
 __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const E* __restrict__ dh, int DP, int DOFF,
                                                      const E* __restrict__ z, int M, int C,
-                                                     const float* __restrict__ bn, float* __restrict__ part) {
-  __shared__ float sh[2][BLK * 8];
+                                                     const float* __restrict__ bn, A* __restrict__ part) {
+  __shared__ A sh[2][BLK * 8];
   const int CG = C >> 3, RL = BLK / CG;
   const int cg = threadIdx.x % CG, rl = threadIdx.x / CG;
-  float s1[8], s2[8];
+  A s1[8], s2[8];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = 0.f;
+  for (int j = 0; j < 8; ++j) s1[j] = s2[j] = A(0);
   if (rl < RL) {
     float sc[8], be[8], mu[8], is[8];
 #pragma unroll
@@ -2199,9 +2201,9 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const E* __restrict__ dh, i
         for (int j = 0; j < 8; ++j) {
           const float zz = el(zv[u], j);
           const float pre = fmaf(zz - mu[j], sc[j], be[j]);
-          const float d = pre > 0.f ? el(dv[u], j) : 0.f;
+          const A d = pre > 0.f ? A(el(dv[u], j)) : A(0);
           s1[j] += d;
-          s2[j] += d * ((zz - mu[j]) * is[j]);
+          s2[j] += d * ((A(zz) - A(mu[j])) * A(is[j]));
         }
       }
     }
@@ -2215,7 +2217,7 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const E* __restrict__ dh, i
   // fixed-order combine over the row lanes: channel c = cg*8 + j
   for (int c = threadIdx.x; c < C; c += BLK) {
     const int g8 = c >> 3, j = c & 7;
-    float a = 0.f, b = 0.f;
+    A a = A(0), b = A(0);
     for (int r = 0; r < RL; ++r) {
       a += sh[0][(r * CG + g8) * 8 + j];
       b += sh[1][(r * CG + g8) * 8 + j];
@@ -2635,12 +2637,12 @@ static int bn_apply(const void* z, int m, int c, const float* bn, void* out, int
   return RPC_OK;
 }
 
-template <typename E>
-static int bnbwd_stats(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn, float* part,
+template <typename E, typename A>
+static int bnbwd_stats(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn, A* part,
                        void* stream) {
   if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
   const int nb = rpc_dense_bnbwd_blocks(m);
-  hipLaunchKernelGGL(k_bnbwd_stats<E>, dim3(nb), dim3(BLK), 0, (hipStream_t)stream, (const E*)dh, dp, doff,
+  hipLaunchKernelGGL((k_bnbwd_stats<E, A>), dim3(nb), dim3(BLK), 0, (hipStream_t)stream, (const E*)dh, dp, doff,
                      (const E*)z, m, c, bn, part);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
@@ -2672,11 +2674,11 @@ extern "C" int rpc_dense_bn_apply_f32(const float* z, int m, int c, const float*
 }
 extern "C" int rpc_dense_bnbwd_stats(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
                                      float* part, void* stream) {
-  return bnbwd_stats<u16>(dh, dp, doff, z, m, c, bn, part, stream);
+  return bnbwd_stats<u16, float>(dh, dp, doff, z, m, c, bn, part, stream);
 }
 extern "C" int rpc_dense_bnbwd_stats_f32(const float* dh, int dp, int doff, const float* z, int m, int c,
-                                         const float* bn, float* part, void* stream) {
-  return bnbwd_stats<float>(dh, dp, doff, z, m, c, bn, part, stream);
+                                         const float* bn, double* part, void* stream) {
+  return bnbwd_stats<float, double>(dh, dp, doff, z, m, c, bn, part, stream);
 }
 extern "C" int rpc_dense_bnbwd_apply(const void* dh, int dp, int doff, const void* z, int m, int c, const float* bn,
                                      const float* bnb, void* dz, void* stream) {

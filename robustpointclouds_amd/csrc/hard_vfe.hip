@@ -21,11 +21,6 @@
 
 #include "common.h"
 
-extern "C" int rpc_bn_finalize(const float* part, int nblk, int c, int n, int mode, const float* gamma,
-                               const float* beta, float eps, float momentum, float* running_mean,
-                               float* running_var, const float* fwd_bn, float* bn_out, float* dgamma,
-                               float* dbeta, void* workspace, void* stream);
-
 namespace rpc {
 namespace hvfe {
 

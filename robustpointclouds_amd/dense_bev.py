@@ -88,6 +88,9 @@ class ConvTimer:
 
 
 TIMER = None
+# parity tests: a list -> every training forward appends (bn module, z [Mo][co], bn [4co], B, Ho, Wo) per
+# layer (the stored pre-BatchNorm image and its scale/beta/mean/invstd: the engine's ReLU decisions)
+DEBUG = None
 
 # ---- HIP graphs over the fixed-shape dense part. The SECOND / SECONDFPN forward and backward issue
 # ~100 launches per step from Python (weight prep, conv, BN finalize / apply, wgrad, dgrad) with fixed
@@ -377,7 +380,7 @@ def _forward_layer(eng, L, h, pitch, B, H, W, training, dev, st, out=None, out_p
         y = out
     _ffi.check(eng.bn_apply(_ffi.ptr(z), Mo, L.co, _ffi.ptr(bn), _ffi.ptr(y), out_pitch, out_off, st),
                "rpc_dense_bn_apply")
-    rec = dict(L=L, h=h, pitch=pitch, z=z, bn=bn, wd=wd, R=R, S=S, O=O, in_hw=(H, W), Mo=Mo)
+    rec = dict(L=L, h=h, pitch=pitch, z=z, bn=bn, wd=wd, R=R, S=S, O=O, in_hw=(H, W), Mo=Mo, out_bhw=(B, Ho, Wo))
     return y, rec, Ho, Wo
 
 
@@ -401,13 +404,15 @@ def _backward_layer(eng, rec, dh, dh_pitch, dh_off, dev, st, need_dx, dx_out=Non
         nb = part.shape[0]
     else:
         nb = lib.rpc_dense_bnbwd_blocks(Mo)
-        part = torch.empty((nb, 2 * co), dtype=torch.float32, device=dev)
+        # the fp32 (parity) engine sums in double (sparse BEV images: the sums cancel)
+        part = torch.empty((nb, 2 * co), dtype=torch.float64 if eng.f32 else torch.float32, device=dev)
         _ffi.check(eng.bnbwd_stats(_ffi.ptr(dh), dh_pitch, dh_off, _ffi.ptr(rec["z"]), Mo, co,
                                    _ffi.ptr(rec["bn"]), _ffi.ptr(part), st), "rpc_dense_bnbwd_stats")
     bnb = torch.empty(5 * co, dtype=torch.float32, device=dev)
     dgamma = torch.empty(co, dtype=torch.float32, device=dev)
     dbeta = torch.empty(co, dtype=torch.float32, device=dev)
-    _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nb, co, Mo, 1, _ffi.ptr(L.bnm.weight), _ffi.ptr(L.bnm.bias),
+    mode = 1 | (4 if part.dtype == torch.float64 else 0)   # RPC_BN_PART_F64
+    _ffi.check(lib.rpc_bn_finalize(_ffi.ptr(part), nb, co, Mo, mode, _ffi.ptr(L.bnm.weight), _ffi.ptr(L.bnm.bias),
                                    0.0, 0.0, None, None, _ffi.ptr(rec["bn"]), _ffi.ptr(bnb), _ffi.ptr(dgamma),
                                    _ffi.ptr(dbeta), None, st), "rpc_bn_finalize(bwd)")
     dz = torch.empty((Mo, co), dtype=eng.dt, device=dev)
@@ -546,6 +551,11 @@ def _backbone_bwd(eng, recs, params, need_x, gouts):
     return (dx,) + tuple(grads.get(id(p)) for p in params), None
 
 
+def _debug_trace(recs, training):
+    if DEBUG is not None and training:
+        DEBUG.extend((r["L"].bnm, r["z"], r["bn"]) + tuple(r["out_bhw"]) for r in recs)
+
+
 def _alias(t):
     return None if t is None else t.detach()
 
@@ -573,6 +583,7 @@ class BackboneFn(torch.autograd.Function):
         else:
             outs, recs = _backbone_fwd(eng, mod, x)
         ctx.recs = recs
+        _debug_trace([r for b in recs for r in b], mod.training)
         return outs
 
     @staticmethod
@@ -632,6 +643,7 @@ class NeckFn(torch.autograd.Function):
         else:
             out, st_ = _neck_fwd(eng, mod, h0, h1)
         ctx.recs, ctx.Ctot = st_
+        _debug_trace(ctx.recs, mod.training)
         ctx.eng = eng
         ctx.cache = graph_cache(mod)
         ctx.param_list = params

@@ -206,7 +206,7 @@ class SparseEncoder(nn.Module):
         self.output_channels = output_channels
         self._grids = {}
         self.timer = None   # optional KernelTimer (bench.py roofline), see below
-        self.debug = None   # optional list: backward appends (layer, dy) for diagnostics
+        self.debug = None   # optional list: backward appends (layer, coors, z, dy, bn, out) for diagnostics
         self.flop_probe = None   # optional list: forward appends [(rulebook, C_in, C_out)] per step (bench.py)
         # perf mode: forward / dgrad convs on bf16 MFMA with bf16 gathered rows (fp32 accumulate,
         # fp32 BatchNorm statistics); parity mode (default) is fp32 end to end
@@ -726,7 +726,8 @@ class SparseEncoderFn(torch.autograd.Function):
                     G[sp.res].append(dy)
             if ctx.enc.debug is not None:
                 ctx.enc.debug.append((li, rec["coors_out"].cpu().numpy(), rec["z"].detach().cpu().double(),
-                                      dy.detach().cpu().double()))
+                                      dy.detach().cpu().double(), rec["bn"].detach().cpu().double(),
+                                      rec["out"].detach().cpu() if rec.get("out") is not None else None))
             # BatchNorm backward statistics of this layer -> bnb, dgamma, dbeta
             bnb = torch.empty(5 * sp.co, dtype=torch.float32, device=dev)
             dgamma = torch.empty_like(rec["gamma"])

@@ -39,12 +39,14 @@ import robustpointclouds_amd.plugin.models  # noqa: F401
 from oracle import anchor_head as oh
 from oracle import voxelize as ov
 from oracle.perturber import OraclePerturber, perturb_voxels
-from oracle.sparse_encoder import OracleSparseEncoder
+from oracle.sparse_encoder import OracleSparseEncoder, implementation_masks
+from robustpointclouds_amd import dense_bev
 from robustpointclouds_amd.adversarial_loss import parse_losses
 from robustpointclouds_amd.anchor_head import pack_gt
 from robustpointclouds_amd.plugin.models.detectors.adversarial_voxelnet import AdversarialVoxelNet
 from robustpointclouds_amd.synthetic import KITTI_PC_RANGE, KITTI_VOXEL_SIZE, kitti_batch
 from robustpointclouds_amd.trainer import Trainer, make_kitti_model
+from tests._dense_masks import FlipStats, engine_masks, follow_masks
 
 pytestmark = pytest.mark.gpu
 B = 6
@@ -52,6 +54,7 @@ LOSS_TOL = 1e-4
 GRAD_REL = 2e-2
 GRAD_F64_MAX = 1e-2
 GRAD_F64_MEAN = 2e-3
+FLIP_PRE_MAX = 1e-4   # a dense ReLU decision float64 makes differently lies within this of 0 (x channel max |pre|)
 # Round 3 measured middle.11.gamma at 1.005e-2 from float64 and loosened this bound; round 4 re-ran the test with
 # each backward variant switched off (tools/gpu_e2e_ab.sh: default, RPC_SPARSE_NATIVE=0, RPC_DENSE_BNFUSE=0, both;
 # profiles/r04_e2e_backward_ab.log): all four give the same gradients — the one-call sparse backward is bit-identical
@@ -66,12 +69,16 @@ class _VFE(nn.Module):            # upstream HardSimpleVFE formula (…3class.py
 
 
 class _Middle(nn.Module):
+    """The oracle sparse encoder; with `masks`, evaluated on the HIP encoder's ReLU decisions."""
+
     def __init__(self, enc, dtype):
         super().__init__()
         self.enc, self.dtype = enc, dtype
+        self.masks = None
 
     def forward(self, feats, coors, batch_size):
-        return self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size).to(self.dtype)
+        return self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size,
+                                masks=self.masks).to(self.dtype)
 
 
 class _Adversary(nn.Module):
@@ -133,6 +140,7 @@ class _Oracle:
 
     def __init__(self, model, hidden, w, dtype):
         self.dtype = dtype
+        self.model = model
         self.enc = OracleSparseEncoder(model.middle_encoder, dtype=dtype)
         self.backbone = copy.deepcopy(model.backbone).cpu().to(dtype)
         self.neck = copy.deepcopy(model.neck).cpu().to(dtype)
@@ -146,12 +154,19 @@ class _Oracle:
         self.ref.train()
         self.ref._epoch = 3
 
-    def step(self, rv, rn, rc, cb, cl, B):
+    def step(self, rv, rn, rc, cb, cl, B, masks=None, dense_masks=None, flips=None):
+        """masks / dense_masks: the sparse encoder's / the dense engine's ReLU decisions (oracle/sparse_encoder.py,
+        tests/_dense_masks.py); the dense decisions that differ from this oracle's own are counted in `flips`."""
+        self.ref.middle_encoder.masks = masks
+        hooks = [] if dense_masks is None else follow_masks((self.model.backbone, self.model.neck),
+                                                            (self.backbone, self.neck), dense_masks, flips)
         rbatch = dict(voxels=dict(voxels=torch.from_numpy(rv).to(self.dtype), num_points=torch.from_numpy(rn),
                                   coors=torch.from_numpy(rc)), batch_size=B)
         self.losses = self.ref.loss(rbatch, dict(gt_boxes=cb, gt_labels=cl))
         self.total, _ = parse_losses(self.losses)
         self.total.backward()
+        for h in hooks:
+            h.remove()
 
     def grads(self, nlin, natt, nbn):
         out = []
@@ -201,7 +216,9 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
     o32 = _Oracle(model, hidden, w, torch.float32)
     o64 = _Oracle(model, hidden, w, torch.float64)
 
-    # ---- HIP step
+    # ---- HIP step (the sparse encoder's debug trace on: its ReLU decisions for the oracle, below)
+    model.middle_encoder.debug = []
+    dense_bev.DEBUG = []
     gpts = [torch.from_numpy(p).to(dev) for p in pts]
     batch = model.data_preprocessor(dict(inputs=dict(points=gpts)), training=True)["inputs"]
     batch["batch_size"] = B
@@ -225,8 +242,20 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
 
     # ---- oracle steps
     cb, cl = pack_gt(list(zip(boxes, labels)), torch.device("cpu"))
-    o32.step(rv, rn, rc, cb, cl, B)
-    o64.step(rv, rn, rc, cb, cl, B)
+    # the sparse encoder's oracle on HIP's ReLU decisions (oracle/sparse_encoder.py `masks`): an fp32 pre-activation
+    # within a rounding of 0 lands on either side, and one flipped decision moved gradients by up to 1e-2 (middle.8.gamma
+    # 1.09e-2 vs the fp32 oracle's own 1.21e-2, gpurun_out r05j) — float64 arithmetic on the same branch instead
+    masks = implementation_masks(model.middle_encoder.debug)
+    model.middle_encoder.debug = None
+    # likewise the dense SECOND / SECONDFPN on the engine's decisions (tests/_dense_masks.py; one flipped
+    # decision moved backbone.blocks.1.1.bias by 1.04e-2 for Car, gpurun_out r05m)
+    dmasks = engine_masks(dense_bev.DEBUG)
+    dense_bev.DEBUG = None
+    flips = FlipStats()
+    o32.step(rv, rn, rc, cb, cl, B, masks, dmasks)
+    o64.step(rv, rn, rc, cb, cl, B, masks, dmasks, flips)
+    print(f"dense ReLU decisions differing from float64's: {flips.flips} (max |pre| {flips.worst:.1e} of channel max)")
+    assert flips.worst <= FLIP_PRE_MAX, flips.worst
     rlosses, rtotal = o32.losses, o32.total
 
     # ---- losses: every key within 1e-4 of the fp32 oracle

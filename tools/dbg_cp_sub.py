@@ -10,7 +10,7 @@ import time
 import torch
 
 sys.path.insert(0, ".")
-from tests.test_gpu_e2e_parity_centerpoint import (OracleStep, frames, hip_grads,  # noqa: E402
+from tests.test_gpu_e2e_parity_centerpoint import (OracleStep, frames, hip_grads, init_mid_cell_offsets,  # noqa: E402
                                                    oracle_voxels)
 from robustpointclouds_amd.adversarial_loss import parse_losses  # noqa: E402
 from robustpointclouds_amd.center_head import pack_gt  # noqa: E402
@@ -20,11 +20,7 @@ rel = lambda a, b: float((a.double().cpu() - b.double().cpu()).norm() / b.double
 dev = torch.device("cuda")
 torch.manual_seed(21)
 model = make_nus_model(device=dev, epoch=3)
-with torch.no_grad():
-    for th in model.pts_bbox_head.task_heads:
-        for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
-            dcn.conv_offset.weight.normal_(0, 0.02)
-            dcn.conv_offset.bias.uniform_(-0.5, 0.5)
+init_mid_cell_offsets(model)
 Trainer._select_engines(model, bf16=False)
 model.train()
 pts, gts = frames()

@@ -5,7 +5,7 @@ import pytest
 import torch
 
 from oracle import voxelize as ov
-from oracle.sparse_encoder import OracleSparseEncoder, spconv_pairs, subm_pairs
+from oracle.sparse_encoder import OracleSparseEncoder, implementation_masks, spconv_pairs, subm_pairs
 from robustpointclouds_amd.sparse_encoder import SparseEncoder
 from robustpointclouds_amd.synthetic import KITTI_PC_RANGE, KITTI_VOXEL_SIZE, kitti_frame
 
@@ -39,9 +39,17 @@ def test_sparse_encoder_forward_backward_matches_oracle(B, stride, basic):
             m[1].bias.uniform_(-0.2, 0.2)
     orc = OracleSparseEncoder(enc)
     f = torch.from_numpy(feats).to(dev).requires_grad_(True)
+    enc.debug = []
     out = enc(f, torch.from_numpy(coors).to(dev), B)
+    G = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
+    (out * G.to(dev)).sum().backward()
+    # the float64 oracle on the HIP encoder's ReLU decisions (oracle/sparse_encoder.py `masks`): an fp32
+    # pre-activation within a rounding of 0 falls on either side, and one on the other side moved beta6 by
+    # 3e-3 of its max (r05, after the fp32 GEMM's two-level sums changed the rounding)
+    masks = implementation_masks(enc.debug)
+    enc.debug = None
     ref_f = torch.from_numpy(feats).double().requires_grad_(True)
-    ref = orc.forward(ref_f, coors, B)
+    ref = orc.forward(ref_f, coors, B, masks=masks)
     assert out.shape == ref.shape == (B, 256, 200, 176)
     o = out.detach().cpu().double()
     scale = ref.abs().max().item()
@@ -50,8 +58,6 @@ def test_sparse_encoder_forward_backward_matches_oracle(B, stride, basic):
     for m, p in zip(enc.layers(), orc.params):
         np.testing.assert_allclose(m[1].running_mean.cpu().numpy(), p["rm"].numpy(), rtol=1e-4, atol=1e-5)
         np.testing.assert_allclose(m[1].running_var.cpu().numpy(), p["rv"].numpy(), rtol=1e-3, atol=1e-5)
-    G = torch.randn(out.shape, generator=torch.Generator().manual_seed(1))
-    (out * G.to(dev)).sum().backward()
     (ref * G.double()).sum().backward()
     # gradients pass through 12 train-mode BatchNorm backwards (mean-subtracting, so fp32
     # cancellation; fp32 sums over ~1e4 rows x 27 offsets): relative L2 error <= 1e-3 and

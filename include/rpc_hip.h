@@ -228,6 +228,10 @@ int rpc_sparse_res_backward(const float* g1, const float* g2, const float* out, 
 #define RPC_DENSE_BF16 2
 int rpc_sparse_to_dense(const float* z, const float* bn, const int* coors, int n, int c,
                         const int* shape /* B,D,H,W */, int flags, void* dense, void* stream);
+/* the cells rpc_sparse_to_dense writes for coors (c % 4 == 0) set back to 0: a persistent dense buffer
+ * is cleared where the previous step scattered instead of zero-filled whole (same flags). */
+int rpc_sparse_dense_clear(const int* coors, int n, int c, const int* shape /* B,D,H,W */, int flags, void* dense,
+                           void* stream);
 int rpc_dense_to_sparse_grad(const void* grad_dense, const float* z, const float* bn, const int* coors,
                              int n, int c, const int* shape, int flags, float* dy, float* part, void* stream);
 

@@ -142,6 +142,7 @@ SIGNATURES = {
     "rpc_bn_finalize": (i32, [vp, i32, i32, i32, i32, vp, vp, C.c_float, C.c_float, vp, vp, vp, vp, vp, vp,
                               vp, vp]),
     "rpc_sparse_to_dense": (i32, [vp, vp, vp, i32, i32, ip, i32, vp, vp]),
+    "rpc_sparse_dense_clear": (i32, [vp, i32, i32, ip, i32, vp, vp]),
     "rpc_dense_to_sparse_grad": (i32, [vp, vp, vp, vp, i32, i32, ip, i32, vp, vp, vp]),
     "rpc_to_bf16_rows": (i32, [vp, vp, i32, i32, i32, vp, vp]),
     "rpc_bnbwd_to_bf16_rows": (i32, [vp, vp, vp, i32, i32, vp, vp]),

@@ -673,6 +673,20 @@ __global__ __launch_bounds__(BLK) void k_to_dense_v4(const float* __restrict__ z
   for (int j = 0; j < 4; ++j)
     store_val(dense + dense_index<NHWC>(cr, c + j, C, s), fmaxf(fmaf(zz[j] - m[j], a[j], b[j]), 0.0f));
 }
+// the cells k_to_dense_v4 wrote for these coordinates set back to 0 (rpc_sparse_dense_clear): a persistent
+// dense image is re-cleared where the previous step scattered instead of zero-filled whole
+template <typename T, bool NHWC>
+__global__ __launch_bounds__(BLK) void k_dense_clear_v4(const int* __restrict__ coors, int N, int C, Shape s,
+                                                        T* __restrict__ dense) {
+  const int C4 = C >> 2;
+  const int t = blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * C4) return;
+  const int r = t / C4, c = (t - r * C4) * 4;
+  const int4 co = *(const int4*)(coors + 4 * r);
+  const int cr[4] = {co.x, co.y, co.z, co.w};
+#pragma unroll
+  for (int j = 0; j < 4; ++j) store_val(dense + dense_index<NHWC>(cr, c + j, C, s), 0.0f);
+}
 template <typename T, bool NHWC>
 __global__ __launch_bounds__(FBLK) void k_from_dense(const T* __restrict__ gd, const float* __restrict__ z,
                                                     const float* __restrict__ bn, const int* __restrict__ coors,
@@ -1364,6 +1378,25 @@ extern "C" int rpc_sparse_to_dense(const float* z, const float* bn, const int* c
     case 2: hipLaunchKernelGGL((k_to_dense<__hip_bfloat16, false>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s,
                                (__hip_bfloat16*)dense); break;
     default: hipLaunchKernelGGL((k_to_dense<__hip_bfloat16, true>), g, dim3(BLK), 0, st, z, bn, coors, N, C, s,
+                                (__hip_bfloat16*)dense);
+  }
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_sparse_dense_clear(const int* coors, int N, int C, const int* shape /* B,D,H,W */, int flags,
+                                      void* dense, void* stream) {
+  if (N < 0 || C < 4 || (C & 3) || !shape || (flags & ~3) || (long long)N * (C / 4) >= (1LL << 31)) return RPC_ERR_ARG;
+  if (N == 0) return RPC_OK;
+  Shape s{shape[0], shape[1], shape[2], shape[3]};
+  hipStream_t st = (hipStream_t)stream;
+  dim3 g4(cdiv((long long)N * (C / 4), BLK));
+  switch (flags) {
+    case 0: hipLaunchKernelGGL((k_dense_clear_v4<float, false>), g4, dim3(BLK), 0, st, coors, N, C, s, (float*)dense); break;
+    case 1: hipLaunchKernelGGL((k_dense_clear_v4<float, true>), g4, dim3(BLK), 0, st, coors, N, C, s, (float*)dense); break;
+    case 2: hipLaunchKernelGGL((k_dense_clear_v4<__hip_bfloat16, false>), g4, dim3(BLK), 0, st, coors, N, C, s,
+                               (__hip_bfloat16*)dense); break;
+    default: hipLaunchKernelGGL((k_dense_clear_v4<__hip_bfloat16, true>), g4, dim3(BLK), 0, st, coors, N, C, s,
                                 (__hip_bfloat16*)dense);
   }
   RPC_LAUNCH_CHECK();

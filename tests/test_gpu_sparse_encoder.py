@@ -214,3 +214,21 @@ def test_native_backward_bit_identical_to_layer_loop(bf16, basic):
         se.NATIVE_BACKWARD = saved
     for i, (a, b) in enumerate(zip(res[False], res[True])):
         assert torch.equal(a, b), i
+
+
+@pytest.mark.parametrize("bf16", [False, True])
+def test_dense_buffer_cleared_between_steps(bf16):
+    """The persistent dense BEV buffer is cleared where the previous step scattered (rpc_sparse_dense_clear),
+    not zero-filled whole: a step after a step on other voxels equals the same step on a fresh buffer,
+    bit for bit."""
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    enc = SparseEncoder(4, [41, 1600, 1408]).to(dev)
+    enc.bf16 = bf16
+    fa, ca = _inputs(2, 3, seed=0)
+    fb, cb = _inputs(2, 3, seed=7)
+    enc(torch.from_numpy(fa).to(dev), torch.from_numpy(ca).to(dev), 2)
+    got = enc(torch.from_numpy(fb).to(dev), torch.from_numpy(cb).to(dev), 2).clone()
+    enc.__dict__.pop("_dense_bufs")
+    want = enc(torch.from_numpy(fb).to(dev), torch.from_numpy(cb).to(dev), 2)
+    assert torch.equal(got, want)   # (a cell of the first step left behind would differ from the fresh zeros)

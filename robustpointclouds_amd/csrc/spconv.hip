@@ -962,13 +962,16 @@ __global__ __launch_bounds__(BLK) void k_res_bwd_v4(const float* __restrict__ g1
 // (not once per offset) and the K gathered x tiles sit side by side in LDS. Thread (k, ci, half)
 // keeps the CO sums of dW[k][ci][:] in registers over its half of the tile rows; the dz row it
 // reads is the same for all lanes of the wave (an LDS broadcast).
+// NT threads: one (k, ci, half) triple each (512 for CI = 5: 27 x 5 x 2 = 270 > 256)
 template <int CI, int CO, int AT>
-__global__ __launch_bounds__(BLK) void k_wgrad_narrow(WgradArgs g) {
+constexpr int wn_threads() { return MAXK * CI * 2 <= BLK ? BLK : 2 * BLK; }
+template <int CI, int CO, int AT, int NT = wn_threads<CI, CO, AT>()>
+__global__ __launch_bounds__(NT) void k_wgrad_narrow(WgradArgs g) {
   constexpr int RT = 64;
   __shared__ __attribute__((aligned(16))) float sA[MAXK * RT * CI];
   __shared__ __attribute__((aligned(16))) float sD[RT * CO];
   __shared__ int sN[RT * MAXK];
-  __shared__ float sH[BLK / 2][CO];
+  __shared__ float sH[NT / 2][CO];
   const int tid = threadIdx.x, K = g.K;
   const int rb0 = blockIdx.x * g.rows_per, rb1 = min(g.Nout, rb0 + g.rows_per);
   const int pair = tid >> 1, half = tid & 1;          // (k, ci) pair, row parity
@@ -980,31 +983,31 @@ __global__ __launch_bounds__(BLK) void k_wgrad_narrow(WgradArgs g) {
   // every staging loop below issues all of its thread's global loads before the first LDS store (one
   // round trip per phase; as plain strided loops each load waited for the store before it: ~18 exposed
   // latencies per 64-row sub-tile)
-  constexpr int PN = (RT * MAXK + BLK - 1) / BLK, PD = (RT * CO + BLK - 1) / BLK;
+  constexpr int PN = (RT * MAXK + NT - 1) / NT, PD = (RT * CO + NT - 1) / NT;
   for (int rb = rb0; rb < rb1; rb += RT) {
     __syncthreads();
     {
       int nv[PN];
 #pragma unroll
       for (int i = 0; i < PN; ++i) {
-        const int q = tid + i * BLK;
+        const int q = tid + i * NT;
         const int r = q / K, k = q - r * K, row = rb + r;
         nv[i] = (q < RT * K && row < rb1) ? g.nbr[(long long)row * K + k] : -1;
       }
 #pragma unroll
       for (int i = 0; i < PN; ++i)
-        if (tid + i * BLK < RT * K) sN[tid + i * BLK] = nv[i];
+        if (tid + i * NT < RT * K) sN[tid + i * NT] = nv[i];
       float dv[PD], zv[PD];
 #pragma unroll
       for (int i = 0; i < PD; ++i) {
-        const int q = tid + i * BLK, r = q / CO, n = q - r * CO, row = rb + r;
+        const int q = tid + i * NT, r = q / CO, n = q - r * CO, row = rb + r;
         const bool ok = q < RT * CO && row < rb1;
         dv[i] = ok ? g.dy[(long long)row * CO + n] : 0.0f;
         zv[i] = ok ? g.z[(long long)row * CO + n] : 0.0f;
       }
 #pragma unroll
       for (int i = 0; i < PD; ++i) {
-        const int q = tid + i * BLK, r = q / CO, n = q - r * CO, row = rb + r;
+        const int q = tid + i * NT, r = q / CO, n = q - r * CO, row = rb + r;
         if (q >= RT * CO) continue;
         float v = 0.0f;
         if (row < rb1) {
@@ -1019,13 +1022,13 @@ __global__ __launch_bounds__(BLK) void k_wgrad_narrow(WgradArgs g) {
       float4 gv[PN];
 #pragma unroll
       for (int i = 0; i < PN; ++i) {
-        const int q = tid + i * BLK, k = q / RT, r = q - k * RT;
+        const int q = tid + i * NT, k = q / RT, r = q - k * RT;
         const int src = q < K * RT ? sN[r * K + k] : -1;
         gv[i] = src >= 0 ? *(const float4*)(g.a + (long long)src * 4) : make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
       for (int i = 0; i < PN; ++i) {
-        const int q = tid + i * BLK;
+        const int q = tid + i * NT;
         if (q >= K * RT) continue;
         const int k = q / RT, r = q - k * RT;
         float4 v = gv[i];
@@ -1038,7 +1041,7 @@ __global__ __launch_bounds__(BLK) void k_wgrad_narrow(WgradArgs g) {
         *(float4*)&sA[q * 4] = v;
       }
     } else {
-      for (int q = tid; q < K * RT * CI; q += BLK) {
+      for (int q = tid; q < K * RT * CI; q += NT) {
         const int k = q / (RT * CI), rem = q - k * (RT * CI), r = rem / CI, c = rem - r * CI;
         const int src = sN[r * K + k];
         float v = 0.0f;
@@ -1081,6 +1084,156 @@ __global__ __launch_bounds__(BLK) void k_wgrad_narrow(WgradArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ narrow input layer (conv_input, CI 4 / 5 -> 16)
+// The fp32 input layer as row passes instead of the 16 x 16 MFMA GEMM (4 of whose 16 K columns were real and
+// which walked the K offsets one barrier pair each: 21.8 / 76 us forward, 52 / 194 us data gradient on the
+// metric's / CenterPoint's layer 0). Block = 64 rows (one BatchNorm partial row, the GEMM's BM), thread = (row,
+// quarter q of the 16 output / dz channels); the block's neighbour indices and the K weight taps are staged in
+// LDS once; the gathers go out 9 offsets at a time with unconditional (clamped) loads, so each thread waits
+// three round trips instead of one per offset. Per offset the CI (forward) / 4-channel (data gradient)
+// products are summed first and then added to the running total (the GEMM's two-level order).
+constexpr int L0R = 64, L0T = 256, L0G = 9;   // rows per block (= BM), threads, offsets per gather group
+template <int CI>
+__global__ __launch_bounds__(L0T) void k_l0_fwd(const float* __restrict__ x, const int* __restrict__ nbr, int K,
+                                                const float* __restrict__ W, int n_out, float* __restrict__ z,
+                                                float* __restrict__ part) {
+  constexpr int CO = 16;
+  __shared__ float sW[MAXK * CI * CO];
+  __shared__ int sN[L0R * MAXK];
+  __shared__ float sP[L0T / 64][2][CO];
+  const int tid = threadIdx.x, r = tid >> 2, q = tid & 3, lane = tid & 63, w = tid >> 6;
+  const int r0 = blockIdx.x * L0R, nr = min(L0R, n_out - r0);
+  for (int i = tid; i < K * CI * CO; i += L0T) sW[i] = W[i];
+  for (int i = tid; i < L0R * K; i += L0T) sN[i] = i < nr * K ? nbr[(long long)r0 * K + i] : -1;
+  __syncthreads();
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int k0 = 0; k0 < K; k0 += L0G) {
+    int src[L0G];
+    float xv[L0G][CI];
+#pragma unroll
+    for (int u = 0; u < L0G; ++u) {
+      src[u] = k0 + u < K ? sN[r * K + k0 + u] : -1;
+      const long long s = src[u] < 0 ? 0 : src[u];
+#pragma unroll
+      for (int c = 0; c < CI; ++c) xv[u][c] = x[s * CI + c];
+    }
+#pragma unroll
+    for (int u = 0; u < L0G; ++u) {
+      if (src[u] < 0) continue;
+      const float* wk = sW + (k0 + u) * CI * CO + q * 4;
+      float t[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < CI; ++c)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = fmaf(xv[u][c], wk[c * CO + j], t[j]);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[j] += t[j];
+    }
+  }
+  const bool live = r < nr;
+  if (live) *(float4*)(z + (long long)(r0 + r) * CO + q * 4) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+  if (part == nullptr) return;
+  float s1[4], s2[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    s1[j] = live ? acc[j] : 0.f;
+    s2[j] = live ? acc[j] * acc[j] : 0.f;
+  }
+#pragma unroll
+  for (int o = 4; o < 64; o <<= 1)   // the wave's 16 rows of this quarter, fixed xor order
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s1[j] += __shfl_xor(s1[j], o, 64);
+      s2[j] += __shfl_xor(s2[j], o, 64);
+    }
+  if (lane < 4) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sP[w][0][q * 4 + j] = s1[j];
+      sP[w][1][q * 4 + j] = s2[j];
+    }
+  }
+  __syncthreads();
+  if (tid < 2 * CO) {
+    const int which = tid / CO, c = tid - which * CO;
+    part[(long long)blockIdx.x * 2 * CO + tid] =
+        ((sP[0][which][c] + sP[1][which][c]) + sP[2][which][c]) + sP[3][which][c];
+  }
+}
+
+// data gradient of the input layer: din[r][n] = sum_k sum_o dz[nbr(r, k)][o] W[k][n][o] (n < CI), dz formed on
+// load from (dy, z, bnb) of the 16-channel layer as k_gemm's A_BNBWD does; thread (row, quarter q of the 16 dz
+// channels), the 4 quarters added in a fixed xor order
+template <int CI>
+__global__ __launch_bounds__(L0T) void k_l0_dgrad(const float* __restrict__ dy, const float* __restrict__ zz,
+                                                  const float* __restrict__ bnb, const int* __restrict__ nbr, int K,
+                                                  int rev, const float* __restrict__ W, int n_in,
+                                                  float* __restrict__ din) {
+  constexpr int CO = 16;
+  __shared__ float sW[MAXK * CI * CO];
+  __shared__ int sN[L0R * MAXK];
+  const int tid = threadIdx.x, r = tid >> 2, q = tid & 3;
+  const int r0 = blockIdx.x * L0R, nr = min(L0R, n_in - r0);
+  for (int i = tid; i < K * CI * CO; i += L0T) sW[i] = W[i];
+  for (int i = tid; i < L0R * K; i += L0T) {
+    const int rr = i / K, k = i - rr * K;
+    sN[i] = rr < nr ? nbr[(long long)(r0 + rr) * K + (rev ? K - 1 - k : k)] : -1;
+  }
+  float gi[4], m1[4], m2[4], mu[4], is[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = q * 4 + j;
+    gi[j] = bnb[c];
+    m1[j] = bnb[CO + c];
+    m2[j] = bnb[2 * CO + c];
+    mu[j] = bnb[3 * CO + c];
+    is[j] = bnb[4 * CO + c];
+  }
+  __syncthreads();
+  float acc[CI];
+#pragma unroll
+  for (int n = 0; n < CI; ++n) acc[n] = 0.f;
+  for (int k0 = 0; k0 < K; k0 += L0G) {
+    int src[L0G];
+    float4 dv[L0G], zv[L0G];
+#pragma unroll
+    for (int u = 0; u < L0G; ++u) {
+      src[u] = k0 + u < K ? sN[r * K + k0 + u] : -1;
+      const long long s = src[u] < 0 ? 0 : src[u];
+      dv[u] = *(const float4*)(dy + s * CO + q * 4);
+      zv[u] = *(const float4*)(zz + s * CO + q * 4);
+    }
+#pragma unroll
+    for (int u = 0; u < L0G; ++u) {
+      if (src[u] < 0) continue;
+      const float d4[4] = {dv[u].x, dv[u].y, dv[u].z, dv[u].w}, z4[4] = {zv[u].x, zv[u].y, zv[u].z, zv[u].w};
+      float v[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xh = (z4[j] - mu[j]) * is[j];
+        v[j] = gi[j] * (d4[j] - m1[j] - xh * m2[j]);
+      }
+      const float* wk = sW + (k0 + u) * CI * CO + q * 4;
+#pragma unroll
+      for (int n = 0; n < CI; ++n) {
+        float t = 0.f;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t = fmaf(v[j], wk[n * CO + j], t);
+        acc[n] += t;
+      }
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < CI; ++n) {
+    acc[n] += __shfl_xor(acc[n], 1, 64);
+    acc[n] += __shfl_xor(acc[n], 2, 64);
+  }
+  if (q == 0 && r < nr) {
+#pragma unroll
+    for (int n = 0; n < CI; ++n) din[(long long)(r0 + r) * CI + n] = acc[n];
+  }
+}
+
 // ------------------------------------------------------------------ dispatch
 template <int CI, int CO>
 static void launch_gemm_t(int at, int et, const GemmArgs& a, int nblk, hipStream_t st) {
@@ -1103,7 +1256,7 @@ static int launch_gemm(int CI, int CO, int at, int et, const GemmArgs& a, int nb
   return RPC_ERR_UNSUPPORTED;
 }
 
-static bool wgrad_narrow(int CI, int CO, int K) { return (CI == 4 || CI == 5) && CO == 16 && K * CI * 2 <= BLK; }
+static bool wgrad_narrow(int CI, int CO, int K) { return (CI == 4 || CI == 5) && CO == 16 && K <= MAXK; }
 
 static int wgrad_narrow_chunks(int n) {   // 256-row chunks: ~1.5 blocks per CU at 100k rows
   const int c = (n + 255) / 256;
@@ -1228,6 +1381,13 @@ extern "C" int rpc_spconv_forward(const float* in, const float* in_bn /* scale,s
                                   float* z_out, float* part, void* stream) {
   if (n_out < 0 || K > MAXK) return RPC_ERR_ARG;
   if (n_out == 0) return RPC_OK;
+  if (in_bn == nullptr && CO == 16 && (CI == 4 || CI == 5)) {   // the narrow input layer
+    const dim3 grid(cdiv(n_out, L0R));
+    if (CI == 4) hipLaunchKernelGGL(k_l0_fwd<4>, grid, dim3(L0T), 0, (hipStream_t)stream, in, nbr, K, W, n_out, z_out, part);
+    else hipLaunchKernelGGL(k_l0_fwd<5>, grid, dim3(L0T), 0, (hipStream_t)stream, in, nbr, K, W, n_out, z_out, part);
+    RPC_LAUNCH_CHECK();
+    return RPC_OK;
+  }
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.a = in;
@@ -1256,6 +1416,15 @@ extern "C" int rpc_spconv_dgrad(const float* dy_out, const float* z_out, const f
                                 void* stream) {
   if (n_in < 0 || K > MAXK) return RPC_ERR_ARG;
   if (n_in == 0) return RPC_OK;
+  if (prev_z == nullptr && CO == 16 && (CI == 4 || CI == 5)) {   // into the narrow input layer's rows
+    const dim3 grid(cdiv(n_in, L0R));
+    if (CI == 4)
+      hipLaunchKernelGGL(k_l0_dgrad<4>, grid, dim3(L0T), 0, (hipStream_t)stream, dy_out, z_out, bnb, map, K, rev, W, n_in, din);
+    else
+      hipLaunchKernelGGL(k_l0_dgrad<5>, grid, dim3(L0T), 0, (hipStream_t)stream, dy_out, z_out, bnb, map, K, rev, W, n_in, din);
+    RPC_LAUNCH_CHECK();
+    return RPC_OK;
+  }
   GemmArgs a;
   memset(&a, 0, sizeof(a));
   a.a = dy_out;
@@ -1317,8 +1486,10 @@ extern "C" int rpc_spconv_wgrad(const float* in, const float* in_bn, int CI, con
     a.rows_per = ((cdiv(n_out, chunks) + 63) / 64) * 64;
 #define NW(ci)                                                                                              \
     if (CI == ci) {                                                                                         \
-      if (in_bn) hipLaunchKernelGGL((k_wgrad_narrow<ci, 16, A_BNRELU>), dim3(chunks), dim3(BLK), 0, st, a); \
-      else hipLaunchKernelGGL((k_wgrad_narrow<ci, 16, A_RAW>), dim3(chunks), dim3(BLK), 0, st, a);          \
+      if (in_bn) hipLaunchKernelGGL((k_wgrad_narrow<ci, 16, A_BNRELU>), dim3(chunks),                       \
+                                    dim3(wn_threads<ci, 16, A_BNRELU>()), 0, st, a);                        \
+      else hipLaunchKernelGGL((k_wgrad_narrow<ci, 16, A_RAW>), dim3(chunks), dim3(wn_threads<ci, 16, A_RAW>()), \
+                              0, st, a);                                                                    \
     }
     NW(4) NW(5)
 #undef NW

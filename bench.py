@@ -85,18 +85,23 @@ def _gt(boxes, labels, dev):
 PEAK = {"fp32_mfma": 157.3, "bf16_mfma": 2500.0}   # TFLOP/s dense, MI355X_MICROARCH.md
 
 
-def _traffic(kernel_tag):
-    """HBM bytes per launch of one kernel from the newest committed PMC summary that has it
-    (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, KB -> bytes) and that summary's file name,
-    else (None, None). `kernel_tag` is matched against the kernel's name without its argument list."""
+def _traffic(kernel_tag, model="voxelnet"):
+    """HBM bytes per launch of one kernel from the newest committed PMC summary of this model's step that has
+    it (tools/pmc_traffic.py: FETCH_SIZE x 2 + WRITE_SIZE, KB -> bytes) and that summary's file name, else
+    (None, None). `kernel_tag` is matched against the kernel's name without its argument list. Summaries are
+    rNN_pmc_traffic_vMM.json (the SECOND steps: 3-class, Car, strong) or rNN_pmc_traffic_<model>_vMM.json
+    (e.g. centerpoint): a kernel of the same name runs other shapes in another model's step."""
     import glob
     import re
 
-    def order(f):   # rNN_pmc_traffic_vMM.json: newest round, then newest version (mtimes do not survive copies)
-        m = re.search(r"r(\d+)_pmc_traffic_v(\d+)", os.path.basename(f))
-        return (int(m.group(1)), int(m.group(2))) if m else (-1, -1)
-    files = sorted(glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "*pmc_traffic*.json")),
-                   key=order)
+    model = "centerpoint" if model == "centerpoint" else "voxelnet"
+
+    def parse(f):   # newest round, then newest version (mtimes do not survive copies)
+        m = re.search(r"r(\d+)_pmc_traffic_(?:([a-z]+)_)?v(\d+)", os.path.basename(f))
+        return ((int(m.group(1)), int(m.group(3))), m.group(2) or "voxelnet") if m else ((-1, -1), "voxelnet")
+    files = sorted((f for f in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
+                                                      "*pmc_traffic*.json")) if parse(f)[1] == model),
+                   key=lambda f: parse(f)[0])
     loose = kernel_tag[:-1] + "," if kernel_tag.endswith(">") else None   # trailing template arguments omitted
     for f in reversed(files):
         d = json.load(open(f))
@@ -441,7 +446,7 @@ def main():
             peak = PEAK["fp32_mfma"] if a.fp32 else PEAK["bf16_mfma"]
             ents = []
             for name, k in ks.items():
-                tr_bytes, tr_src = _traffic(name)
+                tr_bytes, tr_src = _traffic(name, a.model)
                 ents.append(dict(bound="mfma", kernel=name, achieved=round(k["tflops"], 3), peak=peak, unit="TFLOP/s",
                                  frac=round(k["tflops"] / peak, 4), traffic=tr_bytes, traffic_source=tr_src,
                                  avg_launch_ms=round(k["avg_ms"], 4), launches=k["launches"],
@@ -488,7 +493,7 @@ def main():
             # the sparse conv kernels (HIP events per launch; FLOPs from the valid rulebook pairs)
             for name, k in sks.items():
                 pk = PEAK["bf16_mfma"] if k["dtype"] == "bf16" else PEAK["fp32_mfma"]
-                tr_bytes, tr_src = _traffic(name)
+                tr_bytes, tr_src = _traffic(name, a.model)
                 alls.append(dict(bound="mfma", kernel=name, achieved=round(k["tflops"], 3), peak=pk, unit="TFLOP/s",
                                  frac=round(k["tflops"] / pk, 4), traffic=tr_bytes, traffic_source=tr_src,
                                  avg_launch_ms=round(k["avg_ms"], 4), launches=k["launches"],
@@ -503,7 +508,7 @@ def main():
             tag = ks["kernel"]
             res["roofline"] = dict(bound="mfma", achieved=round(ks["tflops"], 3), peak=peak,
                                    unit="TFLOP/s", frac=round(ks["tflops"] / peak, 4),
-                                   traffic=_traffic(tag)[0],
+                                   traffic=_traffic(tag, a.model)[0],
                                    kernel=f"{tag} (sparse conv {op} {ci}->{co}, {ks['dtype']} MFMA)",
                                    avg_launch_ms=round(ks["avg_ms"], 4),
                                    flops_per_launch=ks["flops_per_launch"], launches=ks["launches"],

@@ -40,7 +40,8 @@ def run(model_fn, data, steps, warm):
 
 
 dev = torch.device("cuda")
-for name in ("kitti", "nus"):
+ONLY = sys.argv[1] if len(sys.argv) > 1 else None   # "ring" / "morton": one kitti variant, 12 steps (for rocprofv3)
+for name in (("kitti",) if ONLY else ("kitti", "nus")):
     if name == "kitti":
         data = bench._batches(4, 6, 0, dev, 3)
         vs, lo = (0.05, 0.05, 0.1), (0.0, -40.0, -3.0)
@@ -52,6 +53,9 @@ for name in ("kitti", "nus"):
         mk = lambda: make_nus_model(device=dev, epoch=3)
         steps, warm = 10, 4
     sdata = [([torch.from_numpy(morton_sort(p.cpu().numpy(), vs, lo)).to(dev) for p in pts], gt) for pts, gt in data]
+    if ONLY:
+        print(ONLY, run(mk, data if ONLY == "ring" else sdata, 8, 4), flush=True)
+        break
     res = {"ring": [], "morton": []}
     for rep in range(2):
         res["ring"].append(run(mk, data, steps, warm))

@@ -560,6 +560,48 @@ __global__ __launch_bounds__(BLK) void k_dz_bf16_v8(const float* __restrict__ dy
   }
 }
 
+// The same pass with one float4 (4 channels) of the flattened [N][C] rows per thread: every load instruction reads
+// 1 KB of consecutive bytes (the 8-channel form's lanes read 32 B each at a 32-B stride of the other lanes' rows: two
+// half-used 2 KB spans per operand and row — 2.6 TB/s on CenterPoint's 16-channel layers). The grid stride is a
+// multiple of C / 4 (C / 4 divides BLK), so a thread's channels and BatchNorm parameters never change. Same
+// arithmetic per element, so the same bits.
+constexpr int RV4 = 4;
+__global__ __launch_bounds__(BLK) void k_dz_bf16_v4(const float* __restrict__ dy, const float* __restrict__ z,
+                                                    const float* __restrict__ bnb, int N, int C,
+                                                    u16* __restrict__ dz) {
+  const int C4 = C >> 2;
+  const long long total = (long long)N * C4;
+  const long long t0 = (long long)blockIdx.x * BLK + threadIdx.x;
+  const int c = (int)(t0 % C4) * 4;
+  const float4 g4 = *(const float4*)(bnb + c), a4 = *(const float4*)(bnb + C + c), b4 = *(const float4*)(bnb + 2 * C + c);
+  const float4 u4 = *(const float4*)(bnb + 3 * C + c), i4 = *(const float4*)(bnb + 4 * C + c);
+  const float gi[4] = {g4.x, g4.y, g4.z, g4.w}, m1[4] = {a4.x, a4.y, a4.z, a4.w}, m2[4] = {b4.x, b4.y, b4.z, b4.w};
+  const float mb[4] = {u4.x, u4.y, u4.z, u4.w}, ib[4] = {i4.x, i4.y, i4.z, i4.w};
+  const long long step = (long long)gridDim.x * BLK;
+  for (long long i0 = t0; i0 < total; i0 += RV4 * step) {
+    float4 d[RV4], zz[RV4];
+#pragma unroll
+    for (int u = 0; u < RV4; ++u) {
+      const long long i = min(i0 + u * step, total - 1);
+      d[u] = ((const float4*)dy)[i];
+      zz[u] = ((const float4*)z)[i];
+    }
+#pragma unroll
+    for (int u = 0; u < RV4; ++u) {
+      const long long i = i0 + u * step;
+      if (i >= total) break;
+      const float dv[4] = {d[u].x, d[u].y, d[u].z, d[u].w}, zv[4] = {zz[u].x, zz[u].y, zz[u].z, zz[u].w};
+      u16 o[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float xh = (zv[j] - mb[j]) * ib[j];
+        o[j] = to_h16<0>(gi[j] * (dv[j] - m1[j] - xh * m2[j]));
+      }
+      *(uint2*)(dz + i * 4) = *(const uint2*)o;
+    }
+  }
+}
+
 // W fp32 [K][CI][CO] -> B^T bf16 [K][NGP][KGP]; fwd: n = co, kk = ci ; dgrad: n = ci, kk = co
 __device__ __forceinline__ void wprep_elem(long long t, const float* __restrict__ W, int CI, int CO, int dgrad,
                                            int NGP, int KGP, u16* __restrict__ bt, int fmt = 0) {
@@ -842,7 +884,12 @@ extern "C" int rpc_bnbwd_to_bf16_rows(const float* dy, const float* z, const flo
   if (n < 0 || c < 1) return RPC_ERR_ARG;
   if (n == 0) return RPC_OK;
   int cp = r8(c);
-  if (c % 8 == 0 && BLK % (c / 8) == 0 && (long long)n * c < (1LL << 31))
+  if (c % 8 == 0 && BLK % (c / 4) == 0 && (long long)n * c < (1LL << 31)) {
+    const long long per = (long long)BLK * RV4;
+    const long long nb = ((long long)n * (c / 4) + per - 1) / per;
+    hipLaunchKernelGGL(k_dz_bf16_v4, dim3((unsigned)(nb < 1 ? 1 : (nb > 8192 ? 8192 : nb))), dim3(BLK), 0,
+                       (hipStream_t)stream, dy, z, bnb, n, c, (u16*)dz);
+  } else if (c % 8 == 0 && BLK % (c / 8) == 0 && (long long)n * c < (1LL << 31))
     hipLaunchKernelGGL(k_dz_bf16_v8, dim3(rowpass_blocks(n, c)), dim3(BLK), 0, (hipStream_t)stream, dy, z, bnb, n, c,
                        (u16*)dz);
   else

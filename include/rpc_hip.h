@@ -524,6 +524,16 @@ int rpc_loss_tail_forward(const float* head_losses, const float* pert_losses, fl
                           void* stream);
 int rpc_loss_tail_backward(const float* pert_losses, float reg_coef, const float* grad_out, float* grad_head,
                            float* grad_pert, void* stream);
+/* Loss combination of AdversarialCenterPoint.loss_by_feat_single (models/detectors/adversarial_centerpoint.py:
+ * 203-257; the perturber's l2_norm scalar as the documented fix of :81) + parse_losses over the CenterHead's packed task
+ * losses (device fp32 [n]: task t heatmap 2t, bbox 2t+1) and l2 (device fp32 scalar); negw = -min(w*epoch/10, w),
+ * rw = regularization_weight. out [n + 4] = task losses, loss_adversarial (det > 0 ? negw*det : 0, det = sum of the
+ * finite clamp(v, 0, 100)), loss_l2_regularization = rw*l2, perturbation_l2_norm = l2, total (dict order).
+ * Backward: grad_out [n + 4] -> grad_losses [n], grad_l2 [1]. Values bit-identical to the torch composition. */
+int rpc_center_tail_forward(const float* task_losses, int n, const float* l2, float negw, float rw, float* out,
+                            void* stream);
+int rpc_center_tail_backward(const float* task_losses, int n, float negw, float rw, const float* grad_out,
+                             float* grad_losses, float* grad_l2, void* stream);
 
 /* torch.nn.utils.clip_grad_norm_(max_norm) + torch.optim.AdamW step as mmengine's OptimWrapper runs
  * them (configs/adversarial/adversarial-second_hv_secfpn_8xb6-80e_kitti-3d-3class.py:130-140),

@@ -190,6 +190,8 @@ SIGNATURES = {
     "rpc_dense_wprep_batch_f32": (i32, [vp, i32, vp]),
     "rpc_loss_tail_forward": (i32, [vp, vp, C.c_float, vp, vp]),
     "rpc_loss_tail_backward": (i32, [vp, C.c_float, vp, vp, vp, vp]),
+    "rpc_center_tail_forward": (i32, [vp, i32, vp, C.c_float, C.c_float, vp, vp]),
+    "rpc_center_tail_backward": (i32, [vp, i32, C.c_float, C.c_float, vp, vp, vp, vp]),
     "rpc_clip_adamw_workspace_size": (sz, [i32]),
     "rpc_clip_adamw": (i32, [vp, vp, vp, vp, vp, vp, vp, vp, i32, i32, vp, C.POINTER(RpcAdamWHyper), C.c_float, vp,
                              vp, sz, vp]),

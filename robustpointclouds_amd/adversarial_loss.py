@@ -72,6 +72,73 @@ def _fused_tail(losses_pts, loss_dict, epoch, regularization_weight):
     return res
 
 
+class CenterTailFn(torch.autograd.Function):
+    """(task losses [n], l2 []) -> out [n + 4] (csrc/step_tail.hip, rpc_center_tail_forward/backward): the
+    AdversarialCenterPoint combination + parse_losses in one single-lane kernel each way."""
+
+    @staticmethod
+    def forward(ctx, v, l2, negw, rw):
+        lib = _ffi.load()
+        v = v.detach().float().contiguous()
+        l2c = l2.detach().float().reshape(1).contiguous()
+        n = v.numel()
+        out = torch.empty(n + 4, dtype=torch.float32, device=v.device)
+        _ffi.check(lib.rpc_center_tail_forward(_ffi.ptr(v), n, _ffi.ptr(l2c), float(negw), float(rw), _ffi.ptr(out),
+                                               _ffi.stream_of(out)), "rpc_center_tail_forward")
+        ctx.save_for_backward(v)
+        ctx.negw, ctx.rw, ctx.l2_shape = float(negw), float(rw), l2.shape
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        lib = _ffi.load()
+        (v,) = ctx.saved_tensors
+        g = g.float().contiguous()
+        gv = torch.empty_like(v)
+        gl2 = torch.empty(1, dtype=torch.float32, device=g.device)
+        _ffi.check(lib.rpc_center_tail_backward(_ffi.ptr(v), v.numel(), ctx.negw, ctx.rw, _ffi.ptr(g), _ffi.ptr(gv),
+                                                _ffi.ptr(gl2), _ffi.stream_of(g)), "rpc_center_tail_backward")
+        return gv, gl2.reshape(ctx.l2_shape), None, None
+
+
+def center_combination(losses: dict, l2, w: float, regularization_weight: float, device) -> dict:
+    """AdversarialCenterPoint.loss_by_feat_single's combination in torch ops
+    (models/detectors/adversarial_centerpoint.py:203-257, with the l2 scalar of the documented :81 fix): every
+    Tensor-valued 'loss' entry clamped to [0, 100] and NaN/Inf-skipped, summed; loss_adversarial = -w * det when
+    det > 0 (the `.item() > 0` branch of :232 as a device select); loss_l2_regularization = regularization_weight
+    * l2; perturbation_l2_norm. fused_center_tail computes the same values on the HIP tail."""
+    losses = dict(losses)
+    det = torch.zeros((), device=device)
+    for k, v in losses.items():
+        if "loss" in k and isinstance(v, torch.Tensor):
+            c = torch.clamp(v, min=0.0, max=100.0)
+            det = det + torch.where(torch.isfinite(c), c, torch.zeros_like(c))
+    adv = -w * det
+    losses["loss_adversarial"] = torch.where(det > 0, adv, torch.zeros_like(adv))
+    losses["loss_l2_regularization"] = regularization_weight * l2
+    losses["perturbation_l2_norm"] = l2.detach()
+    return losses
+
+
+def fused_center_tail(task_losses: dict, packed, l2, w: float, regularization_weight: float):
+    """AdversarialCenterPoint.loss_by_feat_single's combination over the CenterHead's packed task losses (a
+    PackedCenterLosses dict whose values are packed[0..n) in order): a FusedLosses dict (views of one device
+    vector) whose `.total` is parse_losses' sum, or None when the inputs are not that layout."""
+    n = len(task_losses)
+    if (packed is None or not packed.is_cuda or packed.dim() != 1 or packed.numel() != n or not isinstance(l2, torch.Tensor)
+            or not l2.is_cuda or l2.numel() != 1 or packed.dtype != torch.float32 or l2.dtype != torch.float32):
+        return None
+    out = CenterTailFn.apply(packed, l2, -w, regularization_weight)
+    res = FusedLosses()
+    for i, k in enumerate(task_losses):
+        res[k] = out[i]
+    res["loss_adversarial"] = out[n]
+    res["loss_l2_regularization"] = out[n + 1]
+    res["perturbation_l2_norm"] = out[n + 2].detach()
+    res.total = out[n + 3]
+    return res
+
+
 def _zero(device):
     return torch.tensor(0.0, device=device, requires_grad=True)
 

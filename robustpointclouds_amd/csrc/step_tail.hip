@@ -64,6 +64,57 @@ __global__ __launch_bounds__(64) void k_loss_tail_bwd(const float* __restrict__ 
   gpert[3] = 10.0f * (g[6] + gt + 0.01f * gadv);
 }
 
+// Loss tail of AdversarialCenterPoint.loss_by_feat_single (plugin detectors/adversarial_centerpoint.py, restating
+// models/detectors/adversarial_centerpoint.py:203-257 with the documented l2 fix) + parse_losses, over the CenterHead's
+// packed task losses v[n] (task t: heatmap 2t, bbox 2t + 1):
+//   det = (0 + w_0) + w_1 + ...,  w_i = isfinite(c_i) ? c_i : 0,  c_i = clamp(v_i, 0, 100) (torch: NaN stays NaN)
+//   out[0..n)  v (identity)
+//   out[n]     loss_adversarial = det > 0 ? det * negw : 0          (negw = -min(w * epoch / 10, w))
+//   out[n+1]   loss_l2_regularization = l2 * rw
+//   out[n+2]   perturbation_l2_norm = l2 (no gradient)
+//   out[n+3]   total = ((v_0 + v_1 + ... + v_{n-1}) + out[n]) + out[n+1]   (parse_losses, dict order)
+// Single lane, the torch composition's fp32 operation order: its values bit for bit, instead of ~60 scalar torch
+// kernels forward and ~40 backward.
+__device__ __forceinline__ float torch_clamp(float v, float lo, float hi) {
+  return v != v ? v : fminf(fmaxf(v, lo), hi);
+}
+__device__ __forceinline__ float center_det(const float* __restrict__ v, int n) {
+  float det = 0.0f;
+  for (int i = 0; i < n; ++i) {
+    const float c = torch_clamp(v[i], 0.0f, 100.0f);
+    det = __fadd_rn(det, isfinite(c) ? c : 0.0f);
+  }
+  return det;
+}
+__global__ __launch_bounds__(64) void k_center_tail_fwd(const float* __restrict__ v, int n, const float* __restrict__ l2p,
+                                                        float negw, float rw, float* __restrict__ out) {
+  if (threadIdx.x != 0) return;
+  const float det = center_det(v, n);
+  const float adv = det > 0.0f ? __fmul_rn(det, negw) : 0.0f;
+  const float l2 = *l2p, reg = __fmul_rn(l2, rw);
+  float total = n > 0 ? v[0] : 0.0f;
+  for (int i = 0; i < n; ++i) out[i] = v[i];
+  for (int i = 1; i < n; ++i) total = __fadd_rn(total, v[i]);
+  total = __fadd_rn(__fadd_rn(total, adv), reg);
+  out[n] = adv;
+  out[n + 1] = reg;
+  out[n + 2] = l2;
+  out[n + 3] = total;
+}
+__global__ __launch_bounds__(64) void k_center_tail_bwd(const float* __restrict__ v, int n, float negw, float rw,
+                                                        const float* __restrict__ g, float* __restrict__ gv,
+                                                        float* __restrict__ gl2) {
+  const float gt = g[n + 3];
+  const float det = center_det(v, n);
+  const float ddet = det > 0.0f ? __fmul_rn(__fadd_rn(g[n], gt), negw) : 0.0f;
+  for (int i = threadIdx.x; i < n; i += 64) {
+    const float c = torch_clamp(v[i], 0.0f, 100.0f);
+    const bool pass = isfinite(c) && v[i] >= 0.0f && v[i] <= 100.0f;   // clamp's gradient mask is inclusive
+    gv[i] = __fadd_rn(__fadd_rn(g[i], gt), pass ? ddet : 0.0f);
+  }
+  if (threadIdx.x == 0) *gl2 = __fmul_rn(__fadd_rn(g[n + 1], gt), rw);
+}
+
 // ------------------------------------------------------------------ clip_grad_norm_ + AdamW
 constexpr int kChunk = RPC_OPTIM_CHUNK;
 constexpr int OBLK = 256;
@@ -251,6 +302,23 @@ extern "C" int rpc_loss_tail_backward(const float* pert_losses, float reg_coef, 
   if (!pert_losses || !grad_out || !grad_head || !grad_pert) return RPC_ERR_ARG;
   hipLaunchKernelGGL(k_loss_tail_bwd, dim3(1), dim3(64), 0, (hipStream_t)stream, pert_losses, reg_coef, grad_out,
                      grad_head, grad_pert);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_center_tail_forward(const float* task_losses, int n, const float* l2, float negw, float rw,
+                                       float* out, void* stream) {
+  if (!task_losses || !l2 || !out || n < 0 || n > 256) return RPC_ERR_ARG;
+  hipLaunchKernelGGL(k_center_tail_fwd, dim3(1), dim3(64), 0, (hipStream_t)stream, task_losses, n, l2, negw, rw, out);
+  RPC_LAUNCH_CHECK();
+  return RPC_OK;
+}
+
+extern "C" int rpc_center_tail_backward(const float* task_losses, int n, float negw, float rw, const float* grad_out,
+                                        float* grad_losses, float* grad_l2, void* stream) {
+  if (!task_losses || !grad_out || !grad_losses || !grad_l2 || n < 0 || n > 256) return RPC_ERR_ARG;
+  hipLaunchKernelGGL(k_center_tail_bwd, dim3(1), dim3(64), 0, (hipStream_t)stream, task_losses, n, negw, rw, grad_out,
+                     grad_losses, grad_l2);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -24,6 +24,7 @@ from typing import Dict, List
 import torch
 from torch import Tensor
 
+from robustpointclouds_amd.adversarial_loss import FusedLosses, center_combination, fused_center_tail
 from robustpointclouds_amd.centerpoint import CenterPoint
 from robustpointclouds_amd.registry import MODELS as _LOCAL_MODELS
 from robustpointclouds_amd.voxelnet import HardSimpleVFE
@@ -90,7 +91,10 @@ class AdversarialCenterPoint(CenterPoint):
         if batch_inputs_dict.get("points", None) is not None or "voxels" in batch_inputs_dict:
             vd = dict(batch_inputs_dict["voxels"])
             vd.setdefault("batch_size", batch_inputs_dict.get("batch_size"))
-            losses.update(self.loss_by_feat_single(vd, batch_data_samples, **kwargs))
+            res = self.loss_by_feat_single(vd, batch_data_samples, **kwargs)
+            if isinstance(res, FusedLosses):   # keeps the fused tail's parse_losses total
+                return res
+            losses.update(res)
         return losses
 
     def loss_by_feat_single(self, voxel_dict, batch_data_samples, **kwargs):
@@ -103,16 +107,14 @@ class AdversarialCenterPoint(CenterPoint):
         device = voxel_dict["voxels"].device
         zero = lambda: torch.zeros((), device=device, requires_grad=True)
         if self.training and self._current_l2_norm is not None:
-            det = torch.zeros((), device=device)
-            for k, v in losses.items():
-                if "loss" in k and isinstance(v, torch.Tensor):
-                    c = torch.clamp(v, min=0.0, max=100.0)
-                    det = det + torch.where(torch.isfinite(c), c, torch.zeros_like(c))
             w = min(self.adversarial_loss_weight * (self._epoch / 10.0), self.adversarial_loss_weight)
-            adv = -w * det
-            losses["loss_adversarial"] = torch.where(det > 0, adv, torch.zeros_like(adv))
-            losses["loss_l2_regularization"] = self.regularization_weight * self._current_l2_norm
-            losses["perturbation_l2_norm"] = self._current_l2_norm.detach()
+            # the HIP tail (csrc/step_tail.hip) over the CenterHead's packed losses: the same values bit for
+            # bit as the torch composition, in one launch each way instead of ~100 scalar kernels
+            fused = fused_center_tail(losses, getattr(losses, "packed", None), self._current_l2_norm, w,
+                                      self.regularization_weight)
+            if fused is not None:
+                return fused
+            losses = center_combination(losses, self._current_l2_norm, w, self.regularization_weight, device)
         else:
             losses["loss_adversarial"] = zero()
             losses["loss_l2_regularization"] = zero()

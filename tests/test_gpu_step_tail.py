@@ -122,3 +122,46 @@ def test_clip_adamw_gradient_views_at_odd_offsets():
             torch.testing.assert_close(x.detach(), y.detach(), rtol=2e-6, atol=1e-8)
         ours.zero_grad()
         ref.zero_grad()
+
+
+@pytest.mark.parametrize("case", ["plain", "edges", "all_zero"])
+@pytest.mark.parametrize("epoch", [3, 12])
+def test_center_tail_matches_torch_combination(case, epoch):
+    """AdversarialCenterPoint's fused tail (rpc_center_tail_*) against the torch composition it replaces
+    (adversarial_loss.center_combination, the CPU path the centerpoint_* golden fixtures pin) + parse_losses on
+    the same 12 task losses: values bit-exact, gradients within 1e-6 — including NaN / inf / negative / > 100
+    entries (skipped or clamped) and all-zero losses (det = 0: no adversarial term)."""
+    from robustpointclouds_amd.adversarial_loss import center_combination, fused_center_tail
+    from robustpointclouds_amd.center_head import PackedCenterLosses
+    vals = {"plain": [0.71, 2.3, 0.12, 1.9, 0.05, 3.3, 0.4, 1.1, 0.9, 2.7, 0.33, 0.8],
+            "edges": [0.71, float("nan"), -0.5, 150.0, 0.0, 100.0, float("inf"), 1.1, 0.9, -float("inf"), 0.33, 0.8],
+            "all_zero": [0.0] * 12}[case]
+
+    def inputs():
+        v = torch.tensor(vals, device=DEV, requires_grad=True)
+        l2 = (torch.tensor([0.0, 0.37], device=DEV, requires_grad=True))
+        return v, l2
+
+    def as_dict(v):
+        d = PackedCenterLosses({f"task{t}.{k}": v[2 * t + j] for t in range(6)
+                                for j, k in enumerate(("loss_heatmap", "loss_bbox"))})
+        d.packed = v
+        return d
+
+    w = min(0.05 * epoch / 10.0, 0.05)
+    v1, l2a = inputs()
+    fused = fused_center_tail(as_dict(v1), v1, l2a[1], w, 0.005)
+    assert isinstance(fused, FusedLosses)
+    tot_f, log_f = parse_losses(fused)
+    v2, l2b = inputs()
+    ref = center_combination(as_dict(v2), l2b[1], w, 0.005, DEV)
+    tot_r, log_r = parse_losses(ref)
+    assert list(log_f) == list(log_r)
+    for k in log_r:
+        a, b = log_f[k].detach(), log_r[k].detach()
+        assert torch.equal(a, b) or (torch.isnan(a) and torch.isnan(b)), (k, a, b)
+    if torch.isfinite(tot_r):
+        tot_f.backward()
+        tot_r.backward()
+        torch.testing.assert_close(v1.grad, v2.grad, rtol=1e-6, atol=0)
+        torch.testing.assert_close(l2a.grad, l2b.grad, rtol=1e-6, atol=0)

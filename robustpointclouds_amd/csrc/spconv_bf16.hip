@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 #include <string.h>
 #include <algorithm>
+#include <type_traits>
 
 #include "common.h"
 #include <stdlib.h>
@@ -639,8 +640,13 @@ __global__ __launch_bounds__(BLK) void k_wprep_batch(SWprepBatch b) {
 // sub-tile the dz rows (shared by the KG offsets) and the gathered h rows are staged ROW-MAJOR
 // in LDS (one ds_write_b128 per 16-B chunk) and read back column-wise with ds_read_b64_tr_b16.
 // Row pitch = C + 16 elements and the (group, half, q) -> row map below make the transposed
-// reads conflict-free for C = 32/64/128. The neighbour indices of 512 rows are preloaded into
-// LDS so the gathers of sub-tile s+1 are issued (register staging) before the MFMAs of sub-tile s.
+// reads conflict-free for C = 32/64/128.
+// Loads run as a three-stage register pipeline over the sub-tiles t of the chunk: the neighbour
+// indices of t + 3 and the row gathers of t + 2 are issued while the MFMAs of t run (two sub-tiles
+// of gathers in flight; r05: one, behind an LDS index stage whose every read was waited out before
+// its gather was issued). Every load is issued unconditionally — a missing neighbour, a row past
+// the chunk or an idle lane reads a zero row (indices: an offset past the buffer range) — so the
+// compiler counts the loads in flight and each wait retires exactly one stage.
 // Partial slabs [chunk][K][ci][co] are reduced in a fixed order by k_slab_reduce (common.h).
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -658,18 +664,28 @@ __device__ __forceinline__ uint4 f16x8_to_bf16x8(uint4 v) {
   return *(const uint4*)o;
 }
 
-// weight-gradient block: 4 waves; 8 for the 128 x 128 tiles, whose 3 offsets per block (KG = 3) then fit
-// 24 accumulator tiles per wave (192 VGPRs, no spill): each staged dz sub-tile serves 3 offsets instead
-// of 1 — CenterPoint k_wgrad_bf16<128,128> 458 -> 403 us per launch (r04_step_kernels_centerpoint_wg3.txt;
-// the step unchanged: these run on the side stream beside the data-gradient chain)
-__host__ __device__ constexpr int wg_threads(int ci, int co) { return ci * co >= 128 * 128 ? 512 : 256; }
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));   // first-class 16-B value (HIP's uint4 is a
+// struct: its copies were memcpys that kept the load registers in scratch)
+__device__ __attribute__((aligned(16))) u32x4 g_wg_zero[1];
+template <int P, class T>
+__device__ __forceinline__ T& pick(T& a, T& b) {
+  if constexpr (P == 0) return a; else return b;
+}   // the row a masked gather reads (zeros)
+
+// weight-gradient block: 4 waves; 8 from 64 x 64 up. With 3 offsets per block (KG = 3) each staged dz
+// sub-tile serves 3 offsets (CenterPoint k_wgrad_bf16<128,128> 458 -> 403 us per launch at r04,
+// r04_step_kernels_centerpoint_wg3.txt); 8 waves halve each thread's share of the two gather stages in
+// flight, which keeps the 64-channel tiles at 2 blocks per CU (<= 128 VGPRs)
+__host__ __device__ constexpr int wg_threads(int ci, int co) { return ci * co >= 64 * 64 ? 512 : 256; }
+__host__ __device__ constexpr int wg_min_blocks(int ci, int co) {
+  return ci * co >= 128 * 128 ? 1 : (ci * co >= 64 * 64 ? 2 : 4);
+}
 template <int CI, int CO, int KG, bool HF16 = false>
-__global__ __launch_bounds__(wg_threads(CI, CO), (CI * CO <= 32 * 32) ? 4 : 1) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
+__global__ __launch_bounds__(wg_threads(CI, CO), wg_min_blocks(CI, CO)) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
                                                     int K, int N, int rows_per, const u16* __restrict__ dz, int DP,
                                                     float* __restrict__ part) {
   constexpr int TB = wg_threads(CI, CO), NWV = TB / 64;   // threads, waves
   constexpr int RT = 64;                                   // rows per sub-tile (2 MFMA k-steps)
-  constexpr int SEG = 512;                                 // rows per neighbour preload
   constexpr int CIR = (CI + 15) / 16 * 16;
   constexpr int PA = CIR + 16, PD = CO + 16;               // LDS row pitch (elements)
   constexpr int MT = CIR / 16, NT = CO / 16;
@@ -680,7 +696,7 @@ __global__ __launch_bounds__(wg_threads(CI, CO), (CI * CO <= 32 * 32) ? 4 : 1) v
   constexpr int NA = (RT * CA + TB - 1) / TB, ND = (RT * CD + TB - 1) / TB;
   __shared__ __attribute__((aligned(16))) u16 sA[KG][RT * PA];
   __shared__ __attribute__((aligned(16))) u16 sD[RT * PD];
-  __shared__ int sN[SEG * KG];
+  __shared__ unsigned sAny[4][NWV];                        // per sub-tile (ring of 4): offsets with a neighbour
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int wm = w % WM, wn = w / WM;
   // 1-D grid over (chunk, offset group), XCD-aware: the groups of one row chunk are consecutive items on
@@ -690,6 +706,7 @@ __global__ __launch_bounds__(wg_threads(CI, CO), (CI * CO <= 32 * 32) ? 4 : 1) v
   const int item = dn::xcd_remap(blockIdx.x, gridDim.x);
   const int chunk = item / ngroups, k0 = (item - chunk * ngroups) * KG;
   const int rb0 = chunk * rows_per, rb1 = min(N, rb0 + rows_per);
+  const int nsub = rb1 > rb0 ? (rb1 - rb0 + RT - 1) / RT : 0;
   f32x4 acc[KG][TPW];
 #pragma unroll
   for (int g = 0; g < KG; ++g)
@@ -701,105 +718,127 @@ __global__ __launch_bounds__(wg_threads(CI, CO), (CI * CO <= 32 * 32) ? 4 : 1) v
   // transposed-read lane geometry: group g4, lane i = 4q + p of the group
   const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3;
   const int rowoff = 4 * g4 + qq;                          // + 16*half + 32*kstep
-  uint4 ra[KG][NA], rd[ND];
-  for (int seg = rb0; seg < rb1; seg += SEG) {
-    const int se = min(rb1, seg + SEG);
-    __syncthreads();
-    {
-      // all of a thread's index loads in flight at once, from clamped addresses (a guarded load per
-      // pass compiled to a branch that waited for its load before the next pass: 2-6 round trips)
-      // (32-bit buffer offsets; an index outside the map reads as -1 via the OOB-zero + select)
-      constexpr int NQ = (SEG * KG + TB - 1) / TB;
-      const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc((void*)nbr, (short)0, 0x7fffffff, 0x00020000);
-      int v[NQ];
+  const u32x4* const zrow = g_wg_zero;
+  constexpr unsigned OOB = 0x80000000u;
+  // (32-bit buffer offsets for the indices: the host checks n_out * K * 4 < 2^31)
+  const __amdgpu_buffer_rsrc_t rn = __builtin_amdgcn_make_buffer_rsrc((void*)nbr, (short)0, 0x7fffffff, 0x00020000);
+  // the neighbour index of (row slot j, offset g) of sub-tile t: raw value (0 when masked: see a_ok)
+  auto load_idx = [&](int t, int (&I)[KG][NA]) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < NQ; ++i) {
-        const int q = tid + i * TB, r = q / KG, g = q - r * KG, row = seg + r, k = k0 + g;
-        unsigned off = (q < SEG * KG && row < se && k < K) ? (unsigned)(row * K + k) * 4u : 0x80000000u;
+    for (int j = 0; j < NA; ++j) {
+      const int q = tid + j * TB, row = rb0 + t * RT + q / CA;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        unsigned off = ((RT * CA) % TB == 0 || q < RT * CA) && row < rb1 && k0 + g < K
+                           ? (unsigned)(row * K + k0 + g) * 4u : OOB;
         asm volatile("" : "+v"(off));
-        v[i] = off == 0x80000000u ? -1 : __builtin_amdgcn_raw_buffer_load_b32(rn, off, 0, 0);
+        I[g][j] = __builtin_amdgcn_raw_buffer_load_b32(rn, off, 0, 0);
+      }
+    }
+  };
+  // the gathers of sub-tile t (h rows by the indices I, dz rows), and its per-wave offset mask -> sAny
+  auto load_rows = [&](int t, const int (&I)[KG][NA], u32x4 (&GA)[KG][NA], u32x4 (&GD)[ND]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int q = tid + j * TB, r = q / CD, c8 = q - r * CD, row = rb0 + t * RT + r;
+      const u32x4* p = ((RT * CD) % TB == 0 || q < RT * CD) && row < rb1
+                           ? (const u32x4*)(dz + (long long)row * DP + c8 * 8) : zrow;
+      GD[j] = *p;
+    }
+    unsigned m = 0;
+#pragma unroll
+    for (int j = 0; j < NA; ++j) {
+      const int q = tid + j * TB, r = q / CA, c8 = q - r * CA, row = rb0 + t * RT + r;
+#pragma unroll
+      for (int g = 0; g < KG; ++g) {
+        const bool ok = ((RT * CA) % TB == 0 || q < RT * CA) && row < rb1 && k0 + g < K && I[g][j] >= 0;
+        const u32x4* p = ok ? (const u32x4*)(h + (long long)I[g][j] * HP + c8 * 8) : zrow;
+        GA[g][j] = *p;
+        m |= ok ? 1u << g : 0u;
+      }
+    }
+    unsigned wmask = 0;
+#pragma unroll
+    for (int g = 0; g < KG; ++g) wmask |= __ballot((m >> g) & 1u) != 0 ? 1u << g : 0u;
+    if (lane == 0) sAny[t & 3][w] = wmask;
+  };
+  auto mfma_tile = [&](unsigned any) __attribute__((always_inline)) {
+#pragma unroll
+    for (int ks = 0; ks < RT / 32; ++ks) {
+      const int r0 = 32 * ks + rowoff;
+      bf16x8 bv[WNT];                                    // dz fragments, shared by the KG offsets
+#pragma unroll
+      for (int b = 0; b < WNT; ++b) {
+        const int n = wn + WN * b;
+        s16x4 x[2] = {tr_read(&sD[r0 * PD + n * 16 + 4 * pp]), tr_read(&sD[(r0 + 16) * PD + n * 16 + 4 * pp])};
+        bv[b] = *(bf16x8*)x;
       }
 #pragma unroll
-      for (int i = 0; i < NQ; ++i)
-        if (tid + i * TB < SEG * KG) sN[tid + i * TB] = v[i];
+      for (int g = 0; g < KG; ++g) {
+        if (!((any >> g) & 1u)) continue;
+#pragma unroll
+        for (int a = 0; a < WMT; ++a) {
+          const int m = wm + WM * a;
+          s16x4 x[2] = {tr_read(&sA[g][r0 * PA + m * 16 + 4 * pp]), tr_read(&sA[g][(r0 + 16) * PA + m * 16 + 4 * pp])};
+          bf16x8 av = *(bf16x8*)x;
+#pragma unroll
+          for (int b = 0; b < WNT; ++b)
+            acc[g][a * WNT + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[b], acc[g][a * WNT + b], 0, 0, 0);
+        }
+      }
     }
+  };
+  // step t: stage t's rows (gathered two steps ago) into LDS, issue indices t + 3 and gathers t + 2 (into
+  // the registers just freed), then the MFMAs of t. Register sets ping-pong by the parity P of t, chosen at
+  // compile time (a run-time choice between two register arrays put them in scratch).
+  int I0[KG][NA], I1[KG][NA];
+  u32x4 A0[KG][NA], D0[ND], A1[KG][NA], D1[ND];
+  auto step = [&](auto par, int t) __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    auto& GA = pick<P>(A0, A1);
+    auto& GD = pick<P>(D0, D1);
+    auto& In = pick<P>(I0, I1);
+    auto& If = pick<P>(I1, I0);
+    __syncthreads();   // the MFMAs of t - 1 are done with the LDS tiles
+#pragma unroll
+    for (int j = 0; j < ND; ++j) {
+      const int q = tid + j * TB;
+      if ((RT * CD) % TB == 0 || q < RT * CD) {
+        const int r = q / CD, c8 = q - r * CD;
+        *(u32x4*)&sD[r * PD + c8 * 8] = GD[j];
+      }
+    }
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+#pragma unroll
+      for (int j = 0; j < NA; ++j) {
+        const int q = tid + j * TB;
+        if ((RT * CA) % TB == 0 || q < RT * CA) {
+          const int r = q / CA, c8 = q - r * CA;
+          *(u32x4*)&sA[g][r * PA + c8 * 8] =
+              HF16 ? __builtin_bit_cast(u32x4, f16x8_to_bf16x8(__builtin_bit_cast(uint4, GA[g][j]))) : GA[g][j];
+        }
+      }
     __syncthreads();
-    auto load = [&](int rs) {   // global -> registers for the sub-tile starting at segment row rs
+    unsigned any = 0;
 #pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        int q = tid + j * TB;
-        rd[j] = make_uint4(0u, 0u, 0u, 0u);
-        if (q < RT * CD) {
-          int r = q / CD, c8 = q - r * CD, row = seg + rs + r;
-          if (row < se) rd[j] = *(const uint4*)(dz + (long long)row * DP + c8 * 8);
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < KG; ++g)
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-          int q = tid + j * TB;
-          ra[g][j] = make_uint4(0u, 0u, 0u, 0u);
-          if (q < RT * CA) {
-            int r = q / CA, c8 = q - r * CA;
-            int src = (rs + r < SEG) ? sN[(rs + r) * KG + g] : -1;
-            if (src >= 0) ra[g][j] = *(const uint4*)(h + (long long)src * HP + c8 * 8);
-          }
-        }
-    };
-    load(0);
-    for (int rs = 0; rs < se - seg; rs += RT) {
-      __syncthreads();   // previous sub-tile's MFMAs are done with the LDS tiles
-#pragma unroll
-      for (int j = 0; j < ND; ++j) {
-        int q = tid + j * TB;
-        if (q < RT * CD) {
-          int r = q / CD, c8 = q - r * CD;
-          *(uint4*)&sD[r * PD + c8 * 8] = rd[j];
-        }
-      }
-#pragma unroll
-      for (int g = 0; g < KG; ++g)
-#pragma unroll
-        for (int j = 0; j < NA; ++j) {
-          int q = tid + j * TB;
-          if (q < RT * CA) {
-            int r = q / CA, c8 = q - r * CA;
-            *(uint4*)&sA[g][r * PA + c8 * 8] = HF16 ? f16x8_to_bf16x8(ra[g][j]) : ra[g][j];
-          }
-        }
-      // which offsets have any neighbour in this sub-tile (wave-uniform, from the LDS indices)
-      bool any[KG];
-#pragma unroll
-      for (int g = 0; g < KG; ++g) any[g] = __ballot(sN[min(rs + lane, SEG - 1) * KG + g] >= 0 && rs + lane < SEG) != 0;
-      __syncthreads();
-      if (rs + RT < se - seg) load(rs + RT);               // in flight during the MFMAs below
-#pragma unroll
-      for (int ks = 0; ks < RT / 32; ++ks) {
-        const int r0 = 32 * ks + rowoff;
-        bf16x8 bv[WNT];                                    // dz fragments, shared by the KG offsets
-#pragma unroll
-        for (int b = 0; b < WNT; ++b) {
-          const int n = wn + WN * b;
-          s16x4 x[2] = {tr_read(&sD[r0 * PD + n * 16 + 4 * pp]), tr_read(&sD[(r0 + 16) * PD + n * 16 + 4 * pp])};
-          bv[b] = *(bf16x8*)x;
-        }
-#pragma unroll
-        for (int g = 0; g < KG; ++g) {
-          if (!any[g]) continue;
-#pragma unroll
-          for (int a = 0; a < WMT; ++a) {
-            const int m = wm + WM * a;
-            s16x4 x[2] = {tr_read(&sA[g][r0 * PA + m * 16 + 4 * pp]),
-                          tr_read(&sA[g][(r0 + 16) * PA + m * 16 + 4 * pp])};
-            bf16x8 av = *(bf16x8*)x;
-#pragma unroll
-            for (int b = 0; b < WNT; ++b)
-              acc[g][a * WNT + b] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av, bv[b], acc[g][a * WNT + b], 0, 0, 0);
-          }
-        }
-      }
+    for (int v = 0; v < NWV; ++v) any |= sAny[t & 3][v];
+    load_idx(t + 3, If);
+    load_rows(t + 2, In, GA, GD);
+    mfma_tile(any);
+  };
+  if (nsub > 0) {
+    load_idx(0, I0);
+    load_idx(1, I1);
+    load_rows(0, I0, A0, D0);
+    load_idx(2, I0);
+    load_rows(1, I1, A1, D1);
+    int t = 0;
+    for (; t + 1 < nsub; t += 2) {
+      step(std::integral_constant<int, 0>{}, t);
+      step(std::integral_constant<int, 1>{}, t + 1);
     }
+    if (t < nsub) step(std::integral_constant<int, 0>{}, t);
   }
 #pragma unroll
   for (int g = 0; g < KG; ++g) {

@@ -1,0 +1,99 @@
+"""Standalone timing of the sparse bf16 weight gradient (rpc_spconv_wgrad_bf16, slab reduction included) and of the
+bf16 forward / data-gradient GEMMs on the rulebooks of one bench step: a training step runs with a KernelTimer that
+records every sparse launch's neighbour table; each bf16 layer is then re-timed ALONE (random bf16 rows of the same
+shapes, median of rounds), next to its in-step time from the same timer (which runs beside the other stream).
+
+    python tools/spwg_bench.py [centerpoint|voxelnet] [ops=wgrad,fwd,dgrad]
+Knob: RPC_SPWG_VARIANTS="0,1" times rpc_sparse_tune(1, v) per value (weight-gradient kernel variant)."""
+import collections
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from robustpointclouds_amd import _ffi  # noqa: E402
+from robustpointclouds_amd.sparse_encoder import KernelTimer  # noqa: E402
+from robustpointclouds_amd.trainer import Trainer, make_kitti_model, make_nus_model  # noqa: E402
+
+
+def r8(c):
+    return (c + 7) // 8 * 8
+
+
+def timeit(fn, iters=10, rounds=5):
+    fn()
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        e1.synchronize()
+        ts.append(e0.elapsed_time(e1) * 1e3 / iters)
+    return sorted(ts)[len(ts) // 2]
+
+
+def main():
+    model_name = sys.argv[1] if len(sys.argv) > 1 else "centerpoint"
+    ops = (sys.argv[2] if len(sys.argv) > 2 else "wgrad").split(",")
+    variants = [int(v) for v in os.environ.get("RPC_SPWG_VARIANTS", "0").split(",")]
+    dev = torch.device("cuda")
+    torch.manual_seed(0)
+    if model_name == "centerpoint":
+        model = make_nus_model(device=dev, epoch=3)
+        data = bench._nus_batches(2, 4, 0, dev)
+    else:
+        model = make_kitti_model(num_classes=3, device=dev, epoch=3)
+        data = bench._batches(2, 6, 0, dev, 3)
+    tr = Trainer(model, bf16=True, device=dev)
+    for i in range(3):
+        tr.train_step(*data[i % 2], next_points=data[(i + 1) % 2][0])
+    torch.cuda.synchronize()
+    timer = KernelTimer()
+    model.middle_encoder.timer = timer
+    timer.enabled = True
+    tr.train_step(*data[1], next_points=data[0][0])
+    torch.cuda.synchronize()
+    timer.enabled = False
+    lib = _ffi.load()
+    st = _ffi.stream_of(torch.empty(1, device=dev))
+    tot = collections.defaultdict(float)
+    for (e0, e1, nbr, ci, co, kname, dt) in timer.recs:
+        if dt != "bf16":
+            continue
+        op = "wgrad" if "wgrad" in kname else ("fwd" if kname.endswith(", 0>") or ", 0, " in kname else "other")
+        if op not in ops:
+            continue
+        instep = e0.elapsed_time(e1) * 1e3
+        n_out, K = nbr.shape
+        n_in = int(nbr.max().item()) + 1
+        pairs = int((nbr >= 0).sum().item())
+        fl = 2.0 * pairs * ci * co
+        h = (torch.rand(n_in, r8(ci), device=dev) * 2 - 1).to(torch.bfloat16)
+        dz = (torch.rand(n_out, r8(co), device=dev) * 2 - 1).to(torch.bfloat16)
+        row = [f"{kname:42s} n_out {n_out:7d} pairs {pairs:8d} in-step {instep:7.1f} us"]
+        if op == "wgrad":
+            wsz = lib.rpc_spconv_wgrad_bf16_workspace_size(n_out, K, ci, co)
+            ws = _ffi.workspace(wsz, dev)
+            dW = torch.empty(K, ci, co, device=dev)
+            for v in variants:
+                lib.rpc_sparse_tune(1, v)
+
+                def run():
+                    _ffi.check(lib.rpc_spconv_wgrad_bf16(_ffi.ptr(h), ci, _ffi.ptr(nbr), K, n_out, _ffi.ptr(dz), co,
+                                                         _ffi.ptr(dW), _ffi.ptr(ws), wsz, st), "wgrad")
+                us = timeit(run)
+                tot[v] += us
+                row.append(f"v{v} {us:7.1f} us {fl / (us * 1e-6) / 1e12:6.1f} TF")
+            lib.rpc_sparse_tune(1, 0)
+        print("  ".join(row), flush=True)
+    print("total standalone us per variant:", {k: round(v, 1) for k, v in tot.items()}, flush=True)
+
+
+if __name__ == "__main__":
+    main()

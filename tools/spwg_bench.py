@@ -66,7 +66,12 @@ def main():
     for (e0, e1, nbr, ci, co, kname, dt) in timer.recs:
         if dt != "bf16":
             continue
-        op = "wgrad" if "wgrad" in kname else ("fwd" if kname.endswith(", 0>") or ", 0, " in kname else "other")
+        if "wgrad" in kname:
+            op = "wgrad"
+        elif "k_gemm_bf16" in kname:
+            op = "fwd" if kname.rstrip(">").split(",")[2].strip() == "0" else "dgrad"
+        else:
+            continue
         if op not in ops:
             continue
         instep = e0.elapsed_time(e1) * 1e3
@@ -91,8 +96,26 @@ def main():
                 tot[v] += us
                 row.append(f"v{v} {us:7.1f} us {fl / (us * 1e-6) / 1e12:6.1f} TF")
             lib.rpc_sparse_tune(1, 0)
+        else:
+            # the GEMM core on this rulebook, plain epilogue (submanifold layers: map = nbr, the data gradient
+            # reads it reversed; strided layers are skipped — their data gradient runs on the input-side map)
+            if nbr.shape[0] != n_in:
+                continue
+            kg, ng = (ci, co) if op == "fwd" else (co, ci)
+            NGP, KGP = (ng + 15) // 16 * 16, (kg + 31) // 32 * 32
+            a = (torch.rand(n_out, r8(kg), device=dev) * 2 - 1).to(torch.bfloat16)
+            bt = (torch.rand(K, NGP, KGP, device=dev) * 0.1).to(torch.bfloat16)
+            out = torch.empty(n_out, ng, device=dev)
+            rev = 0 if op == "fwd" else 1
+
+            def run():
+                _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(a), n_out, kg, _ffi.ptr(nbr), K, rev, n_out, _ffi.ptr(bt), ng,
+                                                      _ffi.ptr(out), None, None, None, 2, st), "gemm")
+            us = timeit(run)
+            tot[op] += us
+            row.append(f"v0 {us:7.1f} us {fl / (us * 1e-6) / 1e12:6.1f} TF (plain epilogue)")
         print("  ".join(row), flush=True)
-    print("total standalone us per variant:", {k: round(v, 1) for k, v in tot.items()}, flush=True)
+    print("total standalone us per variant / op:", {k: round(v, 1) for k, v in tot.items()}, flush=True)
 
 
 if __name__ == "__main__":

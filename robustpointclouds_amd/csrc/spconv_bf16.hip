@@ -675,13 +675,15 @@ __device__ __forceinline__ T& pick(T& a, T& b) {
 // weight-gradient block: 4 waves; 8 from 64 x 64 up. With 3 offsets per block (KG = 3) each staged dz
 // sub-tile serves 3 offsets (CenterPoint k_wgrad_bf16<128,128> 458 -> 403 us per launch at r04,
 // r04_step_kernels_centerpoint_wg3.txt); 8 waves halve each thread's share of the two gather stages in
-// flight, which keeps the 64-channel tiles at 2 blocks per CU (<= 128 VGPRs)
+// flight (64 x 64: 100 VGPRs, two blocks per CU). HIP's second launch bound is the minimum number of waves
+// per SIMD: capping 64 x 128 at 128 VGPRs (4) spilled and measured slower than 154 VGPRs at one block per CU
+// (159.7 vs 147.4 us standalone, gpurun_out r05wg4)
 __host__ __device__ constexpr int wg_threads(int ci, int co) { return ci * co >= 64 * 64 ? 512 : 256; }
-__host__ __device__ constexpr int wg_min_blocks(int ci, int co) {
+__host__ __device__ constexpr int wg_min_waves(int ci, int co) {
   return ci * co >= 128 * 128 ? 1 : (ci * co >= 64 * 64 ? 2 : 4);
 }
 template <int CI, int CO, int KG, bool HF16 = false>
-__global__ __launch_bounds__(wg_threads(CI, CO), wg_min_blocks(CI, CO)) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
+__global__ __launch_bounds__(wg_threads(CI, CO), wg_min_waves(CI, CO)) void k_wgrad_bf16(const u16* __restrict__ h, int HP, const int* __restrict__ nbr,
                                                     int K, int N, int rows_per, const u16* __restrict__ dz, int DP,
                                                     float* __restrict__ part) {
   constexpr int TB = wg_threads(CI, CO), NWV = TB / 64;   // threads, waves

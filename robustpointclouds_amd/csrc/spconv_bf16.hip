@@ -31,23 +31,26 @@ namespace spb {
 
 constexpr int BLK = 256;
 constexpr int BM = 64;          // rows per BatchNorm partial row (rpc_spconv_gemm_blocks)
-// GEMM waves per block (16 rows each; all share one LDS weight tile per offset): 8 — the tile is
-// fetched once per 128 rows — unless the 128 x 128 tiles' LDS ring would leave one block per CU
+// GEMM waves per block (16 x RT rows each; all share one LDS weight tile per step): 8 — the tile is
+// fetched once per 128 rows — except the 128 x 128 tiles: 4 waves of 32 rows
 __host__ __device__ constexpr int gw_of(int kgp, int nt) { return kgp * nt * 16 >= 128 * 128 ? 4 : 8; }
 // 16-row MFMA tiles per wave: every weight fragment a wave reads from LDS feeds RT MFMAs. Two for the
 // mid-size tiles (K x 16*NT of 32x32 .. 64x32), whose time went to LDS weight reads (every wave re-read
 // the whole tile per offset for its 16 rows): r02v30 <32,2,0> 35.0 -> 30.0 us, <32,2,1> 38.5 -> 36.5,
 // <64,2,1> 49 -> 42. Measured and kept at RT=1: the 64x64 tiles (88 VGPRs, 5 waves/SIMD: <64,4,1>
 // 47 -> 54 us) and the 32x16 tiles (<32,1,0> 21.3 -> 23.4 us). The 128 x 128 tiles (CenterPoint) take two
-// (128-row blocks, one per CU: 88 KB of LDS, 262 registers): forward 259 -> 262, data gradient 624 -> 606,
-// plain 407 -> 370 us per launch (profiles/r04_step_kernels_centerpoint_rt2.txt) — the weight tile
-// staging and its LDS reads were not the limit either; the data-gradient launches run beside the
-// 128 x 128 weight gradient on the side stream
+// (r04, then one 128-row block per CU: forward 259 -> 262, data gradient 624 -> 606, plain 407 -> 370 us per
+// launch, profiles/r04_step_kernels_centerpoint_rt2.txt; since r05 two blocks per CU, see ksplit_of)
 __host__ __device__ constexpr int rt_of(int kgp, int nt) {
   return ((kgp * nt >= 64 && kgp * nt <= 128 && nt <= 4) || (kgp == 128 && nt == 8)) ? 2 : 1;
 }
+// K halves per offset step: the 128 x 128 tiles stage their weight tile half a K at a time (2 x 20 KB of LDS
+// instead of 2 x 34 KB), so two 128-row blocks share a CU (r05: one, with 88 KB of LDS and 262 VGPRs — the
+// launch was bound by the rows one block keeps in flight: 4 x 32-row and 8 x 16-row wave layouts timed the same).
+// Standalone 279 -> 190 us per launch, CenterPoint 179-180 -> 188-189 frames/s (profiles/r05_gemm128_ksplit_ab.txt)
+__host__ __device__ constexpr int ksplit_of(int kgp, int nt) { return (kgp == 128 && nt == 8) ? 2 : 1; }
 __host__ __device__ constexpr int gemm_waves_per_simd(int kgp, int nt) {
-  return kgp * nt >= 1024 ? 1 : rt_of(kgp, nt) == 2 ? 5 : ((kgp * nt <= 256 && nt <= 4 && kgp <= 64) ? 8 : 1);
+  return kgp * nt >= 1024 ? 2 : rt_of(kgp, nt) == 2 ? 5 : ((kgp * nt <= 256 && nt <= 4 && kgp <= 64) ? 8 : 1);
 }
 constexpr int MAXK = 27;
 
@@ -178,10 +181,10 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
   constexpr int RT = rt_of(KGP, NT), GW = gw_of(KGP, NT), GBLK = 64 * GW, WR = 16 * RT, GBM = WR * GW;
   constexpr int KS = KGP / 32;
   constexpr int NGP = NT * 16;
-  // LDS row stride: 8 mod 16 dwords (conflict-free b128 reads), except the 128 x 128 tiles, whose
-  // smaller 16-B pad keeps two blocks per CU (a 144-element pitch leaves one: 1.7x slower)
-  constexpr int LS = (KGP >= 128 && NT >= 8) ? KGP + 8 : KGP + 16;
-  constexpr int BV = NGP * KGP / 8;           // 16-B vectors per offset tile
+  constexpr int KSP = ksplit_of(KGP, NT), KGH = KGP / KSP, KSH = KS / KSP;   // K halves per offset step
+  // LDS row stride: 8 mod 16 dwords (conflict-free b128 reads)
+  constexpr int LS = KGH + 16;
+  constexpr int BV = NGP * KGH / 8;           // 16-B vectors per step's weight tile
   constexpr int BPT = (BV + GBLK - 1) / GBLK;
   __shared__ __attribute__((aligned(16))) u16 sB[2][NGP * LS];
   __shared__ int sN[GBM * MAXK];
@@ -249,12 +252,12 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
 
   const int arow = w * WR + (lane & 15);
   const int ag = lane >> 4;
-  auto load_b = [&](int k, uint4 (&dst)[BPT]) {
-    const unsigned base = (unsigned)k * (unsigned)(NGP * KGP * 2);
+  auto load_b = [&](int k, int kh, uint4 (&dst)[BPT]) {
+    const unsigned base = (unsigned)k * (unsigned)(NGP * KGP * 2) + (unsigned)(kh * KGH * 2);
 #pragma unroll
     for (int j = 0; j < BPT; ++j) {
-      const int v = tid + j * GBLK;
-      unsigned off = (BV % GBLK == 0 || v < BV) ? base + (unsigned)v * 16u : OOB;
+      const int v = tid + j * GBLK, e = v * 8, n = e / KGH, c = e - n * KGH;
+      unsigned off = (BV % GBLK == 0 || v < BV) ? base + (unsigned)(n * KGP + c) * 2u : OOB;
       asm volatile("" : "+v"(off));
       dst[j] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsb, off, 0, 0));
     }
@@ -264,7 +267,7 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     for (int j = 0; j < BPT; ++j) {
       int v = tid + j * GBLK;
       if (BV % GBLK == 0 || v < BV) {
-        int e = v * 8, n = e / KGP, c = e - n * KGP;
+        int e = v * 8, n = e / KGH, c = e - n * KGH;
         *(uint4*)&sB[buf][n * LS + c] = src[j];
       }
     }
@@ -276,39 +279,42 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     // returns as zeros. With conditional loads the compiler could not count the loads in flight: the
     // weight-tile LDS store waited on vmcnt(0), i.e. for the next offset's gathers too, every offset.
     // Offsets are 32-bit: the host checks that the source table and the weight tiles fit below 2 GB.
-    auto load_a = [&](int k, uint4 (&dst)[RT][KS]) {
+    auto load_a = [&](int k, int kh, uint4 (&dst)[RT][KSH]) {
 #pragma unroll
       for (int rt = 0; rt < RT; ++rt) {
         const int src = sN[(arow + rt * 16) * MAXK + k];
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
-          const int c0 = ks * 32 + ag * 8;
+        for (int ks = 0; ks < KSH; ++ks) {
+          const int c0 = (kh * KSH + ks) * 32 + ag * 8;
           unsigned off = (src >= 0 && c0 < g.CP) ? ((unsigned)src * (unsigned)g.CP + (unsigned)c0) * 2u : OOB;
           asm volatile("" : "+v"(off));   // keeps the select a select (else: one load per branch of a diamond)
           dst[rt][ks] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rsa, off, 0, 0));
         }
       }
     };
-    uint4 a0[RT][KS], a1[RT][KS], bw0[BPT], bw1[BPT];
-    load_b(klist[0], bw0);
+    // steps t = offset index * KSP + K half
+    const int NS = NK * KSP;
+    uint4 a0[RT][KSH], a1[RT][KSH], bw0[BPT], bw1[BPT];
+    load_b(klist[0], 0, bw0);
     store_b(0, bw0);
-    load_b(klist[NK > 1 ? 1 : 0], bw0);
-    load_a(klist[0], a0);
+    load_b(klist[(NS > 1 ? 1 : 0) / KSP], (NS > 1 ? 1 : 0) % KSP, bw0);
+    load_a(klist[0], 0, a0);
     __syncthreads();
     // one offset per step. Loads run ahead: the A fragments of offset t+1 and the weight tile of
     // offset t+2 are issued at the top of step t, so the LDS store of tile t+1 (loaded one step
     // earlier) and the MFMAs of offset t wait only on loads a whole step old. A fragments and weight
     // registers ping-pong (a0 / a1, bw0 / bw1: no register copy that would wait on the newest loads);
     // the steps near the end re-fetch the last offset so the load count per step is fixed.
-    auto step = [&](int t, const uint4 (&ac)[RT][KS], uint4 (&an)[RT][KS], const uint4 (&bc)[BPT],
+    auto step = [&](int t, const uint4 (&ac)[RT][KSH], uint4 (&an)[RT][KSH], const uint4 (&bc)[BPT],
                     uint4 (&bn)[BPT]) {
-      const int k = klist[t];
-      load_b(klist[t + 2 < NK ? t + 2 : NK - 1], bn);
-      load_a(klist[t + 1 < NK ? t + 1 : t], an);
+      const int k = klist[t / KSP];
+      const int t2 = t + 2 < NS ? t + 2 : NS - 1, t1 = t + 1 < NS ? t + 1 : t;
+      load_b(klist[t2 / KSP], t2 % KSP, bn);
+      load_a(klist[t1 / KSP], t1 % KSP, an);
       if ((my >> k) & 1u) {
         const u16* bb = sB[t & 1] + (lane & 15) * LS + ag * 8;
 #pragma unroll
-        for (int ks = 0; ks < KS; ++ks) {
+        for (int ks = 0; ks < KSH; ++ks) {
 #pragma unroll
           for (int n = 0; n < NT; ++n) {
             const uint4 bv = *(const uint4*)(bb + n * 16 * LS + ks * 32);
@@ -324,11 +330,11 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
     // gave the compiler a path step(t) -> step(t+2) on which a1's gathers were still in flight, and a
     // vmcnt(0) at the loop head for it)
     int t = 0;
-    for (; t + 1 < NK; t += 2) {
+    for (; t + 1 < NS; t += 2) {
       step(t, a0, a1, bw0, bw1);
       step(t + 1, a1, a0, bw1, bw0);
     }
-    if (t < NK) step(t, a0, a1, bw0, bw1);
+    if (t < NS) step(t, a0, a1, bw0, bw1);
   };
   if (NK > 0) mainloop();
 

@@ -3,7 +3,7 @@ bf16 forward / data-gradient GEMMs on the rulebooks of one bench step: a trainin
 records every sparse launch's neighbour table; each bf16 layer is then re-timed ALONE (random bf16 rows of the same
 shapes, median of rounds), next to its in-step time from the same timer (which runs beside the other stream).
 
-    python tools/spwg_bench.py [centerpoint|voxelnet] [ops=wgrad,fwd,dgrad]
+    python tools/spwg_bench.py [centerpoint|voxelnet] [ops=wgrad,fwd,dgrad,sdgrad]
 Knob: RPC_SPWG_VARIANTS="0,1" times rpc_sparse_tune(1, v) per value (weight-gradient kernel variant)."""
 import collections
 import os
@@ -72,7 +72,7 @@ def main():
             op = "fwd" if kname.rstrip(">").split(",")[2].strip() == "0" else "dgrad"
         else:
             continue
-        if op not in ops:
+        if op not in ops and not (op == "fwd" and "sdgrad" in ops):
             continue
         instep = e0.elapsed_time(e1) * 1e3
         n_out, K = nbr.shape
@@ -96,10 +96,33 @@ def main():
                 tot[v] += us
                 row.append(f"v{v} {us:7.1f} us {fl / (us * 1e-6) / 1e12:6.1f} TF")
             lib.rpc_sparse_tune(1, 0)
+        elif op == "fwd" and nbr.shape[0] != n_in and "sdgrad" in ops:
+            # a strided layer: its data gradient runs on the input-side map nbr_in[i][k] = o (nbr[o][k] = i),
+            # timed as is and with the input rows grouped by neighbour mask (stable sort: rows of one block then
+            # share their few offsets — for stride 2 the coordinate parity decides which ones)
+            o_idx, k_idx = torch.nonzero(nbr >= 0, as_tuple=True)
+            nin = torch.full((n_in, K), -1, dtype=torch.int32, device=dev)
+            nin[nbr[o_idx, k_idx].long(), k_idx] = o_idx.to(torch.int32)
+            bits = (1 << torch.arange(K, device=dev, dtype=torch.int64))
+            mask = ((nin >= 0).to(torch.int64) * bits).sum(1)
+            nin_sorted = nin[torch.sort(mask, stable=True).indices].contiguous()
+            NGP, KGP = (ci + 15) // 16 * 16, (co + 31) // 32 * 32
+            a = (torch.rand(n_out, r8(co), device=dev) * 2 - 1).to(torch.bfloat16)
+            bt = (torch.rand(K, NGP, KGP, device=dev) * 0.1).to(torch.bfloat16)
+            out = torch.empty(n_in, ci, device=dev)
+            for tag, mp in (("as is", nin), ("mask-sorted", nin_sorted)):
+                def run():
+                    _ffi.check(lib.rpc_spconv_gemm_bf16_n(_ffi.ptr(a), n_out, co, _ffi.ptr(mp), K, 0, n_in, _ffi.ptr(bt),
+                                                          ci, _ffi.ptr(out), None, None, None, 2, st), "gemm")
+                us = timeit(run)
+                tot["sdgrad " + tag] += us
+                row.append(f"dgrad {tag} {us:7.1f} us")
+            print("  ".join(row).replace("in-step", "(fwd in-step)"), flush=True)
+            continue
         else:
             # the GEMM core on this rulebook, plain epilogue (submanifold layers: map = nbr, the data gradient
-            # reads it reversed; strided layers are skipped — their data gradient runs on the input-side map)
-            if nbr.shape[0] != n_in:
+            # reads it reversed; strided layers: see sdgrad)
+            if nbr.shape[0] != n_in or op not in ops:
                 continue
             kg, ng = (ci, co) if op == "fwd" else (co, ci)
             NGP, KGP = (ng + 15) // 16 * 16, (kg + 31) // 32 * 32

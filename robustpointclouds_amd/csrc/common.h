@@ -105,7 +105,9 @@ __device__ __forceinline__ T ld_agent(const T* p) {
 // Fixed-order reduction of split-K slabs: dW[e] = sum_c part[c * total + e] (c ascending within
 // each of 8 interleaved lanes, lanes combined as a fixed pairwise tree), in double. Block = 64
 // outputs x 8 lanes, each lane with 8 loads in flight -> deterministic and latency-tolerant (the
-// 64-channel head weight-gradient slabs of CenterPoint ran at 0.6 TB/s with 4 x 4).
+// 64-channel head weight-gradient slabs of CenterPoint ran at 0.6 TB/s with 4 x 4). Predicated: a
+// missing chunk reads a clamped address and adds 0.0 (r05: a remainder loop, one load per round trip,
+// took every launch with fewer than 64 slabs — the sparse weight gradients' 28-56 — to ~1 TB/s)
 template <int DUMMY = 0>
 __global__ __launch_bounds__(512) void k_slab_reduce(const float* __restrict__ part, int chunks, long long total,
                                                      float* __restrict__ out) {
@@ -114,15 +116,16 @@ __global__ __launch_bounds__(512) void k_slab_reduce(const float* __restrict__ p
   const long long e = (long long)blockIdx.x * 64 + o;
   double s = 0.0;
   if (e < total) {
-    int c = q;
-    for (; c + 56 < chunks; c += 64) {
+    for (int c = q; c < chunks; c += 64) {
       float a[8];
 #pragma unroll
-      for (int k = 0; k < 8; ++k) a[k] = part[(long long)(c + 8 * k) * total + e];
+      for (int k = 0; k < 8; ++k) {   // clamped address + select (a conditional load waits for itself)
+        const float v = part[(long long)min(c + 8 * k, chunks - 1) * total + e];
+        a[k] = c + 8 * k < chunks ? v : 0.0f;
+      }
 #pragma unroll
       for (int k = 0; k < 8; ++k) s += (double)a[k];
     }
-    for (; c < chunks; c += 8) s += (double)part[(long long)c * total + e];
   }
   sh[q][o] = s;
   __syncthreads();

@@ -27,7 +27,7 @@ DCN offsets (r05). The DCN offset gradient is piecewise constant in the sampling
 sample crosses a bilinear cell edge. With the offsets of r04's test (conv_offset weights N(0, 0.02), biases
 U(-0.5, 0.5): positions spread over whole cells) ~12 of each DCN's 590k samples lie within 1e-5 of an edge, and
 a 1e-5 relative change of the neck output (fp32 rounding: HIP 1.1e-5, torch fp32 4e-6) moves 1-3 of them across
-(tools/dbg_cp_flip.py, gpurun_out r05b). One crossing near a GT peak moved that DCN's offset-conv gradient by
+(tools/archive/dbg_cp_flip.py, gpurun_out r05b). One crossing near a GT peak moved that DCN's offset-conv gradient by
 2.3e-2 and, through the shared conv, every gradient upstream by ~1e-2 — for HIP and equally for the float64 oracle
 fed HIP's neck output (tools/dbg_cp_sub.py: f64 | N_hip mean 5.5e-3), while HIP fed the float64 neck output was
 1.4e-4 (mean) / 2.0e-3 (max) from float64. The test therefore draws offsets that keep every sampling position

@@ -499,7 +499,9 @@ def main():
                                  avg_launch_ms=round(k["avg_ms"], 4), launches=k["launches"],
                                  flops_per_launch=k["flops_per_launch"], ms_per_step=round(k["total_ms"] / 2, 4),
                                  work="2*C_in*C_out FLOP per valid rulebook pair (sparse conv, " + k["dtype"] +
-                                      " MFMA; timed in the per-layer backward loop)"))
+                                      " MFMA; timed in the per-layer backward loop" +
+                                      ("; a weight gradient's time includes its fixed-order slab reduce, launched by "
+                                       "the same C-ABI call" if "wgrad" in name else "") + ")"))
             alls.sort(key=lambda e: -e["ms_per_step"])
             res["roofline"] = dict(alls[0])
             res["roofline_kernels"] = alls + ents

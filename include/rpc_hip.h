@@ -409,7 +409,9 @@ int rpc_dense_conv_s1_kernel(int map, int cout, const int* row_img);
  * 128-multiple channels (0: tap-sharing row-segment kernel with the next sub-step's operand reads issued
  * before this one's MFMAs, default; 1: per-tap kernel; 2: the row-segment kernel's former read-then-MFMA
  * loop); knob 4 = k_conv3x3x / k_conv3x3y loop variants and timing arms (128: x with operand reads a
- * quarter step ahead / y's former read-then-MFMA loop; bit-identical to the defaults) */
+ * quarter step ahead / y's former read-then-MFMA loop; bit-identical to the defaults); knob 5 = the
+ * 64-channel-multiple k_conv3x3's output channels per block (0: 32 when the 64-channel grid is under one
+ * round of two blocks per CU, default; 1: always 64; 2: always 32; bit-identical results) */
 int rpc_dense_tune(int knob, int value);
 /* dW (torch layout; kind 0 = Conv2d [co][ci][kh][kw], 1 = ConvTranspose2d [ci][co][kh][kw]) of the
  * forward map (S1/S2/P1/U2): sum over rows of x[src_row(row,t)][ci] * dz[row][co]; ci, co % 128 == 0 */

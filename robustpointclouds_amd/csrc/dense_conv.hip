@@ -369,9 +369,12 @@ struct C3 {
   const float* bnp;
 };
 
-template <int DUMMY = 0>
+// TNB = 32 (half the output channels per block, twice the blocks): the grids of less than one round of two
+// blocks per CU (CenterPoint's 64-channel head convs at 4 x 128 x 128: 256 tiles) — one wave per SIMD left every
+// step's LDS-read / MFMA / barrier chain exposed
+template <int DUMMY = 0, int TNB = 64>
 __global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
-  constexpr int TNB = 64;                 // output channels per block
+  static_assert(TNB == 64 || TNB == 32, "k_conv3x3: 32 or 64 output channels per block");
   constexpr int WCO = TNB;                // output channels per wave
   constexpr int NI = WCO / 16;            // 16-channel MFMA tiles per wave
   __shared__ __attribute__((aligned(16))) u16 sA[HR * LP3];
@@ -423,12 +426,12 @@ __global__ __launch_bounds__(CBLK, 2) void k_conv3x3(C3 g) {
     const int kc_ = (s) / 9, t_ = (s) - kc_ * 9;                                \
     const u16* p_ = wbase + t_ * wtap + kc_ * BK;                               \
     R##a = *(const uint4*)p_;                                                   \
-    R##b = *(const uint4*)(p_ + whalf);                                         \
+    if constexpr (TNB == 64) R##b = *(const uint4*)(p_ + whalf);                \
   }
-#define C3_WSTORE(R, buf)                                        \
-  {                                                              \
-    *(uint4*)&sW[buf][wrow * LP3 + wseg] = R##a;                  \
-    *(uint4*)&sW[buf][(wrow + 32) * LP3 + wseg] = R##b;           \
+#define C3_WSTORE(R, buf)                                                     \
+  {                                                                           \
+    *(uint4*)&sW[buf][wrow * LP3 + wseg] = R##a;                               \
+    if constexpr (TNB == 64) *(uint4*)&sW[buf][(wrow + 32) * LP3 + wseg] = R##b; \
   }
   uint4 r0a, r0b, r1a, r1b, r2a, r2b;
 
@@ -2431,6 +2434,15 @@ static bool s1_xwide(const int* r_img, int cout) {
   return cout % 128 == 0 && (g_s1_variant == 3 || (g_s1_variant == 0 && !s1_small(r_img, cout)));
 }
 
+// k_conv3x3 at 32 output channels per block when the 64-channel grid is less than one round of its two
+// blocks per CU (knob 5 / RPC_DENSE_S1N32: 0 = by shape, 1 = never, 2 = always)
+static int g_s1_n32 = env_int("RPC_DENSE_S1N32", 0);
+static bool s1_n32(int tiles, int cout) {
+  if (g_s1_n32 == 1) return false;
+  if (g_s1_n32 == 2) return true;
+  return (long long)tiles * (cout / 64) < 2LL * cu_count();
+}
+
 static bool s1_wide(int tiles, int cout) {
   if (cout % 128 || g_s1_variant == 1) return false;
   if (g_s1_variant == 2) return true;
@@ -2453,6 +2465,11 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   if (knob == 4) {
     const int old = g_s1x_dbg;
     if (value >= 0 && value <= 255) g_s1x_dbg = value;
+    return old;
+  }
+  if (knob == 5) {
+    const int old = g_s1_n32;
+    if (value >= 0 && value <= 2) g_s1_n32 = value;
     return old;
   }
   if (knob == 2) {
@@ -2501,6 +2518,8 @@ static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t 
     return RPC_ERR_UNSUPPORTED;
   } else if (s1_wide(g.R.B * TY * TX, g.COUT)) {
     hipLaunchKernelGGL(k_conv3x3w<0>, dim3(g.R.B * TY * TX * (g.COUT / 128)), dim3(WB), 0, st, c);
+  } else if (s1_n32(g.R.B * TY * TX, g.COUT)) {
+    hipLaunchKernelGGL((k_conv3x3<0, 32>), dim3(g.R.B * TY * TX, g.COUT / 32), dim3(CBLK), 0, st, c);
   } else {
     hipLaunchKernelGGL(k_conv3x3<0>, dim3(g.R.B * TY * TX, g.COUT / 64), dim3(CBLK), 0, st, c);
   }

@@ -375,6 +375,36 @@ def test_s1_lds_dma_kernel_bitexact_vs_register_staged(ci, co, B, H, W):
     _close_bf16(outs[0][0], ref)
 
 
+@pytest.mark.parametrize("ci,co,B,H,W", [(64, 64, 4, 128, 128), (320, 64, 2, 37, 45), (64, 320, 1, 40, 24),
+                                         (64, 192, 2, 17, 33), (256, 256, 1, 64, 64)])
+def test_s1_conv3x3_32_channel_blocks_bitexact(ci, co, B, H, W):
+    """k_conv3x3 at 32 output channels per block (rpc_dense_tune knob 5 = 2; by shape for the grids under one
+    round of two blocks per CU, e.g. CenterPoint's 64-channel head convs) against 64 per block (knob 5 = 1):
+    every output channel sums the same MFMA products in the same order, so outputs, the accumulate path and the
+    BatchNorm partial rows are bit-identical; and the output against the fp64 conv."""
+    lib = _ffi.load()
+    x = _rand(B, ci, H, W, seed=31)
+    Wt = _rand(co, ci, 3, 3, seed=32, scale=0.05)
+    wf, _ = _wprep(Wt, 0, 9, 1)
+    img = (B, H, W)
+    base = _rand(B, co, H, W, seed=33)
+    outs = []
+    for variant in (2, 1):
+        old0, old5 = lib.rpc_dense_tune(0, 1), lib.rpc_dense_tune(5, variant)
+        try:
+            z, part = _conv(S1, _nhwc(x), ci, wf, co, img, img, img, stats=True)
+            acc = _nhwc(base).reshape(-1, co).clone()
+            _conv(S1, _nhwc(x), ci, wf, co, img, img, img, out=acc, accum=True)
+        finally:
+            lib.rpc_dense_tune(0, old0)
+            lib.rpc_dense_tune(5, old5)
+        outs.append((z, part, acc))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    ref = F.conv2d(x.double(), Wt.double(), padding=1).permute(0, 2, 3, 1).reshape(-1, co)
+    _close_bf16(outs[0][0], ref)
+
+
 @pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 6, 200, 176), (256, 128, 2, 200, 176), (256, 256, 2, 100, 88),
                                          (128, 128, 1, 16, 32), (256, 128, 2, 37, 45), (128, 256, 2, 33, 17),
                                          (128, 128, 3, 24, 40), (128, 256, 1, 9, 130), (384, 128, 1, 21, 70),

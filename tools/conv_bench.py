@@ -1,5 +1,6 @@
 """A/B timing of the S1 (3x3 stride-1) dense-conv kernels at the SECOND config shapes, interleaved
-rounds in one process (rpc_dense_tune knob 0: 0 = by shape, 1 = k_conv3x3, 2 = k_conv3x3w), HIP events on the
+rounds in one process (rpc_dense_tune knob 0: 0 = by shape, 1 = k_conv3x3, 2 = k_conv3x3w; or --knob 5: k_conv3x3's
+channels per block, 1 = 64, 2 = 32), HIP events on the
 launch stream. Prints per shape and variant the median / min µs and TFLOP/s (2*B*H*W*ci*co*9)."""
 import json
 import sys
@@ -12,7 +13,7 @@ from robustpointclouds_amd import _ffi  # noqa: E402
 SHAPES = [(6, 200, 176, 128, 128), (6, 200, 176, 256, 128), (6, 200, 176, 128, 256), (6, 100, 88, 256, 256)]
 
 
-def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None):
+def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None, knob=0):
     lib = _ffi.load()
     dev = torch.device("cuda")
     st = torch.cuda.current_stream()
@@ -28,7 +29,7 @@ def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None):
         times = {v: [] for v in variants}
         for r in range(rounds):
             for v in variants:
-                lib.rpc_dense_tune(0, v)
+                lib.rpc_dense_tune(knob, v)
                 for _ in range(2):
                     lib.rpc_dense_conv(0, _ffi.ptr(x), ci, ci, _ffi.ptr(wt), co, _ffi.ptr(z), co, 0, 0, _ffi.ptr(part),
                                        img, img, img, _ffi.stream_of(z))
@@ -41,7 +42,7 @@ def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None):
                 e1.record(st)
                 e1.synchronize()
                 times[v].append(e0.elapsed_time(e1) * 1e3 / iters)
-        lib.rpc_dense_tune(0, 0)
+        lib.rpc_dense_tune(knob, 0)
         key = f"B{B} {H}x{W} {ci}->{co}"
         res[key] = {}
         for v in variants:
@@ -58,7 +59,8 @@ if __name__ == "__main__":
     ap.add_argument("--variants", default="0,1,2")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--knob", type=int, default=0, help="rpc_dense_tune knob the variants set (0 or 5)")
     ap.add_argument("--shapes", default="", help="B,H,W,ci,co;... (default: the SECOND config shapes)")
     a = ap.parse_args()
     shapes = [tuple(int(x) for x in sh.split(",")) for sh in a.shapes.split(";") if sh] or None
-    main(a.rounds, a.iters, tuple(int(v) for v in a.variants.split(",")), shapes)
+    main(a.rounds, a.iters, tuple(int(v) for v in a.variants.split(",")), shapes, a.knob)

@@ -148,11 +148,13 @@ class HeadConvFn(torch.autograd.Function):
             raise RuntimeError(f"HIP head conv needs <= {HEAD_PAD} outputs and C_in % 128 == 0 (got {N}, {Cin})")
         dev = x.device
         st = _ffi.stream_of(x)
-        wp = Fn.pad(weight.detach().reshape(N, Cin).float(), (0, 0, 0, HEAD_PAD - N)).contiguous()
+        # rows N .. HEAD_PAD-1 written as zero by the kernel (co_src = N): no padded fp32 copy
+        w32 = weight.detach().reshape(N, Cin).float().contiguous()
         wf = torch.empty((1, HEAD_PAD, Cin), dtype=torch.bfloat16, device=dev)
         wd = torch.empty((1, Cin, HEAD_PAD), dtype=torch.bfloat16, device=dev)
-        _ffi.check(lib.rpc_dense_wprep(_ffi.ptr(wp), 0, Cin, HEAD_PAD, 1, 0, _ffi.ptr(wf), _ffi.ptr(wd), st),
-                   "rpc_dense_wprep(head)")
+        desc = (_ffi.RpcDenseWprep * 1)(_ffi.RpcDenseWprep(w32.data_ptr(), wf.data_ptr(), wd.data_ptr(), 0, Cin,
+                                                           HEAD_PAD, 1, 0, N))
+        _ffi.check(lib.rpc_dense_wprep_batch(desc, 1, st), "rpc_dense_wprep_batch(head)")
         z = torch.empty((B * H * W, HEAD_PAD), dtype=torch.bfloat16, device=dev)
         img = _ffi.int_arr((B, H, W))
         _ffi.check(lib.rpc_dense_conv(P1, _ffi.ptr(x), Cin, Cin, _ffi.ptr(wf), HEAD_PAD, _ffi.ptr(z), HEAD_PAD, 0, 0,
@@ -366,11 +368,12 @@ class Anchor3DHead(nn.Module):
         return torch.cat([c.weight for c in convs], 0), torch.cat([c.bias for c in convs], 0)
 
     # ------------------------------------------------------------------ head outputs
-    def _z(self, x):
+    def _z(self, x, w=None):
         """(z, layout, N): the stacked 1x1 conv WITHOUT bias as the HIP GEMM image [B*H*W, pad]:
         bf16 input -> the bf16 engine (pad HEAD_PAD); fp32 input -> the fp32 engine (pad
-        head_pad_f32(N))."""
-        w, _ = self._stacked()
+        head_pad_f32(N)). w: the stacked weight when the caller already built it."""
+        if w is None:
+            w, _ = self._stacked()
         N = w.shape[0]
         B, _, H, W = x.shape
         if not x.is_cuda:
@@ -384,8 +387,8 @@ class Anchor3DHead(nn.Module):
         return z, dict(B=B, H=H, W=W, bf16=0, sb=H * W * NP, shw=NP, sn=1, nwrite=NP), N
 
     def forward_single(self, x):
-        z, lay, N = self._z(x)
-        _, b = self._stacked()
+        w, b = self._stacked()
+        z, lay, N = self._z(x, w)
         y = (z[:, :N].float() + b.float()).view(lay["B"], lay["H"], lay["W"], N).permute(0, 3, 1, 2)
         A = self.num_anchors
         outs = torch.split(y, [A * self.num_classes, A * 7] + ([A * 2] if self.use_direction_classifier else []),
@@ -448,8 +451,8 @@ class Anchor3DHead(nn.Module):
         if not feat.is_cuda:
             raise RuntimeError("Anchor3DHead.loss runs on the HIP kernels only (no CPU path)")
         gb, gl = pack_gt(batch_data_samples, feat.device)
-        z, lay, _ = self._z(feat)
-        _, b = self._stacked()
+        w, b = self._stacked()
+        z, lay, _ = self._z(feat, w)
         return self.loss_from_z(z, b, lay, gb, gl)
 
 

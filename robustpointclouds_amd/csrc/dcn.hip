@@ -43,6 +43,10 @@ constexpr int WE = TE + 4;     // input window edge (covers floor(y - 1 + i + dy
 constexpr int WR = WE * WE;    // window pixels (144)
 constexpr int PW = C + 8;      // window LDS pitch (elements)
 constexpr int P = C + 16;      // tile LDS pitch (elements, conflict-free transposed reads)
+// backward partial row per tile: dW diagonal blocks (KT * 1024), the offset-bias gradient (2 * KT), padded to 64 bytes
+// (the rows, the reduced row and the window slabs after them stay 16-byte aligned for the vector stores)
+constexpr int PWR = KT * 1024 + 32;
+static_assert(2 * KT <= 32, "offset-bias gradient fits the row padding");
 
 __device__ __forceinline__ u16 f2bf(float f) { return __builtin_bit_cast(u16, (__bf16)f); }
 __device__ __forceinline__ float bf2f(u16 h) { return __uint_as_float((unsigned)h << 16); }
@@ -345,7 +349,7 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
       }
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        pw_part[(((size_t)blockIdx.x * KT + k) * 4 + w) * 256 + (4 * g4 + r) * 16 + (lane & 15)] = aw[r];
+        pw_part[(size_t)blockIdx.x * PWR + (k * 4 + w) * 256 + (4 * g4 + r) * 16 + (lane & 15)] = aw[r];
       f32x4 d[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) d[n] = (f32x4){0.f, 0.f, 0.f, 0.f};
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
   }
   __syncthreads();
   if (tid < 2 * KT)
-    pb_part[(size_t)blockIdx.x * 2 * KT + tid] = ((sPb[tid] + sPb[2 * KT + tid]) + sPb[4 * KT + tid]) + sPb[6 * KT + tid];
+    pb_part[(size_t)blockIdx.x * PWR + tid] = ((sPb[tid] + sPb[2 * KT + tid]) + sPb[4 * KT + tid]) + sPb[6 * KT + tid];
   // the window's input gradient -> this tile's slab [144][64] (k_gather_dx sums the <= 4 covering
   // slabs per pixel in a fixed order: no atomics, deterministic)
   float* wdst = win_part + (size_t)blockIdx.x * WR * C;
@@ -480,9 +484,12 @@ __global__ __launch_bounds__(BLK) void k_gather_dx(Geo g, const float* __restric
   dx[e] += s;
 }
 
-// dWdiag [9][4][16 co][16 ci] -> module layout [64 co][16 ci][3][3]
-__global__ __launch_bounds__(BLK) void k_wstore(const float* __restrict__ d, float* __restrict__ dW) {
+// dWdiag [9][4][16 co][16 ci] -> module layout [64 co][16 ci][3][3]; the reduced row's last 2 * KT values (the offset
+// bias gradient) -> db
+__global__ __launch_bounds__(BLK) void k_wstore(const float* __restrict__ d, float* __restrict__ dW,
+                                                float* __restrict__ db) {
   const int e = blockIdx.x * BLK + threadIdx.x;
+  if (e < 2 * KT) db[e] = d[KT * 1024 + e];
   if (e >= KT * 4 * 256) return;
   const int k = e / 1024, r = e - k * 1024, gq = r / 256, m = (r / 16) % 16, n = r % 16;
   dW[((gq * CG + m) * CG + n) * KT + k] = d[e];
@@ -675,7 +682,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_f32(Geo g, const float* __restrict_
         a4[2] = fmaf(d, cv.z, a4[2]);
         a4[3] = fmaf(d, cv.w, a4[3]);
       }
-      float* dst = pw_part + (((size_t)blockIdx.x * KT + k) * 4 + wq_) * 256 + wco * 16 + wci;
+      float* dst = pw_part + (size_t)blockIdx.x * PWR + (k * 4 + wq_) * 256 + wco * 16 + wci;
       *(float4*)dst = make_float4(a4[0], a4[1], a4[2], a4[3]);
     }
     __syncthreads();
@@ -697,7 +704,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_f32(Geo g, const float* __restrict_
   if (tid < 2 * KT) {
     float sacc = 0.0f;
     for (int pp = 0; pp < 64; ++pp) sacc += sOff[pp * 2 * KT + tid];
-    pb_part[(size_t)blockIdx.x * 2 * KT + tid] = sacc;
+    pb_part[(size_t)blockIdx.x * PWR + tid] = sacc;
   }
   float* wdst = win_part + (size_t)blockIdx.x * WR * C;
   for (int i = tid; i < WR * C / 4; i += BLK) ((float4*)wdst)[i] = ((const float4*)sWin)[i];
@@ -740,7 +747,7 @@ extern "C" size_t rpc_dcn_backward_workspace_size(int B, int H, int W) {
   Geo g;
   if (!check_geo(B, H, W, &g)) return 0;
   const size_t tiles = (size_t)B * g.TY * g.TX;
-  return (tiles * KT * 1024 + tiles * 2 * KT + KT * 1024 + tiles * WR * C) * sizeof(float);
+  return (tiles * PWR + PWR + tiles * WR * C) * sizeof(float);
 }
 
 // dch: offset-gradient channels written per pixel. C (64): a padded image of its own (channels 18..doffp-1
@@ -760,18 +767,19 @@ static int dcn_backward_bf16(const void* x, int xp, const void* off, int offp, c
   if (ws_bytes < rpc_dcn_backward_workspace_size(B, H, W)) return RPC_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const int tiles = B * g.TY * g.TX;
+  // per-tile partial rows [tiles][PWR]: the weight-gradient diagonal blocks, then the offset-bias gradient (one
+  // slab reduce for both)
   float* pw = (float*)workspace;
-  float* pb = pw + (size_t)tiles * KT * 1024;
-  float* dwd = pb + (size_t)tiles * 2 * KT;
-  float* win = dwd + KT * 1024;
+  float* pb = pw + KT * 1024;
+  float* dwd = pw + (size_t)tiles * PWR;
+  float* win = dwd + PWR;
   hipLaunchKernelGGL(k_bwd, dim3(tiles), dim3(BLK), 0, st, g, (const u16*)x, xp, (const u16*)off, offp, off_bias,
                      (const u16*)w_bwd, (const u16*)dout, dop, dx, (u16*)doff, doffp, dch, pw, pb, win);
   RPC_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_gather_dx, dim3((unsigned)(((long long)B * H * W * C + BLK - 1) / BLK)), dim3(BLK), 0, st, g,
                      (const float*)win, dx);
-  slab_reduce(pw, tiles, (long long)KT * 1024, dwd, st);
-  slab_reduce(pb, tiles, 2 * KT, doff_bias, st);
-  hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW);
+  slab_reduce(pw, tiles, PWR, dwd, st);
+  hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW, doff_bias);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
@@ -818,18 +826,19 @@ static int dcn_backward_f32(const float* x, int xp, const float* off, int offp, 
   if (ws_bytes < rpc_dcn_backward_workspace_size(B, H, Wd)) return RPC_ERR_WORKSPACE;
   hipStream_t st = (hipStream_t)stream;
   const int tiles = B * g.TY * g.TX;
+  // per-tile partial rows [tiles][PWR]: the weight-gradient diagonal blocks, then the offset-bias gradient (one
+  // slab reduce for both)
   float* pw = (float*)workspace;
-  float* pb = pw + (size_t)tiles * KT * 1024;
-  float* dwd = pb + (size_t)tiles * 2 * KT;
-  float* win = dwd + KT * 1024;
+  float* pb = pw + KT * 1024;
+  float* dwd = pw + (size_t)tiles * PWR;
+  float* win = dwd + PWR;
   hipLaunchKernelGGL(k_bwd_f32, dim3(tiles), dim3(BLK), 0, st, g, x, xp, off, offp, off_bias, W, dout, dop, dx, doff,
                      doffp, dch, pw, pb, win);
   RPC_LAUNCH_CHECK();
   hipLaunchKernelGGL(k_gather_dx, dim3((unsigned)(((long long)B * H * Wd * C + BLK - 1) / BLK)), dim3(BLK), 0, st, g,
                      (const float*)win, dx);
-  slab_reduce(pw, tiles, (long long)KT * 1024, dwd, st);
-  slab_reduce(pb, tiles, 2 * KT, doff_bias, st);
-  hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW);
+  slab_reduce(pw, tiles, PWR, dwd, st);
+  hipLaunchKernelGGL(k_wstore, dim3((KT * 1024 + BLK - 1) / BLK), dim3(BLK), 0, st, dwd, dW, doff_bias);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -212,6 +212,15 @@ def _dense_flops_per_frame(model, H, W):
     return total
 
 
+def _perf_kernel_dtype():
+    """The perf mode's operand formats, read from the modules that choose them."""
+    from robustpointclouds_amd import sparse_encoder as se
+    fwd = "fp16" if se.FWD_FMT == 1 else "bf16"
+    return (f"fp32 voxelize / sparse layer 0 / head losses; perturber hidden layers fp32 MFMA (weight gradient "
+            f"split-bf16); sparse layers 1-11 on MFMA with {fwd} forward operands and bf16 backward (dz) operands "
+            f"(fp32 accumulate, fp32 BN statistics); SECOND/FPN/head convs bf16 MFMA (fp32 accumulate)")
+
+
 def _perturber_flops_per_point(adv):
     from torch import nn
     lin = [m for m in list(adv.model) + list(adv.attention or []) if isinstance(m, nn.Linear)]
@@ -288,7 +297,8 @@ def _parity_mode(a, data, ready, dev, nus, fpf):
                                     work="the headline's algorithmic FLOPs per frame (dense + sparse + perturber, "
                                          "forward + data gradient + weight gradient) per GPU")
     if stages:
-        res["stage_roofline"] = dict(bound="hbm", unit="GB/s", stages=stages)
+        res["stage_roofline"] = dict(bound="hbm", unit="GB/s",
+                                     stages={k: v for k, v in stages.items() if not k.startswith("perturber")})
     if model.__dict__.get("adversary") is not None or getattr(model, "adversary", None) is not None:
         res["perturber_roofline"] = _perturber_stages(stages, n_valid, model.adversary, PEAK["fp32_mfma"])
     del tr, model
@@ -369,17 +379,18 @@ def main():
     if dist.is_initialized():
         dist.barrier()
     dt = time.perf_counter() - t0
-    # per-launch HIP-event timing of the roofline kernels and of the HBM-bound stages: ROCm cannot record
-    # timing events inside a captured graph, so 2 more steps of the same workload run with the dense
-    # graphs off and the timers on (same kernels, shapes and inputs as the timed steps; rocprof summaries
-    # under profiles/ agree); the second of them also counts the step's algorithmic FLOPs
+    # per-launch HIP-event timing of the roofline kernels: ROCm cannot record timing events inside a captured
+    # graph, so 2 more steps of the same workload run with the dense graphs off and the kernel timers on (same
+    # kernels, shapes and inputs as the timed steps; rocprof summaries under profiles/ agree); the second of
+    # them also counts the step's algorithmic FLOPs. The HBM-bound stages are timed in 2 further steps of their
+    # own (dense graphs on, as in the timed loop), so no per-launch event pair of the kernel timers falls inside
+    # a stage's event pair (the per-sparse-launch events had inflated sparse_fwd / sparse_bwd)
     from robustpointclouds_amd import stage_timer
     graphs = dense_bev.GRAPHS
     dense_bev.GRAPHS = False
     timer.enabled = True
     if sparse_timer is not None:
         sparse_timer.enabled = True
-    stage_timer.TIMER.enabled = True
     me = getattr(model, "middle_encoder", None)
     for i in range(a.steps, a.steps + 2):
         if i == a.steps + 1 and me is not None:
@@ -389,8 +400,12 @@ def main():
     timer.enabled = False
     if sparse_timer is not None:
         sparse_timer.enabled = False
-    stage_timer.TIMER.enabled = False
     dense_bev.GRAPHS = graphs
+    stage_timer.TIMER.enabled = True
+    for i in range(a.steps + 2, a.steps + 4):
+        tr.train_step(*data[i % NB], next_points=data[(i + 1) % NB][0], next_ready=ready)
+    torch.cuda.synchronize()
+    stage_timer.TIMER.enabled = False
     ks = timer.summary()
     sks = sparse_timer.per_kernel() if sparse_timer is not None else {}
     stages = stage_timer.TIMER.summary()
@@ -436,8 +451,7 @@ def main():
                                global_batch=world * a.batch, frames_per_gpu=a.batch,
                                dense_dtype="fp32" if a.fp32 else "bf16",
                                kernel_dtype=("fp32 (voxelize, perturber, sparse encoder)" if a.fp32 else
-                                             "fp32 voxelize/perturber/sparse layer 0; bf16 MFMA (fp32 accumulate,"
-                                             " fp32 BN statistics) sparse layers 1-11"),
+                                             _perf_kernel_dtype()),
                                parallelism=f"dp{world}",
                                dist_backend=dist.get_backend() if dist.is_initialized() else None))
         if ks and op is None:
@@ -516,8 +530,10 @@ def main():
                                    flops_per_launch=ks["flops_per_launch"], launches=ks["launches"],
                                    work="2*C_in*C_out FLOP per valid rulebook pair")
         if stages:
-            # HBM-bound stages: compulsory bytes (stage_timer.py) / HIP-event time / 8 TB/s
-            res["stage_roofline"] = dict(bound="hbm", unit="GB/s", stages=stages)
+            # HBM-bound stages: compulsory bytes (stage_timer.py) / HIP-event time / 8 TB/s. The perturber is not
+            # one (its fp32 activations, not its voxels, are its traffic): its stages are in perturber_roofline
+            res["stage_roofline"] = dict(bound="hbm", unit="GB/s", timed_apart_from_kernel_timers=True,
+                                         stages={k: v for k, v in stages.items() if not k.startswith("perturber")})
         if step_flops is not None:
             # whole-step algorithmic FLOP rate, the per-frame constant counted on this run's
             # synthetic frames: dense convs from the module shapes, sparse convs from the valid rulebook pairs,

@@ -143,6 +143,11 @@ typedef struct {
   int vfe_features;       /* fused mode: HardSimpleVFE num_features (4 KITTI) */
   int wgrad_split_bf16;   /* perf mode: hidden-layer weight gradients on bf16 MFMA with hi/lo-split fp32
                              operands (~2^-16 relative per product); 0 = fp32 MFMA (parity mode) */
+  int act16;              /* perf mode: 16-bit activation rows of the hidden layers in the workspace — bit 0:
+                             pre-activations z_1..z_3 fp16 (the reference AMP's Linear outputs, train.py:91-103);
+                             bit 1 (with wgrad_split_bf16): gradient rows dh_1..dh_3, dz_1..dz_4 bf16. Applied
+                             when every hidden shape is an encoder-decoder step (width x2 or /2, >= 16), else
+                             fp32 rows; fp32 arithmetic and fp32/double BatchNorm sums either way. 0 = parity */
 } rpc_perturber_cfg;
 
 size_t rpc_perturber_workspace_size(const rpc_perturber_cfg* cfg, int rows, int slots);

@@ -141,12 +141,16 @@ class OracleSparseEncoder:
                                     rm=m[1].running_mean.detach().cpu().to(dtype).clone(),
                                     rv=m[1].running_var.detach().cpu().to(dtype).clone()))
 
-    def forward(self, feats, coors, B, keep=False, masks=None):
+    def forward(self, feats, coors, B, keep=False, masks=None, flips=None):
         """masks (optional): per layer (coors, bool [n, co]) — the ReLU decisions of the implementation under test,
         rows matched here by coordinates; the layer's output is then (pre [+ identity]) * mask instead of relu(...):
         float64 arithmetic on the implementation's own branch of the piecewise-linear encoder. A pre-activation
         within an fp32 rounding of 0 lands on either side in fp32; evaluated on the other branch, one such element
-        moved every gradient below its layer by ~1e-3 (tests/test_gpu_sparse_layers.py)."""
+        moved every gradient below its layer by ~1e-3 (tests/test_gpu_sparse_layers.py).
+        flips (optional, with masks; tests/_dense_masks.FlipStats or any object with `flips`, `worst`, `per_layer`):
+        every adopted decision that differs from this oracle's own (act > 0) is counted, and `worst` records the
+        largest |act| / max |act| of its channel over them — how far from zero an adopted decision may lie is
+        bounded by the tests (FLIP_PRE_MAX), so a wrong-sign kernel is not copied into the oracle unseen."""
         x = torch.as_tensor(feats).to(self.dtype)
         c = np.asarray(coors, np.int64)
         cache = {}
@@ -182,7 +186,20 @@ class OracleSparseEncoder:
             act = pre + outs[res] if res >= 0 else pre                         # SparseBasicBlock: + identity
             if masks is not None:
                 mc, mm = masks[li]
-                x = act * torch.from_numpy(_match(c_out, np.asarray(mc), np.asarray(mm))).to(self.dtype)
+                m = torch.from_numpy(_match(c_out, np.asarray(mc), np.asarray(mm)))
+                if flips is not None:
+                    a = act.detach()
+                    d = m != (a > 0)
+                    nd = int(d.sum())
+                    w = 0.0
+                    if nd:
+                        sc = a.abs().amax(0, keepdim=True).clamp_min(1e-30)
+                        w = float((a.abs() / sc)[d].max())
+                        flips.flips += nd
+                        flips.worst = max(flips.worst, w)
+                    if hasattr(flips, "per_layer"):
+                        flips.per_layer.append((li, nd, w))
+                x = act * m.to(self.dtype)
             else:
                 x = torch.relu(act)
             outs.append(x)

@@ -31,7 +31,8 @@ ip = C.POINTER(C.c_int)
 class PerturberCfg(C.Structure):
     _fields_ = [("F", C.c_int), ("hidden", C.c_int * 3), ("use_attention", C.c_int),
                 ("training", C.c_int), ("sensor_error_bound", C.c_float), ("bn_eps", C.c_float),
-                ("bn_momentum", C.c_float), ("vfe_features", C.c_int), ("wgrad_split_bf16", C.c_int)]
+                ("bn_momentum", C.c_float), ("vfe_features", C.c_int), ("wgrad_split_bf16", C.c_int),
+                ("act16", C.c_int)]
 
 
 class RpcHardVfeCfg(C.Structure):

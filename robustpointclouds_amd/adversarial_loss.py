@@ -123,9 +123,10 @@ def center_combination(losses: dict, l2, w: float, regularization_weight: float,
 def fused_center_tail(task_losses: dict, packed, l2, w: float, regularization_weight: float):
     """AdversarialCenterPoint.loss_by_feat_single's combination over the CenterHead's packed task losses (a
     PackedCenterLosses dict whose values are packed[0..n) in order): a FusedLosses dict (views of one device
-    vector) whose `.total` is parse_losses' sum, or None when the inputs are not that layout."""
+    vector) whose `.total` is parse_losses' sum, or None when the inputs are not that layout (or more task losses
+    than rpc_center_tail_forward's one-wave-per-256 kernel takes)."""
     n = len(task_losses)
-    if (packed is None or not packed.is_cuda or packed.dim() != 1 or packed.numel() != n or not isinstance(l2, torch.Tensor)
+    if (n > 256 or packed is None or not packed.is_cuda or packed.dim() != 1 or packed.numel() != n or not isinstance(l2, torch.Tensor)
             or not l2.is_cuda or l2.numel() != 1 or packed.dtype != torch.float32 or l2.dtype != torch.float32):
         return None
     out = CenterTailFn.apply(packed, l2, -w, regularization_weight)

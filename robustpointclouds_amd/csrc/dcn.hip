@@ -446,6 +446,8 @@ __global__ __launch_bounds__(BLK) void k_bwd(Geo g, const u16* __restrict__ x, i
   __syncthreads();
   if (tid < 2 * KT)
     pb_part[(size_t)blockIdx.x * PWR + tid] = ((sPb[tid] + sPb[2 * KT + tid]) + sPb[4 * KT + tid]) + sPb[6 * KT + tid];
+  else if (tid < 32)   // the row's 64-byte padding: zeros, so the slab reduce never sums uninitialised words
+    pb_part[(size_t)blockIdx.x * PWR + tid] = 0.0f;
   // the window's input gradient -> this tile's slab [144][64] (k_gather_dx sums the <= 4 covering
   // slabs per pixel in a fixed order: no atomics, deterministic)
   float* wdst = win_part + (size_t)blockIdx.x * WR * C;
@@ -705,6 +707,8 @@ __global__ __launch_bounds__(BLK) void k_bwd_f32(Geo g, const float* __restrict_
     float sacc = 0.0f;
     for (int pp = 0; pp < 64; ++pp) sacc += sOff[pp * 2 * KT + tid];
     pb_part[(size_t)blockIdx.x * PWR + tid] = sacc;
+  } else if (tid < 32) {
+    pb_part[(size_t)blockIdx.x * PWR + tid] = 0.0f;
   }
   float* wdst = win_part + (size_t)blockIdx.x * WR * C;
   for (int i = tid; i < WR * C / 4; i += BLK) ((float4*)wdst)[i] = ((const float4*)sWin)[i];

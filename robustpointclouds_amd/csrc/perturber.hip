@@ -21,6 +21,7 @@
 // the points (one batched launch for all layers), summed in double in a fixed order and
 // passed through the reference's grad hook clamp(nan_to_num(g), -0.1, 0.1).
 #include <hipcub/hipcub.hpp>
+#include <type_traits>
 #include <math.h>
 #include <string.h>
 
@@ -43,6 +44,7 @@ constexpr int TSTRIDE = 1 + NGRP;
 
 struct Dev {
   int F, A, C[7];
+  int a16;         // effective rpc_perturber_cfg.act16 (0 unless every hidden shape has a 16-bit instantiation)
   int S;           // channel stride of the SoA activation buffers (>= N)
   int rows, slots, fused, training, use_att, vfe_f;
   float eps, mom;
@@ -1281,6 +1283,67 @@ __device__ __forceinline__ fvec<Q> ldq(const float* p, int n, int N) {
 }
 template <int Q>
 __device__ __forceinline__ void stq(float* p, int n, fvec<Q> v) { *(fvec<Q>*)(p + n) = v; }
+
+// 16-bit activation rows (perf mode, rpc_perturber_cfg.act16): the same channel-major [C][S] rows with 2-byte
+// elements — fp16 for the hidden pre-activations z_1..z_3 (the reference AMP's Linear outputs, train.py:91-103;
+// finite values saturate at +-65504 like the fp16 sparse rows), bf16 for the gradient rows dh / dz_1..dz_4
+// (unscaled gradients ~1e-7 need bf16's range; the AMP's loss scaling has no counterpart here). Values that
+// are stored are also what the producer's BatchNorm sums see (rnd), so the statistics describe the rows.
+typedef _Float16 f16;
+typedef __bf16 b16;
+__device__ __forceinline__ float rnd(float v, float*) { return v; }
+__device__ __forceinline__ float rnd(float v, f16*) { return (float)(f16)fminf(fmaxf(v, -65504.0f), 65504.0f); }
+__device__ __forceinline__ float rnd(float v, b16*) { return (float)(b16)v; }
+template <typename T>
+__device__ __forceinline__ float rnd_as(float v) { return rnd(v, (T*)nullptr); }
+template <int Q, typename T>
+__device__ __forceinline__ fvec<Q> ldq(const T* p, int n, int N) {
+  if constexpr (sizeof(T) == 4) {
+    return ldq<Q>((const float*)p, n, N);
+  } else {
+    typedef T tv __attribute__((ext_vector_type(Q)));
+    const tv h = *(const tv*)(p + n);
+    fvec<Q> v;
+#pragma unroll
+    for (int i = 0; i < Q; ++i) v[i] = n + i < N ? (float)h[i] : 0.0f;
+    return v;
+  }
+}
+// the values must already be representable (rnd_as<T>): the conversion is then exact
+template <int Q, typename T>
+__device__ __forceinline__ void stq(T* p, int n, fvec<Q> v) {
+  if constexpr (sizeof(T) == 4) {
+    stq<Q>((float*)p, n, v);
+  } else {
+    typedef T tv __attribute__((ext_vector_type(Q)));
+    tv h;
+#pragma unroll
+    for (int i = 0; i < Q; ++i) h[i] = (T)v[i];
+    *(tv*)(p + n) = h;
+  }
+}
+// element types of one hidden-layer launch (host-chosen per layer, see row_types)
+template <class ZI, class ZO>
+struct FwdT {
+  using zi = ZI;   // z_{l-1} rows read
+  using zo = ZO;   // z_l rows written
+};
+template <class ZL, class ZP, class GI, class GO, class DZ>
+struct BwdT {
+  using zl = ZL;   // z_l rows read
+  using zp = ZP;   // z_{l-1} rows read (ReLU mask of h_{l-1})
+  using gi = GI;   // dh_l rows read
+  using go = GO;   // dh_{l-1} rows written
+  using dz = DZ;   // dz_l rows written (read by the weight gradient)
+};
+using FwdF32 = FwdT<float, float>;
+using BwdF32 = BwdT<float, float, float, float, float>;
+// 16-bit activation rows (act16) are instantiated for the encoder-decoder shapes of the configs in scope (each
+// hidden width twice or half the previous: [64, 128, 64] 3-class, [16, 32, 64] nuScenes); any other hidden shape
+// keeps fp32 rows for the whole perturber (fill_dev)
+__host__ __device__ constexpr bool a16_shape(int CI, int CO) {
+  return CI >= 16 && CO >= 16 && CI % 16 == 0 && CO % 16 == 0 && CI * CO <= 8192 && (CI == 2 * CO || CO == 2 * CI);
+}
 // W_l [R][CI] row-major -> LDS rows of pitch P: all of a thread's loads in flight before its first LDS
 // store (a load -> store loop waited out one L2 round trip per pass: 16 at the start of every block)
 template <int NTOT, int CI, int P>
@@ -1305,8 +1368,10 @@ __host__ __device__ constexpr int tiles_per_group(int ks) { return ks * 4 <= 64 
 // the 4 tiles' D values for output row 4g + i are 4 consecutive points (one 16-byte store). Every
 // weight read from LDS feeds 4 MFMAs. Groups go to waves block-fastest (t = wave * GRID + block) so
 // each CU gets an equal share when N / 64 is not much larger than the wave count.
-template <int CI, int CO>
+template <int CI, int CO, class RT>
 __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
+  using ZI = typename RT::zi;
+  using ZO = typename RT::zo;
   constexpr int P = pitch_mod(CI, 4), NT = CO / 16, KS = CI / 4, TQ = tiles_per_group(KS), GP = 16 * TQ;
   __shared__ float sW[CO * P];
   __shared__ float sp[3 * CI + CO];
@@ -1323,8 +1388,8 @@ __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
   const float* bias = sp + 3 * CI;
   const int N = d.meta[0];
   const int lane = threadIdx.x & 63, a = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
-  const float* zin = d.z[l - 1];
-  float* zout = d.z[l];
+  const ZI* zin = (const ZI*)d.z[l - 1];
+  ZO* zout = (ZO*)d.z[l];
   for (int t = wv * GRID + blockIdx.x; t * GP < N; t += GRID * MFW) {
     const int n0 = t * GP, na = n0 + TQ * a;
     fvec<TQ> hv[KS];
@@ -1351,14 +1416,14 @@ __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
         for (int q = 0; q < TQ; ++q) v[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(hv[s][q], w, v[q], 0, 0, 0);
       }
       float t1 = 0.0f, t2 = 0.0f;
-      float* row = zout + (size_t)(16 * j + a) * d.S;
+      ZO* row = zout + (size_t)(16 * j + a) * d.S;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int nb = n0 + TQ * (4 * g + i);
         fvec<TQ> o;
 #pragma unroll
         for (int q = 0; q < TQ; ++q) {
-          o[q] = nb + q < N ? v[q][i] : 0.0f;
+          o[q] = nb + q < N ? rnd_as<ZO>(v[q][i]) : 0.0f;
           t1 += o[q];
           t2 = fmaf(o[q], o[q], t2);
         }
@@ -1376,8 +1441,13 @@ __global__ __launch_bounds__(MFBLK) void k_fwd_mid_mf(Dev d, int l) {
 
 // layer l (4..1) backward: dz_l = BN_l backward of dh_l (stored), dh_{l-1} = relu'(h_{l-1}) W_l^T dz_l,
 // BN_{l-1} backward sums (sum dh, sum dh * xhat). Same interleaved point groups as the forward.
-template <int CI, int CO>
+template <int CI, int CO, class RT>
 __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
+  using ZL = typename RT::zl;
+  using ZP = typename RT::zp;
+  using GI = typename RT::gi;
+  using GO = typename RT::go;
+  using DZ = typename RT::dz;
   constexpr int P = pitch_mod(CI, 16), NT = CI / 16, KS = CO / 4, TQ = tiles_per_group(KS), GP = 16 * TQ;
   __shared__ float sW[CO * P];
   __shared__ float sp[7 * CO + 4 * CI];
@@ -1402,11 +1472,11 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
   const float* m2 = m1 + CO;
   const float* gi = m2 + CO;
   const int lane = threadIdx.x & 63, a = lane & 15, g = lane >> 4, wv = threadIdx.x >> 6;
-  const float* dhin = d.dh[src];
-  float* dhout = d.dh[src ^ 1];
-  const float* zl = d.z[l];
-  const float* zp = d.z[l - 1];
-  float* dzl = d.dz[l];
+  const GI* dhin = (const GI*)d.dh[src];
+  GO* dhout = (GO*)d.dh[src ^ 1];
+  const ZL* zl = (const ZL*)d.z[l];
+  const ZP* zp = (const ZP*)d.z[l - 1];
+  DZ* dzl = (DZ*)d.dz[l];
   for (int t = wv * GRID + blockIdx.x; t * GP < N; t += GRID * MFW) {
     const int n0 = t * GP, na = n0 + TQ * a;
     fvec<TQ> dzv[KS];
@@ -1430,7 +1500,14 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
           const float xh = (zv[u][q] - bo[2 * CO + o]) * bo[3 * CO + o];
           dzv[s][q] = na + q < N ? gi[o] * (dv[u][q] - m1[o] - xh * m2[o]) : 0.0f;
         }
-        stq<TQ>(dzl + (size_t)o * d.S, na, dzv[s]);
+        if constexpr (sizeof(DZ) == 4) {
+          stq<TQ>(dzl + (size_t)o * d.S, na, dzv[s]);
+        } else {   // the weight gradient's rows (bf16); this kernel's data gradient keeps the fp32 values
+          fvec<TQ> r;
+#pragma unroll
+          for (int q = 0; q < TQ; ++q) r[q] = rnd_as<DZ>(dzv[s][q]);
+          stq<TQ>(dzl + (size_t)o * d.S, na, r);
+        }
       }
       asm volatile("" ::: "memory");  // bound the loads in flight (register pressure)
     }
@@ -1450,7 +1527,7 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
         for (int q = 0; q < TQ; ++q) v[q] = __builtin_amdgcn_mfma_f32_16x16x4f32(dzv[s][q], w, v[q], 0, 0, 0);
       }
       float t1 = 0.0f, t2 = 0.0f;
-      float* row = dhout + (size_t)c * d.S;
+      GO* row = dhout + (size_t)c * d.S;
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int nb = n0 + TQ * (4 * g + i);
@@ -1458,7 +1535,7 @@ __global__ __launch_bounds__(MFBLK) void k_bwd_mid_mf(Dev d, int l, int src) {
 #pragma unroll
         for (int q = 0; q < TQ; ++q) {
           const float hv = fmaxf(fmaf(zc[i][q] - bi[2 * CI + c], bi[c], bi[CI + c]), 0.0f);
-          o[q] = (nb + q < N && hv > 0.0f) ? v[q][i] : 0.0f;
+          o[q] = (nb + q < N && hv > 0.0f) ? rnd_as<GO>(v[q][i]) : 0.0f;
           t1 += o[q];
           t2 += o[q] * ((zc[i][q] - bi[2 * CI + c]) * bi[3 * CI + c]);
         }
@@ -1590,8 +1667,10 @@ __device__ __forceinline__ void split_bf16x8(const float* v, bf16x8_t& hi, bf16x
   }
 }
 
-template <int CO, int CI>
+template <int CO, int CI, class DZ, class ZP>
 __global__ __launch_bounds__(BLK, 2) void k_wgrad_bx3(Dev d, MfJobs J) {
+  // DZ / ZP: element types of the dz_l / z_{l-1} rows (float, or the 16-bit rows of act16); bf16 dz rows are
+  // their own hi part (lo = 0 exactly), so their lo * hi product is skipped
   // above 8 accumulator tiles the output tiles are split in two halves (along the wider of CO / CI): waves
   // (2p + h) take half h of the tiles over the point stream p (32-point blocks, the 2 streams interleaved),
   // so a wave holds at most 16 tiles plus its hi / lo operand splits without spilling; the operand rows of
@@ -1631,15 +1710,15 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad_bx3(Dev d, MfJobs J) {
     f32x4 dv[TOW][2], zv[TCW][2];
 #pragma unroll
     for (int i = 0; i < TOW; ++i) {
-      const float* row = job.dz + (size_t)(16 * (o0 + i) + a) * d.S;
-      dv[i][0] = ld4(row, nb, r1);
-      dv[i][1] = ld4(row, nb + 4, r1);
+      const DZ* row = (const DZ*)job.dz + (size_t)(16 * (o0 + i) + a) * d.S;
+      dv[i][0] = ldq<4>(row, nb, r1);
+      dv[i][1] = ldq<4>(row, nb + 4, r1);
     }
 #pragma unroll
     for (int jc = 0; jc < TCW; ++jc) {
-      const float* row = job.z + (size_t)(16 * (c0 + jc) + a) * d.S;
-      zv[jc][0] = ld4(row, nb, r1);
-      zv[jc][1] = ld4(row, nb + 4, r1);
+      const ZP* row = (const ZP*)job.z + (size_t)(16 * (c0 + jc) + a) * d.S;
+      zv[jc][0] = ldq<4>(row, nb, r1);
+      zv[jc][1] = ldq<4>(row, nb + 4, r1);
     }
     bf16x8_t ah[TOW], al[TOW];
 #pragma unroll
@@ -1665,7 +1744,8 @@ __global__ __launch_bounds__(BLK, 2) void k_wgrad_bx3(Dev d, MfJobs J) {
       split_bf16x8(t, bh, bl);
 #pragma unroll
       for (int i = 0; i < TOW; ++i) {
-        acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][jc], 0, 0, 0);
+        if constexpr (!std::is_same<DZ, b16>::value)
+          acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh, acc[i][jc], 0, 0, 0);
         acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl, acc[i][jc], 0, 0, 0);
         acc[i][jc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh, acc[i][jc], 0, 0, 0);
       }
@@ -1854,6 +1934,12 @@ static int fill_dev(const rpc_perturber_cfg* cfg, const float* const* P, const f
   d.F = cfg->F;
   d.A = cfg->F / 2 > 1 ? cfg->F / 2 : 1;
   widths(cfg, d.C);
+  // 16-bit rows only where every hidden layer has them, and the bf16 dz rows only with the split-bf16 weight
+  // gradient (the fp32-MFMA k_wgrad_mf reads fp32 rows)
+  d.a16 = cfg->act16 & 3;
+  for (int l = 1; l < 5; ++l)
+    if (!a16_shape(d.C[l], d.C[l + 1])) d.a16 = 0;
+  if (!cfg->wgrad_split_bf16) d.a16 &= ~2;
   d.rows = rows;
   d.slots = slots;
   d.S = (int)chan_stride(rows, slots);
@@ -1948,15 +2034,50 @@ static int launch_last(int CI, Dev& d, hipStream_t st, bool bwd) {
   }
   return RPC_OK;
 }
+template <bool H>
+using Z16 = typename std::conditional<H, f16, float>::type;
+template <bool H>
+using G16 = typename std::conditional<H, b16, float>::type;
+// row types of layer l: z_1..z_3 16-bit (z_0 / z_4 stay fp32: the per-point boundary passes read them), dh_l
+// 16-bit between hidden layers (dh_4 comes from the fp32 output-layer pass, dh_0 feeds the fp32 layer-0 pass)
+template <int CI, int CO, bool ZH, bool GH>
+static void launch_mid16(Dev& d, int l, hipStream_t st, bool bwd, int src) {
+  if (bwd) {
+    if (l == 4)
+      hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO, BwdT<float, Z16<ZH>, float, G16<GH>, G16<GH>>>), dim3(GRID), dim3(MFBLK),
+                         0, st, d, l, src);
+    else if (l == 1)
+      hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO, BwdT<Z16<ZH>, float, G16<GH>, float, G16<GH>>>), dim3(GRID), dim3(MFBLK),
+                         0, st, d, l, src);
+    else
+      hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO, BwdT<Z16<ZH>, Z16<ZH>, G16<GH>, G16<GH>, G16<GH>>>), dim3(GRID),
+                         dim3(MFBLK), 0, st, d, l, src);
+  } else {
+    if (l == 1)
+      hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO, FwdT<float, Z16<ZH>>>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
+    else if (l == 4)
+      hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO, FwdT<Z16<ZH>, float>>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
+    else
+      hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO, FwdT<Z16<ZH>, Z16<ZH>>>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
+  }
+}
 // hidden layer l: fp32-MFMA kernels where the tile shape fits (forward: CO % 16, backward: CI % 16),
 // the per-point VALU kernels otherwise (8-channel layers of the small configs)
 template <int CI, int CO>
 static void launch_mid_t(Dev& d, int l, hipStream_t st, bool bwd, int src) {
+  if constexpr (a16_shape(CI, CO)) {
+    switch (d.a16) {
+      case 1: launch_mid16<CI, CO, true, false>(d, l, st, bwd, src); return;
+      case 2: launch_mid16<CI, CO, false, true>(d, l, st, bwd, src); return;
+      case 3: launch_mid16<CI, CO, true, true>(d, l, st, bwd, src); return;
+      default: break;
+    }
+  }
   if (bwd) {
-    if constexpr (CI % 16 == 0) hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO>), dim3(GRID), dim3(MFBLK), 0, st, d, l, src);
+    if constexpr (CI % 16 == 0) hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO, BwdF32>), dim3(GRID), dim3(MFBLK), 0, st, d, l, src);
     else hipLaunchKernelGGL((k_bwd_mid<CI, CO>), dim3(GRID), dim3(BLK), 0, st, d, l, src);
   } else {
-    if constexpr (CO % 16 == 0) hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
+    if constexpr (CO % 16 == 0) hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO, FwdF32>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
     else hipLaunchKernelGGL((k_fwd_mid<CI, CO>), dim3(GRID), dim3(BLK), 0, st, d, l);
   }
 }
@@ -1979,26 +2100,35 @@ static int launch_mid(int CI, int CO, Dev& d, int l, hipStream_t st, bool bwd, i
   }
 }
 static bool wgrad_mf_ok(int CO, int CI) { return CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192; }
+// zh16: the jobs' z_{l-1} rows are fp16 (act16 bit 0, layers 2..4); dz rows are bf16 under act16 bit 1 (the
+// split-bf16 kernel only: act16 is a perf-mode option like wgrad_split_bf16)
 template <int CO, int CI>
-static void launch_wgrad_mf_t(Dev& d, const MfJobs& M, int njob, bool split, hipStream_t st) {
+static void launch_wgrad_mf_t(Dev& d, const MfJobs& M, int njob, bool split, bool zh16, hipStream_t st) {
   if constexpr (CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192) {
-    if (split)
-      hipLaunchKernelGGL((k_wgrad_bx3<CO, CI>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M);
-    else
+    if (split) {
+      const bool gh = d.a16 & 2;
+      if constexpr (a16_shape(CI, CO)) {
+        if (zh16 && gh) { hipLaunchKernelGGL((k_wgrad_bx3<CO, CI, b16, f16>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M); return; }
+        if (zh16) { hipLaunchKernelGGL((k_wgrad_bx3<CO, CI, float, f16>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M); return; }
+        if (gh) { hipLaunchKernelGGL((k_wgrad_bx3<CO, CI, b16, float>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M); return; }
+      }
+      hipLaunchKernelGGL((k_wgrad_bx3<CO, CI, float, float>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M);
+    } else {
       hipLaunchKernelGGL((k_wgrad_mf<CO, CI>), dim3(M.KS, njob), dim3(BLK), 0, st, d, M);
+    }
   }
 }
 template <int CO>
-static void launch_wgrad_mf_ci(int CI, Dev& d, const MfJobs& M, int njob, bool split, hipStream_t st) {
+static void launch_wgrad_mf_ci(int CI, Dev& d, const MfJobs& M, int njob, bool split, bool zh16, hipStream_t st) {
   switch (CI) {
-#define CASE(c) case c: launch_wgrad_mf_t<CO, c>(d, M, njob, split, st); break;
+#define CASE(c) case c: launch_wgrad_mf_t<CO, c>(d, M, njob, split, zh16, st); break;
     RPC_HID(CASE)
 #undef CASE
   }
 }
-static void launch_wgrad_mf(int CO, int CI, Dev& d, const MfJobs& M, int njob, bool split, hipStream_t st) {
+static void launch_wgrad_mf(int CO, int CI, Dev& d, const MfJobs& M, int njob, bool split, bool zh16, hipStream_t st) {
   switch (CO) {
-#define CASE(c) case c: launch_wgrad_mf_ci<c>(CI, d, M, njob, split, st); break;
+#define CASE(c) case c: launch_wgrad_mf_ci<c>(CI, d, M, njob, split, zh16, st); break;
     RPC_HID(CASE)
 #undef CASE
   }
@@ -2177,21 +2307,23 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
     }
     RPC_LAUNCH_CHECK();
   }
+  // one launch per distinct (shape, z_{l-1} row type), covering every layer of that kind
+  auto zh16 = [&](int k) { return (d.a16 & 1) && k - 1 >= 1 && k - 1 <= 3; };
   for (int l = 1; l < 5; ++l) {
     if (!is_mf[l]) continue;
-    bool first = true;   // one launch per distinct shape, covering every layer of that shape
+    auto same = [&](int k) { return is_mf[k] && d.C[k + 1] == d.C[l + 1] && d.C[k] == d.C[l] && zh16(k) == zh16(l); };
+    bool first = true;
     for (int k = 1; k < l; ++k)
-      if (is_mf[k] && d.C[k + 1] == d.C[l + 1] && d.C[k] == d.C[l]) first = false;
+      if (same(k)) first = false;
     if (!first) continue;
     MfJobs M;
     memset(&M, 0, sizeof(M));
     int nm = 0;
     for (int k = l; k < 5; ++k)
-      if (is_mf[k] && d.C[k + 1] == d.C[l + 1] && d.C[k] == d.C[l])
-        M.j[nm++] = MfJob{d.dz[k], d.z[k - 1], d.bn[k - 1], J.j[k].eoff};
+      if (same(k)) M.j[nm++] = MfJob{d.dz[k], d.z[k - 1], d.bn[k - 1], J.j[k].eoff};
     M.total = J.total;
     M.KS = ks;
-    launch_wgrad_mf(d.C[l + 1], d.C[l], d, M, nm, cfg->wgrad_split_bf16 != 0, st);
+    launch_wgrad_mf(d.C[l + 1], d.C[l], d, M, nm, cfg->wgrad_split_bf16 != 0, zh16(l), st);
     RPC_LAUNCH_CHECK();
   }
   for (int l = 0; l < 5; ++l) {

@@ -687,6 +687,18 @@ __global__ __launch_bounds__(BLK) void k_dense_clear_v4(const int* __restrict__ 
 #pragma unroll
   for (int j = 0; j < 4; ++j) store_val(dense + dense_index<NHWC>(cr, c + j, C, s), 0.0f);
 }
+// any C / any N (rpc_sparse_dense_clear when C % 4 != 0 or N * C / 4 does not fit an int): one element per thread,
+// 64-bit element index, like k_to_dense's scalar form
+template <typename T, bool NHWC>
+__global__ __launch_bounds__(BLK) void k_dense_clear(const int* __restrict__ coors, long long N, int C, Shape s,
+                                                     T* __restrict__ dense) {
+  const long long t = (long long)blockIdx.x * BLK + threadIdx.x;
+  if (t >= N * C) return;
+  const long long r = t / C;
+  const int c = (int)(t - r * C);
+  const int cr[4] = {coors[4 * r], coors[4 * r + 1], coors[4 * r + 2], coors[4 * r + 3]};
+  store_val(dense + dense_index<NHWC>(cr, c, C, s), 0.0f);
+}
 template <typename T, bool NHWC>
 __global__ __launch_bounds__(FBLK) void k_from_dense(const T* __restrict__ gd, const float* __restrict__ z,
                                                     const float* __restrict__ bn, const int* __restrict__ coors,
@@ -1557,10 +1569,25 @@ extern "C" int rpc_sparse_to_dense(const float* z, const float* bn, const int* c
 
 extern "C" int rpc_sparse_dense_clear(const int* coors, int N, int C, const int* shape /* B,D,H,W */, int flags,
                                       void* dense, void* stream) {
-  if (N < 0 || C < 4 || (C & 3) || !shape || (flags & ~3) || (long long)N * (C / 4) >= (1LL << 31)) return RPC_ERR_ARG;
+  if (N < 0 || C < 1 || !shape || (flags & ~3)) return RPC_ERR_ARG;
   if (N == 0) return RPC_OK;
   Shape s{shape[0], shape[1], shape[2], shape[3]};
   hipStream_t st = (hipStream_t)stream;
+  if ((C & 3) || (long long)N * (C / 4) >= (1LL << 31)) {   // scalar form (mirrors k_to_dense's fallback)
+    dim3 g1(cdiv((long long)N * C, BLK));
+    switch (flags) {
+      case 0: hipLaunchKernelGGL((k_dense_clear<float, false>), g1, dim3(BLK), 0, st, coors, (long long)N, C, s,
+                                 (float*)dense); break;
+      case 1: hipLaunchKernelGGL((k_dense_clear<float, true>), g1, dim3(BLK), 0, st, coors, (long long)N, C, s,
+                                 (float*)dense); break;
+      case 2: hipLaunchKernelGGL((k_dense_clear<__hip_bfloat16, false>), g1, dim3(BLK), 0, st, coors, (long long)N,
+                                 C, s, (__hip_bfloat16*)dense); break;
+      default: hipLaunchKernelGGL((k_dense_clear<__hip_bfloat16, true>), g1, dim3(BLK), 0, st, coors, (long long)N,
+                                  C, s, (__hip_bfloat16*)dense);
+    }
+    RPC_LAUNCH_CHECK();
+    return RPC_OK;
+  }
   dim3 g4(cdiv((long long)N * (C / 4), BLK));
   switch (flags) {
     case 0: hipLaunchKernelGGL((k_dense_clear_v4<float, false>), g4, dim3(BLK), 0, st, coors, N, C, s, (float*)dense); break;

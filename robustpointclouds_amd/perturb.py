@@ -24,7 +24,7 @@ from . import stage_timer
 
 
 def make_cfg(F, hidden, use_attention, training, sensor_error_bound, bn_eps=1e-3, bn_momentum=0.1,
-             vfe_features=4, wgrad_split_bf16=False):
+             vfe_features=4, wgrad_split_bf16=False, act16=0):
     cfg = _ffi.PerturberCfg()
     cfg.F = int(F)
     for k in range(3):
@@ -36,6 +36,7 @@ def make_cfg(F, hidden, use_attention, training, sensor_error_bound, bn_eps=1e-3
     cfg.bn_momentum = float(bn_momentum)
     cfg.vfe_features = int(vfe_features)
     cfg.wgrad_split_bf16 = int(bool(wgrad_split_bf16))
+    cfg.act16 = int(act16) & 3
     return cfg
 
 

@@ -243,7 +243,7 @@ class VoxelPerturber(nn.Module):
         bn = [m for m in self.model if isinstance(m, nn.BatchNorm1d)][0]
         return _P.make_cfg(F, self._kernel_hidden, self.use_spatial_attention, self.training,
                            self.sensor_error_bound, bn.eps, bn.momentum, vfe_features,
-                           getattr(self, "wgrad_split_bf16", False))
+                           getattr(self, "wgrad_split_bf16", False), getattr(self, "act16", 0))
 
     def _ensure_width(self, F):
         if F != self.in_features:

@@ -658,7 +658,10 @@ class SparseEncoderFn(torch.autograd.Function):
                        "rpc_sparse_dense_clear")
             # (the coordinates may come from a rulebook side stream: not reusable before this clear has run)
             prev_coors.record_stream(torch.cuda.current_stream(dev))
-        bufs[bkey] = (base, last["coors_out"], last["n_out"])      # most recently used last
+        # the coordinates kept for the next clear must be this step's own: a submanifold last layer's output
+        # coordinates are its input's (possibly the caller's tensor, which it may refill in place) — keep a copy
+        keep = last["coors_out"].clone() if last["spec"].kind == "subm" else last["coors_out"]
+        bufs[bkey] = (base, keep, last["n_out"])      # most recently used last
         if enc.dense_nhwc:   # channels_last image, logically [B, C*D, H, W]
             dense = base.permute(0, 3, 1, 2)
         else:

@@ -27,9 +27,16 @@ def engine_masks(trace):
 
 
 class FlipStats:
+    """Adopted ReLU decisions that differ from the oracle's own: used by follow_masks (dense) and by
+    oracle/sparse_encoder.OracleSparseEncoder.forward(flips=...) (sparse)."""
+
     def __init__(self):
         self.flips = 0
         self.worst = 0.0   # max |pre| / max_channel |pre| over the flipped decisions
+        self.per_layer = []   # sparse: (layer, differing decisions, worst) per layer
+
+    def __repr__(self):
+        return f"FlipStats(flips={self.flips}, worst={self.worst:.3e})"
 
 
 def follow_masks(hip_mods, ref_mods, masks, stats=None):

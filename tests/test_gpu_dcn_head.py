@@ -211,18 +211,30 @@ def _ref_head(head, x, B, H, W):
     return torch.cat(hms, 1), torch.cat(boxes, 1), P
 
 
+@pytest.mark.parametrize("offsets", ["random", "zero"])
 @pytest.mark.parametrize("mode", ["bf16", "fp32"])
-def test_center_head_forward_backward(mode):
+def test_center_head_forward_backward(mode, offsets):
+    """offsets "random": offset convs drawn so the samples spread over whole cells; "zero": upstream's own starting
+    state — the DCNSeparateHead offset convs are zero-initialised, so every sample lies exactly ON an integer
+    position (a cell edge), where mmcv's offset gradient is one-sided (get_coordinate_weight on the cell
+    [floor(p), floor(p) + 1]; samples at p = -1 or p = H lie outside and carry none). The offset-conv gradients
+    are then the whole learning signal of the DCN offsets in the reference's first step."""
     f32 = mode == "fp32"
     tol_out, tol_x, cos_min = (1e-4, 1e-3, 0.99999) if f32 else (3e-2, None, 0.98)
     torch.manual_seed(0)
     B, Cin, H, W = 2, 128, 32, 32
     head = CenterHead(in_channels=Cin).to(DEV)
-    with torch.no_grad():   # non-zero offsets (the offset convs are zero-initialised)
-        for th in head.task_heads:
+    if offsets == "zero":
+        for th in head.task_heads:   # (the constructor's own init, asserted)
             for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
-                dcn.conv_offset.weight.normal_(0, 0.05)
-                dcn.conv_offset.bias.uniform_(-0.5, 0.5)
+                assert float(dcn.conv_offset.weight.abs().max()) == 0.0
+                assert float(dcn.conv_offset.bias.abs().max()) == 0.0
+    else:
+        with torch.no_grad():   # non-zero offsets (the offset convs are zero-initialised)
+            for th in head.task_heads:
+                for dcn in (th.feature_adapt_cls, th.feature_adapt_reg):
+                    dcn.conv_offset.weight.normal_(0, 0.05)
+                    dcn.conv_offset.bias.uniform_(-0.5, 0.5)
     x = _bf(torch.randn(B, Cin, H, W)).float()
     xd = x.to(DEV).to(torch.float32 if f32 else torch.bfloat16).requires_grad_(True)
     preds = head([xd])

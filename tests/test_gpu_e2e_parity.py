@@ -54,7 +54,7 @@ LOSS_TOL = 1e-4
 GRAD_REL = 2e-2
 GRAD_F64_MAX = 1e-2
 GRAD_F64_MEAN = 2e-3
-FLIP_PRE_MAX = 1e-4   # a dense ReLU decision float64 makes differently lies within this of 0 (x channel max |pre|)
+FLIP_PRE_MAX = 1e-4   # a dense or sparse ReLU decision float64 makes differently lies within this of 0 (x channel max)
 # Round 3 measured middle.11.gamma at 1.005e-2 from float64 and loosened this bound; round 4 re-ran the test with
 # each backward variant switched off (tools/gpu_e2e_ab.sh: default, RPC_SPARSE_NATIVE=0, RPC_DENSE_BNFUSE=0, both;
 # profiles/r04_e2e_backward_ab.log): all four give the same gradients — the one-call sparse backward is bit-identical
@@ -75,10 +75,11 @@ class _Middle(nn.Module):
         super().__init__()
         self.enc, self.dtype = enc, dtype
         self.masks = None
+        self.flips = None   # FlipStats: adopted sparse decisions that differ from this oracle's own
 
     def forward(self, feats, coors, batch_size):
         return self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size,
-                                masks=self.masks).to(self.dtype)
+                                masks=self.masks, flips=self.flips).to(self.dtype)
 
 
 class _Adversary(nn.Module):
@@ -154,10 +155,12 @@ class _Oracle:
         self.ref.train()
         self.ref._epoch = 3
 
-    def step(self, rv, rn, rc, cb, cl, B, masks=None, dense_masks=None, flips=None):
+    def step(self, rv, rn, rc, cb, cl, B, masks=None, dense_masks=None, flips=None, sparse_flips=None):
         """masks / dense_masks: the sparse encoder's / the dense engine's ReLU decisions (oracle/sparse_encoder.py,
-        tests/_dense_masks.py); the dense decisions that differ from this oracle's own are counted in `flips`."""
+        tests/_dense_masks.py); the decisions that differ from this oracle's own are counted in `flips` (dense) and
+        `sparse_flips` (sparse)."""
         self.ref.middle_encoder.masks = masks
+        self.ref.middle_encoder.flips = sparse_flips
         hooks = [] if dense_masks is None else follow_masks((self.model.backbone, self.model.neck),
                                                             (self.backbone, self.neck), dense_masks, flips)
         rbatch = dict(voxels=dict(voxels=torch.from_numpy(rv).to(self.dtype), num_points=torch.from_numpy(rn),
@@ -251,11 +254,14 @@ def test_adversarial_step_fp32_hip_matches_oracle(classes):
     # decision moved backbone.blocks.1.1.bias by 1.04e-2 for Car, gpurun_out r05m)
     dmasks = engine_masks(dense_bev.DEBUG)
     dense_bev.DEBUG = None
-    flips = FlipStats()
+    flips, sflips = FlipStats(), FlipStats()
     o32.step(rv, rn, rc, cb, cl, B, masks, dmasks)
-    o64.step(rv, rn, rc, cb, cl, B, masks, dmasks, flips)
+    o64.step(rv, rn, rc, cb, cl, B, masks, dmasks, flips, sflips)
     print(f"dense ReLU decisions differing from float64's: {flips.flips} (max |pre| {flips.worst:.1e} of channel max)")
+    print(f"sparse ReLU decisions differing from float64's: {sflips.flips} (max |act| {sflips.worst:.1e} of channel "
+          f"max; per layer {sflips.per_layer})")
     assert flips.worst <= FLIP_PRE_MAX, flips.worst
+    assert sflips.worst <= FLIP_PRE_MAX, sflips
     rlosses, rtotal = o32.losses, o32.total
 
     # ---- losses: every key within 1e-4 of the fp32 oracle

@@ -16,8 +16,8 @@ Tolerances: voxels bit-exact; every loss key within 1e-4 * max(1, |ref|) of the 
 parameter gradient within GRAD_F64_MAX relative L2 of float64, their mean within GRAD_F64_MEAN, cosine >= COS_MIN
 (the fixed bounds of tests/test_gpu_e2e_parity.py). Both oracles evaluate the sparse encoder and the dense
 SECOND / SECONDFPN on HIP's ReLU decisions (same-branch parity: oracle/sparse_encoder.py `masks`,
-tests/_dense_masks.py), and every dense decision the float64 oracle would take differently must lie within
-FLIP_PRE_MAX of zero. r05 (gpurun_out r05o): 43 / 115 such decisions, all within 3.6e-6 of the channel's max
+tests/_dense_masks.py), and every dense or sparse decision the float64 oracle would take differently must lie
+within FLIP_PRE_MAX of zero (r06: the sparse decisions are bounded too). r05 (gpurun_out r05o): 43 / 115 such decisions, all within 3.6e-6 of the channel's max
 |pre|; HIP 4.7e-5 / 2.8e-4 mean, 1.2e-3 / 2.1e-3 max from float64 (fp32 oracle 3.8e-4 / 2.6e-4 mean) for
 B = 2 one-sweep / B = 4 three-sweep frames. Without the dense masks one decision at x_hat ~ 0 with a large
 gradient behind it moved the CenterPoint backbone's gradients by 1.3e-2 (tools/dbg_cp_bb.py: blocks.1.7.bias
@@ -89,9 +89,11 @@ class _Middle(nn.Module):
         self.enc, self.dtype = enc, dtype
         self.out = None
         self.masks = None
+        self.flips = None   # FlipStats: adopted sparse decisions that differ from this oracle's own
 
     def forward(self, feats, coors, batch_size):
-        out = self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size, masks=self.masks).to(self.dtype)
+        out = self.enc.forward(feats.to(self.dtype), coors.numpy(), batch_size, masks=self.masks,
+                               flips=self.flips).to(self.dtype)
         self.out = out.detach()
         return out
 
@@ -196,10 +198,12 @@ class OracleStep:
         self.ref.train()
         self.ref._epoch = model._epoch
 
-    def step(self, rv, rn, rc, gts, masks=None, dense_masks=None, flips=None):
-        """masks: the sparse encoder's ReLU decisions (oracle/sparse_encoder.py); dense_masks: the dense engine's
-        (tests/_dense_masks.py) for SECOND + SECONDFPN, whose decisions that differ are counted in `flips`."""
+    def step(self, rv, rn, rc, gts, masks=None, dense_masks=None, flips=None, sparse_flips=None):
+        """masks: the sparse encoder's ReLU decisions (oracle/sparse_encoder.py), whose decisions that differ from
+        this oracle's own are counted in `sparse_flips`; dense_masks: the dense engine's (tests/_dense_masks.py) for
+        SECOND + SECONDFPN, counted in `flips`."""
         self.ref.pts_middle_encoder.masks = masks
+        self.ref.pts_middle_encoder.flips = sparse_flips
         hooks = [] if dense_masks is None else follow_masks(
             (self.model.pts_backbone, self.model.pts_neck), (self.ref.pts_backbone, self.ref.pts_neck), dense_masks,
             flips)
@@ -303,11 +307,14 @@ def test_adversarial_centerpoint_step_fp32_hip_matches_oracle(B, sweeps):
     assert np.array_equal(vd["voxels"].cpu().numpy().view(np.uint32), rv.view(np.uint32))
 
     # ---- oracle steps
-    flips = FlipStats()
+    flips, sflips = FlipStats(), FlipStats()
     o32.step(rv, rn, rc, ogts, masks, dmasks)
-    o64.step(rv, rn, rc, ogts, masks, dmasks, flips)
+    o64.step(rv, rn, rc, ogts, masks, dmasks, flips, sflips)
     print(f"dense ReLU decisions differing from float64's: {flips.flips} (max |pre| {flips.worst:.1e} of channel max)")
+    print(f"sparse ReLU decisions differing from float64's: {sflips.flips} (max |act| {sflips.worst:.1e} of channel "
+          f"max; per layer {sflips.per_layer})")
     assert flips.worst <= FLIP_PRE_MAX, flips.worst
+    assert sflips.worst <= FLIP_PRE_MAX, sflips
     eps_mid = _rel(mid["hip"].float().cpu(), o64.ref.pts_middle_encoder.out)
     print(f"B={B} sweeps={sweeps} voxels {rv.shape[0]}; encoder output: HIP vs float64 {eps_mid:.2e} "
           f"(fp32 oracle {_rel(o32.ref.pts_middle_encoder.out, o64.ref.pts_middle_encoder.out):.2e})")

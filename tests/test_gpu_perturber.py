@@ -269,3 +269,52 @@ def test_wgrad_split_bf16_close_to_fp32():
             assert rel <= 1e-4, (n, rel)
         else:
             assert torch.equal(a, b), n
+
+
+# (gradient rel-L2, cosine) bounds per act16: bf16 gradient rows alone round each term once (unbiased: sums keep
+# ~2^-9 / sqrt(N)); fp16 pre-activations flip ReLU decisions (docstring)
+GRAD_BOUNDS = {2: (1e-2, 0.9999), 3: (0.1, 0.995)}
+
+
+@pytest.mark.parametrize("act16", [2, 3])
+def test_act16_rows_close_to_fp32(act16):
+    """Perf mode's 16-bit hidden-layer rows (rpc_perturber_cfg.act16: 2 = bf16 gradient rows dh / dz (the bench's
+    default), 3 = also fp16 pre-activations z_1..z_3) against fp32 rows on the same step (metric widths [64, 128, 64], 60k points,
+    split-bf16 weight gradients both ways). The reference AMP (train.py:91-103) runs these Linear layers in fp16.
+    Bounds (measured r06 in the test output): perturbation (out - x) and the four loss terms within 5e-3 relative;
+    every parameter gradient within GRAD_REL relative L2 and cosine >= GRAD_COS, the biases before train-mode
+    BatchNorm excepted (exact gradient 0: summation noise). The gradient bound is loose by construction: with a
+    random upstream gradient G the BatchNorm-beta / weight gradients are sums of zero-mean terms (~sqrt(N) of
+    N), and every ReLU decision a 16-bit pre-activation takes differently (an fp16 rounding of z ~ 10 is ~5e-3
+    of the normalised unit: ~0.2 % of the decisions) moves such a sum by a whole term — the same mechanism as
+    the sparse encoder's (tests/test_gpu_sparse_layers.py). Training-level agreement is bounded by
+    tests/test_gpu_bf16_trajectory.py on the real loss."""
+    from robustpointclouds_amd.plugin.models.adversarial.voxel_perturber import VoxelPerturber
+    dev = torch.device("cuda")
+    torch.manual_seed(7)
+    vp = VoxelPerturber(hidden_channels=[64, 128, 64]).to(dev).train()
+    vp.wgrad_split_bf16 = True
+    g = torch.Generator().manual_seed(8)
+    x = (torch.randn(60000, 4, generator=g) * torch.tensor([20.0, 20.0, 1.0, 0.3])).to(dev)
+    G = (torch.randn(60000, 4, generator=g) * 1e-4).to(dev)
+    res = {}
+    for a in (0, act16):
+        vp.act16 = a
+        vp.zero_grad(set_to_none=True)
+        out, ld = vp(x)
+        ((out * G).sum() + 1e-3 * ld["l2_norm"]).backward()
+        torch.cuda.synchronize()
+        res[a] = (out.detach().clone(), {k: float(v) for k, v in ld.items()},
+                  {n: p.grad.detach().clone() for n, p in vp.named_parameters()})
+    (o0, l0, g0), (o1, l1, g1) = res[0], res[act16]
+    rel = lambda a, b: float((a - b).norm() / b.norm().clamp_min(1e-30))
+    ep = rel(o1 - x, o0 - x)
+    el = max(abs(l1[k] - l0[k]) / max(abs(l0[k]), 1e-12) for k in l0)
+    lin = [n for n, m in vp.model.named_children() if isinstance(m, torch.nn.Linear)]
+    noise = {f"model.{lin[l]}.bias" for l in range(0, 5)}
+    cos = lambda a, b: float((a.flatten() @ b.flatten()) / (a.norm() * b.norm()).clamp_min(1e-30))
+    eg = sorted(((rel(g1[n], g0[n]), n, cos(g1[n], g0[n])) for n in g0 if n not in noise), reverse=True)
+    print(f"act16={act16}: perturbation rel {ep:.2e}, losses rel {el:.2e}, worst gradients {eg[:4]}")
+    assert ep <= 5e-3 and el <= 5e-3, (ep, el)
+    grad_rel, grad_cos = GRAD_BOUNDS[act16]
+    assert eg[0][0] <= grad_rel and min(e[2] for e in eg) >= grad_cos, eg[:4]

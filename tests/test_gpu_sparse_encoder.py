@@ -8,8 +8,10 @@ from oracle import voxelize as ov
 from oracle.sparse_encoder import OracleSparseEncoder, implementation_masks, spconv_pairs, subm_pairs
 from robustpointclouds_amd.sparse_encoder import SparseEncoder
 from robustpointclouds_amd.synthetic import KITTI_PC_RANGE, KITTI_VOXEL_SIZE, kitti_frame
+from tests._dense_masks import FlipStats
 
 pytestmark = pytest.mark.gpu
+FLIP_PRE_MAX = 1e-4   # an adopted ReLU decision float64 takes differently lies within this of 0 (x channel max |act|)
 
 
 def _inputs(B, stride=3, seed=0):
@@ -49,7 +51,11 @@ def test_sparse_encoder_forward_backward_matches_oracle(B, stride, basic):
     masks = implementation_masks(enc.debug)
     enc.debug = None
     ref_f = torch.from_numpy(feats).double().requires_grad_(True)
-    ref = orc.forward(ref_f, coors, B, masks=masks)
+    flips = FlipStats()
+    ref = orc.forward(ref_f, coors, B, masks=masks, flips=flips)
+    print(f"sparse ReLU decisions differing from float64's: {flips.flips} (max |act| {flips.worst:.1e} of channel "
+          f"max; per layer {flips.per_layer})")
+    assert flips.worst <= FLIP_PRE_MAX, flips
     assert out.shape == ref.shape == (B, 256, 200, 176)
     o = out.detach().cpu().double()
     scale = ref.abs().max().item()
@@ -232,3 +238,36 @@ def test_dense_buffer_cleared_between_steps(bf16):
     enc.__dict__.pop("_dense_bufs")
     want = enc(torch.from_numpy(fb).to(dev), torch.from_numpy(cb).to(dev), 2)
     assert torch.equal(got, want)   # (a cell of the first step left behind would differ from the fresh zeros)
+
+
+@pytest.mark.parametrize("C,flags", [(6, 0), (6, 1), (6, 3), (8, 2)])
+def test_dense_clear_any_width(C, flags):
+    """rpc_sparse_dense_clear for output widths that are not a multiple of 4 (its scalar form) and the
+    vector form: exactly the cells of the given coordinates (every channel, NCHW [B][C*D][H][W] or NHWC
+    [B][H][W][C*D]) become 0, every other cell keeps its value."""
+    from robustpointclouds_amd import _ffi
+    dev = torch.device("cuda")
+    B, D, H, W = 2, 2, 9, 7
+    rng = np.random.default_rng(C + flags)
+    cells = rng.choice(B * D * H * W, 23, replace=False)
+    b, r = np.divmod(cells, D * H * W)
+    z, r = np.divmod(r, H * W)
+    y, x = np.divmod(r, W)
+    coors = torch.from_numpy(np.stack([b, z, y, x], 1).astype(np.int32)).to(dev)
+    dt = torch.bfloat16 if flags & 2 else torch.float32
+    nhwc = bool(flags & 1)
+    dense = torch.arange(1, B * C * D * H * W + 1, dtype=torch.float32).to(dt).to(dev)
+    dense = dense.view((B, H, W, C * D) if nhwc else (B, C * D, H, W))
+    want = dense.clone()
+    for bi, zi, yi, xi in zip(b, z, y, x):
+        for c in range(C):
+            if nhwc:
+                want[bi, yi, xi, c * D + zi] = 0
+            else:
+                want[bi, c * D + zi, yi, xi] = 0
+    lib = _ffi.load()
+    st = _ffi.stream_of(dense)
+    _ffi.check(lib.rpc_sparse_dense_clear(_ffi.ptr(coors), len(cells), C, _ffi.int_arr((B, D, H, W)), flags,
+                                          _ffi.ptr(dense), st), "clear")
+    torch.cuda.synchronize()
+    assert torch.equal(dense, want)

@@ -14,7 +14,8 @@ import torch
 from oracle.sparse_encoder import OracleSparseEncoder, implementation_masks
 from robustpointclouds_amd import sparse_encoder as SE
 from robustpointclouds_amd.sparse_encoder import SparseEncoder
-from tests.test_gpu_sparse_encoder import _inputs
+from tests._dense_masks import FlipStats
+from tests.test_gpu_sparse_encoder import FLIP_PRE_MAX, _inputs
 
 pytestmark = pytest.mark.gpu
 
@@ -24,10 +25,10 @@ def _key(c):
     return ((c[:, 0] * 64 + c[:, 1]) * 2048 + c[:, 2]) * 2048 + c[:, 3]
 
 
-def _oracle_run(enc, feats, coors, G, masks=None, **kw):
+def _oracle_run(enc, feats, coors, G, masks=None, flips=None, **kw):
     orc = OracleSparseEncoder(enc, **kw)
     f = torch.from_numpy(feats).double().requires_grad_(True)
-    ref = orc.forward(f, coors, 1, keep=True, masks=masks)
+    ref = orc.forward(f, coors, 1, keep=True, masks=masks, flips=flips)
     (ref * G.double()).sum().backward()
     return orc, f.grad
 
@@ -55,7 +56,11 @@ def test_per_layer_errors(capsys, mode, monkeypatch):
     # on the other side moves every gradient below it by ~1e-3 — the 1e-4 bar then measures the arithmetic
     masks = implementation_masks(enc.debug) if mode == "fp32" else None
     enc.debug = None
-    orc, ref_fg = _oracle_run(enc, feats, coors, G, masks=masks)
+    sflips = FlipStats() if masks is not None else None
+    orc, ref_fg = _oracle_run(enc, feats, coors, G, masks=masks, flips=sflips)
+    if sflips is not None:   # the adopted decisions float64 takes differently lie within FLIP_PRE_MAX of 0
+        print(f"sparse ReLU decisions differing from float64's: {sflips}")
+        assert sflips.worst <= FLIP_PRE_MAX, sflips
     emu, emu_fg = (_oracle_run(enc, feats, coors, G, bf16_from=1, fwd_fp16=mode == "perf")
                    if mode != "fp32" else (None, None))
     worst_z = 0.0

@@ -57,11 +57,11 @@ def select_engines(model: nn.Module, bf16: bool, pin: bool = False) -> None:
         # perf mode: the perturber's hidden-layer weight gradients on split-bf16 MFMA (perturb.make_cfg);
         # RPC_PERT_SPLIT=0 keeps them on fp32 MFMA
         adv.wgrad_split_bf16 = bool(bf16) and os.environ.get("RPC_PERT_SPLIT", "1") != "0"
-        # perf mode: 16-bit hidden-layer rows (rpc_perturber_cfg.act16): 2 = bf16 gradient rows (default);
-        # 1 / 3 add fp16 pre-activations, which flip ReLU decisions enough to move the 6-step adversary update
-        # cosine vs fp32 from 0.9955 to 0.9940 (tests/test_gpu_bf16_trajectory.py bound 0.995: not the default);
-        # RPC_PERT_ACT16 overrides, 0 keeps fp32 rows
-        adv.act16 = int(os.environ.get("RPC_PERT_ACT16", "2")) if bf16 else 0
+        # perf mode option: 16-bit hidden-layer rows (rpc_perturber_cfg.act16: 2 = bf16 gradient rows, 1 / 3 =
+        # fp16 pre-activations / both). Off by default: measured r06 (profiles/r06_pert_act16_ab.txt) act16 = 2
+        # takes the perturber backward 0.51 -> 0.435 ms (+0.5 % step) but moves the 6-step adversary update
+        # cosine vs fp32 to 0.9949 and act16 = 3 to 0.9940, under tests/test_gpu_bf16_trajectory.py's 0.995
+        adv.act16 = int(os.environ.get("RPC_PERT_ACT16", "0")) if bf16 else 0
     model.__dict__["_engine_mode"] = bool(bf16)
     if pin:
         model.__dict__["_engine_pinned"] = True

@@ -348,6 +348,17 @@ def _conv_nobn_bwd(eng, rec, dz, dev, st, need_dx=True, dx_out=None, accumulate=
     return dx, dW[:rec["n"]]
 
 
+# test hook (tests/test_gpu_dcn_head.py): when a list, each training forward appends one entry per ConvModule
+# BatchNorm — (module name, z [cells][co] pre-BN image, bn [4co] scale / beta / mean / invstd, channel slice, B,
+# H, W) — from which the engine's exact ReLU decisions are recomputed (tests/_dense_masks.py engine_masks form)
+DEBUG = None
+
+
+def _debug(name, rec, sl, B, H, W):
+    if DEBUG is not None:
+        DEBUG.append((name, rec["z"].detach(), rec["bn"].detach(), sl, B, H, W))
+
+
 def _conv_module_layer(cm):
     return db._Layer(db.S1, cm.conv, cm.bn, 0, cm.conv.in_channels, cm.conv.out_channels, 9)
 
@@ -380,6 +391,8 @@ class CenterHeadFn(torch.autograd.Function):
         y0, rsh, _, _ = db._forward_layer(eng, Lsh, xi, Cin, B, H, W, training, dev, st,
                                           wts=prep[id(head.shared_conv.conv)])
         bns = [head.shared_conv.bn]
+        if training:
+            _debug("shared_conv", rsh, None, B, H, W)
         trecs = []
         c0 = 0
         # the DCN offsets of every task and branch: one 64 -> 18 * 2 * tasks conv of the shared image
@@ -411,6 +424,8 @@ class CenterHeadFn(torch.autograd.Function):
             hcls, rc, _, _ = db._forward_layer(eng, L, tr["cls"]["feat"], 64, B, H, W, training, dev, st,
                                                wts=prep[id(th.cls_head[0].conv)])
             bns.append(th.cls_head[0].bn)
+            if training:
+                _debug(f"task_heads.{t}.cls_head.0", rc, None, B, H, W)
             fc = th.cls_head[1]
             z, frec = _conv_nobn_fwd(eng, fc.weight, 64, hcls, 64, B, H, W, dev, st, prep[id(fc)])
             _ffi.check(pack(_ffi.ptr(z), _PAD, th.num_cls, _ffi.ptr(fc.bias.detach().float().contiguous()),
@@ -427,6 +442,8 @@ class CenterHeadFn(torch.autograd.Function):
                                              wts=prep[("regcat", id(th))])
             if training:
                 cbn.write_back()
+                for k, name in enumerate(_BOX_ORDER):
+                    _debug(f"task_heads.{t}.task_head.{name}.0", rr, slice(64 * k, 64 * (k + 1)), B, H, W)
             bns.extend(cbn.bns)
             fcs = [getattr(th.task_head, name)[1] for name in _BOX_ORDER]
             nb = sum(f.weight.shape[0] for f in fcs)

@@ -2096,6 +2096,230 @@ __global__ __launch_bounds__(WSB, 1) void k_wgrad_s1(WG g, int nseg_x, int seg_p
   }
 }
 
+// ------------------------------------------------------------------ 3x3 stride-1 weight gradient, column walk, 9 taps
+// k_wgrad_s1c: the S1 weight gradient with ONE block per (SEG-pixel column strip, 64 ci x 128 co tile, run of
+// image rows) accumulating all 9 taps, walking the strip DOWN the image. An x row r (pixels x0 - 1 .. x0 + SEG)
+// is staged once and serves output rows r + 1, r, r - 1 (dy = 0, 1, 2) at its three column shifts (dx); the dz
+// row y once for all 9 taps. Per output row the block stages one x row (SEG + 2 px x 128 B) and one dz row (SEG
+// px x 256 B) for 9 x 64 x 128 MACs per pixel: 2.6 KB of LDS-DMA per MFLOP against k_wgrad_s1's 5.2 (3 taps of
+// one kernel row per staged tile) — the S1 weight gradient is bound by its per-CU staging.
+// Steps walk the x rows r = -1 .. H of each image (zero rows at -1 and H, so no row ever mixes two images); the
+// step of x row r computes output row r - 1 (none for r < 1). A run of steps [s0, s1) is preceded by its two
+// warm-up rows s0 - 2, s0 - 1 (staged, not computed). Ring: XS = L + 3 x-row slots (three read per step, L in
+// flight), DS = L + 1 dz slots; every wave issues the same PW DMA instructions per step, so one counted vmcnt
+// retires a step. Rows are unpadded: x rows of 128 B with granule g at slot g ^ (((p >> 1) & 3) << 1), dz rows
+// of 256 B at g ^ ((p & 7) << 1) (pixel p): every transposed operand read (8 consecutive pixels x one granule
+// pair per 32 lanes) hits 32 distinct 8-byte bank words. 8 waves = 4 (16 ci) x 2 (64 co), each 9 taps x 4
+// accumulator tiles (144 VGPRs), two waves per SIMD. Partial sums go to part[run][strip][t][ci][co] (the
+// k_wgrad_reduce slab layout: chunks = runs x strips).
+constexpr int WC_L = 2;     // steps of DMA look-ahead
+template <int SEG>
+struct S1C {
+  static constexpr int XR = SEG + 2, NXI = (XR + 7) / 8, NDI = SEG / 4, NI = NXI + NDI, PW = (NI + 7) / 8;
+  static constexpr int XSB = NXI * 1024, DSB = NDI * 1024, XS = WC_L + 3, DS = WC_L + 1;
+  static constexpr int LDSB = XS * XSB + DS * DSB;
+  static_assert(LDSB <= 160 * 1024, "ring");
+};
+__device__ __forceinline__ int s1c_xswz(int p) { return ((p >> 1) & 3) << 1; }
+__device__ __forceinline__ int s1c_dswz(int p) { return (p & 7) << 1; }
+template <int SEG, int DBG = 0>   // DBG: timing arms (knob 7) — 1: no slab stores, 2: no MFMAs, 4: no LDS reads
+__global__ __launch_bounds__(WSB, 1) void k_wgrad_s1c(WG g, int nstrip, int steps_per) {
+  using K = S1C<SEG>;
+  constexpr int PW = K::PW, NXI = K::NXI, NI = K::NI, XR = K::XR;
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[K::LDSB];
+  unsigned char* const xring = lds;
+  unsigned char* const dring = lds + K::XS * K::XSB;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);   // wave-uniform: the DMA table below stays scalar
+  const int wci = w >> 1, wco = w & 1;
+  const int nco = g.CO / 128, ntile = (g.CI / 64) * nco;
+  const int lid = xcd_remap(blockIdx.x, gridDim.x);        // a run's tiles and strips adjacent (one XCD's L2)
+  const int tile = lid % ntile, rest = lid / ntile;
+  const int strip = rest % nstrip, run = rest / nstrip;
+  const int ci0 = (tile / nco) * 64, co0 = (tile % nco) * 128;
+  const int H = g.R.H, W = g.R.W, HP = H + 2;
+  const int nsteps = g.R.B * HP;
+  const int s0 = min(nsteps, run * steps_per), s1 = min(nsteps, s0 + steps_per);
+  const int x0 = strip * SEG;
+
+  // ---- per-lane DMA constants: instruction k = w + 8m (surplus ones repeat the last: same bytes, same place);
+  // k < NXI: x pixels 8k .. 8k + 7 (lane L: pixel 8k + L / 8, slot L % 8), else dz pixels 4k' .. 4k' + 3 (lane L:
+  // pixel 4k' + L / 16, slot L % 16); the lane's source granule is its slot ^ swizzle(pixel)
+  const u16* const gx = g.x;
+  const u16* const gdz = g.dz;
+  const int XP = g.XP, DP = g.DP;
+  int loff[PW];   // per lane: element offset of its granule in the image row, -1: zero (outside the image)
+#pragma unroll
+  for (int m = 0; m < PW; ++m) {
+    const int k = min(w + 8 * m, NI - 1);
+    if (k < NXI) {
+      const int p = 8 * k + (lane >> 3), sl = lane & 7, xc = x0 - 1 + p;
+      loff[m] = (p < XR && xc >= 0 && xc < W) ? xc * XP + ci0 + (sl ^ s1c_xswz(p)) * 8 : -1;
+    } else {
+      const int kd = k - NXI, p = 4 * kd + (lane >> 4), sl = lane & 15, xc = x0 + p;
+      loff[m] = xc < W ? xc * DP + co0 + (sl ^ s1c_dswz(p)) * 8 : -1;
+    }
+  }
+  // step s: x row r = s % HP - 1 of image s / HP into x slot s % XS; for r >= 1 the dz row r - 1 into dz slot
+  // s % DS; rows outside the image / steps outside [0, nsteps) read the zero row
+  struct Iss {
+    const u16* xsrc;   // image row base of the x row (nullptr: zero row)
+    const u16* dsrc;   // of the dz row
+    unsigned char* xdst;
+    unsigned char* ddst;
+  };
+  auto issue_prep = [&](int s) {
+    const int b = s >= 0 ? s / HP : 0, r = s >= 0 ? s - b * HP - 1 : -1;
+    const bool live = s >= 0 && s < nsteps;
+    const bool xrow = live && r >= 0 && r < H, drow = live && r >= 1;
+    const int xs = ((s % K::XS) + K::XS) % K::XS, ds = ((s % K::DS) + K::DS) % K::DS;
+    Iss q;
+    q.xsrc = xrow ? gx + (size_t)(b * H + r) * W * XP : nullptr;
+    q.dsrc = drow ? gdz + (size_t)(b * H + r - 1) * W * DP : nullptr;
+    q.xdst = xring + xs * K::XSB;
+    q.ddst = dring + ds * K::DSB;
+    return q;
+  };
+  auto issue_one = [&](const Iss& q, int m) {
+    const int k = min(w + 8 * m, NI - 1);   // (uniform)
+    const bool isx = k < NXI;
+    const u16* base = isx ? q.xsrc : q.dsrc;
+    const u16* src = (loff[m] >= 0 && base != nullptr) ? base + loff[m] : (const u16*)g_zero_row;
+    glds16(src, (isx ? q.xdst + k * 1024 : q.ddst + (k - NXI) * 1024));
+  };
+  auto issue = [&](int s) {
+    const Iss q = issue_prep(s);
+#pragma unroll
+    for (int m = 0; m < PW; ++m) issue_one(q, m);
+  };
+
+  // ---- operand offsets (as k_wgrad_s1): lane reads pixel rowoff (+16) of a 32-pixel K-step, 4 channels 4 (lane & 3)
+  const int g4 = lane >> 4, qq = (lane & 15) >> 2, pp = lane & 3, rowoff = 4 * g4 + qq;
+  unsigned aoff[3], boff[4];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    const int p = rowoff + dx, gr = 2 * wci + (pp >> 1);
+    aoff[dx] = p * 128 + ((gr ^ s1c_xswz(p)) << 4) + 8 * (pp & 1);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int gr = ((wco * 64 + j * 16) >> 3) + (pp >> 1);
+    boff[j] = rowoff * 256 + ((gr ^ s1c_dswz(rowoff)) << 4) + 8 * (pp & 1);
+  }
+  f32x4 acc[9][4];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[t][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
+
+  const unsigned xl0 = (unsigned)(size_t)((__attribute__((address_space(3))) unsigned char*)xring);
+  const unsigned dl0 = (unsigned)(size_t)((__attribute__((address_space(3))) unsigned char*)dring);
+  if (s0 < s1) {
+#pragma unroll
+    for (int k = 0; k < WC_L; ++k) issue(s0 - 2 + k);
+    for (int s = s0 - 2; s < s1; ++s) {
+      // retire step s (the L - 1 younger steps stay in flight), publish, then refill the slots step s - 1 read
+      asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"((WC_L - 1) * PW) : "memory");
+      const int r = s - (s / HP) * HP - 1;   // (s >= s0 - 2 >= -2; only s >= s0 computes)
+      // a computing step spreads the DMA of step s + L over its MFMA groups (issued between them, each piece's
+      // issue cost lies under the wave's MFMAs instead of delaying its first operand reads); DBG 8: all at once.
+      // (Written as two ifs, not an early `continue`: with the continue the compiler kept the DMA state live
+      // across both paths and spilled the accumulators.)
+      const Iss iq = issue_prep(s + WC_L);
+      const bool comp = s >= s0 && r >= 1;
+      if (!comp || (DBG & 8)) {
+#pragma unroll
+        for (int m = 0; m < PW; ++m) issue_one(iq, m);
+      }
+      if (comp) {
+      // x slots of steps s - 2, s - 1, s = x rows y - 1, y, y + 1 of output row y = r - 1 (dy = 0, 1, 2)
+      unsigned xb[3];
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy) xb[dy] = xl0 + (unsigned)(((s - 2 + dy) % K::XS) * K::XSB);
+      const unsigned db = dl0 + (unsigned)((s % K::DS) * K::DSB);
+      // per K-step of 32 pixels: 4 dz fragments + 3 x fragments per kernel row dy; the reads of the next
+      // kernel row (or the next K-step's dz and first row) are issued before this row's 12 MFMAs, so each
+      // wave's LDS reads lie under its own MFMAs (two fragment buffers per operand)
+#define S1C_RB(BV, ks)                                                                                      \
+      if (!(DBG & 4)) _Pragma("unroll") for (int j = 0; j < 4; ++j) {                                        \
+        const unsigned pb = db + boff[j] + 32 * (ks) * 256;                                                 \
+        s16x4 v[2] = {tr_read_asm(pb), tr_read_asm(pb + 16 * 256)};                                         \
+        BV[j] = *(bf16x8*)v;                                                                                \
+      }
+#define S1C_RA(AV, ks, dy)                                                                                  \
+      if (!(DBG & 4)) _Pragma("unroll") for (int dx = 0; dx < 3; ++dx) {                                     \
+        const unsigned pa = xb[dy] + aoff[dx] + 32 * (ks) * 128;                                            \
+        s16x4 v[2] = {tr_read_asm(pa), tr_read_asm(pa + 16 * 128)};                                         \
+        AV[dx] = *(bf16x8*)v;                                                                               \
+      }
+#define S1C_WAIT_A(AV) asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(AV[0]), "+v"(AV[1]), "+v"(AV[2]));
+#define S1C_WAIT_AB(AV, BV)                                                                                 \
+      asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(AV[0]), "+v"(AV[1]), "+v"(AV[2]), "+v"(BV[0]), "+v"(BV[1]), \
+                   "+v"(BV[2]), "+v"(BV[3]));
+#define S1C_MMA(AV, BV, dy)                                                                                 \
+      if (!(DBG & 2)) _Pragma("unroll") for (int dx = 0; dx < 3; ++dx)                                       \
+        _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                       \
+          acc[(dy) * 3 + dx][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(AV[dx], BV[j], acc[(dy) * 3 + dx][j], 0, 0, 0);
+      constexpr int NG = 3 * (SEG / 32);   // MFMA groups per step
+#define S1C_ISSUE(gi)                                                                                       \
+      if (!(DBG & 8)) _Pragma("unroll") for (int m = (gi) * PW / NG; m < ((gi) + 1) * PW / NG; ++m) issue_one(iq, m);
+      // one dz fragment buffer (a second one spilled): the next K-step's dz and first x row are read after
+      // this K-step's last MFMA group has been issued
+      bf16x8 bc[4], a0[3], a1[3];
+      S1C_RB(bc, 0)
+      S1C_RA(a0, 0, 0)
+#pragma unroll
+      for (int ks = 0; ks < SEG / 32; ++ks) {
+        S1C_WAIT_AB(a0, bc)
+        S1C_RA(a1, ks, 1)
+        S1C_MMA(a0, bc, 0)
+        S1C_ISSUE(ks * 3 + 0)
+        S1C_WAIT_A(a1)
+        S1C_RA(a0, ks, 2)
+        S1C_MMA(a1, bc, 1)
+        S1C_ISSUE(ks * 3 + 1)
+        S1C_WAIT_A(a0)
+        S1C_MMA(a0, bc, 2)
+        S1C_ISSUE(ks * 3 + 2)
+        if (ks + 1 < SEG / 32) {
+          S1C_RB(bc, ks + 1)
+          S1C_RA(a0, ks + 1, 0)
+        }
+      }
+#undef S1C_RB
+#undef S1C_RA
+#undef S1C_WAIT_A
+#undef S1C_WAIT_AB
+#undef S1C_MMA
+#undef S1C_ISSUE
+      }
+    }
+    // drain the look-ahead DMAs before the block exits
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  // lane (a15 = lane & 15, g4) of tile (t, j) holds dW[t][ci0 + 16 wci + 4 g4 + r][co0 + 64 wco + 16 j + a15]
+  const size_t slab = (size_t)g.CI * g.CO;
+  float* out = g.part + (size_t)(run * nstrip + strip) * 9 * slab;
+  if (DBG & 1) {
+    float t = 0.f;
+#pragma unroll
+    for (int k = 0; k < 9; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) t += acc[k][j][0] + acc[k][j][1] + acc[k][j][2] + acc[k][j][3];
+    if (t == 12345.f) out[tid] = t;
+    return;
+  }
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int ci = ci0 + 16 * wci + 4 * g4 + r, co = co0 + 64 * wco + 16 * j + (lane & 15);
+        out[t * slab + (size_t)ci * g.CO + co] = acc[t][j][r];
+      }
+}
+
 // ------------------------------------------------------------------ BatchNorm passes (8 channels / thread)
 // Every pass maps a 256-thread block to (256 / CG) row lanes x CG channel groups of 8 (CG = C / 8),
 // so a thread keeps its 8 channels' BatchNorm parameters in registers for all of its rows, and
@@ -2437,6 +2661,40 @@ static bool s1_xwide(const int* r_img, int cout) {
 // k_conv3x3 at 32 output channels per block when the 64-channel grid is less than one round of its two
 // blocks per CU (knob 5 / RPC_DENSE_S1N32: 0 = by shape, 1 = never, 2 = always)
 static int g_s1_n32 = env_int("RPC_DENSE_S1N32", 0);
+// k_wgrad_s1c segment length (knob 6 / RPC_DENSE_S1C_SEG: 0 = by shape, else 32 / 64 / 96)
+static int g_s1c_seg = env_int("RPC_DENSE_S1C_SEG", 0);
+static int g_s1c_dbg = 0;   // knob 7: k_wgrad_s1c timing arms (0 = the real kernel)
+
+// k_wgrad_s1c geometry: column strips of SEG pixels (the segment length with the least padding of an image row),
+// tiles of 64 ci x 128 co, runs of steps sized so strips x tiles x runs fills one round of the CUs (one block per
+// CU); the slabs it writes (runs x strips of [9][CI][CO]) are the workspace
+struct S1cGeo {
+  int seg, nstrip, nrun, steps_per;
+};
+static S1cGeo s1c_geometry(const Img& R, int ci, int co, int force_seg = 0) {
+  S1cGeo q;
+  // the segment (32 / 64 / 96 pixels) with the least padding of an image row, the longest on a tie (fewer
+  // barriers per MFMA); knob 6 / RPC_DENSE_S1C_SEG forces one
+  const int cand[3] = {96, 64, 32};
+  q.seg = 96;
+  int best = 1 << 30;
+  for (int k = 0; k < 3; ++k) {
+    const int pad = (R.W + cand[k] - 1) / cand[k] * cand[k] - R.W;
+    if (pad < best) { best = pad; q.seg = cand[k]; }
+  }
+  if (g_s1c_seg == 32 || g_s1c_seg == 64 || g_s1c_seg == 96) q.seg = g_s1c_seg;
+  if (force_seg) q.seg = force_seg;
+  q.nstrip = (R.W + q.seg - 1) / q.seg;
+  const int per = q.nstrip * (ci / 64) * (co / 128);
+  const int nsteps = R.B * (R.H + 2);
+  int nrun = cu_count() / per > 0 ? cu_count() / per : 1;
+  nrun = nrun < nsteps ? nrun : nsteps;
+  q.steps_per = (nsteps + nrun - 1) / nrun;
+  q.nrun = (nsteps + q.steps_per - 1) / q.steps_per;
+  return q;
+}
+static bool s1c_ok(int ci, int co) { return ci % 64 == 0 && co % 128 == 0; }
+
 static bool s1_n32(int tiles, int cout) {
   if (g_s1_n32 == 1) return false;
   if (g_s1_n32 == 2) return true;
@@ -2470,6 +2728,16 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   if (knob == 5) {
     const int old = g_s1_n32;
     if (value >= 0 && value <= 2) g_s1_n32 = value;
+    return old;
+  }
+  if (knob == 7) {
+    const int old = g_s1c_dbg;
+    if (value >= 0) g_s1c_dbg = value;
+    return old;
+  }
+  if (knob == 6) {
+    const int old = g_s1c_seg;
+    if (value >= 0) g_s1c_seg = value;
     return old;
   }
   if (knob == 2) {
@@ -2598,7 +2866,15 @@ extern "C" int rpc_dense_conv_blocks(int map, const int* r_img) {
 extern "C" size_t rpc_dense_wgrad_workspace_size(int map, const int* r_img, int ci, int co) {
   const int M = r_img[0] * r_img[1] * r_img[2];
   const int T = map_wtaps(map);
-  return (size_t)wgrad_chunks(M, T, ci, co) * T * ci * co * sizeof(float);
+  size_t n = (size_t)wgrad_chunks(M, T, ci, co);
+  if (map == M_S1 && s1c_ok(ci, co)) {   // any S1 kernel and segment (knobs 1 / 6 may switch between launches)
+    for (int seg = 32; seg <= 96; seg += 32) {
+      const S1cGeo q = s1c_geometry(img3(r_img), ci, co, seg);
+      const size_t c = (size_t)q.nrun * q.nstrip;
+      n = c > n ? c : n;
+    }
+  }
+  return n * T * ci * co * sizeof(float);
 }
 
 extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci, const void* dz, int dp, int co,
@@ -2619,7 +2895,26 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
   }
   const int rows_per = ((M + chunks - 1) / chunks + 63) / 64 * 64;
   WG g{(const u16*)x, xp, (const u16*)dz, dp, ci, co, R, S, O, M, rows_per, part};
-  if (map == M_S1 && ci % 128 == 0 && co % 128 == 0 && (g_wgrad_variant == 0 || g_wgrad_variant == 2)) {
+  int nred = chunks;
+  if (map == M_S1 && s1c_ok(ci, co) && g_wgrad_variant == 3) {
+    // column walk, all 9 taps per block
+    const S1cGeo q = s1c_geometry(R, ci, co);
+    nred = q.nrun * q.nstrip;
+    if (ws_bytes < (size_t)nred * slab * sizeof(float)) return RPC_ERR_WORKSPACE;
+    if ((size_t)M * (xp > dp ? xp : dp) >= (1ULL << 31)) return RPC_ERR_UNSUPPORTED;   // 32-bit lane offsets
+    const dim3 grid(q.nrun * q.nstrip * (ci / 64) * (co / 128));
+    if (q.seg == 96) {
+      switch (g_s1c_dbg) {
+        case 1: hipLaunchKernelGGL((k_wgrad_s1c<96, 1>), grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per); break;
+        case 3: hipLaunchKernelGGL((k_wgrad_s1c<96, 3>), grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per); break;
+        case 7: hipLaunchKernelGGL((k_wgrad_s1c<96, 7>), grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per); break;
+        case 5: hipLaunchKernelGGL((k_wgrad_s1c<96, 5>), grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per); break;
+        case 8: hipLaunchKernelGGL((k_wgrad_s1c<96, 8>), grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per); break;
+        default: hipLaunchKernelGGL((k_wgrad_s1c<96>), grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per);
+      }
+    } else if (q.seg == 64) hipLaunchKernelGGL(k_wgrad_s1c<64>, grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per);
+    else hipLaunchKernelGGL(k_wgrad_s1c<32>, grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per);
+  } else if (map == M_S1 && ci % 128 == 0 && co % 128 == 0 && (g_wgrad_variant == 0 || g_wgrad_variant == 2)) {
     // tap-sharing row-segment kernel: segment length with the least padding of the image row
     const int seg = (R.W + 63) / 64 * 64 <= (R.W + 31) / 32 * 32 ? 64 : 32;
     const int nsx = (R.W + seg - 1) / seg, nseg = R.B * R.H * nsx;
@@ -2640,7 +2935,7 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
     default: launch_wgrad<M_U2>(g, chunks, st); break;
   }
   RPC_LAUNCH_CHECK();
-  hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(cdivu(slab, 64)), dim3(256), 0, st, (const float*)part, chunks, kind, ci, co,
+  hipLaunchKernelGGL(k_wgrad_reduce<0>, dim3(cdivu(slab, 64)), dim3(256), 0, st, (const float*)part, nred, kind, ci, co,
                      T, dW);
   RPC_LAUNCH_CHECK();
   return RPC_OK;

@@ -597,3 +597,42 @@ def test_wprep_batch_matches_per_layer_prep():
                                        _ffi.stream_of(W)), "rpc_dense_wprep")
         torch.cuda.synchronize()
         assert torch.equal(wf, rf) and torch.equal(wd, rd), (kind, ci, co, T, flip)
+
+
+@pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 2, 200, 176), (256, 256, 2, 100, 88), (256, 128, 1, 37, 45),
+                                         (64, 128, 2, 17, 70), (192, 256, 1, 5, 130), (128, 128, 3, 1, 33)])
+def test_s1_wgrad_column_walk_kernel(ci, co, B, H, W):
+    """k_wgrad_s1c (rpc_dense_tune knob 1 = 3: column strips walked down the image, all 9 taps per block, one staged
+    x row per output row) against float64 torch at 1e-5 of the gradient scale and against the per-tap kernel k_wgrad
+    (knob 1 = 1: the same bf16 products, fp32 sums in another order) within 2e-6; run twice, bit-identical; every
+    segment length (knob 6: 32, 64, 96 pixels) within 1e-5 of float64. Shapes:
+    the metric's S1 layers at batch 2, 64-channel tiles (ci 64, 192), one-row images, strips past the image edge."""
+    lib = _ffi.load()
+    x = _rand(B, ci, H, W, seed=41)
+    dz = _rand(B, co, H, W, seed=42)
+    Wt = _rand(co, ci, 3, 3, seed=43, scale=0.05)
+    wr = Wt.double().requires_grad_(True)
+    F.conv2d(x.double(), wr, padding=1).backward(dz.double())
+    img = _ffi.int_arr((B, H, W))
+    wsz = lib.rpc_dense_wgrad_workspace_size(S1, img, ci, co)
+    ws = _ffi.workspace(wsz, DEV)
+    xn, dn = _nhwc(x), _nhwc(dz)
+    outs = []
+    for variant, seg in ((3, 0), (3, 0), (1, 0), (3, 32), (3, 64), (3, 96)):
+        old = lib.rpc_dense_tune(1, variant)
+        old6 = lib.rpc_dense_tune(6, seg)
+        try:
+            dW = torch.full(Wt.shape, float("nan"), dtype=torch.float32, device=DEV)
+            _ffi.check(lib.rpc_dense_wgrad(S1, 0, _ffi.ptr(xn), ci, ci, _ffi.ptr(dn), co, co, img, img, img,
+                                           _ffi.ptr(dW), _ffi.ptr(ws), wsz, _ffi.stream_of(dW)), "rpc_dense_wgrad")
+            torch.cuda.synchronize()
+        finally:
+            lib.rpc_dense_tune(1, old)
+            lib.rpc_dense_tune(6, old6)
+        outs.append(dW.double().cpu())
+    scale = wr.grad.abs().max().item()
+    assert (outs[0] - wr.grad).abs().max().item() <= 1e-5 * scale
+    assert (outs[0] - outs[2]).abs().max().item() <= 2e-6 * scale
+    assert torch.equal(outs[0], outs[1])
+    for o in outs[3:]:   # every segment length (knob 6)
+        assert (o - wr.grad).abs().max().item() <= 1e-5 * scale

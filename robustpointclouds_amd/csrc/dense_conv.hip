@@ -2263,13 +2263,15 @@ __global__ __launch_bounds__(WSB, 1) void k_wgrad_s1c(WG g, int nstrip, int step
       constexpr int NG = 3 * (SEG / 32);   // MFMA groups per step
 #define S1C_ISSUE(gi)                                                                                       \
       if (!(DBG & 8)) _Pragma("unroll") for (int m = (gi) * PW / NG; m < ((gi) + 1) * PW / NG; ++m) issue_one(iq, m);
-      // one dz fragment buffer (a second one spilled): the next K-step's dz and first x row are read after
-      // this K-step's last MFMA group has been issued
-      bf16x8 bc[4], a0[3], a1[3];
-      S1C_RB(bc, 0)
+      // dz fragments double-buffered: the next K-step's dz and first x row are read before this K-step's last
+      // MFMA group
+      bf16x8 b0[4], b1[4], a0[3], a1[3];
+      S1C_RB(b0, 0)
       S1C_RA(a0, 0, 0)
 #pragma unroll
       for (int ks = 0; ks < SEG / 32; ++ks) {
+        bf16x8* bc = (ks & 1) ? b1 : b0;   // (constant after unrolling)
+        bf16x8* bn = (ks & 1) ? b0 : b1;
         S1C_WAIT_AB(a0, bc)
         S1C_RA(a1, ks, 1)
         S1C_MMA(a0, bc, 0)
@@ -2279,11 +2281,15 @@ __global__ __launch_bounds__(WSB, 1) void k_wgrad_s1c(WG g, int nstrip, int step
         S1C_MMA(a1, bc, 1)
         S1C_ISSUE(ks * 3 + 1)
         S1C_WAIT_A(a0)
+        if (ks + 1 < SEG / 32) {
+          S1C_RB(bn, ks + 1)
+          S1C_RA(a1, ks + 1, 0)
+        }
         S1C_MMA(a0, bc, 2)
         S1C_ISSUE(ks * 3 + 2)
         if (ks + 1 < SEG / 32) {
-          S1C_RB(bc, ks + 1)
-          S1C_RA(a0, ks + 1, 0)
+#pragma unroll
+          for (int dx = 0; dx < 3; ++dx) a0[dx] = a1[dx];
         }
       }
 #undef S1C_RB
@@ -2631,7 +2637,11 @@ static int env_int(const char* name, int dflt) {
   return v && *v ? atoi(v) : dflt;
 }
 static int g_s1_variant = env_int("RPC_DENSE_S1", 0);   // A/B: RPC_DENSE_S1=<knob 0 value> for a whole run
-static int g_wgrad_variant = env_int("RPC_DENSE_WGRAD", 0);   // A/B: RPC_DENSE_WGRAD=<knob 1 value>
+// S1 weight gradient (knob 1 / RPC_DENSE_WGRAD): 0 = by shape (k_wgrad_s1c where ci % 64 == 0 and co % 128 == 0,
+// else k_wgrad_s1 for 128-multiples, else k_wgrad), 1 = k_wgrad, 2 = k_wgrad_s1 without its read pipeline,
+// 3 = k_wgrad_s1c, 4 = k_wgrad_s1 (r03-r05 default). r06: k_wgrad_s1c 0.88 vs k_wgrad_s1 1.00 ms per 3-class step
+// (tools/s1wg_bench.py, profiles/r06_s1wg_ab.txt)
+static int g_wgrad_variant = env_int("RPC_DENSE_WGRAD", 0);
 static int g_s1x_dbg = 0;          // knob 4: k_conv3x3x timing experiments (0 = the real kernel)
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
@@ -2896,7 +2906,7 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
   const int rows_per = ((M + chunks - 1) / chunks + 63) / 64 * 64;
   WG g{(const u16*)x, xp, (const u16*)dz, dp, ci, co, R, S, O, M, rows_per, part};
   int nred = chunks;
-  if (map == M_S1 && s1c_ok(ci, co) && g_wgrad_variant == 3) {
+  if (map == M_S1 && s1c_ok(ci, co) && (g_wgrad_variant == 0 || g_wgrad_variant == 3)) {
     // column walk, all 9 taps per block
     const S1cGeo q = s1c_geometry(R, ci, co);
     nred = q.nrun * q.nstrip;
@@ -2914,7 +2924,8 @@ extern "C" int rpc_dense_wgrad(int map, int kind, const void* x, int xp, int ci,
       }
     } else if (q.seg == 64) hipLaunchKernelGGL(k_wgrad_s1c<64>, grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per);
     else hipLaunchKernelGGL(k_wgrad_s1c<32>, grid, dim3(WSB), 0, st, g, q.nstrip, q.steps_per);
-  } else if (map == M_S1 && ci % 128 == 0 && co % 128 == 0 && (g_wgrad_variant == 0 || g_wgrad_variant == 2)) {
+  } else if (map == M_S1 && ci % 128 == 0 && co % 128 == 0 &&
+             (g_wgrad_variant == 0 || g_wgrad_variant == 2 || g_wgrad_variant == 4)) {
     // tap-sharing row-segment kernel: segment length with the least padding of the image row
     const int seg = (R.W + 63) / 64 * 64 <= (R.W + 31) / 32 * 32 ? 64 : 32;
     const int nsx = (R.W + seg - 1) / seg, nseg = R.B * R.H * nsx;

@@ -555,7 +555,7 @@ def test_s1_wgrad_tap_sharing_kernel(ci, co, B, H, W):
     ws = _ffi.workspace(wsz, DEV)
     xn, dn = _nhwc(x), _nhwc(dz)
     outs = []
-    for variant in (0, 1, 2):
+    for variant in (4, 1, 2):   # (knob 1: 4 = k_wgrad_s1, 1 = k_wgrad, 2 = k_wgrad_s1's former loop)
         old = lib.rpc_dense_tune(1, variant)
         try:
             dW = torch.full(Wt.shape, float("nan"), dtype=torch.float32, device=DEV)

@@ -1,6 +1,6 @@
 """S1 weight-gradient timing (rpc_dense_wgrad, its slab reduce included) on the metric's SECOND shapes, per
-rpc_dense_tune knob-1 variant: 0 = k_wgrad_s1 (row segments, 3 taps per block), 3 = k_wgrad_s1c (column walk,
-9 taps per block). HIP-event us per call, median of rounds.
+rpc_dense_tune knob-1 variant: 4 = k_wgrad_s1 (row segments, 3 taps per block), 3 = k_wgrad_s1c (column walk,
+9 taps per block; the default 0 since r06). HIP-event us per call, median of rounds.
 
     python tools/s1wg_bench.py [variants...]
 """
@@ -19,7 +19,7 @@ SHAPES = [("200x176 256->128", (6, 200, 176), 256, 128, 1), ("200x176 128->128",
 
 
 def main():
-    variants = sys.argv[1:] or ["0", "3"]   # "v" or "v:seg" or "v:seg:dbg" (knobs 6 / 7: k_wgrad_s1c segment, arms)
+    variants = sys.argv[1:] or ["4", "3"]   # "v" or "v:seg" or "v:seg:dbg" (knobs 6 / 7: k_wgrad_s1c segment, arms)
     lib = _ffi.load()
     dev = torch.device("cuda")
     tot = {v: 0.0 for v in variants}

@@ -36,7 +36,9 @@ constexpr int GRID = 256;        // blocks of every per-point VALU pass (= parti
 constexpr int MFW = 8;           // waves per block of the MFMA hidden-layer passes: 256 blocks x 8
 constexpr int MFBLK = MFW * 64;  // waves = 2 waves per SIMD on 256 CUs (256 VGPRs), GRID partial rows
 constexpr int MAXF = 8;
-constexpr int MAXC = 128;
+constexpr int MAXC = 128;         // widest layer of the MFMA hidden-layer kernels (their LDS sums)
+constexpr int MAXW = 256;         // widest hidden layer: wider ones run on the per-point VALU kernels
+constexpr int PSTR = 2 * MAXW;    // row stride of the partial-sum rows part / gpart
 constexpr int NTICKET = 16;       // hand-off points per pass (each TSTRIDE counters, see grid_col_totals)
 constexpr int GS = 16;            // blocks per first-level reduction group
 constexpr int NGRP = GRID / GS;   // groups
@@ -72,12 +74,12 @@ struct Dev {
   float* z[5];     // [C_{l+1}][S] channel-major
   float* bn[5];    // [4*C]: scale (gamma*invstd), beta, mean, invstd
   double* bnsum[5];  // backward: [2*C] sum dy, sum dy*xhat
-  double* part;    // [GRID][2*MAXC]
-  double* gpart;   // [NGRP][2*MAXC] group sums of part
+  double* part;    // [GRID][PSTR]
+  double* gpart;   // [NGRP][PSTR] group sums of part
   float* pstat;    // [4*MAXF]: mean_f, s_f, cimb_f, S
   unsigned* ticket;
   float* dz[6];    // dz_0..dz_4 [C_{l+1}][S], dz_5 [F][S]
-  float* dh[2];    // [MAXC][S] post-ReLU grads, ping-pong
+  float* dh[2];    // [MAXW][S] post-ReLU grads, ping-pong
   float* dsig;     // [S]
   float* da;       // [A][S]
   float* aact;     // [A][S]
@@ -115,21 +117,21 @@ struct ChanAcc {
     for (int k = 0; k < K; ++k) {
       int c = k * 64 + lane;
       if (c < C) {
-        lds[(w * 2 + 0) * MAXC + c] = s[0][k];
-        lds[(w * 2 + 1) * MAXC + c] = s[1][k];
+        lds[(w * 2 + 0) * MAXW + c] = s[0][k];
+        lds[(w * 2 + 1) * MAXW + c] = s[1][k];
       }
     }
     __syncthreads();
     for (int j = threadIdx.x; j < 2 * C; j += BLK) {
       int which = j / C, c = j - which * C;
       double t = 0.0;
-      for (int ww = 0; ww < NWAVE; ++ww) t += lds[(ww * 2 + which) * MAXC + c];
-      part[(size_t)blockIdx.x * 2 * MAXC + j] = t;
+      for (int ww = 0; ww < NWAVE; ++ww) t += lds[(ww * 2 + which) * MAXW + c];
+      part[(size_t)blockIdx.x * PSTR + j] = t;
     }
   }
 };
 
-// Column totals of the GRID partial rows part[r][0..ncol) (ncol <= 2 * MAXC), handed off in two
+// Column totals of the GRID partial rows part[r][0..ncol) (ncol <= PSTR), handed off in two
 // levels: the last-arriving block of each group of GS consecutive blocks sums its group's rows in row
 // order into gpart[q]; the last group finisher sums gpart[0..NGRP) in group order into lds[0..ncol)
 // and returns true (every other block returns false). Each level issues all of its GS resp. NGRP
@@ -143,17 +145,17 @@ __device__ bool grid_col_totals(Dev& d, int k, int ncol, double* lds, int* flag)
   for (int j = threadIdx.x; j < ncol; j += blockDim.x) {
     double v[GS];
 #pragma unroll
-    for (int i = 0; i < GS; ++i) v[i] = d.part[(size_t)(q * GS + i) * 2 * MAXC + j];
+    for (int i = 0; i < GS; ++i) v[i] = d.part[(size_t)(q * GS + i) * PSTR + j];
     double t = 0.0;
 #pragma unroll
     for (int i = 0; i < GS; ++i) t += v[i];
-    d.gpart[(size_t)q * 2 * MAXC + j] = t;
+    d.gpart[(size_t)q * PSTR + j] = t;
   }
   if (!last_block_arrive_2d(tk, flag, NGRP)) return false;
   for (int j = threadIdx.x; j < ncol; j += blockDim.x) {
     double v[NGRP];
 #pragma unroll
-    for (int i = 0; i < NGRP; ++i) v[i] = d.gpart[(size_t)i * 2 * MAXC + j];
+    for (int i = 0; i < NGRP; ++i) v[i] = d.gpart[(size_t)i * PSTR + j];
     double t = 0.0;
 #pragma unroll
     for (int i = 0; i < NGRP; ++i) t += v[i];
@@ -260,7 +262,7 @@ __global__ __launch_bounds__(BLK) void k_xstats(Dev d) {
   if (threadIdx.x < 2 * F + 1) {
     double t = 0.0;
     for (int ww = 0; ww < NWAVE; ++ww) t += lds[ww * 2 * MAXC + threadIdx.x];
-    d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
+    d.part[(size_t)blockIdx.x * PSTR + threadIdx.x] = t;
   }
   if (!grid_col_totals(d, 0, 2 * F + 1, lds, &lastf)) return;
   if (threadIdx.x == 0) {
@@ -294,11 +296,14 @@ __device__ __forceinline__ void load_xn(const Dev& d, int slot, float (&xv)[F], 
   }
 }
 
+// VALU hidden layers whose weights exceed 64 KB read them from global memory (wave-uniform loads)
+__host__ __device__ constexpr bool wide_w(int CI, int CO) { return CI * CO > 16384; }
+
 // layer 0: xn -> z0 (+ batch stats / finalize BN0)
 template <int F, int CO>
 __global__ __launch_bounds__(BLK) void k_fwd_first(Dev d) {
   __shared__ float sW[CO * F + CO];
-  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ double lds[NWAVE * 2 * MAXW];
   __shared__ int lastf;
   for (int j = threadIdx.x; j < CO * F; j += BLK) sW[j] = d.W[0][j];
   for (int j = threadIdx.x; j < CO; j += BLK) sW[CO * F + j] = d.b[0][j];
@@ -332,14 +337,16 @@ __global__ __launch_bounds__(BLK) void k_fwd_first(Dev d) {
 // layer l (1..4): relu(bn_{l-1}(z_{l-1})) -> z_l
 template <int CI, int CO>
 __global__ __launch_bounds__(BLK) void k_fwd_mid(Dev d, int l) {
-  __shared__ float sW[CO * CI + CO + 3 * CI];
-  __shared__ double lds[NWAVE * 2 * MAXC];
+  constexpr int WN = wide_w(CI, CO) ? 0 : CO * CI;  // weights staged in LDS (else read from global)
+  __shared__ float sW[WN + CO + 3 * CI];
+  __shared__ double lds[NWAVE * 2 * MAXW];
   __shared__ int lastf;
-  for (int j = threadIdx.x; j < CO * CI; j += BLK) sW[j] = d.W[l][j];
-  for (int j = threadIdx.x; j < CO; j += BLK) sW[CO * CI + j] = d.b[l][j];
-  for (int j = threadIdx.x; j < 3 * CI; j += BLK) sW[CO * CI + CO + j] = d.bn[l - 1][j];
+  for (int j = threadIdx.x; j < WN; j += BLK) sW[j] = d.W[l][j];
+  for (int j = threadIdx.x; j < CO; j += BLK) sW[WN + j] = d.b[l][j];
+  for (int j = threadIdx.x; j < 3 * CI; j += BLK) sW[WN + CO + j] = d.bn[l - 1][j];
   __syncthreads();
-  const float* sc = sW + CO * CI + CO;
+  const float* Wl = WN ? sW : d.W[l];
+  const float* sc = sW + WN + CO;
   const float* sh = sc + CI;
   const float* mu = sh + CI;
   const int N = d.meta[0];
@@ -355,9 +362,9 @@ __global__ __launch_bounds__(BLK) void k_fwd_mid(Dev d, int l) {
       h[c] = act ? fmaxf(fmaf(zi[(size_t)c * d.S] - mu[c], sc[c], sh[c]), 0.0f) : 0.0f;
 #pragma unroll
     for (int o = 0; o < CO; ++o) {
-      float a = sW[CO * CI + o];
+      float a = sW[WN + o];
 #pragma unroll
-      for (int c = 0; c < CI; ++c) a = fmaf(sW[o * CI + c], h[c], a);
+      for (int c = 0; c < CI; ++c) a = fmaf(Wl[o * CI + c], h[c], a);
       float z = act ? a : 0.0f;
       if (act) d.z[l][(size_t)o * d.S + i] = z;
       if (d.training) acc.add1(o, z, z * z);
@@ -449,7 +456,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_last(Dev d) {
   if (threadIdx.x < NS) {
     double t = 0.0;
     for (int ww = 0; ww < NWAVE; ++ww) t += lds[ww * 2 * MAXC + threadIdx.x];
-    d.part[(size_t)blockIdx.x * 2 * MAXC + threadIdx.x] = t;
+    d.part[(size_t)blockIdx.x * PSTR + threadIdx.x] = t;
   }
   if (!grid_col_totals(d, 6, NS, lds, &lastf)) return;
   if (threadIdx.x == 0) {
@@ -540,7 +547,7 @@ __device__ void bnb_finalize(Dev& d, int l, double* lds) {
 template <int CI, int F>
 __global__ __launch_bounds__(BLK) void k_bwd_last(Dev d) {
   __shared__ float sW[F * CI + F + 4 * CI];
-  __shared__ double lds[NWAVE * 2 * MAXC];
+  __shared__ double lds[NWAVE * 2 * MAXW];
   __shared__ int lastf;
   for (int j = threadIdx.x; j < F * CI; j += BLK) sW[j] = d.W[5][j];
   for (int j = threadIdx.x; j < F; j += BLK) sW[F * CI + j] = d.b[5][j];
@@ -640,22 +647,24 @@ __global__ __launch_bounds__(BLK) void k_bwd_last(Dev d) {
 // BN layer l backward (l = 4..1): dz_l from dh_l'; dh_{l-1}' = relu'(.) * W_l^T dz_l
 template <int CI, int CO>
 __global__ __launch_bounds__(BLK) void k_bwd_mid(Dev d, int l, int src) {
-  __shared__ float sW[CO * CI + 7 * CO + 4 * CI];
-  __shared__ double lds[NWAVE * 2 * MAXC];
+  constexpr int WN = wide_w(CI, CO) ? 0 : CO * CI;  // weights staged in LDS (else read from global)
+  __shared__ float sW[WN + 7 * CO + 4 * CI];
+  __shared__ double lds[NWAVE * 2 * MAXW];
   __shared__ int lastf;
   const int N = d.meta[0];
   const double invN = 1.0 / N;
-  for (int j = threadIdx.x; j < CO * CI; j += BLK) sW[j] = d.W[l][j];
-  for (int j = threadIdx.x; j < 4 * CO; j += BLK) sW[CO * CI + j] = d.bn[l][j];
-  for (int j = threadIdx.x; j < 4 * CI; j += BLK) sW[CO * CI + 4 * CO + j] = d.bn[l - 1][j];
+  for (int j = threadIdx.x; j < WN; j += BLK) sW[j] = d.W[l][j];
+  for (int j = threadIdx.x; j < 4 * CO; j += BLK) sW[WN + j] = d.bn[l][j];
+  for (int j = threadIdx.x; j < 4 * CI; j += BLK) sW[WN + 4 * CO + j] = d.bn[l - 1][j];
   for (int j = threadIdx.x; j < CO; j += BLK) {
-    float* m = sW + CO * CI + 4 * CO + 4 * CI;
+    float* m = sW + WN + 4 * CO + 4 * CI;
     m[j] = (float)(d.bnsum[l][j] * invN);
     m[CO + j] = (float)(d.bnsum[l][CO + j] * invN);
     m[2 * CO + j] = d.g[l][j] * d.bn[l][3 * CO + j];
   }
   __syncthreads();
-  const float* bo = sW + CO * CI;      // scale, beta, mean, invstd of layer l
+  const float* Wl = WN ? sW : d.W[l];
+  const float* bo = sW + WN;           // scale, beta, mean, invstd of layer l
   const float* bi = bo + 4 * CO;       // of layer l-1
   const float* m1 = bi + 4 * CI;
   const float* m2 = m1 + CO;
@@ -680,7 +689,7 @@ __global__ __launch_bounds__(BLK) void k_bwd_mid(Dev d, int l, int src) {
     for (int c = 0; c < CI; ++c) {
       float s = 0.0f;
 #pragma unroll
-      for (int o = 0; o < CO; ++o) s = fmaf(sW[o * CI + c], dz[o], s);
+      for (int o = 0; o < CO; ++o) s = fmaf(Wl[o * CI + c], dz[o], s);
       float zc = zp[(size_t)c * d.S];
       float hv = fmaxf(fmaf(zc - bi[2 * CI + c], bi[c], bi[CI + c]), 0.0f);
       s = (act && hv > 0.0f) ? s : 0.0f;
@@ -743,7 +752,7 @@ __global__ __launch_bounds__(BLK) void k_fwd_first_pp(Dev d) {
 constexpr int CSB = 1024;
 template <int C, int MODE>
 __global__ __launch_bounds__(CSB) void k_colstats(Dev d, int l, const float* __restrict__ gsrc, int tk) {
-  __shared__ double lds[2 * MAXC];
+  __shared__ double lds[PSTR];
   __shared__ int lastf;
   const int N = d.meta[0];
   const int rows_per = ((N + GRID - 1) / GRID + 15) & ~15;
@@ -785,8 +794,8 @@ __global__ __launch_bounds__(CSB) void k_colstats(Dev d, int l, const float* __r
       s2 += __shfl_xor(s2, o, 64);
     }
     if (q == 0 && c < C) {
-      d.part[(size_t)blockIdx.x * 2 * MAXC + c] = s1;
-      d.part[(size_t)blockIdx.x * 2 * MAXC + C + c] = s2;
+      d.part[(size_t)blockIdx.x * PSTR + c] = s1;
+      d.part[(size_t)blockIdx.x * PSTR + C + c] = s2;
     }
   }
   if (!grid_col_totals(d, tk, 2 * C, lds, &lastf)) return;
@@ -939,16 +948,22 @@ struct Jobs {
 constexpr int EPT = 8;
 constexpr int TR = 64;
 
+// LDS rows are [r][CO + 1] dz and [r][CI + 2] h values; the row tile tr shrinks so that layers up to MAXW
+// channels wide fit the same 66 KB as the 64-row tile of MAXC-wide ones.
+constexpr int WG_LDS = 2 * TR * (MAXC + 1);
 template <int F>
 __global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
-  __shared__ float sdz[TR * (MAXC + 1)];
-  __shared__ float shh[TR * (MAXC + 1)];
+  __shared__ float sbuf[WG_LDS];
   int chunk = blockIdx.x / J.KS, ks = blockIdx.x - chunk * J.KS;
   int jb = 0;
   while (jb + 1 < J.njob && chunk >= J.cbase[jb + 1]) ++jb;
   const Job& job = J.j[jb];
   const int e0 = (chunk - J.cbase[jb]) * BLK * EPT;
   const int CO = job.CO, CI = job.CI, CI1 = CI + 1;
+  const int SZ = CO + 1, SH = CI1 + 1;
+  const int tr = min(TR, WG_LDS / (SZ + SH));
+  float* sdz = sbuf;
+  float* shh = sbuf + tr * SZ;
   const int N = d.meta[0];
   const int rows_per = (N + J.KS - 1) / J.KS;
   const int r0 = ks * rows_per, r1 = min(N, r0 + rows_per);
@@ -961,15 +976,15 @@ __global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
     eo[k] = e < job.nelem ? e / CI1 : -1;
     ei[k] = e < job.nelem ? e - (e / CI1) * CI1 : 0;
   }
-  for (int rb = r0; rb < r1; rb += TR) {
-    int nr = min(TR, r1 - rb);
+  for (int rb = r0; rb < r1; rb += tr) {
+    int nr = min(tr, r1 - rb);
     __syncthreads();
-    for (int q = threadIdx.x; q < TR * CO; q += BLK) {
-      int o = q / TR, r = q - o * TR;
-      sdz[r * (MAXC + 1) + o] = r < nr ? job.dz[(size_t)o * d.S + rb + r] : 0.0f;
+    for (int q = threadIdx.x; q < tr * CO; q += BLK) {
+      int o = q / tr, r = q - o * tr;
+      sdz[r * SZ + o] = r < nr ? job.dz[(size_t)o * d.S + rb + r] : 0.0f;
     }
-    for (int q = threadIdx.x; q < TR * CI1; q += BLK) {
-      int c = q / TR, r = q - c * TR;
+    for (int q = threadIdx.x; q < tr * CI1; q += BLK) {
+      int c = q / tr, r = q - c * tr;
       float v = 0.0f;
       if (r < nr) {
         int n = rb + r;
@@ -984,7 +999,7 @@ __global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
           v = job.h[(size_t)c * d.S + n];
         }
       }
-      shh[r * (MAXC + 1) + c] = v;
+      shh[r * SH + c] = v;
     }
     __syncthreads();
 #pragma unroll
@@ -993,7 +1008,7 @@ __global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
       float a = acc[k];
       const float* pz = sdz + eo[k];
       const float* ph = shh + ei[k];
-      for (int r = 0; r < TR; ++r) a = fmaf(pz[r * (MAXC + 1)], ph[r * (MAXC + 1)], a);
+      for (int r = 0; r < tr; ++r) a = fmaf(pz[r * SZ], ph[r * SH], a);
       acc[k] = a;
     }
   }
@@ -1253,7 +1268,7 @@ __device__ __forceinline__ void tile_flush(double* part, const double* lds) {
     int which = j / C, c = j - which * C;
     double t = 0.0;
     for (int ww = 0; ww < MFW; ++ww) t += lds[(ww * 2 + which) * MAXC + c];
-    part[(size_t)blockIdx.x * 2 * MAXC + j] = t;
+    part[(size_t)blockIdx.x * PSTR + j] = t;
   }
 }
 
@@ -1852,7 +1867,7 @@ static int widths(const rpc_perturber_cfg* cfg, int C[7]) {
   C[6] = cfg->F;
   if (cfg->F < 4 || cfg->F > 5) return RPC_ERR_UNSUPPORTED;
   for (int k = 1; k < 6; ++k)
-    if (C[k] != 8 && C[k] != 16 && C[k] != 32 && C[k] != 64 && C[k] != 128) return RPC_ERR_UNSUPPORTED;
+    if (C[k] != 8 && C[k] != 16 && C[k] != 32 && C[k] != 64 && C[k] != 128 && C[k] != MAXW) return RPC_ERR_UNSUPPORTED;
   return RPC_OK;
 }
 
@@ -1878,10 +1893,10 @@ static int make_layout(const rpc_perturber_cfg* cfg, int rows, int slots, Layout
   for (int l = 0; l < 5; ++l) { L->z[l] = o; o += al(sizeof(float) * Nmax * C[l + 1]); }
   for (int l = 0; l < 5; ++l) { L->bn[l] = o; o += al(sizeof(float) * 4 * C[l + 1]); }
   for (int l = 0; l < 5; ++l) { L->bnsum[l] = o; o += al(sizeof(double) * 2 * C[l + 1]); }
-  L->part = o; o += al(sizeof(double) * GRID * 2 * MAXC);
+  L->part = o; o += al(sizeof(double) * GRID * PSTR);
   L->pstat = o; o += al(sizeof(float) * 4 * MAXF);
   L->ticket = o; o += al(sizeof(unsigned) * NTICKET * TSTRIDE);
-  L->gpart = o; o += al(sizeof(double) * NGRP * 2 * MAXC);
+  L->gpart = o; o += al(sizeof(double) * NGRP * PSTR);
   for (int l = 0; l < 5; ++l) { L->dz[l] = o; o += al(sizeof(float) * Nmax * C[l + 1]); }
   L->dz[5] = o; o += al(sizeof(float) * Nmax * cfg->F);
   int cmax = 0;
@@ -1991,7 +2006,7 @@ static int fill_dev(const rpc_perturber_cfg* cfg, const float* const* P, const f
 }
 
 // ---- width dispatch
-#define RPC_HID(X) X(8) X(16) X(32) X(64) X(128)
+#define RPC_HID(X) X(8) X(16) X(32) X(64) X(128) X(256)
 
 // per-point passes cover every slot the batch can have (S >= N); blocks past N exit at once
 static inline dim3 pp_grid(const Dev& d) { return dim3((unsigned)((d.S + BLK - 1) / BLK)); }
@@ -2062,7 +2077,7 @@ static void launch_mid16(Dev& d, int l, hipStream_t st, bool bwd, int src) {
   }
 }
 // hidden layer l: fp32-MFMA kernels where the tile shape fits (forward: CO % 16, backward: CI % 16),
-// the per-point VALU kernels otherwise (8-channel layers of the small configs)
+// the per-point VALU kernels otherwise (8-channel layers of the small configs, and layers wider than MAXC)
 template <int CI, int CO>
 static void launch_mid_t(Dev& d, int l, hipStream_t st, bool bwd, int src) {
   if constexpr (a16_shape(CI, CO)) {
@@ -2073,11 +2088,12 @@ static void launch_mid_t(Dev& d, int l, hipStream_t st, bool bwd, int src) {
       default: break;
     }
   }
+  constexpr bool mf = CI <= MAXC && CO <= MAXC;
   if (bwd) {
-    if constexpr (CI % 16 == 0) hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO, BwdF32>), dim3(GRID), dim3(MFBLK), 0, st, d, l, src);
+    if constexpr (mf && CI % 16 == 0) hipLaunchKernelGGL((k_bwd_mid_mf<CI, CO, BwdF32>), dim3(GRID), dim3(MFBLK), 0, st, d, l, src);
     else hipLaunchKernelGGL((k_bwd_mid<CI, CO>), dim3(GRID), dim3(BLK), 0, st, d, l, src);
   } else {
-    if constexpr (CO % 16 == 0) hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO, FwdF32>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
+    if constexpr (mf && CO % 16 == 0) hipLaunchKernelGGL((k_fwd_mid_mf<CI, CO, FwdF32>), dim3(GRID), dim3(MFBLK), 0, st, d, l);
     else hipLaunchKernelGGL((k_fwd_mid<CI, CO>), dim3(GRID), dim3(BLK), 0, st, d, l);
   }
 }
@@ -2099,12 +2115,14 @@ static int launch_mid(int CI, int CO, Dev& d, int l, hipStream_t st, bool bwd, i
     default: return RPC_ERR_UNSUPPORTED;
   }
 }
-static bool wgrad_mf_ok(int CO, int CI) { return CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192; }
+static bool wgrad_mf_ok(int CO, int CI) {
+  return CO % 16 == 0 && CI % 16 == 0 && CO <= MAXC && CI <= MAXC && CO * CI <= 8192;
+}
 // zh16: the jobs' z_{l-1} rows are fp16 (act16 bit 0, layers 2..4); dz rows are bf16 under act16 bit 1 (the
 // split-bf16 kernel only: act16 is a perf-mode option like wgrad_split_bf16)
 template <int CO, int CI>
 static void launch_wgrad_mf_t(Dev& d, const MfJobs& M, int njob, bool split, bool zh16, hipStream_t st) {
-  if constexpr (CO % 16 == 0 && CI % 16 == 0 && CO * CI <= 8192) {
+  if constexpr (CO % 16 == 0 && CI % 16 == 0 && CO <= MAXC && CI <= MAXC && CO * CI <= 8192) {
     if (split) {
       const bool gh = d.a16 & 2;
       if constexpr (a16_shape(CI, CO)) {

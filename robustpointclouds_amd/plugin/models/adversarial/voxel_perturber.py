@@ -11,8 +11,8 @@ Declared deviations (SURVEY.md findings 2, §5):
   reference does (:61) and the model is rebuilt lazily if a forward brings another F;
 * the grad hook clamp(nan_to_num(g), -0.1, 0.1) (:465-475) is applied inside the backward
   kernel to each parameter's full gradient (identical values; no per-tensor hook launches);
-* any hidden_channels up to 128 (the reference builds any widths, :82-103): widths the kernels
-  are not instantiated for (8, 16, 32, 64, 128) run zero-padded to the next one — padded Linear
+* any hidden_channels up to 256 (the reference builds any widths, :82-103): widths the kernels
+  are not instantiated for (8, 16, 32, 64, 128, 256) run zero-padded to the next one — padded Linear
   rows / columns and BatchNorm affine entries are zero, so a padded channel is identically 0 after
   its BatchNorm + ReLU and feeds nothing; the real channels' values, batch statistics and
   gradients are unchanged (autograd slices the padded gradients back), and the running
@@ -37,15 +37,14 @@ from robustpointclouds_amd import perturb as _P
 from ..builder import ADVERSARIES
 
 _HIST_CAP = 1 << 16
-_NATIVE = (8, 16, 32, 64, 128)   # hidden widths the perturber kernels are instantiated for
+_NATIVE = (8, 16, 32, 64, 128, 256)   # hidden widths the perturber kernels are instantiated for
 
 
 def _native_width(c: int) -> int:
     for n in _NATIVE:
         if c <= n:
             return n
-    raise ValueError(f"VoxelPerturber: hidden width {c} > {_NATIVE[-1]} is not supported by the HIP kernels "
-                     "(e.g. configs/adversarial/adversarial-second_strong_v2.py's 256; widths <= 128 are)")
+    raise ValueError(f"VoxelPerturber: hidden width {c} > {_NATIVE[-1]} is not supported by the HIP kernels")
 
 
 class _GradHookClamp(torch.autograd.Function):

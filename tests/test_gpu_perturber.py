@@ -180,16 +180,20 @@ def test_vfe_mean_bit_exact():
     assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("hidden", [[12, 24, 40], [8, 100, 20]])
+@pytest.mark.parametrize("hidden", [[12, 24, 40], [8, 100, 20], [64, 128, 256, 128], [40, 200, 130]])
 def test_plugin_arbitrary_widths_match_oracle(hidden):
     """The reference builds any hidden_channels (voxel_perturber.py:82-103); non-native widths run
     zero-padded to the kernel widths. Forward, loss terms, every parameter gradient (after the
-    ±0.1 hook clamp) and the BatchNorm running statistics must match the float64 oracle."""
+    ±0.1 hook clamp) and the BatchNorm running statistics must match the float64 oracle.
+    [64, 128, 256, 128] is configs/adversarial/adversarial-second_strong_v2.py's list (the reference reads
+    its first three entries): its 256-wide layers run on the per-point VALU kernels; [40, 200, 130] pads
+    to [64, 256, 256]."""
     from robustpointclouds_amd.plugin.models.adversarial.voxel_perturber import VoxelPerturber
     dev = torch.device("cuda")
     torch.manual_seed(3)
     vp = VoxelPerturber(hidden_channels=hidden).to(dev).train()
-    assert vp._padded()
+    hidden = hidden[:3]
+    assert vp._padded() == (hidden != [64, 128, 256])
     lin = [m for m in vp.model if isinstance(m, torch.nn.Linear)]
     bns = [m for m in vp.model if isinstance(m, torch.nn.BatchNorm1d)]
     att = [m for m in vp.attention if isinstance(m, torch.nn.Linear)]

@@ -134,7 +134,8 @@ int rpc_hard_vfe_backward(const RpcHardVfeCfg* cfg, float* const* params, const 
 
 typedef struct {
   int F;                  /* point features (4 KITTI, 5 NuScenes) */
-  int hidden[3];          /* hidden_channels */
+  int hidden[3];          /* hidden_channels, each 8, 16, 32, 64, 128 or 256 (the plugin zero-pads others;
+                             256-wide layers run on the per-point VALU kernels); else RPC_ERR_UNSUPPORTED */
   int use_attention;      /* use_spatial_attention */
   int training;           /* 1 = batch-stat BN + train bounds, 0 = running stats + eval bounds */
   float sensor_error_bound;

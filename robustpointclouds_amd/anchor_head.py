@@ -278,7 +278,9 @@ class HeadLossFn(torch.autograd.Function):
         ctx.save_for_backward(z, bias, asg, out, gb, ws, tab)
         ctx.cfg, ctx.M, ctx.wsz, ctx.layout = cfg, M, wsz, layout
         ctx.mark_non_differentiable(asg)
-        return out[:3].clone(), asg, out[3:].clone()
+        # no zero-filled gradients for the assignment / positive count (a [B, H*W*A] memset per step)
+        ctx.set_materialize_grads(False)
+        return out[:3], asg, out[3:]
 
     @staticmethod
     def backward(ctx, g, _g_asg, _g_npos):

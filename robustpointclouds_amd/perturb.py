@@ -101,6 +101,7 @@ class PerturberFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.save_for_backward(x, ws, *[p for p in params])
         ctx.mark_non_differentiable(losses)
+        ctx.set_materialize_grads(False)   # the flags' gradient stays None (no zero-fill launch)
         return out, losses[:4].clone(), losses
 
     @staticmethod
@@ -135,6 +136,7 @@ class PerturbVoxelsFn(torch.autograd.Function):
         ctx.cfg = cfg
         ctx.save_for_backward(voxels, num_points, ws, *params)
         ctx.mark_non_differentiable(out, losses)
+        ctx.set_materialize_grads(False)   # no zero-filled [V, P, F] / flags gradients per step
         return vfe, losses[:4].clone(), out, losses
 
     @staticmethod

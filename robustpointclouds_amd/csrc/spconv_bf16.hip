@@ -353,6 +353,33 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
       const int r = r0 + w * WR + rt * 16 + (lane >> 4) * 4 + j;
       prow[rt][j] = r < g.Nout ? r : -1;
     }
+  // E_DGRAD / E_RES: the BatchNorm parameters of the block's columns are staged in LDS (the weight tiles' space, free
+  // after the loop's last barrier), and with few output tiles every tile's z rows are loaded before the first store
+  // (one round trip for the epilogue instead of one per tile: the stores of tile n may alias the loads of tile n + 1
+  // as far as the compiler knows; 4 * RT * NT registers, only where RT * NT <= 4)
+  float* const sEbn = (float*)&sB[0][0];   // [4][NGP]: scale, beta, mean, invstd
+  if constexpr (EPI == E_DGRAD || EPI == E_RES) {
+    static_assert(4 * NGP * 4 <= (int)sizeof(sB), "sEbn");
+    const int C = g.CO_real;
+    for (int j = tid; j < 4 * NGP; j += GBLK) {
+      const int q = j / NGP, c = j - q * NGP;
+      sEbn[j] = g.ebn[q * C + min(c, C - 1)];
+    }
+    __syncthreads();
+  }
+  constexpr bool PRE = EPI == E_DGRAD && RT * NT <= 4;
+  float zpre[PRE ? RT : 1][PRE ? NT : 1][4];
+  if constexpr (PRE) {
+    const int C = g.CO_real;
+#pragma unroll
+    for (int n = 0; n < NT; ++n) {
+      const int cc = min(n * 16 + (lane & 15), C - 1);
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) zpre[rt][n][j] = g.ez[(long long)max(prow[rt][j], 0) * C + cc];
+    }
+  }
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
 #pragma unroll
@@ -362,9 +389,14 @@ __global__ __launch_bounds__(64 * gw_of(KGP, NT), gemm_waves_per_simd(KGP, NT)) 
       if (EPI == E_DGRAD || EPI == E_RES) {
         const int C = g.CO_real, cc = min(col, C - 1);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pb[q] = g.ebn[q * C + cc];   // scale, beta, mean, invstd
+        for (int q = 0; q < 4; ++q) pb[q] = sEbn[q * NGP + col];   // scale, beta, mean, invstd (of column cc)
+        if constexpr (PRE) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)max(prow[rt][j], 0) * C + cc];
+          for (int j = 0; j < 4; ++j) zr[j] = zpre[PRE ? rt : 0][PRE ? n : 0][j];
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j) zr[j] = g.ez[(long long)max(prow[rt][j], 0) * C + cc];
+        }
       }
       if (EPI == E_RES) {
         const int C = g.CO_real, cc = min(col, C - 1);

@@ -1025,8 +1025,11 @@ __global__ __launch_bounds__(BLK) void k_wgrad(Dev d, Jobs J) {
 // sweep over a per-block table of source rows (raw / BatchNorm+ReLU / normalised-x gather), double
 // buffered: the next tile's loads are in flight while the current one is summed.
 // (One block grid per job — 4 jobs x 256 ranges of 7 serial tiles — took 97 us.)
-// 1024 threads (16 waves per CU keep the staging loads in flight); WPRE float4 per thread: nrow <= 768
-constexpr int TRP = 64, TPP = TRP + 1, WPB = 1024, WPRE = 12, WEPT = 2;
+// 1024 threads (16 waves per CU keep the staging loads in flight); WPRE float4 per thread: nrow * TR / 4 <= 12288.
+// TR = points per tile, the largest of 256 / 128 / 64 whose two tile buffers fit the LDS (host): a block's range is
+// a chain of tiles (fetch one ahead, two barriers per tile), so fewer, larger tiles shorten it (r06: 64-point tiles
+// made nuScenes' 10-sweep batch ~60 tiles per block)
+constexpr int WPB = 1024, WPRE = 12, WEPT = 2;
 struct RowSrc {
   const float* p;   // channel row base ([S] floats); XN: nullptr
   float mu, sc, be; // BNRELU: relu((v - mu) * sc + be)
@@ -1042,8 +1045,9 @@ __device__ __forceinline__ float row_value(const Dev& d, const RowSrc& rs, int n
   const float v = rs.p[n];
   return rs.kind == H_BNRELU ? fmaxf(fmaf(v - rs.mu, rs.sc, rs.be), 0.0f) : v;
 }
-template <int F>
+template <int F, int TRP>
 __global__ __launch_bounds__(WPB) void k_wgrad_pp(Dev d, Jobs J, int nrow) {
+  constexpr int TPP = TRP + 1;
   extern __shared__ float sbuf[];
   RowSrc* rows = (RowSrc*)(sbuf + 2 * ((nrow * TPP + 3) & ~3));
   const int N = d.meta[0];
@@ -2311,17 +2315,26 @@ extern "C" int rpc_perturber_backward(const rpc_perturber_cfg* cfg, const float*
     // one launch over KS point ranges covering every VALU job (LDS sized to the jobs' tile rows)
     int nrow = 0, nel = 0;
     for (int k = 0; k < nv; ++k) { nrow += JV.j[k].CO + JV.j[k].CI; nel += JV.j[k].nelem; }
-    const size_t lds = (size_t)2 * ((nrow * TPP + 3) & ~3) * sizeof(float) + (size_t)nrow * sizeof(RowSrc);
-    if (nel > WPB * WEPT || lds > 160 * 1024 || nrow * (TRP / 4) > WPB * WPRE) {
+    auto lds_of = [&](int tr) {
+      return (size_t)2 * ((nrow * (tr + 1) + 3) & ~3) * sizeof(float) + (size_t)nrow * sizeof(RowSrc);
+    };
+    int tr = 0;
+    for (int t = 256; t >= 64 && !tr; t >>= 1)
+      if (lds_of(t) <= 160 * 1024 && nrow * (t / 4) <= WPB * WPRE) tr = t;
+    if (nel > WPB * WEPT || !tr) {
       // wide VALU hidden layers (CO * CI > 8192): the per-job chunked kernel
       if (F == 4) hipLaunchKernelGGL((k_wgrad<4>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
       else hipLaunchKernelGGL((k_wgrad<5>), dim3(chunks * ks), dim3(BLK), 0, st, d, JV);
-    } else if (F == 4) {
-      if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_wgrad_pp<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((k_wgrad_pp<4>), dim3(ks), dim3(WPB), lds, st, d, JV, nrow);
     } else {
-      if (lds > 64 * 1024) (void)hipFuncSetAttribute((const void*)k_wgrad_pp<5>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      hipLaunchKernelGGL((k_wgrad_pp<5>), dim3(ks), dim3(WPB), lds, st, d, JV, nrow);
+      const size_t lds = lds_of(tr);
+#define WPP_CASE(FF, TT)                                                                                      \
+  if (F == FF && tr == TT) {                                                                                  \
+    if (lds > 64 * 1024)                                                                                      \
+      (void)hipFuncSetAttribute((const void*)k_wgrad_pp<FF, TT>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds); \
+    hipLaunchKernelGGL((k_wgrad_pp<FF, TT>), dim3(ks), dim3(WPB), lds, st, d, JV, nrow);                     \
+  }
+      WPP_CASE(4, 256) WPP_CASE(4, 128) WPP_CASE(4, 64) WPP_CASE(5, 256) WPP_CASE(5, 128) WPP_CASE(5, 64)
+#undef WPP_CASE
     }
     RPC_LAUNCH_CHECK();
   }

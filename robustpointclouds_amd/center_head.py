@@ -286,24 +286,78 @@ def _prep_head(eng, head, dev, st):
 class _CatBN:
     """The BatchNorm2d modules of k ConvModules that share their input, side by side as one 64k-channel
     BatchNorm for one wide conv + BN + ReLU launch sequence (the attributes dense_bev._forward_layer /
-    _backward_layer read); write_back() returns the updated running statistics to the modules (one
-    multi-tensor copy)."""
+    _backward_layer read): views of a task's channels in the _HeadBufs buffers (the running statistics the
+    kernels update go back to the modules through _HeadBufs.write_back)."""
 
-    def __init__(self, bns):
+    def __init__(self, bns, bufs, sl):
         self.bns = bns
         self.eps, self.momentum = float(bns[0].eps), float(bns[0].momentum)
         if any(float(b.eps) != self.eps or float(b.momentum) != self.momentum for b in bns):
             raise NotImplementedError("CenterHead: the separate-head BatchNorms must share eps / momentum")
-        self.weight = torch.cat([b.weight.detach().float() for b in bns]).contiguous()
-        self.bias = torch.cat([b.bias.detach().float() for b in bns]).contiguous()
-        self.running_mean = torch.cat([b.running_mean for b in bns]).contiguous()
-        self.running_var = torch.cat([b.running_var for b in bns]).contiguous()
-        self.sizes = [b.running_mean.shape[0] for b in bns]
+        self.weight, self.bias = bufs.w[sl], bufs.b[sl]
+        self.running_mean, self.running_var = bufs.rm[sl], bufs.rv[sl]
+
+
+class _HeadBufs:
+    """Every task's separate-head BatchNorms (tasks x 5 ConvModules of 64 channels: weight, bias, running mean / var)
+    and final-conv biases in persistent flat buffers, filled by ONE multi-tensor copy per forward (was 5 cats per
+    task: 30 launches per CenterPoint step), with per-task _CatBN-like views; write_back() returns every task's
+    running statistics in one multi-tensor copy. Rebuilt when the modules or the device change."""
+
+    @staticmethod
+    def key_of(head, dev):
+        return (str(dev),) + tuple(id(getattr(th.task_head, name)) for th in head.task_heads for name in _BOX_ORDER)
+
+    def __init__(self, head, dev):
+        self.key = self.key_of(head, dev)
+        self.cms = [[getattr(th.task_head, name)[0] for name in _BOX_ORDER] for th in head.task_heads]
+        self.fcs = [[getattr(th.task_head, name)[1] for name in _BOX_ORDER] for th in head.task_heads]
+        self.bns = [cm.bn for cms in self.cms for cm in cms]
+        self.fbs = [f.bias for fcs in self.fcs for f in fcs]
+        nc = sum(b.num_features for b in self.bns)
+        self.w, self.b, self.rm, self.rv = (torch.empty(nc, dtype=torch.float32, device=dev) for _ in range(4))
+        self.fb = torch.empty(sum(f.numel() for f in self.fbs), dtype=torch.float32, device=dev)
+        sz = [b.num_features for b in self.bns]
+        fsz = [f.numel() for f in self.fbs]
+        self.dst = (list(self.w.split(sz)) + list(self.b.split(sz)) + list(self.rm.split(sz)) + list(self.rv.split(sz))
+                    + list(self.fb.split(fsz)))
+        self.views, self.fviews = [], []
+        c = f = 0
+        for t, cms in enumerate(self.cms):
+            n = sum(cm.bn.num_features for cm in cms)
+            nf = sum(x.bias.numel() for x in self.fcs[t])
+            self.views.append(_CatBN([cm.bn for cm in cms], self, slice(c, c + n)))
+            self.fviews.append(self.fb[f:f + nf])
+            c, f = c + n, f + nf
+
+    # not part of a copied or pickled module (the copy builds its own on its first forward)
+    def __deepcopy__(self, memo):
+        return None
+
+    def __reduce__(self):
+        return (_no_bufs, ())
+
+    def fill(self):
+        src = ([b.weight.detach() for b in self.bns] + [b.bias.detach() for b in self.bns] +
+               [b.running_mean for b in self.bns] + [b.running_var for b in self.bns] + [x.detach() for x in self.fbs])
+        torch._foreach_copy_(self.dst, src)
 
     def write_back(self):
-        dst = [b.running_mean for b in self.bns] + [b.running_var for b in self.bns]
-        src = list(self.running_mean.split(self.sizes)) + list(self.running_var.split(self.sizes))
-        torch._foreach_copy_(dst, src)
+        sz = [b.num_features for b in self.bns]
+        torch._foreach_copy_([b.running_mean for b in self.bns] + [b.running_var for b in self.bns],
+                             list(self.rm.split(sz)) + list(self.rv.split(sz)))
+
+
+def _no_bufs():
+    return None
+
+
+def _head_bufs(head, dev):
+    hb = head.__dict__.get("_head_bufs")
+    if hb is None or hb.key != _HeadBufs.key_of(head, dev):
+        hb = head.__dict__["_head_bufs"] = _HeadBufs(head, dev)
+    hb.fill()
+    return hb
 
 
 class _CatConv:
@@ -399,6 +453,7 @@ class CenterHeadFn(torch.autograd.Function):
         nof = prep[("offcat", "n")]
         cof = -(-nof // 64) * 64
         ozc, orec = _conv_nobn_fwd(eng, None, 64, y0, 64, B, H, W, dev, st, prep[("offcat",)], n=nof, co=cof)
+        hbufs = _head_bufs(head, dev)
         for t, th in enumerate(head.task_heads):
             tr = {}
             for br, dcn in (("cls", th.feature_adapt_cls), ("reg", th.feature_adapt_reg)):
@@ -435,13 +490,12 @@ class CenterHeadFn(torch.autograd.Function):
             # reg branches -> anno_box channels: the five ConvModules of the separate head share their input
             # (the DCN feature): one 64 -> 320 conv + BatchNorm + ReLU; the five final convs as one
             # block-diagonal 320 -> sum(n_i) conv whose outputs are the task's contiguous anno_box channels
-            cms = [getattr(th.task_head, name)[0] for name in _BOX_ORDER]
-            cbn = _CatBN([cm.bn for cm in cms])
+            cms = hbufs.cms[t]
+            cbn = hbufs.views[t]
             Lr = db._Layer(db.S1, _CatConv(prep[("regcat", id(th), "W")]), cbn, 0, 64, 64 * len(cms), 9)
             hr, rr, _, _ = db._forward_layer(eng, Lr, tr["reg"]["feat"], 64, B, H, W, training, dev, st,
                                              wts=prep[("regcat", id(th))])
             if training:
-                cbn.write_back()
                 for k, name in enumerate(_BOX_ORDER):
                     _debug(f"task_heads.{t}.task_head.{name}.0", rr, slice(64 * k, 64 * (k + 1)), B, H, W)
             bns.extend(cbn.bns)
@@ -449,13 +503,13 @@ class CenterHeadFn(torch.autograd.Function):
             nb = sum(f.weight.shape[0] for f in fcs)
             z, frec = _conv_nobn_fwd(eng, None, 64 * len(cms), hr, 64 * len(cms), B, H, W, dev, st,
                                      prep[("regbd", id(th))], n=nb)
-            bcat = torch.cat([f.bias.detach().float() for f in fcs])
-            _ffi.check(pack(_ffi.ptr(z), _PAD, nb, _ffi.ptr(bcat), _ffi.ptr(box), head.box_pitch, 10 * t, cells, st),
-                       "rpc_head_pack")
+            _ffi.check(pack(_ffi.ptr(z), _PAD, nb, _ffi.ptr(hbufs.fviews[t]), _ffi.ptr(box), head.box_pitch, 10 * t,
+                            cells, st), "rpc_head_pack")
             tr["reg_cm"] = (rr, cms)
             tr["regs"] = (frec, fcs, 10 * t, nb)
             trecs.append(tr)
         if training:
+            hbufs.write_back()
             _ffi.bump_batches(bns)
         ctx.head, ctx.rsh, ctx.trecs, ctx.orec = head, rsh, trecs, orec
         ctx.bd_idx = prep[("regbd", "idx")]

@@ -211,6 +211,7 @@ class OracleStep:
                                  coors=torch.from_numpy(rc)), batch_size=len(gts["boxes"]))
         self.losses = self.ref.loss(batch, gts)
         self.total, _ = parse_losses(self.losses)
+        print(f"  {self.enc.dtype} oracle forward done; backward ...", flush=True)
         self.total.backward()
         for h in hooks:
             h.remove()
@@ -308,7 +309,9 @@ def test_adversarial_centerpoint_step_fp32_hip_matches_oracle(B, sweeps):
 
     # ---- oracle steps
     flips, sflips = FlipStats(), FlipStats()
+    print(f"HIP step done ({rv.shape[0]} voxels); fp32 oracle step ...", flush=True)
     o32.step(rv, rn, rc, ogts, masks, dmasks)
+    print("fp32 oracle step done; float64 oracle step ...", flush=True)
     o64.step(rv, rn, rc, ogts, masks, dmasks, flips, sflips)
     print(f"dense ReLU decisions differing from float64's: {flips.flips} (max |pre| {flips.worst:.1e} of channel max)")
     print(f"sparse ReLU decisions differing from float64's: {sflips.flips} (max |act| {sflips.worst:.1e} of channel "

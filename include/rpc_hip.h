@@ -417,7 +417,9 @@ int rpc_dense_conv_s1_kernel(int map, int cout, const int* row_img);
  * loop); knob 4 = k_conv3x3x / k_conv3x3y loop variants and timing arms (128: x with operand reads a
  * quarter step ahead / y's former read-then-MFMA loop; bit-identical to the defaults); knob 5 = the
  * 64-channel-multiple k_conv3x3's output channels per block (0: 32 when the 64-channel grid is under one
- * round of two blocks per CU, default; 1: always 64; 2: always 32; bit-identical results) */
+ * round of two blocks per CU, default; 1: always 64; 2: always 32; bit-identical results); knob 8 = the
+ * 16x16-pixel kernel's split tail (1: the items past the last whole round of one block per CU run as two
+ * 64-channel blocks each when they fit one round, default; 0: off; bit-identical results) */
 int rpc_dense_tune(int knob, int value);
 /* dW (torch layout; kind 0 = Conv2d [co][ci][kh][kw], 1 = ConvTranspose2d [ci][co][kh][kw]) of the
  * forward map (S1/S2/P1/U2): sum over rows of x[src_row(row,t)][ci] * dz[row][co]; ci, co % 128 == 0 */

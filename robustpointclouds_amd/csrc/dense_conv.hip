@@ -367,6 +367,7 @@ struct C3 {
   // part then receives that layer's BatchNorm-backward partial sums (sum dm, sum dm * xhat), dm = dh * [pre > 0]
   const u16* bnz;
   const float* bnp;
+  int ysplit;      // k_conv3x3y: the last ysplit items run as two 64-channel blocks each (launch_s1)
 };
 
 // TNB = 32 (half the output channels per block, twice the blocks): the grids of less than one round of two
@@ -1286,17 +1287,28 @@ constexpr int YHBUF = 23 * 1024;               // halo buffer: 360 rows (22.5 KB
 constexpr int YHI = 6;                         // halo DMA instructions per wave (23 over 4 waves)
 constexpr int YLDS = 2 * YHBUF + WRING * XWTILE;   // 79872 B
 
-template <int DBG = 0>
-__global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
-  __shared__ __attribute__((aligned(1024))) unsigned char lds[YLDS];   // ONE LDS object (see k_conv3x3x)
+// the DMA waits of k_conv3x3y's steps: retire all but the youngest weight tile (WI instructions per wave), or at
+// taps HTAP, HTAP + 1 all but that tile and the next chunk's halo (YHI = 6 instructions)
+template <int WI>
+__device__ __forceinline__ void c3y_vm_tile() {
+  if constexpr (WI == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+}
+template <int WI>
+__device__ __forceinline__ void c3y_vm_halo() {
+  if constexpr (WI == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+}
+
+// CH = 64 (the split tail, C3::ysplit): the same block over half the output channels of its tile — 16 MFMAs per
+// step on a 64 x 32 weight tile (one DMA instruction per wave), the epilogue's stores / sums on its 64 channels
+template <int DBG, int CH>
+__device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, const int tile, const int n0) {
+  static_assert(CH == 128 || CH == 64, "k_conv3x3y: 128 or 64 output channels per block");
+  constexpr int NI = CH / 16, WI = CH / 64;   // accumulator fragments per wave; weight DMAs per wave and step
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int ncob = g.COUT >> 7;
-  const int ntiles = g.B * g.TY * g.TX;
-  const int item = xcd_remap(blockIdx.x, ntiles * ncob);           // tile-major: a tile's co-blocks adjacent
-  const int tile = item / ncob, cob = item - tile * ncob;
   const int b = tile / (g.TY * g.TX), trem = tile - b * g.TY * g.TX;
   const int ty0 = (trem / g.TX) * CT, tx0 = (trem % g.TX) * CT;
-  const int n0 = cob * 128;
   const int NKC = g.CIN / XBK, NS = 9 * NKC;
   unsigned char* const hbuf = lds;
   unsigned char* const wring = lds + 2 * YHBUF;
@@ -1317,10 +1329,10 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
                   : 0x80000000u;
   }
   // weights: instructions 2w, 2w + 1 write rows (2w + m)*16 + (lane >> 2) = output channel n0 + r
-  unsigned wofs[2];
+  unsigned wofs[WI];
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const int r = (2 * w + m) * 16 + (lane >> 2), j = lane & 3;
+  for (int m = 0; m < WI; ++m) {
+    const int r = (WI * w + m) * 16 + (lane >> 2), j = lane & 3;
     wofs[m] = (unsigned)(((n0 + r) * g.CIN + (j ^ xswz(r)) * 8) * 2);
   }
   auto issue_halo = [&](int kc, int hb) {
@@ -1335,9 +1347,9 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     s = min(s, NS - 1);
     const int kc = s / 9, t = s - kc * 9;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
+    for (int m = 0; m < WI; ++m)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(
-          rwt, (__attribute__((address_space(3))) void*)(wring + (s & (WRING - 1)) * XWTILE + (2 * w + m) * 1024), 16,
+          rwt, (__attribute__((address_space(3))) void*)(wring + (s & (WRING - 1)) * XWTILE + (WI * w + m) * 1024), 16,
           wofs[m], t * wtap + kc * XBK * 2, 0, 0);
   };
 
@@ -1348,9 +1360,9 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
 #pragma unroll
   for (int dx = 0; dx < 3; ++dx) hoff[dx] = (w * 4 * YHP + dx + a15) * XROW + ((q ^ xswz(dx + a15)) * 16);
 
-  f32x4 acc[8][4];
+  f32x4 acc[NI][4];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int i = 0; i < NI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4){0.f, 0.f, 0.f, 0.f};
 
@@ -1364,7 +1376,8 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
   if constexpr (PIPE) issue_w(WDIST);
   const bool live = ty0 + w * 4 < g.H;
   // halo 0 + tile 0 (+ tile 1 when pipelined: the youngest tile stays in flight)
-  asm volatile("s_waitcnt vmcnt(2)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  c3y_vm_tile<WI>();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
   // per step: issue the DMAs two steps ahead, read this step's 12 fragments, 32 MFMAs, retire the next
   // step's tile (vmcnt(2); vmcnt(8) at taps HTAP, HTAP + 1 whose younger DMAs include the halo), barrier
 #define C3Y_STEP(t, LIVE)                                                                                     \
@@ -1376,20 +1389,20 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       const unsigned char* hb_ = hbuf + (kc & 1) * YHBUF;                                                     \
       const unsigned char* wt_ = wring + (s_ & (WRING - 1)) * XWTILE;                                         \
       constexpr int dy_ = (t) / 3, dx_ = (t) % 3;                                                             \
-      bf16x8 av[8], bv[4];                                                                                    \
+      bf16x8 av[NI], bv[4];                                                                                    \
       _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                           \
         bv[j] = *(const bf16x8*)(hb_ + hoff[dx_] + (j + dy_) * YHP * XROW);                                   \
-      _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
+      _Pragma("unroll") for (int i = 0; i < NI; ++i)                                                          \
         av[i] = *(const bf16x8*)(wt_ + woff + i * 16 * XROW);                                                 \
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                                      \
       __builtin_amdgcn_s_setprio(1);                                                                          \
-      _Pragma("unroll") for (int i = 0; i < 8; ++i)                                                           \
+      _Pragma("unroll") for (int i = 0; i < NI; ++i)                                                          \
         _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                         \
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);              \
       __builtin_amdgcn_s_setprio(0);                                                                          \
     }                                                                                                         \
-    if ((t) == HTAP || (t) == HTAP + 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                      \
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                     \
+    if ((t) == HTAP || (t) == HTAP + 1) c3y_vm_halo<WI>();                                                        \
+    else c3y_vm_tile<WI>();                                                                                       \
     asm volatile("s_barrier" ::: "memory");                                                                   \
   }
   // pipelined form: the 32 MFMAs of a step run as four quarters of 2 weight fragments x 4 halo
@@ -1419,7 +1432,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
   __builtin_amdgcn_s_setprio(1);                                                                            \
   _Pragma("unroll") for (int i_ = 0; i_ < 2; ++i_)                                                          \
     _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                           \
-      acc[(qq) * 2 + i_][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA[i_], FB[j], acc[(qq) * 2 + i_][j], 0, 0, 0); \
+      acc[((qq) * 2 + i_) % NI][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA[i_], FB[j], acc[((qq) * 2 + i_) % NI][j], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);
 #define C3Y_PSTEP(i, FB, NB, LIVE)                                                                          \
   {                                                                                                         \
@@ -1427,7 +1440,15 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     const int kq_ = kc + (i) / 9, s_ = kq_ * 9 + t_;                                                        \
     issue_w(s_ + WDIST + 1);                                                                                \
     if (t_ == HTAP) issue_halo(min(kq_ + 1, NKC - 1), (kq_ + 1) & 1);                                       \
-    if (LIVE) {                                                                                             \
+    if (LIVE && CH == 64) {                                                                                 \
+      C3Y_PREAD_A(ay, s_, 1)                                                                                \
+      asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
+      C3Y_PMMA(ax, FB, 0)                                                                                   \
+      C3Y_PREAD_A(ax, s_ + 1, 0)                                                                            \
+      C3Y_PREAD_B(NB, (t_ + 1) % 9, kq_ + (t_ == 8))                                                        \
+      asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");                                                    \
+      C3Y_PMMA(ay, FB, 1)                                                                                   \
+    } else if (LIVE) {                                                                                      \
       C3Y_PREAD_A(ay, s_, 1)                                                                                \
       asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
       C3Y_PMMA(ax, FB, 0)                                                                                   \
@@ -1442,8 +1463,8 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");                                                    \
       C3Y_PMMA(ay, FB, 3)                                                                                   \
     }                                                                                                       \
-    if (t_ == HTAP || t_ == HTAP + 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");                      \
-    else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                                                   \
+    if (t_ == HTAP || t_ == HTAP + 1) c3y_vm_halo<WI>();                                                        \
+    else c3y_vm_tile<WI>();                                                                                     \
     asm volatile("s_barrier" ::: "memory");                                                                 \
   }
 #define C3Y_PKC(LIVE)                                                                                       \
@@ -1504,7 +1525,8 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     // fused BatchNorm-backward sums: the 16 pre-activation loads of this thread's store column are issued
     // before the accumulator tile is staged, so their latency lies under the staging and its barrier
     uint4 zpre[CT];
-    if (g.bnz != nullptr) {
+    const bool cact = CH == 128 || (tid & 15) < CH / 8;   // this thread's 16-byte chunk is one of the block's
+    if (g.bnz != nullptr && cact) {
       const int zc_ = tid & 15, zx_ = min(tx0 + (tid >> 4), g.W - 1);
 #pragma unroll
       for (int k = 0; k < CT; ++k)
@@ -1517,7 +1539,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       for (int j = 0; j < 4; ++j) {
         const int p = (w * 4 + j) * CT + a15;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
+        for (int i = 0; i < NI; ++i) {
           const int gr = (i * 2 + (q >> 1)) ^ (p & 15);
           const unsigned lo = (unsigned)f2bf(acc[i][j][0]) | ((unsigned)f2bf(acc[i][j][1]) << 16);
           const unsigned hi = (unsigned)f2bf(acc[i][j][2]) | ((unsigned)f2bf(acc[i][j][3]) << 16);
@@ -1530,7 +1552,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     float t1[8], t2[8], bsc[8], bbe[8], bmu[8], bis[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) t1[e] = t2[e] = 0.f;
-    if (g.bnz != nullptr) {
+    if (g.bnz != nullptr && cact) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int ch = n0 + c * 8 + e;
@@ -1541,7 +1563,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       }
     }
     const int x = tx0 + px;
-    if (g.bnz != nullptr) {
+    if (g.bnz != nullptr && cact) {
       // BatchNorm-backward sums of the layer this gradient enters: all 16 pre-activation loads issued
       // before the first is used (clamped addresses; a load per pixel waited out one round trip each)
 #pragma unroll
@@ -1564,7 +1586,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       }
     }
 #pragma unroll 4
-    for (int k = 0; k < (g.bnz != nullptr ? 0 : CT); ++k) {
+    for (int k = 0; k < (g.bnz != nullptr || !cact ? 0 : CT); ++k) {
       const int y = ty0 + k, p = k * CT + px;
       if (y >= g.H || x >= g.W) continue;
       const size_t pix = (size_t)(b * g.H + y) * g.W + x;
@@ -1601,7 +1623,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
       const int k2 = tid >> 7, ch = tid & 127;
       const float s = ((sR[(0 * 2 + k2) * 128 + ch] + sR[(1 * 2 + k2) * 128 + ch]) + sR[(2 * 2 + k2) * 128 + ch]) +
                       sR[(3 * 2 + k2) * 128 + ch];
-      g.part[(size_t)tile * 2 * g.COUT + k2 * g.COUT + n0 + ch] = s;
+      if (ch < CH) g.part[(size_t)tile * 2 * g.COUT + k2 * g.COUT + n0 + ch] = s;
     }
     return;
   }
@@ -1609,7 +1631,7 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
   // of 64 channels (BatchNorm sums of half the accumulator tiles live at a time)
   float* sP = (float*)lds;   // [4 waves][2][128]
 #pragma unroll
-  for (int ih = 0; ih < 2; ++ih) {
+  for (int ih = 0; ih < CH / 64; ++ih) {
     float s1[4][4], s2[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1669,7 +1691,26 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
     const int k2 = tid >> 7, ch = tid & 127;
     const float s = ((sP[(0 * 2 + k2) * 128 + ch] + sP[(1 * 2 + k2) * 128 + ch]) + sP[(2 * 2 + k2) * 128 + ch]) +
                     sP[(3 * 2 + k2) * 128 + ch];
-    g.part[(size_t)tile * 2 * g.COUT + k2 * g.COUT + n0 + ch] = s;
+    if (ch < CH) g.part[(size_t)tile * 2 * g.COUT + k2 * g.COUT + n0 + ch] = s;
+  }
+}
+
+
+// the grid: the first nitems - ysplit items (tile-major, a tile's co-blocks adjacent, XCD-aware) one 128-channel
+// block each, then the last ysplit items as two 64-channel blocks each (dispatched last: the tail of the launch)
+template <int DBG = 0>
+__global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
+  __shared__ __attribute__((aligned(1024))) unsigned char lds[YLDS];   // ONE LDS object (see k_conv3x3x)
+  const int ncob = g.COUT >> 7;
+  const int nfull = g.B * g.TY * g.TX * ncob - g.ysplit;
+  if ((int)blockIdx.x < nfull) {
+    const int item = xcd_remap(blockIdx.x, nfull);
+    const int tile = item / ncob;
+    conv3x3y_body<DBG, 128>(g, lds, tile, (item - tile * ncob) * 128);
+  } else if constexpr (DBG == 0) {
+    const int t = (int)blockIdx.x - nfull, item = nfull + (t >> 1);
+    const int tile = item / ncob;
+    conv3x3y_body<0, 64>(g, lds, tile, (item - tile * ncob) * 128 + (t & 1) * 64);
   }
 }
 
@@ -2643,6 +2684,7 @@ static int g_s1_variant = env_int("RPC_DENSE_S1", 0);   // A/B: RPC_DENSE_S1=<kn
 // (tools/s1wg_bench.py, profiles/r06_s1wg_ab.txt)
 static int g_wgrad_variant = env_int("RPC_DENSE_WGRAD", 0);
 static int g_s1x_dbg = 0;          // knob 4: k_conv3x3x timing experiments (0 = the real kernel)
+static int g_y_split = env_int("RPC_DENSE_YSPLIT", 1);   // knob 8: k_conv3x3y split tail (C3::ysplit), 0 = off
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
 // 128-multiple outputs, by shape: k_conv3x3y (two 4-wave 16x16 blocks per CU) when its grid is more than
@@ -2750,6 +2792,11 @@ extern "C" int rpc_dense_tune(int knob, int value) {
     if (value >= 0) g_s1c_seg = value;
     return old;
   }
+  if (knob == 8) {
+    const int old = g_y_split;
+    if (value == 0 || value == 1) g_y_split = value;
+    return old;
+  }
   if (knob == 2) {
     const int old = g_ig_order;
     if (value >= 0) g_ig_order = value;
@@ -2763,11 +2810,15 @@ extern "C" int rpc_dense_tune(int knob, int value) {
 static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t st) {
   const int TY = (g.R.H + CT - 1) / CT, TX = (g.R.W + CT - 1) / CT;
   C3 c{g.src, g.SP, g.CIN, g.wt, g.COUT, g.out, g.OP, g.OOFF, g.accum, g.part, g.R.B, g.R.H, g.R.W, TY, TX,
-       bnz, bnp};
+       bnz, bnp, 0};
   const bool fits32 = (long long)g.M * g.SP * 2 < (1LL << 31) && 9LL * g.COUT * g.CIN * 2 < (1LL << 31);
   const int rimg[3] = {g.R.B, g.R.H, g.R.W};
   if (s1_ytwo(rimg, g.COUT) && fits32) {
-    const dim3 grid(g.R.B * TY * TX * (g.COUT / 128));
+    // the items past the last whole round of one block per CU (k_conv3x3y's time is a staircase in
+    // ceil(items / CUs), profiles/r06_conv3x3y_tiles.txt) run as 64-channel halves when those fit one round
+    const int items = g.R.B * TY * TX * (g.COUT / 128), tail = items % cu_count();
+    c.ysplit = (g_y_split && g_s1x_dbg == 0 && items > cu_count() && 2 * tail <= cu_count()) ? tail : 0;
+    const dim3 grid(items + c.ysplit);
     switch (g_s1x_dbg) {
       case 1: hipLaunchKernelGGL(k_conv3x3y<1>, grid, dim3(YB), 0, st, c); break;
       case 17: hipLaunchKernelGGL(k_conv3x3y<17>, grid, dim3(YB), 0, st, c); break;

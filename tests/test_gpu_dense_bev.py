@@ -462,6 +462,50 @@ def test_s1_wide_tile_kernel(ci, co, B, H, W, variant):
     assert torch.all((sp - want).abs() <= 1e-5 * scale + 1e-6)
 
 
+@pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 6, 200, 176), (256, 128, 6, 200, 176), (128, 128, 2, 200, 176),
+                                         (128, 256, 3, 200, 176), (128, 128, 4, 128, 144)])
+def test_s1_y_split_tail_bitexact(ci, co, B, H, W):
+    """k_conv3x3y's split tail (rpc_dense_tune knob 8): the items past the last whole round of one block per CU run
+    as two 64-channel blocks each — the same MFMAs in the same order per output channel, so the output, the
+    accumulate path, the BatchNorm partial rows and the fused BatchNorm-backward partials are bit-identical to the
+    unsplit launch. Shapes: the metric's 858-tile layers (tail 90 on 256 CUs), 286 tiles (tail 30), 1716 items
+    (tail 180: more than half a round, not split), 288 whole tiles (tail 32)."""
+    lib = _ffi.load()
+    img = (B, H, W)
+    ri = _ffi.int_arr(img)
+    x = _nhwc(_rand(B, ci, H, W, seed=51))
+    wf, _ = _wprep(_rand(co, ci, 3, 3, seed=52, scale=0.05), 0, 9, 1)
+    base = _nhwc(_rand(B, co, H, W, seed=53)).reshape(-1, co)
+    M = B * H * W
+    z = _nhwc(_rand(B, co, H, W, seed=54)).reshape(M, co)
+    g = torch.Generator().manual_seed(55)
+    bn = torch.cat([torch.rand(co, generator=g) + 0.5, torch.randn(co, generator=g) * 0.2,
+                    torch.randn(co, generator=g) * 0.1, torch.rand(co, generator=g) + 0.5]).float().to(DEV)
+    outs = {}
+    old0 = lib.rpc_dense_tune(0, 4)
+    try:
+        for v in (0, 1):
+            old8 = lib.rpc_dense_tune(8, v)
+            try:
+                rows = lib.rpc_dense_conv_part_rows(S1, co, ri)
+                y, part = _conv(S1, x, ci, wf, co, img, img, img, stats=True)
+                acc = base.clone()
+                _conv(S1, x, ci, wf, co, img, img, img, out=acc, accum=True)
+                pb = torch.zeros((rows, 2 * co), device=DEV)
+                dh = torch.empty((M, co), dtype=torch.bfloat16, device=DEV)
+                _ffi.check(lib.rpc_dense_conv_bnbwd(_ffi.ptr(x), ci, ci, _ffi.ptr(wf), co, _ffi.ptr(dh), co,
+                                                    _ffi.ptr(z), _ffi.ptr(bn), _ffi.ptr(pb), ri,
+                                                    _ffi.stream_of(dh)), "rpc_dense_conv_bnbwd")
+                torch.cuda.synchronize()
+            finally:
+                lib.rpc_dense_tune(8, old8)
+            outs[v] = (y, part, acc, dh, pb)
+    finally:
+        lib.rpc_dense_tune(0, old0)
+    for a, b in zip(outs[0], outs[1]):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("ci,co,B,H,W", [(128, 128, 6, 200, 176), (256, 128, 6, 200, 176), (256, 256, 6, 100, 88),
                                          (128, 128, 2, 24, 40), (128, 256, 1, 9, 130)])
 def test_s1_dgrad_with_fused_bn_backward_sums(ci, co, B, H, W):

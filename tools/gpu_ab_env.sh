@@ -1,11 +1,11 @@
 #!/bin/bash
-# short same-box bench A/B over environment settings: tools/gpu_ab_env.sh TAG "ENV1" "ENV2" ...  (ENV "-" = defaults)
+# short same-box bench A/B over environment settings: [REPS=n] tools/gpu_ab_env.sh TAG "ENV1" "ENV2" ...  (ENV "-" = defaults)
 set -o pipefail
 OUT=gpurun_out/$1; shift
 mkdir -p $OUT
 export TMPDIR=/tmp
 i=0
-for rep in 1 2; do
+for rep in $(seq 1 ${REPS:-2}); do
   for e in "$@"; do
     i=$((i+1))
     envs=""; [ "$e" != "-" ] && envs="$e"

@@ -2400,7 +2400,16 @@ __device__ __forceinline__ void st8(float* p, const float* v) {
 }
 
 // h = relu((z - mean) * scale + beta) -> image rows at (OP, OOFF); bn = scale, beta, mean, invstd
-template <typename E>
+// row mapping of the elementwise passes (knob 9): V = 0 grid-stride batches of RU rows (a thread's rows
+// gridDim * RL apart); V = 1 / 2: each block one contiguous chunk of RL * 4 / RL * 8 rows, all in flight at once
+template <int V>
+__device__ __forceinline__ int ew_row(int m0, int u, int step, int RL) {
+  return V == 0 ? m0 + u * step : m0 + u * RL;
+}
+template <int V>
+constexpr int ew_ru() { return V == 2 ? 8 : RU; }
+
+template <typename E, int V = 0>
 __global__ __launch_bounds__(BLK) void k_bn_apply(const E* __restrict__ z, int M, int C, const float* __restrict__ bn,
                                                   E* __restrict__ out, int OP, int OOFF) {
   const int CG = C >> 3, RL = BLK / CG;
@@ -2414,17 +2423,18 @@ __global__ __launch_bounds__(BLK) void k_bn_apply(const E* __restrict__ z, int M
     sh[j] = bn[C + c];
     mu[j] = bn[2 * C + c];
   }
+  constexpr int R = ew_ru<V>();
   const int step = gridDim.x * RL;
-  for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
-    Raw8<E> v[RU];
+  for (int m0 = V == 0 ? blockIdx.x * RL + rl : blockIdx.x * RL * R + rl; m0 < M; m0 += V == 0 ? R * step : R * step) {
+    Raw8<E> v[R];
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int m = m0 + u * step;
+    for (int u = 0; u < R; ++u) {
+      const int m = ew_row<V>(m0, u, step, RL);
       if (m < M) v[u] = ld8(z + (size_t)m * C + cg * 8);
     }
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int m = m0 + u * step;
+    for (int u = 0; u < R; ++u) {
+      const int m = ew_row<V>(m0, u, step, RL);
       if (m >= M) continue;
       float o[8];
 #pragma unroll
@@ -2502,7 +2512,7 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_stats(const E* __restrict__ dh, i
 }
 
 // dz = gi * (dm - m1 - xhat * m2) -> [M][C]; bnb = gi, m1, m2, mean, invstd; bn = forward
-template <typename E>
+template <typename E, int V = 0>
 __global__ __launch_bounds__(BLK) void k_bnbwd_apply(const E* __restrict__ dh, int DP, int DOFF,
                                                      const E* __restrict__ z, int M, int C,
                                                      const float* __restrict__ bn, const float* __restrict__ bnb,
@@ -2523,20 +2533,21 @@ __global__ __launch_bounds__(BLK) void k_bnbwd_apply(const E* __restrict__ dh, i
     mb[j] = bnb[3 * C + c];
     ib[j] = bnb[4 * C + c];
   }
+  constexpr int R = ew_ru<V>();
   const int step = gridDim.x * RL;
-  for (int m0 = blockIdx.x * RL + rl; m0 < M; m0 += RU * step) {
-    Raw8<E> dv[RU], zv[RU];
+  for (int m0 = V == 0 ? blockIdx.x * RL + rl : blockIdx.x * RL * R + rl; m0 < M; m0 += R * step) {
+    Raw8<E> dv[R], zv[R];
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int m = m0 + u * step;
+    for (int u = 0; u < R; ++u) {
+      const int m = ew_row<V>(m0, u, step, RL);
       if (m < M) {
         dv[u] = ld8(dh + (size_t)m * DP + DOFF + cg * 8);
         zv[u] = ld8(z + (size_t)m * C + cg * 8);
       }
     }
 #pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int m = m0 + u * step;
+    for (int u = 0; u < R; ++u) {
+      const int m = ew_row<V>(m0, u, step, RL);
       if (m >= M) continue;
       float o[8];
 #pragma unroll
@@ -2662,6 +2673,12 @@ using namespace rpc::dn;
 static inline Img img3(const int* d) { return Img{d[0], d[1], d[2]}; }
 
 // elementwise BatchNorm passes: blocks of (256 / (C/8)) row lanes, ~2*RU rows per thread
+// one contiguous chunk of RL * R rows per block (V = 1, 2)
+static unsigned ew_chunks(long long m, int c, int R) {
+  const long long rl = BLK / (c / 8 > 0 ? c / 8 : 1);
+  const long long b = (m + rl * R - 1) / (rl * R);
+  return (unsigned)(b < 1 ? 1 : (b > 2147483647LL ? 2147483647LL : b));
+}
 static unsigned ew_blocks(long long m, int c) {
   const long long rl = BLK / (c / 8 > 0 ? c / 8 : 1);
   long long b = (m + rl * 2 * RU - 1) / (rl * 2 * RU);
@@ -2677,6 +2694,11 @@ static int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return v && *v ? atoi(v) : dflt;
 }
+// knob 9 / RPC_DENSE_EW: the row mapping of the BatchNorm elementwise passes — 0: each block one contiguous chunk
+// of rows, all in flight at once (k_bn_apply 4 rows per thread, V = 1; k_bnbwd_apply 8, V = 2; default), 1: the
+// former grid-stride batches (V = 0). Same bits either way (tools/ew_bench.py, profiles/r06_ew_rows_ab.txt:
+// 200x176x6 x 128 bn_apply 17.9 -> 16.8 us, bnbwd_apply 27.2 -> 25.8 us)
+static int g_ew_var = env_int("RPC_DENSE_EW", 0);
 static int g_s1_variant = env_int("RPC_DENSE_S1", 0);   // A/B: RPC_DENSE_S1=<knob 0 value> for a whole run
 // S1 weight gradient (knob 1 / RPC_DENSE_WGRAD): 0 = by shape (k_wgrad_s1c where ci % 64 == 0 and co % 128 == 0,
 // else k_wgrad_s1 for 128-multiples, else k_wgrad), 1 = k_wgrad, 2 = k_wgrad_s1 without its read pipeline,
@@ -2795,6 +2817,11 @@ extern "C" int rpc_dense_tune(int knob, int value) {
   if (knob == 8) {
     const int old = g_y_split;
     if (value == 0 || value == 1) g_y_split = value;
+    return old;
+  }
+  if (knob == 9) {
+    const int old = g_ew_var;
+    if (value == 0 || value == 1) g_ew_var = value;
     return old;
   }
   if (knob == 2) {
@@ -3007,8 +3034,13 @@ template <typename E>
 static int bn_apply(const void* z, int m, int c, const float* bn, void* out, int op, int ooff, void* stream) {
   if (m < 0 || c < 8 || c > 2048 || (c & 7) || (op & 7) || (ooff & 7) || op < ooff + c) return RPC_ERR_ARG;
   if (m == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_bn_apply<E>, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
-                     (const E*)z, m, c, bn, (E*)out, op, ooff);
+  const hipStream_t st = (hipStream_t)stream;
+  if (g_ew_var == 1)
+    hipLaunchKernelGGL((k_bn_apply<E, 0>), dim3(ew_blocks(m, c)), dim3(BLK), 0, st, (const E*)z, m, c, bn, (E*)out,
+                       op, ooff);
+  else
+    hipLaunchKernelGGL((k_bn_apply<E, 1>), dim3(ew_chunks(m, c, RU)), dim3(BLK), 0, st, (const E*)z, m, c, bn, (E*)out,
+                       op, ooff);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }
@@ -3029,8 +3061,13 @@ static int bnbwd_apply(const void* dh, int dp, int doff, const void* z, int m, i
                        const float* bnb, void* dz, void* stream) {
   if (m < 0 || c < 8 || c > 2048 || (c & 7) || (dp & 7) || (doff & 7)) return RPC_ERR_ARG;
   if (m == 0) return RPC_OK;
-  hipLaunchKernelGGL(k_bnbwd_apply<E>, dim3(ew_blocks(m, c)), dim3(BLK), 0, (hipStream_t)stream,
-                     (const E*)dh, dp, doff, (const E*)z, m, c, bn, bnb, (E*)dz);
+  const hipStream_t st = (hipStream_t)stream;
+  if (g_ew_var == 1)
+    hipLaunchKernelGGL((k_bnbwd_apply<E, 0>), dim3(ew_blocks(m, c)), dim3(BLK), 0, st, (const E*)dh, dp, doff,
+                       (const E*)z, m, c, bn, bnb, (E*)dz);
+  else
+    hipLaunchKernelGGL((k_bnbwd_apply<E, 2>), dim3(ew_chunks(m, c, 8)), dim3(BLK), 0, st, (const E*)dh, dp, doff,
+                       (const E*)z, m, c, bn, bnb, (E*)dz);
   RPC_LAUNCH_CHECK();
   return RPC_OK;
 }

@@ -13,7 +13,7 @@ from robustpointclouds_amd import _ffi  # noqa: E402
 SHAPES = [(6, 200, 176, 128, 128), (6, 200, 176, 256, 128), (6, 200, 176, 128, 256), (6, 100, 88, 256, 256)]
 
 
-def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None, knob=0):
+def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None, knob=0, bnbwd=False):
     lib = _ffi.load()
     dev = torch.device("cuda")
     st = torch.cuda.current_stream()
@@ -25,20 +25,29 @@ def main(rounds=5, iters=10, variants=(0, 1, 2), shapes=None, knob=0):
         img = _ffi.int_arr((B, H, W))
         nblk = lib.rpc_dense_conv_blocks(0, img)
         part = torch.empty(nblk, 2 * co, device=dev)
+        zb = torch.randn(B * H * W, co, device=dev).to(torch.bfloat16)
+        bnp = torch.cat([torch.rand(co) + 0.5, torch.randn(co) * 0.2, torch.randn(co) * 0.1,
+                         torch.rand(co) + 0.5]).to(dev)
+
+        def launch():
+            if bnbwd:   # the data gradient with the fused BatchNorm-backward sums of the layer it enters
+                _ffi.check(lib.rpc_dense_conv_bnbwd(_ffi.ptr(x), ci, ci, _ffi.ptr(wt), co, _ffi.ptr(z), co, _ffi.ptr(zb),
+                                                    _ffi.ptr(bnp), _ffi.ptr(part), img, _ffi.stream_of(z)), "bnbwd")
+            else:
+                lib.rpc_dense_conv(0, _ffi.ptr(x), ci, ci, _ffi.ptr(wt), co, _ffi.ptr(z), co, 0, 0, _ffi.ptr(part),
+                                   img, img, img, _ffi.stream_of(z))
         flops = 2.0 * B * H * W * ci * co * 9
         times = {v: [] for v in variants}
         for r in range(rounds):
             for v in variants:
                 lib.rpc_dense_tune(knob, v)
                 for _ in range(2):
-                    lib.rpc_dense_conv(0, _ffi.ptr(x), ci, ci, _ffi.ptr(wt), co, _ffi.ptr(z), co, 0, 0, _ffi.ptr(part),
-                                       img, img, img, _ffi.stream_of(z))
+                    launch()
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 e0.record(st)
                 for _ in range(iters):
-                    lib.rpc_dense_conv(0, _ffi.ptr(x), ci, ci, _ffi.ptr(wt), co, _ffi.ptr(z), co, 0, 0, _ffi.ptr(part),
-                                       img, img, img, _ffi.stream_of(z))
+                    launch()
                 e1.record(st)
                 e1.synchronize()
                 times[v].append(e0.elapsed_time(e1) * 1e3 / iters)
@@ -61,6 +70,7 @@ if __name__ == "__main__":
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--knob", type=int, default=0, help="rpc_dense_tune knob the variants set (0 or 5)")
     ap.add_argument("--shapes", default="", help="B,H,W,ci,co;... (default: the SECOND config shapes)")
+    ap.add_argument("--bnbwd", action="store_true", help="time rpc_dense_conv_bnbwd (fused BN-backward sums)")
     a = ap.parse_args()
     shapes = [tuple(int(x) for x in sh.split(",")) for sh in a.shapes.split(";") if sh] or None
-    main(a.rounds, a.iters, tuple(int(v) for v in a.variants.split(",")), shapes, a.knob)
+    main(a.rounds, a.iters, tuple(int(v) for v in a.variants.split(",")), shapes, a.knob, a.bnbwd)

@@ -421,7 +421,9 @@ int rpc_dense_conv_s1_kernel(int map, int cout, const int* row_img);
  * 16x16-pixel kernel's split tail (1: the items past the last whole round of one block per CU run as two
  * 64-channel blocks each when they fit one round, default; 0: off; bit-identical results); knob 9 = the row
  * mapping of rpc_dense_bn_apply / rpc_dense_bnbwd_apply (0: one contiguous chunk of rows per block, default;
- * 1: grid-stride batches; bit-identical results) */
+ * 1: grid-stride batches; bit-identical results); knob 10 = the 16x16-pixel kernel's pre-activation prefetch for
+ * rpc_dense_conv_bnbwd (1: the epilogue's first rows loaded during the last K-chunk, default; 0: all in the
+ * epilogue; bit-identical results) */
 int rpc_dense_tune(int knob, int value);
 /* dW (torch layout; kind 0 = Conv2d [co][ci][kh][kw], 1 = ConvTranspose2d [ci][co][kh][kw]) of the
  * forward map (S1/S2/P1/U2): sum over rows of x[src_row(row,t)][ci] * dz[row][co]; ci, co % 128 == 0 */

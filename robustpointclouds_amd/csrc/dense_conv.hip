@@ -1302,7 +1302,10 @@ __device__ __forceinline__ void c3y_vm_halo() {
 
 // CH = 64 (the split tail, C3::ysplit): the same block over half the output channels of its tile — 16 MFMAs per
 // step on a 64 x 32 weight tile (one DMA instruction per wave), the epilogue's stores / sums on its 64 channels
-template <int DBG, int CH>
+// ZPF (data gradients with fused BatchNorm-backward sums): the epilogue's first ZPN pre-activation rows are loaded during
+// the last K-chunk — issued after its last real weight tile (step 5); the later steps issue no weight DMAs (in every
+// launch: they were clamped repeats), so the loads stay in flight through steps 6-8 and the accumulator staging
+template <int DBG, int CH, bool ZPF = false>
 __device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, const int tile, const int n0) {
   static_assert(CH == 128 || CH == 64, "k_conv3x3y: 128 or 64 output channels per block");
   constexpr int NI = CH / 16, WI = CH / 64;   // accumulator fragments per wave; weight DMAs per wave and step
@@ -1369,6 +1372,15 @@ __device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, c
   // operand fragments read a quarter step ahead (C3Y_PSTEP); DBG bit 128 (and the timing arms 1 / 16):
   // the former loop, which reads a step's 12 fragments, waits for all of them, then runs its 32 MFMAs
   // (200x176 128->128 72.6 -> 66.9 us, 128->256 113.9 -> 109.8 us, profiles/r03_conv_pipe.log)
+  // ZPF: the epilogue's first ZPN pre-activation rows of this thread's 16-byte column chunk (see C3Y_PKCZ)
+  constexpr int ZPN = 4, ZQ = ZPF ? ZPN : 0;   // ZQ: the prefetch loads outstanding after the last weight tile
+  uint4 zpa[ZPF ? ZPN : 1];
+  const int zpx_ = min(tx0 + (tid >> 4), g.W - 1), zpch_ = min(n0 + (tid & 15) * 8, g.COUT - 8);
+#define C3Y_ZISSUE                                                                                          \
+  {                                                                                                         \
+    _Pragma("unroll") for (int k_ = 0; k_ < ZPN; ++k_) zpa[k_] =                                            \
+        *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k_, g.H - 1)) * g.W + zpx_) * g.COUT + zpch_); \
+  }
   constexpr bool PIPE = (DBG & (128 | 16 | 1)) == 0;
   issue_halo(0, 0);
 #pragma unroll
@@ -1434,12 +1446,13 @@ __device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, c
     _Pragma("unroll") for (int j = 0; j < 4; ++j)                                                           \
       acc[((qq) * 2 + i_) % NI][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(FA[i_], FB[j], acc[((qq) * 2 + i_) % NI][j], 0, 0, 0); \
   __builtin_amdgcn_s_setprio(0);
-#define C3Y_PSTEP(i, FB, NB, LIVE)                                                                          \
+#define C3Y_PSTEP(i, FB, NB, LIVE, MODE)                                                                    \
   {                                                                                                         \
     constexpr int t_ = (i) % 9;                                                                             \
     const int kq_ = kc + (i) / 9, s_ = kq_ * 9 + t_;                                                        \
-    issue_w(s_ + WDIST + 1);                                                                                \
+    if constexpr ((MODE) != 2) issue_w(s_ + WDIST + 1);                                                     \
     if (t_ == HTAP) issue_halo(min(kq_ + 1, NKC - 1), (kq_ + 1) & 1);                                       \
+    if constexpr ((MODE) == 1) C3Y_ZISSUE                                                                   \
     if (LIVE && CH == 64) {                                                                                 \
       C3Y_PREAD_A(ay, s_, 1)                                                                                \
       asm volatile("s_waitcnt lgkmcnt(2)" ::: "memory");                                                    \
@@ -1463,26 +1476,43 @@ __device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, c
       asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");                                                    \
       C3Y_PMMA(ay, FB, 3)                                                                                   \
     }                                                                                                       \
-    if (t_ == HTAP || t_ == HTAP + 1) c3y_vm_halo<WI>();                                                        \
-    else c3y_vm_tile<WI>();                                                                                     \
+    if constexpr ((MODE) == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(WI + ZPN) : "memory");           \
+    else if constexpr ((MODE) == 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(ZQ) : "memory");             \
+    else if (t_ == HTAP || t_ == HTAP + 1) c3y_vm_halo<WI>();                                              \
+    else c3y_vm_tile<WI>();                                                                                 \
     asm volatile("s_barrier" ::: "memory");                                                                 \
   }
 #define C3Y_PKC(LIVE)                                                                                       \
-  C3Y_PSTEP(0, fb0, fb1, LIVE) C3Y_PSTEP(1, fb1, fb0, LIVE) C3Y_PSTEP(2, fb0, fb1, LIVE)                    \
-  C3Y_PSTEP(3, fb1, fb0, LIVE) C3Y_PSTEP(4, fb0, fb1, LIVE) C3Y_PSTEP(5, fb1, fb0, LIVE)                    \
-  C3Y_PSTEP(6, fb0, fb1, LIVE) C3Y_PSTEP(7, fb1, fb0, LIVE) C3Y_PSTEP(8, fb0, fb1, LIVE)
+  C3Y_PSTEP(0, fb0, fb1, LIVE, 0) C3Y_PSTEP(1, fb1, fb0, LIVE, 0) C3Y_PSTEP(2, fb0, fb1, LIVE, 0)           \
+  C3Y_PSTEP(3, fb1, fb0, LIVE, 0) C3Y_PSTEP(4, fb0, fb1, LIVE, 0) C3Y_PSTEP(5, fb1, fb0, LIVE, 0)           \
+  C3Y_PSTEP(6, fb0, fb1, LIVE, 0) C3Y_PSTEP(7, fb1, fb0, LIVE, 0) C3Y_PSTEP(8, fb0, fb1, LIVE, 0)
+// the last K-chunk: steps 6-8 issue no weight DMA (they were repeats of the last tile, clamped) and wait for
+// vmcnt ZQ; ZPF: step 5 issues the last real weight tile and then the ZPN pre-activation loads (vmcnt WI + ZPN
+// retires only the older tile), which stay in flight through steps 6-8 and the staging
+#define C3Y_PKCZ(LIVE)                                                                                      \
+  C3Y_PSTEP(0, fb0, fb1, LIVE, 0) C3Y_PSTEP(1, fb1, fb0, LIVE, 0) C3Y_PSTEP(2, fb0, fb1, LIVE, 0)           \
+  C3Y_PSTEP(3, fb1, fb0, LIVE, 0) C3Y_PSTEP(4, fb0, fb1, LIVE, 0) C3Y_PSTEP(5, fb1, fb0, LIVE, ZPF ? 1 : 0)  \
+  C3Y_PSTEP(6, fb0, fb1, LIVE, 2) C3Y_PSTEP(7, fb1, fb0, LIVE, 2) C3Y_PSTEP(8, fb0, fb1, LIVE, 2)
   if constexpr (PIPE) {
     bf16x8 ax[2], ay[2], fb0[4], fb1[4];
     if (live) {
       C3Y_PREAD_A(ax, 0, 0)
       C3Y_PREAD_B(fb0, 0, 0)
-      for (int kc = 0; kc < NKC; ++kc) {   // 9 steps (odd): the next chunk's halo fragments move back to fb0
+      for (int kc = 0; kc < NKC - 1; ++kc) {   // 9 steps (odd): the next chunk's halo fragments move back to fb0
         C3Y_PKC(true)
 #pragma unroll
         for (int j = 0; j < 4; ++j) fb0[j] = fb1[j];
       }
+      {
+        const int kc = NKC - 1;
+        C3Y_PKCZ(true)
+      }
     } else {
-      for (int kc = 0; kc < NKC; ++kc) { C3Y_PKC(false) }
+      for (int kc = 0; kc < NKC - 1; ++kc) { C3Y_PKC(false) }
+      {
+        const int kc = NKC - 1;
+        C3Y_PKCZ(false)
+      }
     }
   } else if (DBG & 16) {
   } else if (live) {
@@ -1512,11 +1542,16 @@ __device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, c
   }
 #undef C3Y_STEP
 #undef C3Y_PKC
+#undef C3Y_PKCZ
+#undef C3Y_ZISSUE
 #undef C3Y_PSTEP
 #undef C3Y_PMMA
 #undef C3Y_PREAD_A
 #undef C3Y_PREAD_B
-  asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if constexpr (PIPE)   // every weight / halo DMA retired by the last steps' waits; ZPF: the pre-activation loads stay
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::"n"(ZQ) : "memory");
+  else
+    asm volatile("s_waitcnt vmcnt(0)\n\ts_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 
   // ---- epilogue: lane holds co = n0 + i*16 + 4q + r of pixel (4w + j, a15)
   if (!g.accum) {
@@ -1529,9 +1564,12 @@ __device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, c
     if (g.bnz != nullptr && cact) {
       const int zc_ = tid & 15, zx_ = min(tx0 + (tid >> 4), g.W - 1);
 #pragma unroll
-      for (int k = 0; k < CT; ++k)
-        zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + zx_) * g.COUT + n0 +
-                                  zc_ * 8);
+      for (int k = 0; k < CT; ++k) {
+        if (ZPF && PIPE && k < ZPN) zpre[k] = zpa[k % (ZPF ? ZPN : 1)];
+        else
+          zpre[k] = *(const uint4*)(g.bnz + ((size_t)(b * g.H + min(ty0 + k, g.H - 1)) * g.W + zx_) * g.COUT + n0 +
+                                    zc_ * 8);
+      }
     }
     unsigned char* tileb = lds;
     if (live) {
@@ -1698,7 +1736,7 @@ __device__ __forceinline__ void conv3x3y_body(const C3& g, unsigned char* lds, c
 
 // the grid: the first nitems - ysplit items (tile-major, a tile's co-blocks adjacent, XCD-aware) one 128-channel
 // block each, then the last ysplit items as two 64-channel blocks each (dispatched last: the tail of the launch)
-template <int DBG = 0>
+template <int DBG = 0, bool ZPF = false>
 __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
   __shared__ __attribute__((aligned(1024))) unsigned char lds[YLDS];   // ONE LDS object (see k_conv3x3x)
   const int ncob = g.COUT >> 7;
@@ -1706,11 +1744,11 @@ __global__ __launch_bounds__(YB, 2) void k_conv3x3y(C3 g) {
   if ((int)blockIdx.x < nfull) {
     const int item = xcd_remap(blockIdx.x, nfull);
     const int tile = item / ncob;
-    conv3x3y_body<DBG, 128>(g, lds, tile, (item - tile * ncob) * 128);
+    conv3x3y_body<DBG, 128, ZPF>(g, lds, tile, (item - tile * ncob) * 128);
   } else if constexpr (DBG == 0) {
     const int t = (int)blockIdx.x - nfull, item = nfull + (t >> 1);
     const int tile = item / ncob;
-    conv3x3y_body<0, 64>(g, lds, tile, (item - tile * ncob) * 128 + (t & 1) * 64);
+    conv3x3y_body<0, 64, ZPF>(g, lds, tile, (item - tile * ncob) * 128 + (t & 1) * 64);
   }
 }
 
@@ -2706,7 +2744,8 @@ static int g_s1_variant = env_int("RPC_DENSE_S1", 0);   // A/B: RPC_DENSE_S1=<kn
 // (tools/s1wg_bench.py, profiles/r06_s1wg_ab.txt)
 static int g_wgrad_variant = env_int("RPC_DENSE_WGRAD", 0);
 static int g_s1x_dbg = 0;          // knob 4: k_conv3x3x timing experiments (0 = the real kernel)
-static int g_y_split = env_int("RPC_DENSE_YSPLIT", 1);   // knob 8: k_conv3x3y split tail (C3::ysplit), 0 = off
+static int g_y_split = env_int("RPC_DENSE_YSPLIT", 1);
+static int g_y_zpf = env_int("RPC_DENSE_YZPF", 1);   // knob 10: k_conv3x3y<0, true> for fused BN-backward data gradients   // knob 8: k_conv3x3y split tail (C3::ysplit), 0 = off
 static int g_ig_order = 0;        // implicit-GEMM grid: 0 = by shape (flat for 2 channel blocks), 1 = 2-D   // S1 weight gradient: 0 = k_wgrad_s1 (128-multiple channels), 1 = k_wgrad
 
 // 128-multiple outputs, by shape: k_conv3x3y (two 4-wave 16x16 blocks per CU) when its grid is more than
@@ -2814,6 +2853,11 @@ extern "C" int rpc_dense_tune(int knob, int value) {
     if (value >= 0) g_s1c_seg = value;
     return old;
   }
+  if (knob == 10) {
+    const int old = g_y_zpf;
+    if (value == 0 || value == 1) g_y_zpf = value;
+    return old;
+  }
   if (knob == 8) {
     const int old = g_y_split;
     if (value == 0 || value == 1) g_y_split = value;
@@ -2853,7 +2897,9 @@ static int launch_s1(const IG& g, const u16* bnz, const float* bnp, hipStream_t 
       case 65: hipLaunchKernelGGL(k_conv3x3y<65>, grid, dim3(YB), 0, st, c); break;
       case 81: hipLaunchKernelGGL(k_conv3x3y<81>, grid, dim3(YB), 0, st, c); break;
       case 128: hipLaunchKernelGGL(k_conv3x3y<128>, grid, dim3(YB), 0, st, c); break;
-      default: hipLaunchKernelGGL(k_conv3x3y<0>, grid, dim3(YB), 0, st, c);
+      default:
+        if (bnz != nullptr && g_y_zpf) hipLaunchKernelGGL((k_conv3x3y<0, true>), grid, dim3(YB), 0, st, c);
+        else hipLaunchKernelGGL(k_conv3x3y<0>, grid, dim3(YB), 0, st, c);
     }
   } else if (s1_xwide(rimg, g.COUT)) {
     if (!fits32) return RPC_ERR_UNSUPPORTED;   // 32-bit buffer offsets (part rows are those of 16x32 tiles)

@@ -102,12 +102,25 @@ def _traffic(kernel_tag, model="voxelnet"):
     files = sorted((f for f in glob.glob(os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles",
                                                       "*pmc_traffic*.json")) if parse(f)[1] == model),
                    key=lambda f: parse(f)[0])
-    loose = kernel_tag[:-1] + "," if kernel_tag.endswith(">") else None   # trailing template arguments omitted
+    # k_conv3x3y's data gradients with fused BatchNorm-backward sums are their own instantiation (<0, true>, r06):
+    # "<0> +bnbwd" takes that one's traffic, the plain "<0>" the <0, false> one; other kernels' "+bnbwd" launches
+    # share the plain kernel's name and have no traffic figure of their own
+    bnb = kernel_tag.endswith(" +bnbwd")
+    tag = kernel_tag[:-len(" +bnbwd")] if bnb else kernel_tag
+    exact = [tag[:-1] + (", true>" if bnb else ", false>")] if tag.endswith(">") else []
+    if not bnb:
+        exact.append(tag)
+    loose = tag[:-1] + "," if tag.endswith(">") and not bnb else None   # trailing template arguments omitted
     for f in reversed(files):
         d = json.load(open(f))
-        for name, v in d.get("kernels", {}).items():
+        ks = d.get("kernels", {})
+        for name, v in ks.items():
             base = name.split("(")[0].strip()
-            if base == kernel_tag or name.startswith(kernel_tag + "(") or (loose and base.startswith(loose)):
+            if base in exact or any(name.startswith(e + "(") for e in exact):
+                return v.get("hbm_bytes_per_launch"), os.path.basename(f)
+        for name, v in ks.items():
+            base = name.split("(")[0].strip()
+            if loose and base.startswith(loose):
                 return v.get("hbm_bytes_per_launch"), os.path.basename(f)
     return None, None
 

@@ -950,10 +950,21 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
   // per step: 1 weight DMA XWD tiles ahead (+ XHI halo DMAs at tap HTAP, after it); the tile of the next
   // step is retired by vmcnt(XWD - 1), or vmcnt(XWD - 1 + XHI) at taps HTAP .. HTAP + XWD - 1 while the
   // halo is younger than that tile (it is retired XWD steps after its issue)
-#define C3X_STEP(t, LIVE)                                                                                     \
+// the step's wait: retire the next step's tile (vmcnt 3; 9 while the halo issued at HTAP is younger than it); LAST
+// (the last K-chunk, which issues no weight DMA past the last real tile): the tiles still in flight at step t are
+// those of steps t + 1 .. 8, so vmcnt(7 - t) from step 9 - XWD on (the halo is retired by then)
+#define C3X_VMWAIT(t, LAST)                                                                                   \
+  {                                                                                                           \
+    if ((t) >= HTAP && (t) < HTAP + XWD) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");                     \
+    else if ((LAST) && (t) == 5) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");                            \
+    else if ((LAST) && (t) == 6) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");                            \
+    else if ((LAST) && (t) >= 7) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");                            \
+    else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");                                                     \
+  }
+#define C3X_STEP(t, LIVE, LAST)                                                                               \
   {                                                                                                           \
     const int s_ = kc * 9 + (t);                                                                              \
-    issue_w(s_ + XWD);                                                                                        \
+    if (!(LAST) || (t) + XWD < 9) issue_w(s_ + XWD);                                                          \
     if ((t) == HTAP) issue_halo(min(kc + 1, NKC - 1), (kc + 1) & 1);                                          \
     const unsigned char* hb_ = hbuf + (kc & 1) * XHBUF;                                                       \
     const unsigned char* wt_ = wring + (s_ & (XWR - 1)) * XWTILE;                                             \
@@ -969,10 +980,7 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
       _Pragma("unroll") for (int j = 0; j < 8; ++j)                                                           \
         bv[j] = *(const bf16x8*)(hb_ + hoff[dx_] + ((j >> 1) + dy_) * XHP * XROW + (j & 1) * 16 * XROW);      \
     }                                                                                                         \
-    if (grp) {                                                                                                \
-      if ((t) >= HTAP && (t) < HTAP + XWD) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");                   \
-      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");                                                   \
-    }                                                                                                         \
+    if (grp) C3X_VMWAIT(t, LAST)                                                                              \
     if (DBG & 16) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); else asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");                                           \
     if (LIVE && !(DBG & 1)) {                                                                                 \
       __builtin_amdgcn_s_setprio(1);                                                                          \
@@ -981,10 +989,7 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(av[i], bv[j], acc[i][j], 0, 0, 0);              \
       __builtin_amdgcn_s_setprio(0);                                                                          \
     }                                                                                                         \
-    if (!grp) {                                                                                               \
-      if ((t) >= HTAP && (t) < HTAP + XWD) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");                   \
-      else asm volatile("s_waitcnt vmcnt(3)" ::: "memory");                                                   \
-    }                                                                                                         \
+    if (!grp) C3X_VMWAIT(t, LAST)                                                                             \
     if (!(DBG & 16)) asm volatile("s_barrier" ::: "memory");                                                  \
   }
   // pipelined form: a step's 32 MFMAs run as four quarters (the 4 weight fragments x the 2 halo fragments
@@ -1057,31 +1062,25 @@ __global__ __launch_bounds__(WB, 2) void k_conv3x3x(C3 g) {
       for (int kc = 0; kc < NKC; ++kc) { C3X_PKC(false) }
     }
   } else if (live) {
-    for (int kc = 0; kc < NKC; ++kc) {
-      C3X_STEP(0, true)
-      C3X_STEP(1, true)
-      C3X_STEP(2, true)
-      C3X_STEP(3, true)
-      C3X_STEP(4, true)
-      C3X_STEP(5, true)
-      C3X_STEP(6, true)
-      C3X_STEP(7, true)
-      C3X_STEP(8, true)
+#define C3X_KC(LIVE, LAST)                                                                                    \
+  C3X_STEP(0, LIVE, LAST) C3X_STEP(1, LIVE, LAST) C3X_STEP(2, LIVE, LAST) C3X_STEP(3, LIVE, LAST)             \
+  C3X_STEP(4, LIVE, LAST) C3X_STEP(5, LIVE, LAST) C3X_STEP(6, LIVE, LAST) C3X_STEP(7, LIVE, LAST)             \
+  C3X_STEP(8, LIVE, LAST)
+    for (int kc = 0; kc < NKC - 1; ++kc) { C3X_KC(true, false) }
+    {
+      const int kc = NKC - 1;
+      C3X_KC(true, true)
     }
   } else {   // DMA issue and barriers only
-    for (int kc = 0; kc < NKC; ++kc) {
-      C3X_STEP(0, false)
-      C3X_STEP(1, false)
-      C3X_STEP(2, false)
-      C3X_STEP(3, false)
-      C3X_STEP(4, false)
-      C3X_STEP(5, false)
-      C3X_STEP(6, false)
-      C3X_STEP(7, false)
-      C3X_STEP(8, false)
+    for (int kc = 0; kc < NKC - 1; ++kc) { C3X_KC(false, false) }
+    {
+      const int kc = NKC - 1;
+      C3X_KC(false, true)
     }
   }
 #undef C3X_STEP
+#undef C3X_KC
+#undef C3X_VMWAIT
 #undef C3X_PKC
 #undef C3X_PSTEP
 #undef C3X_PMMA
